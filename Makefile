@@ -1,0 +1,50 @@
+# Build of the MI355X backend (HIP, gfx950) and of the CPU oracle.
+#   make            -> product library + oracle
+#   make ref        -> oracle/_ref (reference rigid sources; needs /root/reference)
+PKG      := little-physics-engine_amd
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+# Parity flags: no FMA contraction, correctly rounded fp32 div/sqrt, IEEE denormals.
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
+            -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero \
+            -Wall -Wno-unused-function
+CC       ?= gcc
+CXX      ?= g++
+OFLAGS   := -O2 -fPIC -ffp-contract=off -Wall
+
+HIP_SRC  := $(wildcard $(PKG)/csrc/*.hip)
+HIP_HDR  := $(wildcard $(PKG)/csrc/*.h) include/lpe.h
+HIP_OBJ  := $(patsubst $(PKG)/csrc/%.hip,build/%.o,$(HIP_SRC))
+LIB      := $(PKG)/liblpe_hip.so
+
+ORC_SRC  := $(wildcard oracle/*.c)
+ORX_SRC  := $(wildcard oracle/*.cpp)
+ORACLE   := oracle/liblpe_oracle.so
+
+all: $(LIB) $(ORACLE)
+
+build/%.o: $(PKG)/csrc/%.hip $(HIP_HDR)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(HIP_OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-rpath,/opt/rocm/lib
+
+build/oracle/%.o: oracle/%.c oracle/*.h include/lpe.h
+	@mkdir -p build/oracle
+	$(CC) -std=c11 $(OFLAGS) -c $< -o $@
+
+build/oracle/%.opp: oracle/%.cpp oracle/*.h include/lpe.h
+	@mkdir -p build/oracle
+	$(CXX) -std=c++17 $(OFLAGS) -c $< -o $@
+
+$(ORACLE): $(patsubst oracle/%.c,build/oracle/%.o,$(ORC_SRC)) $(patsubst oracle/%.cpp,build/oracle/%.opp,$(ORX_SRC))
+	$(CXX) -shared -fPIC -o $@ $^ -lm
+
+ref:
+	$(MAKE) -f oracle/Makefile.ref
+
+clean:
+	rm -rf build $(LIB) $(ORACLE) oracle/_ref
+
+.PHONY: all ref clean

@@ -1,0 +1,199 @@
+/*
+ * lpe.h — C ABI of the MI355X-native per-tick physics backend.
+ *
+ * This is the drop-in boundary for the hot path of little-physics-engine
+ * (reference snapshot 2025-05-23).  The reference has no C ABI: its device
+ * objects are C++ members of Systems::FluidSystem (include/systems/fluid/
+ * fluid.hpp:328-355) and its rigid path is a chain of static C++ functions
+ * (src/systems/rigid/rigid_body_collision.cpp:24-50).  Every entry point
+ * below names the reference code it replaces.  The C++ host mirror in
+ * little-physics-engine_amd/host/ (Systems::FluidSystem,
+ * Systems::RigidBodyCollisionSystem, ...) gathers the ECS into these plain
+ * arrays and calls through here, exactly where the reference called Metal or
+ * its CPU solvers.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only.  Host arrays are caller-owned and only
+ *    borrowed for the duration of a call.  Device buffers belong to lpe_ctx
+ *    and are grow-only (like FluidSystem::initBuffersIfNeeded,
+ *    fluid.cpp:170-248).
+ *  - Every function returns an int status, LPE_OK (0) on success.  No C++
+ *    exception crosses this boundary.  lpe_last_error() gives a message.
+ *  - One HIP stream per context; a context is not re-entrant.
+ *  - y points down (gravity is +y), SI units, as in the reference.
+ */
+#ifndef LPE_H
+#define LPE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LPE_ABI_VERSION 1
+
+enum lpe_status {
+    LPE_OK = 0,
+    LPE_ERR_HIP = 1,        /* a HIP runtime call failed                       */
+    LPE_ERR_ARG = 2,        /* bad argument (null pointer, negative count ...) */
+    LPE_ERR_STATE = 3,      /* call out of order (e.g. tick before upload)     */
+    LPE_ERR_CAPACITY = 4,   /* a particle left the device grid capacity        */
+    LPE_ERR_OVERFLOW = 5,   /* a per-particle/per-pair fixed list overflowed   */
+    LPE_ERR_NO_DEVICE = 6   /* no HIP device (reference: fluid.cpp:97-100)     */
+};
+
+/* Reference: GPU_MAX_PER_CELL (fluid.hpp:56) and GPU_POLYGON_MAX_VERTS
+ * (fluid.hpp:93).  The HIP grid hash is a counting sort with no per-cell cap;
+ * the cap is only reported (max occupancy) so scenes can be checked against
+ * the reference's limit. */
+#define LPE_REF_MAX_PER_CELL 64
+#define LPE_MAX_POLY_VERTS 16
+
+/* ------------------------------------------------------------------------ */
+/* Fluid configuration: field-for-field mirror of Systems::FluidConfig       */
+/* (include/systems/fluid/fluid.hpp:131-200); defaults via                   */
+/* lpe_fluid_config_default().                                               */
+/* ------------------------------------------------------------------------ */
+typedef struct lpe_fluid_config {
+    float gravity;            /* 9.81  (used only by the coupling solver)   */
+    float restDensity;        /* 0.5                                          */
+    float stiffness;          /* 200                                          */
+    float viscosity;          /* 0.03                                         */
+    struct {                  /* fluid.hpp:140-148                            */
+        float safetyMargin;       /* 0.001 */
+        float relaxFactor;        /* 0.9   */
+        float maxCorrection;      /* 0.1   */
+        float maxVelocityUpdate;  /* 1.0   (read but unused, as reference)    */
+        float minSafeDistance;    /* 1e-10 */
+        float velocityDamping;    /* 0.3   (read but unused, as reference)    */
+        float minPositionChange;  /* 1e-6  */
+    } positionSolver;
+    struct {                  /* fluid.hpp:151-179                            */
+        float maxForce;               /* 0.15  */
+        float maxTorque;              /* 0.03  */
+        float fluidForceScale;        /* 100   */
+        float fluidForceMax;          /* 5e4   */
+        float buoyancyStrength;       /* 0.2   */
+        float viscosityScale;         /* 0.05  */
+        float depthScale;             /* 0.04  */
+        float depthTransitionRate;    /* 2.0   */
+        float depthEstimateScale;     /* 10.0  */
+        float pressureForceRatio;     /* 1.0   */
+        float viscousForceRatio;      /* 0.3   */
+        float angularDampingThreshold;/* 0.5   */
+        float angularDampingFactor;   /* 0.005 */
+        float maxSafeVelocitySq;      /* 80    */
+        float minPenetration;         /* 1e-6  */
+        float minRelVelocity;         /* 1e-6  */
+    } impulseSolver;
+    struct {                  /* fluid.hpp:182-186                            */
+        float gridEpsilon;        /* 1e-6  */
+        float smoothingLength;    /* 0.05  */
+        float boundaryOffset;     /* 0.001 */
+    } gridConfig;
+    struct {                  /* fluid.hpp:189-194                            */
+        float minDistanceThreshold;   /* 1e-14 */
+        float minDensityThreshold;    /* 1e-12 */
+        float minTimestep;            /* 1e-10 */
+        float fallbackTimestep;       /* 1e-4  */
+    } numericalConfig;
+    float dampingFactor;      /* 1.0 (rigid write-back damping)               */
+    int   numSubSteps;        /* 10                                           */
+    int   threadsPerGroup;    /* 256 (only sizes the reference's bbox partials)*/
+} lpe_fluid_config;
+
+/* Rigid body as seen by the fluid coupling: byte-for-byte mirror of
+ * Systems::GPURigidBody (fluid.hpp:94-125, 200 B).  Filled by the host
+ * mirror's gatherRigidBodies (reference fluid.cpp:304-438). */
+typedef struct lpe_gpu_rigid {
+    int32_t shapeType;          /* 0 = Circle, 1 = Polygon                     */
+    float posX, posY, angle, radius;
+    int32_t vertCount;
+    float vertsX[LPE_MAX_POLY_VERTS];
+    float vertsY[LPE_MAX_POLY_VERTS];
+    float vx, vy, omega, mass, inertia;
+    float minX, maxX, minY, maxY;
+    float accumFx, accumFy, accumTorque;
+} lpe_gpu_rigid;
+
+/* Per-tick statistics of the SPH step (for the parity harness / bench). */
+typedef struct lpe_sph_stats {
+    int32_t maxCellOccupancy;   /* max particles in one reference 2h cell     */
+    int32_t notInserted;        /* particles outside the reference grid, last sub-step */
+    int32_t capacityOverflow;   /* non-zero if a particle left the device grid */
+    int32_t listOverflow;       /* non-zero if a per-particle rigid list overflowed */
+    int32_t gridDimX, gridDimY; /* reference grid dims of the last sub-step   */
+    int32_t gridMinX, gridMinY;
+    float   cellSize;
+} lpe_sph_stats;
+
+typedef struct lpe_ctx lpe_ctx;
+
+/* ---- lifecycle -------------------------------------------------------- */
+/* Replaces FluidSystem::FluidSystem (fluid.cpp:72-125): device, queue and
+ * code-object set-up.  The code object is loaded once per process, so a
+ * reference-style reset() that re-creates systems does not reload it. */
+int  lpe_create(int device, lpe_ctx **out);
+/* Replaces FluidSystem::~FluidSystem (fluid.cpp:127-147). */
+int  lpe_destroy(lpe_ctx *ctx);
+const char *lpe_last_error(const lpe_ctx *ctx);
+int  lpe_abi_version(void);
+int  lpe_device_count(int *count);
+/* Blocks until all work queued on the context's stream is done. */
+int  lpe_sync(lpe_ctx *ctx);
+
+/* ---- SPH fluid (Systems::FluidSystem) ----------------------------------- */
+int  lpe_fluid_config_default(lpe_fluid_config *cfg);
+/* Replaces the FluidConfig → GPUFluidParams packing (fluid.cpp:614-666,
+ * :759-818). */
+int  lpe_sph_set_config(lpe_ctx *ctx, const lpe_fluid_config *cfg);
+/* Replaces gatherFluidParticles' output copy into the particle buffer
+ * (fluid.cpp:250-302, :996-1000).  n fluid particles in gather order; the
+ * arrays are fp32 (the reference casts double→float at gather).  h is
+ * config.gridConfig.smoothingLength for every particle (fluid.cpp:292), so it
+ * is not an input.  ax = ay = 0 and vh = v at every gather (fluid.cpp:287-290);
+ * lpe_sph_upload re-establishes that. */
+int  lpe_sph_upload(lpe_ctx *ctx, int n,
+                    const float *x, const float *y,
+                    const float *vx, const float *vy,
+                    const float *mass,
+                    const float *density, const float *pressure);
+/* Replaces the rigid part of FluidSystem::update (fluid.cpp:975-1007):
+ * r bodies in gatherRigidBodies order.  accum* are ignored (reset to 0). */
+int  lpe_sph_upload_rigids(lpe_ctx *ctx, int r, const lpe_gpu_rigid *rigids);
+/* Replaces multiStepVelocityVerlet (fluid.cpp:582-956): numSubSteps
+ * sub-steps of kick/drift → grid hash → density → forces → finish →
+ * rigid–fluid impulse (if r > 0) → rigid–fluid push-out, followed by the
+ * once-per-tick rigid velocity write-back arithmetic (fluid.cpp:545-562).
+ * dt_tick = SharedSystemConfig.SecondsPerTick * TimeAcceleration
+ * (fluid.cpp:592).  Asynchronous: results are read with lpe_sph_download*. */
+int  lpe_sph_step(lpe_ctx *ctx, double dt_tick);
+/* Replaces writeBackToECS's source data (fluid.cpp:496-524).  Any pointer
+ * may be NULL to skip that field.  Blocks until the step is complete. */
+int  lpe_sph_download(lpe_ctx *ctx, float *x, float *y, float *vx, float *vy,
+                      float *density, float *pressure);
+/* Extra fields for parity tests: half-step velocity and acceleration. */
+int  lpe_sph_download_aux(lpe_ctx *ctx, float *vxHalf, float *vyHalf,
+                          float *ax, float *ay);
+/* Replaces writeBackRigidBodies' source data (fluid.cpp:526-580): the
+ * rigid array after v += F/m, ω += τ/I, × dampingFactor (accum reset to 0).
+ * The pre-write-back accumulators are returned in accumF{x,y},accumTorque
+ * when accum is non-NULL (3 floats per body). */
+int  lpe_sph_download_rigids(lpe_ctx *ctx, lpe_gpu_rigid *rigids, float *accum);
+int  lpe_sph_get_stats(lpe_ctx *ctx, lpe_sph_stats *stats);
+
+/* Parity probe: the reference's assignCells cell index for each particle
+ * (fluid_kernels.metal:212-241: cellY*gridDimX + cellX, or -1 if "not
+ * inserted") computed from the CURRENT device positions with the grid the
+ * reference would derive from them (fluid.cpp:717-752).  Runs one kick-free
+ * hash pass; does not advance the simulation. */
+int  lpe_sph_probe_cells(lpe_ctx *ctx, int32_t *cell_index, lpe_sph_stats *stats);
+/* Parity probe: density and pressure of the current positions (one hash +
+ * density pass, no integration; fluid_kernels.metal:246-307). */
+int  lpe_sph_probe_density(lpe_ctx *ctx, float *density, float *pressure);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LPE_H */

@@ -1,0 +1,112 @@
+// lpe_internal.h — shared internals of the HIP backend (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+#include <string>
+#include "../../include/lpe.h"
+
+namespace lpe {
+
+// Device mirror of the reference's per-sub-step grid (fluid.cpp:737-752)
+// plus the absolute device grid the counting sort runs on.
+struct GridParams {
+    float cellSize;        // 2 * max(0.05, h)                   fluid.cpp:724-737
+    int gridMinX, gridMinY; // reference grid origin (cells)      fluid.cpp:743-744
+    int gridMaxX, gridMaxY; // floor(max/cs)                      fluid.cpp:745-746
+    int gridDimX, gridDimY; // max-min+1 clamped to >= 1          fluid.cpp:748-751
+};
+
+// Particle state in cell-sorted order (SoA fp32).  `id` is the gather index
+// of the particle (the reference's particle index i, fluid.cpp:268-299).
+struct PState {
+    float *x = nullptr, *y = nullptr, *vx = nullptr, *vy = nullptr;
+    float *vhx = nullptr, *vhy = nullptr, *ax = nullptr, *ay = nullptr;
+    float *m = nullptr;
+    int32_t *id = nullptr;
+};
+
+struct SphDev {
+    int n = 0, cap_n = 0;
+    PState P;                     // primary state (sorted order of the last sub-step)
+    PState S;                     // permutation target of the current sub-step
+    float *rho = nullptr, *pr = nullptr;  // in S/P slot order
+    // counting-sort grid hash over (2h cell, h quadrant) bins
+    uint32_t *key = nullptr;      // bin of each P slot
+    int32_t *tmpId = nullptr;     // scatter output: particle id per new slot
+    int32_t *tmpOld = nullptr;    // scatter output: old P slot per new slot
+    int32_t *count = nullptr;     // per bin
+    int32_t *start = nullptr;     // nbins+1
+    int32_t *cursor = nullptr;    // nbins
+    int32_t *blocksum = nullptr;  // scan partials
+    float4 *bboxPart = nullptr;   // per-block bbox partials (minX, maxX, minY, maxY)
+    int cap_cells = 0;
+    // absolute device grid: origin (cells) and dims, fixed per upload
+    int ox = 0, oy = 0, W = 0, H = 0;
+    float cs = 0.1f;
+    GridParams *gp = nullptr;     // device copy of the reference grid
+    int32_t *status = nullptr;    // [16] flags / stats
+    // rigid coupling
+    int nr = 0, cap_nr = 0;
+    lpe_gpu_rigid *rig = nullptr;
+    float *accum = nullptr;       // [3R] running + [3R] last tick
+    int32_t *rbinStart = nullptr; // rigid bins (absolute grid of bin size bcs)
+    int32_t *rbinList = nullptr;
+    int32_t *rbinCount = nullptr;
+    int cap_rbins = 0, cap_rlist = 0;
+    int bx0 = 0, by0 = 0, bW = 0, bH = 0;
+    float bcs = 0.25f;
+    int rlist_len = 0;
+    lpe_fluid_config cfg{};
+    bool cfg_set = false;
+    bool rig_dirty = true;
+};
+
+// status slots
+enum StatusSlot {
+    ST_CAP_OVERFLOW = 0,
+    ST_MAX_OCC = 1,
+    ST_NOT_INSERTED = 2,
+    ST_LIST_OVERFLOW = 3,
+    ST_COUNT = 16
+};
+
+}  // namespace lpe
+
+struct lpe_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    lpe::SphDev sph;
+    void *rigid = nullptr;  // lpe::RigidDev*, owned by lpe_rigid.hip
+};
+
+#define LPE_HIP(ctx, call)                                                       \
+    do {                                                                         \
+        hipError_t e_ = (call);                                                  \
+        if (e_ != hipSuccess) {                                                  \
+            (ctx)->err = std::string(#call) + ": " + hipGetErrorString(e_);      \
+            return LPE_ERR_HIP;                                                  \
+        }                                                                        \
+    } while (0)
+
+#define LPE_CHECK_LAUNCH(ctx, name)                                              \
+    do {                                                                         \
+        hipError_t e_ = hipGetLastError();                                       \
+        if (e_ != hipSuccess) {                                                  \
+            (ctx)->err = std::string("launch ") + name + ": " + hipGetErrorString(e_); \
+            return LPE_ERR_HIP;                                                  \
+        }                                                                        \
+    } while (0)
+
+template <typename T>
+static inline int lpe_grow(lpe_ctx *ctx, T **p, int *cap, long want, long elems_alloc) {
+    if (want <= *cap && *p) return LPE_OK;
+    if (*p) { (void)hipFree(*p); *p = nullptr; }
+    hipError_t e = hipMalloc((void **)p, sizeof(T) * (size_t)(elems_alloc > 0 ? elems_alloc : 1));
+    if (e != hipSuccess) { ctx->err = std::string("hipMalloc: ") + hipGetErrorString(e); return LPE_ERR_HIP; }
+    *cap = (int)want;
+    return LPE_OK;
+}
+
+int lpe_rigid_destroy_internal(lpe_ctx *ctx);

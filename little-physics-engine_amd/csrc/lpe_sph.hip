@@ -1,0 +1,1123 @@
+// lpe_sph.hip — SPH fluid step of the MI355X backend (Systems::FluidSystem).
+//
+// Replaces the 9 Metal kernels of src/systems/fluid/fluid_kernels.metal and the
+// host orchestration of src/systems/fluid/fluid.cpp:582-1021 with a
+// device-resident pipeline over particle state kept in cell-sorted order:
+//
+//   per sub-step (fluid.cpp:598-950):
+//     k_kick_drift   velocityVerletHalf (metal:408-423) + bin key + histogram
+//                    (wave-aggregated atomics) + per-block bbox partials
+//                    (metal:446-514)
+//     k_scan_*       exclusive scan of the bin histogram; the bbox finish
+//                    (fluid.cpp:440-494) and the reference grid
+//                    (fluid.cpp:717-752) are computed on device, no host sync
+//     k_scatter      new slot per particle (wave-aggregated atomics)
+//     k_rank_permute canonical order inside each bin + permutation of the
+//                    state into the new sorted order
+//     k_density      computeDensity (metal:246-307)
+//     k_forces_couple computeForces (metal:312-403) + velocityVerletFinish
+//                    (metal:428-441) + rigidFluidImpulseSolver (metal:679-924)
+//                    + rigidFluidPositionSolver (metal:533-668), fused per particle
+//   per tick:
+//     k_rbin_*       rigids binned by AABB (rigids are frozen during the
+//                    sub-steps, fluid.cpp:953-955): a particle tests only the
+//                    rigids of its bin, in ascending rigid index
+//     k_rigid_writeback  writeBackRigidBodies arithmetic (fluid.cpp:545-562)
+//
+// Bins are (reference 2h cell, h-sized quadrant).  The stencil walk visits the
+// 3x3 reference cells row-major (metal:272-283) and each cell's quadrants
+// row-major, ascending particle index inside a quadrant: the canonical order
+// of oracle/sph_oracle.c.  Quadrants farther than h from the particle are
+// skipped; they can only hold particles with r^2 >= h^2, which the reference
+// discards (metal:291, :365), so the sums are unchanged bit for bit.
+//
+// The "not inserted" rule (metal:231-234: a particle in a cell outside the
+// per-sub-step grid is in no cell list) is reproduced exactly: bins live on a
+// fixed absolute grid and every stencil walk skips cells outside the
+// reference grid [gridMin, gridMin + dim).
+//
+// Numerics: fp32, no FMA contraction (-ffp-contract=off), correctly rounded
+// division and sqrt, tanh/pow via fp64 rounded once; with the canonical orders
+// above the fluid state is bit-identical to the oracle.  Only the rigid
+// accumulators use float atomics (order-dependent in the last bits, as the
+// reference's own atomics, metal:892-898).
+#include "lpe_internal.h"
+#include "sph_coupling.h"
+#include <cmath>
+#include <cstring>
+#include <vector>
+#include <algorithm>
+
+namespace lpe {
+
+static constexpr float PI_F = 3.14159265358979323846f;  // metal:17 evaluated in fp32
+static constexpr int TPB = 256;
+static constexpr int SCAN_ELEMS = 1024;   // elements per scan block (256 thr x 4)
+static constexpr int MAX_KICK_BLOCKS = 2048;
+
+// kernel coefficients (metal:19-38), fp32
+__device__ __forceinline__ float poly6Coeff2D(float h) {
+    float h2 = h * h; float h4 = h2 * h2; float h8 = h4 * h4;
+    return 4.0f / (PI_F * h8);
+}
+__device__ __forceinline__ float spikyCoeff2D(float h) {
+    float h2 = h * h; float h4 = h2 * h2; float h5 = h4 * h;
+    return -30.0f / (PI_F * h5);
+}
+__device__ __forceinline__ float viscLaplacianCoeff2D(float h) {
+    float h2 = h * h; float h4 = h2 * h2; float h5 = h4 * h;
+    return 40.0f / (PI_F * h5);
+}
+
+// ---------------------------------------------------------------------------
+// wave helpers (wave64)
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+// Run-length aggregation of equal consecutive keys inside a wave.  Returns the
+// lane that starts this lane's run; *runlen is set on run-start lanes.
+__device__ __forceinline__ int wave_runs(uint32_t k, bool active, int *runlen, bool *is_start) {
+    int lane = lane_id();
+    uint32_t prev = __shfl_up(k, 1);
+    int prev_active = __shfl_up((int)active, 1);
+    bool st = active && (lane == 0 || prev != k || !prev_active);
+    unsigned long long starts = __ballot(st);
+    unsigned long long act = __ballot(active);
+    unsigned long long stop = starts | ~act;
+    unsigned long long above = (lane == 63) ? 0ull : (stop & (~0ull << (lane + 1)));
+    int next = above ? __ffsll((long long)above) - 1 : 64;
+    unsigned long long below = starts & ((lane == 63) ? ~0ull : ((1ull << (lane + 1)) - 1));
+    int first = below ? 63 - __clzll(below) : lane;
+    *runlen = next - lane;
+    *is_start = st;
+    return first;
+}
+
+// ---------------------------------------------------------------------------
+// k_kick_drift: velocityVerletHalf + bin key + histogram + bbox partials.
+// first != 0: first sub-step of a tick; the gather set a = 0 (fluid.cpp:289-290).
+__global__ void __launch_bounds__(TPB)
+k_kick_drift(int n, float dt, float hdt, int first, int probe, float eps, float cs,
+             int ox, int oy, int W, int H, PState P, uint32_t *__restrict__ key,
+             int32_t *__restrict__ count, float4 *__restrict__ bboxPart,
+             int32_t *__restrict__ status) {
+    float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
+    const int stride = gridDim.x * TPB;
+    const int iters = (n + stride - 1) / stride;
+    for (int it = 0; it < iters; it++) {
+        int i = it * stride + blockIdx.x * TPB + threadIdx.x;
+        bool active = i < n;
+        uint32_t k = 0xFFFFFFFFu;
+        if (active) {
+            float px, py;
+            if (probe) {
+                px = P.x[i]; py = P.y[i];
+            } else {
+                float a_x = first ? 0.f : P.ax[i];
+                float a_y = first ? 0.f : P.ay[i];
+                float hx = P.vx[i] + hdt * a_x;
+                float hy = P.vy[i] + hdt * a_y;
+                px = P.x[i] + hx * dt;
+                py = P.y[i] + hy * dt;
+                P.x[i] = px; P.y[i] = py; P.vhx[i] = hx; P.vhy[i] = hy;
+            }
+            float tx = (px + eps) / cs, ty = (py + eps) / cs;
+            int gx = (int)floorf(tx), gy = (int)floorf(ty);
+            int qx = (int)floorf(2.0f * tx) - 2 * gx;
+            int qy = (int)floorf(2.0f * ty) - 2 * gy;
+            int kx = gx - ox, ky = gy - oy;
+            if (kx < 0 || kx >= W || ky < 0 || ky >= H) {
+                atomicOr(&status[ST_CAP_OVERFLOW], 1);
+                kx = min(max(kx, 0), W - 1);
+                ky = min(max(ky, 0), H - 1);
+            }
+            k = (((uint32_t)ky * (uint32_t)W + (uint32_t)kx) << 2) | (uint32_t)(qy * 2 + qx);
+            key[i] = k;
+            mnx = fminf(mnx, px); mxx = fmaxf(mxx, px);
+            mny = fminf(mny, py); mxy = fmaxf(mxy, py);
+        }
+        int len; bool st;
+        (void)wave_runs(k, active, &len, &st);
+        if (st) atomicAdd(&count[k], len);
+    }
+    // block bbox partial (exact: min/max are order independent)
+    for (int off = 32; off > 0; off >>= 1) {
+        mnx = fminf(mnx, __shfl_xor(mnx, off));
+        mxx = fmaxf(mxx, __shfl_xor(mxx, off));
+        mny = fminf(mny, __shfl_xor(mny, off));
+        mxy = fmaxf(mxy, __shfl_xor(mxy, off));
+    }
+    __shared__ float4 wb[TPB / 64];
+    if (lane_id() == 0) wb[threadIdx.x >> 6] = make_float4(mnx, mxx, mny, mxy);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float4 b = wb[0];
+        for (int w = 1; w < TPB / 64; w++) {
+            b.x = fminf(b.x, wb[w].x); b.y = fmaxf(b.y, wb[w].y);
+            b.z = fminf(b.z, wb[w].z); b.w = fmaxf(b.w, wb[w].w);
+        }
+        bboxPart[blockIdx.x] = b;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// scan
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    int lane = lane_id();
+    for (int off = 1; off < 64; off <<= 1) {
+        int t = __shfl_up(v, off);
+        if (lane >= off) v += t;
+    }
+    return v;
+}
+
+// block-wide exclusive scan of one int per thread (TPB threads); returns total
+__device__ __forceinline__ int block_excl_scan(int v, int *total) {
+    __shared__ int wsum[TPB / 64];
+    int lane = lane_id(), w = threadIdx.x >> 6;
+    int incl = wave_incl_scan(v);
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int off = 0, tot = 0;
+    for (int k = 0; k < TPB / 64; k++) { if (k < w) off += wsum[k]; tot += wsum[k]; }
+    __syncthreads();
+    *total = tot;
+    return off + incl - v;
+}
+
+__global__ void __launch_bounds__(TPB)
+k_scan_reduce(int C, const int32_t *__restrict__ cnt, int32_t *__restrict__ bsum) {
+    int base = blockIdx.x * SCAN_ELEMS;
+    int s = 0;
+    for (int k = 0; k < 4; k++) {
+        int c = base + k * TPB + threadIdx.x;
+        if (c < C) s += cnt[c];
+    }
+    int tot;
+    (void)block_excl_scan(s, &tot);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+// one block: scan the block sums; if gp != null, finish the bbox from the
+// partials (fluid.cpp:440-494) and derive the reference grid (fluid.cpp:717-752)
+__global__ void __launch_bounds__(TPB)
+k_scan_blocks(int nb, int32_t *__restrict__ bsum, int32_t *__restrict__ start_last,
+              const float4 *__restrict__ bboxPart, int nparts, float cs,
+              GridParams *__restrict__ gp, int32_t *__restrict__ status) {
+    int carry = 0;
+    for (int b0 = 0; b0 < nb; b0 += TPB) {
+        int b = b0 + threadIdx.x;
+        int v = (b < nb) ? bsum[b] : 0;
+        int tot;
+        int ex = block_excl_scan(v, &tot);
+        if (b < nb) bsum[b] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) *start_last = carry;
+    if (!gp) return;
+    float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
+    for (int p = threadIdx.x; p < nparts; p += TPB) {
+        float4 b = bboxPart[p];
+        mnx = fminf(mnx, b.x); mxx = fmaxf(mxx, b.y);
+        mny = fminf(mny, b.z); mxy = fmaxf(mxy, b.w);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        mnx = fminf(mnx, __shfl_xor(mnx, off));
+        mxx = fmaxf(mxx, __shfl_xor(mxx, off));
+        mny = fminf(mny, __shfl_xor(mny, off));
+        mxy = fmaxf(mxy, __shfl_xor(mxy, off));
+    }
+    __shared__ float4 wb[TPB / 64];
+    if (lane_id() == 0) wb[threadIdx.x >> 6] = make_float4(mnx, mxx, mny, mxy);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float4 b = wb[0];
+        for (int w = 1; w < TPB / 64; w++) {
+            b.x = fminf(b.x, wb[w].x); b.y = fmaxf(b.y, wb[w].y);
+            b.z = fminf(b.z, wb[w].z); b.w = fmaxf(b.w, wb[w].w);
+        }
+        float minX = b.x, maxX = b.y, minY = b.z, maxY = b.w;
+        if (minX > maxX) { float t = minX; minX = maxX; maxX = t; }
+        if (minY > maxY) { float t = minY; minY = maxY; maxY = t; }
+        minX -= 1e-6f;
+        minY -= 1e-6f;
+        GridParams g;
+        g.cellSize = cs;
+        g.gridMinX = (int)floorf(minX / cs);
+        g.gridMinY = (int)floorf(minY / cs);
+        g.gridMaxX = (int)floorf(maxX / cs);
+        g.gridMaxY = (int)floorf(maxY / cs);
+        g.gridDimX = g.gridMaxX - g.gridMinX + 1;
+        g.gridDimY = g.gridMaxY - g.gridMinY + 1;
+        if (g.gridDimX < 1) g.gridDimX = 1;
+        if (g.gridDimY < 1) g.gridDimY = 1;
+        *gp = g;
+        status[ST_NOT_INSERTED] = 0;
+    }
+}
+
+// final scan pass; one thread = 4 consecutive bins = one reference cell when
+// the bins are the (cell, quadrant) bins of the fluid (do_stats).
+__global__ void __launch_bounds__(TPB)
+k_scan_final(int C, int W, int ox, int oy, int32_t *__restrict__ cnt,
+             const int32_t *__restrict__ bsum, int32_t *__restrict__ start,
+             int32_t *__restrict__ cursor, const GridParams *__restrict__ gp,
+             int32_t *__restrict__ status, int do_stats) {
+    __shared__ int s_max, s_out;
+    if (threadIdx.x == 0) { s_max = 0; s_out = 0; }
+    __syncthreads();
+    GridParams g{};
+    if (do_stats) g = *gp;
+    int base = blockIdx.x * SCAN_ELEMS + threadIdx.x * 4;
+    int v[4];
+    int s = 0;
+    for (int k = 0; k < 4; k++) {
+        int c = base + k;
+        v[k] = (c < C) ? cnt[c] : 0;
+        s += v[k];
+    }
+    if (do_stats && s > 0) {
+        int cell = base >> 2;
+        int gx = cell % W + ox, gy = cell / W + oy;
+        // the reference grid excludes gx > gridMax (no epsilon on the max side,
+        // fluid.cpp:745-746 vs metal:224-226): those particles are "not inserted"
+        bool in = gx >= g.gridMinX && gx < g.gridMinX + g.gridDimX &&
+                  gy >= g.gridMinY && gy < g.gridMinY + g.gridDimY;
+        if (in) atomicMax(&s_max, s); else atomicAdd(&s_out, s);
+    }
+    int tot;
+    int ex = block_excl_scan(s, &tot) + bsum[blockIdx.x];
+    for (int k = 0; k < 4; k++) {
+        int c = base + k;
+        if (c < C) { start[c] = ex; cursor[c] = ex; cnt[c] = 0; }
+        ex += v[k];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (s_max) atomicMax(&status[ST_MAX_OCC], s_max);
+        if (s_out) atomicAdd(&status[ST_NOT_INSERTED], s_out);
+    }
+}
+
+// new slot per particle: slot = cursor[bin]++ (wave-aggregated)
+__global__ void __launch_bounds__(TPB)
+k_scatter(int n, const uint32_t *__restrict__ key, const int32_t *__restrict__ id,
+          int32_t *__restrict__ cursor, int32_t *__restrict__ tmpId,
+          int32_t *__restrict__ tmpOld) {
+    int i = blockIdx.x * TPB + threadIdx.x;
+    bool active = i < n;
+    uint32_t k = active ? key[i] : 0xFFFFFFFFu;
+    int len; bool st;
+    int first = wave_runs(k, active, &len, &st);
+    int base = 0;
+    if (st) base = atomicAdd(&cursor[k], len);
+    base = __shfl(base, first);
+    if (active) {
+        int slot = base + (lane_id() - first);
+        tmpId[slot] = id[i];
+        tmpOld[slot] = i;
+    }
+}
+
+// canonical order inside a bin (ascending particle id) + state permutation P -> S
+__global__ void __launch_bounds__(TPB)
+k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restrict__ start,
+               const int32_t *__restrict__ tmpId, const int32_t *__restrict__ tmpOld,
+               PState P, PState S, int probe) {
+    int s = blockIdx.x * TPB + threadIdx.x;
+    if (s >= n) return;
+    int o = tmpOld[s];
+    int myid = tmpId[s];
+    uint32_t k = key[o];
+    int b = start[k], e = start[k + 1];
+    int rank = 0;
+    for (int j = b; j < e; j++) rank += (tmpId[j] < myid) ? 1 : 0;
+    int d = b + rank;
+    S.x[d] = P.x[o]; S.y[d] = P.y[o];
+    S.vx[d] = P.vx[o]; S.vy[d] = P.vy[o];
+    S.m[d] = P.m[o]; S.id[d] = myid;
+    if (!probe) { S.vhx[d] = P.vhx[o]; S.vhy[d] = P.vhy[o]; }
+}
+
+// ---------------------------------------------------------------------------
+// Does quadrant q of reference cell (gcx, gcy) lie within distance h of the
+// particle at t = (x + eps) / cs?  Conservative (box widened by 1e-3 cell,
+// 0.1% margin on h^2): a skipped quadrant only holds particles with
+// r^2 >= h^2 in fp32, whose terms the reference discards.
+__device__ __forceinline__ bool quad_near(float tx, float ty, int gcx, int gcy, int q, float cs,
+                                          float h2) {
+    float lox = (float)gcx + (float)(q & 1) * 0.5f, loy = (float)gcy + (float)(q >> 1) * 0.5f;
+    const float mg = 1e-3f;
+    float dx = fmaxf(fmaxf(lox - mg - tx, tx - (lox + 0.5f + mg)), 0.f) * cs;
+    float dy = fmaxf(fmaxf(loy - mg - ty, ty - (loy + 0.5f + mg)), 0.f) * cs;
+    return dx * dx + dy * dy < h2 * 1.001f;
+}
+
+// computeDensity (metal:246-307), one thread per sorted slot
+__global__ void __launch_bounds__(TPB)
+k_density(int n, float h, float eps, float stiffness, float restDensity, int W, int ox, int oy,
+          const GridParams *__restrict__ gp, const int32_t *__restrict__ start,
+          const float *__restrict__ sx, const float *__restrict__ sy, const float *__restrict__ sm,
+          float *__restrict__ rho, float *__restrict__ pr) {
+    int s = blockIdx.x * TPB + threadIdx.x;
+    if (s >= n) return;
+    const GridParams g = *gp;
+    const float cs = g.cellSize;
+    float xi = sx[s], yi = sy[s];
+    float h2 = h * h;
+    float poly6 = poly6Coeff2D(h);
+    float acc = 0.0f;
+    float tx = (xi + eps) / cs, ty = (yi + eps) / cs;
+    int gx = (int)floorf(tx), gy = (int)floorf(ty);
+    int cellX = gx - g.gridMinX, cellY = gy - g.gridMinY;
+    for (int ny = -1; ny <= 1; ny++) {
+        int cy = cellY + ny;
+        if (cy < 0 || cy >= g.gridDimY) continue;
+        int gcy = cy + g.gridMinY;
+        for (int nx = -1; nx <= 1; nx++) {
+            int cx = cellX + nx;
+            if (cx < 0 || cx >= g.gridDimX) continue;
+            int gcx = cx + g.gridMinX;
+            int cbase = (((gcy - oy) * W) + (gcx - ox)) << 2;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (!quad_near(tx, ty, gcx, gcy, q, cs, h2)) continue;
+                int b = start[cbase + q], e = start[cbase + q + 1];
+                for (int k = b; k < e; k++) {
+                    float dx = xi - sx[k], dy = yi - sy[k];
+                    float r2 = dx * dx + dy * dy;
+                    if (r2 < h2) {
+                        float diff = h2 - r2;
+                        float w = poly6 * diff * diff * diff;
+                        acc += sm[k] * w;
+                    }
+                }
+            }
+        }
+    }
+    float pres = stiffness * (acc - restDensity);
+    if (pres < 0.f) pres = 0.f;
+    rho[s] = acc;
+    pr[s] = pres;
+}
+
+struct SphStepParams {
+    int n, W, ox, oy;
+    float h, eps, dt, hdt;
+    float viscosity, minDist, minDens;
+};
+
+// computeForces + velocityVerletFinish + impulse + push-out; reads S, writes P
+__global__ void __launch_bounds__(TPB)
+k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict__ gp,
+                const int32_t *__restrict__ start, PState S, const float *__restrict__ rho,
+                const float *__restrict__ pr, PState P,
+                const lpe_gpu_rigid *__restrict__ rig, const int32_t *__restrict__ rbinStart,
+                const int32_t *__restrict__ rbinList, float *__restrict__ accum) {
+    int s = blockIdx.x * TPB + threadIdx.x;
+    if (s >= sp.n) return;
+    const GridParams g = *gp;
+    const float cs = g.cellSize;
+    const float xi = S.x[s], yi = S.y[s];
+    const float vxi = S.vx[s], vyi = S.vy[s];
+    const float pi = pr[s], rhoi = rho[s];
+    const float hi = sp.h;
+    const float h2 = hi * hi;
+    float sumFx = 0.f, sumFy = 0.f;
+    float tx = (xi + sp.eps) / cs, ty = (yi + sp.eps) / cs;
+    int gx = (int)floorf(tx), gy = (int)floorf(ty);
+    int cellX = gx - g.gridMinX, cellY = gy - g.gridMinY;
+    for (int ny = -1; ny <= 1; ny++) {
+        int cy = cellY + ny;
+        if (cy < 0 || cy >= g.gridDimY) continue;
+        int gcy = cy + g.gridMinY;
+        for (int nx = -1; nx <= 1; nx++) {
+            int cx = cellX + nx;
+            if (cx < 0 || cx >= g.gridDimX) continue;
+            int gcx = cx + g.gridMinX;
+            int cbase = (((gcy - sp.oy) * sp.W) + (gcx - sp.ox)) << 2;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                if (!quad_near(tx, ty, gcx, gcy, q, cs, h2)) continue;
+                int b = start[cbase + q], e = start[cbase + q + 1];
+                for (int k = b; k < e; k++) {
+                    if (k == s) continue;
+                    float dx = xi - S.x[k], dy = yi - S.y[k];
+                    float r2 = dx * dx + dy * dy;
+                    if (r2 < sp.minDist) continue;
+                    float hj = sp.h;
+                    float h_ij = 0.5f * (hi + hj);
+                    float h_ij2 = h_ij * h_ij;
+                    if (r2 >= h_ij2) continue;
+                    float r = sqrtf(r2);
+                    float pj = pr[k], rhoj = rho[k];
+                    if (rhoj < sp.minDens || rhoi < sp.minDens) continue;
+                    float mj = S.m[k];
+                    float term = (pi / (rhoi * rhoi)) + (pj / (rhoj * rhoj));
+                    float spF = spikyCoeff2D(h_ij);
+                    float diff = (h_ij - r);
+                    float wSpiky = spF * (diff * diff);
+                    float rx = dx / r, ry = dy / r;
+                    float fxPress = -mj * term * wSpiky;
+                    float fx = fxPress * rx;
+                    float fy = fxPress * ry;
+                    float vx_ij = vxi - S.vx[k], vy_ij = vyi - S.vy[k];
+                    float lapC = viscLaplacianCoeff2D(h_ij);
+                    float wVisc = lapC * diff;
+                    float fVisc = sp.viscosity * mj * (wVisc / rhoj);
+                    fx -= fVisc * vx_ij;
+                    fy -= fVisc * vy_ij;
+                    sumFx += fx;
+                    sumFy += fy;
+                }
+            }
+        }
+    }
+    CoupleState st;
+    st.x = xi; st.y = yi;
+    st.vhx = S.vhx[s]; st.vhy = S.vhy[s];
+    st.ax = sumFx; st.ay = sumFy;
+    // velocityVerletFinish (metal:428-441)
+    st.vx = st.vhx + sp.hdt * st.ax;
+    st.vy = st.vhy + sp.hdt * st.ay;
+    st.mass = S.m[s]; st.rho = rhoi; st.p = pi;
+    int k0 = 0, k1 = 0;
+    if (cp.nr > 0) {
+        float fbx = fminf(fmaxf(floorf(st.x / cp.bcs) - (float)cp.bx0, 0.f), (float)(cp.bW - 1));
+        float fby = fminf(fmaxf(floorf(st.y / cp.bcs) - (float)cp.by0, 0.f), (float)(cp.bH - 1));
+        int bin = (int)fby * cp.bW + (int)fbx;
+        k0 = rbinStart[bin]; k1 = rbinStart[bin + 1];
+        // impulse solver: dispatched only if R > 0 (fluid.cpp:910)
+        couple_impulse(st, cp, sp.dt, rig, rbinList, k0, k1, accum);
+    }
+    couple_position(st, cp, rig, rbinList, k0, k1);
+    P.x[s] = st.x; P.y[s] = st.y;
+    P.vx[s] = st.vx; P.vy[s] = st.vy;
+    P.vhx[s] = st.vhx; P.vhy[s] = st.vhy;
+    P.ax[s] = st.ax; P.ay[s] = st.ay;
+    P.m[s] = st.mass; P.id[s] = S.id[s];
+}
+
+// ---------------------------------------------------------------------------
+// rigid binning (once per tick)
+__device__ __forceinline__ int bin_of(float v, float bcs, int b0, int nb) {
+    float t = floorf(v / bcs) - (float)b0;
+    t = fminf(fmaxf(t, 0.f), (float)(nb - 1));
+    return (int)t;
+}
+__global__ void k_rbin_count(int nr, const lpe_gpu_rigid *__restrict__ rig, float bcs,
+                             int bx0, int by0, int bW, int bH, int32_t *__restrict__ cnt) {
+    int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nr) return;
+    const lpe_gpu_rigid &b = rig[r];
+    int x0 = bin_of(b.minX, bcs, bx0, bW), x1 = bin_of(b.maxX, bcs, bx0, bW);
+    int y0 = bin_of(b.minY, bcs, by0, bH), y1 = bin_of(b.maxY, bcs, by0, bH);
+    for (int yy = y0; yy <= y1; yy++)
+        for (int xx = x0; xx <= x1; xx++) atomicAdd(&cnt[yy * bW + xx], 1);
+}
+__global__ void k_rbin_fill(int nr, const lpe_gpu_rigid *__restrict__ rig, float bcs,
+                            int bx0, int by0, int bW, int bH, int32_t *__restrict__ cursor,
+                            int32_t *__restrict__ list) {
+    int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nr) return;
+    const lpe_gpu_rigid &b = rig[r];
+    int x0 = bin_of(b.minX, bcs, bx0, bW), x1 = bin_of(b.maxX, bcs, bx0, bW);
+    int y0 = bin_of(b.minY, bcs, by0, bH), y1 = bin_of(b.maxY, bcs, by0, bH);
+    for (int yy = y0; yy <= y1; yy++)
+        for (int xx = x0; xx <= x1; xx++) list[atomicAdd(&cursor[yy * bW + xx], 1)] = r;
+}
+// insertion sort of each bin's list -> ascending rigid index
+__global__ void k_rbin_sort(int B, const int32_t *__restrict__ start, int32_t *__restrict__ list) {
+    int b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b >= B) return;
+    int s = start[b], e = start[b + 1];
+    for (int k = s + 1; k < e; k++) {
+        int v = list[k];
+        int j = k - 1;
+        while (j >= s && list[j] > v) { list[j + 1] = list[j]; j--; }
+        list[j + 1] = v;
+    }
+}
+
+// writeBackRigidBodies arithmetic (fluid.cpp:545-562), once per tick
+__global__ void k_rigid_writeback(int nr, lpe_gpu_rigid *__restrict__ rig,
+                                  float *__restrict__ accum, float *__restrict__ accum_out,
+                                  float damping) {
+    int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nr) return;
+    lpe_gpu_rigid &rb = rig[r];
+    float fx = accum[3 * r], fy = accum[3 * r + 1], tq = accum[3 * r + 2];
+    accum_out[3 * r] = fx; accum_out[3 * r + 1] = fy; accum_out[3 * r + 2] = tq;
+    float invMass = (rb.mass > 1e-12f) ? (1.f / rb.mass) : 0.f;
+    float invInertia = (rb.inertia > 1e-12f) ? (1.f / rb.inertia) : 0.f;
+    rb.vx += fx * invMass;
+    rb.vy += fy * invMass;
+    rb.vx *= damping;
+    rb.vy *= damping;
+    rb.omega += tq * invInertia;
+    rb.omega *= damping;
+    rb.accumFx = 0.f; rb.accumFy = 0.f; rb.accumTorque = 0.f;
+    accum[3 * r] = 0.f; accum[3 * r + 1] = 0.f; accum[3 * r + 2] = 0.f;
+}
+
+// reference cell index (metal:224-236) of each particle, written at its id
+__global__ void k_ref_cells(int n, float eps, const float *__restrict__ x,
+                            const float *__restrict__ y, const int32_t *__restrict__ id,
+                            const GridParams *__restrict__ gp, int32_t *__restrict__ out) {
+    int i = blockIdx.x * TPB + threadIdx.x;
+    if (i >= n) return;
+    const GridParams g = *gp;
+    int gx = (int)floorf((x[i] + eps) / g.cellSize);
+    int gy = (int)floorf((y[i] + eps) / g.cellSize);
+    int cx = gx - g.gridMinX, cy = gy - g.gridMinY;
+    out[id[i]] = (cx < 0 || cx >= g.gridDimX || cy < 0 || cy >= g.gridDimY) ? -1
+                                                                             : cy * g.gridDimX + cx;
+}
+
+struct Fields6 { const float *src[6]; float *dst[6]; };
+
+// scatter sorted-order arrays back to gather order (for downloads)
+__global__ void k_unpermute(int n, const int32_t *__restrict__ id, int nf, Fields6 f) {
+    int i = blockIdx.x * TPB + threadIdx.x;
+    if (i >= n) return;
+    int d = id[i];
+    for (int k = 0; k < nf; k++) f.dst[k][d] = f.src[k][i];
+}
+
+}  // namespace lpe
+
+using namespace lpe;
+
+// ===========================================================================
+// host side
+static inline int nblk(long n, int t = TPB) { return (int)((n + t - 1) / t); }
+
+static void pstate_free(PState &p) {
+    void *ptrs[] = {p.x, p.y, p.vx, p.vy, p.vhx, p.vhy, p.ax, p.ay, p.m, p.id};
+    for (void *q : ptrs) if (q) (void)hipFree(q);
+    p = PState();
+}
+
+static void sph_free(SphDev &d) {
+    pstate_free(d.P);
+    pstate_free(d.S);
+    void *ptrs[] = {d.rho, d.pr, d.key, d.tmpId, d.tmpOld, d.count, d.start, d.cursor,
+                    d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.accum, d.rbinStart,
+                    d.rbinList, d.rbinCount};
+    for (void *p : ptrs) if (p) (void)hipFree(p);
+    d = SphDev();
+}
+
+extern "C" int lpe_abi_version(void) { return LPE_ABI_VERSION; }
+
+extern "C" int lpe_device_count(int *count) {
+    if (!count) return LPE_ERR_ARG;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
+    *count = c;
+    return LPE_OK;
+}
+
+extern "C" int lpe_create(int device, lpe_ctx **out) {
+    if (!out) return LPE_ERR_ARG;
+    *out = nullptr;
+    int c = 0;
+    if (hipGetDeviceCount(&c) != hipSuccess || c <= 0) return LPE_ERR_NO_DEVICE;
+    if (device < 0 || device >= c) return LPE_ERR_ARG;
+    if (hipSetDevice(device) != hipSuccess) return LPE_ERR_HIP;
+    lpe_ctx *ctx = new lpe_ctx();
+    ctx->device = device;
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete ctx;
+        return LPE_ERR_HIP;
+    }
+    lpe_fluid_config_default(&ctx->sph.cfg);
+    *out = ctx;
+    return LPE_OK;
+}
+
+extern "C" int lpe_destroy(lpe_ctx *ctx) {
+    if (!ctx) return LPE_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    sph_free(ctx->sph);
+    lpe_rigid_destroy_internal(ctx);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return LPE_OK;
+}
+
+extern "C" const char *lpe_last_error(const lpe_ctx *ctx) {
+    return ctx ? ctx->err.c_str() : "null context";
+}
+
+extern "C" int lpe_sync(lpe_ctx *ctx) {
+    if (!ctx) return LPE_ERR_ARG;
+    LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LPE_OK;
+}
+
+extern "C" int lpe_fluid_config_default(lpe_fluid_config *c) {
+    if (!c) return LPE_ERR_ARG;
+    std::memset(c, 0, sizeof(*c));
+    c->gravity = 9.81f; c->restDensity = 0.5f; c->stiffness = 200.0f; c->viscosity = 0.03f;
+    c->positionSolver.safetyMargin = 0.001f; c->positionSolver.relaxFactor = 0.9f;
+    c->positionSolver.maxCorrection = 0.1f; c->positionSolver.maxVelocityUpdate = 1.0f;
+    c->positionSolver.minSafeDistance = 1e-10f; c->positionSolver.velocityDamping = 0.3f;
+    c->positionSolver.minPositionChange = 1e-6f;
+    c->impulseSolver.maxForce = 0.15f; c->impulseSolver.maxTorque = 0.03f;
+    c->impulseSolver.fluidForceScale = 100.0f; c->impulseSolver.fluidForceMax = 50000.0f;
+    c->impulseSolver.buoyancyStrength = 0.2f; c->impulseSolver.viscosityScale = 0.05f;
+    c->impulseSolver.depthScale = 0.04f; c->impulseSolver.depthTransitionRate = 2.0f;
+    c->impulseSolver.depthEstimateScale = 10.0f; c->impulseSolver.pressureForceRatio = 1.0f;
+    c->impulseSolver.viscousForceRatio = 0.3f; c->impulseSolver.angularDampingThreshold = 0.5f;
+    c->impulseSolver.angularDampingFactor = 0.005f; c->impulseSolver.maxSafeVelocitySq = 80.0f;
+    c->impulseSolver.minPenetration = 1e-6f; c->impulseSolver.minRelVelocity = 1e-6f;
+    c->gridConfig.gridEpsilon = 1e-6f; c->gridConfig.smoothingLength = 0.05f;
+    c->gridConfig.boundaryOffset = 0.001f;
+    c->numericalConfig.minDistanceThreshold = 1e-14f;
+    c->numericalConfig.minDensityThreshold = 1e-12f;
+    c->numericalConfig.minTimestep = 1e-10f; c->numericalConfig.fallbackTimestep = 1e-4f;
+    c->dampingFactor = 1.0f; c->numSubSteps = 10; c->threadsPerGroup = 256;
+    return LPE_OK;
+}
+
+extern "C" int lpe_sph_set_config(lpe_ctx *ctx, const lpe_fluid_config *cfg) {
+    if (!ctx || !cfg) return LPE_ERR_ARG;
+    if (cfg->numSubSteps < 0) return LPE_ERR_ARG;
+    ctx->sph.cfg = *cfg;
+    ctx->sph.cfg_set = true;
+    ctx->sph.rig_dirty = true;
+    return LPE_OK;
+}
+
+// cellSize = 2 * max(0.05, max_i h_i), h_i = smoothingLength (fluid.cpp:724-737)
+static float ref_cell_size(const lpe_fluid_config &c) {
+    float maxH = 0.05f;
+    if (c.gridConfig.smoothingLength > maxH) maxH = c.gridConfig.smoothingLength;
+    return 2.f * maxH;
+}
+
+// absolute device grid covering the particle bbox with a generous margin
+static int sph_plan_grid(lpe_ctx *ctx, const float *x, const float *y, int n) {
+    SphDev &d = ctx->sph;
+    float cs = ref_cell_size(d.cfg);
+    float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
+    for (int i = 0; i < n; i++) {
+        mnx = std::min(mnx, x[i]); mxx = std::max(mxx, x[i]);
+        mny = std::min(mny, y[i]); mxy = std::max(mxy, y[i]);
+    }
+    if (n == 0) { mnx = mny = 0.f; mxx = mxy = 1.f; }
+    // margin: 25% of the extent on every side, at least 64 cells
+    float ex = std::max(mxx - mnx, mxy - mny);
+    int pad = std::max(64, (int)(0.25f * ex / cs) + 8);
+    int gx0 = (int)std::floor(mnx / cs) - pad;
+    int gy0 = (int)std::floor(mny / cs) - pad;
+    int gx1 = (int)std::floor(mxx / cs) + pad;
+    int gy1 = (int)std::floor(mxy / cs) + pad;
+    d.cs = cs;
+    d.ox = gx0; d.oy = gy0;
+    d.W = gx1 - gx0 + 1; d.H = gy1 - gy0 + 1;
+    long C = 4L * d.W * d.H;
+    if (C > (1L << 29)) { ctx->err = "device grid too large"; return LPE_ERR_CAPACITY; }
+    if (C > d.cap_cells) {
+        if (d.count) (void)hipFree(d.count);
+        if (d.start) (void)hipFree(d.start);
+        if (d.cursor) (void)hipFree(d.cursor);
+        if (d.blocksum) (void)hipFree(d.blocksum);
+        d.count = d.start = d.cursor = d.blocksum = nullptr;
+        LPE_HIP(ctx, hipMalloc((void **)&d.count, sizeof(int32_t) * C));
+        LPE_HIP(ctx, hipMalloc((void **)&d.start, sizeof(int32_t) * (C + 1)));
+        LPE_HIP(ctx, hipMalloc((void **)&d.cursor, sizeof(int32_t) * C));
+        LPE_HIP(ctx, hipMalloc((void **)&d.blocksum, sizeof(int32_t) * (C / SCAN_ELEMS + 2)));
+        d.cap_cells = (int)C;
+    }
+    LPE_HIP(ctx, hipMemsetAsync(d.count, 0, sizeof(int32_t) * C, ctx->stream));
+    return LPE_OK;
+}
+
+static int pstate_alloc(lpe_ctx *ctx, PState &p, size_t N, bool with_a) {
+    float **fl[] = {&p.x, &p.y, &p.vx, &p.vy, &p.vhx, &p.vhy, &p.m};
+    for (float **q : fl) LPE_HIP(ctx, hipMalloc((void **)q, sizeof(float) * N));
+    if (with_a) {
+        LPE_HIP(ctx, hipMalloc((void **)&p.ax, sizeof(float) * N));
+        LPE_HIP(ctx, hipMalloc((void **)&p.ay, sizeof(float) * N));
+    }
+    LPE_HIP(ctx, hipMalloc((void **)&p.id, sizeof(int32_t) * N));
+    return LPE_OK;
+}
+
+static int sph_alloc_particles(lpe_ctx *ctx, int n) {
+    SphDev &d = ctx->sph;
+    if (n <= d.cap_n && d.P.x) return LPE_OK;
+    pstate_free(d.P);
+    pstate_free(d.S);
+    void *ptrs[] = {d.rho, d.pr, d.key, d.tmpId, d.tmpOld, d.bboxPart};
+    for (void *p : ptrs) if (p) (void)hipFree(p);
+    size_t N = (size_t)std::max(n, 1);
+    int st = pstate_alloc(ctx, d.P, N, true);
+    if (st) return st;
+    st = pstate_alloc(ctx, d.S, N, false);
+    if (st) return st;
+    LPE_HIP(ctx, hipMalloc((void **)&d.rho, sizeof(float) * N));
+    LPE_HIP(ctx, hipMalloc((void **)&d.pr, sizeof(float) * N));
+    LPE_HIP(ctx, hipMalloc((void **)&d.key, sizeof(uint32_t) * N));
+    LPE_HIP(ctx, hipMalloc((void **)&d.tmpId, sizeof(int32_t) * N));
+    LPE_HIP(ctx, hipMalloc((void **)&d.tmpOld, sizeof(int32_t) * N));
+    LPE_HIP(ctx, hipMalloc((void **)&d.bboxPart, sizeof(float4) * MAX_KICK_BLOCKS));
+    d.cap_n = n;
+    if (!d.gp) {
+        LPE_HIP(ctx, hipMalloc((void **)&d.gp, sizeof(GridParams)));
+        LPE_HIP(ctx, hipMalloc((void **)&d.status, sizeof(int32_t) * ST_COUNT));
+        LPE_HIP(ctx, hipMemsetAsync(d.gp, 0, sizeof(GridParams), ctx->stream));
+    }
+    return LPE_OK;
+}
+
+extern "C" int lpe_sph_upload(lpe_ctx *ctx, int n, const float *x, const float *y,
+                              const float *vx, const float *vy, const float *mass,
+                              const float *density, const float *pressure) {
+    if (!ctx || n < 0) return LPE_ERR_ARG;
+    if (n > 0 && (!x || !y || !vx || !vy || !mass)) return LPE_ERR_ARG;
+    (void)hipSetDevice(ctx->device);
+    SphDev &d = ctx->sph;
+    int st = sph_alloc_particles(ctx, n);
+    if (st) return st;
+    d.n = n;
+    d.rig_dirty = true;
+    st = sph_plan_grid(ctx, x, y, n);
+    if (st) return st;
+    size_t B = sizeof(float) * (size_t)n;
+    hipStream_t s = ctx->stream;
+    if (n > 0) {
+        std::vector<int32_t> ids(n);
+        for (int i = 0; i < n; i++) ids[i] = i;
+        LPE_HIP(ctx, hipMemcpyAsync(d.P.x, x, B, hipMemcpyHostToDevice, s));
+        LPE_HIP(ctx, hipMemcpyAsync(d.P.y, y, B, hipMemcpyHostToDevice, s));
+        LPE_HIP(ctx, hipMemcpyAsync(d.P.vx, vx, B, hipMemcpyHostToDevice, s));
+        LPE_HIP(ctx, hipMemcpyAsync(d.P.vy, vy, B, hipMemcpyHostToDevice, s));
+        LPE_HIP(ctx, hipMemcpyAsync(d.P.m, mass, B, hipMemcpyHostToDevice, s));
+        LPE_HIP(ctx, hipMemcpyAsync(d.P.vhx, vx, B, hipMemcpyHostToDevice, s));
+        LPE_HIP(ctx, hipMemcpyAsync(d.P.vhy, vy, B, hipMemcpyHostToDevice, s));
+        LPE_HIP(ctx, hipMemsetAsync(d.P.ax, 0, B, s));
+        LPE_HIP(ctx, hipMemsetAsync(d.P.ay, 0, B, s));
+        LPE_HIP(ctx, hipMemcpyAsync(d.P.id, ids.data(), sizeof(int32_t) * n,
+                                    hipMemcpyHostToDevice, s));
+        // density / pressure are carried from the ECS (fluid.cpp:294-295); they
+        // are recomputed before any use, and are stored in P's slot order
+        if (density) LPE_HIP(ctx, hipMemcpyAsync(d.rho, density, B, hipMemcpyHostToDevice, s));
+        else LPE_HIP(ctx, hipMemsetAsync(d.rho, 0, B, s));
+        if (pressure) LPE_HIP(ctx, hipMemcpyAsync(d.pr, pressure, B, hipMemcpyHostToDevice, s));
+        else LPE_HIP(ctx, hipMemsetAsync(d.pr, 0, B, s));
+        LPE_HIP(ctx, hipStreamSynchronize(s));
+    }
+    LPE_HIP(ctx, hipMemsetAsync(d.status, 0, sizeof(int32_t) * ST_COUNT, s));
+    return LPE_OK;
+}
+
+extern "C" int lpe_sph_upload_rigids(lpe_ctx *ctx, int r, const lpe_gpu_rigid *rigids) {
+    if (!ctx || r < 0 || (r > 0 && !rigids)) return LPE_ERR_ARG;
+    (void)hipSetDevice(ctx->device);
+    SphDev &d = ctx->sph;
+    if (r > d.cap_nr || !d.rig) {
+        if (d.rig) (void)hipFree(d.rig);
+        if (d.accum) (void)hipFree(d.accum);
+        LPE_HIP(ctx, hipMalloc((void **)&d.rig, sizeof(lpe_gpu_rigid) * (size_t)std::max(r, 1)));
+        LPE_HIP(ctx, hipMalloc((void **)&d.accum, sizeof(float) * 6 * (size_t)std::max(r, 1)));
+        d.cap_nr = std::max(r, 1);
+    }
+    d.nr = r;
+    if (r > 0) {
+        std::vector<lpe_gpu_rigid> tmp(rigids, rigids + r);
+        for (auto &b : tmp) b.accumFx = b.accumFy = b.accumTorque = 0.f;
+        LPE_HIP(ctx, hipMemcpyAsync(d.rig, tmp.data(), sizeof(lpe_gpu_rigid) * r,
+                                    hipMemcpyHostToDevice, ctx->stream));
+        LPE_HIP(ctx, hipMemsetAsync(d.accum, 0, sizeof(float) * 6 * r, ctx->stream));
+        LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
+    d.rig_dirty = true;
+    return LPE_OK;
+}
+
+static void sph_couple_params(const SphDev &d, CoupleParams &cp) {
+    const lpe_fluid_config &c = d.cfg;
+    cp.gravity = c.gravity; cp.restDensity = c.restDensity; cp.viscosity = c.viscosity;
+    cp.maxForce = c.impulseSolver.maxForce; cp.maxTorque = c.impulseSolver.maxTorque;
+    cp.viscosityScale = c.impulseSolver.viscosityScale; cp.depthScale = c.impulseSolver.depthScale;
+    cp.depthTransitionRate = c.impulseSolver.depthTransitionRate;
+    cp.pressureForceRatio = c.impulseSolver.pressureForceRatio;
+    cp.viscousForceRatio = c.impulseSolver.viscousForceRatio;
+    cp.angDampThr = c.impulseSolver.angularDampingThreshold;
+    cp.angDampFactor = c.impulseSolver.angularDampingFactor;
+    cp.depthEstimateScale = c.impulseSolver.depthEstimateScale;
+    cp.maxSafeVelocitySq = c.impulseSolver.maxSafeVelocitySq;
+    cp.minPenetration = c.impulseSolver.minPenetration;
+    cp.minRelVelocity = c.impulseSolver.minRelVelocity;
+    cp.fluidForceScale = c.impulseSolver.fluidForceScale;
+    cp.fluidForceMax = c.impulseSolver.fluidForceMax;
+    cp.buoyancyStrength = c.impulseSolver.buoyancyStrength;
+    cp.safetyMargin = c.positionSolver.safetyMargin;
+    cp.relaxFactor = c.positionSolver.relaxFactor;
+    cp.minSafeDistance = c.positionSolver.minSafeDistance;
+    cp.minPositionChange = c.positionSolver.minPositionChange;
+    cp.maxCorrection = c.positionSolver.maxCorrection;
+    cp.boundaryOffset = c.gridConfig.boundaryOffset;
+    cp.bx0 = d.bx0; cp.by0 = d.by0; cp.bW = d.bW; cp.bH = d.bH; cp.bcs = d.bcs;
+    cp.nr = d.nr;
+}
+
+// exclusive scan of C counts into start/cursor (and, for the fluid bins, the
+// bbox finish + reference grid)
+static int sph_scan(lpe_ctx *ctx, int C, int32_t *cnt, int32_t *start, int32_t *cursor,
+                    int32_t *bsum, int nparts, bool fluid) {
+    SphDev &d = ctx->sph;
+    int nb = (C + SCAN_ELEMS - 1) / SCAN_ELEMS;
+    hipStream_t s = ctx->stream;
+    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(TPB), 0, s, C, cnt, bsum);
+    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(TPB), 0, s, nb, bsum, start + C, d.bboxPart,
+                       nparts, d.cs, fluid ? d.gp : (GridParams *)nullptr, d.status);
+    hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(TPB), 0, s, C, d.W, d.ox, d.oy, cnt, bsum,
+                       start, cursor, d.gp, d.status, fluid ? 1 : 0);
+    LPE_CHECK_LAUNCH(ctx, "scan");
+    return LPE_OK;
+}
+
+static int sph_build_rigid_bins(lpe_ctx *ctx) {
+    SphDev &d = ctx->sph;
+    if (d.nr <= 0 || !d.rig_dirty) return LPE_OK;
+    // bin grid over the fluid device grid extent; bins of 0.25 m (>= 2h cells)
+    d.bcs = std::max(0.25f, d.cs);
+    d.bx0 = (int)std::floor(d.ox * d.cs / d.bcs) - 1;
+    d.by0 = (int)std::floor(d.oy * d.cs / d.bcs) - 1;
+    d.bW = (int)std::ceil(d.W * d.cs / d.bcs) + 3;
+    d.bH = (int)std::ceil(d.H * d.cs / d.bcs) + 3;
+    int B = d.bW * d.bH;
+    int nbs = (B + SCAN_ELEMS - 1) / SCAN_ELEMS;
+    if (B > d.cap_rbins) {
+        if (d.rbinStart) (void)hipFree(d.rbinStart);
+        if (d.rbinCount) (void)hipFree(d.rbinCount);
+        LPE_HIP(ctx, hipMalloc((void **)&d.rbinStart, sizeof(int32_t) * (B + 1)));
+        LPE_HIP(ctx, hipMalloc((void **)&d.rbinCount, sizeof(int32_t) * ((size_t)B * 2 + nbs + 4)));
+        d.cap_rbins = B;
+    }
+    hipStream_t s = ctx->stream;
+    LPE_HIP(ctx, hipMemsetAsync(d.rbinCount, 0, sizeof(int32_t) * B, s));
+    hipLaunchKernelGGL(k_rbin_count, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig, d.bcs,
+                       d.bx0, d.by0, d.bW, d.bH, d.rbinCount);
+    int32_t *cursor = d.rbinCount + B;
+    int st = sph_scan(ctx, B, d.rbinCount, d.rbinStart, cursor, d.rbinCount + 2 * B, 0, false);
+    if (st) return st;
+    // the list length is needed on the host once per rigid upload
+    int total = 0;
+    LPE_HIP(ctx, hipMemcpyAsync(&total, d.rbinStart + B, sizeof(int), hipMemcpyDeviceToHost, s));
+    LPE_HIP(ctx, hipStreamSynchronize(s));
+    if (total > d.cap_rlist || !d.rbinList) {
+        if (d.rbinList) (void)hipFree(d.rbinList);
+        LPE_HIP(ctx, hipMalloc((void **)&d.rbinList, sizeof(int32_t) * std::max(total, 1)));
+        d.cap_rlist = std::max(total, 1);
+    }
+    d.rlist_len = total;
+    hipLaunchKernelGGL(k_rbin_fill, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig, d.bcs,
+                       d.bx0, d.by0, d.bW, d.bH, cursor, d.rbinList);
+    hipLaunchKernelGGL(k_rbin_sort, dim3(nblk(B, 128)), dim3(128), 0, s, B, d.rbinStart, d.rbinList);
+    LPE_CHECK_LAUNCH(ctx, "rbin");
+    d.rig_dirty = false;
+    return LPE_OK;
+}
+
+// one grid hash: kick (unless probe) + histogram + scan + scatter + rank/permute
+static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool probe) {
+    SphDev &d = ctx->sph;
+    hipStream_t s = ctx->stream;
+    int C = 4 * d.W * d.H;
+    int kb = std::min(MAX_KICK_BLOCKS, std::max(1, nblk(d.n)));
+    hipLaunchKernelGGL(k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
+                       first ? 1 : 0, probe ? 1 : 0, d.cfg.gridConfig.gridEpsilon, d.cs, d.ox,
+                       d.oy, d.W, d.H, d.P, d.key, d.count, d.bboxPart, d.status);
+    LPE_CHECK_LAUNCH(ctx, "k_kick_drift");
+    int st = sph_scan(ctx, C, d.count, d.start, d.cursor, d.blocksum, kb, true);
+    if (st) return st;
+    hipLaunchKernelGGL(k_scatter, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.P.id, d.cursor,
+                       d.tmpId, d.tmpOld);
+    hipLaunchKernelGGL(k_rank_permute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.start,
+                       d.tmpId, d.tmpOld, d.P, d.S, probe ? 1 : 0);
+    LPE_CHECK_LAUNCH(ctx, "hash");
+    return LPE_OK;
+}
+
+static int sph_density(lpe_ctx *ctx) {
+    SphDev &d = ctx->sph;
+    const lpe_fluid_config &c = d.cfg;
+    hipLaunchKernelGGL(k_density, dim3(nblk(d.n)), dim3(TPB), 0, ctx->stream, d.n,
+                       c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
+                       c.restDensity, d.W, d.ox, d.oy, d.gp, d.start, d.S.x, d.S.y, d.S.m,
+                       d.rho, d.pr);
+    LPE_CHECK_LAUNCH(ctx, "k_density");
+    return LPE_OK;
+}
+
+extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
+    if (!ctx) return LPE_ERR_ARG;
+    SphDev &d = ctx->sph;
+    if (d.n <= 0) return LPE_OK;  // fluid.cpp:969-972
+    if (!d.P.x) return LPE_ERR_STATE;
+    (void)hipSetDevice(ctx->device);
+    const lpe_fluid_config &c = d.cfg;
+    float dt = (float)dt_tick;                       // fluid.cpp:592
+    float subDt = dt / (float)c.numSubSteps;         // fluid.cpp:593
+    float halfDt = 0.5f * subDt;
+    hipStream_t s = ctx->stream;
+    int st = sph_build_rigid_bins(ctx);
+    if (st) return st;
+    LPE_HIP(ctx, hipMemsetAsync(d.status + ST_MAX_OCC, 0, sizeof(int32_t), s));
+    SphStepParams sp;
+    sp.n = d.n; sp.W = d.W; sp.ox = d.ox; sp.oy = d.oy;
+    sp.h = c.gridConfig.smoothingLength; sp.eps = c.gridConfig.gridEpsilon;
+    sp.dt = subDt; sp.hdt = halfDt;
+    sp.viscosity = c.viscosity;
+    sp.minDist = c.numericalConfig.minDistanceThreshold;
+    sp.minDens = c.numericalConfig.minDensityThreshold;
+    CoupleParams cp;
+    sph_couple_params(d, cp);
+    for (int step = 0; step < c.numSubSteps; step++) {
+        st = sph_hash(ctx, subDt, halfDt, step == 0, false);
+        if (st) return st;
+        st = sph_density(ctx);
+        if (st) return st;
+        hipLaunchKernelGGL(k_forces_couple, dim3(nblk(d.n)), dim3(TPB), 0, s, sp, cp, d.gp,
+                           d.start, d.S, d.rho, d.pr, d.P, d.rig, d.rbinStart, d.rbinList,
+                           d.accum);
+        LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
+    }
+    if (d.nr > 0) {
+        hipLaunchKernelGGL(k_rigid_writeback, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig,
+                           d.accum, d.accum + 3 * d.nr, c.dampingFactor);
+        LPE_CHECK_LAUNCH(ctx, "k_rigid_writeback");
+    }
+    return LPE_OK;
+}
+
+// gather-order download of up to 6 sorted-order fields keyed by `id`; the S
+// arrays (dead between sub-steps) are the staging buffers
+static int sph_unpermute_download(lpe_ctx *ctx, const int32_t *id, int nf, const float **src,
+                                  float **host) {
+    SphDev &d = ctx->sph;
+    hipStream_t s = ctx->stream;
+    float *stage[6] = {d.S.x, d.S.y, d.S.vx, d.S.vy, d.S.vhx, d.S.vhy};
+    Fields6 f{};
+    for (int k = 0; k < nf; k++) { f.src[k] = src[k]; f.dst[k] = stage[k]; }
+    hipLaunchKernelGGL(k_unpermute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, id, nf, f);
+    LPE_CHECK_LAUNCH(ctx, "k_unpermute");
+    for (int k = 0; k < nf; k++)
+        if (host[k])
+            LPE_HIP(ctx, hipMemcpyAsync(host[k], stage[k], sizeof(float) * d.n,
+                                        hipMemcpyDeviceToHost, s));
+    LPE_HIP(ctx, hipStreamSynchronize(s));
+    return LPE_OK;
+}
+
+static int check_status(lpe_ctx *ctx) {
+    SphDev &d = ctx->sph;
+    if (!d.status) return LPE_OK;
+    int32_t status[ST_COUNT];
+    LPE_HIP(ctx, hipMemcpy(status, d.status, sizeof(status), hipMemcpyDeviceToHost));
+    if (status[ST_CAP_OVERFLOW]) {
+        ctx->err = "a fluid particle left the device grid capacity";
+        return LPE_ERR_CAPACITY;
+    }
+    return LPE_OK;
+}
+
+extern "C" int lpe_sph_download(lpe_ctx *ctx, float *x, float *y, float *vx, float *vy,
+                                float *density, float *pressure) {
+    if (!ctx) return LPE_ERR_ARG;
+    SphDev &d = ctx->sph;
+    if (d.n > 0) {
+        const float *src[6] = {d.P.x, d.P.y, d.P.vx, d.P.vy, d.rho, d.pr};
+        float *dst[6] = {x, y, vx, vy, density, pressure};
+        int st = sph_unpermute_download(ctx, d.P.id, 6, src, dst);
+        if (st) return st;
+    }
+    return check_status(ctx);
+}
+
+extern "C" int lpe_sph_download_aux(lpe_ctx *ctx, float *vxHalf, float *vyHalf, float *ax,
+                                    float *ay) {
+    if (!ctx) return LPE_ERR_ARG;
+    SphDev &d = ctx->sph;
+    if (d.n <= 0) return LPE_OK;
+    const float *src[4] = {d.P.vhx, d.P.vhy, d.P.ax, d.P.ay};
+    float *dst[4] = {vxHalf, vyHalf, ax, ay};
+    return sph_unpermute_download(ctx, d.P.id, 4, src, dst);
+}
+
+extern "C" int lpe_sph_download_rigids(lpe_ctx *ctx, lpe_gpu_rigid *rigids, float *accum) {
+    if (!ctx) return LPE_ERR_ARG;
+    SphDev &d = ctx->sph;
+    hipStream_t s = ctx->stream;
+    if (d.nr > 0) {
+        if (rigids)
+            LPE_HIP(ctx, hipMemcpyAsync(rigids, d.rig, sizeof(lpe_gpu_rigid) * d.nr,
+                                        hipMemcpyDeviceToHost, s));
+        if (accum)
+            LPE_HIP(ctx, hipMemcpyAsync(accum, d.accum + 3 * d.nr, sizeof(float) * 3 * d.nr,
+                                        hipMemcpyDeviceToHost, s));
+    }
+    LPE_HIP(ctx, hipStreamSynchronize(s));
+    return LPE_OK;
+}
+
+extern "C" int lpe_sph_get_stats(lpe_ctx *ctx, lpe_sph_stats *out) {
+    if (!ctx || !out) return LPE_ERR_ARG;
+    SphDev &d = ctx->sph;
+    std::memset(out, 0, sizeof(*out));
+    if (!d.status) return LPE_OK;
+    LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    int32_t status[ST_COUNT];
+    GridParams g;
+    LPE_HIP(ctx, hipMemcpy(status, d.status, sizeof(status), hipMemcpyDeviceToHost));
+    LPE_HIP(ctx, hipMemcpy(&g, d.gp, sizeof(g), hipMemcpyDeviceToHost));
+    out->maxCellOccupancy = status[ST_MAX_OCC];
+    out->notInserted = status[ST_NOT_INSERTED];
+    out->capacityOverflow = status[ST_CAP_OVERFLOW];
+    out->listOverflow = status[ST_LIST_OVERFLOW];
+    out->gridDimX = g.gridDimX; out->gridDimY = g.gridDimY;
+    out->gridMinX = g.gridMinX; out->gridMinY = g.gridMinY;
+    out->cellSize = g.cellSize;
+    return LPE_OK;
+}
+
+extern "C" int lpe_sph_probe_cells(lpe_ctx *ctx, int32_t *cell_index, lpe_sph_stats *stats) {
+    if (!ctx || !cell_index) return LPE_ERR_ARG;
+    SphDev &d = ctx->sph;
+    if (d.n <= 0) return LPE_OK;
+    (void)hipSetDevice(ctx->device);
+    LPE_HIP(ctx, hipMemsetAsync(d.status + ST_MAX_OCC, 0, sizeof(int32_t), ctx->stream));
+    int st = sph_hash(ctx, 0.f, 0.f, false, true);
+    if (st) return st;
+    hipLaunchKernelGGL(k_ref_cells, dim3(nblk(d.n)), dim3(TPB), 0, ctx->stream, d.n,
+                       d.cfg.gridConfig.gridEpsilon, d.P.x, d.P.y, d.P.id, d.gp, d.tmpId);
+    LPE_CHECK_LAUNCH(ctx, "k_ref_cells");
+    LPE_HIP(ctx, hipMemcpyAsync(cell_index, d.tmpId, sizeof(int32_t) * d.n, hipMemcpyDeviceToHost,
+                                ctx->stream));
+    LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (stats) return lpe_sph_get_stats(ctx, stats);
+    return LPE_OK;
+}
+
+extern "C" int lpe_sph_probe_density(lpe_ctx *ctx, float *density, float *pressure) {
+    if (!ctx) return LPE_ERR_ARG;
+    SphDev &d = ctx->sph;
+    if (d.n <= 0) return LPE_OK;
+    (void)hipSetDevice(ctx->device);
+    int st = sph_hash(ctx, 0.f, 0.f, false, true);
+    if (st) return st;
+    st = sph_density(ctx);
+    if (st) return st;
+    // rho/p are in S slot order here; S.x.. are the unpermute staging buffers,
+    // so keep S.id aside in tmpOld first
+    LPE_HIP(ctx, hipMemcpyAsync(d.tmpOld, d.S.id, sizeof(int32_t) * d.n, hipMemcpyDeviceToDevice,
+                                ctx->stream));
+    const float *src[2] = {d.rho, d.pr};
+    float *dst[2] = {density, pressure};
+    return sph_unpermute_download(ctx, d.tmpOld, 2, src, dst);
+}

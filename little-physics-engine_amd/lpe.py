@@ -1,0 +1,226 @@
+"""ctypes binding of the MI355X backend's C ABI (include/lpe.h).
+
+This is the Python-side caller used by tests/ and bench.py.  The production
+caller is the C++ host mirror under host/ (Systems::FluidSystem & co.), which
+binds the same symbols.  The library is the in-tree liblpe_hip.so; there is no
+fallback: if it is missing or has no device, calls fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "liblpe_hip.so")
+
+LPE_OK = 0
+STATUS = {0: "OK", 1: "ERR_HIP", 2: "ERR_ARG", 3: "ERR_STATE", 4: "ERR_CAPACITY",
+          5: "ERR_OVERFLOW", 6: "ERR_NO_DEVICE"}
+MAX_POLY_VERTS = 16
+
+
+class LpeError(RuntimeError):
+    pass
+
+
+# --------------------------------------------------------------------------
+# struct mirrors (include/lpe.h)
+class _PosSolver(C.Structure):
+    _fields_ = [(n, C.c_float) for n in (
+        "safetyMargin", "relaxFactor", "maxCorrection", "maxVelocityUpdate",
+        "minSafeDistance", "velocityDamping", "minPositionChange")]
+
+
+class _ImpSolver(C.Structure):
+    _fields_ = [(n, C.c_float) for n in (
+        "maxForce", "maxTorque", "fluidForceScale", "fluidForceMax", "buoyancyStrength",
+        "viscosityScale", "depthScale", "depthTransitionRate", "depthEstimateScale",
+        "pressureForceRatio", "viscousForceRatio", "angularDampingThreshold",
+        "angularDampingFactor", "maxSafeVelocitySq", "minPenetration", "minRelVelocity")]
+
+
+class _GridCfg(C.Structure):
+    _fields_ = [(n, C.c_float) for n in ("gridEpsilon", "smoothingLength", "boundaryOffset")]
+
+
+class _NumCfg(C.Structure):
+    _fields_ = [(n, C.c_float) for n in (
+        "minDistanceThreshold", "minDensityThreshold", "minTimestep", "fallbackTimestep")]
+
+
+class FluidConfig(C.Structure):
+    """Mirror of Systems::FluidConfig (fluid.hpp:131-200)."""
+    _fields_ = [("gravity", C.c_float), ("restDensity", C.c_float), ("stiffness", C.c_float),
+                ("viscosity", C.c_float), ("positionSolver", _PosSolver),
+                ("impulseSolver", _ImpSolver), ("gridConfig", _GridCfg),
+                ("numericalConfig", _NumCfg), ("dampingFactor", C.c_float),
+                ("numSubSteps", C.c_int), ("threadsPerGroup", C.c_int)]
+
+
+class SphStats(C.Structure):
+    _fields_ = [("maxCellOccupancy", C.c_int32), ("notInserted", C.c_int32),
+                ("capacityOverflow", C.c_int32), ("listOverflow", C.c_int32),
+                ("gridDimX", C.c_int32), ("gridDimY", C.c_int32),
+                ("gridMinX", C.c_int32), ("gridMinY", C.c_int32), ("cellSize", C.c_float)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# numpy mirror of lpe_gpu_rigid / Systems::GPURigidBody (fluid.hpp:94-125), 200 B
+RIGID_DTYPE = np.dtype([
+    ("shapeType", "<i4"), ("posX", "<f4"), ("posY", "<f4"), ("angle", "<f4"), ("radius", "<f4"),
+    ("vertCount", "<i4"), ("vertsX", "<f4", (MAX_POLY_VERTS,)), ("vertsY", "<f4", (MAX_POLY_VERTS,)),
+    ("vx", "<f4"), ("vy", "<f4"), ("omega", "<f4"), ("mass", "<f4"), ("inertia", "<f4"),
+    ("minX", "<f4"), ("maxX", "<f4"), ("minY", "<f4"), ("maxY", "<f4"),
+    ("accumFx", "<f4"), ("accumFy", "<f4"), ("accumTorque", "<f4")])
+assert RIGID_DTYPE.itemsize == 200
+
+_FP = C.POINTER(C.c_float)
+_IP = C.POINTER(C.c_int32)
+
+
+def _fp(a):
+    if a is None:
+        return None
+    assert a.dtype == np.float32 and a.flags.c_contiguous
+    return a.ctypes.data_as(_FP)
+
+
+_lib = None
+
+# every symbol declared in include/lpe.h (checked by tests/test_abi.py)
+SIGNATURES = {
+    "lpe_abi_version": ([], C.c_int),
+    "lpe_device_count": ([_IP], C.c_int),
+    "lpe_create": ([C.c_int, C.POINTER(C.c_void_p)], C.c_int),
+    "lpe_destroy": ([C.c_void_p], C.c_int),
+    "lpe_last_error": ([C.c_void_p], C.c_char_p),
+    "lpe_sync": ([C.c_void_p], C.c_int),
+    "lpe_fluid_config_default": ([C.POINTER(FluidConfig)], C.c_int),
+    "lpe_sph_set_config": ([C.c_void_p, C.POINTER(FluidConfig)], C.c_int),
+    "lpe_sph_upload": ([C.c_void_p, C.c_int] + [_FP] * 7, C.c_int),
+    "lpe_sph_upload_rigids": ([C.c_void_p, C.c_int, C.c_void_p], C.c_int),
+    "lpe_sph_step": ([C.c_void_p, C.c_double], C.c_int),
+    "lpe_sph_download": ([C.c_void_p] + [_FP] * 6, C.c_int),
+    "lpe_sph_download_aux": ([C.c_void_p] + [_FP] * 4, C.c_int),
+    "lpe_sph_download_rigids": ([C.c_void_p, C.c_void_p, _FP], C.c_int),
+    "lpe_sph_get_stats": ([C.c_void_p, C.POINTER(SphStats)], C.c_int),
+    "lpe_sph_probe_cells": ([C.c_void_p, _IP, C.POINTER(SphStats)], C.c_int),
+    "lpe_sph_probe_density": ([C.c_void_p, _FP, _FP], C.c_int),
+}
+
+
+def lib():
+    """Load the in-tree HIP library (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise LpeError(f"{LIB_PATH} not built: run `make` (or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, (args, res) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.argtypes = args
+            f.restype = res
+        _lib = L
+    return _lib
+
+
+def default_fluid_config() -> FluidConfig:
+    cfg = FluidConfig()
+    lib().lpe_fluid_config_default(C.byref(cfg))
+    return cfg
+
+
+def device_count() -> int:
+    c = C.c_int32(0)
+    lib().lpe_device_count(C.byref(c))
+    return c.value
+
+
+class Context:
+    """One lpe_ctx (one HIP device + stream)."""
+
+    def __init__(self, device: int = 0):
+        self._h = C.c_void_p()
+        st = lib().lpe_create(device, C.byref(self._h))
+        if st != LPE_OK:
+            raise LpeError(f"lpe_create(device={device}) failed: {STATUS.get(st, st)}")
+        self.n = 0
+        self.nr = 0
+
+    def close(self):
+        if self._h:
+            lib().lpe_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, st, what):
+        if st != LPE_OK:
+            msg = lib().lpe_last_error(self._h)
+            raise LpeError(f"{what}: {STATUS.get(st, st)}: {msg.decode() if msg else ''}")
+
+    def sync(self):
+        self._chk(lib().lpe_sync(self._h), "lpe_sync")
+
+    # ---- SPH -----------------------------------------------------------
+    def sph_set_config(self, cfg: FluidConfig):
+        self._chk(lib().lpe_sph_set_config(self._h, C.byref(cfg)), "lpe_sph_set_config")
+
+    def sph_upload(self, x, y, vx, vy, m, density=None, pressure=None):
+        arrs = [np.ascontiguousarray(a, dtype=np.float32) if a is not None else None
+                for a in (x, y, vx, vy, m, density, pressure)]
+        self._keep = arrs
+        self.n = int(arrs[0].shape[0])
+        self._chk(lib().lpe_sph_upload(self._h, self.n, *[_fp(a) for a in arrs]), "lpe_sph_upload")
+
+    def sph_upload_rigids(self, rigids):
+        r = np.ascontiguousarray(rigids, dtype=RIGID_DTYPE)
+        self.nr = int(r.shape[0])
+        self._chk(lib().lpe_sph_upload_rigids(self._h, self.nr, r.ctypes.data if self.nr else None),
+                  "lpe_sph_upload_rigids")
+
+    def sph_step(self, dt_tick: float):
+        self._chk(lib().lpe_sph_step(self._h, float(dt_tick)), "lpe_sph_step")
+
+    def sph_download(self):
+        out = {k: np.empty(self.n, np.float32) for k in ("x", "y", "vx", "vy", "density", "pressure")}
+        self._chk(lib().lpe_sph_download(self._h, *[_fp(out[k]) for k in
+                  ("x", "y", "vx", "vy", "density", "pressure")]), "lpe_sph_download")
+        aux = {k: np.empty(self.n, np.float32) for k in ("vxHalf", "vyHalf", "ax", "ay")}
+        self._chk(lib().lpe_sph_download_aux(self._h, *[_fp(aux[k]) for k in
+                  ("vxHalf", "vyHalf", "ax", "ay")]), "lpe_sph_download_aux")
+        out.update(aux)
+        return out
+
+    def sph_download_rigids(self):
+        r = np.zeros(self.nr, RIGID_DTYPE)
+        acc = np.zeros(3 * max(self.nr, 1), np.float32)
+        self._chk(lib().lpe_sph_download_rigids(self._h, r.ctypes.data if self.nr else None,
+                                                _fp(acc)), "lpe_sph_download_rigids")
+        return r, acc[:3 * self.nr].reshape(-1, 3)
+
+    def sph_stats(self) -> dict:
+        s = SphStats()
+        self._chk(lib().lpe_sph_get_stats(self._h, C.byref(s)), "lpe_sph_get_stats")
+        return s.as_dict()
+
+    def sph_probe_cells(self):
+        cells = np.empty(self.n, np.int32)
+        s = SphStats()
+        self._chk(lib().lpe_sph_probe_cells(self._h, cells.ctypes.data_as(_IP), C.byref(s)),
+                  "lpe_sph_probe_cells")
+        return cells, s.as_dict()
+
+    def sph_probe_density(self):
+        rho = np.empty(self.n, np.float32)
+        p = np.empty(self.n, np.float32)
+        self._chk(lib().lpe_sph_probe_density(self._h, _fp(rho), _fp(p)), "lpe_sph_probe_density")
+        return rho, p

@@ -1,0 +1,246 @@
+"""Seeded synthetic scenes and the reference's gathers.
+
+The reference scenarios seed from time() (simple_fluid.cpp:130,
+fluid_and_polygons.cpp:126), so scenes here come from this generator
+(numpy PCG64 with a fixed seed) and reuse the reference's entity recipes:
+walls after makeWall / makeBoundaryWall (simple_fluid.cpp:19-54), pentagons
+after fluid_and_polygons.cpp:141-160, fluid lattices after
+simple_fluid.cpp:131-139.  Creation order is walls, then rigids, then fluid.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+try:
+    from . import lpe as _lpe  # type: ignore
+except ImportError:  # loaded by path
+    import importlib.util
+    import os
+    _spec = importlib.util.spec_from_file_location(
+        "lpe", os.path.join(os.path.dirname(os.path.abspath(__file__)), "lpe.py"))
+    _lpe = importlib.util.module_from_spec(_spec)
+    _spec.loader.exec_module(_lpe)
+
+RIGID_DTYPE = _lpe.RIGID_DTYPE
+MAX_POLY_VERTS = _lpe.MAX_POLY_VERTS
+
+LATTICE_S = 0.025                    # lattice spacing s = h/2
+FLUID_MASS = 0.5 * LATTICE_S ** 2    # m = rho0 * s^2 (rho0 = 0.5, fluid.hpp:135)
+WALL_MASS = 1e30
+WALL_THICK = 0.1
+
+
+# ---------------------------------------------------------------------------
+# shape builders (polygon.hpp:154-284), double precision
+def regular_polygon(sides: int, sz: float) -> np.ndarray:
+    """buildRegularPolygon (polygon.hpp:154-167): (sz cos a, -sz sin a)."""
+    step = 2.0 * math.pi / float(sides)
+    return np.array([(sz * math.cos(i * step), -sz * math.sin(i * step)) for i in range(sides)],
+                    dtype=np.float64)
+
+
+def random_convex_polygon(rng, sz: float) -> np.ndarray:
+    """buildRandomConvexPolygon (polygon.hpp:182-203) with this generator's rng."""
+    sides = int(rng.integers(3, 8))
+    step = 2.0 * math.pi / float(sides)
+    angle = 0.0
+    out = []
+    for _ in range(sides):
+        r = float(rng.uniform(0.5 * sz, sz))
+        out.append((r * math.cos(angle), -r * math.sin(angle)))
+        angle += step
+    return np.array(out, dtype=np.float64)
+
+
+def polygon_inertia(verts: np.ndarray, mass: float) -> float:
+    """calculatePolygonInertia (polygon.hpp:266-284), same summation order."""
+    num = 0.0
+    den = 0.0
+    n = len(verts)
+    for i in range(n):
+        j = (i + 1) % n
+        xi, yi = float(verts[i, 0]), float(verts[i, 1])
+        xj, yj = float(verts[j, 0]), float(verts[j, 1])
+        cross = xi * yj - yi * xj
+        num += cross * ((xi * xi + yi * yi) + (xi * xj + yi * yj) + (xj * xj + yj * yj))
+        den += cross
+    return (mass * num) / (6.0 * den)
+
+
+# ---------------------------------------------------------------------------
+class Bodies:
+    """Solid bodies in creation order (walls first).  Mirrors the components
+    the reference's rigid path reads: Position, Velocity, Mass, AngularPosition,
+    AngularVelocity, Inertia, Boundary, Sleep, PolygonShape / CircleShape."""
+
+    def __init__(self):
+        self.rows = []
+
+    def add(self, **kw):
+        row = dict(x=0.0, y=0.0, vx=0.0, vy=0.0, mass=1.0, angle=0.0, omega=0.0,
+                   has_angpos=True, has_angvel=False, has_inertia=False, inertia=1.0,
+                   boundary=False, has_sleep=True, asleep=False, sleep_counter=0,
+                   circle=False, radius=0.0, verts=None, shape_size=0.0)
+        row.update(kw)
+        self.rows.append(row)
+
+    def __len__(self):
+        return len(self.rows)
+
+
+def add_walls(b: Bodies, U: float):
+    """Four Boundary walls (simple_fluid.cpp:19-54, :87-108): mass 1e30, asleep."""
+    hw = WALL_THICK * 0.5
+    for (cx, cy, halfW, halfH) in ((0.0, U * 0.5, hw, U * 0.5), (U, U * 0.5, hw, U * 0.5),
+                                   (U * 0.5, 0.0, U * 0.5, hw), (U * 0.5, U, U * 0.5, hw)):
+        verts = np.array([(-halfW, -halfH), (-halfW, halfH), (halfW, halfH), (halfW, -halfH)],
+                         np.float64)
+        b.add(x=cx, y=cy, mass=WALL_MASS, boundary=True, asleep=True, sleep_counter=9999999,
+              verts=verts, shape_size=halfH, has_angvel=False, has_inertia=False)
+
+
+def add_pentagon_lattice(b: Bodies, rng, nx, ny, x0, y0, pitch, radius_fn, mass_mean=5.0,
+                         mass_std=0.2, vel_scale=0.5):
+    """Pentagons after fluid_and_polygons.cpp:141-160 on an nx x ny lattice."""
+    i = 0
+    for row in range(ny):
+        for col in range(nx):
+            r = radius_fn(i)
+            verts = regular_polygon(5, r)
+            mass = max(0.1, float(rng.normal(mass_mean, mass_std)))
+            vx = float(rng.normal(0.0, vel_scale)) * 0.2
+            vy = abs(float(rng.normal(0.0, vel_scale)))
+            b.add(x=x0 + col * pitch, y=y0 + row * pitch, vx=vx, vy=vy, mass=mass,
+                  verts=verts, shape_size=r, has_angvel=True, has_inertia=True,
+                  inertia=polygon_inertia(verts, mass))
+            i += 1
+
+
+def fluid_lattice(rng, nx, ny, x0, y0, s=LATTICE_S, mass=FLUID_MASS):
+    """nx x ny lattice at spacing s with uniform jitter +-0.1 s
+    (simple_fluid.cpp:131-139).  Row-major creation order; float64 like the ECS."""
+    col = np.tile(np.arange(nx, dtype=np.float64), ny)
+    row = np.repeat(np.arange(ny, dtype=np.float64), nx)
+    jx = rng.uniform(-0.1, 0.1, nx * ny) * s
+    jy = rng.uniform(-0.1, 0.1, nx * ny) * s
+    x = x0 + (col + 0.5) * s + jx
+    y = y0 + (row + 0.5) * s + jy
+    n = nx * ny
+    return dict(x=x, y=y, vx=np.zeros(n), vy=np.zeros(n), mass=np.full(n, mass),
+                density=np.zeros(n), pressure=np.zeros(n))
+
+
+# ---------------------------------------------------------------------------
+def gather_rigids(b: Bodies, order=None) -> np.ndarray:
+    """FluidSystem::gatherRigidBodies (fluid.cpp:304-438) for the given body
+    order: float pose, polygon world verts computed in double from
+    float(angle) and cast to float, AABB of the float verts; circles use
+    float radius.  Missing mass/inertia default to 1."""
+    idx = list(range(len(b))) if order is None else list(order)
+    out = np.zeros(len(idx), RIGID_DTYPE)
+    for k, i in enumerate(idx):
+        r = b.rows[i]
+        rb = out[k]
+        posX = np.float32(r["x"])
+        posY = np.float32(r["y"])
+        angle = np.float32(r["angle"]) if r["has_angpos"] else np.float32(0.0)
+        rb["posX"], rb["posY"], rb["angle"] = posX, posY, angle
+        rb["vx"], rb["vy"] = np.float32(r["vx"]), np.float32(r["vy"])
+        rb["omega"] = np.float32(r["omega"]) if r["has_angvel"] else np.float32(0.0)
+        rb["mass"] = np.float32(r["mass"])
+        rb["inertia"] = np.float32(r["inertia"]) if r["has_inertia"] else np.float32(1.0)
+        if r["circle"]:
+            rad = np.float32(r["radius"])
+            rb["shapeType"] = 0
+            rb["radius"] = rad
+            rb["vertCount"] = 0
+            rb["minX"], rb["maxX"] = posX - rad, posX + rad
+            rb["minY"], rb["maxY"] = posY - rad, posY + rad
+        else:
+            verts = r["verts"][:MAX_POLY_VERTS]
+            rb["shapeType"] = 1
+            rb["vertCount"] = len(verts)
+            c = math.cos(float(angle))
+            s = math.sin(float(angle))
+            wx = np.array([r["x"] + (lx * c - ly * s) for lx, ly in verts], np.float64)
+            wy = np.array([r["y"] + (lx * s + ly * c) for lx, ly in verts], np.float64)
+            fx = wx.astype(np.float32)
+            fy = wy.astype(np.float32)
+            rb["vertsX"][:len(verts)] = fx
+            rb["vertsY"][:len(verts)] = fy
+            rb["minX"], rb["maxX"] = fx.min(), fx.max()
+            rb["minY"], rb["maxY"] = fy.min(), fy.max()
+    return out
+
+
+# ---------------------------------------------------------------------------
+# named scenes
+def scene(name: str):
+    """Returns dict(U, fluid, bodies, seed, desc)."""
+    if name == "C2":     # 64k SPH dam break, U = 20 m, R = 4 walls
+        U, seed = 20.0, 2
+        rng = np.random.default_rng(seed)
+        b = Bodies()
+        add_walls(b, U)
+        fl = fluid_lattice(rng, 256, 256, 0.15, U - 0.15 - 256 * LATTICE_S)
+        return dict(U=U, fluid=fl, bodies=b, seed=seed, desc="C2: 256x256 dam break, U=20")
+    if name == "C4":     # 256k SPH + 512 pentagons, U = 32 m
+        U, seed = 32.0, 4
+        rng = np.random.default_rng(seed)
+        b = Bodies()
+        add_walls(b, U)
+        sizes = (0.25, 0.35, 0.45)
+        fx0 = 0.5 * (U - 512 * LATTICE_S)
+        add_pentagon_lattice(b, rng, 32, 16, 0.5 * (U - 31 * 0.9), U - 0.15 - 512 * LATTICE_S - 16 * 0.9,
+                             0.9, lambda i: sizes[i % 3])
+        fl = fluid_lattice(rng, 512, 512, fx0, U - 0.15 - 512 * LATTICE_S)
+        return dict(U=U, fluid=fl, bodies=b, seed=seed, desc="C4: 512x512 SPH + 512 pentagons, U=32")
+    if name == "M":      # metric scene: 256k SPH + 4096 pentagons (+4 walls), U = 32 m
+        U, seed = 32.0, 6
+        rng = np.random.default_rng(seed)
+        b = Bodies()
+        add_walls(b, U)
+        pool_top = U - 0.15 - 256 * LATTICE_S
+        add_pentagon_lattice(b, rng, 128, 32, 0.5 * (U - 127 * 0.24), pool_top - 0.3 - 31 * 0.24,
+                             0.24, lambda i: 0.1)
+        fl = fluid_lattice(rng, 1024, 256, 0.5 * (U - 1024 * LATTICE_S), pool_top)
+        return dict(U=U, fluid=fl, bodies=b, seed=seed,
+                    desc="M: 1024x256 SPH pool + 4096 pentagons (128x32 @0.24 m), U=32")
+    if name.startswith("small"):   # test scenes: small{N} fluid + a few rigids
+        parts = name[5:].split("_")
+        side = int(parts[0]) if parts and parts[0] else 64
+        nrig = int(parts[1]) if len(parts) > 1 else 8
+        U, seed = 6.0, 11 + side + nrig
+        rng = np.random.default_rng(seed)
+        b = Bodies()
+        add_walls(b, U)
+        x0 = 0.5 * (U - side * LATTICE_S)
+        top = U - 0.15 - side * LATTICE_S
+        if nrig:
+            ncol = max(1, int(math.ceil(math.sqrt(nrig))))
+            nrow = (nrig + ncol - 1) // ncol
+            add_pentagon_lattice(b, rng, ncol, nrow, x0 + 0.2, top + 0.12, 0.3,
+                                 lambda i: 0.1 + 0.02 * (i % 3))
+            del b.rows[4 + nrig:]
+        fl = fluid_lattice(rng, side, side, x0, top)
+        return dict(U=U, fluid=fl, bodies=b, seed=seed, desc=f"small: {side}^2 fluid + {nrig} pentagons")
+    raise KeyError(name)
+
+
+def particles_aos(fl) -> np.ndarray:
+    """GPUFluidParticle array as gatherFluidParticles builds it (fluid.cpp:282-295)."""
+    from_keys = ("x", "y", "vx", "vy")
+    n = len(fl["x"])
+    p = np.zeros((n, 13), np.float32)
+    for k, name in enumerate(from_keys):
+        p[:, k] = fl[name].astype(np.float32)
+    p[:, 4] = p[:, 2]
+    p[:, 5] = p[:, 3]
+    p[:, 8] = fl["mass"].astype(np.float32)
+    p[:, 9] = 0.05
+    p[:, 10] = 1000.0
+    p[:, 11] = fl["density"].astype(np.float32)
+    p[:, 12] = fl["pressure"].astype(np.float32)
+    return p

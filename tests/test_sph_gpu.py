@@ -1,0 +1,129 @@
+"""GPU parity of the SPH path (HIP, through the C ABI) against the CPU oracle.
+
+Bar (BASELINE.json north_star): bit-exact reference grid-cell indices; fp32
+state within 1e-5 relative.  Without rigid contact the HIP path is expected to
+be bit-identical to oracle/sph_oracle.c (same canonical orders, no FMA
+contraction, correctly rounded div/sqrt); with rigid coupling the device
+tanhf/powf and the float-atomic rigid accumulators allow ulp-level drift, so
+those cases use the 1e-5 relative bar (scaled by the field's magnitude).
+"""
+import numpy as np
+import pytest
+
+from conftest import lpe, scenes
+
+pytestmark = pytest.mark.gpu
+DT = 1.0 / 120.0
+
+
+def _upload(ctx, fl, rigids=None, cfg=None):
+    ctx.sph_set_config(cfg or lpe.default_fluid_config())
+    ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+    ctx.sph_upload_rigids(rigids if rigids is not None else np.zeros(0, lpe.RIGID_DTYPE))
+
+
+def _close(a, b, rtol=1e-5, scale=None):
+    a = np.asarray(a, np.float64)
+    b = np.asarray(b, np.float64)
+    sc = np.maximum(np.abs(b), scale if scale is not None else 0.0)
+    return np.abs(a - b) <= rtol * sc + 1e-30
+
+
+@pytest.mark.parametrize("name", ["small64_0", "small96_0"])
+def test_cells_bit_exact(gpu_ctx, oracle_mod, name):
+    s = scenes.scene(name)
+    _upload(gpu_ctx, s["fluid"])
+    cells, st = gpu_ctx.sph_probe_cells()
+    ref, g = oracle_mod.cells(scenes.particles_aos(s["fluid"]))
+    assert (st["gridMinX"], st["gridMinY"], st["gridDimX"], st["gridDimY"]) == \
+        (g.gridMinX, g.gridMinY, g.gridDimX, g.gridDimY)
+    np.testing.assert_array_equal(cells, ref)
+
+
+def test_cells_not_inserted_edge(gpu_ctx, oracle_mod):
+    """A particle within eps below a cell boundary at the global max is 'not
+    inserted' (fluid.cpp:745-746 has no epsilon, metal:224-226 does)."""
+    rng = np.random.default_rng(5)
+    n = 2000
+    x = rng.uniform(1.0, 2.0, n)
+    y = rng.uniform(1.0, 2.0, n)
+    x[0] = np.float32(2.3) - np.float32(5e-7)   # max x, just below the 2.3 boundary
+    y[1] = np.float32(2.4) - np.float32(4e-7)
+    fl = dict(x=x, y=y, vx=np.zeros(n), vy=np.zeros(n), mass=np.full(n, scenes.FLUID_MASS),
+              density=np.zeros(n), pressure=np.zeros(n))
+    _upload(gpu_ctx, fl)
+    cells, st = gpu_ctx.sph_probe_cells()
+    ref, g = oracle_mod.cells(scenes.particles_aos(fl))
+    assert (ref < 0).sum() >= 1
+    np.testing.assert_array_equal(cells, ref)
+    assert st["notInserted"] == int((ref < 0).sum())
+
+
+@pytest.mark.parametrize("name", ["small64_0", "small96_0"])
+def test_density_bit_exact(gpu_ctx, oracle_mod, name):
+    s = scenes.scene(name)
+    _upload(gpu_ctx, s["fluid"])
+    rho, p = gpu_ctx.sph_probe_density()
+    rrho, rp, g, st = oracle_mod.density(scenes.particles_aos(s["fluid"]))
+    np.testing.assert_array_equal(rho, rrho)
+    np.testing.assert_array_equal(p, rp)
+
+
+def test_tick_walls_only_bit_exact(gpu_ctx, oracle_mod):
+    """One full tick (10 sub-steps) with only the 4 walls (R > 0 dispatches the
+    impulse kernel, but no particle touches a wall)."""
+    s = scenes.scene("small64_0")
+    rig = scenes.gather_rigids(s["bodies"])
+    _upload(gpu_ctx, s["fluid"], rig)
+    gpu_ctx.sph_step(DT)
+    out = gpu_ctx.sph_download()
+    ref, rref, acc, st = oracle_mod.fluid_tick(scenes.particles_aos(s["fluid"]), rig, DT)
+    for k, col in (("x", 0), ("y", 1), ("vx", 2), ("vy", 3), ("vxHalf", 4), ("vyHalf", 5),
+                   ("ax", 6), ("ay", 7), ("density", 11), ("pressure", 12)):
+        np.testing.assert_array_equal(out[k], ref[:, col], err_msg=k)
+    stats = gpu_ctx.sph_stats()
+    assert stats["maxCellOccupancy"] == st.maxOcc
+    assert stats["maxCellOccupancy"] <= lpe_max_per_cell()
+
+
+def lpe_max_per_cell():
+    return 64
+
+
+@pytest.mark.parametrize("name", ["small64_8", "small96_12"])
+def test_tick_coupled(gpu_ctx, oracle_mod, name):
+    """One tick with pentagons sinking into the fluid: impulse + push-out.
+    The fluid state is bit-identical (canonical orders, fp64-rounded tanh/pow);
+    the rigid accumulators are float atomics on the GPU (the reference uses
+    float atomics too, metal:892-898), so they match to summation-order ulps."""
+    s = scenes.scene(name)
+    rig = scenes.gather_rigids(s["bodies"])
+    _upload(gpu_ctx, s["fluid"], rig)
+    gpu_ctx.sph_step(DT)
+    out = gpu_ctx.sph_download()
+    r_out, acc = gpu_ctx.sph_download_rigids()
+    ref, rref, racc, st = oracle_mod.fluid_tick(scenes.particles_aos(s["fluid"]), rig, DT)
+    assert np.abs(racc).sum() > 0, "scene must exercise the coupling"
+    for k, col in (("x", 0), ("y", 1), ("vx", 2), ("vy", 3), ("vxHalf", 4), ("vyHalf", 5),
+                   ("ax", 6), ("ay", 7), ("density", 11), ("pressure", 12)):
+        np.testing.assert_array_equal(out[k], ref[:, col], err_msg=k)
+    for j in range(3):
+        tot = np.abs(racc[:, j]).max()
+        np.testing.assert_allclose(acc[:, j], racc[:, j], rtol=1e-5, atol=1e-6 * tot + 1e-12)
+    for k in ("vx", "vy", "omega"):
+        np.testing.assert_allclose(r_out[k], rref[k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def test_multi_tick_invariants(gpu_ctx):
+    """Several resident ticks: finite state, occupancy within the reference cap."""
+    s = scenes.scene("small96_12")
+    rig = scenes.gather_rigids(s["bodies"])
+    _upload(gpu_ctx, s["fluid"], rig)
+    for _ in range(5):
+        gpu_ctx.sph_step(DT)
+    out = gpu_ctx.sph_download()
+    for k in ("x", "y", "vx", "vy", "density"):
+        assert np.isfinite(out[k]).all(), k
+    st = gpu_ctx.sph_stats()
+    assert st["capacityOverflow"] == 0
+    assert 0 < st["maxCellOccupancy"] <= 64
