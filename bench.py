@@ -1,0 +1,191 @@
+"""bench.py — physics steps/s of the MI355X backend on the metric scene.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--scene M]
+
+A step is one tick (ECSSimulator::tick, src/sim.cpp:156-163) of the resident
+device pipeline on the scene BASELINE.json's metric is quoted on: M = 256k SPH
+particles + 4096 pentagons + 4 walls, synthetic seeded input
+already resident in HBM.  For N > 1 (torch.distributed.run, one rank per GPU)
+every rank advances its own replica of the scene (weak scaling, no data-path
+collective); the control plane (barrier, max over ranks) uses gloo.
+
+Rank 0 prints ONE JSON line (the driver contract), including the live
+roofline of the dominant kernel (HIP events on the library's stream) and the
+CPU baseline (the oracle, 1 thread, on a bounded sample of the same workload).
+"""
+from __future__ import annotations
+
+import argparse
+import importlib.util
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "little-physics-engine_amd")
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+
+def _load(name, path):
+    if name in sys.modules:
+        return sys.modules[name]
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+# Algorithmic (compulsory) bytes per launch, SURVEY.md §8(d) staged model
+# (fp32 SoA, per particle per sub-step); C = reference grid cells.
+def kernel_bytes(name, n, cells):
+    model = {
+        "k_kick_drift": 44.0 * n,                    # x,y,vx,vy,ax,ay -> x,y,vh + key
+        "k_density": 24.0 * n + 8.0 * cells,         # idx,x,y,m -> rho,p ; cell ranges
+        "k_forces_couple": (40.0 + 24.0 + 8.0) * n,  # forces + finish + coupling test
+        "k_scatter": 12.0 * n / 2.0,                 # counting sort (12 B) split over
+        "k_rank_permute": 12.0 * n / 2.0,            #   scatter + rank
+    }
+    return model.get(name)
+
+
+def cpu_baseline(scene_name, budget_s=20.0):
+    """The oracle (C restatement, 1 thread) ticking the same scene."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle  # noqa: E402  (checker / baseline only)
+    scenes = _load("scenes", os.path.join(PKG, "scenes.py"))
+    s = scenes.scene(scene_name)
+    p = scenes.particles_aos(s["fluid"])
+    rig = scenes.gather_rigids(s["bodies"])
+    ticks = 0
+    t0 = time.perf_counter()
+    while True:
+        p, rig, _, _ = oracle.fluid_tick(p, rig, 1.0 / 120.0)
+        ticks += 1
+        el = time.perf_counter() - t0
+        if el > budget_s or el / ticks * (ticks + 1) > budget_s * 1.5:
+            break
+    return dict(value=ticks / el, unit="ticks/s", cores=1, kind="port",
+                sample=f"{ticks} tick(s) of scene {scene_name} ({len(p)} SPH particles, "
+                       f"{len(rig)} rigids) through oracle/sph_oracle.c, 1 thread, -O2")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--scene", default="M")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+
+    lpe = _load("lpe", os.path.join(PKG, "lpe.py"))
+    scenes = _load("scenes", os.path.join(PKG, "scenes.py"))
+    s = scenes.scene(args.scene)
+    fl = s["fluid"]
+    rig = scenes.gather_rigids(s["bodies"])
+    dt_tick = 1.0 / 120.0
+
+    ctx = lpe.Context(local)
+    ctx.sph_set_config(lpe.default_fluid_config())
+    ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+    ctx.sph_upload_rigids(rig)
+
+    for _ in range(args.warmup):
+        ctx.sph_step(dt_tick)
+    ctx.sync()
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+
+    ctx.timing(True)
+    ctx.timing_reset()
+    barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        ctx.sph_step(dt_tick)
+    ctx.sync()
+    t1 = time.perf_counter()
+    barrier()
+    elapsed = t1 - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    times = ctx.timing_read()
+    ctx.timing(False)
+    stats = ctx.sph_stats()
+    out = ctx.sph_download()   # also checks the capacity flag
+
+    if rank != 0:
+        if dist is not None:
+            dist.barrier()
+        return
+
+    import numpy as np
+    assert np.isfinite(out["x"]).all() and np.isfinite(out["vy"]).all()
+    n = len(fl["x"])
+    cells = stats["gridDimX"] * stats["gridDimY"]
+    dom = max(times.items(), key=lambda kv: kv[1][0])
+    dname, (dms, dcalls) = dom
+    avg_s = dms / max(dcalls, 1) / 1e3
+    b = kernel_bytes(dname, n, cells)
+    roof = None
+    if b is not None:
+        ach = b / avg_s / 1e9
+        roof = dict(kernel=dname, bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS,
+                    unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4), traffic=None,
+                    avg_us=round(avg_s * 1e6, 2), algorithmic_bytes=b)
+    dens = times.get("k_density")
+    roof_d = None
+    if dens:
+        avg_d = dens[0] / max(dens[1], 1) / 1e3
+        bd = kernel_bytes("k_density", n, cells)
+        roof_d = dict(kernel="k_density", achieved=round(bd / avg_d / 1e9, 1), unit="GB/s",
+                      frac=round(bd / avg_d / 1e9 / HBM_PEAK_GBS, 4), avg_us=round(avg_d * 1e6, 2))
+    value = world * args.steps / elapsed
+    line = {
+        "metric": "physics steps/sec at 256k SPH + 4k rigids; 1/2/4/8 MI355X vs HBM roofline",
+        "value": round(value, 2),
+        "unit": "ticks/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded scene generator, SURVEY.md §8(d))",
+        "config": {"workload": s["desc"], "scene": args.scene, "fluid_particles": n,
+                   "rigid_bodies": len(rig), "substeps": 10, "dt": dt_tick,
+                   "systems": ["FluidSystem (SPH + rigid-fluid coupling)"],
+                   "parallelism": f"replica x{world}"},
+        "roofline": roof,
+        "roofline_density": roof_d,
+        "kernels_us": {k: round(v[0] / max(v[1], 1) * 1e3, 2) for k, v in times.items()},
+        "max_cell_occupancy": stats["maxCellOccupancy"],
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(args.scene)
+    print(json.dumps(line))
+    if dist is not None:
+        dist.barrier()
+
+
+if __name__ == "__main__":
+    main()

@@ -143,6 +143,17 @@ int  lpe_device_count(int *count);
 /* Blocks until all work queued on the context's stream is done. */
 int  lpe_sync(lpe_ctx *ctx);
 
+/* ---- kernel timing (bench / profiling; no reference counterpart) ------- */
+/* When enabled, every launch of a named kernel on the context's stream is
+ * bracketed by a pair of HIP events.  lpe_timing_read() waits for the stream,
+ * accumulates the event durations and returns, for the i-th kernel name seen,
+ * its name, total milliseconds and launch count (returns LPE_ERR_ARG when i is
+ * past the last name).  lpe_timing_reset() clears the totals. */
+int  lpe_timing_enable(lpe_ctx *ctx, int on);
+int  lpe_timing_reset(lpe_ctx *ctx);
+int  lpe_timing_read(lpe_ctx *ctx, int i, char *name, int name_cap,
+                     double *total_ms, long *calls);
+
 /* ---- SPH fluid (Systems::FluidSystem) ----------------------------------- */
 int  lpe_fluid_config_default(lpe_fluid_config *cfg);
 /* Replaces the FluidConfig → GPUFluidParams packing (fluid.cpp:614-666,

@@ -4,6 +4,8 @@
 #include <cstdint>
 #include <cstdio>
 #include <string>
+#include <vector>
+#include <utility>
 #include "../../include/lpe.h"
 
 namespace lpe {
@@ -73,13 +75,45 @@ enum StatusSlot {
 
 }  // namespace lpe
 
+namespace lpe {
+// Optional per-kernel HIP-event timing on the context's stream (bench.py uses
+// it for the live roofline numbers).  Event pairs are recorded around each
+// launch of a named kernel and resolved at lpe_timing_read().
+struct KernelTimer {
+    bool on = false;
+    std::vector<std::string> names;
+    std::vector<std::vector<std::pair<hipEvent_t, hipEvent_t>>> pending;
+    std::vector<double> total_ms;
+    std::vector<long> calls;
+    std::vector<hipEvent_t> pool;
+    int slot(const char *name);
+    hipEvent_t get();
+};
+}  // namespace lpe
+
 struct lpe_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
     lpe::SphDev sph;
     void *rigid = nullptr;  // lpe::RigidDev*, owned by lpe_rigid.hip
+    lpe::KernelTimer timer;
 };
+
+// Records a start event before and a stop event after `launch` when timing is on.
+#define LPE_TIMED(ctx, name, launch)                                             \
+    do {                                                                         \
+        if ((ctx)->timer.on) {                                                   \
+            int ts_ = (ctx)->timer.slot(name);                                   \
+            hipEvent_t e0_ = (ctx)->timer.get(), e1_ = (ctx)->timer.get();       \
+            (void)hipEventRecord(e0_, (ctx)->stream);                            \
+            launch;                                                              \
+            (void)hipEventRecord(e1_, (ctx)->stream);                            \
+            (ctx)->timer.pending[ts_].push_back({e0_, e1_});                     \
+        } else {                                                                 \
+            launch;                                                              \
+        }                                                                        \
+    } while (0)
 
 #define LPE_HIP(ctx, call)                                                       \
     do {                                                                         \
@@ -110,3 +144,4 @@ static inline int lpe_grow(lpe_ctx *ctx, T **p, int *cap, long want, long elems_
 }
 
 int lpe_rigid_destroy_internal(lpe_ctx *ctx);
+int lpe_timer_destroy_internal(lpe_ctx *ctx);

@@ -641,6 +641,7 @@ extern "C" int lpe_destroy(lpe_ctx *ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     sph_free(ctx->sph);
     lpe_rigid_destroy_internal(ctx);
+    lpe_timer_destroy_internal(ctx);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return LPE_OK;
@@ -872,11 +873,11 @@ static int sph_scan(lpe_ctx *ctx, int C, int32_t *cnt, int32_t *start, int32_t *
     SphDev &d = ctx->sph;
     int nb = (C + SCAN_ELEMS - 1) / SCAN_ELEMS;
     hipStream_t s = ctx->stream;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(TPB), 0, s, C, cnt, bsum);
-    hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(TPB), 0, s, nb, bsum, start + C, d.bboxPart,
-                       nparts, d.cs, fluid ? d.gp : (GridParams *)nullptr, d.status);
-    hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(TPB), 0, s, C, d.W, d.ox, d.oy, cnt, bsum,
-                       start, cursor, d.gp, d.status, fluid ? 1 : 0);
+    LPE_TIMED(ctx, "k_scan_reduce", hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(TPB), 0, s, C, cnt, bsum));
+    LPE_TIMED(ctx, "k_scan_blocks", hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(TPB), 0, s, nb, bsum, start + C, d.bboxPart,
+                       nparts, d.cs, fluid ? d.gp : (GridParams *)nullptr, d.status));
+    LPE_TIMED(ctx, "k_scan_final", hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(TPB), 0, s, C, d.W, d.ox, d.oy, cnt, bsum,
+                       start, cursor, d.gp, d.status, fluid ? 1 : 0));
     LPE_CHECK_LAUNCH(ctx, "scan");
     return LPE_OK;
 }
@@ -901,8 +902,8 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
     }
     hipStream_t s = ctx->stream;
     LPE_HIP(ctx, hipMemsetAsync(d.rbinCount, 0, sizeof(int32_t) * B, s));
-    hipLaunchKernelGGL(k_rbin_count, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig, d.bcs,
-                       d.bx0, d.by0, d.bW, d.bH, d.rbinCount);
+    LPE_TIMED(ctx, "k_rbin_count", hipLaunchKernelGGL(k_rbin_count, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig, d.bcs,
+                       d.bx0, d.by0, d.bW, d.bH, d.rbinCount));
     int32_t *cursor = d.rbinCount + B;
     int st = sph_scan(ctx, B, d.rbinCount, d.rbinStart, cursor, d.rbinCount + 2 * B, 0, false);
     if (st) return st;
@@ -916,9 +917,9 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
         d.cap_rlist = std::max(total, 1);
     }
     d.rlist_len = total;
-    hipLaunchKernelGGL(k_rbin_fill, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig, d.bcs,
-                       d.bx0, d.by0, d.bW, d.bH, cursor, d.rbinList);
-    hipLaunchKernelGGL(k_rbin_sort, dim3(nblk(B, 128)), dim3(128), 0, s, B, d.rbinStart, d.rbinList);
+    LPE_TIMED(ctx, "k_rbin_fill", hipLaunchKernelGGL(k_rbin_fill, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig, d.bcs,
+                       d.bx0, d.by0, d.bW, d.bH, cursor, d.rbinList));
+    LPE_TIMED(ctx, "k_rbin_sort", hipLaunchKernelGGL(k_rbin_sort, dim3(nblk(B, 128)), dim3(128), 0, s, B, d.rbinStart, d.rbinList));
     LPE_CHECK_LAUNCH(ctx, "rbin");
     d.rig_dirty = false;
     return LPE_OK;
@@ -930,16 +931,16 @@ static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool pr
     hipStream_t s = ctx->stream;
     int C = 4 * d.W * d.H;
     int kb = std::min(MAX_KICK_BLOCKS, std::max(1, nblk(d.n)));
-    hipLaunchKernelGGL(k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
+    LPE_TIMED(ctx, "k_kick_drift", hipLaunchKernelGGL(k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
                        first ? 1 : 0, probe ? 1 : 0, d.cfg.gridConfig.gridEpsilon, d.cs, d.ox,
-                       d.oy, d.W, d.H, d.P, d.key, d.count, d.bboxPart, d.status);
+                       d.oy, d.W, d.H, d.P, d.key, d.count, d.bboxPart, d.status));
     LPE_CHECK_LAUNCH(ctx, "k_kick_drift");
     int st = sph_scan(ctx, C, d.count, d.start, d.cursor, d.blocksum, kb, true);
     if (st) return st;
-    hipLaunchKernelGGL(k_scatter, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.P.id, d.cursor,
-                       d.tmpId, d.tmpOld);
-    hipLaunchKernelGGL(k_rank_permute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.start,
-                       d.tmpId, d.tmpOld, d.P, d.S, probe ? 1 : 0);
+    LPE_TIMED(ctx, "k_scatter", hipLaunchKernelGGL(k_scatter, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.P.id, d.cursor,
+                       d.tmpId, d.tmpOld));
+    LPE_TIMED(ctx, "k_rank_permute", hipLaunchKernelGGL(k_rank_permute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.start,
+                       d.tmpId, d.tmpOld, d.P, d.S, probe ? 1 : 0));
     LPE_CHECK_LAUNCH(ctx, "hash");
     return LPE_OK;
 }
@@ -947,10 +948,10 @@ static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool pr
 static int sph_density(lpe_ctx *ctx) {
     SphDev &d = ctx->sph;
     const lpe_fluid_config &c = d.cfg;
-    hipLaunchKernelGGL(k_density, dim3(nblk(d.n)), dim3(TPB), 0, ctx->stream, d.n,
+    LPE_TIMED(ctx, "k_density", hipLaunchKernelGGL(k_density, dim3(nblk(d.n)), dim3(TPB), 0, ctx->stream, d.n,
                        c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
                        c.restDensity, d.W, d.ox, d.oy, d.gp, d.start, d.S.x, d.S.y, d.S.m,
-                       d.rho, d.pr);
+                       d.rho, d.pr));
     LPE_CHECK_LAUNCH(ctx, "k_density");
     return LPE_OK;
 }
@@ -983,14 +984,14 @@ extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
         if (st) return st;
         st = sph_density(ctx);
         if (st) return st;
-        hipLaunchKernelGGL(k_forces_couple, dim3(nblk(d.n)), dim3(TPB), 0, s, sp, cp, d.gp,
+        LPE_TIMED(ctx, "k_forces_couple", hipLaunchKernelGGL(k_forces_couple, dim3(nblk(d.n)), dim3(TPB), 0, s, sp, cp, d.gp,
                            d.start, d.S, d.rho, d.pr, d.P, d.rig, d.rbinStart, d.rbinList,
-                           d.accum);
+                           d.accum));
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
     }
     if (d.nr > 0) {
-        hipLaunchKernelGGL(k_rigid_writeback, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig,
-                           d.accum, d.accum + 3 * d.nr, c.dampingFactor);
+        LPE_TIMED(ctx, "k_rigid_writeback", hipLaunchKernelGGL(k_rigid_writeback, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig,
+                           d.accum, d.accum + 3 * d.nr, c.dampingFactor));
         LPE_CHECK_LAUNCH(ctx, "k_rigid_writeback");
     }
     return LPE_OK;
@@ -1005,7 +1006,7 @@ static int sph_unpermute_download(lpe_ctx *ctx, const int32_t *id, int nf, const
     float *stage[6] = {d.S.x, d.S.y, d.S.vx, d.S.vy, d.S.vhx, d.S.vhy};
     Fields6 f{};
     for (int k = 0; k < nf; k++) { f.src[k] = src[k]; f.dst[k] = stage[k]; }
-    hipLaunchKernelGGL(k_unpermute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, id, nf, f);
+    LPE_TIMED(ctx, "k_unpermute", hipLaunchKernelGGL(k_unpermute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, id, nf, f));
     LPE_CHECK_LAUNCH(ctx, "k_unpermute");
     for (int k = 0; k < nf; k++)
         if (host[k])
@@ -1094,8 +1095,8 @@ extern "C" int lpe_sph_probe_cells(lpe_ctx *ctx, int32_t *cell_index, lpe_sph_st
     LPE_HIP(ctx, hipMemsetAsync(d.status + ST_MAX_OCC, 0, sizeof(int32_t), ctx->stream));
     int st = sph_hash(ctx, 0.f, 0.f, false, true);
     if (st) return st;
-    hipLaunchKernelGGL(k_ref_cells, dim3(nblk(d.n)), dim3(TPB), 0, ctx->stream, d.n,
-                       d.cfg.gridConfig.gridEpsilon, d.P.x, d.P.y, d.P.id, d.gp, d.tmpId);
+    LPE_TIMED(ctx, "k_ref_cells", hipLaunchKernelGGL(k_ref_cells, dim3(nblk(d.n)), dim3(TPB), 0, ctx->stream, d.n,
+                       d.cfg.gridConfig.gridEpsilon, d.P.x, d.P.y, d.P.id, d.gp, d.tmpId));
     LPE_CHECK_LAUNCH(ctx, "k_ref_cells");
     LPE_HIP(ctx, hipMemcpyAsync(cell_index, d.tmpId, sizeof(int32_t) * d.n, hipMemcpyDeviceToHost,
                                 ctx->stream));

@@ -99,6 +99,10 @@ SIGNATURES = {
     "lpe_destroy": ([C.c_void_p], C.c_int),
     "lpe_last_error": ([C.c_void_p], C.c_char_p),
     "lpe_sync": ([C.c_void_p], C.c_int),
+    "lpe_timing_enable": ([C.c_void_p, C.c_int], C.c_int),
+    "lpe_timing_reset": ([C.c_void_p], C.c_int),
+    "lpe_timing_read": ([C.c_void_p, C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_double),
+                         C.POINTER(C.c_long)], C.c_int),
     "lpe_fluid_config_default": ([C.POINTER(FluidConfig)], C.c_int),
     "lpe_sph_set_config": ([C.c_void_p, C.POINTER(FluidConfig)], C.c_int),
     "lpe_sph_upload": ([C.c_void_p, C.c_int] + [_FP] * 7, C.c_int),
@@ -169,6 +173,28 @@ class Context:
 
     def sync(self):
         self._chk(lib().lpe_sync(self._h), "lpe_sync")
+
+    # ---- kernel timing -------------------------------------------------
+    def timing(self, on: bool = True):
+        self._chk(lib().lpe_timing_enable(self._h, 1 if on else 0), "lpe_timing_enable")
+
+    def timing_reset(self):
+        self._chk(lib().lpe_timing_reset(self._h), "lpe_timing_reset")
+
+    def timing_read(self) -> dict:
+        """{kernel_name: (total_ms, calls)} accumulated since the last reset."""
+        out = {}
+        i = 0
+        buf = C.create_string_buffer(128)
+        while True:
+            ms = C.c_double(0)
+            calls = C.c_long(0)
+            st = lib().lpe_timing_read(self._h, i, buf, 128, C.byref(ms), C.byref(calls))
+            if st != LPE_OK:
+                break
+            out[buf.value.decode()] = (ms.value, calls.value)
+            i += 1
+        return out
 
     # ---- SPH -----------------------------------------------------------
     def sph_set_config(self, cfg: FluidConfig):
