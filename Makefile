@@ -18,7 +18,7 @@ HIP_OBJ  := $(patsubst $(PKG)/csrc/%.hip,build/%.o,$(HIP_SRC))
 LIB      := $(PKG)/liblpe_hip.so
 
 ORC_SRC  := $(wildcard oracle/*.c)
-ORX_SRC  := $(wildcard oracle/*.cpp)
+ORX_SRC  := $(filter-out oracle/ref_driver.cpp,$(wildcard oracle/*.cpp))
 ORACLE   := oracle/liblpe_oracle.so
 
 all: $(LIB) $(ORACLE)

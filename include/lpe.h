@@ -128,6 +128,79 @@ typedef struct lpe_sph_stats {
     float   cellSize;
 } lpe_sph_stats;
 
+/* ------------------------------------------------------------------------ */
+/* Rigid path data: one solid body, its ECS components flattened.            */
+/* Filled by the host mirror from entt views (reference components:           */
+/* include/entities/entity_components.hpp:6-133, include/math/polygon.hpp:30-44). */
+/* ------------------------------------------------------------------------ */
+enum lpe_body_flags {
+    LPE_BODY_HAS_PHASE   = 1u << 0,   /* Components::ParticlePhase present       */
+    LPE_BODY_SOLID       = 1u << 1,   /* ... and phase == Solid                  */
+    LPE_BODY_LIQUID      = 1u << 2,   /* ... and phase == Liquid                 */
+    LPE_BODY_BOUNDARY    = 1u << 3,   /* Components::Boundary present            */
+    LPE_BODY_HAS_SLEEP   = 1u << 4,   /* Components::Sleep present               */
+    LPE_BODY_ASLEEP      = 1u << 5,   /* Sleep::asleep                           */
+    LPE_BODY_HAS_ANGPOS  = 1u << 6,   /* Components::AngularPosition present     */
+    LPE_BODY_HAS_ANGVEL  = 1u << 7,   /* Components::AngularVelocity present     */
+    LPE_BODY_HAS_INERTIA = 1u << 8,   /* Components::Inertia present             */
+    LPE_BODY_CIRCLE      = 1u << 9,   /* CircleShape present (narrowphase.cpp:38) */
+    LPE_BODY_POLYGON     = 1u << 10,  /* PolygonShape present                    */
+    LPE_BODY_HAS_MASS    = 1u << 11,  /* Components::Mass present                */
+    LPE_BODY_HAS_VEL     = 1u << 12   /* Components::Velocity present            */
+};
+
+typedef struct lpe_body {
+    uint32_t eid;        /* raw entt::entity value: orders pairs (broadphase.cpp:264) */
+    uint32_t flags;      /* lpe_body_flags                                           */
+    double x, y, angle;  /* Position, AngularPosition::angle                          */
+    double vx, vy, omega;/* Velocity, AngularVelocity::omega                          */
+    double mass, inertia;/* Mass::value, Inertia::I                                   */
+    double radius;       /* CircleShape::radius                                       */
+    int32_t vert_off;    /* PolygonShape vertices: [vert_off, vert_off+vert_cnt) of   */
+    int32_t vert_cnt;    /*   the shared local-vertex array (x, y pairs, double)      */
+    int32_t sleep_counter;
+    int32_t pad;
+} lpe_body;
+
+/* A narrowphase contact (collision_data.hpp:22-28): a and b are body indices,
+ * n points from A to B; pair is the index of its broadphase pair. */
+typedef struct lpe_contact {
+    int32_t a, b, pair, pad;
+    double nx, ny, pen, px, py;
+} lpe_contact;
+
+/* Configuration of RigidBodyCollisionSystem::update and the integrator systems.
+ * Reference defaults: BroadphaseConfig (broadphase.hpp:25-34),
+ * ContactSolverConfig (contact_solver.hpp:21-27), PositionSolverConfig
+ * (position_solver.hpp:21-34), GravityConfig (gravity.hpp:27-34),
+ * RotationConfig (rotation.hpp:28-34), BoundaryConfig (boundary.hpp:30-39),
+ * SleepConfig (sleep.hpp:31-40).  The reference hard-wires the rigid
+ * sub-configs (rigid_body_collision.cpp:30, :44, :48); pgsIterations and
+ * posIterations are exposed here with the reference defaults (10, 10). */
+typedef struct lpe_rigid_config {
+    double universeSize;          /* SharedSystemConfig::UniverseSizeMeters   */
+    double metersPerPixel;        /* SharedSystemConfig::MetersPerPixel       */
+    int32_t quadtreeCapacity;     /* 8 (tree shape only; pair SET unaffected) */
+    int32_t pgsIterations;        /* 10                                        */
+    double boundaryBuffer;        /* 500                                       */
+    double smallParticleThreshold;/* 0.01                                      */
+    float frictionCoeff;          /* 0.5f                                      */
+    int32_t posIterations;        /* 10                                        */
+    double baumgarte;             /* 0.02                                      */
+    double slop;                  /* 0.001                                     */
+    double gravity;               /* 9.8   (GravityConfig)                     */
+    double planetaryMassThreshold;/* 1e10                                      */
+    double angularDamping;        /* 0.98  (RotationConfig)                    */
+    double maxAngularSpeed;       /* 20                                        */
+    double marginPixels;          /* 15    (BoundaryConfig)                    */
+    double bounceDamping;         /* 0.7                                       */
+    double maxSpeed;              /* 1.0                                       */
+    double linearSleepThreshold;  /* 0.5   (SleepConfig)                       */
+    double angularSleepThreshold; /* 0.5                                       */
+    int32_t sleepFramesThreshold; /* 60                                        */
+    int32_t pad;
+} lpe_rigid_config;
+
 typedef struct lpe_ctx lpe_ctx;
 
 /* ---- lifecycle -------------------------------------------------------- */

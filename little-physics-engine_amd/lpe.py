@@ -78,6 +78,52 @@ RIGID_DTYPE = np.dtype([
     ("accumFx", "<f4"), ("accumFy", "<f4"), ("accumTorque", "<f4")])
 assert RIGID_DTYPE.itemsize == 200
 
+# numpy mirror of lpe_body (include/lpe.h): one solid body's ECS components
+BODY_DTYPE = np.dtype([
+    ("eid", "<u4"), ("flags", "<u4"), ("x", "<f8"), ("y", "<f8"), ("angle", "<f8"),
+    ("vx", "<f8"), ("vy", "<f8"), ("omega", "<f8"), ("mass", "<f8"), ("inertia", "<f8"),
+    ("radius", "<f8"), ("vert_off", "<i4"), ("vert_cnt", "<i4"), ("sleep_counter", "<i4"),
+    ("pad", "<i4")])
+assert BODY_DTYPE.itemsize == 96
+CONTACT_DTYPE = np.dtype([("a", "<i4"), ("b", "<i4"), ("pair", "<i4"), ("pad", "<i4"),
+                          ("nx", "<f8"), ("ny", "<f8"), ("pen", "<f8"), ("px", "<f8"),
+                          ("py", "<f8")])
+assert CONTACT_DTYPE.itemsize == 56
+
+BODY_HAS_PHASE, BODY_SOLID, BODY_LIQUID, BODY_BOUNDARY = 1, 2, 4, 8
+BODY_HAS_SLEEP, BODY_ASLEEP, BODY_HAS_ANGPOS, BODY_HAS_ANGVEL = 16, 32, 64, 128
+BODY_HAS_INERTIA, BODY_CIRCLE, BODY_POLYGON, BODY_HAS_MASS, BODY_HAS_VEL = 256, 512, 1024, 2048, 4096
+
+
+class RigidConfig(C.Structure):
+    """Mirror of lpe_rigid_config (include/lpe.h)."""
+    _fields_ = [("universeSize", C.c_double), ("metersPerPixel", C.c_double),
+                ("quadtreeCapacity", C.c_int32), ("pgsIterations", C.c_int32),
+                ("boundaryBuffer", C.c_double), ("smallParticleThreshold", C.c_double),
+                ("frictionCoeff", C.c_float), ("posIterations", C.c_int32),
+                ("baumgarte", C.c_double), ("slop", C.c_double), ("gravity", C.c_double),
+                ("planetaryMassThreshold", C.c_double), ("angularDamping", C.c_double),
+                ("maxAngularSpeed", C.c_double), ("marginPixels", C.c_double),
+                ("bounceDamping", C.c_double), ("maxSpeed", C.c_double),
+                ("linearSleepThreshold", C.c_double), ("angularSleepThreshold", C.c_double),
+                ("sleepFramesThreshold", C.c_int32), ("pad", C.c_int32)]
+
+
+def rigid_config(universe=6.0, pgs_iterations=10, **kw) -> RigidConfig:
+    """Reference defaults (broadphase.hpp, contact_solver.hpp, position_solver.hpp,
+    gravity/rotation/boundary/sleep .hpp)."""
+    c = RigidConfig(universeSize=universe, metersPerPixel=0.01, quadtreeCapacity=8,
+                    pgsIterations=pgs_iterations, boundaryBuffer=500.0,
+                    smallParticleThreshold=0.01, frictionCoeff=0.5, posIterations=10,
+                    baumgarte=0.02, slop=0.001, gravity=9.8, planetaryMassThreshold=1e10,
+                    angularDamping=0.98, maxAngularSpeed=20.0, marginPixels=15.0,
+                    bounceDamping=0.7, maxSpeed=1.0, linearSleepThreshold=0.5,
+                    angularSleepThreshold=0.5, sleepFramesThreshold=60)
+    for k, v in kw.items():
+        setattr(c, k, v)
+    return c
+
+
 _FP = C.POINTER(C.c_float)
 _IP = C.POINTER(C.c_int32)
 

@@ -229,6 +229,112 @@ def scene(name: str):
     raise KeyError(name)
 
 
+def to_bodies(b: Bodies, eid_base: int = 1):
+    """lpe_body array + shared local-vertex array, in creation order.  Entity
+    ids follow a fresh registry: SimulatorState is entity 0 (sim.cpp:95-96),
+    bodies are created next."""
+    L = _lpe
+    out = np.zeros(len(b), L.BODY_DTYPE)
+    verts = []
+    for i, r in enumerate(b.rows):
+        f = L.BODY_HAS_PHASE | L.BODY_SOLID | L.BODY_HAS_MASS | L.BODY_HAS_VEL
+        if r["boundary"]:
+            f |= L.BODY_BOUNDARY
+        if r["has_sleep"]:
+            f |= L.BODY_HAS_SLEEP
+        if r["asleep"]:
+            f |= L.BODY_ASLEEP
+        if r["has_angpos"]:
+            f |= L.BODY_HAS_ANGPOS
+        if r["has_angvel"]:
+            f |= L.BODY_HAS_ANGVEL
+        if r["has_inertia"]:
+            f |= L.BODY_HAS_INERTIA
+        o = out[i]
+        o["eid"] = eid_base + i
+        if r["circle"]:
+            f |= L.BODY_CIRCLE
+            o["radius"] = r["radius"]
+            o["vert_off"] = len(verts) // 2
+            o["vert_cnt"] = 0
+        else:
+            f |= L.BODY_POLYGON
+            o["vert_off"] = len(verts) // 2
+            o["vert_cnt"] = len(r["verts"])
+            verts.extend(np.asarray(r["verts"], np.float64).ravel().tolist())
+        o["flags"] = f
+        for k in ("x", "y", "angle", "vx", "vy", "omega", "mass", "inertia"):
+            o[k] = r[k]
+        o["sleep_counter"] = r["sleep_counter"]
+    return out, np.array(verts if verts else [0.0, 0.0], np.float64)
+
+
+def rigid_scene(name: str):
+    """Rigid-only scenes: returns dict(U, bodies, desc, pgs_iterations)."""
+    if name == "C1":     # 128-box stack (SURVEY.md §8(d)), U = 6 m, seed 1
+        U = 6.0
+        b = Bodies()
+        add_walls(b, U)
+        box = regular_polygon(4, 0.2)
+        half = 0.2 * math.cos(math.pi / 4)
+        floor = U - WALL_THICK * 0.5
+        for row in range(16):
+            for col in range(8):
+                x = 0.5 * U + (col - 3.5) * 0.4
+                y = floor - half - 0.002 - row * 0.29
+                b.add(x=x, y=y, mass=1.0, angle=math.pi / 4, verts=box, shape_size=0.2,
+                      has_angvel=True, has_inertia=True, inertia=polygon_inertia(box, 1.0))
+        return dict(U=U, bodies=b, pgs_iterations=10, desc="C1: 8x16 box stack, U=6")
+    if name.startswith("C3") or name.startswith("pile"):
+        # C3: 64x64 random-polygon pile (random_polygons.cpp:133-207 recipe,
+        # sizes 0.1-0.25), U = 40 m, 16 PGS iterations; pile{k}: k x k version
+        k = 64 if name.startswith("C3") else int(name[4:])
+        U = 40.0 if k >= 32 else max(6.0, 0.55 * k + 2.0)
+        rng = np.random.default_rng(3 + (0 if k == 64 else 1000 + k))
+        b = Bodies()
+        add_walls(b, U)
+        x0 = 0.5 * (U - (k - 1) * 0.55)
+        y0 = U - 0.3 - (k - 1) * 0.55
+        for row in range(k):
+            for col in range(k):
+                size = float(rng.uniform(0.1, 0.25))
+                if rng.uniform() < 0.6:
+                    verts = regular_polygon(int(rng.integers(3, 9)), size)
+                else:
+                    verts = random_convex_polygon(rng, size)
+                mass = max(0.1, float(rng.normal(1.0, 0.1)))
+                b.add(x=x0 + col * 0.55, y=y0 + row * 0.55, vx=float(rng.uniform(-2, 2)),
+                      vy=float(rng.uniform(-2, 2)), mass=mass, omega=float(rng.uniform(-1, 1)),
+                      verts=verts, shape_size=size, has_angvel=True, has_inertia=True,
+                      inertia=polygon_inertia(verts, mass))
+        return dict(U=U, bodies=b, pgs_iterations=16 if k == 64 else 10,
+                    desc=f"{'C3' if k == 64 else 'pile'}: {k}x{k} random convex polygons, U={U:g}")
+    if name.startswith("mix"):   # small mixed scene with circles, for parity tests
+        k = int(name[3:]) if len(name) > 3 else 8
+        U = 6.0
+        rng = np.random.default_rng(77 + k)
+        b = Bodies()
+        add_walls(b, U)
+        for row in range(k):
+            for col in range(k):
+                x = 0.5 * U + (col - (k - 1) / 2) * 0.32 + float(rng.uniform(-0.03, 0.03))
+                y = U - 0.4 - row * 0.3
+                mass = max(0.1, float(rng.normal(1.0, 0.1)))
+                if rng.uniform() < 0.3:
+                    r = float(rng.uniform(0.08, 0.16))
+                    b.add(x=x, y=y, vx=float(rng.uniform(-1, 1)), vy=float(rng.uniform(0, 2)),
+                          mass=mass, circle=True, radius=r, has_angvel=True, has_inertia=True,
+                          inertia=0.5 * mass * r * r, omega=float(rng.uniform(-1, 1)))
+                else:
+                    verts = regular_polygon(int(rng.integers(3, 9)), float(rng.uniform(0.1, 0.18)))
+                    b.add(x=x, y=y, vx=float(rng.uniform(-1, 1)), vy=float(rng.uniform(0, 2)),
+                          mass=mass, verts=verts, angle=float(rng.uniform(0, 6.28)),
+                          has_angvel=True, has_inertia=True, omega=float(rng.uniform(-1, 1)),
+                          inertia=polygon_inertia(verts, mass))
+        return dict(U=U, bodies=b, pgs_iterations=10, desc=f"mix: {k}x{k} circles+polygons, U=6")
+    raise KeyError(name)
+
+
 def particles_aos(fl) -> np.ndarray:
     """GPUFluidParticle array as gatherFluidParticles builds it (fluid.cpp:282-295)."""
     from_keys = ("x", "y", "vx", "vy")

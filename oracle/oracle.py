@@ -109,3 +109,155 @@ def fluid_tick(p, rigids, dt_tick, cfg=None):
     if rc != 0:
         raise RuntimeError(f"lpeo_fluid_tick -> {rc}")
     return p, r, acc[:3 * len(r)].reshape(-1, 3), st
+
+
+# ---------------------------------------------------------------------------
+# rigid path (oracle/rigid_oracle.cpp)
+class RigidStats(C.Structure):
+    _fields_ = [("pairs", C.c_int32), ("contacts", C.c_int32), ("manifolds", C.c_int32),
+                ("dynamicBodies", C.c_int32)]
+
+
+_rigid_ready = False
+
+
+def _rigid_lib():
+    global _rigid_ready
+    L = lib()
+    if not _rigid_ready:
+        RC = C.POINTER(lpe.RigidConfig)
+        L.lpeo_broadphase.argtypes = [RC, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+        L.lpeo_narrowphase.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p,
+                                       C.c_void_p, C.c_int]
+        L.lpeo_pgs.argtypes = [RC, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        L.lpeo_position_solver.argtypes = [RC, C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p]
+        L.lpeo_rigid_update.argtypes = [RC, C.c_int, C.c_void_p, C.c_void_p, C.POINTER(RigidStats)]
+        L.lpeo_rigid_tick.argtypes = [RC, C.c_int, C.c_void_p, C.c_void_p, C.c_double, C.c_double,
+                                      C.POINTER(RigidStats)]
+        for f in ("lpeo_boundary", "lpeo_sleep"):
+            getattr(L, f).argtypes = [RC, C.c_int, C.c_void_p]
+        for f in ("lpeo_gravity", "lpeo_rotation"):
+            getattr(L, f).argtypes = [RC, C.c_int, C.c_void_p, C.c_double]
+        L.lpeo_movement.argtypes = [C.c_int, C.c_void_p, C.c_double]
+        _rigid_ready = True
+    return L
+
+
+def _bodies(b):
+    return np.ascontiguousarray(b, dtype=lpe.BODY_DTYPE).copy()
+
+
+def broadphase(cfg, bodies, verts):
+    b = _bodies(bodies)
+    v = np.ascontiguousarray(verts, np.float64)
+    cap = 4096
+    while True:
+        out = np.zeros(2 * cap, np.int32)
+        n = _rigid_lib().lpeo_broadphase(C.byref(cfg), len(b), b.ctypes.data, v.ctypes.data,
+                                         out.ctypes.data, cap)
+        if n >= 0:
+            return out[:2 * n].reshape(-1, 2)
+        cap = -n
+
+
+def narrowphase(bodies, verts, pairs):
+    b = _bodies(bodies)
+    v = np.ascontiguousarray(verts, np.float64)
+    p = np.ascontiguousarray(pairs, np.int32).reshape(-1)
+    cap = max(16, 4 * len(p))
+    while True:
+        out = np.zeros(cap, lpe.CONTACT_DTYPE)
+        n = _rigid_lib().lpeo_narrowphase(len(b), b.ctypes.data, v.ctypes.data, len(p) // 2,
+                                          p.ctypes.data, out.ctypes.data, cap)
+        if n >= 0:
+            return out[:n]
+        cap = -n
+
+
+def pgs(cfg, bodies, contacts, order=None):
+    b = _bodies(bodies)
+    c = np.ascontiguousarray(contacts, lpe.CONTACT_DTYPE)
+    o = None if order is None else np.ascontiguousarray(order, np.int32)
+    _rigid_lib().lpeo_pgs(C.byref(cfg), len(b), b.ctypes.data, len(c), c.ctypes.data,
+                          None if o is None else o.ctypes.data)
+    return b
+
+
+def position_solver(cfg, bodies, contacts, order=None):
+    b = _bodies(bodies)
+    c = np.ascontiguousarray(contacts, lpe.CONTACT_DTYPE)
+    o = None if order is None else np.ascontiguousarray(order, np.int32)
+    _rigid_lib().lpeo_position_solver(C.byref(cfg), len(b), b.ctypes.data, len(c), c.ctypes.data,
+                                      None if o is None else o.ctypes.data)
+    return b
+
+
+def rigid_update(cfg, bodies, verts):
+    b = _bodies(bodies)
+    v = np.ascontiguousarray(verts, np.float64)
+    st = RigidStats()
+    _rigid_lib().lpeo_rigid_update(C.byref(cfg), len(b), b.ctypes.data, v.ctypes.data, C.byref(st))
+    return b, st
+
+
+def rigid_tick(cfg, bodies, verts, dt_state, dt_move=None):
+    b = _bodies(bodies)
+    v = np.ascontiguousarray(verts, np.float64)
+    st = RigidStats()
+    _rigid_lib().lpeo_rigid_tick(C.byref(cfg), len(b), b.ctypes.data, v.ctypes.data,
+                                 float(dt_state), float(dt_state if dt_move is None else dt_move),
+                                 C.byref(st))
+    return b, st
+
+
+def integrate(cfg, bodies, which, dt=None):
+    b = _bodies(bodies)
+    L = _rigid_lib()
+    if which in ("boundary", "sleep"):
+        getattr(L, "lpeo_" + which)(C.byref(cfg), len(b), b.ctypes.data)
+    elif which in ("gravity", "rotation"):
+        getattr(L, "lpeo_" + which)(C.byref(cfg), len(b), b.ctypes.data, float(dt))
+    else:
+        L.lpeo_movement(len(b), b.ctypes.data, float(dt))
+    return b
+
+
+# ---------------------------------------------------------------------------
+# the reference itself (oracle/_ref/liblpe_ref.so, built by oracle/Makefile.ref
+# only where /root/reference exists)
+REF_PATH = os.path.join(HERE, "_ref", "liblpe_ref.so")
+
+
+def ref_available():
+    return os.path.exists(REF_PATH)
+
+
+def ref_rigid_ticks(cfg, bodies, verts, nticks, dt):
+    """Runs the reference systems for nticks; returns the final bodies and the
+    stage outputs of the last tick (pairs in quadtree order, contacts in
+    narrowphase order, PGS contact order, snapshots)."""
+    L = C.CDLL(REF_PATH)
+    f = L.lpref_rigid_ticks
+    f.argtypes = [C.POINTER(lpe.RigidConfig), C.c_double, C.c_double, C.c_double, C.c_double,
+                  C.c_int, C.c_void_p, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p,
+                  C.c_void_p, C.c_int, C.POINTER(C.c_int32), C.c_void_p, C.c_int,
+                  C.POINTER(C.c_int32), C.c_void_p]
+    b = _bodies(bodies)
+    v = np.ascontiguousarray(verts, np.float64)
+    n = len(b)
+    before = np.zeros(n, lpe.BODY_DTYPE)
+    apgs = np.zeros(n, lpe.BODY_DTYPE)
+    apos = np.zeros(n, lpe.BODY_DTYPE)
+    pcap = 64 * n + 1024
+    ccap = 4 * pcap
+    pairs = np.zeros(2 * pcap, np.int32)
+    cs = np.zeros(ccap, lpe.CONTACT_DTYPE)
+    order = np.zeros(ccap, np.int32)
+    npairs = C.c_int32(0)
+    nc = C.c_int32(0)
+    f(C.byref(cfg), float(dt), 1.0, 1.0, 1.0, n, b.ctypes.data, v.ctypes.data, int(nticks),
+      before.ctypes.data, apgs.ctypes.data, apos.ctypes.data, pairs.ctypes.data, pcap,
+      C.byref(npairs), cs.ctypes.data, ccap, C.byref(nc), order.ctypes.data)
+    return dict(final=b, before_rigid=before, after_pgs=apgs, after_pos=apos,
+                pairs=pairs[:2 * npairs.value].reshape(-1, 2).copy(),
+                contacts=cs[:nc.value].copy(), pgs_order=order[:nc.value].copy())

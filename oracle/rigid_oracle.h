@@ -1,0 +1,63 @@
+/* rigid_oracle.h — TEST INFRASTRUCTURE ONLY (see rigid_oracle.cpp header). */
+#ifndef LPE_RIGID_ORACLE_H
+#define LPE_RIGID_ORACLE_H
+#include <stdint.h>
+#include "../include/lpe.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct lpeo_rigid_stats {
+    int32_t pairs, contacts, manifolds, dynamicBodies;
+} lpeo_rigid_stats;
+
+void lpeo_rigid_config_default(lpe_rigid_config *c);
+
+/* Broadphase::detectCollisions pair SET (broadphase.cpp:233-295), in the
+ * canonical order (eid_a, eid_b) ascending, eid_a < eid_b.  pairs receives
+ * body-index pairs.  Returns the pair count, or -(count) if cap is too small. */
+int lpeo_broadphase(const lpe_rigid_config *cfg, int nb, const lpe_body *bodies,
+                    const double *verts, int32_t *pairs, int cap);
+
+/* narrowPhase (narrowphase.cpp:352-420) over the given pairs, in pair order.
+ * Returns the contact count, or -(count) if cap is too small. */
+int lpeo_narrowphase(int nb, const lpe_body *bodies, const double *verts, int np,
+                     const int32_t *pairs, lpe_contact *out, int cap);
+
+/* ContactSolver::solveContactConstraints (contact_solver.cpp:449-543): rows
+ * are visited in `order` (contact indices; NULL = identity).  Updates vx, vy,
+ * omega of dynamic bodies. */
+int lpeo_pgs(const lpe_rigid_config *cfg, int nb, lpe_body *bodies, int nc,
+             const lpe_contact *contacts, const int32_t *order);
+
+/* PositionSolver::positionalSolver (position_solver.cpp:299-325): contacts
+ * visited in `order` (NULL = identity).  Updates x, y, angle. */
+int lpeo_position_solver(const lpe_rigid_config *cfg, int nb, lpe_body *bodies, int nc,
+                         const lpe_contact *contacts, const int32_t *order);
+
+/* RigidBodyCollisionSystem::update (rigid_body_collision.cpp:24-50) with the
+ * canonical orders: pairs by (eid_a, eid_b); PGS manifolds in pair order;
+ * position solver in narrowphase order. */
+int lpeo_rigid_update(const lpe_rigid_config *cfg, int nb, lpe_body *bodies,
+                      const double *verts, lpeo_rigid_stats *stats);
+
+/* Integrator / tick-parity systems (one pass each). */
+void lpeo_boundary(const lpe_rigid_config *cfg, int nb, lpe_body *bodies);
+void lpeo_gravity(const lpe_rigid_config *cfg, int nb, lpe_body *bodies, double dt);
+void lpeo_rotation(const lpe_rigid_config *cfg, int nb, lpe_body *bodies, double dt);
+void lpeo_movement(int nb, lpe_body *bodies, double dt);
+void lpeo_sleep(const lpe_rigid_config *cfg, int nb, lpe_body *bodies);
+
+/* ECSSimulator::tick for a scene without fluid (FluidSystem returns early,
+ * fluid.cpp:969-972; Barnes-Hut returns early for masses < 1e3,
+ * barnes_hut.cpp:54-70): Boundary, Gravity, RigidBodyCollision, Rotation,
+ * Movement, Sleep.  dt_state = SecondsPerTick * baseTimeAcceleration *
+ * timeScale (gravity, rotation); dt_move = SecondsPerTick * TimeAcceleration. */
+int lpeo_rigid_tick(const lpe_rigid_config *cfg, int nb, lpe_body *bodies, const double *verts,
+                    double dt_state, double dt_move, lpeo_rigid_stats *stats);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
