@@ -277,6 +277,49 @@ int  lpe_sph_probe_cells(lpe_ctx *ctx, int32_t *cell_index, lpe_sph_stats *stats
  * density pass, no integration; fluid_kernels.metal:246-307). */
 int  lpe_sph_probe_density(lpe_ctx *ctx, float *density, float *pressure);
 
+/* ---- rigid bodies (Systems::RigidBodyCollisionSystem + integrators) ---- */
+typedef struct lpe_rigid_stats {
+    int32_t pairs;          /* broadphase pairs                                */
+    int32_t contacts;       /* narrowphase contacts                            */
+    int32_t pgsLevels;      /* dependency levels of one PGS sweep              */
+    int32_t posLevels;      /* dependency levels of one position-solver sweep  */
+    int32_t overflow;       /* non-zero if a fixed-capacity list overflowed    */
+    int32_t pad;
+} lpe_rigid_stats;
+
+int  lpe_rigid_config_default(lpe_rigid_config *cfg);
+int  lpe_rigid_set_config(lpe_ctx *ctx, const lpe_rigid_config *cfg);
+/* Bodies (ECS gather of every entity the rigid path or the integrators read)
+ * and the shared local-vertex array (x, y pairs).  Body order is free; pair
+ * order is by lpe_body::eid. */
+int  lpe_rigid_upload(lpe_ctx *ctx, int nb, const lpe_body *bodies, int nverts,
+                      const double *verts);
+/* RigidBodyCollisionSystem::update (rigid_body_collision.cpp:24-50) on the
+ * device: broadphase pair set (broadphase.cpp:233-295) in canonical order
+ * (eid_a, eid_b); GJK/EPA/clipping narrowphase in fp64
+ * (narrowphase.cpp:352-420); PGS (contact_solver.cpp:449-543) and Baumgarte
+ * position solver (position_solver.cpp:299-325) as exact sequential
+ * Gauss-Seidel sweeps in that order, run level by level on the device. */
+int  lpe_rigid_step(lpe_ctx *ctx, lpe_rigid_stats *stats);
+/* Same with caller-supplied orders (parity mode): `pairs` (np body-index
+ * pairs) replaces the broadphase and fixes the narrowphase / position-solver
+ * order; `pgs_order` (NULL = contact order) is the PGS contact visiting order,
+ * e.g. the reference's unordered_map manifold order
+ * (contact_manager.cpp:169-245). */
+int  lpe_rigid_step_ordered(lpe_ctx *ctx, int np, const int32_t *pairs, int nc_order,
+                            const int32_t *pgs_order, lpe_rigid_stats *stats);
+/* Integrator systems on the device, in this order when their bit is set:
+ * 1 Boundary (boundary.cpp:13-70), 2 Gravity (gravity.cpp:19-58),
+ * 4 Rotation (rotation.cpp:18-60), 8 Movement (movement.cpp:13-39),
+ * 16 Sleep (sleep.cpp:19-67).  dt_state = SecondsPerTick *
+ * baseTimeAcceleration * timeScale (gravity, rotation); dt_move =
+ * SecondsPerTick * TimeAcceleration (movement). */
+int  lpe_rigid_integrate(lpe_ctx *ctx, int systems, double dt_state, double dt_move);
+int  lpe_rigid_download(lpe_ctx *ctx, lpe_body *bodies);
+/* Last step's pairs and contacts (parity probes). */
+int  lpe_rigid_download_contacts(lpe_ctx *ctx, int pair_cap, int32_t *pairs, int contact_cap,
+                                 lpe_contact *contacts, int32_t *np, int32_t *nc);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,3 +1,1342 @@
-// lpe_rigid.hip — rigid-body path (placeholder until the rigid kernels land).
+// lpe_rigid.hip — rigid-body path of the MI355X backend
+// (Systems::RigidBodyCollisionSystem, src/systems/rigid/*.cpp, and the
+// integrator systems src/systems/{boundary,gravity,rotation,movement,sleep}.cpp).
+//
+// Device pipeline of one RigidBodyCollisionSystem::update
+// (rigid_body_collision.cpp:24-50):
+//   k_rb_prep       per-body AABB (computeAABB, broadphase.cpp:158-191) and
+//                   the candidate test (Solid + Mass + Phase, inside the
+//                   quadtree root, broadphase.cpp:200-223)
+//   k_bp_pairs      tiled all-pairs AABB test in entity-id order: the pair SET
+//                   of detectCollisions (broadphase.cpp:233-295), which equals
+//                   brute force over the inserted boxes; emitted in canonical
+//                   (eid_a, eid_b) order by count -> scan -> fill -> segment sort
+//   k_narrow        one thread per pair, fp64: GJK (gjk.cpp:73-123), EPA
+//                   (epa.cpp:32-97), single contacts or reference-face
+//                   clipping (narrowphase.cpp:126-350); contacts compacted in
+//                   pair order
+//   PGS             rows in fp32 (contact_solver.cpp:133-253); the sequential
+//                   Gauss-Seidel sweep (solveLcpPgs, :381-440) is executed
+//                   level by level: an item's level is one more than the level
+//                   of the previous item (in sweep order) sharing a dynamic
+//                   body, so every level is a set of independent rows and the
+//                   result is bit-identical to the sequential sweep in the same
+//                   order.  One 1024-thread workgroup, body velocities in LDS.
+//   position solver the same schedule over contacts in narrowphase order,
+//                   fp64 (position_solver.cpp:215-290), body poses in LDS.
+// Orders: canonical (pairs by entity id; manifolds = pairs) by default, or
+// caller-supplied (lpe_rigid_step_ordered) to replay the reference's quadtree
+// and std::unordered_map orders bit for bit.
 #include "lpe_internal.h"
-int lpe_rigid_destroy_internal(lpe_ctx *ctx) { (void)ctx; return LPE_OK; }
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+namespace lpe {
+
+static constexpr int RTPB = 256;
+static constexpr int MAXC = 36;        // contacts per pair slot (poly-poly <= nB + 3)
+static constexpr int EPA_MAX = 104;    // EPA polygon: 3 + 100 insertions + 1
+static constexpr int CLIP_MAX = 40;    // clip output <= nB + 3
+static constexpr int MAXV = 32;        // polygon vertex cap of the device narrowphase
+static constexpr int SOLVE_TPB = 1024;
+
+struct RigidDev {
+    int nb = 0, cap_nb = 0;
+    lpe_body *bodies = nullptr;
+    double *verts = nullptr;
+    int nverts = 0, cap_verts = 0;
+    int32_t *rank = nullptr, *byRank = nullptr;
+    double4 *aabb = nullptr;
+    int32_t *cand = nullptr;
+    // pairs
+    int32_t *pcount = nullptr, *pstart = nullptr, *pcursor = nullptr;
+    int2 *pairs = nullptr;
+    int32_t *pairRankB = nullptr;
+    int cap_pairs = 0;
+    // contacts
+    lpe_contact *cslots = nullptr;
+    int32_t *ccount = nullptr, *cstart = nullptr;
+    lpe_contact *contacts = nullptr;
+    int cap_contacts = 0;
+    // scan partials
+    int32_t *bsum = nullptr;
+    int cap_bsum = 0;
+    // PGS / position solver
+    int32_t *order = nullptr;                 // PGS visiting order (contact indices)
+    float4 *rowN = nullptr;                   // dirX, dirY, effN, effF
+    float4 *rowR = nullptr;                   // rxA, ryA, rxB, ryB
+    int2 *rowAB = nullptr;                    // body indices (-1 = static)
+    float *vel0 = nullptr;                    // float3 per body (PGS load)
+    float *imii = nullptr;                    // float2 per body (invMass, invInertia)
+    int32_t *inContact = nullptr;             // per body flags
+    double *posState = nullptr;               // per body: invM, invI (pos solver)
+    int2 *posAB = nullptr;
+    int32_t *posItem = nullptr;               // kept contact index per pos item
+    // scheduling (shared by both solvers)
+    int32_t *sItemA = nullptr, *sItemB = nullptr, *sPrevA = nullptr, *sPrevB = nullptr;
+    int32_t *sLevel = nullptr, *sBCount = nullptr, *sBStart = nullptr, *sBCursor = nullptr;
+    int32_t *sEnt = nullptr, *sSorted = nullptr, *sLCount = nullptr, *sLStart = nullptr,
+            *sLCursor = nullptr, *sLOrder = nullptr;
+    int32_t *counts = nullptr;                // [0]=np [1]=nc [2]=pgs levels [3]=pos levels [4]=npos [5]=heavy
+    lpe_rigid_config cfg{};
+    bool cfg_set = false;
+    int last_np = 0, last_nc = 0;
+};
+
+static RigidDev *rdev(lpe_ctx *ctx) {
+    if (!ctx->rigid) ctx->rigid = new RigidDev();
+    return (RigidDev *)ctx->rigid;
+}
+
+// ---------------------------------------------------------------------------
+// generic exclusive scan of n ints (3 launches); start has n+1 entries
+__device__ __forceinline__ int r_wave_incl(int v) {
+    int lane = threadIdx.x & 63;
+    for (int off = 1; off < 64; off <<= 1) {
+        int t = __shfl_up(v, off);
+        if (lane >= off) v += t;
+    }
+    return v;
+}
+__device__ __forceinline__ int r_block_excl(int v, int *total) {
+    __shared__ int wsum[RTPB / 64];
+    int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int incl = r_wave_incl(v);
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int off = 0, tot = 0;
+    for (int k = 0; k < RTPB / 64; k++) { if (k < w) off += wsum[k]; tot += wsum[k]; }
+    __syncthreads();
+    *total = tot;
+    return off + incl - v;
+}
+__global__ void __launch_bounds__(RTPB) k_rscan_reduce(const int32_t *nptr, int ncap,
+                                                       const int32_t *__restrict__ cnt,
+                                                       int32_t *__restrict__ bsum) {
+    int n = nptr ? *nptr : ncap;
+    int base = blockIdx.x * 1024;
+    int s = 0;
+    for (int k = 0; k < 4; k++) {
+        int c = base + k * RTPB + threadIdx.x;
+        if (c < n) s += cnt[c];
+    }
+    int tot;
+    (void)r_block_excl(s, &tot);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+__global__ void __launch_bounds__(RTPB) k_rscan_blocks(const int32_t *nptr, int ncap,
+                                                       int32_t *__restrict__ bsum,
+                                                       int32_t *__restrict__ start) {
+    int n = nptr ? *nptr : ncap;
+    int nb = (n + 1023) / 1024;
+    int carry = 0;
+    for (int b0 = 0; b0 < nb; b0 += RTPB) {
+        int b = b0 + threadIdx.x;
+        int v = (b < nb) ? bsum[b] : 0;
+        int tot;
+        int ex = r_block_excl(v, &tot);
+        if (b < nb) bsum[b] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) start[n] = carry;
+}
+__global__ void __launch_bounds__(RTPB) k_rscan_final(const int32_t *nptr, int ncap,
+                                                      const int32_t *__restrict__ cnt,
+                                                      const int32_t *__restrict__ bsum,
+                                                      int32_t *__restrict__ start,
+                                                      int32_t *__restrict__ cursor) {
+    int n = nptr ? *nptr : ncap;
+    int base = blockIdx.x * 1024 + threadIdx.x * 4;
+    int v[4], s = 0;
+    for (int k = 0; k < 4; k++) { int c = base + k; v[k] = (c < n) ? cnt[c] : 0; s += v[k]; }
+    int tot;
+    int ex = r_block_excl(s, &tot) + ((base < n || threadIdx.x == 0) ? bsum[blockIdx.x] : 0);
+    for (int k = 0; k < 4; k++) {
+        int c = base + k;
+        if (c < n) { start[c] = ex; if (cursor) cursor[c] = ex; }
+        ex += v[k];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// geometry (fp64), restating vector_math.cpp / polygon.hpp
+struct D2 { double x, y; };
+__device__ __forceinline__ D2 d2(double x, double y) { D2 r; r.x = x; r.y = y; return r; }
+__device__ __forceinline__ D2 sub(D2 a, D2 b) { return d2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ D2 add(D2 a, D2 b) { return d2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ D2 neg(D2 a) { return d2(-a.x, -a.y); }
+__device__ __forceinline__ D2 mul(D2 a, double s) { return d2(a.x * s, a.y * s); }
+__device__ __forceinline__ double dot(D2 a, D2 b) { return a.x * b.x + a.y * b.y; }
+__device__ __forceinline__ double crs(D2 a, D2 b) { return a.x * b.y - a.y * b.x; }
+__device__ __forceinline__ D2 nrm(D2 a) {                       // vector_math.cpp:130-137
+    double len = sqrt(a.x * a.x + a.y * a.y);
+    if (len > 1e-9) return d2(a.x / len, a.y / len);
+    return d2(1.0, 0.0);
+}
+
+struct DShape {
+    bool circle;
+    double radius;
+    D2 pos;
+    double angle;
+    const double *lv;
+    int nv;
+};
+__device__ __forceinline__ DShape dshape(const lpe_body &b, const double *verts) {
+    DShape s;
+    s.circle = (b.flags & LPE_BODY_CIRCLE) != 0;
+    s.radius = s.circle ? b.radius : 0.0;
+    s.pos = d2(b.x, b.y);
+    s.angle = (b.flags & LPE_BODY_HAS_ANGPOS) ? b.angle : 0.0;
+    s.lv = verts + 2 * (size_t)b.vert_off;
+    s.nv = s.circle ? 0 : b.vert_cnt;
+    return s;
+}
+__device__ D2 support1(const DShape &s, D2 d) {
+    if (s.circle) {                                               // polygon.hpp:90-101
+        double len = sqrt(d.x * d.x + d.y * d.y);
+        D2 dn = d;
+        if (len > 1e-9) { dn.x /= len; dn.y /= len; }
+        return d2(s.pos.x + dn.x * s.radius, s.pos.y + dn.y * s.radius);
+    }
+    double c = cos(s.angle), sn = sin(s.angle);                   // polygon.hpp:55-76
+    double best = -1e9;
+    D2 bp = d2(0.0, 0.0);
+    for (int i = 0; i < s.nv; i++) {
+        double lx = s.lv[2 * i], ly = s.lv[2 * i + 1];
+        double wx = s.pos.x + (lx * c - ly * sn);
+        double wy = s.pos.y + (lx * sn + ly * c);
+        double proj = wx * d.x + wy * d.y;
+        if (proj > best) { best = proj; bp = d2(wx, wy); }
+    }
+    return bp;
+}
+__device__ __forceinline__ D2 support(const DShape &A, const DShape &B, D2 d) {
+    D2 pA = support1(A, d);
+    D2 pB = support1(B, d2(-d.x, -d.y));
+    return d2(pA.x - pB.x, pA.y - pB.y);
+}
+
+// GJKIntersect (gjk.cpp:73-123) with handleSimplex (:9-71); pts[0] oldest
+__device__ bool gjk(const DShape &A, const DShape &B, D2 *pts, int &np) {
+    D2 dir = d2(1, 0);
+    np = 0;
+    pts[np++] = support(A, B, dir);
+    if (dot(pts[0], dir) < 0) return false;
+    dir = neg(pts[0]);
+    int it = 0;
+    while (true) {
+        it++;
+        if (it > 100) return false;
+        D2 p = support(A, B, dir);
+        double proj = dot(p, dir);
+        if (proj < 0) return false;
+        pts[np++] = p;
+        if (np == 2) {
+            D2 a = pts[1], b = pts[0];
+            D2 ab = sub(b, a), ao = neg(a);
+            if (dot(ab, ao) > 0) {
+                D2 perp = d2(-ab.y, ab.x);
+                if (dot(perp, ao) < 0) perp = d2(ab.y, -ab.x);
+                dir = perp;
+            } else {
+                pts[0] = a; np = 1;
+                dir = ao;
+            }
+        } else {
+            D2 a = pts[2], b = pts[1], c = pts[0];
+            D2 ab = sub(b, a), ac = sub(c, a), ao = neg(a);
+            D2 abPerp = d2(ab.y, -ab.x);
+            if (dot(abPerp, ac) > 0) abPerp = d2(-ab.y, ab.x);
+            D2 acPerp = d2(ac.y, -ac.x);
+            if (dot(acPerp, ab) > 0) acPerp = d2(-ac.y, ac.x);
+            if (dot(ab, ao) > 0 && dot(abPerp, ao) > 0) {
+                pts[0] = pts[1]; pts[1] = pts[2]; np = 2;       // erase(begin)
+                dir = abPerp;
+            } else if (dot(ac, ao) > 0 && dot(acPerp, ao) > 0) {
+                pts[1] = pts[2]; np = 2;                         // erase(begin + 1)
+                dir = acPerp;
+            } else {
+                return true;
+            }
+        }
+    }
+}
+
+// EPA (epa.cpp:32-97)
+__device__ bool epa(const DShape &A, const DShape &B, const D2 *simplex, D2 &n, double &pen) {
+    D2 poly[EPA_MAX];
+    int np = 3;
+    poly[0] = simplex[0]; poly[1] = simplex[1]; poly[2] = simplex[2];
+    {
+        D2 ab = sub(poly[1], poly[0]), ac = sub(poly[2], poly[0]);
+        if (fabs(crs(ab, ac)) < 1e-14) return false;
+    }
+    {
+        double cv = (poly[1].x - poly[0].x) * (poly[2].y - poly[0].y) -
+                    (poly[1].y - poly[0].y) * (poly[2].x - poly[0].x);
+        if (cv < 0) { D2 t = poly[0]; poly[0] = poly[2]; poly[2] = t; }
+    }
+    for (int iter = 0; iter < 100; iter++) {
+        double closest = 1.7976931348623157e308;
+        int ce = -1;
+        D2 en = d2(0, 0);
+        for (int i = 0; i < np; i++) {
+            int j = (i + 1) % np;
+            D2 e = sub(poly[j], poly[i]);
+            D2 nn = nrm(d2(e.y, -e.x));
+            double dist = dot(nn, poly[i]);
+            if (dist < 0) { nn.x = -nn.x; nn.y = -nn.y; dist = -dist; }
+            if (dist < closest) { closest = dist; ce = i; en = nn; }
+        }
+        if (ce < 0) return false;
+        D2 p = support(A, B, en);
+        double d = dot(p, en);
+        if (d - closest < 1e-9) { n = en; pen = d; return true; }
+        int at = (ce + 1) % np;
+        for (int k = np; k > at; k--) poly[k] = poly[k - 1];
+        poly[at] = p;
+        np++;
+    }
+    return false;
+}
+
+__device__ __forceinline__ void world_verts(const DShape &s, D2 *v) {  // narrowphase.cpp:56-81
+    for (int i = 0; i < s.nv; i++) {
+        double lx = s.lv[2 * i], ly = s.lv[2 * i + 1];
+        double rx = lx * cos(s.angle) - ly * sin(s.angle);
+        double ry = lx * sin(s.angle) + ly * cos(s.angle);
+        v[i] = d2(s.pos.x + rx, s.pos.y + ry);
+    }
+}
+__device__ int clip_face(const D2 *in, int n, D2 pn, double off, D2 *out) {  // :203-234
+    int m = 0;
+    for (int i = 0; i < n; i++) {
+        int j = (i + 1) % n;
+        D2 p1 = in[i], p2 = in[j];
+        double dd1 = dot(pn, p1) - off, dd2 = dot(pn, p2) - off;
+        bool in1 = dd1 <= 0.0, in2 = dd2 <= 0.0;
+        if (in1 && m < CLIP_MAX) out[m++] = p1;
+        if (in1 != in2 && m < CLIP_MAX) {
+            double t = dd1 / (dd1 - dd2);
+            out[m++] = add(p1, mul(sub(p2, p1), t));
+        }
+    }
+    return m;
+}
+
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool body_candidate(const lpe_body &b) {
+    return (b.flags & LPE_BODY_HAS_MASS) && (b.flags & LPE_BODY_HAS_PHASE) && (b.flags & LPE_BODY_SOLID);
+}
+
+__global__ void k_rb_prep(int nb, const lpe_body *__restrict__ bodies, const double *__restrict__ verts,
+                          double lo, double hi, double4 *__restrict__ aabb, int32_t *__restrict__ cand) {
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb) return;
+    const lpe_body b = bodies[i];
+    double mnx, mny, mxx, mxy;
+    double angle = (b.flags & LPE_BODY_HAS_ANGPOS) ? b.angle : 0.0;
+    if (b.flags & LPE_BODY_CIRCLE) {
+        double r = b.radius;
+        mnx = b.x - r; mxx = b.x + r; mny = b.y - r; mxy = b.y + r;
+    } else {
+        mnx = b.x; mxx = b.x; mny = b.y; mxy = b.y;
+        const double *lv = verts + 2 * (size_t)b.vert_off;
+        for (int k = 0; k < b.vert_cnt; k++) {
+            double vx = lv[2 * k], vy = lv[2 * k + 1];
+            double rx = vx * cos(angle) - vy * sin(angle);
+            double ry = vx * sin(angle) + vy * cos(angle);
+            double wx = b.x + rx, wy = b.y + ry;
+            if (wx < mnx) mnx = wx;
+            if (wx > mxx) mxx = wx;
+            if (wy < mny) mny = wy;
+            if (wy > mxy) mxy = wy;
+        }
+    }
+    aabb[i] = make_double4(mnx, mny, mxx, mxy);
+    bool ok = body_candidate(b) && !(mxx < lo || mnx > hi || mxy < lo || mny > hi);
+    cand[i] = ok ? 1 : 0;
+}
+
+// tiled all-pairs test in rank (entity id) order; mode 0 counts, 1 fills
+__global__ void __launch_bounds__(RTPB)
+k_bp_pairs(int nb, int mode, const int32_t *__restrict__ byRank, const lpe_body *__restrict__ bodies,
+           const double4 *__restrict__ aabb, const int32_t *__restrict__ cand, double small,
+           int32_t *__restrict__ pcount, const int32_t *__restrict__ pstart,
+           int32_t *__restrict__ pcursor, int2 *__restrict__ pairs, int32_t *__restrict__ pairRankB,
+           int cap_pairs, int32_t *__restrict__ status) {
+    if (blockIdx.y < blockIdx.x) return;
+    __shared__ double4 tb[RTPB];
+    __shared__ int tc[RTPB], ti[RTPB];
+    __shared__ uint32_t tf[RTPB];
+    int rb0 = blockIdx.y * RTPB;
+    {
+        int r = rb0 + threadIdx.x;
+        if (r < nb) {
+            int j = byRank[r];
+            tb[threadIdx.x] = aabb[j]; tc[threadIdx.x] = cand[j]; ti[threadIdx.x] = j;
+            tf[threadIdx.x] = bodies[j].flags;
+        } else {
+            tc[threadIdx.x] = 0;
+        }
+    }
+    __syncthreads();
+    int ra = blockIdx.x * RTPB + threadIdx.x;
+    if (ra >= nb) return;
+    int ia = byRank[ra];
+    if (!cand[ia]) return;
+    double4 A = aabb[ia];
+    bool aB = (bodies[ia].flags & LPE_BODY_BOUNDARY) != 0;
+    double sa = fmax(A.z - A.x, A.w - A.y);
+    int cnt = 0;
+    for (int k = 0; k < RTPB; k++) {
+        int rbk = rb0 + k;
+        if (rbk <= ra || !tc[k]) continue;
+        double4 B = tb[k];
+        if (A.z < B.x || A.x > B.z) continue;                  // boxesOverlap (broadphase.cpp:35-39)
+        if (A.w < B.y || A.y > B.w) continue;
+        bool bB = (tf[k] & LPE_BODY_BOUNDARY) != 0;
+        if (aB && bB) continue;
+        double sb = fmax(B.z - B.x, B.w - B.y);
+        if (sa < small && sb < small) continue;
+        if (mode == 0) {
+            cnt++;
+        } else {
+            int slot = atomicAdd(&pcursor[ra], 1);   // cursor starts at pstart[ra]
+            if (slot < cap_pairs) { pairs[slot] = make_int2(ia, ti[k]); pairRankB[slot] = rbk; }
+            else atomicOr(&status[0], 1);
+        }
+    }
+    if (mode == 0 && cnt) atomicAdd(&pcount[ra], cnt);
+}
+
+__global__ void k_bp_sort(int nb, const int32_t *__restrict__ pstart, int2 *__restrict__ pairs,
+                          int32_t *__restrict__ rk, int cap_pairs) {
+    int r = blockIdx.x * RTPB + threadIdx.x;
+    if (r >= nb) return;
+    int s = pstart[r], e = min(pstart[r + 1], cap_pairs);
+    for (int k = s + 1; k < e; k++) {
+        int v = rk[k];
+        int2 p = pairs[k];
+        int j = k - 1;
+        while (j >= s && rk[j] > v) { rk[j + 1] = rk[j]; pairs[j + 1] = pairs[j]; j--; }
+        rk[j + 1] = v; pairs[j + 1] = p;
+    }
+}
+
+// narrowPhase (narrowphase.cpp:352-420): one thread per pair
+__global__ void __launch_bounds__(128)
+k_narrow(const int32_t *__restrict__ npptr, const int2 *__restrict__ pairs,
+         const lpe_body *__restrict__ bodies, const double *__restrict__ verts,
+         lpe_contact *__restrict__ slots, int32_t *__restrict__ ccount) {
+    int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= *npptr) return;
+    int2 pr = pairs[k];
+    const lpe_body ba = bodies[pr.x], bb = bodies[pr.y];
+    DShape A = dshape(ba, verts), B = dshape(bb, verts);
+    int cnt = 0;
+    D2 simplex[4];
+    int ns;
+    lpe_contact *out = slots + (size_t)k * MAXC;
+    if (gjk(A, B, simplex, ns)) {
+        D2 n;
+        double pen;
+        if (epa(A, B, simplex, n, pen)) {
+            lpe_contact c;
+            c.a = pr.x; c.b = pr.y; c.pair = k; c.pad = 0;
+            c.nx = n.x; c.ny = n.y; c.pen = pen;
+            if (A.circle || B.circle) {
+                D2 cp;
+                if (A.circle && B.circle) cp = sub(B.pos, mul(n, B.radius));
+                else if (A.circle) cp = add(A.pos, mul(n, A.radius));
+                else cp = sub(B.pos, mul(n, B.radius));
+                c.px = cp.x; c.py = cp.y;
+                out[cnt++] = c;
+            } else {
+                // buildPolygonPolygonContacts (narrowphase.cpp:304-350), reference face on A
+                D2 av[MAXV], bv[CLIP_MAX], t1[CLIP_MAX], t2[CLIP_MAX];
+                int na = min(A.nv, MAXV), nbv = min(B.nv, MAXV);
+                world_verts(A, av);
+                DShape Bc = B; Bc.nv = nbv;
+                world_verts(Bc, bv);
+                int fa = 0;
+                double bestDot = -1e30;
+                for (int i = 0; i < na; i++) {                   // findBestFace (:126-145)
+                    int j = (i + 1) % na;
+                    D2 e = sub(av[j], av[i]);
+                    D2 fn = nrm(d2(-e.y, e.x));
+                    double d = dot(fn, n);
+                    if (d > bestDot) { bestDot = d; fa = i; }
+                }
+                D2 v1 = av[fa], v2 = av[(fa + 1) % na];
+                D2 ea = sub(v2, v1);
+                D2 refN = nrm(d2(-ea.y, ea.x));
+                double faceOff = dot(refN, v1);
+                D2 edge = nrm(sub(v2, v1));
+                D2 botN = neg(edge);
+                int m1 = clip_face(bv, nbv, refN, faceOff, t1);
+                int m2 = clip_face(t1, m1, edge, dot(edge, v2), t2);
+                int m3 = clip_face(t2, m2, botN, dot(botN, v1), t1);
+                double planeOff = dot(refN, v1);
+                for (int q = 0; q < m3 && cnt < MAXC; q++) {
+                    c.pen = -(dot(refN, t1[q]) - planeOff);
+                    c.px = t1[q].x; c.py = t1[q].y;
+                    out[cnt++] = c;
+                }
+            }
+        }
+    }
+    ccount[k] = cnt;
+}
+
+__global__ void k_compact(const int32_t *__restrict__ npptr, const lpe_contact *__restrict__ slots,
+                          const int32_t *__restrict__ ccount, const int32_t *__restrict__ cstart,
+                          lpe_contact *__restrict__ out, int cap) {
+    int k = blockIdx.x * RTPB + threadIdx.x;
+    if (k >= *npptr) return;
+    int s = cstart[k];
+    for (int j = 0; j < ccount[k]; j++)
+        if (s + j < cap) out[s + j] = slots[(size_t)k * MAXC + j];
+}
+
+// ---------------------------------------------------------------------------
+// PGS preparation (contact_solver.cpp:42-253)
+__device__ __forceinline__ bool infinite_mass(const lpe_body &b) {
+    return (b.flags & LPE_BODY_HAS_MASS) && b.mass > 1e29;
+}
+__device__ __forceinline__ bool can_rotate(const lpe_body &b) {
+    if (!(b.flags & LPE_BODY_HAS_ANGVEL) || !(b.flags & LPE_BODY_HAS_INERTIA)) return false;
+    return b.inertia > 1e-12 && b.inertia < 1e29;
+}
+
+__global__ void k_mark_contacts(const int32_t *__restrict__ ncptr, const lpe_contact *__restrict__ cs,
+                                int32_t *__restrict__ inContact) {
+    int k = blockIdx.x * RTPB + threadIdx.x;
+    if (k >= *ncptr) return;
+    inContact[cs[k].a] = 1;
+    inContact[cs[k].b] = 1;
+}
+
+__global__ void k_pgs_bodies(int nb, const lpe_body *__restrict__ bodies, float *__restrict__ vel0,
+                             float *__restrict__ imii) {
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb) return;
+    const lpe_body b = bodies[i];
+    double m = b.mass;
+    float im = (m > 1e29) ? 0.f : (float)(1.0 / m);
+    float iv = 0.f;
+    bool cr = can_rotate(b);
+    if (cr) {
+        double I = b.inertia;
+        if (I > 1e-12 && I < 1e29) iv = (float)(1.0 / I);
+    }
+    imii[2 * i] = im; imii[2 * i + 1] = iv;
+    vel0[3 * i] = (float)b.vx;
+    vel0[3 * i + 1] = (float)b.vy;
+    vel0[3 * i + 2] = cr ? (float)b.omega : 0.f;
+}
+
+__device__ __forceinline__ float cross2f(float ax, float ay, float bx, float by) {
+    float l0 = ax * by, l1 = ay * bx;                      // cross2fNeon (:207-214)
+    return l0 - l1;
+}
+
+// buildConstraintRows (:133-197) + computeEffectiveMass (:216-253), item t
+__global__ void k_pgs_rows(const int32_t *__restrict__ ncptr, const int32_t *__restrict__ order,
+                           const lpe_contact *__restrict__ cs, const lpe_body *__restrict__ bodies,
+                           const float *__restrict__ imii, float4 *__restrict__ rowN,
+                           float4 *__restrict__ rowR, int2 *__restrict__ rowAB,
+                           int32_t *__restrict__ sItemA, int32_t *__restrict__ sItemB) {
+    int t = blockIdx.x * RTPB + threadIdx.x;
+    if (t >= *ncptr) return;
+    const lpe_contact c = cs[order ? order[t] : t];
+    const lpe_body A = bodies[c.a], B = bodies[c.b];
+    int a = infinite_mass(A) ? -1 : c.a;
+    int b = infinite_mass(B) ? -1 : c.b;
+    D2 u = nrm(d2(c.nx, c.ny));
+    float dirX = (float)u.x, dirY = (float)u.y;
+    float rxA = (float)(c.px - A.x), ryA = (float)(c.py - A.y);
+    float rxB = (float)(c.px - B.x), ryB = (float)(c.py - B.y);
+    float imA = 0.f, imB = 0.f, iiA = 0.f, iiB = 0.f;
+    if (a >= 0) { imA = imii[2 * a]; iiA = imii[2 * a + 1]; }
+    if (b >= 0) { imB = imii[2 * b]; iiB = imii[2 * b + 1]; }
+    float effN, effF;
+    {
+        float rAxn = cross2f(rxA, ryA, dirX, dirY), rBxn = cross2f(rxB, ryB, dirX, dirY);
+        float sum = imA + imB + (rAxn * rAxn) * iiA + (rBxn * rBxn) * iiB;
+        effN = (sum < 1e-12F) ? 0.F : 1.F / sum;
+    }
+    {
+        float fx = -dirY, fy = dirX;
+        float rAxn = cross2f(rxA, ryA, fx, fy), rBxn = cross2f(rxB, ryB, fx, fy);
+        float sum = imA + imB + (rAxn * rAxn) * iiA + (rBxn * rBxn) * iiB;
+        effF = (sum < 1e-12F) ? 0.F : 1.F / sum;
+    }
+    rowN[t] = make_float4(dirX, dirY, effN, effF);
+    rowR[t] = make_float4(rxA, ryA, rxB, ryB);
+    rowAB[t] = make_int2(a, b);
+    sItemA[t] = a;
+    sItemB[t] = b;
+}
+
+// ---------------------------------------------------------------------------
+// level scheduling of a sequential sweep (items touching bodies sItemA/B)
+__global__ void k_sched_count(const int32_t *__restrict__ kptr, const int32_t *__restrict__ ia,
+                              const int32_t *__restrict__ ib, int32_t *__restrict__ bcount) {
+    int t = blockIdx.x * RTPB + threadIdx.x;
+    if (t >= *kptr) return;
+    if (ia[t] >= 0) atomicAdd(&bcount[ia[t]], 1);
+    if (ib[t] >= 0) atomicAdd(&bcount[ib[t]], 1);
+}
+__global__ void k_sched_fill(const int32_t *__restrict__ kptr, const int32_t *__restrict__ ia,
+                             const int32_t *__restrict__ ib, int32_t *__restrict__ cursor,
+                             int32_t *__restrict__ ent) {
+    int t = blockIdx.x * RTPB + threadIdx.x;
+    if (t >= *kptr) return;
+    if (ia[t] >= 0) ent[atomicAdd(&cursor[ia[t]], 1)] = t;
+    if (ib[t] >= 0) ent[atomicAdd(&cursor[ib[t]], 1)] = t;
+}
+// per body segment: sort item ids ascending, then link prev pointers
+__global__ void k_sched_link(int nb, const int32_t *__restrict__ bstart, int32_t *__restrict__ ent,
+                             const int32_t *__restrict__ ia, int32_t *__restrict__ prevA,
+                             int32_t *__restrict__ prevB) {
+    int body = blockIdx.x * RTPB + threadIdx.x;
+    if (body >= nb) return;
+    int s = bstart[body], e = bstart[body + 1];
+    for (int k = s + 1; k < e; k++) {
+        int v = ent[k];
+        int j = k - 1;
+        while (j >= s && ent[j] > v) { ent[j + 1] = ent[j]; j--; }
+        ent[j + 1] = v;
+    }
+    for (int k = s; k < e; k++) {
+        int t = ent[k];
+        int p = (k > s) ? ent[k - 1] : -1;
+        if (ia[t] == body) prevA[t] = p; else prevB[t] = p;
+    }
+}
+// longest-chain level by monotone relaxation in one workgroup
+__global__ void __launch_bounds__(SOLVE_TPB)
+k_sched_levels(const int32_t *__restrict__ kptr, const int32_t *__restrict__ prevA,
+               const int32_t *__restrict__ prevB, int32_t *__restrict__ level,
+               int32_t *__restrict__ nlevels) {
+    __shared__ int changed, mx;
+    int K = *kptr;
+    for (int t = threadIdx.x; t < K; t += SOLVE_TPB) level[t] = 0;
+    __syncthreads();
+    while (true) {
+        if (threadIdx.x == 0) changed = 0;
+        __syncthreads();
+        int ch = 0;
+        for (int t = threadIdx.x; t < K; t += SOLVE_TPB) {
+            int pa = prevA[t], pb = prevB[t];
+            int L = 0;
+            if (pa >= 0) L = max(L, __hip_atomic_load(&level[pa], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) + 1);
+            if (pb >= 0) L = max(L, __hip_atomic_load(&level[pb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) + 1);
+            if (L > level[t]) {
+                __hip_atomic_store(&level[t], L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                ch = 1;
+            }
+        }
+        if (ch) changed = 1;
+        __syncthreads();
+        if (!changed) break;
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) mx = -1;
+    __syncthreads();
+    int lm = -1;
+    for (int t = threadIdx.x; t < K; t += SOLVE_TPB) lm = max(lm, level[t]);
+    atomicMax(&mx, lm);
+    __syncthreads();
+    if (threadIdx.x == 0) *nlevels = mx + 1;
+}
+__global__ void k_level_count(const int32_t *__restrict__ kptr, const int32_t *__restrict__ level,
+                              int32_t *__restrict__ lcount) {
+    int t = blockIdx.x * RTPB + threadIdx.x;
+    if (t >= *kptr) return;
+    atomicAdd(&lcount[level[t]], 1);
+}
+__global__ void k_level_fill(const int32_t *__restrict__ kptr, const int32_t *__restrict__ level,
+                             int32_t *__restrict__ lcursor, int32_t *__restrict__ lorder) {
+    int t = blockIdx.x * RTPB + threadIdx.x;
+    if (t >= *kptr) return;
+    lorder[atomicAdd(&lcursor[level[t]], 1)] = t;
+}
+
+// ---------------------------------------------------------------------------
+// solveLcpPgs (:381-440) level by level; body velocities in LDS
+__global__ void __launch_bounds__(SOLVE_TPB)
+k_pgs_solve(int nb, const int32_t *__restrict__ nlevels, const int32_t *__restrict__ lstart,
+            const int32_t *__restrict__ lorder, const float4 *__restrict__ rowN,
+            const float4 *__restrict__ rowR, const int2 *__restrict__ rowAB,
+            const float *__restrict__ imii, float *__restrict__ vel, int iters, float mu,
+            float *__restrict__ lamN, float *__restrict__ lamF, const int32_t *__restrict__ ncptr) {
+    extern __shared__ float sv[];   // 3 floats per body
+    for (int i = threadIdx.x; i < 3 * nb; i += SOLVE_TPB) sv[i] = vel[i];
+    int K = *ncptr;
+    for (int t = threadIdx.x; t < K; t += SOLVE_TPB) { lamN[t] = 0.f; lamF[t] = 0.f; }
+    __syncthreads();
+    const int L = *nlevels;
+    for (int it = 0; it < iters; it++) {
+        for (int l = 0; l < L; l++) {
+            int s = lstart[l], e = lstart[l + 1];
+            for (int q = s + threadIdx.x; q < e; q += SOLVE_TPB) {
+                int t = lorder[q];
+                float4 rn = rowN[t], rr = rowR[t];
+                int2 ab = rowAB[t];
+                float imA = 0.f, iiA = 0.f, imB = 0.f, iiB = 0.f;
+                if (ab.x >= 0) { imA = imii[2 * ab.x]; iiA = imii[2 * ab.x + 1]; }
+                if (ab.y >= 0) { imB = imii[2 * ab.y]; iiB = imii[2 * ab.y + 1]; }
+                // rows: normal (dir) then friction (-dirY, dirX)
+                for (int row = 0; row < 2; row++) {
+                    float dX = row == 0 ? rn.x : -rn.y;
+                    float dY = row == 0 ? rn.y : rn.x;
+                    float eff = row == 0 ? rn.z : rn.w;
+                    float vxA = 0.f, vyA = 0.f, wA = 0.f, vxB = 0.f, vyB = 0.f, wB = 0.f;
+                    if (ab.x >= 0) { vxA = sv[3 * ab.x]; vyA = sv[3 * ab.x + 1]; wA = sv[3 * ab.x + 2]; }
+                    if (ab.y >= 0) { vxB = sv[3 * ab.y]; vyB = sv[3 * ab.y + 1]; wB = sv[3 * ab.y + 2]; }
+                    float ax = vxA - wA * rr.y, ay = vyA + wA * rr.x;
+                    float bx = vxB - wB * rr.w, by = vyB + wB * rr.z;
+                    float relX = bx - ax, relY = by - ay;
+                    float vrel = relX * dX + relY * dY;
+                    float old, lo, hi;
+                    if (row == 0) { old = lamN[t]; lo = 0.0f; hi = 1e20f; }
+                    else {
+                        old = lamF[t];
+                        float limit = mu * lamN[t];
+                        lo = -limit; hi = limit;
+                    }
+                    float dl = -eff * (vrel + 0.0f);
+                    float nl = old + dl;
+                    if (nl < lo) nl = lo;
+                    if (nl > hi) nl = hi;
+                    dl = nl - old;
+                    if (row == 0) lamN[t] = nl; else lamF[t] = nl;
+                    if (fabsf(dl) < 1e-15F) continue;                // applyImpulse (:315-356)
+                    if (ab.x >= 0) {
+                        sv[3 * ab.x] -= dX * (dl * imA);
+                        sv[3 * ab.x + 1] -= dY * (dl * imA);
+                        float crossA = rr.x * dY - rr.y * dX;
+                        sv[3 * ab.x + 2] -= crossA * dl * iiA;
+                    }
+                    if (ab.y >= 0) {
+                        sv[3 * ab.y] += dX * (dl * imB);
+                        sv[3 * ab.y + 1] += dY * (dl * imB);
+                        float crossB = rr.z * dY - rr.w * dX;
+                        sv[3 * ab.y + 2] += crossB * dl * iiB;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = threadIdx.x; i < 3 * nb; i += SOLVE_TPB) vel[i] = sv[i];
+}
+
+// write velocities of dynamic bodies in the DOF table (:516-529)
+__global__ void k_pgs_writeback(int nb, lpe_body *__restrict__ bodies, const float *__restrict__ vel,
+                                const int32_t *__restrict__ inContact) {
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb || !inContact[i]) return;
+    lpe_body &b = bodies[i];
+    if (infinite_mass(b)) return;
+    b.vx = vel[3 * i];
+    b.vy = vel[3 * i + 1];
+    if (can_rotate(b)) b.omega = vel[3 * i + 2];
+}
+
+// ---------------------------------------------------------------------------
+// position solver (position_solver.cpp)
+__device__ __forceinline__ bool solid_body(const lpe_body &b) {
+    return (b.flags & LPE_BODY_HAS_PHASE) && (b.flags & LPE_BODY_SOLID);
+}
+// loadBodyData (:125-168): invM, invI, canRotate(bit0), valid(bit1), solid(bit2)
+__global__ void k_pos_bodies(int nb, const lpe_body *__restrict__ bodies, double *__restrict__ st) {
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb) return;
+    const lpe_body b = bodies[i];
+    double invM = (b.mass > 1e29) ? 0.0 : (1.0 / b.mass);
+    double invI = 0.0;
+    int fl = 0;
+    if (b.flags & LPE_BODY_HAS_INERTIA) {
+        double I = b.inertia;
+        if (I < 1e29 && I > 1e-12) { fl |= 1; invI = 1.0 / I; }
+    }
+    if (b.flags & LPE_BODY_HAS_MASS) fl |= 2;
+    if (solid_body(b)) fl |= 4;
+    st[3 * i] = invM;
+    st[3 * i + 1] = invI;
+    st[3 * i + 2] = (double)fl;
+}
+// gatherPositionData (:67-120): keep contacts with at least one Solid body;
+// a body is a dependency only if it can move (invM != 0 or canRotate)
+__global__ void k_pos_items(const int32_t *__restrict__ ncptr, const lpe_contact *__restrict__ cs,
+                            const lpe_body *__restrict__ bodies, const double *__restrict__ st,
+                            int32_t *__restrict__ keep) {
+    int k = blockIdx.x * RTPB + threadIdx.x;
+    if (k >= *ncptr) return;
+    const lpe_contact c = cs[k];
+    keep[k] = (solid_body(bodies[c.a]) || solid_body(bodies[c.b])) ? 1 : 0;
+}
+__global__ void k_pos_fill(const int32_t *__restrict__ ncptr, const int32_t *__restrict__ keep,
+                           const int32_t *__restrict__ kstart, const lpe_contact *__restrict__ cs,
+                           const double *__restrict__ st, int32_t *__restrict__ item,
+                           int32_t *__restrict__ ia, int32_t *__restrict__ ib,
+                           int32_t *__restrict__ inPos) {
+    int k = blockIdx.x * RTPB + threadIdx.x;
+    if (k >= *ncptr || !keep[k]) return;
+    int t = kstart[k];
+    const lpe_contact c = cs[k];
+    item[t] = k;
+    auto movable = [&](int b) {
+        return st[3 * b] != 0.0 || ((int)st[3 * b + 2] & 1);
+    };
+    ia[t] = movable(c.a) ? c.a : -1;
+    ib[t] = movable(c.b) ? c.b : -1;
+    inPos[c.a] = 1;
+    inPos[c.b] = 1;
+}
+__global__ void __launch_bounds__(SOLVE_TPB)
+k_pos_solve(int nb, const int32_t *__restrict__ nlevels, const int32_t *__restrict__ lstart,
+            const int32_t *__restrict__ lorder, const int32_t *__restrict__ item,
+            const lpe_contact *__restrict__ cs, const double *__restrict__ st,
+            lpe_body *__restrict__ bodies, const int32_t *__restrict__ inPos, int iters,
+            double baumgarte, double slop) {
+    extern __shared__ double sp[];   // x, y, angle per body
+    for (int i = threadIdx.x; i < nb; i += SOLVE_TPB) {
+        const lpe_body &b = bodies[i];
+        sp[3 * i] = b.x; sp[3 * i + 1] = b.y;
+        sp[3 * i + 2] = (b.flags & LPE_BODY_HAS_ANGPOS) ? b.angle : 0.0;
+    }
+    __syncthreads();
+    const int L = *nlevels;
+    for (int it = 0; it < iters; it++) {
+        for (int l = 0; l < L; l++) {
+            int s = lstart[l], e = lstart[l + 1];
+            for (int q = s + threadIdx.x; q < e; q += SOLVE_TPB) {
+                const lpe_contact c = cs[item[lorder[q]]];
+                int fa = (int)st[3 * c.a + 2], fb = (int)st[3 * c.b + 2];
+                if (!(fa & 2) || !(fb & 2)) continue;
+                if (!(fa & 4) && !(fb & 4)) continue;
+                double pen = c.pen - slop;
+                if (pen <= 0.0) continue;
+                D2 n = nrm(d2(c.nx, c.ny));
+                double corr = baumgarte * pen;
+                double invMA = st[3 * c.a], invMB = st[3 * c.b];
+                double invIA = st[3 * c.a + 1], invIB = st[3 * c.b + 1];
+                D2 rA = d2(c.px - sp[3 * c.a], c.py - sp[3 * c.a + 1]);
+                D2 rB = d2(c.px - sp[3 * c.b], c.py - sp[3 * c.b + 1]);
+                double rAn = crs(rA, n), rBn = crs(rB, n);
+                double denom = invMA + invMB + (rAn * rAn) * invIA + (rBn * rBn) * invIB;
+                if (denom < 1e-12) continue;
+                double sc = corr / denom;
+                double dx = n.x * sc, dy = n.y * sc;
+                sp[3 * c.a] -= dx * invMA;
+                sp[3 * c.a + 1] -= dy * invMA;
+                if (fa & 1) sp[3 * c.a + 2] -= rAn * sc * invIA;
+                sp[3 * c.b] += dx * invMB;
+                sp[3 * c.b + 1] += dy * invMB;
+                if (fb & 1) sp[3 * c.b + 2] += rBn * sc * invIB;
+            }
+            __syncthreads();
+        }
+    }
+    // storeBodyData (:176-197)
+    for (int i = threadIdx.x; i < nb; i += SOLVE_TPB) {
+        if (!inPos[i]) continue;
+        int f = (int)st[3 * i + 2];
+        if (!(f & 2)) continue;
+        lpe_body &b = bodies[i];
+        b.x = sp[3 * i]; b.y = sp[3 * i + 1];
+        if ((f & 1) && (b.flags & LPE_BODY_HAS_ANGPOS)) b.angle = sp[3 * i + 2];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// integrator systems (per body, fp64)
+__global__ void k_boundary(int nb, lpe_body *__restrict__ bodies, double m, double U, double damp,
+                           double maxSpeed) {   // boundary.cpp:13-70
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb) return;
+    lpe_body b = bodies[i];
+    if (!(b.flags & LPE_BODY_HAS_VEL)) return;
+    if ((b.flags & LPE_BODY_HAS_SLEEP) && (b.flags & LPE_BODY_ASLEEP)) return;
+    bool bounced = false;
+    if (b.x < m) { b.x = m; b.vx = fabs(b.vx) * damp; bounced = true; }
+    else if (b.x > U - m) { b.x = U - m; b.vx = -fabs(b.vx) * damp; bounced = true; }
+    if (b.y < m) { b.y = m; b.vy = fabs(b.vy) * damp; bounced = true; }
+    else if (b.y > U - m) { b.y = U - m; b.vy = -fabs(b.vy) * damp; bounced = true; }
+    if (bounced) {
+        double sp = sqrt(b.vx * b.vx + b.vy * b.vy);
+        if (sp > maxSpeed) { b.vx = (b.vx / sp) * maxSpeed; b.vy = (b.vy / sp) * maxSpeed; }
+    }
+    bodies[i] = b;
+}
+__device__ __forceinline__ bool gravity_view(const lpe_body &b) {
+    return (b.flags & LPE_BODY_HAS_PHASE) && (b.flags & LPE_BODY_HAS_VEL) &&
+           (b.flags & LPE_BODY_HAS_MASS) && !(b.flags & LPE_BODY_BOUNDARY);
+}
+__global__ void k_gravity_check(int nb, const lpe_body *__restrict__ bodies, double thr,
+                                int32_t *__restrict__ heavy) {   // gravity.cpp:43-51
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb) return;
+    if (thr > 0.0 && gravity_view(bodies[i]) && bodies[i].mass >= thr) atomicOr(heavy, 1);
+}
+__global__ void k_gravity(int nb, lpe_body *__restrict__ bodies, double g, double dt,
+                          const int32_t *__restrict__ heavy) {   // gravity.cpp:53-57
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb || *heavy) return;
+    if (gravity_view(bodies[i])) bodies[i].vy += g * dt;
+}
+__global__ void k_rotation(int nb, lpe_body *__restrict__ bodies, double dt, double damping,
+                           double maxw) {   // rotation.cpp:18-60
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb) return;
+    lpe_body b = bodies[i];
+    if (!(b.flags & LPE_BODY_HAS_ANGPOS) || !(b.flags & LPE_BODY_HAS_ANGVEL)) return;
+    if (b.flags & LPE_BODY_BOUNDARY) return;
+    const double Pi = 3.141592654;
+    b.angle += b.omega * dt;
+    if (damping < 1.0) b.omega *= damping;
+    if (maxw > 0) {
+        if (b.omega > maxw) b.omega = maxw;
+        if (b.omega < -maxw) b.omega = -maxw;
+    }
+    if (b.angle > 2.0 * Pi) b.angle -= 2.0 * Pi;
+    else if (b.angle < 0) b.angle += 2.0 * Pi;
+    bodies[i] = b;
+}
+__global__ void k_movement(int nb, lpe_body *__restrict__ bodies, double dt) {  // movement.cpp:13-39
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb) return;
+    lpe_body b = bodies[i];
+    if (!(b.flags & LPE_BODY_HAS_VEL) || (b.flags & LPE_BODY_BOUNDARY)) return;
+    if ((b.flags & LPE_BODY_HAS_PHASE) && (b.flags & LPE_BODY_LIQUID)) return;
+    b.x += b.vx * dt;
+    b.y += b.vy * dt;
+    bodies[i] = b;
+}
+__global__ void k_sleep(int nb, lpe_body *__restrict__ bodies, double lin, double ang,
+                        int frames) {   // sleep.cpp:19-67
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb) return;
+    lpe_body b = bodies[i];
+    const uint32_t need = LPE_BODY_HAS_VEL | LPE_BODY_HAS_PHASE | LPE_BODY_HAS_MASS | LPE_BODY_HAS_SLEEP;
+    if ((b.flags & need) != need || (b.flags & LPE_BODY_BOUNDARY)) return;
+    double speed = sqrt(b.vx * b.vx + b.vy * b.vy);
+    double as = (b.flags & LPE_BODY_HAS_ANGVEL) ? fabs(b.omega) : 0.0;
+    bool asleep = (b.flags & LPE_BODY_ASLEEP) != 0;
+    if (speed < lin && as < ang) {
+        if (!asleep) {
+            b.sleep_counter++;
+            if (b.sleep_counter > frames) asleep = true;
+        }
+    } else {
+        b.sleep_counter = 0;
+        asleep = false;
+    }
+    if (asleep) {
+        b.flags |= LPE_BODY_ASLEEP;
+        b.vx = 0; b.vy = 0;
+        if (b.flags & LPE_BODY_HAS_ANGVEL) b.omega = 0;
+    } else {
+        b.flags &= ~LPE_BODY_ASLEEP;
+    }
+    bodies[i] = b;
+}
+
+}  // namespace lpe
+
+using namespace lpe;
+
+// ===========================================================================
+// host side
+static inline int rblk(long n, int t = RTPB) { return (int)((n + t - 1) / t); }
+
+template <typename T>
+static int rgrow(lpe_ctx *ctx, T **p, size_t n) {
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    hipError_t e = hipMalloc((void **)p, sizeof(T) * std::max<size_t>(n, 1));
+    if (e != hipSuccess) { ctx->err = std::string("hipMalloc: ") + hipGetErrorString(e); return LPE_ERR_HIP; }
+    return LPE_OK;
+}
+
+int lpe_rigid_destroy_internal(lpe_ctx *ctx) {
+    RigidDev *d = (RigidDev *)ctx->rigid;
+    if (!d) return LPE_OK;
+    void *ptrs[] = {d->bodies, d->verts, d->rank, d->byRank, d->aabb, d->cand, d->pcount, d->pstart,
+                    d->pcursor, d->pairs, d->pairRankB, d->cslots, d->ccount, d->cstart, d->contacts,
+                    d->bsum, d->order, d->rowN, d->rowR, d->rowAB, d->vel0, d->imii, d->inContact,
+                    d->posState, d->posAB, d->posItem, d->sItemA, d->sItemB, d->sPrevA, d->sPrevB,
+                    d->sLevel, d->sBCount, d->sBStart, d->sBCursor, d->sEnt, d->sSorted, d->sLCount,
+                    d->sLStart, d->sLCursor, d->sLOrder, d->counts};
+    for (void *p : ptrs) if (p) (void)hipFree(p);
+    delete d;
+    ctx->rigid = nullptr;
+    return LPE_OK;
+}
+
+extern "C" int lpe_rigid_config_default(lpe_rigid_config *c) {
+    if (!c) return LPE_ERR_ARG;
+    std::memset(c, 0, sizeof(*c));
+    c->universeSize = 6.0; c->metersPerPixel = 0.01; c->quadtreeCapacity = 8;
+    c->boundaryBuffer = 500.0; c->smallParticleThreshold = 0.01; c->pgsIterations = 10;
+    c->frictionCoeff = 0.5f; c->posIterations = 10; c->baumgarte = 0.02; c->slop = 0.001;
+    c->gravity = 9.8; c->planetaryMassThreshold = 1e10; c->angularDamping = 0.98;
+    c->maxAngularSpeed = 20.0; c->marginPixels = 15.0; c->bounceDamping = 0.7; c->maxSpeed = 1.0;
+    c->linearSleepThreshold = 0.5; c->angularSleepThreshold = 0.5; c->sleepFramesThreshold = 60;
+    return LPE_OK;
+}
+
+extern "C" int lpe_rigid_set_config(lpe_ctx *ctx, const lpe_rigid_config *cfg) {
+    if (!ctx || !cfg) return LPE_ERR_ARG;
+    RigidDev *d = rdev(ctx);
+    d->cfg = *cfg;
+    d->cfg_set = true;
+    return LPE_OK;
+}
+
+static int rigid_alloc_bodies(lpe_ctx *ctx, RigidDev *d, int nb) {
+    if (nb <= d->cap_nb && d->bodies) return LPE_OK;
+    int st = 0;
+    size_t N = (size_t)nb;
+    if ((st = rgrow(ctx, &d->bodies, N))) return st;
+    if ((st = rgrow(ctx, &d->rank, N))) return st;
+    if ((st = rgrow(ctx, &d->byRank, N))) return st;
+    if ((st = rgrow(ctx, &d->aabb, N))) return st;
+    if ((st = rgrow(ctx, &d->cand, N))) return st;
+    if ((st = rgrow(ctx, &d->pcount, N))) return st;
+    if ((st = rgrow(ctx, &d->pstart, N + 1))) return st;
+    if ((st = rgrow(ctx, &d->pcursor, N))) return st;
+    if ((st = rgrow(ctx, &d->vel0, 3 * N))) return st;
+    if ((st = rgrow(ctx, &d->imii, 2 * N))) return st;
+    if ((st = rgrow(ctx, &d->inContact, 2 * N))) return st;
+    if ((st = rgrow(ctx, &d->posState, 3 * N))) return st;
+    if ((st = rgrow(ctx, &d->sBCount, N))) return st;
+    if ((st = rgrow(ctx, &d->sBStart, N + 1))) return st;
+    if ((st = rgrow(ctx, &d->sBCursor, N))) return st;
+    if (!d->counts && (st = rgrow(ctx, &d->counts, 16))) return st;
+    d->cap_nb = nb;
+    return LPE_OK;
+}
+
+static int rigid_alloc_pairs(lpe_ctx *ctx, RigidDev *d, int cap_pairs) {
+    if (cap_pairs <= d->cap_pairs && d->pairs) return LPE_OK;
+    int st = 0;
+    size_t P = (size_t)cap_pairs;
+    if ((st = rgrow(ctx, &d->pairs, P))) return st;
+    if ((st = rgrow(ctx, &d->pairRankB, P))) return st;
+    if ((st = rgrow(ctx, &d->cslots, P * MAXC))) return st;
+    if ((st = rgrow(ctx, &d->ccount, P))) return st;
+    if ((st = rgrow(ctx, &d->cstart, P + 1))) return st;
+    d->cap_pairs = cap_pairs;
+    return LPE_OK;
+}
+
+static int rigid_alloc_contacts(lpe_ctx *ctx, RigidDev *d, int cap) {
+    if (cap <= d->cap_contacts && d->contacts) return LPE_OK;
+    int st = 0;
+    size_t K = (size_t)cap;
+    if ((st = rgrow(ctx, &d->contacts, K))) return st;
+    if ((st = rgrow(ctx, &d->order, K))) return st;
+    if ((st = rgrow(ctx, &d->rowN, K))) return st;
+    if ((st = rgrow(ctx, &d->rowR, K))) return st;
+    if ((st = rgrow(ctx, &d->rowAB, K))) return st;
+    if ((st = rgrow(ctx, &d->posItem, K))) return st;
+    if ((st = rgrow(ctx, &d->posAB, K))) return st;
+    int32_t **arrs[] = {&d->sItemA, &d->sItemB, &d->sPrevA, &d->sPrevB, &d->sLevel, &d->sSorted,
+                        &d->sLOrder};
+    for (int32_t **a : arrs) if ((st = rgrow(ctx, a, K))) return st;
+    if ((st = rgrow(ctx, &d->sEnt, 2 * K))) return st;
+    if ((st = rgrow(ctx, &d->sLCount, K + 1))) return st;
+    if ((st = rgrow(ctx, &d->sLStart, K + 2))) return st;
+    if ((st = rgrow(ctx, &d->sLCursor, K + 1))) return st;
+    d->cap_contacts = cap;
+    return LPE_OK;
+}
+
+static int rigid_alloc_bsum(lpe_ctx *ctx, RigidDev *d, long n) {
+    int need = (int)(n / 1024 + 4);
+    if (need <= d->cap_bsum && d->bsum) return LPE_OK;
+    int st = rgrow(ctx, &d->bsum, (size_t)need);
+    if (st) return st;
+    d->cap_bsum = need;
+    return LPE_OK;
+}
+
+// exclusive scan of n (device count nptr or host ncap) ints; start[n] = total
+static int rscan(lpe_ctx *ctx, RigidDev *d, const int32_t *nptr, int ncap, const int32_t *cnt,
+                 int32_t *start, int32_t *cursor) {
+    int st = rigid_alloc_bsum(ctx, d, ncap);
+    if (st) return st;
+    int nb = ncap / 1024 + 1;
+    hipStream_t s = ctx->stream;
+    LPE_TIMED(ctx, "k_rscan_reduce", hipLaunchKernelGGL(k_rscan_reduce, dim3(nb), dim3(RTPB), 0, s, nptr, ncap, cnt, d->bsum));
+    LPE_TIMED(ctx, "k_rscan_blocks", hipLaunchKernelGGL(k_rscan_blocks, dim3(1), dim3(RTPB), 0, s, nptr, ncap, d->bsum, start));
+    LPE_TIMED(ctx, "k_rscan_final", hipLaunchKernelGGL(k_rscan_final, dim3(nb), dim3(RTPB), 0, s, nptr, ncap, cnt, d->bsum, start, cursor));
+    LPE_CHECK_LAUNCH(ctx, "rscan");
+    return LPE_OK;
+}
+
+extern "C" int lpe_rigid_upload(lpe_ctx *ctx, int nb, const lpe_body *bodies, int nverts,
+                                const double *verts) {
+    if (!ctx || nb < 0 || nverts < 0 || (nb > 0 && !bodies) || (nverts > 0 && !verts))
+        return LPE_ERR_ARG;
+    (void)hipSetDevice(ctx->device);
+    RigidDev *d = rdev(ctx);
+    if (!d->cfg_set) { lpe_rigid_config_default(&d->cfg); d->cfg_set = true; }
+    static bool lds_attr = false;
+    if (!lds_attr) {
+        (void)hipFuncSetAttribute((const void *)k_pgs_solve, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k_pos_solve, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        lds_attr = true;
+    }
+    int st = rigid_alloc_bodies(ctx, d, std::max(nb, 1));
+    if (st) return st;
+    if (nverts > d->cap_verts || !d->verts) {
+        if ((st = rgrow(ctx, &d->verts, 2 * (size_t)std::max(nverts, 1)))) return st;
+        d->cap_verts = nverts;
+    }
+    d->nb = nb;
+    d->nverts = nverts;
+    hipStream_t s = ctx->stream;
+    if (nb > 0) {
+        for (int i = 0; i < nb; i++) {
+            const lpe_body &b = bodies[i];
+            if (!(b.flags & LPE_BODY_CIRCLE) && (b.vert_off < 0 || b.vert_cnt < 0 ||
+                                                  b.vert_off + b.vert_cnt > nverts ||
+                                                  b.vert_cnt > MAXV)) {
+                ctx->err = "lpe_rigid_upload: polygon vertex range out of bounds (or > 32 vertices)";
+                return LPE_ERR_ARG;
+            }
+        }
+        // rank = position in entity-id order (pairs are ordered by eid)
+        std::vector<int32_t> byRank(nb), rank(nb);
+        for (int i = 0; i < nb; i++) byRank[i] = i;
+        std::stable_sort(byRank.begin(), byRank.end(),
+                         [&](int a, int b) { return bodies[a].eid < bodies[b].eid; });
+        for (int r = 0; r < nb; r++) rank[byRank[r]] = r;
+        LPE_HIP(ctx, hipMemcpyAsync(d->bodies, bodies, sizeof(lpe_body) * nb, hipMemcpyHostToDevice, s));
+        LPE_HIP(ctx, hipMemcpyAsync(d->rank, rank.data(), sizeof(int32_t) * nb, hipMemcpyHostToDevice, s));
+        LPE_HIP(ctx, hipMemcpyAsync(d->byRank, byRank.data(), sizeof(int32_t) * nb, hipMemcpyHostToDevice, s));
+        if (nverts > 0)
+            LPE_HIP(ctx, hipMemcpyAsync(d->verts, verts, sizeof(double) * 2 * nverts, hipMemcpyHostToDevice, s));
+        LPE_HIP(ctx, hipStreamSynchronize(s));
+    }
+    if (d->cap_pairs == 0) {
+        if ((st = rigid_alloc_pairs(ctx, d, std::max(16 * nb, 1024)))) return st;
+        if ((st = rigid_alloc_contacts(ctx, d, std::max(64 * nb, 4096)))) return st;
+    }
+    return LPE_OK;
+}
+
+// schedule items [0, K) (device count kptr, host bound kcap) whose dependency
+// bodies are sItemA/sItemB; result: levels count in *nlev, lstart/lorder
+static int rigid_schedule(lpe_ctx *ctx, RigidDev *d, const int32_t *kptr, int kcap,
+                          int32_t *nlev) {
+    hipStream_t s = ctx->stream;
+    int nb = d->nb;
+    LPE_HIP(ctx, hipMemsetAsync(d->sBCount, 0, sizeof(int32_t) * nb, s));
+    LPE_HIP(ctx, hipMemsetAsync(d->sPrevA, 0xFF, sizeof(int32_t) * kcap, s));
+    LPE_HIP(ctx, hipMemsetAsync(d->sPrevB, 0xFF, sizeof(int32_t) * kcap, s));
+    LPE_TIMED(ctx, "k_sched_count", hipLaunchKernelGGL(k_sched_count, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sItemA, d->sItemB, d->sBCount));
+    int st = rscan(ctx, d, nullptr, nb, d->sBCount, d->sBStart, d->sBCursor);
+    if (st) return st;
+    LPE_TIMED(ctx, "k_sched_fill", hipLaunchKernelGGL(k_sched_fill, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sItemA, d->sItemB, d->sBCursor, d->sEnt));
+    LPE_TIMED(ctx, "k_sched_link", hipLaunchKernelGGL(k_sched_link, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->sBStart, d->sEnt, d->sItemA, d->sPrevA, d->sPrevB));
+    LPE_TIMED(ctx, "k_sched_levels", hipLaunchKernelGGL(k_sched_levels, dim3(1), dim3(SOLVE_TPB), 0, s, kptr, d->sPrevA, d->sPrevB, d->sLevel, nlev));
+    LPE_HIP(ctx, hipMemsetAsync(d->sLCount, 0, sizeof(int32_t) * (kcap + 1), s));
+    LPE_TIMED(ctx, "k_level_count", hipLaunchKernelGGL(k_level_count, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sLevel, d->sLCount));
+    st = rscan(ctx, d, nlev, kcap + 1, d->sLCount, d->sLStart, d->sLCursor);
+    if (st) return st;
+    LPE_TIMED(ctx, "k_level_fill", hipLaunchKernelGGL(k_level_fill, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sLevel, d->sLCursor, d->sLOrder));
+    LPE_CHECK_LAUNCH(ctx, "schedule");
+    return LPE_OK;
+}
+
+// broadphase (canonical) or upload of caller pairs, then narrowphase; syncs
+// once to size the contact list
+static int rigid_detect(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pairs_in) {
+    hipStream_t s = ctx->stream;
+    const lpe_rigid_config &c = d->cfg;
+    int nb = d->nb;
+    for (int attempt = 0; attempt < 4; attempt++) {
+        LPE_HIP(ctx, hipMemsetAsync(d->counts, 0, sizeof(int32_t) * 16, s));
+        if (pairs_in) {
+            if (np_in > d->cap_pairs) {
+                int st = rigid_alloc_pairs(ctx, d, np_in + 1024);
+                if (st) return st;
+            }
+            if (np_in > 0)
+                LPE_HIP(ctx, hipMemcpyAsync(d->pairs, pairs_in, sizeof(int32_t) * 2 * np_in, hipMemcpyHostToDevice, s));
+            LPE_HIP(ctx, hipMemcpyAsync(d->counts, &np_in, sizeof(int32_t), hipMemcpyHostToDevice, s));
+        } else {
+            double lo = -c.boundaryBuffer, hi = -c.boundaryBuffer + (c.universeSize + 2 * c.boundaryBuffer);
+            LPE_TIMED(ctx, "k_rb_prep", hipLaunchKernelGGL(k_rb_prep, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->verts, lo, hi, d->aabb, d->cand));
+            LPE_HIP(ctx, hipMemsetAsync(d->pcount, 0, sizeof(int32_t) * nb, s));
+            dim3 g(rblk(nb), rblk(nb));
+            LPE_TIMED(ctx, "k_bp_pairs", hipLaunchKernelGGL(k_bp_pairs, g, dim3(RTPB), 0, s, nb, 0, d->byRank, d->bodies, d->aabb, d->cand, c.smallParticleThreshold, d->pcount, d->pstart, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6));
+            int st = rscan(ctx, d, nullptr, nb, d->pcount, d->pstart, d->pcursor);
+            if (st) return st;
+            LPE_TIMED(ctx, "k_bp_pairs", hipLaunchKernelGGL(k_bp_pairs, g, dim3(RTPB), 0, s, nb, 1, d->byRank, d->bodies, d->aabb, d->cand, c.smallParticleThreshold, d->pcount, d->pstart, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6));
+            LPE_TIMED(ctx, "k_bp_sort", hipLaunchKernelGGL(k_bp_sort, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->pstart, d->pairs, d->pairRankB, d->cap_pairs));
+            LPE_HIP(ctx, hipMemcpyAsync(d->counts, d->pstart + nb, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+        }
+        LPE_TIMED(ctx, "k_narrow", hipLaunchKernelGGL(k_narrow, dim3(rblk(d->cap_pairs, 128)), dim3(128), 0, s, d->counts, d->pairs, d->bodies, d->verts, d->cslots, d->ccount));
+        int st = rscan(ctx, d, d->counts, d->cap_pairs, d->ccount, d->cstart, nullptr);
+        if (st) return st;
+        int32_t hc[8];
+        LPE_HIP(ctx, hipMemcpyAsync(hc, d->counts, sizeof(int32_t) * 8, hipMemcpyDeviceToHost, s));
+        int32_t ncv = 0;
+        LPE_HIP(ctx, hipStreamSynchronize(s));
+        int np = hc[0];
+        if (hc[6] || np > d->cap_pairs) {   // pair buffer overflow: grow and redo
+            st = rigid_alloc_pairs(ctx, d, std::max(2 * d->cap_pairs, np + 1024));
+            if (st) return st;
+            continue;
+        }
+        LPE_HIP(ctx, hipMemcpy(&ncv, d->cstart + np, sizeof(int32_t), hipMemcpyDeviceToHost));
+        if (ncv > d->cap_contacts) {
+            st = rigid_alloc_contacts(ctx, d, ncv + 4096);
+            if (st) return st;
+        }
+        LPE_HIP(ctx, hipMemcpyAsync(d->counts + 1, &ncv, sizeof(int32_t), hipMemcpyHostToDevice, s));
+        LPE_TIMED(ctx, "k_compact", hipLaunchKernelGGL(k_compact, dim3(rblk(d->cap_pairs)), dim3(RTPB), 0, s, d->counts, d->cslots, d->ccount, d->cstart, d->contacts, d->cap_contacts));
+        LPE_CHECK_LAUNCH(ctx, "detect");
+        d->last_np = np;
+        d->last_nc = ncv;
+        return LPE_OK;
+    }
+    ctx->err = "rigid pair buffer kept overflowing";
+    return LPE_ERR_OVERFLOW;
+}
+
+static int rigid_solve(lpe_ctx *ctx, RigidDev *d, const int32_t *pgs_order, lpe_rigid_stats *stats) {
+    hipStream_t s = ctx->stream;
+    const lpe_rigid_config &c = d->cfg;
+    int nb = d->nb, nc = d->last_nc;
+    if (nc == 0) return LPE_OK;    // early out (rigid_body_collision.cpp:35-37)
+    if ((size_t)nb * 3 * sizeof(double) > 160 * 1024) {
+        ctx->err = "rigid solver: too many bodies for the LDS-resident solve (max 6826)";
+        return LPE_ERR_CAPACITY;
+    }
+    if (pgs_order)
+        LPE_HIP(ctx, hipMemcpyAsync(d->order, pgs_order, sizeof(int32_t) * nc, hipMemcpyHostToDevice, s));
+    // ---- PGS
+    LPE_HIP(ctx, hipMemsetAsync(d->inContact, 0, sizeof(int32_t) * 2 * nb, s));
+    LPE_TIMED(ctx, "k_mark_contacts", hipLaunchKernelGGL(k_mark_contacts, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->contacts, d->inContact));
+    LPE_TIMED(ctx, "k_pgs_bodies", hipLaunchKernelGGL(k_pgs_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->imii));
+    LPE_TIMED(ctx, "k_pgs_rows", hipLaunchKernelGGL(k_pgs_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, pgs_order ? d->order : (const int32_t *)nullptr, d->contacts, d->bodies, d->imii, d->rowN, d->rowR, d->rowAB, d->sItemA, d->sItemB));
+    int st = rigid_schedule(ctx, d, d->counts + 1, nc, d->counts + 2);
+    if (st) return st;
+    // lambdas live in sPrevA/sPrevB (reinterpreted) after scheduling
+    float *lamN = (float *)d->sPrevA, *lamF = (float *)d->sPrevB;
+    size_t lds = sizeof(float) * 3 * (size_t)nb;
+    LPE_TIMED(ctx, "k_pgs_solve", hipLaunchKernelGGL(k_pgs_solve, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts + 2, d->sLStart, d->sLOrder, d->rowN, d->rowR, d->rowAB, d->imii, d->vel0, c.pgsIterations, c.frictionCoeff, lamN, lamF, d->counts + 1));
+    LPE_TIMED(ctx, "k_pgs_writeback", hipLaunchKernelGGL(k_pgs_writeback, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->inContact));
+    LPE_CHECK_LAUNCH(ctx, "pgs");
+    // ---- position solver (narrowphase order)
+    int32_t *inPos = d->inContact + nb;
+    int32_t *keep = d->sLCount, *kstart = d->sLStart;   // reuse after PGS
+    LPE_TIMED(ctx, "k_pos_bodies", hipLaunchKernelGGL(k_pos_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->posState));
+    LPE_TIMED(ctx, "k_pos_items", hipLaunchKernelGGL(k_pos_items, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->contacts, d->bodies, d->posState, keep));
+    st = rscan(ctx, d, d->counts + 1, nc, keep, kstart, nullptr);
+    if (st) return st;
+    // kept-contact count -> counts[4]
+    LPE_HIP(ctx, hipMemcpyAsync(d->counts + 4, kstart + nc, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    LPE_TIMED(ctx, "k_pos_fill", hipLaunchKernelGGL(k_pos_fill, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, keep, kstart, d->contacts, d->posState, d->posItem, d->sItemA, d->sItemB, inPos));
+    st = rigid_schedule(ctx, d, d->counts + 4, nc, d->counts + 3);
+    if (st) return st;
+    size_t lds2 = sizeof(double) * 3 * (size_t)nb;
+    LPE_TIMED(ctx, "k_pos_solve", hipLaunchKernelGGL(k_pos_solve, dim3(1), dim3(SOLVE_TPB), lds2, s, nb, d->counts + 3, d->sLStart, d->sLOrder, d->posItem, d->contacts, d->posState, d->bodies, inPos, c.posIterations, c.baumgarte, c.slop));
+    LPE_CHECK_LAUNCH(ctx, "position solver");
+    if (stats) {
+        int32_t hc[8];
+        LPE_HIP(ctx, hipMemcpyAsync(hc, d->counts, sizeof(int32_t) * 8, hipMemcpyDeviceToHost, s));
+        LPE_HIP(ctx, hipStreamSynchronize(s));
+        stats->pgsLevels = hc[2];
+        stats->posLevels = hc[3];
+    }
+    return LPE_OK;
+}
+
+static int rigid_step_impl(lpe_ctx *ctx, int np, const int32_t *pairs, int nc_order,
+                           const int32_t *pgs_order, lpe_rigid_stats *stats) {
+    if (!ctx) return LPE_ERR_ARG;
+    RigidDev *d = rdev(ctx);
+    if (stats) std::memset(stats, 0, sizeof(*stats));
+    if (d->nb <= 0) return LPE_OK;
+    (void)hipSetDevice(ctx->device);
+    int st = rigid_detect(ctx, d, np, pairs);
+    if (st) return st;
+    if (pgs_order && nc_order != d->last_nc) {
+        ctx->err = "lpe_rigid_step_ordered: pgs_order length differs from the contact count";
+        return LPE_ERR_ARG;
+    }
+    if (stats) { stats->pairs = d->last_np; stats->contacts = d->last_nc; }
+    return rigid_solve(ctx, d, pgs_order, stats);
+}
+
+extern "C" int lpe_rigid_step(lpe_ctx *ctx, lpe_rigid_stats *stats) {
+    return rigid_step_impl(ctx, 0, nullptr, 0, nullptr, stats);
+}
+
+extern "C" int lpe_rigid_step_ordered(lpe_ctx *ctx, int np, const int32_t *pairs, int nc_order,
+                                      const int32_t *pgs_order, lpe_rigid_stats *stats) {
+    if (!ctx || np < 0 || (np > 0 && !pairs)) return LPE_ERR_ARG;
+    return rigid_step_impl(ctx, np, pairs ? pairs : (const int32_t *)"", nc_order, pgs_order, stats);
+}
+
+extern "C" int lpe_rigid_integrate(lpe_ctx *ctx, int systems, double dt_state, double dt_move) {
+    if (!ctx) return LPE_ERR_ARG;
+    RigidDev *d = rdev(ctx);
+    int nb = d->nb;
+    if (nb <= 0) return LPE_OK;
+    const lpe_rigid_config &c = d->cfg;
+    hipStream_t s = ctx->stream;
+    if (systems & 1)
+        LPE_TIMED(ctx, "k_boundary", hipLaunchKernelGGL(k_boundary, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.marginPixels * c.metersPerPixel, c.universeSize, c.bounceDamping, c.maxSpeed));
+    if (systems & 2) {
+        LPE_HIP(ctx, hipMemsetAsync(d->counts + 5, 0, sizeof(int32_t), s));
+        LPE_TIMED(ctx, "k_gravity_check", hipLaunchKernelGGL(k_gravity_check, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.planetaryMassThreshold, d->counts + 5));
+        LPE_TIMED(ctx, "k_gravity", hipLaunchKernelGGL(k_gravity, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.gravity, dt_state, d->counts + 5));
+    }
+    if (systems & 4)
+        LPE_TIMED(ctx, "k_rotation", hipLaunchKernelGGL(k_rotation, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, dt_state, c.angularDamping, c.maxAngularSpeed));
+    if (systems & 8)
+        LPE_TIMED(ctx, "k_movement", hipLaunchKernelGGL(k_movement, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, dt_move));
+    if (systems & 16)
+        LPE_TIMED(ctx, "k_sleep", hipLaunchKernelGGL(k_sleep, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.linearSleepThreshold, c.angularSleepThreshold, c.sleepFramesThreshold));
+    LPE_CHECK_LAUNCH(ctx, "integrate");
+    return LPE_OK;
+}
+
+extern "C" int lpe_rigid_download(lpe_ctx *ctx, lpe_body *bodies) {
+    if (!ctx || !bodies) return LPE_ERR_ARG;
+    RigidDev *d = rdev(ctx);
+    if (d->nb > 0)
+        LPE_HIP(ctx, hipMemcpyAsync(bodies, d->bodies, sizeof(lpe_body) * d->nb, hipMemcpyDeviceToHost, ctx->stream));
+    LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LPE_OK;
+}
+
+extern "C" int lpe_rigid_download_contacts(lpe_ctx *ctx, int pair_cap, int32_t *pairs,
+                                           int contact_cap, lpe_contact *contacts, int32_t *np,
+                                           int32_t *nc) {
+    if (!ctx) return LPE_ERR_ARG;
+    RigidDev *d = rdev(ctx);
+    hipStream_t s = ctx->stream;
+    if (np) *np = d->last_np;
+    if (nc) *nc = d->last_nc;
+    if (pairs && d->last_np > 0)
+        LPE_HIP(ctx, hipMemcpyAsync(pairs, d->pairs, sizeof(int2) * std::min(pair_cap, d->last_np), hipMemcpyDeviceToHost, s));
+    if (contacts && d->last_nc > 0)
+        LPE_HIP(ctx, hipMemcpyAsync(contacts, d->contacts, sizeof(lpe_contact) * std::min(contact_cap, d->last_nc), hipMemcpyDeviceToHost, s));
+    LPE_HIP(ctx, hipStreamSynchronize(s));
+    return LPE_OK;
+}

@@ -59,6 +59,14 @@ class FluidConfig(C.Structure):
                 ("numSubSteps", C.c_int), ("threadsPerGroup", C.c_int)]
 
 
+class RigidStats(C.Structure):
+    _fields_ = [("pairs", C.c_int32), ("contacts", C.c_int32), ("pgsLevels", C.c_int32),
+                ("posLevels", C.c_int32), ("overflow", C.c_int32), ("pad", C.c_int32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+
+
 class SphStats(C.Structure):
     _fields_ = [("maxCellOccupancy", C.c_int32), ("notInserted", C.c_int32),
                 ("capacityOverflow", C.c_int32), ("listOverflow", C.c_int32),
@@ -160,7 +168,19 @@ SIGNATURES = {
     "lpe_sph_get_stats": ([C.c_void_p, C.POINTER(SphStats)], C.c_int),
     "lpe_sph_probe_cells": ([C.c_void_p, _IP, C.POINTER(SphStats)], C.c_int),
     "lpe_sph_probe_density": ([C.c_void_p, _FP, _FP], C.c_int),
+    "lpe_rigid_config_default": ([C.POINTER(RigidConfig)], C.c_int),
+    "lpe_rigid_set_config": ([C.c_void_p, C.POINTER(RigidConfig)], C.c_int),
+    "lpe_rigid_upload": ([C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p], C.c_int),
+    "lpe_rigid_step": ([C.c_void_p, C.POINTER(RigidStats)], C.c_int),
+    "lpe_rigid_step_ordered": ([C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
+                                C.POINTER(RigidStats)], C.c_int),
+    "lpe_rigid_integrate": ([C.c_void_p, C.c_int, C.c_double, C.c_double], C.c_int),
+    "lpe_rigid_download": ([C.c_void_p, C.c_void_p], C.c_int),
+    "lpe_rigid_download_contacts": ([C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
+                                     _IP, _IP], C.c_int),
 }
+
+SYS_BOUNDARY, SYS_GRAVITY, SYS_ROTATION, SYS_MOVEMENT, SYS_SLEEP = 1, 2, 4, 8, 16
 
 
 def lib():
@@ -290,6 +310,54 @@ class Context:
         self._chk(lib().lpe_sph_probe_cells(self._h, cells.ctypes.data_as(_IP), C.byref(s)),
                   "lpe_sph_probe_cells")
         return cells, s.as_dict()
+
+    # ---- rigid ----------------------------------------------------------
+    def rigid_set_config(self, cfg: "RigidConfig"):
+        self._chk(lib().lpe_rigid_set_config(self._h, C.byref(cfg)), "lpe_rigid_set_config")
+
+    def rigid_upload(self, bodies, verts):
+        b = np.ascontiguousarray(bodies, dtype=BODY_DTYPE)
+        v = np.ascontiguousarray(verts, dtype=np.float64).reshape(-1)
+        self.nb = len(b)
+        self._rkeep = (b, v)
+        self._chk(lib().lpe_rigid_upload(self._h, len(b), b.ctypes.data, len(v) // 2, v.ctypes.data),
+                  "lpe_rigid_upload")
+
+    def rigid_step(self, pairs=None, pgs_order=None, stats=True):
+        st = RigidStats()
+        if pairs is None and pgs_order is None:
+            r = lib().lpe_rigid_step(self._h, C.byref(st) if stats else None)
+        else:
+            p = np.ascontiguousarray(pairs, np.int32).reshape(-1)
+            o = None if pgs_order is None else np.ascontiguousarray(pgs_order, np.int32)
+            r = lib().lpe_rigid_step_ordered(self._h, len(p) // 2, p.ctypes.data if len(p) else None,
+                                             0 if o is None else len(o),
+                                             None if o is None else o.ctypes.data,
+                                             C.byref(st) if stats else None)
+        self._chk(r, "lpe_rigid_step")
+        return st.as_dict()
+
+    def rigid_integrate(self, systems, dt_state, dt_move=None):
+        self._chk(lib().lpe_rigid_integrate(self._h, int(systems), float(dt_state),
+                                            float(dt_state if dt_move is None else dt_move)),
+                  "lpe_rigid_integrate")
+
+    def rigid_download(self):
+        b = np.zeros(self.nb, BODY_DTYPE)
+        self._chk(lib().lpe_rigid_download(self._h, b.ctypes.data), "lpe_rigid_download")
+        return b
+
+    def rigid_contacts(self):
+        np_ = C.c_int32(0)
+        nc = C.c_int32(0)
+        self._chk(lib().lpe_rigid_download_contacts(self._h, 0, None, 0, None, C.byref(np_),
+                                                    C.byref(nc)), "lpe_rigid_download_contacts")
+        pairs = np.zeros(2 * max(np_.value, 1), np.int32)
+        cs = np.zeros(max(nc.value, 1), CONTACT_DTYPE)
+        self._chk(lib().lpe_rigid_download_contacts(self._h, np_.value, pairs.ctypes.data, nc.value,
+                                                    cs.ctypes.data, C.byref(np_), C.byref(nc)),
+                  "lpe_rigid_download_contacts")
+        return pairs[:2 * np_.value].reshape(-1, 2), cs[:nc.value]
 
     def sph_probe_density(self):
         rho = np.empty(self.n, np.float32)
