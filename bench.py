@@ -22,6 +22,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "little-physics-engine_amd")
 
@@ -52,24 +54,30 @@ def kernel_bytes(name, n, cells):
 
 
 def cpu_baseline(scene_name, budget_s=20.0):
-    """The oracle (C restatement, 1 thread) ticking the same scene."""
+    """The oracle (C/C++ restatement of the reference algorithms, 1 thread)
+    running the same full tick on the same scene."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # noqa: E402  (checker / baseline only)
+    lpe = _load("lpe", os.path.join(PKG, "lpe.py"))
     scenes = _load("scenes", os.path.join(PKG, "scenes.py"))
     s = scenes.scene(scene_name)
     p = scenes.particles_aos(s["fluid"])
-    rig = scenes.gather_rigids(s["bodies"])
+    b, v = scenes.to_bodies(s["bodies"])
+    couple = np.arange(len(b) - 1, -1, -1, dtype=np.int32)
+    fcfg = lpe.default_fluid_config()
+    rcfg = lpe.rigid_config(universe=s["U"])
     ticks = 0
     t0 = time.perf_counter()
     while True:
-        p, rig, _, _ = oracle.fluid_tick(p, rig, 1.0 / 120.0)
+        p, b = oracle.world_tick(fcfg, rcfg, p, b, v, couple, 1.0 / 120.0, 1)
         ticks += 1
         el = time.perf_counter() - t0
         if el > budget_s or el / ticks * (ticks + 1) > budget_s * 1.5:
             break
     return dict(value=ticks / el, unit="ticks/s", cores=1, kind="port",
-                sample=f"{ticks} tick(s) of scene {scene_name} ({len(p)} SPH particles, "
-                       f"{len(rig)} rigids) through oracle/sph_oracle.c, 1 thread, -O2")
+                sample=f"{ticks} full tick(s) of scene {scene_name} ({len(p)} SPH particles, "
+                       f"{len(b)} bodies) through oracle/ (sph_oracle.c + rigid_oracle.cpp "
+                       f"lpeo_world_tick), 1 thread, -O2")
 
 
 def main():
@@ -94,29 +102,27 @@ def main():
     scenes = _load("scenes", os.path.join(PKG, "scenes.py"))
     s = scenes.scene(args.scene)
     fl = s["fluid"]
-    rig = scenes.gather_rigids(s["bodies"])
+    bodies, verts = scenes.to_bodies(s["bodies"])
     dt_tick = 1.0 / 120.0
 
     ctx = lpe.Context(local)
     ctx.sph_set_config(lpe.default_fluid_config())
+    ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+    ctx.rigid_upload(bodies, verts)
     ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
-    ctx.sph_upload_rigids(rig)
+    ctx.world_set_coupling(None)      # every body, reverse insertion (gatherRigidBodies view order)
 
-    for _ in range(args.warmup):
-        ctx.sph_step(dt_tick)
+    ctx.world_tick(dt_tick, args.warmup)
     ctx.sync()
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    ctx.timing(True)
-    ctx.timing_reset()
     barrier()
     ctx.sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ctx.sph_step(dt_tick)
+    ctx.world_tick(dt_tick, args.steps)
     ctx.sync()
     t1 = time.perf_counter()
     barrier()
@@ -126,17 +132,22 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    # per-kernel durations: HIP events on the library's stream over a second
+    # window of the same length (events between launches would add gaps to
+    # the timed window above; kernel durations are unaffected by them)
+    ctx.timing(True)
+    ctx.timing_reset()
+    ctx.world_tick(dt_tick, args.steps)
     times = ctx.timing_read()
     ctx.timing(False)
     stats = ctx.sph_stats()
-    out = ctx.sph_download()   # also checks the capacity flag
+    out = ctx.sph_download()   # also checks the capacity / overflow flags
 
     if rank != 0:
         if dist is not None:
             dist.barrier()
         return
 
-    import numpy as np
     assert np.isfinite(out["x"]).all() and np.isfinite(out["vy"]).all()
     n = len(fl["x"])
     cells = stats["gridDimX"] * stats["gridDimY"]
@@ -169,11 +180,14 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32 (SPH), f64+f32 (rigid: fp64 geometry, fp32 PGS as the reference)",
         "data": "synthetic (seeded scene generator, SURVEY.md §8(d))",
         "config": {"workload": s["desc"], "scene": args.scene, "fluid_particles": n,
-                   "rigid_bodies": len(rig), "substeps": 10, "dt": dt_tick,
-                   "systems": ["FluidSystem (SPH + rigid-fluid coupling)"],
+                   "rigid_bodies": len(bodies), "substeps": 10, "dt": dt_tick,
+                   "systems": ["FluidSystem (SPH + coupling)", "Boundary", "Gravity",
+                               "RigidBodyCollision (broadphase, GJK/EPA, PGS 10 it, position 10 it)",
+                               "Rotation", "Movement", "Sleep"],
+                   "mode": "resident (ECS sync skipped inside the timed region)",
                    "parallelism": f"replica x{world}"},
         "roofline": roof,
         "roofline_density": roof_d,

@@ -320,6 +320,32 @@ int  lpe_rigid_download(lpe_ctx *ctx, lpe_body *bodies);
 int  lpe_rigid_download_contacts(lpe_ctx *ctx, int pair_cap, int32_t *pairs, int contact_cap,
                                  lpe_contact *contacts, int32_t *np, int32_t *nc);
 
+/* ---- resident world tick (ECSSimulator::tick, src/sim.cpp:156-163) ------ */
+/* Time configuration of a tick: SharedSystemConfig::SecondsPerTick and
+ * ::TimeAcceleration (FluidSystem, MovementSystem) and the SimulatorState
+ * entity's baseTimeAcceleration * timeScale (Gravity, Rotation). */
+typedef struct lpe_world_config {
+    double secondsPerTick;
+    double timeAcceleration;
+    double baseTimeAcceleration;
+    double timeScale;
+} lpe_world_config;
+
+/* Coupling rigids of FluidSystem::gatherRigidBodies (fluid.cpp:304-438): the
+ * body indices (into the lpe_rigid_upload array) in the reference's view
+ * order.  nr < 0 selects every uploaded body in descending index order
+ * (reverse insertion, the EnTT view order for bodies uploaded in creation
+ * order). */
+int  lpe_world_set_coupling(lpe_ctx *ctx, int nr, const int32_t *body_index);
+/* nticks device-resident ticks of the reference system order: FluidSystem
+ * (rigid gather -> SPH sub-steps with coupling -> rigid velocity
+ * write-back), Boundary, Gravity (bodies and fluid), RigidBodyCollision,
+ * Rotation, Movement, Sleep (BarnesHut returns early: masses < 1e3,
+ * barnes_hut.cpp:54-70; the call fails with LPE_ERR_ARG otherwise).  Fluid
+ * state stays fp32 between ticks exactly as the ECS round trip of
+ * fluid.cpp:496-524 leaves it. */
+int  lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *cfg, int nticks);
+
 #ifdef __cplusplus
 }
 #endif

@@ -59,6 +59,10 @@ struct SphDev {
     int bx0 = 0, by0 = 0, bW = 0, bH = 0;
     float bcs = 0.25f;
     int rlist_len = 0;
+    int rlist_bound = 0;          // > 0: capacity bound of the bin list (no host sync)
+    int32_t *coupleBody = nullptr;// world mode: body index of each coupling rigid
+    int couple_n = 0, cap_couple = 0;
+    bool fluid_heavy = false;     // a fluid mass >= planetaryMassThreshold
     lpe_fluid_config cfg{};
     bool cfg_set = false;
     bool rig_dirty = true;

@@ -516,20 +516,24 @@ __global__ void k_rbin_count(int nr, const lpe_gpu_rigid *__restrict__ rig, floa
 }
 __global__ void k_rbin_fill(int nr, const lpe_gpu_rigid *__restrict__ rig, float bcs,
                             int bx0, int by0, int bW, int bH, int32_t *__restrict__ cursor,
-                            int32_t *__restrict__ list) {
+                            int32_t *__restrict__ list, int cap, int32_t *__restrict__ status) {
     int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nr) return;
     const lpe_gpu_rigid &b = rig[r];
     int x0 = bin_of(b.minX, bcs, bx0, bW), x1 = bin_of(b.maxX, bcs, bx0, bW);
     int y0 = bin_of(b.minY, bcs, by0, bH), y1 = bin_of(b.maxY, bcs, by0, bH);
     for (int yy = y0; yy <= y1; yy++)
-        for (int xx = x0; xx <= x1; xx++) list[atomicAdd(&cursor[yy * bW + xx], 1)] = r;
+        for (int xx = x0; xx <= x1; xx++) {
+            int slot = atomicAdd(&cursor[yy * bW + xx], 1);
+            if (slot < cap) list[slot] = r;
+            else atomicOr(&status[ST_LIST_OVERFLOW], 1);
+        }
 }
 // insertion sort of each bin's list -> ascending rigid index
-__global__ void k_rbin_sort(int B, const int32_t *__restrict__ start, int32_t *__restrict__ list) {
+__global__ void k_rbin_sort(int B, int32_t *__restrict__ start, int32_t *__restrict__ list, int cap) {
     int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
-    int s = start[b], e = start[b + 1];
+    int s = min(start[b], cap), e = min(start[b + 1], cap);
     for (int k = s + 1; k < e; k++) {
         int v = list[k];
         int j = k - 1;
@@ -602,7 +606,7 @@ static void sph_free(SphDev &d) {
     pstate_free(d.S);
     void *ptrs[] = {d.rho, d.pr, d.key, d.tmpId, d.tmpOld, d.count, d.start, d.cursor,
                     d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.accum, d.rbinStart,
-                    d.rbinList, d.rbinCount};
+                    d.rbinList, d.rbinCount, d.coupleBody};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     d = SphDev();
 }
@@ -907,10 +911,12 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
     int32_t *cursor = d.rbinCount + B;
     int st = sph_scan(ctx, B, d.rbinCount, d.rbinStart, cursor, d.rbinCount + 2 * B, 0, false);
     if (st) return st;
-    // the list length is needed on the host once per rigid upload
-    int total = 0;
-    LPE_HIP(ctx, hipMemcpyAsync(&total, d.rbinStart + B, sizeof(int), hipMemcpyDeviceToHost, s));
-    LPE_HIP(ctx, hipStreamSynchronize(s));
+    // list length: a host-known bound (world mode, no sync) or read back once
+    int total = d.rlist_bound;
+    if (total <= 0) {
+        LPE_HIP(ctx, hipMemcpyAsync(&total, d.rbinStart + B, sizeof(int), hipMemcpyDeviceToHost, s));
+        LPE_HIP(ctx, hipStreamSynchronize(s));
+    }
     if (total > d.cap_rlist || !d.rbinList) {
         if (d.rbinList) (void)hipFree(d.rbinList);
         LPE_HIP(ctx, hipMalloc((void **)&d.rbinList, sizeof(int32_t) * std::max(total, 1)));
@@ -918,8 +924,8 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
     }
     d.rlist_len = total;
     LPE_TIMED(ctx, "k_rbin_fill", hipLaunchKernelGGL(k_rbin_fill, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig, d.bcs,
-                       d.bx0, d.by0, d.bW, d.bH, cursor, d.rbinList));
-    LPE_TIMED(ctx, "k_rbin_sort", hipLaunchKernelGGL(k_rbin_sort, dim3(nblk(B, 128)), dim3(128), 0, s, B, d.rbinStart, d.rbinList));
+                       d.bx0, d.by0, d.bW, d.bH, cursor, d.rbinList, d.cap_rlist, d.status));
+    LPE_TIMED(ctx, "k_rbin_sort", hipLaunchKernelGGL(k_rbin_sort, dim3(nblk(B, 128)), dim3(128), 0, s, B, d.rbinStart, d.rbinList, d.cap_rlist));
     LPE_CHECK_LAUNCH(ctx, "rbin");
     d.rig_dirty = false;
     return LPE_OK;
@@ -1024,6 +1030,10 @@ static int check_status(lpe_ctx *ctx) {
     if (status[ST_CAP_OVERFLOW]) {
         ctx->err = "a fluid particle left the device grid capacity";
         return LPE_ERR_CAPACITY;
+    }
+    if (status[ST_LIST_OVERFLOW]) {
+        ctx->err = "the rigid coupling bin list overflowed its capacity bound";
+        return LPE_ERR_OVERFLOW;
     }
     return LPE_OK;
 }

@@ -1,0 +1,61 @@
+// rigid_dev.h — device state of the rigid path (shared by lpe_rigid.hip and
+// lpe_world.hip).  Not part of the ABI.
+#pragma once
+#include "lpe_internal.h"
+
+namespace lpe {
+
+static constexpr int RTPB = 256;
+static constexpr int MAXC = 36;        // contacts per pair slot (poly-poly <= nB + 3)
+static constexpr int EPA_MAX = 104;    // EPA polygon: 3 + 100 insertions + 1
+static constexpr int CLIP_MAX = 40;    // clip output <= nB + 3
+static constexpr int MAXV = 32;        // polygon vertex cap of the device narrowphase
+static constexpr int SOLVE_TPB = 1024;
+
+struct RigidDev {
+    int nb = 0, cap_nb = 0;
+    lpe_body *bodies = nullptr;
+    double *verts = nullptr;
+    int nverts = 0, cap_verts = 0;
+    int32_t *rank = nullptr, *byRank = nullptr;
+    double4 *aabb = nullptr;
+    int32_t *cand = nullptr;
+    // pairs
+    int32_t *pcount = nullptr, *pstart = nullptr, *pcursor = nullptr;
+    int2 *pairs = nullptr;
+    int32_t *pairRankB = nullptr;
+    int cap_pairs = 0;
+    // contacts
+    lpe_contact *cslots = nullptr;
+    int32_t *ccount = nullptr, *cstart = nullptr;
+    lpe_contact *contacts = nullptr;
+    int cap_contacts = 0;
+    // scan partials
+    int32_t *bsum = nullptr;
+    int cap_bsum = 0;
+    // PGS / position solver
+    int32_t *order = nullptr;                 // PGS visiting order (contact indices)
+    float4 *rowN = nullptr;                   // dirX, dirY, effN, effF
+    float4 *rowR = nullptr;                   // rxA, ryA, rxB, ryB
+    int2 *rowAB = nullptr;                    // body indices (-1 = static)
+    float *vel0 = nullptr;                    // float3 per body (PGS load)
+    float *imii = nullptr;                    // float2 per body (invMass, invInertia)
+    int32_t *inContact = nullptr;             // per body flags
+    double *posState = nullptr;               // per body: invM, invI (pos solver)
+    int2 *posAB = nullptr;
+    int32_t *posItem = nullptr;               // kept contact index per pos item
+    // scheduling (shared by both solvers)
+    int32_t *sItemA = nullptr, *sItemB = nullptr, *sPrevA = nullptr, *sPrevB = nullptr;
+    int32_t *sLevel = nullptr, *sBCount = nullptr, *sBStart = nullptr, *sBCursor = nullptr;
+    int32_t *sEnt = nullptr, *sSorted = nullptr, *sLCount = nullptr, *sLStart = nullptr,
+            *sLCursor = nullptr, *sLOrder = nullptr;
+    int32_t *counts = nullptr;                // [0]=np [1]=nc [2]=pgs levels [3]=pos levels [4]=npos [5]=heavy
+    lpe_rigid_config cfg{};
+    bool cfg_set = false;
+    int last_np = 0, last_nc = 0;
+};
+
+
+RigidDev *rigid_dev(lpe_ctx *ctx);
+
+}  // namespace lpe

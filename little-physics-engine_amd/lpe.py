@@ -180,6 +180,14 @@ SIGNATURES = {
                                      _IP, _IP], C.c_int),
 }
 
+class WorldConfig(C.Structure):
+    _fields_ = [("secondsPerTick", C.c_double), ("timeAcceleration", C.c_double),
+                ("baseTimeAcceleration", C.c_double), ("timeScale", C.c_double)]
+
+
+SIGNATURES["lpe_world_set_coupling"] = ([C.c_void_p, C.c_int, C.c_void_p], C.c_int)
+SIGNATURES["lpe_world_tick"] = ([C.c_void_p, C.POINTER(WorldConfig), C.c_int], C.c_int)
+
 SYS_BOUNDARY, SYS_GRAVITY, SYS_ROTATION, SYS_MOVEMENT, SYS_SLEEP = 1, 2, 4, 8, 16
 
 
@@ -358,6 +366,20 @@ class Context:
                                                     cs.ctypes.data, C.byref(np_), C.byref(nc)),
                   "lpe_rigid_download_contacts")
         return pairs[:2 * np_.value].reshape(-1, 2), cs[:nc.value]
+
+    # ---- world (resident full tick) -------------------------------------
+    def world_set_coupling(self, body_index=None):
+        if body_index is None:
+            self._chk(lib().lpe_world_set_coupling(self._h, -1, None), "lpe_world_set_coupling")
+        else:
+            idx = np.ascontiguousarray(body_index, np.int32)
+            self._ckeep = idx
+            self._chk(lib().lpe_world_set_coupling(self._h, len(idx), idx.ctypes.data),
+                      "lpe_world_set_coupling")
+
+    def world_tick(self, dt=1.0 / 120.0, nticks=1, time_accel=1.0, bta=1.0, ts=1.0):
+        wc = WorldConfig(dt, time_accel, bta, ts)
+        self._chk(lib().lpe_world_tick(self._h, C.byref(wc), int(nticks)), "lpe_world_tick")
 
     def sph_probe_density(self):
         rho = np.empty(self.n, np.float32)

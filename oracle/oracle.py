@@ -261,3 +261,20 @@ def ref_rigid_ticks(cfg, bodies, verts, nticks, dt):
     return dict(final=b, before_rigid=before, after_pgs=apgs, after_pos=apos,
                 pairs=pairs[:2 * npairs.value].reshape(-1, 2).copy(),
                 contacts=cs[:nc.value].copy(), pgs_order=order[:nc.value].copy())
+
+
+def world_tick(fcfg, rcfg, particles, bodies, verts, couple, dt, nticks=1):
+    """lpeo_world_tick: full ticks with fluid + bodies (canonical orders)."""
+    L = _rigid_lib()
+    f = L.lpeo_world_tick
+    f.argtypes = [C.POINTER(lpe.FluidConfig), C.POINTER(lpe.RigidConfig), C.c_double, C.c_double,
+                  C.c_double, C.c_double, C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
+                  C.c_int, C.c_void_p]
+    p = _aos(particles).copy()
+    b = _bodies(bodies)
+    v = np.ascontiguousarray(verts, np.float64)
+    c = np.ascontiguousarray(couple, np.int32)
+    for _ in range(nticks):
+        f(C.byref(fcfg), C.byref(rcfg), float(dt), 1.0, 1.0, 1.0, p.ctypes.data, p.shape[0],
+          b.ctypes.data, len(b), v.ctypes.data, len(c), c.ctypes.data)
+    return p, b

@@ -773,3 +773,105 @@ extern "C" int lpeo_rigid_tick(const lpe_rigid_config *cfg, int nb, lpe_body *bo
     lpeo_sleep(cfg, nb, bodies);
     return nc;
 }
+
+/* ---- the whole tick (ECSSimulator::tick, src/sim.cpp:156-163) ----------- */
+#include "sph_oracle.h"
+
+/* gatherRigidBodies (fluid.cpp:304-438) from a body */
+static lpe_gpu_rigid gather_rigid(const lpe_body &b, const double *verts) {
+    lpe_gpu_rigid rb;
+    std::memset(&rb, 0, sizeof(rb));
+    rb.posX = (float)b.x;
+    rb.posY = (float)b.y;
+    rb.angle = (b.flags & LPE_BODY_HAS_ANGPOS) ? (float)b.angle : 0.0f;
+    if (b.flags & LPE_BODY_HAS_VEL) { rb.vx = (float)b.vx; rb.vy = (float)b.vy; }
+    if (b.flags & LPE_BODY_HAS_ANGVEL) rb.omega = (float)b.omega;
+    rb.mass = (b.flags & LPE_BODY_HAS_MASS) ? (float)b.mass : 1.f;
+    rb.inertia = (b.flags & LPE_BODY_HAS_INERTIA) ? (float)b.inertia : 1.f;
+    rb.minX = rb.posX - 0.5f; rb.maxX = rb.posX + 0.5f;
+    rb.minY = rb.posY - 0.5f; rb.maxY = rb.posY + 0.5f;
+    if (b.flags & LPE_BODY_CIRCLE) {
+        rb.shapeType = 0;
+        rb.radius = (float)b.radius;
+        rb.minX = rb.posX - rb.radius; rb.maxX = rb.posX + rb.radius;
+        rb.minY = rb.posY - rb.radius; rb.maxY = rb.posY + rb.radius;
+    } else {
+        rb.shapeType = 1;
+        int cnt = std::min(b.vert_cnt, (int)LPE_MAX_POLY_VERTS);
+        rb.vertCount = cnt;
+        double c = std::cos((double)rb.angle), s = std::sin((double)rb.angle);
+        float mnx = FLT_MAX, mxx = -FLT_MAX, mny = FLT_MAX, mxy = -FLT_MAX;
+        const double *lv = verts + 2 * (size_t)b.vert_off;
+        for (int i = 0; i < cnt; i++) {
+            double wx = b.x + (lv[2 * i] * c - lv[2 * i + 1] * s);
+            double wy = b.y + (lv[2 * i] * s + lv[2 * i + 1] * c);
+            rb.vertsX[i] = (float)wx;
+            rb.vertsY[i] = (float)wy;
+            if (wx < mnx) mnx = (float)wx;
+            if (wx > mxx) mxx = (float)wx;
+            if (wy < mny) mny = (float)wy;
+            if (wy > mxy) mxy = (float)wy;
+        }
+        rb.minX = mnx; rb.maxX = mxx; rb.minY = mny; rb.maxY = mxy;
+    }
+    return rb;
+}
+
+extern "C" int lpeo_world_tick(const lpe_fluid_config *fcfg, const lpe_rigid_config *rcfg,
+                               double spt, double time_accel, double bta, double ts,
+                               lpeo_particle *parts, int n, lpe_body *bodies, int nb,
+                               const double *verts, int nr, const int32_t *couple) {
+    const double dt_fluid = spt * time_accel, dt_move = spt * time_accel, dt_state = spt * bta * ts;
+    /* 1) FluidSystem::update */
+    if (n > 0) {
+        std::vector<lpe_gpu_rigid> rig(std::max(nr, 1));
+        for (int r = 0; r < nr; r++) rig[r] = gather_rigid(bodies[couple[r]], verts);
+        lpeo_fluid_tick(fcfg, dt_fluid, parts, n, rig.data(), nr, nullptr, nullptr);
+        for (int r = 0; r < nr; r++) {                       /* fluid.cpp:564-579 */
+            lpe_body &b = bodies[couple[r]];
+            if (b.flags & LPE_BODY_HAS_VEL) { b.vx = rig[r].vx; b.vy = rig[r].vy; }
+            if (b.flags & LPE_BODY_HAS_ANGVEL) b.omega = rig[r].omega;
+        }
+    }
+    /* 2) Boundary, 3) Gravity: bodies, and fluid through the double ECS */
+    lpeo_boundary(rcfg, nb, bodies);
+    bool heavy = false;
+    for (int i = 0; i < nb; i++) {
+        const lpe_body &b = bodies[i];
+        if ((b.flags & LPE_BODY_HAS_PHASE) && (b.flags & LPE_BODY_HAS_VEL) && (b.flags & LPE_BODY_HAS_MASS) &&
+            !(b.flags & LPE_BODY_BOUNDARY) && rcfg->planetaryMassThreshold > 0.0 &&
+            b.mass >= rcfg->planetaryMassThreshold)
+            heavy = true;
+    }
+    for (int i = 0; i < n && rcfg->planetaryMassThreshold > 0.0; i++)
+        if (parts[i].mass >= rcfg->planetaryMassThreshold) heavy = true;
+    const double m = rcfg->marginPixels * rcfg->metersPerPixel, U = rcfg->universeSize;
+    for (int i = 0; i < n; i++) {
+        lpeo_particle &p = parts[i];
+        double x = p.x, y = p.y, vx = p.vx, vy = p.vy;
+        bool bounced = false;
+        if (x < m) { x = m; vx = std::abs(vx) * rcfg->bounceDamping; bounced = true; }
+        else if (x > U - m) { x = U - m; vx = -std::abs(vx) * rcfg->bounceDamping; bounced = true; }
+        if (y < m) { y = m; vy = std::abs(vy) * rcfg->bounceDamping; bounced = true; }
+        else if (y > U - m) { y = U - m; vy = -std::abs(vy) * rcfg->bounceDamping; bounced = true; }
+        if (bounced) {
+            double sp = std::sqrt(vx * vx + vy * vy);
+            if (sp > rcfg->maxSpeed) { vx = (vx / sp) * rcfg->maxSpeed; vy = (vy / sp) * rcfg->maxSpeed; }
+        }
+        if (!heavy) vy += rcfg->gravity * dt_state;
+        p.x = (float)x; p.y = (float)y; p.vx = (float)vx; p.vy = (float)vy;
+    }
+    if (!heavy)
+        for (int i = 0; i < nb; i++) {
+            lpe_body &b = bodies[i];
+            if ((b.flags & LPE_BODY_HAS_PHASE) && (b.flags & LPE_BODY_HAS_VEL) &&
+                (b.flags & LPE_BODY_HAS_MASS) && !(b.flags & LPE_BODY_BOUNDARY))
+                b.vy += rcfg->gravity * dt_state;
+        }
+    /* 4) RigidBodyCollisionSystem, 6) Rotation, 7) Movement, 8) Sleep */
+    lpeo_rigid_update(rcfg, nb, bodies, verts, nullptr);
+    lpeo_rotation(rcfg, nb, bodies, dt_state);
+    lpeo_movement(nb, bodies, dt_move);
+    lpeo_sleep(rcfg, nb, bodies);
+    return 0;
+}

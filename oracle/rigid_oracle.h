@@ -57,6 +57,16 @@ void lpeo_sleep(const lpe_rigid_config *cfg, int nb, lpe_body *bodies);
 int lpeo_rigid_tick(const lpe_rigid_config *cfg, int nb, lpe_body *bodies, const double *verts,
                     double dt_state, double dt_move, lpeo_rigid_stats *stats);
 
+/* One full tick with fluid: FluidSystem (gather of the `couple` bodies ->
+ * SPH -> velocity write-back), Boundary, Gravity (bodies and fluid),
+ * RigidBodyCollision, Rotation, Movement, Sleep.  parts: fluid in gather
+ * order (sph_oracle.h).  The canonical orders of both oracles apply. */
+struct lpeo_particle;
+int lpeo_world_tick(const lpe_fluid_config *fcfg, const lpe_rigid_config *rcfg,
+                    double spt, double time_accel, double bta, double ts,
+                    struct lpeo_particle *parts, int n, lpe_body *bodies, int nb,
+                    const double *verts, int nr, const int32_t *couple);
+
 #ifdef __cplusplus
 }
 #endif
