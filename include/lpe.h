@@ -217,8 +217,10 @@ int  lpe_device_count(int *count);
 int  lpe_sync(lpe_ctx *ctx);
 
 /* ---- kernel timing (bench / profiling; no reference counterpart) ------- */
-/* When enabled, every launch of a named kernel on the context's stream is
- * bracketed by a pair of HIP events.  lpe_timing_read() waits for the stream,
+/* on = 1: every launch of a named kernel on the context's stream is
+ * bracketed by a pair of HIP events; on = 2: only the dominant kernels
+ * (k_density, k_forces_couple, k_pgs_solve, k_pos_solve, k_narrow,
+ * k_bp_pairs), so the host stays ahead of the device; on = 0: off.  lpe_timing_read() waits for the stream,
  * accumulates the event durations and returns, for the i-th kernel name seen,
  * its name, total milliseconds and launch count (returns LPE_ERR_ARG when i is
  * past the last name).  lpe_timing_reset() clears the totals. */

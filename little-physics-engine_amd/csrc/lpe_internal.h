@@ -1,6 +1,7 @@
 // lpe_internal.h — shared internals of the HIP backend (not part of the ABI).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <cstdint>
 #include <cstdio>
 #include <string>
@@ -33,6 +34,10 @@ struct SphDev {
     PState P;                     // primary state (sorted order of the last sub-step)
     PState S;                     // permutation target of the current sub-step
     float *rho = nullptr, *pr = nullptr;  // in S/P slot order
+    float4 *nbA = nullptr;        // sorted neighbour records (x, y, m, -)
+    float4 *nbB = nullptr;        // (vx, vy, rho, p / rho^2)
+    int16_t *nlist = nullptr;     // per-slot neighbour list k - s, column-major [cap][n]
+    int32_t *ncount = nullptr;    // neighbours found (> cap: forces walks the bins)
     // counting-sort grid hash over (2h cell, h quadrant) bins
     uint32_t *key = nullptr;      // bin of each P slot
     int32_t *tmpId = nullptr;     // scatter output: particle id per new slot
@@ -84,7 +89,8 @@ namespace lpe {
 // it for the live roofline numbers).  Event pairs are recorded around each
 // launch of a named kernel and resolved at lpe_timing_read().
 struct KernelTimer {
-    bool on = false;
+    int on = 0;                   // 0 off, 1 every kernel, 2 the hot kernels only
+    bool wants(const char *name) const;
     std::vector<std::string> names;
     std::vector<std::vector<std::pair<hipEvent_t, hipEvent_t>>> pending;
     std::vector<double> total_ms;
@@ -105,18 +111,21 @@ struct lpe_ctx {
 };
 
 // Records a start event before and a stop event after `launch` when timing is on.
-#define LPE_TIMED(ctx, name, launch)                                             \
-    do {                                                                         \
-        if ((ctx)->timer.on) {                                                   \
-            int ts_ = (ctx)->timer.slot(name);                                   \
-            hipEvent_t e0_ = (ctx)->timer.get(), e1_ = (ctx)->timer.get();       \
-            (void)hipEventRecord(e0_, (ctx)->stream);                            \
-            launch;                                                              \
-            (void)hipEventRecord(e1_, (ctx)->stream);                            \
-            (ctx)->timer.pending[ts_].push_back({e0_, e1_});                     \
-        } else {                                                                 \
-            launch;                                                              \
-        }                                                                        \
+// Launch a kernel on the context stream; with timing on, the launch carries
+// start/stop events that the runtime stamps at the dispatch's own begin and
+// end (hipExtLaunchKernelGGL), i.e. the kernel's execution time, not the gap
+// between two markers on the stream.
+#define LPE_KERNEL(ctx, name, kernel, grid, block, shmem, stream, ...)                   \
+    do {                                                                                 \
+        if ((ctx)->timer.on && (ctx)->timer.wants(name)) {                               \
+            int ts_ = (ctx)->timer.slot(name);                                           \
+            hipEvent_t e0_ = (ctx)->timer.get(), e1_ = (ctx)->timer.get();               \
+            hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, e0_, e1_, 0,       \
+                                  __VA_ARGS__);                                          \
+            (ctx)->timer.pending[ts_].push_back({e0_, e1_});                             \
+        } else {                                                                         \
+            hipLaunchKernelGGL(kernel, grid, block, shmem, stream, __VA_ARGS__);         \
+        }                                                                                \
     } while (0)
 
 #define LPE_HIP(ctx, call)                                                       \
@@ -148,4 +157,5 @@ static inline int lpe_grow(lpe_ctx *ctx, T **p, int *cap, long want, long elems_
 }
 
 int lpe_rigid_destroy_internal(lpe_ctx *ctx);
+int lpe_sph_cover_box(lpe_ctx *ctx, double x0, double y0, double x1, double y1);
 int lpe_timer_destroy_internal(lpe_ctx *ctx);

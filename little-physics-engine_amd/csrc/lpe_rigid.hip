@@ -1028,9 +1028,9 @@ static int rscan(lpe_ctx *ctx, RigidDev *d, const int32_t *nptr, int ncap, const
     if (st) return st;
     int nb = ncap / 1024 + 1;
     hipStream_t s = ctx->stream;
-    LPE_TIMED(ctx, "k_rscan_reduce", hipLaunchKernelGGL(k_rscan_reduce, dim3(nb), dim3(RTPB), 0, s, nptr, ncap, cnt, d->bsum));
-    LPE_TIMED(ctx, "k_rscan_blocks", hipLaunchKernelGGL(k_rscan_blocks, dim3(1), dim3(RTPB), 0, s, nptr, ncap, d->bsum, start));
-    LPE_TIMED(ctx, "k_rscan_final", hipLaunchKernelGGL(k_rscan_final, dim3(nb), dim3(RTPB), 0, s, nptr, ncap, cnt, d->bsum, start, cursor));
+    LPE_KERNEL(ctx, "k_rscan_reduce", k_rscan_reduce, dim3(nb), dim3(RTPB), 0, s, nptr, ncap, cnt, d->bsum);
+    LPE_KERNEL(ctx, "k_rscan_blocks", k_rscan_blocks, dim3(1), dim3(RTPB), 0, s, nptr, ncap, d->bsum, start);
+    LPE_KERNEL(ctx, "k_rscan_final", k_rscan_final, dim3(nb), dim3(RTPB), 0, s, nptr, ncap, cnt, d->bsum, start, cursor);
     LPE_CHECK_LAUNCH(ctx, "rscan");
     return LPE_OK;
 }
@@ -1096,17 +1096,17 @@ static int rigid_schedule(lpe_ctx *ctx, RigidDev *d, const int32_t *kptr, int kc
     LPE_HIP(ctx, hipMemsetAsync(d->sBCount, 0, sizeof(int32_t) * nb, s));
     LPE_HIP(ctx, hipMemsetAsync(d->sPrevA, 0xFF, sizeof(int32_t) * kcap, s));
     LPE_HIP(ctx, hipMemsetAsync(d->sPrevB, 0xFF, sizeof(int32_t) * kcap, s));
-    LPE_TIMED(ctx, "k_sched_count", hipLaunchKernelGGL(k_sched_count, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sItemA, d->sItemB, d->sBCount));
+    LPE_KERNEL(ctx, "k_sched_count", k_sched_count, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sItemA, d->sItemB, d->sBCount);
     int st = rscan(ctx, d, nullptr, nb, d->sBCount, d->sBStart, d->sBCursor);
     if (st) return st;
-    LPE_TIMED(ctx, "k_sched_fill", hipLaunchKernelGGL(k_sched_fill, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sItemA, d->sItemB, d->sBCursor, d->sEnt));
-    LPE_TIMED(ctx, "k_sched_link", hipLaunchKernelGGL(k_sched_link, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->sBStart, d->sEnt, d->sItemA, d->sPrevA, d->sPrevB));
-    LPE_TIMED(ctx, "k_sched_levels", hipLaunchKernelGGL(k_sched_levels, dim3(1), dim3(SOLVE_TPB), 0, s, kptr, d->sPrevA, d->sPrevB, d->sLevel, nlev));
+    LPE_KERNEL(ctx, "k_sched_fill", k_sched_fill, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sItemA, d->sItemB, d->sBCursor, d->sEnt);
+    LPE_KERNEL(ctx, "k_sched_link", k_sched_link, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->sBStart, d->sEnt, d->sItemA, d->sPrevA, d->sPrevB);
+    LPE_KERNEL(ctx, "k_sched_levels", k_sched_levels, dim3(1), dim3(SOLVE_TPB), 0, s, kptr, d->sPrevA, d->sPrevB, d->sLevel, nlev);
     LPE_HIP(ctx, hipMemsetAsync(d->sLCount, 0, sizeof(int32_t) * (kcap + 1), s));
-    LPE_TIMED(ctx, "k_level_count", hipLaunchKernelGGL(k_level_count, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sLevel, d->sLCount));
+    LPE_KERNEL(ctx, "k_level_count", k_level_count, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sLevel, d->sLCount);
     st = rscan(ctx, d, nlev, kcap + 1, d->sLCount, d->sLStart, d->sLCursor);
     if (st) return st;
-    LPE_TIMED(ctx, "k_level_fill", hipLaunchKernelGGL(k_level_fill, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sLevel, d->sLCursor, d->sLOrder));
+    LPE_KERNEL(ctx, "k_level_fill", k_level_fill, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sLevel, d->sLCursor, d->sLOrder);
     LPE_CHECK_LAUNCH(ctx, "schedule");
     return LPE_OK;
 }
@@ -1129,17 +1129,17 @@ static int rigid_detect(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pai
             LPE_HIP(ctx, hipMemcpyAsync(d->counts, &np_in, sizeof(int32_t), hipMemcpyHostToDevice, s));
         } else {
             double lo = -c.boundaryBuffer, hi = -c.boundaryBuffer + (c.universeSize + 2 * c.boundaryBuffer);
-            LPE_TIMED(ctx, "k_rb_prep", hipLaunchKernelGGL(k_rb_prep, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->verts, lo, hi, d->aabb, d->cand));
+            LPE_KERNEL(ctx, "k_rb_prep", k_rb_prep, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->verts, lo, hi, d->aabb, d->cand);
             LPE_HIP(ctx, hipMemsetAsync(d->pcount, 0, sizeof(int32_t) * nb, s));
             dim3 g(rblk(nb), rblk(nb));
-            LPE_TIMED(ctx, "k_bp_pairs", hipLaunchKernelGGL(k_bp_pairs, g, dim3(RTPB), 0, s, nb, 0, d->byRank, d->bodies, d->aabb, d->cand, c.smallParticleThreshold, d->pcount, d->pstart, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6));
+            LPE_KERNEL(ctx, "k_bp_pairs", k_bp_pairs, g, dim3(RTPB), 0, s, nb, 0, d->byRank, d->bodies, d->aabb, d->cand, c.smallParticleThreshold, d->pcount, d->pstart, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6);
             int st = rscan(ctx, d, nullptr, nb, d->pcount, d->pstart, d->pcursor);
             if (st) return st;
-            LPE_TIMED(ctx, "k_bp_pairs", hipLaunchKernelGGL(k_bp_pairs, g, dim3(RTPB), 0, s, nb, 1, d->byRank, d->bodies, d->aabb, d->cand, c.smallParticleThreshold, d->pcount, d->pstart, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6));
-            LPE_TIMED(ctx, "k_bp_sort", hipLaunchKernelGGL(k_bp_sort, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->pstart, d->pairs, d->pairRankB, d->cap_pairs));
+            LPE_KERNEL(ctx, "k_bp_pairs", k_bp_pairs, g, dim3(RTPB), 0, s, nb, 1, d->byRank, d->bodies, d->aabb, d->cand, c.smallParticleThreshold, d->pcount, d->pstart, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6);
+            LPE_KERNEL(ctx, "k_bp_sort", k_bp_sort, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->pstart, d->pairs, d->pairRankB, d->cap_pairs);
             LPE_HIP(ctx, hipMemcpyAsync(d->counts, d->pstart + nb, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
         }
-        LPE_TIMED(ctx, "k_narrow", hipLaunchKernelGGL(k_narrow, dim3(rblk(d->cap_pairs, 128)), dim3(128), 0, s, d->counts, d->pairs, d->bodies, d->verts, d->cslots, d->ccount));
+        LPE_KERNEL(ctx, "k_narrow", k_narrow, dim3(rblk(d->cap_pairs, 128)), dim3(128), 0, s, d->counts, d->pairs, d->bodies, d->verts, d->cslots, d->ccount);
         int st = rscan(ctx, d, d->counts, d->cap_pairs, d->ccount, d->cstart, nullptr);
         if (st) return st;
         int32_t hc[8];
@@ -1158,7 +1158,7 @@ static int rigid_detect(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pai
             if (st) return st;
         }
         LPE_HIP(ctx, hipMemcpyAsync(d->counts + 1, &ncv, sizeof(int32_t), hipMemcpyHostToDevice, s));
-        LPE_TIMED(ctx, "k_compact", hipLaunchKernelGGL(k_compact, dim3(rblk(d->cap_pairs)), dim3(RTPB), 0, s, d->counts, d->cslots, d->ccount, d->cstart, d->contacts, d->cap_contacts));
+        LPE_KERNEL(ctx, "k_compact", k_compact, dim3(rblk(d->cap_pairs)), dim3(RTPB), 0, s, d->counts, d->cslots, d->ccount, d->cstart, d->contacts, d->cap_contacts);
         LPE_CHECK_LAUNCH(ctx, "detect");
         d->last_np = np;
         d->last_nc = ncv;
@@ -1181,31 +1181,31 @@ static int rigid_solve(lpe_ctx *ctx, RigidDev *d, const int32_t *pgs_order, lpe_
         LPE_HIP(ctx, hipMemcpyAsync(d->order, pgs_order, sizeof(int32_t) * nc, hipMemcpyHostToDevice, s));
     // ---- PGS
     LPE_HIP(ctx, hipMemsetAsync(d->inContact, 0, sizeof(int32_t) * 2 * nb, s));
-    LPE_TIMED(ctx, "k_mark_contacts", hipLaunchKernelGGL(k_mark_contacts, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->contacts, d->inContact));
-    LPE_TIMED(ctx, "k_pgs_bodies", hipLaunchKernelGGL(k_pgs_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->imii));
-    LPE_TIMED(ctx, "k_pgs_rows", hipLaunchKernelGGL(k_pgs_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, pgs_order ? d->order : (const int32_t *)nullptr, d->contacts, d->bodies, d->imii, d->rowN, d->rowR, d->rowAB, d->sItemA, d->sItemB));
+    LPE_KERNEL(ctx, "k_mark_contacts", k_mark_contacts, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->contacts, d->inContact);
+    LPE_KERNEL(ctx, "k_pgs_bodies", k_pgs_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->imii);
+    LPE_KERNEL(ctx, "k_pgs_rows", k_pgs_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, pgs_order ? d->order : (const int32_t *)nullptr, d->contacts, d->bodies, d->imii, d->rowN, d->rowR, d->rowAB, d->sItemA, d->sItemB);
     int st = rigid_schedule(ctx, d, d->counts + 1, nc, d->counts + 2);
     if (st) return st;
     // lambdas live in sPrevA/sPrevB (reinterpreted) after scheduling
     float *lamN = (float *)d->sPrevA, *lamF = (float *)d->sPrevB;
     size_t lds = sizeof(float) * 3 * (size_t)nb;
-    LPE_TIMED(ctx, "k_pgs_solve", hipLaunchKernelGGL(k_pgs_solve, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts + 2, d->sLStart, d->sLOrder, d->rowN, d->rowR, d->rowAB, d->imii, d->vel0, c.pgsIterations, c.frictionCoeff, lamN, lamF, d->counts + 1));
-    LPE_TIMED(ctx, "k_pgs_writeback", hipLaunchKernelGGL(k_pgs_writeback, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->inContact));
+    LPE_KERNEL(ctx, "k_pgs_solve", k_pgs_solve, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts + 2, d->sLStart, d->sLOrder, d->rowN, d->rowR, d->rowAB, d->imii, d->vel0, c.pgsIterations, c.frictionCoeff, lamN, lamF, d->counts + 1);
+    LPE_KERNEL(ctx, "k_pgs_writeback", k_pgs_writeback, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->inContact);
     LPE_CHECK_LAUNCH(ctx, "pgs");
     // ---- position solver (narrowphase order)
     int32_t *inPos = d->inContact + nb;
     int32_t *keep = d->sLCount, *kstart = d->sLStart;   // reuse after PGS
-    LPE_TIMED(ctx, "k_pos_bodies", hipLaunchKernelGGL(k_pos_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->posState));
-    LPE_TIMED(ctx, "k_pos_items", hipLaunchKernelGGL(k_pos_items, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->contacts, d->bodies, d->posState, keep));
+    LPE_KERNEL(ctx, "k_pos_bodies", k_pos_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->posState);
+    LPE_KERNEL(ctx, "k_pos_items", k_pos_items, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->contacts, d->bodies, d->posState, keep);
     st = rscan(ctx, d, d->counts + 1, nc, keep, kstart, nullptr);
     if (st) return st;
     // kept-contact count -> counts[4]
     LPE_HIP(ctx, hipMemcpyAsync(d->counts + 4, kstart + nc, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
-    LPE_TIMED(ctx, "k_pos_fill", hipLaunchKernelGGL(k_pos_fill, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, keep, kstart, d->contacts, d->posState, d->posItem, d->sItemA, d->sItemB, inPos));
+    LPE_KERNEL(ctx, "k_pos_fill", k_pos_fill, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, keep, kstart, d->contacts, d->posState, d->posItem, d->sItemA, d->sItemB, inPos);
     st = rigid_schedule(ctx, d, d->counts + 4, nc, d->counts + 3);
     if (st) return st;
     size_t lds2 = sizeof(double) * 3 * (size_t)nb;
-    LPE_TIMED(ctx, "k_pos_solve", hipLaunchKernelGGL(k_pos_solve, dim3(1), dim3(SOLVE_TPB), lds2, s, nb, d->counts + 3, d->sLStart, d->sLOrder, d->posItem, d->contacts, d->posState, d->bodies, inPos, c.posIterations, c.baumgarte, c.slop));
+    LPE_KERNEL(ctx, "k_pos_solve", k_pos_solve, dim3(1), dim3(SOLVE_TPB), lds2, s, nb, d->counts + 3, d->sLStart, d->sLOrder, d->posItem, d->contacts, d->posState, d->bodies, inPos, c.posIterations, c.baumgarte, c.slop);
     LPE_CHECK_LAUNCH(ctx, "position solver");
     if (stats) {
         int32_t hc[8];
@@ -1252,20 +1252,20 @@ extern "C" int lpe_rigid_integrate(lpe_ctx *ctx, int systems, double dt_state, d
     const lpe_rigid_config &c = d->cfg;
     hipStream_t s = ctx->stream;
     if (systems & 1)
-        LPE_TIMED(ctx, "k_boundary", hipLaunchKernelGGL(k_boundary, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.marginPixels * c.metersPerPixel, c.universeSize, c.bounceDamping, c.maxSpeed));
+        LPE_KERNEL(ctx, "k_boundary", k_boundary, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.marginPixels * c.metersPerPixel, c.universeSize, c.bounceDamping, c.maxSpeed);
     if (systems & (2 | 32)) {   // 32: planetary-mass check only (world tick)
         LPE_HIP(ctx, hipMemsetAsync(d->counts + 5, 0, sizeof(int32_t), s));
-        LPE_TIMED(ctx, "k_gravity_check", hipLaunchKernelGGL(k_gravity_check, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.planetaryMassThreshold, d->counts + 5));
+        LPE_KERNEL(ctx, "k_gravity_check", k_gravity_check, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.planetaryMassThreshold, d->counts + 5);
     }
     if (systems & 2) {
-        LPE_TIMED(ctx, "k_gravity", hipLaunchKernelGGL(k_gravity, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.gravity, dt_state, d->counts + 5));
+        LPE_KERNEL(ctx, "k_gravity", k_gravity, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.gravity, dt_state, d->counts + 5);
     }
     if (systems & 4)
-        LPE_TIMED(ctx, "k_rotation", hipLaunchKernelGGL(k_rotation, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, dt_state, c.angularDamping, c.maxAngularSpeed));
+        LPE_KERNEL(ctx, "k_rotation", k_rotation, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, dt_state, c.angularDamping, c.maxAngularSpeed);
     if (systems & 8)
-        LPE_TIMED(ctx, "k_movement", hipLaunchKernelGGL(k_movement, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, dt_move));
+        LPE_KERNEL(ctx, "k_movement", k_movement, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, dt_move);
     if (systems & 16)
-        LPE_TIMED(ctx, "k_sleep", hipLaunchKernelGGL(k_sleep, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.linearSleepThreshold, c.angularSleepThreshold, c.sleepFramesThreshold));
+        LPE_KERNEL(ctx, "k_sleep", k_sleep, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.linearSleepThreshold, c.angularSleepThreshold, c.sleepFramesThreshold);
     LPE_CHECK_LAUNCH(ctx, "integrate");
     return LPE_OK;
 }

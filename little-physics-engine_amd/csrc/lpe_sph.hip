@@ -54,6 +54,7 @@ static constexpr float PI_F = 3.14159265358979323846f;  // metal:17 evaluated in
 static constexpr int TPB = 256;
 static constexpr int SCAN_ELEMS = 1024;   // elements per scan block (256 thr x 4)
 static constexpr int MAX_KICK_BLOCKS = 2048;
+static constexpr int NLIST_CAP = 64;      // neighbours kept per particle (column-major list)
 
 // kernel coefficients (metal:19-38), fp32
 __device__ __forceinline__ float poly6Coeff2D(float h) {
@@ -318,11 +319,15 @@ k_scatter(int n, const uint32_t *__restrict__ key, const int32_t *__restrict__ i
     }
 }
 
-// canonical order inside a bin (ascending particle id) + state permutation P -> S
+// canonical order inside a bin (ascending particle id) + state permutation
+// P -> sorted slots.  The neighbour loops read packed records: nbA = (x, y, m,
+// -) written here; nbB = (vx, vy | rho, p/rho^2), first half written here,
+// second half by k_density.
 __global__ void __launch_bounds__(TPB)
 k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restrict__ start,
                const int32_t *__restrict__ tmpId, const int32_t *__restrict__ tmpOld,
-               PState P, PState S, int probe) {
+               PState P, PState S, float4 *__restrict__ nbA, float2 *__restrict__ nbB,
+               int probe) {
     int s = blockIdx.x * TPB + threadIdx.x;
     if (s >= n) return;
     int o = tmpOld[s];
@@ -332,145 +337,239 @@ k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restric
     int rank = 0;
     for (int j = b; j < e; j++) rank += (tmpId[j] < myid) ? 1 : 0;
     int d = b + rank;
-    S.x[d] = P.x[o]; S.y[d] = P.y[o];
-    S.vx[d] = P.vx[o]; S.vy[d] = P.vy[o];
-    S.m[d] = P.m[o]; S.id[d] = myid;
+    nbA[d] = make_float4(P.x[o], P.y[o], P.m[o], 0.f);
+    nbB[2 * d] = make_float2(P.vx[o], P.vy[o]);
+    S.id[d] = myid;
     if (!probe) { S.vhx[d] = P.vhx[o]; S.vhy[d] = P.vhy[o]; }
 }
 
 // ---------------------------------------------------------------------------
-// Does quadrant q of reference cell (gcx, gcy) lie within distance h of the
-// particle at t = (x + eps) / cs?  Conservative (box widened by 1e-3 cell,
-// 0.1% margin on h^2): a skipped quadrant only holds particles with
-// r^2 >= h^2 in fp32, whose terms the reference discards.
-__device__ __forceinline__ bool quad_near(float tx, float ty, int gcx, int gcy, int q, float cs,
-                                          float h2) {
-    float lox = (float)gcx + (float)(q & 1) * 0.5f, loy = (float)gcy + (float)(q >> 1) * 0.5f;
-    const float mg = 1e-3f;
-    float dx = fmaxf(fmaxf(lox - mg - tx, tx - (lox + 0.5f + mg)), 0.f) * cs;
-    float dy = fmaxf(fmaxf(loy - mg - ty, ty - (loy + 0.5f + mg)), 0.f) * cs;
-    return dx * dx + dy * dy < h2 * 1.001f;
+// Canonical neighbour walk.  The reference visits the 3x3 reference cells of
+// the particle row-major (metal:272-283); inside a cell our bins are the four
+// h-quadrants row-major, ascending particle id inside a quadrant (the order of
+// oracle/sph_oracle.c).  Only the quadrant columns/rows within `reach` (in
+// quadrant units: 2h/cs widened by 0.2%) of the particle are walked; every
+// quadrant left out holds only particles with r^2 >= h^2 in fp32, whose terms
+// the reference discards (metal:291, :365), so the sums are unchanged bit for
+// bit.  The walked quadrants always lie inside the particle's 3x3 cells, and
+// cells outside the reference grid are skipped (not-inserted particles,
+// metal:231-234).  Quadrants of one cell row and one cell are contiguous
+// bins, so each (cell, quadrant row) is one contiguous slot range.
+__device__ __forceinline__ int sel4(int4 v, int i) {
+    return i == 0 ? v.x : (i == 1 ? v.y : (i == 2 ? v.z : v.w));
 }
 
-// computeDensity (metal:246-307), one thread per sorted slot
-__global__ void __launch_bounds__(TPB)
-k_density(int n, float h, float eps, float stiffness, float restDensity, int W, int ox, int oy,
-          const GridParams *__restrict__ gp, const int32_t *__restrict__ start,
-          const float *__restrict__ sx, const float *__restrict__ sy, const float *__restrict__ sm,
-          float *__restrict__ rho, float *__restrict__ pr) {
-    int s = blockIdx.x * TPB + threadIdx.x;
-    if (s >= n) return;
-    const GridParams g = *gp;
-    const float cs = g.cellSize;
-    float xi = sx[s], yi = sy[s];
-    float h2 = h * h;
-    float poly6 = poly6Coeff2D(h);
-    float acc = 0.0f;
-    float tx = (xi + eps) / cs, ty = (yi + eps) / cs;
-    int gx = (int)floorf(tx), gy = (int)floorf(ty);
-    int cellX = gx - g.gridMinX, cellY = gy - g.gridMinY;
-    for (int ny = -1; ny <= 1; ny++) {
-        int cy = cellY + ny;
-        if (cy < 0 || cy >= g.gridDimY) continue;
-        int gcy = cy + g.gridMinY;
-        for (int nx = -1; nx <= 1; nx++) {
-            int cx = cellX + nx;
-            if (cx < 0 || cx >= g.gridDimX) continue;
-            int gcx = cx + g.gridMinX;
-            int cbase = (((gcy - oy) * W) + (gcx - ox)) << 2;
+// The walk issues every bin-boundary load of the (at most 3x3) cells up front
+// and the candidate records U at a time, so a wave has many loads in flight
+// (the loop is latency bound otherwise: one dependent L2 round trip per
+// candidate).  ld(k) loads candidate k's record, f(k, rec) consumes it; f is
+// called in the canonical order.
+template <int U, class L, class F>
+__device__ __forceinline__ void walk_neighbours(float xi, float yi, float eps, float cs,
+                                                float reach, const GridParams &g, int W, int H,
+                                                int ox, int oy, const int32_t *__restrict__ start,
+                                                L ld, F f) {
+    float u = 2.0f * ((xi + eps) / cs), v = 2.0f * ((yi + eps) / cs);
+    int bx0 = (int)floorf(u - reach), bx1 = (int)floorf(u + reach);
+    int by0 = (int)floorf(v - reach), by1 = (int)floorf(v + reach);
+    // clipped to the reference grid and (a particle that left the device
+    // grid raises ST_CAP_OVERFLOW in k_kick_drift) to the device grid
+    int cxa = max(max(bx0 >> 1, g.gridMinX), ox);
+    int cxb = min(min(bx1 >> 1, g.gridMinX + g.gridDimX - 1), ox + W - 1);
+    int cya = max(max(by0 >> 1, g.gridMinY), oy);
+    int cyb = min(min(by1 >> 1, g.gridMinY + g.gridDimY - 1), oy + H - 1);
+    int4 q[3][3];
+    int qn[3][3];
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (!quad_near(tx, ty, gcx, gcy, q, cs, h2)) continue;
-                int b = start[cbase + q], e = start[cbase + q + 1];
-                for (int k = b; k < e; k++) {
-                    float dx = xi - sx[k], dy = yi - sy[k];
-                    float r2 = dx * dx + dy * dy;
-                    if (r2 < h2) {
-                        float diff = h2 - r2;
-                        float w = poly6 * diff * diff * diff;
-                        acc += sm[k] * w;
-                    }
+    for (int dy = 0; dy < 3; dy++)
+#pragma unroll
+        for (int dx = 0; dx < 3; dx++) {
+            int cy = cya + dy, cx = cxa + dx;
+            if (cy <= cyb && cx <= cxb) {
+                int cbase = (((cy - oy) * W) + (cx - ox)) << 2;
+                q[dy][dx] = *reinterpret_cast<const int4 *>(start + cbase);
+                qn[dy][dx] = start[cbase + 4];
+            } else {
+                q[dy][dx] = make_int4(0, 0, 0, 0);
+                qn[dy][dx] = 0;
+            }
+        }
+#pragma unroll
+    for (int dy = 0; dy < 3; dy++) {
+        int cy = cya + dy;
+        if (cy > cyb) break;
+        int qya = max(by0 - 2 * cy, 0), qyb = min(by1 - 2 * cy, 1);
+#pragma unroll
+        for (int dx = 0; dx < 3; dx++) {
+            int cx = cxa + dx;
+            if (cx > cxb) break;
+            int qxa = max(bx0 - 2 * cx, 0), qxb = min(bx1 - 2 * cx, 1);
+            for (int qy = qya; qy <= qyb; qy++) {
+                int i0 = qy * 2 + qxa, i1 = qy * 2 + qxb + 1;
+                int b = sel4(q[dy][dx], i0);
+                int e = (i1 == 4) ? qn[dy][dx] : sel4(q[dy][dx], i1);
+                for (int k = b; k < e; k += U) {
+                    decltype(ld(0)) r[U];
+#pragma unroll
+                    for (int j = 0; j < U; j++) r[j] = ld(min(k + j, e - 1));
+#pragma unroll
+                    for (int j = 0; j < U; j++)
+                        if (k + j < e) f(k + j, r[j]);
                 }
             }
         }
     }
+}
+
+// XCD-aware block order: hardware block b runs on XCD b % 8; give each XCD a
+// contiguous run of sorted slots so its L2 holds one spatial slab (and its
+// halo) instead of the whole domain.  Launch xcd_grid(nb) blocks.
+static constexpr int NXCD = 8;
+__host__ __device__ __forceinline__ int xcd_grid(int nb) { return ((nb + NXCD - 1) / NXCD) * NXCD; }
+__device__ __forceinline__ int xcd_block(int nb) {
+    int per = (nb + NXCD - 1) / NXCD;
+    int lb = (int)(blockIdx.x % NXCD) * per + (int)(blockIdx.x / NXCD);
+    return lb < nb ? lb : -1;
+}
+
+__device__ __forceinline__ float walk_reach(float h, float cs) {
+    return (2.0f * h / cs) * 1.002f + 2e-3f;
+}
+
+// computeDensity (metal:246-307), one thread per sorted slot
+__global__ void __launch_bounds__(TPB)
+k_density(int n, float h, float eps, float stiffness, float restDensity, int W, int H, int ox, int oy,
+          const GridParams *__restrict__ gp, const int32_t *__restrict__ start,
+          const float4 *__restrict__ nbA, float2 *__restrict__ nbB,
+          float *__restrict__ rho, float *__restrict__ pr, int16_t *__restrict__ nlist,
+          int32_t *__restrict__ ncount) {
+    // neighbour list staged in LDS (column-major per block), written out
+    // coalesced at the end: entry = k - s as int16
+    __shared__ int16_t lds_nl[NLIST_CAP * TPB];
+    int lb = xcd_block((n + TPB - 1) / TPB);
+    int s = lb * TPB + threadIdx.x;
+    if (lb < 0 || s >= n) return;
+    const GridParams g = *gp;
+    const float cs = g.cellSize;
+    const float4 me = nbA[s];
+    const int tid = threadIdx.x;
+    const float xi = me.x, yi = me.y;
+    const float h2 = h * h;
+    const float poly6 = poly6Coeff2D(h);
+    float acc = 0.0f;
+    int cnt = 0;
+    walk_neighbours<4>(xi, yi, eps, cs, walk_reach(h, cs), g, W, H, ox, oy, start,
+                       [&](int k) { return nbA[k]; },
+                       [&](int k, const float4 &o) {
+        float dx = xi - o.x, dy = yi - o.y;
+        float r2 = dx * dx + dy * dy;
+        if (r2 < h2) {
+            float diff = h2 - r2;
+            float w = poly6 * diff * diff * diff;
+            acc += o.z * w;
+            // the forces pass sees exactly these neighbours (r^2 < h_ij^2 with
+            // h_ij = h, metal:360-366), in this order
+            if (k != s) {
+                int off = k - s;
+                if (cnt < NLIST_CAP && off >= -32768 && off <= 32767)
+                    lds_nl[cnt * TPB + tid] = (int16_t)off;
+                else
+                    cnt = NLIST_CAP;          // overflow: forces walks the bins
+                cnt++;
+            }
+        }
+    });
+    ncount[s] = cnt;
+    const int m = cnt <= NLIST_CAP ? cnt : 0;
+    for (int j = 0; j < m; j++) nlist[(size_t)j * n + s] = lds_nl[j * TPB + tid];
     float pres = stiffness * (acc - restDensity);
     if (pres < 0.f) pres = 0.f;
     rho[s] = acc;
     pr[s] = pres;
+    nbB[2 * s + 1] = make_float2(acc, pres / (acc * acc));   // the p_j / rho_j^2 of metal:370
 }
 
 struct SphStepParams {
-    int n, W, ox, oy;
+    int n, W, H, ox, oy;
     float h, eps, dt, hdt;
     float viscosity, minDist, minDens;
 };
 
-// computeForces + velocityVerletFinish + impulse + push-out; reads S, writes P
+// computeForces + velocityVerletFinish + impulse + push-out; reads the sorted
+// records, writes P
 __global__ void __launch_bounds__(TPB)
 k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict__ gp,
-                const int32_t *__restrict__ start, PState S, const float *__restrict__ rho,
-                const float *__restrict__ pr, PState P,
+                const int32_t *__restrict__ start, PState S, const float4 *__restrict__ nbA,
+                const float4 *__restrict__ nbB, const float *__restrict__ pr,
+                const int16_t *__restrict__ nlist, const int32_t *__restrict__ ncount, PState P,
                 const lpe_gpu_rigid *__restrict__ rig, const int32_t *__restrict__ rbinStart,
                 const int32_t *__restrict__ rbinList, float *__restrict__ accum) {
-    int s = blockIdx.x * TPB + threadIdx.x;
-    if (s >= sp.n) return;
+    int lb = xcd_block((sp.n + TPB - 1) / TPB);
+    int s = lb * TPB + threadIdx.x;
+    if (lb < 0 || s >= sp.n) return;
     const GridParams g = *gp;
     const float cs = g.cellSize;
-    const float xi = S.x[s], yi = S.y[s];
-    const float vxi = S.vx[s], vyi = S.vy[s];
-    const float pi = pr[s], rhoi = rho[s];
+    const float4 meA = nbA[s], meB = nbB[s];
+    const float xi = meA.x, yi = meA.y;
+    const float vxi = meB.x, vyi = meB.y;
+    const float rhoi = meB.z;
+    const float pi = pr[s];
     const float hi = sp.h;
-    const float h2 = hi * hi;
+    // all particles carry h = smoothingLength (fluid.cpp:287-292): the pair
+    // smoothing length and its kernel coefficients are per-launch constants
+    const float hj = sp.h;
+    const float h_ij = 0.5f * (hi + hj);
+    const float h_ij2 = h_ij * h_ij;
+    const float spF = spikyCoeff2D(h_ij);
+    const float lapC = viscLaplacianCoeff2D(h_ij);
+    const float pti = meB.w;                      // pi / (rhoi * rhoi)
+    const bool rhoi_ok = !(rhoi < sp.minDens);
     float sumFx = 0.f, sumFy = 0.f;
-    float tx = (xi + sp.eps) / cs, ty = (yi + sp.eps) / cs;
-    int gx = (int)floorf(tx), gy = (int)floorf(ty);
-    int cellX = gx - g.gridMinX, cellY = gy - g.gridMinY;
-    for (int ny = -1; ny <= 1; ny++) {
-        int cy = cellY + ny;
-        if (cy < 0 || cy >= g.gridDimY) continue;
-        int gcy = cy + g.gridMinY;
-        for (int nx = -1; nx <= 1; nx++) {
-            int cx = cellX + nx;
-            if (cx < 0 || cx >= g.gridDimX) continue;
-            int gcx = cx + g.gridMinX;
-            int cbase = (((gcy - sp.oy) * sp.W) + (gcx - sp.ox)) << 2;
+    struct Rec { float4 a, b; };
+    auto pair = [&](int k, const Rec &o) {
+        if (k == s) return;
+        float dx = xi - o.a.x, dy = yi - o.a.y;
+        float r2 = dx * dx + dy * dy;
+        if (r2 < sp.minDist) return;
+        if (r2 >= h_ij2) return;
+        float r = sqrtf(r2);
+        float rhoj = o.b.z;
+        if (rhoj < sp.minDens || !rhoi_ok) return;
+        float mj = o.a.z;
+        float term = pti + o.b.w;
+        float diff = (h_ij - r);
+        float wSpiky = spF * (diff * diff);
+        float rx = dx / r, ry = dy / r;
+        float fxPress = -mj * term * wSpiky;
+        float fx = fxPress * rx;
+        float fy = fxPress * ry;
+        float vx_ij = vxi - o.b.x, vy_ij = vyi - o.b.y;
+        float wVisc = lapC * diff;
+        float fVisc = sp.viscosity * mj * (wVisc / rhoj);
+        fx -= fVisc * vx_ij;
+        fy -= fVisc * vy_ij;
+        sumFx += fx;
+        sumFy += fy;
+    };
+    const int cnt = ncount[s];
+    if (cnt <= NLIST_CAP) {
+        // the density pass's list: the r^2 < h^2 neighbours in canonical
+        // order, so the heavy pair math runs only on real neighbours
+        constexpr int U = 4;
+        for (int j = 0; j < cnt; j += U) {
+            int kk[U];
 #pragma unroll
-            for (int q = 0; q < 4; q++) {
-                if (!quad_near(tx, ty, gcx, gcy, q, cs, h2)) continue;
-                int b = start[cbase + q], e = start[cbase + q + 1];
-                for (int k = b; k < e; k++) {
-                    if (k == s) continue;
-                    float dx = xi - S.x[k], dy = yi - S.y[k];
-                    float r2 = dx * dx + dy * dy;
-                    if (r2 < sp.minDist) continue;
-                    float hj = sp.h;
-                    float h_ij = 0.5f * (hi + hj);
-                    float h_ij2 = h_ij * h_ij;
-                    if (r2 >= h_ij2) continue;
-                    float r = sqrtf(r2);
-                    float pj = pr[k], rhoj = rho[k];
-                    if (rhoj < sp.minDens || rhoi < sp.minDens) continue;
-                    float mj = S.m[k];
-                    float term = (pi / (rhoi * rhoi)) + (pj / (rhoj * rhoj));
-                    float spF = spikyCoeff2D(h_ij);
-                    float diff = (h_ij - r);
-                    float wSpiky = spF * (diff * diff);
-                    float rx = dx / r, ry = dy / r;
-                    float fxPress = -mj * term * wSpiky;
-                    float fx = fxPress * rx;
-                    float fy = fxPress * ry;
-                    float vx_ij = vxi - S.vx[k], vy_ij = vyi - S.vy[k];
-                    float lapC = viscLaplacianCoeff2D(h_ij);
-                    float wVisc = lapC * diff;
-                    float fVisc = sp.viscosity * mj * (wVisc / rhoj);
-                    fx -= fVisc * vx_ij;
-                    fy -= fVisc * vy_ij;
-                    sumFx += fx;
-                    sumFy += fy;
-                }
-            }
+            for (int u = 0; u < U; u++) kk[u] = s + nlist[(size_t)min(j + u, cnt - 1) * sp.n + s];
+            Rec r[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) r[u] = Rec{nbA[kk[u]], nbB[kk[u]]};
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (j + u < cnt) pair(kk[u], r[u]);
         }
+    } else {
+        walk_neighbours<2>(xi, yi, sp.eps, cs, walk_reach(hi, cs), g, sp.W, sp.H, sp.ox, sp.oy, start,
+                           [&](int k) { return Rec{nbA[k], nbB[k]}; }, pair);
     }
     CoupleState st;
     st.x = xi; st.y = yi;
@@ -479,7 +578,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     // velocityVerletFinish (metal:428-441)
     st.vx = st.vhx + sp.hdt * st.ax;
     st.vy = st.vhy + sp.hdt * st.ay;
-    st.mass = S.m[s]; st.rho = rhoi; st.p = pi;
+    st.mass = meA.z; st.rho = rhoi; st.p = pi;
     int k0 = 0, k1 = 0;
     if (cp.nr > 0) {
         float fbx = fminf(fmaxf(floorf(st.x / cp.bcs) - (float)cp.bx0, 0.f), (float)(cp.bW - 1));
@@ -504,30 +603,34 @@ __device__ __forceinline__ int bin_of(float v, float bcs, int b0, int nb) {
     t = fminf(fmaxf(t, 0.f), (float)(nb - 1));
     return (int)t;
 }
+// one wave per rigid, lanes stride over the bins its AABB covers (a wall
+// covers thousands of 0.25 m bins; a thread per rigid serialises on it)
 __global__ void k_rbin_count(int nr, const lpe_gpu_rigid *__restrict__ rig, float bcs,
                              int bx0, int by0, int bW, int bH, int32_t *__restrict__ cnt) {
-    int r = blockIdx.x * blockDim.x + threadIdx.x;
+    int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    int lane = threadIdx.x & 63;
     if (r >= nr) return;
     const lpe_gpu_rigid &b = rig[r];
     int x0 = bin_of(b.minX, bcs, bx0, bW), x1 = bin_of(b.maxX, bcs, bx0, bW);
     int y0 = bin_of(b.minY, bcs, by0, bH), y1 = bin_of(b.maxY, bcs, by0, bH);
-    for (int yy = y0; yy <= y1; yy++)
-        for (int xx = x0; xx <= x1; xx++) atomicAdd(&cnt[yy * bW + xx], 1);
+    int w = x1 - x0 + 1, tot = w * (y1 - y0 + 1);
+    for (int k = lane; k < tot; k += 64) atomicAdd(&cnt[(y0 + k / w) * bW + x0 + k % w], 1);
 }
 __global__ void k_rbin_fill(int nr, const lpe_gpu_rigid *__restrict__ rig, float bcs,
                             int bx0, int by0, int bW, int bH, int32_t *__restrict__ cursor,
                             int32_t *__restrict__ list, int cap, int32_t *__restrict__ status) {
-    int r = blockIdx.x * blockDim.x + threadIdx.x;
+    int r = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    int lane = threadIdx.x & 63;
     if (r >= nr) return;
     const lpe_gpu_rigid &b = rig[r];
     int x0 = bin_of(b.minX, bcs, bx0, bW), x1 = bin_of(b.maxX, bcs, bx0, bW);
     int y0 = bin_of(b.minY, bcs, by0, bH), y1 = bin_of(b.maxY, bcs, by0, bH);
-    for (int yy = y0; yy <= y1; yy++)
-        for (int xx = x0; xx <= x1; xx++) {
-            int slot = atomicAdd(&cursor[yy * bW + xx], 1);
-            if (slot < cap) list[slot] = r;
-            else atomicOr(&status[ST_LIST_OVERFLOW], 1);
-        }
+    int w = x1 - x0 + 1, tot = w * (y1 - y0 + 1);
+    for (int k = lane; k < tot; k += 64) {
+        int slot = atomicAdd(&cursor[(y0 + k / w) * bW + x0 + k % w], 1);
+        if (slot < cap) list[slot] = r;
+        else atomicOr(&status[ST_LIST_OVERFLOW], 1);
+    }
 }
 // insertion sort of each bin's list -> ascending rigid index
 __global__ void k_rbin_sort(int B, int32_t *__restrict__ start, int32_t *__restrict__ list, int cap) {
@@ -604,7 +707,7 @@ static void pstate_free(PState &p) {
 static void sph_free(SphDev &d) {
     pstate_free(d.P);
     pstate_free(d.S);
-    void *ptrs[] = {d.rho, d.pr, d.key, d.tmpId, d.tmpOld, d.count, d.start, d.cursor,
+    void *ptrs[] = {d.rho, d.pr, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.count, d.start, d.cursor,
                     d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.accum, d.rbinStart,
                     d.rbinList, d.rbinCount, d.coupleBody};
     for (void *p : ptrs) if (p) (void)hipFree(p);
@@ -702,24 +805,9 @@ static float ref_cell_size(const lpe_fluid_config &c) {
     return 2.f * maxH;
 }
 
-// absolute device grid covering the particle bbox with a generous margin
-static int sph_plan_grid(lpe_ctx *ctx, const float *x, const float *y, int n) {
+// absolute device grid [gx0, gx1] x [gy0, gy1] (reference cells)
+static int sph_set_grid(lpe_ctx *ctx, int gx0, int gy0, int gx1, int gy1) {
     SphDev &d = ctx->sph;
-    float cs = ref_cell_size(d.cfg);
-    float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
-    for (int i = 0; i < n; i++) {
-        mnx = std::min(mnx, x[i]); mxx = std::max(mxx, x[i]);
-        mny = std::min(mny, y[i]); mxy = std::max(mxy, y[i]);
-    }
-    if (n == 0) { mnx = mny = 0.f; mxx = mxy = 1.f; }
-    // margin: 25% of the extent on every side, at least 64 cells
-    float ex = std::max(mxx - mnx, mxy - mny);
-    int pad = std::max(64, (int)(0.25f * ex / cs) + 8);
-    int gx0 = (int)std::floor(mnx / cs) - pad;
-    int gy0 = (int)std::floor(mny / cs) - pad;
-    int gx1 = (int)std::floor(mxx / cs) + pad;
-    int gy1 = (int)std::floor(mxy / cs) + pad;
-    d.cs = cs;
     d.ox = gx0; d.oy = gy0;
     d.W = gx1 - gx0 + 1; d.H = gy1 - gy0 + 1;
     long C = 4L * d.W * d.H;
@@ -737,7 +825,40 @@ static int sph_plan_grid(lpe_ctx *ctx, const float *x, const float *y, int n) {
         d.cap_cells = (int)C;
     }
     LPE_HIP(ctx, hipMemsetAsync(d.count, 0, sizeof(int32_t) * C, ctx->stream));
+    d.rig_dirty = true;    // the coupling bins span the device grid
     return LPE_OK;
+}
+
+// absolute device grid covering the particle bbox with a generous margin
+static int sph_plan_grid(lpe_ctx *ctx, const float *x, const float *y, int n) {
+    SphDev &d = ctx->sph;
+    float cs = ref_cell_size(d.cfg);
+    float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
+    for (int i = 0; i < n; i++) {
+        mnx = std::min(mnx, x[i]); mxx = std::max(mxx, x[i]);
+        mny = std::min(mny, y[i]); mxy = std::max(mxy, y[i]);
+    }
+    if (n == 0) { mnx = mny = 0.f; mxx = mxy = 1.f; }
+    // margin: 25% of the extent on every side, at least 64 cells
+    float ex = std::max(mxx - mnx, mxy - mny);
+    int pad = std::max(64, (int)(0.25f * ex / cs) + 8);
+    d.cs = cs;
+    return sph_set_grid(ctx, (int)std::floor(mnx / cs) - pad, (int)std::floor(mny / cs) - pad,
+                        (int)std::floor(mxx / cs) + pad, (int)std::floor(mxy / cs) + pad);
+}
+
+// grow the device grid to cover [x0, x1] x [y0, y1] (world mode: the
+// universe the boundary system keeps every body and particle in)
+int lpe_sph_cover_box(lpe_ctx *ctx, double x0, double y0, double x1, double y1) {
+    SphDev &d = ctx->sph;
+    if (d.n <= 0 || d.cs <= 0.f) return LPE_OK;
+    const double cs = d.cs;
+    int gx0 = std::min(d.ox, (int)std::floor(x0 / cs) - 4);
+    int gy0 = std::min(d.oy, (int)std::floor(y0 / cs) - 4);
+    int gx1 = std::max(d.ox + d.W - 1, (int)std::floor(x1 / cs) + 4);
+    int gy1 = std::max(d.oy + d.H - 1, (int)std::floor(y1 / cs) + 4);
+    if (gx0 == d.ox && gy0 == d.oy && gx1 == d.ox + d.W - 1 && gy1 == d.oy + d.H - 1) return LPE_OK;
+    return sph_set_grid(ctx, gx0, gy0, gx1, gy1);
 }
 
 static int pstate_alloc(lpe_ctx *ctx, PState &p, size_t N, bool with_a) {
@@ -756,7 +877,7 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     if (n <= d.cap_n && d.P.x) return LPE_OK;
     pstate_free(d.P);
     pstate_free(d.S);
-    void *ptrs[] = {d.rho, d.pr, d.key, d.tmpId, d.tmpOld, d.bboxPart};
+    void *ptrs[] = {d.rho, d.pr, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.bboxPart};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     size_t N = (size_t)std::max(n, 1);
     int st = pstate_alloc(ctx, d.P, N, true);
@@ -765,6 +886,10 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     if (st) return st;
     LPE_HIP(ctx, hipMalloc((void **)&d.rho, sizeof(float) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.pr, sizeof(float) * N));
+    LPE_HIP(ctx, hipMalloc((void **)&d.nbA, sizeof(float4) * N));
+    LPE_HIP(ctx, hipMalloc((void **)&d.nbB, sizeof(float4) * N));
+    LPE_HIP(ctx, hipMalloc((void **)&d.nlist, sizeof(int16_t) * N * NLIST_CAP));
+    LPE_HIP(ctx, hipMalloc((void **)&d.ncount, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.key, sizeof(uint32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpId, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpOld, sizeof(int32_t) * N));
@@ -877,11 +1002,11 @@ static int sph_scan(lpe_ctx *ctx, int C, int32_t *cnt, int32_t *start, int32_t *
     SphDev &d = ctx->sph;
     int nb = (C + SCAN_ELEMS - 1) / SCAN_ELEMS;
     hipStream_t s = ctx->stream;
-    LPE_TIMED(ctx, "k_scan_reduce", hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(TPB), 0, s, C, cnt, bsum));
-    LPE_TIMED(ctx, "k_scan_blocks", hipLaunchKernelGGL(k_scan_blocks, dim3(1), dim3(TPB), 0, s, nb, bsum, start + C, d.bboxPart,
-                       nparts, d.cs, fluid ? d.gp : (GridParams *)nullptr, d.status));
-    LPE_TIMED(ctx, "k_scan_final", hipLaunchKernelGGL(k_scan_final, dim3(nb), dim3(TPB), 0, s, C, d.W, d.ox, d.oy, cnt, bsum,
-                       start, cursor, d.gp, d.status, fluid ? 1 : 0));
+    LPE_KERNEL(ctx, "k_scan_reduce", k_scan_reduce, dim3(nb), dim3(TPB), 0, s, C, cnt, bsum);
+    LPE_KERNEL(ctx, "k_scan_blocks", k_scan_blocks, dim3(1), dim3(TPB), 0, s, nb, bsum, start + C, d.bboxPart,
+                       nparts, d.cs, fluid ? d.gp : (GridParams *)nullptr, d.status);
+    LPE_KERNEL(ctx, "k_scan_final", k_scan_final, dim3(nb), dim3(TPB), 0, s, C, d.W, d.ox, d.oy, cnt, bsum,
+                       start, cursor, d.gp, d.status, fluid ? 1 : 0);
     LPE_CHECK_LAUNCH(ctx, "scan");
     return LPE_OK;
 }
@@ -906,8 +1031,8 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
     }
     hipStream_t s = ctx->stream;
     LPE_HIP(ctx, hipMemsetAsync(d.rbinCount, 0, sizeof(int32_t) * B, s));
-    LPE_TIMED(ctx, "k_rbin_count", hipLaunchKernelGGL(k_rbin_count, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig, d.bcs,
-                       d.bx0, d.by0, d.bW, d.bH, d.rbinCount));
+    LPE_KERNEL(ctx, "k_rbin_count", k_rbin_count, dim3(nblk(d.nr, 4)), dim3(256), 0, s, d.nr, d.rig, d.bcs,
+                       d.bx0, d.by0, d.bW, d.bH, d.rbinCount);
     int32_t *cursor = d.rbinCount + B;
     int st = sph_scan(ctx, B, d.rbinCount, d.rbinStart, cursor, d.rbinCount + 2 * B, 0, false);
     if (st) return st;
@@ -923,9 +1048,9 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
         d.cap_rlist = std::max(total, 1);
     }
     d.rlist_len = total;
-    LPE_TIMED(ctx, "k_rbin_fill", hipLaunchKernelGGL(k_rbin_fill, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig, d.bcs,
-                       d.bx0, d.by0, d.bW, d.bH, cursor, d.rbinList, d.cap_rlist, d.status));
-    LPE_TIMED(ctx, "k_rbin_sort", hipLaunchKernelGGL(k_rbin_sort, dim3(nblk(B, 128)), dim3(128), 0, s, B, d.rbinStart, d.rbinList, d.cap_rlist));
+    LPE_KERNEL(ctx, "k_rbin_fill", k_rbin_fill, dim3(nblk(d.nr, 4)), dim3(256), 0, s, d.nr, d.rig, d.bcs,
+                       d.bx0, d.by0, d.bW, d.bH, cursor, d.rbinList, d.cap_rlist, d.status);
+    LPE_KERNEL(ctx, "k_rbin_sort", k_rbin_sort, dim3(nblk(B, 128)), dim3(128), 0, s, B, d.rbinStart, d.rbinList, d.cap_rlist);
     LPE_CHECK_LAUNCH(ctx, "rbin");
     d.rig_dirty = false;
     return LPE_OK;
@@ -937,16 +1062,16 @@ static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool pr
     hipStream_t s = ctx->stream;
     int C = 4 * d.W * d.H;
     int kb = std::min(MAX_KICK_BLOCKS, std::max(1, nblk(d.n)));
-    LPE_TIMED(ctx, "k_kick_drift", hipLaunchKernelGGL(k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
+    LPE_KERNEL(ctx, "k_kick_drift", k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
                        first ? 1 : 0, probe ? 1 : 0, d.cfg.gridConfig.gridEpsilon, d.cs, d.ox,
-                       d.oy, d.W, d.H, d.P, d.key, d.count, d.bboxPart, d.status));
+                       d.oy, d.W, d.H, d.P, d.key, d.count, d.bboxPart, d.status);
     LPE_CHECK_LAUNCH(ctx, "k_kick_drift");
     int st = sph_scan(ctx, C, d.count, d.start, d.cursor, d.blocksum, kb, true);
     if (st) return st;
-    LPE_TIMED(ctx, "k_scatter", hipLaunchKernelGGL(k_scatter, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.P.id, d.cursor,
-                       d.tmpId, d.tmpOld));
-    LPE_TIMED(ctx, "k_rank_permute", hipLaunchKernelGGL(k_rank_permute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.start,
-                       d.tmpId, d.tmpOld, d.P, d.S, probe ? 1 : 0));
+    LPE_KERNEL(ctx, "k_scatter", k_scatter, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.P.id, d.cursor,
+                       d.tmpId, d.tmpOld);
+    LPE_KERNEL(ctx, "k_rank_permute", k_rank_permute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.start,
+                       d.tmpId, d.tmpOld, d.P, d.S, d.nbA, (float2 *)d.nbB, probe ? 1 : 0);
     LPE_CHECK_LAUNCH(ctx, "hash");
     return LPE_OK;
 }
@@ -954,10 +1079,10 @@ static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool pr
 static int sph_density(lpe_ctx *ctx) {
     SphDev &d = ctx->sph;
     const lpe_fluid_config &c = d.cfg;
-    LPE_TIMED(ctx, "k_density", hipLaunchKernelGGL(k_density, dim3(nblk(d.n)), dim3(TPB), 0, ctx->stream, d.n,
+    LPE_KERNEL(ctx, "k_density", k_density, dim3(xcd_grid(nblk(d.n))), dim3(TPB), 0, ctx->stream, d.n,
                        c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
-                       c.restDensity, d.W, d.ox, d.oy, d.gp, d.start, d.S.x, d.S.y, d.S.m,
-                       d.rho, d.pr));
+                       c.restDensity, d.W, d.H, d.ox, d.oy, d.gp, d.start, d.nbA, (float2 *)d.nbB,
+                       d.rho, d.pr, d.nlist, d.ncount);
     LPE_CHECK_LAUNCH(ctx, "k_density");
     return LPE_OK;
 }
@@ -977,7 +1102,7 @@ extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
     if (st) return st;
     LPE_HIP(ctx, hipMemsetAsync(d.status + ST_MAX_OCC, 0, sizeof(int32_t), s));
     SphStepParams sp;
-    sp.n = d.n; sp.W = d.W; sp.ox = d.ox; sp.oy = d.oy;
+    sp.n = d.n; sp.W = d.W; sp.H = d.H; sp.ox = d.ox; sp.oy = d.oy;
     sp.h = c.gridConfig.smoothingLength; sp.eps = c.gridConfig.gridEpsilon;
     sp.dt = subDt; sp.hdt = halfDt;
     sp.viscosity = c.viscosity;
@@ -990,14 +1115,14 @@ extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
         if (st) return st;
         st = sph_density(ctx);
         if (st) return st;
-        LPE_TIMED(ctx, "k_forces_couple", hipLaunchKernelGGL(k_forces_couple, dim3(nblk(d.n)), dim3(TPB), 0, s, sp, cp, d.gp,
-                           d.start, d.S, d.rho, d.pr, d.P, d.rig, d.rbinStart, d.rbinList,
-                           d.accum));
+        LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(xcd_grid(nblk(d.n))), dim3(TPB), 0, s, sp, cp, d.gp,
+                           d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.rbinStart, d.rbinList,
+                           d.accum);
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
     }
     if (d.nr > 0) {
-        LPE_TIMED(ctx, "k_rigid_writeback", hipLaunchKernelGGL(k_rigid_writeback, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig,
-                           d.accum, d.accum + 3 * d.nr, c.dampingFactor));
+        LPE_KERNEL(ctx, "k_rigid_writeback", k_rigid_writeback, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig,
+                           d.accum, d.accum + 3 * d.nr, c.dampingFactor);
         LPE_CHECK_LAUNCH(ctx, "k_rigid_writeback");
     }
     return LPE_OK;
@@ -1012,7 +1137,7 @@ static int sph_unpermute_download(lpe_ctx *ctx, const int32_t *id, int nf, const
     float *stage[6] = {d.S.x, d.S.y, d.S.vx, d.S.vy, d.S.vhx, d.S.vhy};
     Fields6 f{};
     for (int k = 0; k < nf; k++) { f.src[k] = src[k]; f.dst[k] = stage[k]; }
-    LPE_TIMED(ctx, "k_unpermute", hipLaunchKernelGGL(k_unpermute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, id, nf, f));
+    LPE_KERNEL(ctx, "k_unpermute", k_unpermute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, id, nf, f);
     LPE_CHECK_LAUNCH(ctx, "k_unpermute");
     for (int k = 0; k < nf; k++)
         if (host[k])
@@ -1105,8 +1230,8 @@ extern "C" int lpe_sph_probe_cells(lpe_ctx *ctx, int32_t *cell_index, lpe_sph_st
     LPE_HIP(ctx, hipMemsetAsync(d.status + ST_MAX_OCC, 0, sizeof(int32_t), ctx->stream));
     int st = sph_hash(ctx, 0.f, 0.f, false, true);
     if (st) return st;
-    LPE_TIMED(ctx, "k_ref_cells", hipLaunchKernelGGL(k_ref_cells, dim3(nblk(d.n)), dim3(TPB), 0, ctx->stream, d.n,
-                       d.cfg.gridConfig.gridEpsilon, d.P.x, d.P.y, d.P.id, d.gp, d.tmpId));
+    LPE_KERNEL(ctx, "k_ref_cells", k_ref_cells, dim3(nblk(d.n)), dim3(TPB), 0, ctx->stream, d.n,
+                       d.cfg.gridConfig.gridEpsilon, d.P.x, d.P.y, d.P.id, d.gp, d.tmpId);
     LPE_CHECK_LAUNCH(ctx, "k_ref_cells");
     LPE_HIP(ctx, hipMemcpyAsync(cell_index, d.tmpId, sizeof(int32_t) * d.n, hipMemcpyDeviceToHost,
                                 ctx->stream));

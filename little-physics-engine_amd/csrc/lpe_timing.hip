@@ -4,6 +4,18 @@
 
 namespace lpe {
 
+// mode 2: the dominant kernels only, so the host keeps enough launches queued
+// ahead of the device (per-kernel events on every launch make the host the
+// bottleneck and the events then time the device idling between launches)
+bool KernelTimer::wants(const char *name) const {
+    if (on == 1) return true;
+    static const char *hot[] = {"k_density", "k_forces_couple", "k_pgs_solve", "k_pos_solve",
+                                "k_narrow", "k_bp_pairs"};
+    for (const char *h : hot)
+        if (std::strcmp(h, name) == 0) return true;
+    return false;
+}
+
 int KernelTimer::slot(const char *name) {
     for (size_t i = 0; i < names.size(); i++)
         if (names[i] == name) return (int)i;
@@ -21,7 +33,9 @@ hipEvent_t KernelTimer::get() {
         return e;
     }
     hipEvent_t e = nullptr;
-    (void)hipEventCreate(&e);
+    // device-scope release: the default system-scope release writes back L2
+    // at every event, which slows the kernels being timed
+    (void)hipEventCreateWithFlags(&e, hipEventReleaseToDevice);
     return e;
 }
 
@@ -45,7 +59,8 @@ static void timer_resolve(lpe_ctx *ctx) {
 
 extern "C" int lpe_timing_enable(lpe_ctx *ctx, int on) {
     if (!ctx) return LPE_ERR_ARG;
-    ctx->timer.on = on != 0;
+    if (on < 0 || on > 2) return LPE_ERR_ARG;
+    ctx->timer.on = on;
     return LPE_OK;
 }
 

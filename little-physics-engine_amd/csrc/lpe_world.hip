@@ -180,26 +180,34 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
         int st = lpe_world_set_coupling(ctx, -1, nullptr);
         if (st) return st;
     }
+    {
+        // the boundary system keeps the fluid inside the universe at the end
+        // of every tick (boundary.cpp:13-70); the sub-steps of one tick move
+        // a particle far less than a metre past it
+        const double U = rc.universeSize;
+        int st = lpe_sph_cover_box(ctx, -1.0, -1.0, U + 1.0, U + 1.0);
+        if (st) return st;
+    }
     for (int t = 0; t < nticks; t++) {
         // 1) FluidSystem::update (fluid.cpp:958-1021)
         if (d.n > 0) {
             int nr = d.couple_n;
             if (nr > 0) {
-                LPE_TIMED(ctx, "k_gather_rigids", hipLaunchKernelGGL(k_gather_rigids, dim3(wblk(nr, 128)), dim3(128), 0, s, nr, d.coupleBody, rd->bodies, rd->verts, d.rig));
+                LPE_KERNEL(ctx, "k_gather_rigids", k_gather_rigids, dim3(wblk(nr, 128)), dim3(128), 0, s, nr, d.coupleBody, rd->bodies, rd->verts, d.rig);
                 d.nr = nr;
                 d.rig_dirty = true;
             }
             int st = lpe_sph_step(ctx, dt_fluid);
             if (st) return st;
             if (nr > 0)
-                LPE_TIMED(ctx, "k_scatter_rigid_vel", hipLaunchKernelGGL(k_scatter_rigid_vel, dim3(wblk(nr, 128)), dim3(128), 0, s, nr, d.coupleBody, d.rig, rd->bodies));
+                LPE_KERNEL(ctx, "k_scatter_rigid_vel", k_scatter_rigid_vel, dim3(wblk(nr, 128)), dim3(128), 0, s, nr, d.coupleBody, d.rig, rd->bodies);
         }
         // 2) BoundarySystem, 3) BasicGravitySystem: bodies and fluid
         // (the planetary-mass check spans bodies and fluid, gravity.cpp:43-51)
         int st = lpe_rigid_integrate(ctx, 1 | 32, dt_state, dt_move);
         if (st) return st;
         if (d.n > 0) {
-            LPE_TIMED(ctx, "k_fluid_boundary_gravity", hipLaunchKernelGGL(k_fluid_boundary_gravity, dim3(wblk(d.n)), dim3(256), 0, s, d.n, d.P, rc.marginPixels * rc.metersPerPixel, rc.universeSize, rc.bounceDamping, rc.maxSpeed, rc.gravity, dt_state, rd->nb > 0 ? rd->counts + 5 : (const int32_t *)nullptr, d.fluid_heavy ? 1 : 0));
+            LPE_KERNEL(ctx, "k_fluid_boundary_gravity", k_fluid_boundary_gravity, dim3(wblk(d.n)), dim3(256), 0, s, d.n, d.P, rc.marginPixels * rc.metersPerPixel, rc.universeSize, rc.bounceDamping, rc.maxSpeed, rc.gravity, dt_state, rd->nb > 0 ? rd->counts + 5 : (const int32_t *)nullptr, d.fluid_heavy ? 1 : 0);
         }
         st = lpe_rigid_integrate(ctx, 2, dt_state, dt_move);
         if (st) return st;

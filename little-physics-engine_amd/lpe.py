@@ -249,8 +249,9 @@ class Context:
         self._chk(lib().lpe_sync(self._h), "lpe_sync")
 
     # ---- kernel timing -------------------------------------------------
-    def timing(self, on: bool = True):
-        self._chk(lib().lpe_timing_enable(self._h, 1 if on else 0), "lpe_timing_enable")
+    def timing(self, on=True):
+        """on: False/0 off, True/1 every kernel, 2 the dominant kernels only."""
+        self._chk(lib().lpe_timing_enable(self._h, int(on)), "lpe_timing_enable")
 
     def timing_reset(self):
         self._chk(lib().lpe_timing_reset(self._h), "lpe_timing_reset")
