@@ -501,7 +501,8 @@ __global__ void k_pgs_rows(const int32_t *__restrict__ ncptr, const int32_t *__r
                            const lpe_contact *__restrict__ cs, const lpe_body *__restrict__ bodies,
                            const float *__restrict__ imii, float4 *__restrict__ rowN,
                            float4 *__restrict__ rowR, int2 *__restrict__ rowAB,
-                           int32_t *__restrict__ sItemA, int32_t *__restrict__ sItemB) {
+                           float4 *__restrict__ rowM, int32_t *__restrict__ sItemA,
+                           int32_t *__restrict__ sItemB) {
     int t = blockIdx.x * RTPB + threadIdx.x;
     if (t >= *ncptr) return;
     const lpe_contact c = cs[order ? order[t] : t];
@@ -530,12 +531,27 @@ __global__ void k_pgs_rows(const int32_t *__restrict__ ncptr, const int32_t *__r
     rowN[t] = make_float4(dirX, dirY, effN, effF);
     rowR[t] = make_float4(rxA, ryA, rxB, ryB);
     rowAB[t] = make_int2(a, b);
+    rowM[t] = make_float4(imA, iiA, imB, iiB);
     sItemA[t] = a;
     sItemB[t] = b;
 }
 
 // ---------------------------------------------------------------------------
-// level scheduling of a sequential sweep (items touching bodies sItemA/B)
+// Exact sequential Gauss-Seidel on the device, by dataflow.
+//
+// A sweep visits items (PGS contacts / position-solver contacts) in a fixed
+// order; an item reads and writes the state of at most two movable bodies.
+// The sequential result is reproduced exactly when every body sees its items
+// in sweep order, sweep after sweep.  Each body carries a version counter (in
+// LDS) = the number of its items already applied; item t of sweep `it` may
+// run once its bodies' counters reach it * cnt + rank (cnt = items of the
+// body, rank = items of the body before t).  No level schedule, no barrier:
+// items run as soon as their inputs are final, and sweeps overlap.
+//
+// Work split: thread j owns items j, j + 1024, ... of every sweep and runs
+// them in (sweep, item) order.  Every thread's queue is a subsequence of the
+// global sequential order, so the earliest unfinished item is always at the
+// head of its queue with its inputs final: progress is guaranteed.
 __global__ void k_sched_count(const int32_t *__restrict__ kptr, const int32_t *__restrict__ ia,
                               const int32_t *__restrict__ ib, int32_t *__restrict__ bcount) {
     int t = blockIdx.x * RTPB + threadIdx.x;
@@ -551,115 +567,113 @@ __global__ void k_sched_fill(const int32_t *__restrict__ kptr, const int32_t *__
     if (ia[t] >= 0) ent[atomicAdd(&cursor[ia[t]], 1)] = t;
     if (ib[t] >= 0) ent[atomicAdd(&cursor[ib[t]], 1)] = t;
 }
-// per body segment: sort item ids ascending, then link prev pointers
-__global__ void k_sched_link(int nb, const int32_t *__restrict__ bstart, int32_t *__restrict__ ent,
-                             const int32_t *__restrict__ ia, int32_t *__restrict__ prevA,
-                             int32_t *__restrict__ prevB) {
-    int body = blockIdx.x * RTPB + threadIdx.x;
-    if (body >= nb) return;
-    int s = bstart[body], e = bstart[body + 1];
-    for (int k = s + 1; k < e; k++) {
-        int v = ent[k];
-        int j = k - 1;
-        while (j >= s && ent[j] > v) { ent[j + 1] = ent[j]; j--; }
-        ent[j + 1] = v;
-    }
-    for (int k = s; k < e; k++) {
-        int t = ent[k];
-        int p = (k > s) ? ent[k - 1] : -1;
-        if (ia[t] == body) prevA[t] = p; else prevB[t] = p;
-    }
-}
-// longest-chain level by monotone relaxation in one workgroup
-__global__ void __launch_bounds__(SOLVE_TPB)
-k_sched_levels(const int32_t *__restrict__ kptr, const int32_t *__restrict__ prevA,
-               const int32_t *__restrict__ prevB, int32_t *__restrict__ level,
-               int32_t *__restrict__ nlevels) {
-    __shared__ int changed, mx;
-    int K = *kptr;
-    for (int t = threadIdx.x; t < K; t += SOLVE_TPB) level[t] = 0;
-    __syncthreads();
-    while (true) {
-        if (threadIdx.x == 0) changed = 0;
-        __syncthreads();
-        int ch = 0;
-        for (int t = threadIdx.x; t < K; t += SOLVE_TPB) {
-            int pa = prevA[t], pb = prevB[t];
-            int L = 0;
-            if (pa >= 0) L = max(L, __hip_atomic_load(&level[pa], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) + 1);
-            if (pb >= 0) L = max(L, __hip_atomic_load(&level[pb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) + 1);
-            if (L > level[t]) {
-                __hip_atomic_store(&level[t], L, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                ch = 1;
-            }
-        }
-        if (ch) changed = 1;
-        __syncthreads();
-        if (!changed) break;
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) mx = -1;
-    __syncthreads();
-    int lm = -1;
-    for (int t = threadIdx.x; t < K; t += SOLVE_TPB) lm = max(lm, level[t]);
-    atomicMax(&mx, lm);
-    __syncthreads();
-    if (threadIdx.x == 0) *nlevels = mx + 1;
-}
-__global__ void k_level_count(const int32_t *__restrict__ kptr, const int32_t *__restrict__ level,
-                              int32_t *__restrict__ lcount) {
+// per item: (rank, cnt) on each of its bodies
+__global__ void k_sched_rank(const int32_t *__restrict__ kptr, const int32_t *__restrict__ ia,
+                             const int32_t *__restrict__ ib, const int32_t *__restrict__ bstart,
+                             const int32_t *__restrict__ ent, int4 *__restrict__ ver) {
     int t = blockIdx.x * RTPB + threadIdx.x;
     if (t >= *kptr) return;
-    atomicAdd(&lcount[level[t]], 1);
-}
-__global__ void k_level_fill(const int32_t *__restrict__ kptr, const int32_t *__restrict__ level,
-                             int32_t *__restrict__ lcursor, int32_t *__restrict__ lorder) {
-    int t = blockIdx.x * RTPB + threadIdx.x;
-    if (t >= *kptr) return;
-    lorder[atomicAdd(&lcursor[level[t]], 1)] = t;
+    int4 v = make_int4(0, 0, 0, 0);
+    int a = ia[t], b = ib[t];
+    if (a >= 0) {
+        int s0 = bstart[a], e0 = bstart[a + 1], r = 0;
+        for (int k = s0; k < e0; k++) r += ent[k] < t ? 1 : 0;
+        v.x = r; v.y = e0 - s0;
+    }
+    if (b >= 0) {
+        int s0 = bstart[b], e0 = bstart[b + 1], r = 0;
+        for (int k = s0; k < e0; k++) r += ent[k] < t ? 1 : 0;
+        v.z = r; v.w = e0 - s0;
+    }
+    ver[t] = v;
 }
 
-// ---------------------------------------------------------------------------
-// solveLcpPgs (:381-440) level by level; body velocities in LDS
+// a wave that sees no progress for this many passes gives up and raises
+// counts[7] (never expected: the schedule is deadlock free by construction)
+static constexpr unsigned FLOW_WATCHDOG = 1u << 24;
+
+__device__ __forceinline__ int ver_acquire(const int *p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void ver_release(int *p, int v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// solveLcpPgs (contact_solver.cpp:381-440): per contact the normal row then
+// the friction row (:449-543), applyImpulse (:315-356); body velocities in LDS.
+// A lane holds its current item and the next one of its queue in registers
+// (loaded one item ahead), so a pass never waits on a global load.
+struct PgsItem {
+    float4 rn, rr, rm;   // dir + eff, lever arms, inverse masses / inertias
+    int2 ab;             // bodies (-1 = static)
+    int4 rv;             // rank/cnt on A, rank/cnt on B
+};
 __global__ void __launch_bounds__(SOLVE_TPB)
-k_pgs_solve(int nb, const int32_t *__restrict__ nlevels, const int32_t *__restrict__ lstart,
-            const int32_t *__restrict__ lorder, const float4 *__restrict__ rowN,
-            const float4 *__restrict__ rowR, const int2 *__restrict__ rowAB,
-            const float *__restrict__ imii, float *__restrict__ vel, int iters, float mu,
-            float *__restrict__ lamN, float *__restrict__ lamF, const int32_t *__restrict__ ncptr) {
-    extern __shared__ float sv[];   // 3 floats per body
+k_pgs_flow(int nb, const int32_t *__restrict__ ncptr, const float4 *__restrict__ rowN,
+           const float4 *__restrict__ rowR, const int2 *__restrict__ rowAB,
+           const float4 *__restrict__ rowM, const int4 *__restrict__ rowV,
+           float *__restrict__ vel, int iters, float mu, float *__restrict__ lamN,
+           float *__restrict__ lamF, int32_t *__restrict__ fault) {
+    extern __shared__ float sv[];   // 3 floats per body, then one version counter per body
+    int *ver = (int *)(sv + 3 * nb);
     for (int i = threadIdx.x; i < 3 * nb; i += SOLVE_TPB) sv[i] = vel[i];
-    int K = *ncptr;
-    for (int t = threadIdx.x; t < K; t += SOLVE_TPB) { lamN[t] = 0.f; lamF[t] = 0.f; }
+    for (int i = threadIdx.x; i < nb; i += SOLVE_TPB) ver[i] = 0;
     __syncthreads();
-    const int L = *nlevels;
-    for (int it = 0; it < iters; it++) {
-        for (int l = 0; l < L; l++) {
-            int s = lstart[l], e = lstart[l + 1];
-            for (int q = s + threadIdx.x; q < e; q += SOLVE_TPB) {
-                int t = lorder[q];
-                float4 rn = rowN[t], rr = rowR[t];
-                int2 ab = rowAB[t];
-                float imA = 0.f, iiA = 0.f, imB = 0.f, iiB = 0.f;
-                if (ab.x >= 0) { imA = imii[2 * ab.x]; iiA = imii[2 * ab.x + 1]; }
-                if (ab.y >= 0) { imB = imii[2 * ab.y]; iiB = imii[2 * ab.y + 1]; }
-                // rows: normal (dir) then friction (-dirY, dirX)
+    const int K = *ncptr;
+    const int j = threadIdx.x;
+    const int R = (K > j) ? (K - j + SOLVE_TPB - 1) / SOLVE_TPB : 0;
+    const int total = iters * R;
+    auto load = [&](int tt) {
+        PgsItem q;
+        q.rn = rowN[tt]; q.rr = rowR[tt]; q.rm = rowM[tt]; q.ab = rowAB[tt]; q.rv = rowV[tt];
+        return q;
+    };
+    int done = 0, it = 0, r = 0, t = j;
+    PgsItem cur{}, nxt{};
+    cur.ab = make_int2(-1, -1);
+    float ln = 0.f, lf = 0.f, nln = 0.f, nlf = 0.f;
+    int nit = 0, nr = 0, nt = j;            // queue position of nxt (R > 1)
+    if (total > 0) cur = load(t);
+    if (R > 1) { nr = 1; nt = j + SOLVE_TPB; nxt = load(nt); }
+    // drain the preheader loads here: otherwise the wait for them lands at
+    // the loop top, where it would also wait out every later prefetch
+    __builtin_amdgcn_s_waitcnt(0);
+    unsigned idle = 0;   // watchdog: passes of this wave without progress
+    bool prog = false;
+    while (__any(done < total)) {
+        idle = __any(prog) ? 0u : idle + 1u;
+        prog = false;
+        if (idle > FLOW_WATCHDOG) {
+            if (threadIdx.x % 64 == 0) atomicOr(fault, 1);
+            break;
+        }
+        if (done < total) {
+            const int2 ab = cur.ab;
+            const int4 rv = cur.rv;
+            const int needA = it * rv.y + rv.x, needB = it * rv.w + rv.z;
+            bool ready = true;
+            if (ab.x >= 0) ready = ver_acquire(&ver[ab.x]) == needA;
+            if (ready && ab.y >= 0) ready = ver_acquire(&ver[ab.y]) == needB;
+            if (ready) {
+                const float4 rn = cur.rn, rr = cur.rr;
+                const float imA = cur.rm.x, iiA = cur.rm.y, imB = cur.rm.z, iiB = cur.rm.w;
+                float vxA = 0.f, vyA = 0.f, wA = 0.f, vxB = 0.f, vyB = 0.f, wB = 0.f;
+                if (ab.x >= 0) { vxA = sv[3 * ab.x]; vyA = sv[3 * ab.x + 1]; wA = sv[3 * ab.x + 2]; }
+                if (ab.y >= 0) { vxB = sv[3 * ab.y]; vyB = sv[3 * ab.y + 1]; wB = sv[3 * ab.y + 2]; }
+#pragma unroll
                 for (int row = 0; row < 2; row++) {
                     float dX = row == 0 ? rn.x : -rn.y;
                     float dY = row == 0 ? rn.y : rn.x;
                     float eff = row == 0 ? rn.z : rn.w;
-                    float vxA = 0.f, vyA = 0.f, wA = 0.f, vxB = 0.f, vyB = 0.f, wB = 0.f;
-                    if (ab.x >= 0) { vxA = sv[3 * ab.x]; vyA = sv[3 * ab.x + 1]; wA = sv[3 * ab.x + 2]; }
-                    if (ab.y >= 0) { vxB = sv[3 * ab.y]; vyB = sv[3 * ab.y + 1]; wB = sv[3 * ab.y + 2]; }
                     float ax = vxA - wA * rr.y, ay = vyA + wA * rr.x;
                     float bx = vxB - wB * rr.w, by = vyB + wB * rr.z;
                     float relX = bx - ax, relY = by - ay;
                     float vrel = relX * dX + relY * dY;
                     float old, lo, hi;
-                    if (row == 0) { old = lamN[t]; lo = 0.0f; hi = 1e20f; }
+                    if (row == 0) { old = ln; lo = 0.0f; hi = 1e20f; }
                     else {
-                        old = lamF[t];
-                        float limit = mu * lamN[t];
+                        old = lf;
+                        float limit = mu * ln;
                         lo = -limit; hi = limit;
                     }
                     float dl = -eff * (vrel + 0.0f);
@@ -667,25 +681,56 @@ k_pgs_solve(int nb, const int32_t *__restrict__ nlevels, const int32_t *__restri
                     if (nl < lo) nl = lo;
                     if (nl > hi) nl = hi;
                     dl = nl - old;
-                    if (row == 0) lamN[t] = nl; else lamF[t] = nl;
-                    if (fabsf(dl) < 1e-15F) continue;                // applyImpulse (:315-356)
+                    if (row == 0) ln = nl; else lf = nl;
+                    if (fabsf(dl) < 1e-15F) continue;
                     if (ab.x >= 0) {
-                        sv[3 * ab.x] -= dX * (dl * imA);
-                        sv[3 * ab.x + 1] -= dY * (dl * imA);
+                        vxA -= dX * (dl * imA);
+                        vyA -= dY * (dl * imA);
                         float crossA = rr.x * dY - rr.y * dX;
-                        sv[3 * ab.x + 2] -= crossA * dl * iiA;
+                        wA -= crossA * dl * iiA;
                     }
                     if (ab.y >= 0) {
-                        sv[3 * ab.y] += dX * (dl * imB);
-                        sv[3 * ab.y + 1] += dY * (dl * imB);
+                        vxB += dX * (dl * imB);
+                        vyB += dY * (dl * imB);
                         float crossB = rr.z * dY - rr.w * dX;
-                        sv[3 * ab.y + 2] += crossB * dl * iiB;
+                        wB += crossB * dl * iiB;
+                    }
+                }
+                if (ab.x >= 0) {
+                    sv[3 * ab.x] = vxA; sv[3 * ab.x + 1] = vyA; sv[3 * ab.x + 2] = wA;
+                    ver_release(&ver[ab.x], needA + 1);
+                }
+                if (ab.y >= 0) {
+                    sv[3 * ab.y] = vxB; sv[3 * ab.y + 1] = vyB; sv[3 * ab.y + 2] = wB;
+                    ver_release(&ver[ab.y], needB + 1);
+                }
+                done++;
+                prog = true;
+                if (R == 1) {
+                    it++;                       // same row next sweep: lambdas stay in registers
+                } else {
+                    // lane-private lambdas: park this row's; the next item's were
+                    // fetched one item ahead (stored >= 1 item before that fetch)
+                    lamN[t] = ln; lamF[t] = lf;
+                    cur = nxt; ln = nln; lf = nlf;
+                    it = nit; r = nr; t = nt;
+                    nr = r + 1; nit = it;
+                    if (nr == R) { nr = 0; nit++; }
+                    nt = j + nr * SOLVE_TPB;
+                    if (done + 1 < total) {
+                        nxt = load(nt);
+                        nln = nit > 0 ? lamN[nt] : 0.f;
+                        nlf = nit > 0 ? lamF[nt] : 0.f;
                     }
                 }
             }
-            __syncthreads();
         }
+        // every lane rejoins here each pass: keeps the compiler from turning
+        // the not-ready path into an inner loop that lanes which progressed
+        // would have to wait out (a SIMT deadlock)
+        __builtin_amdgcn_wave_barrier();
     }
+    __syncthreads();
     for (int i = threadIdx.x; i < 3 * nb; i += SOLVE_TPB) vel[i] = sv[i];
 }
 
@@ -734,16 +779,18 @@ __global__ void k_pos_items(const int32_t *__restrict__ ncptr, const lpe_contact
     const lpe_contact c = cs[k];
     keep[k] = (solid_body(bodies[c.a]) || solid_body(bodies[c.b])) ? 1 : 0;
 }
+// gatherPositionData (:67-120) for kept contact k -> item t (narrowphase
+// order), packed with everything of the item that does not change during
+// the solve (normal, correction, inverse masses, static skips)
 __global__ void k_pos_fill(const int32_t *__restrict__ ncptr, const int32_t *__restrict__ keep,
                            const int32_t *__restrict__ kstart, const lpe_contact *__restrict__ cs,
-                           const double *__restrict__ st, int32_t *__restrict__ item,
+                           const double *__restrict__ st, PosRec *__restrict__ rec,
                            int32_t *__restrict__ ia, int32_t *__restrict__ ib,
-                           int32_t *__restrict__ inPos) {
+                           int32_t *__restrict__ inPos, double baumgarte, double slop) {
     int k = blockIdx.x * RTPB + threadIdx.x;
     if (k >= *ncptr || !keep[k]) return;
     int t = kstart[k];
     const lpe_contact c = cs[k];
-    item[t] = k;
     auto movable = [&](int b) {
         return st[3 * b] != 0.0 || ((int)st[3 * b + 2] & 1);
     };
@@ -751,52 +798,122 @@ __global__ void k_pos_fill(const int32_t *__restrict__ ncptr, const int32_t *__r
     ib[t] = movable(c.b) ? c.b : -1;
     inPos[c.a] = 1;
     inPos[c.b] = 1;
+    int fa = (int)st[3 * c.a + 2], fb = (int)st[3 * c.b + 2];
+    PosRec q;
+    q.a = c.a; q.b = c.b;
+    int fl = 0;
+    if (!(fa & 2) || !(fb & 2)) fl |= 1;                       // solvePositionConstraint (:201-297)
+    if (!(fa & 4) && !(fb & 4)) fl |= 1;
+    double pen = c.pen - slop;
+    if (pen <= 0.0) fl |= 1;
+    if (fa & 1) fl |= 2;
+    if (fb & 1) fl |= 4;
+    D2 n = nrm(d2(c.nx, c.ny));
+    q.nx = n.x; q.ny = n.y;
+    q.corr = baumgarte * pen;
+    q.px = c.px; q.py = c.py;
+    q.invMA = st[3 * c.a]; q.invMB = st[3 * c.b];
+    q.invIA = st[3 * c.a + 1]; q.invIB = st[3 * c.b + 1];
+    q.flags = fl;
+    q.pad = 0;
+    rec[t] = q;
 }
+// PositionSolver::positionalSolver (:299-325) by dataflow; x, y, angle of
+// every body in LDS (fp64); item data double-buffered as in k_pgs_flow
+struct PosItem {
+    PosRec q;
+    int4 rv;
+    int da, db;          // movable dependency bodies (-1 none)
+};
 __global__ void __launch_bounds__(SOLVE_TPB)
-k_pos_solve(int nb, const int32_t *__restrict__ nlevels, const int32_t *__restrict__ lstart,
-            const int32_t *__restrict__ lorder, const int32_t *__restrict__ item,
-            const lpe_contact *__restrict__ cs, const double *__restrict__ st,
-            lpe_body *__restrict__ bodies, const int32_t *__restrict__ inPos, int iters,
-            double baumgarte, double slop) {
-    extern __shared__ double sp[];   // x, y, angle per body
+k_pos_flow(int nb, const int32_t *__restrict__ kptr, const PosRec *__restrict__ rec,
+           const int4 *__restrict__ rowV, const int32_t *__restrict__ ia,
+           const int32_t *__restrict__ ib, lpe_body *__restrict__ bodies,
+           const double *__restrict__ st, const int32_t *__restrict__ inPos, int iters,
+           int32_t *__restrict__ fault) {
+    extern __shared__ double sp[];   // x, y, angle per body, then one version counter per body
+    int *ver = (int *)(sp + 3 * nb);
     for (int i = threadIdx.x; i < nb; i += SOLVE_TPB) {
         const lpe_body &b = bodies[i];
         sp[3 * i] = b.x; sp[3 * i + 1] = b.y;
         sp[3 * i + 2] = (b.flags & LPE_BODY_HAS_ANGPOS) ? b.angle : 0.0;
+        ver[i] = 0;
     }
     __syncthreads();
-    const int L = *nlevels;
-    for (int it = 0; it < iters; it++) {
-        for (int l = 0; l < L; l++) {
-            int s = lstart[l], e = lstart[l + 1];
-            for (int q = s + threadIdx.x; q < e; q += SOLVE_TPB) {
-                const lpe_contact c = cs[item[lorder[q]]];
-                int fa = (int)st[3 * c.a + 2], fb = (int)st[3 * c.b + 2];
-                if (!(fa & 2) || !(fb & 2)) continue;
-                if (!(fa & 4) && !(fb & 4)) continue;
-                double pen = c.pen - slop;
-                if (pen <= 0.0) continue;
-                D2 n = nrm(d2(c.nx, c.ny));
-                double corr = baumgarte * pen;
-                double invMA = st[3 * c.a], invMB = st[3 * c.b];
-                double invIA = st[3 * c.a + 1], invIB = st[3 * c.b + 1];
-                D2 rA = d2(c.px - sp[3 * c.a], c.py - sp[3 * c.a + 1]);
-                D2 rB = d2(c.px - sp[3 * c.b], c.py - sp[3 * c.b + 1]);
-                double rAn = crs(rA, n), rBn = crs(rB, n);
-                double denom = invMA + invMB + (rAn * rAn) * invIA + (rBn * rBn) * invIB;
-                if (denom < 1e-12) continue;
-                double sc = corr / denom;
-                double dx = n.x * sc, dy = n.y * sc;
-                sp[3 * c.a] -= dx * invMA;
-                sp[3 * c.a + 1] -= dy * invMA;
-                if (fa & 1) sp[3 * c.a + 2] -= rAn * sc * invIA;
-                sp[3 * c.b] += dx * invMB;
-                sp[3 * c.b + 1] += dy * invMB;
-                if (fb & 1) sp[3 * c.b + 2] += rBn * sc * invIB;
-            }
-            __syncthreads();
+    const int K = *kptr;
+    const int j = threadIdx.x;
+    const int R = (K > j) ? (K - j + SOLVE_TPB - 1) / SOLVE_TPB : 0;
+    const int total = iters * R;
+    auto load = [&](int tt) {
+        PosItem p;
+        p.q = rec[tt]; p.rv = rowV[tt]; p.da = ia[tt]; p.db = ib[tt];
+        return p;
+    };
+    int done = 0, it = 0, r = 0;
+    PosItem cur{}, nxt{};
+    cur.da = cur.db = -1;
+    int nit = 0, nr = 0;
+    if (total > 0) cur = load(j);
+    if (R > 1) { nr = 1; nxt = load(j + SOLVE_TPB); }
+    __builtin_amdgcn_s_waitcnt(0);     // see k_pgs_flow
+    unsigned idle = 0;
+    bool prog = false;
+    while (__any(done < total)) {
+        idle = __any(prog) ? 0u : idle + 1u;
+        prog = false;
+        if (idle > FLOW_WATCHDOG) {
+            if (threadIdx.x % 64 == 0) atomicOr(fault, 1);
+            break;
         }
+        if (done < total) {
+            const int da = cur.da, db = cur.db;
+            const int needA = it * cur.rv.y + cur.rv.x, needB = it * cur.rv.w + cur.rv.z;
+            bool ready = true;
+            if (da >= 0) ready = ver_acquire(&ver[da]) == needA;
+            if (ready && db >= 0) ready = ver_acquire(&ver[db]) == needB;
+            if (ready) {
+                const PosRec &q = cur.q;
+                if (!(q.flags & 1)) {
+                    const int a = q.a, b = q.b;
+                    D2 rA = d2(q.px - sp[3 * a], q.py - sp[3 * a + 1]);
+                    D2 rB = d2(q.px - sp[3 * b], q.py - sp[3 * b + 1]);
+                    D2 n = d2(q.nx, q.ny);
+                    double rAn = crs(rA, n), rBn = crs(rB, n);
+                    double denom = q.invMA + q.invMB + (rAn * rAn) * q.invIA + (rBn * rBn) * q.invIB;
+                    if (!(denom < 1e-12)) {
+                        double sc = q.corr / denom;
+                        double dx = n.x * sc, dy = n.y * sc;
+                        // a body that cannot move (invM = 0, no rotation) is left
+                        // untouched: its update is x - 0
+                        if (da >= 0) {
+                            sp[3 * a] -= dx * q.invMA;
+                            sp[3 * a + 1] -= dy * q.invMA;
+                            if (q.flags & 2) sp[3 * a + 2] -= rAn * sc * q.invIA;
+                        }
+                        if (db >= 0) {
+                            sp[3 * b] += dx * q.invMB;
+                            sp[3 * b + 1] += dy * q.invMB;
+                            if (q.flags & 4) sp[3 * b + 2] += rBn * sc * q.invIB;
+                        }
+                    }
+                }
+                if (da >= 0) ver_release(&ver[da], needA + 1);
+                if (db >= 0) ver_release(&ver[db], needB + 1);
+                done++;
+                prog = true;
+                if (R == 1) {
+                    it++;
+                } else {
+                    cur = nxt; it = nit; r = nr;
+                    nr = r + 1; nit = it;
+                    if (nr == R) { nr = 0; nit++; }
+                    if (done + 1 < total) nxt = load(j + nr * SOLVE_TPB);
+                }
+            }
+        }
+        __builtin_amdgcn_wave_barrier();   // reconvergence point (see k_pgs_flow)
     }
+    __syncthreads();
     // storeBodyData (:176-197)
     for (int i = threadIdx.x; i < nb; i += SOLVE_TPB) {
         if (!inPos[i]) continue;
@@ -924,9 +1041,9 @@ int lpe_rigid_destroy_internal(lpe_ctx *ctx) {
     void *ptrs[] = {d->bodies, d->verts, d->rank, d->byRank, d->aabb, d->cand, d->pcount, d->pstart,
                     d->pcursor, d->pairs, d->pairRankB, d->cslots, d->ccount, d->cstart, d->contacts,
                     d->bsum, d->order, d->rowN, d->rowR, d->rowAB, d->vel0, d->imii, d->inContact,
-                    d->posState, d->posAB, d->posItem, d->sItemA, d->sItemB, d->sPrevA, d->sPrevB,
-                    d->sLevel, d->sBCount, d->sBStart, d->sBCursor, d->sEnt, d->sSorted, d->sLCount,
-                    d->sLStart, d->sLCursor, d->sLOrder, d->counts};
+                    d->posState, d->posRec, d->posKeep, d->posStart, d->rowM, d->sItemA, d->sItemB,
+                    d->sVer, d->lamN, d->lamF, d->sBCount, d->sBStart, d->sBCursor, d->sEnt,
+                    d->counts};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     delete d;
     ctx->rigid = nullptr;
@@ -972,7 +1089,10 @@ static int rigid_alloc_bodies(lpe_ctx *ctx, RigidDev *d, int nb) {
     if ((st = rgrow(ctx, &d->sBCount, N))) return st;
     if ((st = rgrow(ctx, &d->sBStart, N + 1))) return st;
     if ((st = rgrow(ctx, &d->sBCursor, N))) return st;
-    if (!d->counts && (st = rgrow(ctx, &d->counts, 16))) return st;
+    if (!d->counts) {
+        if ((st = rgrow(ctx, &d->counts, 16))) return st;
+        LPE_HIP(ctx, hipMemsetAsync(d->counts, 0, sizeof(int32_t) * 16, ctx->stream));
+    }
     d->cap_nb = nb;
     return LPE_OK;
 }
@@ -999,15 +1119,15 @@ static int rigid_alloc_contacts(lpe_ctx *ctx, RigidDev *d, int cap) {
     if ((st = rgrow(ctx, &d->rowN, K))) return st;
     if ((st = rgrow(ctx, &d->rowR, K))) return st;
     if ((st = rgrow(ctx, &d->rowAB, K))) return st;
-    if ((st = rgrow(ctx, &d->posItem, K))) return st;
-    if ((st = rgrow(ctx, &d->posAB, K))) return st;
-    int32_t **arrs[] = {&d->sItemA, &d->sItemB, &d->sPrevA, &d->sPrevB, &d->sLevel, &d->sSorted,
-                        &d->sLOrder};
+    if ((st = rgrow(ctx, &d->rowM, K))) return st;
+    if ((st = rgrow(ctx, &d->posRec, K))) return st;
+    if ((st = rgrow(ctx, &d->sVer, K))) return st;
+    if ((st = rgrow(ctx, &d->lamN, K))) return st;
+    if ((st = rgrow(ctx, &d->lamF, K))) return st;
+    int32_t **arrs[] = {&d->sItemA, &d->sItemB, &d->posKeep};
     for (int32_t **a : arrs) if ((st = rgrow(ctx, a, K))) return st;
+    if ((st = rgrow(ctx, &d->posStart, K + 1))) return st;
     if ((st = rgrow(ctx, &d->sEnt, 2 * K))) return st;
-    if ((st = rgrow(ctx, &d->sLCount, K + 1))) return st;
-    if ((st = rgrow(ctx, &d->sLStart, K + 2))) return st;
-    if ((st = rgrow(ctx, &d->sLCursor, K + 1))) return st;
     d->cap_contacts = cap;
     return LPE_OK;
 }
@@ -1044,8 +1164,8 @@ extern "C" int lpe_rigid_upload(lpe_ctx *ctx, int nb, const lpe_body *bodies, in
     if (!d->cfg_set) { lpe_rigid_config_default(&d->cfg); d->cfg_set = true; }
     static bool lds_attr = false;
     if (!lds_attr) {
-        (void)hipFuncSetAttribute((const void *)k_pgs_solve, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void *)k_pos_solve, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k_pgs_flow, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k_pos_flow, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         lds_attr = true;
     }
     int st = rigid_alloc_bodies(ctx, d, std::max(nb, 1));
@@ -1087,27 +1207,18 @@ extern "C" int lpe_rigid_upload(lpe_ctx *ctx, int nb, const lpe_body *bodies, in
     return LPE_OK;
 }
 
-// schedule items [0, K) (device count kptr, host bound kcap) whose dependency
-// bodies are sItemA/sItemB; result: levels count in *nlev, lstart/lorder
-static int rigid_schedule(lpe_ctx *ctx, RigidDev *d, const int32_t *kptr, int kcap,
-                          int32_t *nlev) {
+// per-item (rank, cnt) on the dependency bodies sItemA/sItemB of items
+// [0, K) (device count kptr, host bound kcap) -> sVer
+static int rigid_versions(lpe_ctx *ctx, RigidDev *d, const int32_t *kptr, int kcap) {
     hipStream_t s = ctx->stream;
     int nb = d->nb;
     LPE_HIP(ctx, hipMemsetAsync(d->sBCount, 0, sizeof(int32_t) * nb, s));
-    LPE_HIP(ctx, hipMemsetAsync(d->sPrevA, 0xFF, sizeof(int32_t) * kcap, s));
-    LPE_HIP(ctx, hipMemsetAsync(d->sPrevB, 0xFF, sizeof(int32_t) * kcap, s));
     LPE_KERNEL(ctx, "k_sched_count", k_sched_count, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sItemA, d->sItemB, d->sBCount);
     int st = rscan(ctx, d, nullptr, nb, d->sBCount, d->sBStart, d->sBCursor);
     if (st) return st;
     LPE_KERNEL(ctx, "k_sched_fill", k_sched_fill, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sItemA, d->sItemB, d->sBCursor, d->sEnt);
-    LPE_KERNEL(ctx, "k_sched_link", k_sched_link, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->sBStart, d->sEnt, d->sItemA, d->sPrevA, d->sPrevB);
-    LPE_KERNEL(ctx, "k_sched_levels", k_sched_levels, dim3(1), dim3(SOLVE_TPB), 0, s, kptr, d->sPrevA, d->sPrevB, d->sLevel, nlev);
-    LPE_HIP(ctx, hipMemsetAsync(d->sLCount, 0, sizeof(int32_t) * (kcap + 1), s));
-    LPE_KERNEL(ctx, "k_level_count", k_level_count, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sLevel, d->sLCount);
-    st = rscan(ctx, d, nlev, kcap + 1, d->sLCount, d->sLStart, d->sLCursor);
-    if (st) return st;
-    LPE_KERNEL(ctx, "k_level_fill", k_level_fill, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sLevel, d->sLCursor, d->sLOrder);
-    LPE_CHECK_LAUNCH(ctx, "schedule");
+    LPE_KERNEL(ctx, "k_sched_rank", k_sched_rank, dim3(rblk(kcap)), dim3(RTPB), 0, s, kptr, d->sItemA, d->sItemB, d->sBStart, d->sEnt, d->sVer);
+    LPE_CHECK_LAUNCH(ctx, "versions");
     return LPE_OK;
 }
 
@@ -1118,7 +1229,7 @@ static int rigid_detect(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pai
     const lpe_rigid_config &c = d->cfg;
     int nb = d->nb;
     for (int attempt = 0; attempt < 4; attempt++) {
-        LPE_HIP(ctx, hipMemsetAsync(d->counts, 0, sizeof(int32_t) * 16, s));
+        LPE_HIP(ctx, hipMemsetAsync(d->counts, 0, sizeof(int32_t) * 7, s));   // [7]: solver fault, sticky
         if (pairs_in) {
             if (np_in > d->cap_pairs) {
                 int st = rigid_alloc_pairs(ctx, d, np_in + 1024);
@@ -1147,6 +1258,10 @@ static int rigid_detect(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pai
         int32_t ncv = 0;
         LPE_HIP(ctx, hipStreamSynchronize(s));
         int np = hc[0];
+        if (hc[7]) {
+            ctx->err = "rigid solver watchdog fired (a dataflow solve made no progress)";
+            return LPE_ERR_OVERFLOW;
+        }
         if (hc[6] || np > d->cap_pairs) {   // pair buffer overflow: grow and redo
             st = rigid_alloc_pairs(ctx, d, std::max(2 * d->cap_pairs, np + 1024));
             if (st) return st;
@@ -1173,8 +1288,8 @@ static int rigid_solve(lpe_ctx *ctx, RigidDev *d, const int32_t *pgs_order, lpe_
     const lpe_rigid_config &c = d->cfg;
     int nb = d->nb, nc = d->last_nc;
     if (nc == 0) return LPE_OK;    // early out (rigid_body_collision.cpp:35-37)
-    if ((size_t)nb * 3 * sizeof(double) > 160 * 1024) {
-        ctx->err = "rigid solver: too many bodies for the LDS-resident solve (max 6826)";
+    if ((size_t)nb * (3 * sizeof(double) + sizeof(int)) > 160 * 1024) {
+        ctx->err = "rigid solver: too many bodies for the LDS-resident solve (max 5851)";
         return LPE_ERR_CAPACITY;
     }
     if (pgs_order)
@@ -1183,36 +1298,34 @@ static int rigid_solve(lpe_ctx *ctx, RigidDev *d, const int32_t *pgs_order, lpe_
     LPE_HIP(ctx, hipMemsetAsync(d->inContact, 0, sizeof(int32_t) * 2 * nb, s));
     LPE_KERNEL(ctx, "k_mark_contacts", k_mark_contacts, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->contacts, d->inContact);
     LPE_KERNEL(ctx, "k_pgs_bodies", k_pgs_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->imii);
-    LPE_KERNEL(ctx, "k_pgs_rows", k_pgs_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, pgs_order ? d->order : (const int32_t *)nullptr, d->contacts, d->bodies, d->imii, d->rowN, d->rowR, d->rowAB, d->sItemA, d->sItemB);
-    int st = rigid_schedule(ctx, d, d->counts + 1, nc, d->counts + 2);
+    LPE_KERNEL(ctx, "k_pgs_rows", k_pgs_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, pgs_order ? d->order : (const int32_t *)nullptr, d->contacts, d->bodies, d->imii, d->rowN, d->rowR, d->rowAB, d->rowM, d->sItemA, d->sItemB);
+    int st = rigid_versions(ctx, d, d->counts + 1, nc);
     if (st) return st;
-    // lambdas live in sPrevA/sPrevB (reinterpreted) after scheduling
-    float *lamN = (float *)d->sPrevA, *lamF = (float *)d->sPrevB;
-    size_t lds = sizeof(float) * 3 * (size_t)nb;
-    LPE_KERNEL(ctx, "k_pgs_solve", k_pgs_solve, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts + 2, d->sLStart, d->sLOrder, d->rowN, d->rowR, d->rowAB, d->imii, d->vel0, c.pgsIterations, c.frictionCoeff, lamN, lamF, d->counts + 1);
+    size_t lds = (sizeof(float) * 3 + sizeof(int)) * (size_t)nb;
+    LPE_KERNEL(ctx, "k_pgs_flow", k_pgs_flow, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts + 1, d->rowN, d->rowR, d->rowAB, d->rowM, d->sVer, d->vel0, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF, d->counts + 7);
     LPE_KERNEL(ctx, "k_pgs_writeback", k_pgs_writeback, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->inContact);
     LPE_CHECK_LAUNCH(ctx, "pgs");
     // ---- position solver (narrowphase order)
     int32_t *inPos = d->inContact + nb;
-    int32_t *keep = d->sLCount, *kstart = d->sLStart;   // reuse after PGS
+    int32_t *keep = d->posKeep, *kstart = d->posStart;
     LPE_KERNEL(ctx, "k_pos_bodies", k_pos_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->posState);
     LPE_KERNEL(ctx, "k_pos_items", k_pos_items, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->contacts, d->bodies, d->posState, keep);
     st = rscan(ctx, d, d->counts + 1, nc, keep, kstart, nullptr);
     if (st) return st;
     // kept-contact count -> counts[4]
     LPE_HIP(ctx, hipMemcpyAsync(d->counts + 4, kstart + nc, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
-    LPE_KERNEL(ctx, "k_pos_fill", k_pos_fill, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, keep, kstart, d->contacts, d->posState, d->posItem, d->sItemA, d->sItemB, inPos);
-    st = rigid_schedule(ctx, d, d->counts + 4, nc, d->counts + 3);
+    LPE_KERNEL(ctx, "k_pos_fill", k_pos_fill, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, keep, kstart, d->contacts, d->posState, d->posRec, d->sItemA, d->sItemB, inPos, c.baumgarte, c.slop);
+    st = rigid_versions(ctx, d, d->counts + 4, nc);
     if (st) return st;
-    size_t lds2 = sizeof(double) * 3 * (size_t)nb;
-    LPE_KERNEL(ctx, "k_pos_solve", k_pos_solve, dim3(1), dim3(SOLVE_TPB), lds2, s, nb, d->counts + 3, d->sLStart, d->sLOrder, d->posItem, d->contacts, d->posState, d->bodies, inPos, c.posIterations, c.baumgarte, c.slop);
+    size_t lds2 = (sizeof(double) * 3 + sizeof(int)) * (size_t)nb;
+    LPE_KERNEL(ctx, "k_pos_flow", k_pos_flow, dim3(1), dim3(SOLVE_TPB), lds2, s, nb, d->counts + 4, d->posRec, d->sVer, d->sItemA, d->sItemB, d->bodies, d->posState, inPos, c.posIterations, d->counts + 7);
     LPE_CHECK_LAUNCH(ctx, "position solver");
     if (stats) {
         int32_t hc[8];
         LPE_HIP(ctx, hipMemcpyAsync(hc, d->counts, sizeof(int32_t) * 8, hipMemcpyDeviceToHost, s));
         LPE_HIP(ctx, hipStreamSynchronize(s));
-        stats->pgsLevels = hc[2];
-        stats->posLevels = hc[3];
+        stats->pgsLevels = 0;     // dataflow solve: no level schedule
+        stats->posLevels = 0;
     }
     return LPE_OK;
 }
@@ -1275,7 +1388,14 @@ extern "C" int lpe_rigid_download(lpe_ctx *ctx, lpe_body *bodies) {
     RigidDev *d = rdev(ctx);
     if (d->nb > 0)
         LPE_HIP(ctx, hipMemcpyAsync(bodies, d->bodies, sizeof(lpe_body) * d->nb, hipMemcpyDeviceToHost, ctx->stream));
+    int32_t fault = 0;
+    if (d->counts)
+        LPE_HIP(ctx, hipMemcpyAsync(&fault, d->counts + 7, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
     LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (fault) {
+        ctx->err = "rigid solver watchdog fired (a dataflow solve made no progress)";
+        return LPE_ERR_OVERFLOW;
+    }
     return LPE_OK;
 }
 

@@ -12,6 +12,15 @@ static constexpr int CLIP_MAX = 40;    // clip output <= nB + 3
 static constexpr int MAXV = 32;        // polygon vertex cap of the device narrowphase
 static constexpr int SOLVE_TPB = 1024;
 
+// one position-solver item, packed (the fields of solvePositionConstraint,
+// position_solver.cpp:201-297, that do not change during the solve)
+struct PosRec {
+    double nx, ny, corr, px, py, invMA, invMB, invIA, invIB;
+    int32_t a, b;
+    int32_t flags;       // 1 skipped, 2 A rotates, 4 B rotates
+    int32_t pad;
+};
+
 struct RigidDev {
     int nb = 0, cap_nb = 0;
     lpe_body *bodies = nullptr;
@@ -41,15 +50,16 @@ struct RigidDev {
     float *vel0 = nullptr;                    // float3 per body (PGS load)
     float *imii = nullptr;                    // float2 per body (invMass, invInertia)
     int32_t *inContact = nullptr;             // per body flags
-    double *posState = nullptr;               // per body: invM, invI (pos solver)
-    int2 *posAB = nullptr;
-    int32_t *posItem = nullptr;               // kept contact index per pos item
-    // scheduling (shared by both solvers)
-    int32_t *sItemA = nullptr, *sItemB = nullptr, *sPrevA = nullptr, *sPrevB = nullptr;
-    int32_t *sLevel = nullptr, *sBCount = nullptr, *sBStart = nullptr, *sBCursor = nullptr;
-    int32_t *sEnt = nullptr, *sSorted = nullptr, *sLCount = nullptr, *sLStart = nullptr,
-            *sLCursor = nullptr, *sLOrder = nullptr;
-    int32_t *counts = nullptr;                // [0]=np [1]=nc [2]=pgs levels [3]=pos levels [4]=npos [5]=heavy
+    float4 *rowM = nullptr;                   // imA, iiA, imB, iiB
+    float *lamN = nullptr, *lamF = nullptr;   // accumulated impulses per contact
+    double *posState = nullptr;               // per body: invM, invI, flags (pos solver)
+    PosRec *posRec = nullptr;                 // position-solver items
+    int32_t *posKeep = nullptr, *posStart = nullptr;
+    // dataflow versions (shared by both solvers)
+    int32_t *sItemA = nullptr, *sItemB = nullptr;    // dependency bodies per item (-1 none)
+    int4 *sVer = nullptr;                            // rank/cnt on A, rank/cnt on B
+    int32_t *sBCount = nullptr, *sBStart = nullptr, *sBCursor = nullptr, *sEnt = nullptr;
+    int32_t *counts = nullptr;                // [0]=np [1]=nc [4]=npos [5]=heavy [6]=pair overflow
     lpe_rigid_config cfg{};
     bool cfg_set = false;
     int last_np = 0, last_nc = 0;
