@@ -41,10 +41,34 @@ build/oracle/%.opp: oracle/%.cpp oracle/*.h include/lpe.h
 $(ORACLE): $(patsubst oracle/%.c,build/oracle/%.o,$(ORC_SRC)) $(patsubst oracle/%.cpp,build/oracle/%.opp,$(ORX_SRC))
 	$(CXX) -shared -fPIC -o $@ $^ -lm
 
-ref:
+# C++ host mirror of the reference's system plugins (Systems::FluidSystem,
+# RigidBodyCollisionSystem, the integrator systems) over the C ABI.  It is the
+# drop-in for src/systems/, so it compiles against the reference's own headers
+# (components, ISystem, EnTT): built only where /root/reference exists; the
+# .so travels to the GPU box with the tree.
+REF      ?= /root/reference
+HOSTDIR  := $(PKG)/host
+HOST_SRC := $(HOSTDIR)/lpe_backend.cpp $(wildcard $(HOSTDIR)/src/systems/*.cpp) \
+            $(wildcard $(HOSTDIR)/src/systems/*/*.cpp)
+HOST_HDR := $(HOSTDIR)/lpe_backend.hpp $(wildcard $(HOSTDIR)/include/systems/*/*.hpp) include/lpe.h
+HOST_OBJ := $(patsubst $(HOSTDIR)/%.cpp,build/host/%.o,$(HOST_SRC))
+HOSTLIB  := $(HOSTDIR)/liblpe_systems.so
+HOSTFLAGS := -std=c++17 -O2 -fPIC -ffp-contract=off -Wall -Wno-unused-variable -include algorithm \
+            -I$(HOSTDIR)/include -I$(HOSTDIR) -Iinclude -I$(REF)/include -I$(REF)/vendor/entt/include
+
+build/host/%.o: $(HOSTDIR)/%.cpp $(HOST_HDR)
+	@mkdir -p $(dir $@)
+	$(CXX) $(HOSTFLAGS) -c $< -o $@
+
+$(HOSTLIB): $(HOST_OBJ) $(LIB)
+	$(CXX) -shared -fPIC -o $@ $(HOST_OBJ) -L$(PKG) -llpe_hip -Wl,-rpath,'$$ORIGIN/..' -Wl,-rpath,/opt/rocm/lib
+
+host: $(HOSTLIB)
+
+ref: host
 	$(MAKE) -f oracle/Makefile.ref
 
 clean:
-	rm -rf build $(LIB) $(ORACLE) oracle/_ref
+	rm -rf build $(LIB) $(ORACLE) $(HOSTLIB) oracle/_ref
 
-.PHONY: all ref clean
+.PHONY: all ref host clean

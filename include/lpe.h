@@ -301,8 +301,15 @@ int  lpe_rigid_upload(lpe_ctx *ctx, int nb, const lpe_body *bodies, int nverts,
  * (eid_a, eid_b); GJK/EPA/clipping narrowphase in fp64
  * (narrowphase.cpp:352-420); PGS (contact_solver.cpp:449-543) and Baumgarte
  * position solver (position_solver.cpp:299-325) as exact sequential
- * Gauss-Seidel sweeps in that order, run level by level on the device. */
+ * Gauss-Seidel sweeps in the graph-coloured order: pairs edge-coloured so
+ * that one colour's pairs share no movable body, visited colour by colour,
+ * each pair's contacts in narrowphase order (the reference visits its
+ * unordered_map's order, contact_manager.cpp:169-245).  stats->pgsLevels and
+ * posLevels report the colour count. */
 int  lpe_rigid_step(lpe_ctx *ctx, lpe_rigid_stats *stats);
+/* Colour of each pair of the last lpe_rigid_step (-1: pair without contacts),
+ * for the parity harness; cap entries at most, *ncolours the colour count. */
+int  lpe_rigid_download_colours(lpe_ctx *ctx, int cap, int32_t *pair_colour, int32_t *ncolours);
 /* Same with caller-supplied orders (parity mode): `pairs` (np body-index
  * pairs) replaces the broadphase and fixes the narrowphase / position-solver
  * order; `pgs_order` (NULL = contact order) is the PGS contact visiting order,

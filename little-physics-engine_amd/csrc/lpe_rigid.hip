@@ -588,6 +588,223 @@ __global__ void k_sched_rank(const int32_t *__restrict__ kptr, const int32_t *__
     ver[t] = v;
 }
 
+// Canonical solver order (lpe_rigid_step): graph-coloured Gauss-Seidel
+// (SURVEY.md §7.1 step 7).  The contact pairs are edge-coloured so that no
+// two pairs of one colour share a movable body; the solvers then visit the
+// pairs colour by colour, each pair's contacts in narrowphase order.  The
+// reference's PGS order is an unordered_map's (contact_manager.cpp:169-245)
+// and its position-solver order the quadtree's pair order, so any such order
+// is a valid restatement; this one keeps the dependency depth of a sweep at
+// about (colours x contacts per pair) instead of the length of the longest
+// chain of contacts in entity-id order.  Pairs of one colour touch disjoint
+// movable bodies, so the order inside a colour does not change a single bit.
+//
+// Colouring (deterministic, restated by oracle/rigid_oracle.cpp
+// lpeo_colour_order): rounds; every uncoloured pair claims its movable
+// bodies with the priority (hash(p), p) -- the lowest wins a body; a pair that
+// wins all of them takes the lowest colour free on both and marks it used.
+// Hashed priorities keep the chains of "waits for a lower pair" short (pair
+// indices follow entity ids, i.e. space, so plain index priorities chain
+// across the pile).  One 1024-thread workgroup, per-body state in LDS.
+// Outputs: order (contact per row, colour-major, each pair's rows
+// contiguous), seg (row start, count) per coloured pair in colour-major pair
+// order, cbase (first seg of each colour; cbase[ncol] = coloured pairs).
+static constexpr int MAX_COLOURS = 64;
+__host__ __device__ __forceinline__ uint32_t colour_hash(uint32_t x) {
+    x ^= x >> 16; x *= 0x7feb352du;
+    x ^= x >> 15; x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+__device__ __forceinline__ bool colour_dep(const lpe_body &b) {
+    // a body the PGS writes (finite mass, contact_solver.cpp:70-98) or the
+    // position solver moves (invM != 0 or rotatable, position_solver.cpp:125-168)
+    bool inf = (b.flags & LPE_BODY_HAS_MASS) && b.mass > 1e29;
+    bool rot = (b.flags & LPE_BODY_HAS_INERTIA) && b.inertia > 1e-12 && b.inertia < 1e29;
+    return !inf || rot;
+}
+__global__ void __launch_bounds__(SOLVE_TPB)
+k_pair_colour(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict__ pairs,
+              const int32_t *__restrict__ ccount, const int32_t *__restrict__ cstart,
+              const lpe_body *__restrict__ bodies, int32_t *__restrict__ pcol,
+              int32_t *__restrict__ order, int2 *__restrict__ seg, int32_t *__restrict__ cbase,
+              int32_t *__restrict__ counts) {
+    extern __shared__ unsigned long long su[];              // colours used, per body
+    unsigned long long *claim = su + nb;                     // best claiming priority, per body
+    unsigned char *dep = (unsigned char *)(claim + nb);      // movable body
+    __shared__ int colCnt[MAX_COLOURS], colCur[MAX_COLOURS], colPairs[MAX_COLOURS], colPCur[MAX_COLOURS];
+    __shared__ int s_left, s_fault, s_ncol;
+    const unsigned long long NONE = ~0ull;
+    const int np = *npptr;
+    for (int i = threadIdx.x; i < nb; i += SOLVE_TPB) {
+        su[i] = 0ull;
+        claim[i] = NONE;
+        dep[i] = colour_dep(bodies[i]) ? 1 : 0;
+    }
+    if (threadIdx.x == 0) { s_fault = 0; s_ncol = 0; }
+    // -1: pair without contacts (no item); -2: uncoloured
+    for (int p = threadIdx.x; p < np; p += SOLVE_TPB) pcol[p] = ccount[p] > 0 ? -2 : -1;
+    __syncthreads();
+    for (int round = 0;; round++) {
+        if (threadIdx.x == 0) s_left = 0;
+        for (int p = threadIdx.x; p < np; p += SOLVE_TPB) {       // claims
+            if (pcol[p] != -2) continue;
+            int2 pr = pairs[p];
+            unsigned long long pri = ((unsigned long long)colour_hash((uint32_t)p) << 32) | (uint32_t)p;
+            if (dep[pr.x]) atomicMin(&claim[pr.x], pri);
+            if (dep[pr.y]) atomicMin(&claim[pr.y], pri);
+        }
+        __syncthreads();
+        for (int p = threadIdx.x; p < np; p += SOLVE_TPB) {       // winners pick a colour
+            if (pcol[p] != -2) continue;
+            int2 pr = pairs[p];
+            unsigned long long pri = ((unsigned long long)colour_hash((uint32_t)p) << 32) | (uint32_t)p;
+            int a = dep[pr.x] ? pr.x : -1, b = dep[pr.y] ? pr.y : -1;
+            if ((a < 0 || claim[a] == pri) && (b < 0 || claim[b] == pri)) {
+                unsigned long long forb = (a >= 0 ? su[a] : 0ull) | (b >= 0 ? su[b] : 0ull);
+                int c = __ffsll((long long)~forb) - 1;
+                if (c < 0 || c >= MAX_COLOURS) { s_fault = 1; c = 0; }
+                pcol[p] = -3 - c;                                  // coloured this round
+            } else {
+                s_left = 1;
+            }
+        }
+        __syncthreads();
+        for (int p = threadIdx.x; p < np; p += SOLVE_TPB) {       // commit, release claims
+            int v = pcol[p];
+            if (v == -1 || v >= 0) continue;
+            int2 pr = pairs[p];
+            if (v <= -3) {
+                int c = -3 - v;
+                pcol[p] = c;
+                if (dep[pr.x]) su[pr.x] |= 1ull << c;              // one winner per body
+                if (dep[pr.y]) su[pr.y] |= 1ull << c;
+            }
+            if (dep[pr.x]) claim[pr.x] = NONE;
+            if (dep[pr.y]) claim[pr.y] = NONE;
+        }
+        __syncthreads();
+        const bool more = s_left && !s_fault && round < (1 << 20);
+        __syncthreads();              // every thread has read s_left before it is reset
+        if (!more) break;
+    }
+    // colour-major order: rows and pairs per colour -> bases -> pairs placed whole
+    if (threadIdx.x < MAX_COLOURS) {
+        colCnt[threadIdx.x] = 0; colCur[threadIdx.x] = 0;
+        colPairs[threadIdx.x] = 0; colPCur[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < np; p += SOLVE_TPB) {
+        int c = pcol[p];
+        if (c >= 0) {
+            atomicAdd(&colCnt[c], ccount[p]);
+            atomicAdd(&colPairs[c], 1);
+            atomicMax(&s_ncol, c + 1);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0, pacc = 0;
+        for (int c = 0; c < MAX_COLOURS; c++) {
+            colCur[c] = acc; acc += colCnt[c];
+            colPCur[c] = pacc;
+            if (c <= s_ncol) cbase[c] = pacc;
+            pacc += colPairs[c];
+        }
+        cbase[s_ncol] = pacc;
+        counts[8] = s_ncol;
+        if (s_fault) counts[7] = 1;
+    }
+    __syncthreads();
+    for (int p = threadIdx.x; p < np; p += SOLVE_TPB) {
+        int c = pcol[p];
+        if (c < 0) continue;
+        int n = ccount[p], s0 = cstart[p];
+        int pos = atomicAdd(&colCur[c], n);
+        int q = atomicAdd(&colPCur[c], 1);
+        seg[q] = make_int2(pos, n);
+        for (int j = 0; j < n; j++) order[pos + j] = s0 + j;
+    }
+}
+
+// Colour-synchronous Gauss-Seidel sweeps (canonical order): for each colour,
+// every thread runs whole pairs of that colour (their rows in order), then a
+// barrier.  Equal bit for bit to the sequential sweep in colour-major order.
+// solveLcpPgs (contact_solver.cpp:381-440), rows of buildConstraintRows
+// (:133-197) in fp32, body velocities in LDS.
+__device__ __forceinline__ void pgs_row_pair(float4 rn, float4 rr, float4 rm, int2 ab, float mu,
+                                             float &ln, float &lf, float *sv) {
+    const float imA = rm.x, iiA = rm.y, imB = rm.z, iiB = rm.w;
+    float vxA = 0.f, vyA = 0.f, wA = 0.f, vxB = 0.f, vyB = 0.f, wB = 0.f;
+    if (ab.x >= 0) { vxA = sv[3 * ab.x]; vyA = sv[3 * ab.x + 1]; wA = sv[3 * ab.x + 2]; }
+    if (ab.y >= 0) { vxB = sv[3 * ab.y]; vyB = sv[3 * ab.y + 1]; wB = sv[3 * ab.y + 2]; }
+#pragma unroll
+    for (int row = 0; row < 2; row++) {
+        float dX = row == 0 ? rn.x : -rn.y;
+        float dY = row == 0 ? rn.y : rn.x;
+        float eff = row == 0 ? rn.z : rn.w;
+        float ax = vxA - wA * rr.y, ay = vyA + wA * rr.x;
+        float bx = vxB - wB * rr.w, by = vyB + wB * rr.z;
+        float relX = bx - ax, relY = by - ay;
+        float vrel = relX * dX + relY * dY;
+        float old, lo, hi;
+        if (row == 0) { old = ln; lo = 0.0f; hi = 1e20f; }
+        else {
+            old = lf;
+            float limit = mu * ln;
+            lo = -limit; hi = limit;
+        }
+        float dl = -eff * (vrel + 0.0f);
+        float nl = old + dl;
+        if (nl < lo) nl = lo;
+        if (nl > hi) nl = hi;
+        dl = nl - old;
+        if (row == 0) ln = nl; else lf = nl;
+        if (fabsf(dl) < 1e-15F) continue;
+        if (ab.x >= 0) {
+            vxA -= dX * (dl * imA);
+            vyA -= dY * (dl * imA);
+            float crossA = rr.x * dY - rr.y * dX;
+            wA -= crossA * dl * iiA;
+        }
+        if (ab.y >= 0) {
+            vxB += dX * (dl * imB);
+            vyB += dY * (dl * imB);
+            float crossB = rr.z * dY - rr.w * dX;
+            wB += crossB * dl * iiB;
+        }
+    }
+    if (ab.x >= 0) { sv[3 * ab.x] = vxA; sv[3 * ab.x + 1] = vyA; sv[3 * ab.x + 2] = wA; }
+    if (ab.y >= 0) { sv[3 * ab.y] = vxB; sv[3 * ab.y + 1] = vyB; sv[3 * ab.y + 2] = wB; }
+}
+
+__global__ void __launch_bounds__(SOLVE_TPB)
+k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restrict__ cbase,
+             const int2 *__restrict__ seg, const float4 *__restrict__ rowN,
+             const float4 *__restrict__ rowR, const int2 *__restrict__ rowAB,
+             const float4 *__restrict__ rowM, float *__restrict__ vel, int iters, float mu,
+             float *__restrict__ lamN, float *__restrict__ lamF) {
+    extern __shared__ float sv[];   // 3 floats per body
+    for (int i = threadIdx.x; i < 3 * nb; i += SOLVE_TPB) sv[i] = vel[i];
+    __syncthreads();
+    const int ncol = counts[8];
+    for (int it = 0; it < iters; it++) {
+        for (int c = 0; c < ncol; c++) {
+            const int q1 = cbase[c + 1];
+            for (int q = cbase[c] + threadIdx.x; q < q1; q += SOLVE_TPB) {
+                const int2 sg = seg[q];
+                for (int t = sg.x; t < sg.x + sg.y; t++) {
+                    float ln = it ? lamN[t] : 0.f, lf = it ? lamF[t] : 0.f;
+                    pgs_row_pair(rowN[t], rowR[t], rowM[t], rowAB[t], mu, ln, lf, sv);
+                    lamN[t] = ln; lamF[t] = lf;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = threadIdx.x; i < 3 * nb; i += SOLVE_TPB) vel[i] = sv[i];
+}
+
 // a wave that sees no progress for this many passes gives up and raises
 // counts[7] (never expected: the schedule is deadlock free by construction)
 static constexpr unsigned FLOW_WATCHDOG = 1u << 24;
@@ -771,26 +988,28 @@ __global__ void k_pos_bodies(int nb, const lpe_body *__restrict__ bodies, double
 }
 // gatherPositionData (:67-120): keep contacts with at least one Solid body;
 // a body is a dependency only if it can move (invM != 0 or canRotate)
-__global__ void k_pos_items(const int32_t *__restrict__ ncptr, const lpe_contact *__restrict__ cs,
-                            const lpe_body *__restrict__ bodies, const double *__restrict__ st,
-                            int32_t *__restrict__ keep) {
-    int k = blockIdx.x * RTPB + threadIdx.x;
-    if (k >= *ncptr) return;
-    const lpe_contact c = cs[k];
-    keep[k] = (solid_body(bodies[c.a]) || solid_body(bodies[c.b])) ? 1 : 0;
+// u = position in the solver order (order[u] = contact; NULL: narrowphase order)
+__global__ void k_pos_items(const int32_t *__restrict__ ncptr, const int32_t *__restrict__ order,
+                            const lpe_contact *__restrict__ cs, const lpe_body *__restrict__ bodies,
+                            const double *__restrict__ st, int32_t *__restrict__ keep) {
+    int u = blockIdx.x * RTPB + threadIdx.x;
+    if (u >= *ncptr) return;
+    const lpe_contact c = cs[order ? order[u] : u];
+    keep[u] = (solid_body(bodies[c.a]) || solid_body(bodies[c.b])) ? 1 : 0;
 }
-// gatherPositionData (:67-120) for kept contact k -> item t (narrowphase
-// order), packed with everything of the item that does not change during
+// gatherPositionData (:67-120) for the kept contact at order position u ->
+// item t, packed with everything of the item that does not change during
 // the solve (normal, correction, inverse masses, static skips)
-__global__ void k_pos_fill(const int32_t *__restrict__ ncptr, const int32_t *__restrict__ keep,
+__global__ void k_pos_fill(const int32_t *__restrict__ ncptr, const int32_t *__restrict__ order,
+                           const int32_t *__restrict__ keep,
                            const int32_t *__restrict__ kstart, const lpe_contact *__restrict__ cs,
                            const double *__restrict__ st, PosRec *__restrict__ rec,
                            int32_t *__restrict__ ia, int32_t *__restrict__ ib,
                            int32_t *__restrict__ inPos, double baumgarte, double slop) {
-    int k = blockIdx.x * RTPB + threadIdx.x;
-    if (k >= *ncptr || !keep[k]) return;
-    int t = kstart[k];
-    const lpe_contact c = cs[k];
+    int u = blockIdx.x * RTPB + threadIdx.x;
+    if (u >= *ncptr || !keep[u]) return;
+    int t = kstart[u];
+    const lpe_contact c = cs[order ? order[u] : u];
     auto movable = [&](int b) {
         return st[3 * b] != 0.0 || ((int)st[3 * b + 2] & 1);
     };
@@ -818,6 +1037,99 @@ __global__ void k_pos_fill(const int32_t *__restrict__ ncptr, const int32_t *__r
     q.pad = 0;
     rec[t] = q;
 }
+// Position solver, canonical order: every contact keeps its row position u
+// (non-kept contacts become skipped items), so the colour segments of the PGS
+// apply unchanged; colour-synchronous sweeps (see k_pgs_colour), body poses
+// in LDS (fp64).  solvePositionContactsOnce (position_solver.cpp:215-290).
+__global__ void k_pos_fill_rows(const int32_t *__restrict__ ncptr, const int32_t *__restrict__ order,
+                                const lpe_contact *__restrict__ cs, const lpe_body *__restrict__ bodies,
+                                const double *__restrict__ st, PosRec *__restrict__ rec,
+                                int32_t *__restrict__ inPos, double baumgarte, double slop) {
+    int u = blockIdx.x * RTPB + threadIdx.x;
+    if (u >= *ncptr) return;
+    const lpe_contact c = cs[order[u]];
+    const bool kept = solid_body(bodies[c.a]) || solid_body(bodies[c.b]);   // gatherPositionData (:67-120)
+    int fa = (int)st[3 * c.a + 2], fb = (int)st[3 * c.b + 2];
+    PosRec q;
+    q.a = c.a; q.b = c.b;
+    int fl = kept ? 0 : 1;
+    if (kept) { inPos[c.a] = 1; inPos[c.b] = 1; }
+    if (!(fa & 2) || !(fb & 2)) fl |= 1;
+    if (!(fa & 4) && !(fb & 4)) fl |= 1;
+    double pen = c.pen - slop;
+    if (pen <= 0.0) fl |= 1;
+    if (fa & 1) fl |= 2;
+    if (fb & 1) fl |= 4;
+    D2 n = nrm(d2(c.nx, c.ny));
+    q.nx = n.x; q.ny = n.y;
+    q.corr = baumgarte * pen;
+    q.px = c.px; q.py = c.py;
+    q.invMA = st[3 * c.a]; q.invMB = st[3 * c.b];
+    q.invIA = st[3 * c.a + 1]; q.invIB = st[3 * c.b + 1];
+    q.flags = fl;
+    q.pad = 0;
+    rec[u] = q;
+}
+
+__device__ __forceinline__ void pos_item(const PosRec &q, double *sp) {
+    if (q.flags & 1) return;
+    const int a = q.a, b = q.b;
+    D2 rA = d2(q.px - sp[3 * a], q.py - sp[3 * a + 1]);
+    D2 rB = d2(q.px - sp[3 * b], q.py - sp[3 * b + 1]);
+    D2 n = d2(q.nx, q.ny);
+    double rAn = crs(rA, n), rBn = crs(rB, n);
+    double denom = q.invMA + q.invMB + (rAn * rAn) * q.invIA + (rBn * rBn) * q.invIB;
+    if (denom < 1e-12) return;
+    double sc = q.corr / denom;
+    double dx = n.x * sc, dy = n.y * sc;
+    // an immovable body (invM = 0, no rotation) would get x - 0: skipped, so
+    // pairs of one colour never write a shared static body
+    if (q.invMA != 0.0 || (q.flags & 2)) {
+        sp[3 * a] -= dx * q.invMA;
+        sp[3 * a + 1] -= dy * q.invMA;
+        if (q.flags & 2) sp[3 * a + 2] -= rAn * sc * q.invIA;
+    }
+    if (q.invMB != 0.0 || (q.flags & 4)) {
+        sp[3 * b] += dx * q.invMB;
+        sp[3 * b + 1] += dy * q.invMB;
+        if (q.flags & 4) sp[3 * b + 2] += rBn * sc * q.invIB;
+    }
+}
+
+__global__ void __launch_bounds__(SOLVE_TPB)
+k_pos_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restrict__ cbase,
+             const int2 *__restrict__ seg, const PosRec *__restrict__ rec,
+             lpe_body *__restrict__ bodies, const double *__restrict__ st,
+             const int32_t *__restrict__ inPos, int iters) {
+    extern __shared__ double sp[];   // x, y, angle per body
+    for (int i = threadIdx.x; i < nb; i += SOLVE_TPB) {
+        const lpe_body &b = bodies[i];
+        sp[3 * i] = b.x; sp[3 * i + 1] = b.y;
+        sp[3 * i + 2] = (b.flags & LPE_BODY_HAS_ANGPOS) ? b.angle : 0.0;
+    }
+    __syncthreads();
+    const int ncol = counts[8];
+    for (int it = 0; it < iters; it++) {
+        for (int c = 0; c < ncol; c++) {
+            const int q1 = cbase[c + 1];
+            for (int q = cbase[c] + threadIdx.x; q < q1; q += SOLVE_TPB) {
+                const int2 sg = seg[q];
+                for (int t = sg.x; t < sg.x + sg.y; t++) pos_item(rec[t], sp);
+            }
+            __syncthreads();
+        }
+    }
+    // storeBodyData (:176-197)
+    for (int i = threadIdx.x; i < nb; i += SOLVE_TPB) {
+        if (!inPos[i]) continue;
+        int f = (int)st[3 * i + 2];
+        if (!(f & 2)) continue;
+        lpe_body &b = bodies[i];
+        b.x = sp[3 * i]; b.y = sp[3 * i + 1];
+        if ((f & 1) && (b.flags & LPE_BODY_HAS_ANGPOS)) b.angle = sp[3 * i + 2];
+    }
+}
+
 // PositionSolver::positionalSolver (:299-325) by dataflow; x, y, angle of
 // every body in LDS (fp64); item data double-buffered as in k_pgs_flow
 struct PosItem {
@@ -1043,7 +1355,7 @@ int lpe_rigid_destroy_internal(lpe_ctx *ctx) {
                     d->bsum, d->order, d->rowN, d->rowR, d->rowAB, d->vel0, d->imii, d->inContact,
                     d->posState, d->posRec, d->posKeep, d->posStart, d->rowM, d->sItemA, d->sItemB,
                     d->sVer, d->lamN, d->lamF, d->sBCount, d->sBStart, d->sBCursor, d->sEnt,
-                    d->counts};
+                    d->counts, d->pcol, d->cseg, d->cbase};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     delete d;
     ctx->rigid = nullptr;
@@ -1166,6 +1478,11 @@ extern "C" int lpe_rigid_upload(lpe_ctx *ctx, int nb, const lpe_body *bodies, in
     if (!lds_attr) {
         (void)hipFuncSetAttribute((const void *)k_pgs_flow, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         (void)hipFuncSetAttribute((const void *)k_pos_flow, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k_pgs_colour, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k_pos_colour, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        // k_pair_colour also holds ~1 KB of static LDS
+        (void)hipFuncSetAttribute((const void *)k_pair_colour, hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
+        (void)hipGetLastError();   // a refused attribute must not surface at a later launch check
         lds_attr = true;
     }
     int st = rigid_alloc_bodies(ctx, d, std::max(nb, 1));
@@ -1283,49 +1600,93 @@ static int rigid_detect(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pai
     return LPE_ERR_OVERFLOW;
 }
 
-static int rigid_solve(lpe_ctx *ctx, RigidDev *d, const int32_t *pgs_order, lpe_rigid_stats *stats) {
+// colour: canonical mode (colour-major order for both solvers, see
+// k_pair_colour); otherwise pgs_order (NULL = narrowphase order) for the PGS
+// and narrowphase order for the position solver (reference-order replay)
+static int rigid_solve(lpe_ctx *ctx, RigidDev *d, bool colour, const int32_t *pgs_order,
+                       lpe_rigid_stats *stats) {
     hipStream_t s = ctx->stream;
     const lpe_rigid_config &c = d->cfg;
     int nb = d->nb, nc = d->last_nc;
-    if (nc == 0) return LPE_OK;    // early out (rigid_body_collision.cpp:35-37)
+    if (nc == 0) {                 // early out (rigid_body_collision.cpp:35-37)
+        if (colour) {
+            if (d->pcol && d->last_np > 0)
+                LPE_HIP(ctx, hipMemsetAsync(d->pcol, 0xff, sizeof(int32_t) * d->last_np, s));
+            LPE_HIP(ctx, hipMemsetAsync(d->counts + 8, 0, sizeof(int32_t), s));
+        }
+        return LPE_OK;
+    }
     if ((size_t)nb * (3 * sizeof(double) + sizeof(int)) > 160 * 1024) {
         ctx->err = "rigid solver: too many bodies for the LDS-resident solve (max 5851)";
         return LPE_ERR_CAPACITY;
     }
-    if (pgs_order)
+    const int32_t *ord = nullptr;
+    if (colour) {
+        if (d->cap_pcol < d->cap_pairs || !d->pcol) {
+            int st0 = rgrow(ctx, &d->pcol, (size_t)d->cap_pairs);
+            if (st0) return st0;
+            st0 = rgrow(ctx, &d->cseg, (size_t)d->cap_pairs);
+            if (st0) return st0;
+            d->cap_pcol = d->cap_pairs;
+        }
+        if (!d->cbase) {
+            int st0 = rgrow(ctx, &d->cbase, (size_t)MAX_COLOURS + 1);
+            if (st0) return st0;
+        }
+        size_t lds = (2 * sizeof(unsigned long long) + 1) * (size_t)nb + 16;
+        LPE_KERNEL(ctx, "k_pair_colour", k_pair_colour, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts, d->pairs, d->ccount, d->cstart, d->bodies, d->pcol, d->order, d->cseg, d->cbase, d->counts);
+        ord = d->order;
+    } else if (pgs_order) {
         LPE_HIP(ctx, hipMemcpyAsync(d->order, pgs_order, sizeof(int32_t) * nc, hipMemcpyHostToDevice, s));
+        ord = d->order;
+    }
     // ---- PGS
     LPE_HIP(ctx, hipMemsetAsync(d->inContact, 0, sizeof(int32_t) * 2 * nb, s));
     LPE_KERNEL(ctx, "k_mark_contacts", k_mark_contacts, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->contacts, d->inContact);
     LPE_KERNEL(ctx, "k_pgs_bodies", k_pgs_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->imii);
-    LPE_KERNEL(ctx, "k_pgs_rows", k_pgs_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, pgs_order ? d->order : (const int32_t *)nullptr, d->contacts, d->bodies, d->imii, d->rowN, d->rowR, d->rowAB, d->rowM, d->sItemA, d->sItemB);
-    int st = rigid_versions(ctx, d, d->counts + 1, nc);
-    if (st) return st;
-    size_t lds = (sizeof(float) * 3 + sizeof(int)) * (size_t)nb;
-    LPE_KERNEL(ctx, "k_pgs_flow", k_pgs_flow, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts + 1, d->rowN, d->rowR, d->rowAB, d->rowM, d->sVer, d->vel0, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF, d->counts + 7);
-    LPE_KERNEL(ctx, "k_pgs_writeback", k_pgs_writeback, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->inContact);
-    LPE_CHECK_LAUNCH(ctx, "pgs");
-    // ---- position solver (narrowphase order)
+    LPE_KERNEL(ctx, "k_pgs_rows", k_pgs_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, ord, d->contacts, d->bodies, d->imii, d->rowN, d->rowR, d->rowAB, d->rowM, d->sItemA, d->sItemB);
     int32_t *inPos = d->inContact + nb;
-    int32_t *keep = d->posKeep, *kstart = d->posStart;
-    LPE_KERNEL(ctx, "k_pos_bodies", k_pos_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->posState);
-    LPE_KERNEL(ctx, "k_pos_items", k_pos_items, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->contacts, d->bodies, d->posState, keep);
-    st = rscan(ctx, d, d->counts + 1, nc, keep, kstart, nullptr);
-    if (st) return st;
-    // kept-contact count -> counts[4]
-    LPE_HIP(ctx, hipMemcpyAsync(d->counts + 4, kstart + nc, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
-    LPE_KERNEL(ctx, "k_pos_fill", k_pos_fill, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, keep, kstart, d->contacts, d->posState, d->posRec, d->sItemA, d->sItemB, inPos, c.baumgarte, c.slop);
-    st = rigid_versions(ctx, d, d->counts + 4, nc);
-    if (st) return st;
-    size_t lds2 = (sizeof(double) * 3 + sizeof(int)) * (size_t)nb;
-    LPE_KERNEL(ctx, "k_pos_flow", k_pos_flow, dim3(1), dim3(SOLVE_TPB), lds2, s, nb, d->counts + 4, d->posRec, d->sVer, d->sItemA, d->sItemB, d->bodies, d->posState, inPos, c.posIterations, d->counts + 7);
-    LPE_CHECK_LAUNCH(ctx, "position solver");
+    if (colour) {
+        // canonical order: colour-synchronous sweeps over the colour segments
+        size_t lds = sizeof(float) * 3 * (size_t)nb;
+        LPE_KERNEL(ctx, "k_pgs_colour", k_pgs_colour, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts, d->cbase, d->cseg, d->rowN, d->rowR, d->rowAB, d->rowM, d->vel0, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF);
+        LPE_KERNEL(ctx, "k_pgs_writeback", k_pgs_writeback, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->inContact);
+        LPE_CHECK_LAUNCH(ctx, "pgs");
+        LPE_KERNEL(ctx, "k_pos_bodies", k_pos_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->posState);
+        LPE_KERNEL(ctx, "k_pos_fill_rows", k_pos_fill_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->order, d->contacts, d->bodies, d->posState, d->posRec, inPos, c.baumgarte, c.slop);
+        size_t lds2 = sizeof(double) * 3 * (size_t)nb;
+        LPE_KERNEL(ctx, "k_pos_colour", k_pos_colour, dim3(1), dim3(SOLVE_TPB), lds2, s, nb, d->counts, d->cbase, d->cseg, d->posRec, d->bodies, d->posState, inPos, c.posIterations);
+        LPE_CHECK_LAUNCH(ctx, "position solver");
+    } else {
+        // caller-supplied order (reference replay): exact dataflow sweeps
+        int st = rigid_versions(ctx, d, d->counts + 1, nc);
+        if (st) return st;
+        size_t lds = (sizeof(float) * 3 + sizeof(int)) * (size_t)nb;
+        LPE_KERNEL(ctx, "k_pgs_flow", k_pgs_flow, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts + 1, d->rowN, d->rowR, d->rowAB, d->rowM, d->sVer, d->vel0, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF, d->counts + 7);
+        LPE_KERNEL(ctx, "k_pgs_writeback", k_pgs_writeback, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->inContact);
+        LPE_CHECK_LAUNCH(ctx, "pgs");
+        // position solver in narrowphase order
+        int32_t *keep = d->posKeep, *kstart = d->posStart;
+        LPE_KERNEL(ctx, "k_pos_bodies", k_pos_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->posState);
+        LPE_KERNEL(ctx, "k_pos_items", k_pos_items, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, (const int32_t *)nullptr, d->contacts, d->bodies, d->posState, keep);
+        st = rscan(ctx, d, d->counts + 1, nc, keep, kstart, nullptr);
+        if (st) return st;
+        // kept-contact count -> counts[4]
+        LPE_HIP(ctx, hipMemcpyAsync(d->counts + 4, kstart + nc, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+        LPE_KERNEL(ctx, "k_pos_fill", k_pos_fill, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, (const int32_t *)nullptr, keep, kstart, d->contacts, d->posState, d->posRec, d->sItemA, d->sItemB, inPos, c.baumgarte, c.slop);
+        st = rigid_versions(ctx, d, d->counts + 4, nc);
+        if (st) return st;
+        size_t lds2 = (sizeof(double) * 3 + sizeof(int)) * (size_t)nb;
+        LPE_KERNEL(ctx, "k_pos_flow", k_pos_flow, dim3(1), dim3(SOLVE_TPB), lds2, s, nb, d->counts + 4, d->posRec, d->sVer, d->sItemA, d->sItemB, d->bodies, d->posState, inPos, c.posIterations, d->counts + 7);
+        LPE_CHECK_LAUNCH(ctx, "position solver");
+    }
     if (stats) {
-        int32_t hc[8];
-        LPE_HIP(ctx, hipMemcpyAsync(hc, d->counts, sizeof(int32_t) * 8, hipMemcpyDeviceToHost, s));
+        int32_t hc[16];
+        LPE_HIP(ctx, hipMemcpyAsync(hc, d->counts, sizeof(int32_t) * 16, hipMemcpyDeviceToHost, s));
         LPE_HIP(ctx, hipStreamSynchronize(s));
-        stats->pgsLevels = 0;     // dataflow solve: no level schedule
-        stats->posLevels = 0;
+        // colours of the canonical order (0: a caller-supplied order)
+        stats->pgsLevels = colour ? hc[8] : 0;
+        stats->posLevels = colour ? hc[8] : 0;
     }
     return LPE_OK;
 }
@@ -1344,7 +1705,7 @@ static int rigid_step_impl(lpe_ctx *ctx, int np, const int32_t *pairs, int nc_or
         return LPE_ERR_ARG;
     }
     if (stats) { stats->pairs = d->last_np; stats->contacts = d->last_nc; }
-    return rigid_solve(ctx, d, pgs_order, stats);
+    return rigid_solve(ctx, d, pairs == nullptr, pgs_order, stats);
 }
 
 extern "C" int lpe_rigid_step(lpe_ctx *ctx, lpe_rigid_stats *stats) {
@@ -1412,5 +1773,18 @@ extern "C" int lpe_rigid_download_contacts(lpe_ctx *ctx, int pair_cap, int32_t *
     if (contacts && d->last_nc > 0)
         LPE_HIP(ctx, hipMemcpyAsync(contacts, d->contacts, sizeof(lpe_contact) * std::min(contact_cap, d->last_nc), hipMemcpyDeviceToHost, s));
     LPE_HIP(ctx, hipStreamSynchronize(s));
+    return LPE_OK;
+}
+
+extern "C" int lpe_rigid_download_colours(lpe_ctx *ctx, int cap, int32_t *pair_colour, int32_t *ncolours) {
+    if (!ctx || cap < 0) return LPE_ERR_ARG;
+    RigidDev *d = rdev(ctx);
+    hipStream_t s = ctx->stream;
+    int32_t nc = 0;
+    if (d->counts) LPE_HIP(ctx, hipMemcpyAsync(&nc, d->counts + 8, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (pair_colour && d->pcol && d->last_np > 0 && cap > 0)
+        LPE_HIP(ctx, hipMemcpyAsync(pair_colour, d->pcol, sizeof(int32_t) * std::min(cap, d->last_np), hipMemcpyDeviceToHost, s));
+    LPE_HIP(ctx, hipStreamSynchronize(s));
+    if (ncolours) *ncolours = nc;
     return LPE_OK;
 }

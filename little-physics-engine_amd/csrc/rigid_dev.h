@@ -60,6 +60,11 @@ struct RigidDev {
     int4 *sVer = nullptr;                            // rank/cnt on A, rank/cnt on B
     int32_t *sBCount = nullptr, *sBStart = nullptr, *sBCursor = nullptr, *sEnt = nullptr;
     int32_t *counts = nullptr;                // [0]=np [1]=nc [4]=npos [5]=heavy [6]=pair overflow
+                                              // [7]=solver fault [8]=colours
+    int32_t *pcol = nullptr;                  // colour per pair (canonical order)
+    int2 *cseg = nullptr;                     // (row start, rows) per coloured pair, colour-major
+    int32_t *cbase = nullptr;                 // first cseg entry of each colour (+ end)
+    int cap_pcol = 0;
     lpe_rigid_config cfg{};
     bool cfg_set = false;
     int last_np = 0, last_nc = 0;

@@ -178,6 +178,7 @@ SIGNATURES = {
     "lpe_rigid_download": ([C.c_void_p, C.c_void_p], C.c_int),
     "lpe_rigid_download_contacts": ([C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
                                      _IP, _IP], C.c_int),
+    "lpe_rigid_download_colours": ([C.c_void_p, C.c_int, _IP, _IP], C.c_int),
 }
 
 class WorldConfig(C.Structure):
@@ -367,6 +368,19 @@ class Context:
                                                     cs.ctypes.data, C.byref(np_), C.byref(nc)),
                   "lpe_rigid_download_contacts")
         return pairs[:2 * np_.value].reshape(-1, 2), cs[:nc.value]
+
+    def rigid_colours(self):
+        """(pair colours of the last canonical step, colour count)."""
+        n = C.c_int32(0)
+        self._chk(lib().lpe_rigid_download_colours(self._h, 0, None, C.byref(n)),
+                  "lpe_rigid_download_colours")
+        np_ = C.c_int32(0)
+        self._chk(lib().lpe_rigid_download_contacts(self._h, 0, None, 0, None, C.byref(np_), None),
+                  "lpe_rigid_download_contacts")
+        col = np.zeros(max(np_.value, 1), np.int32)
+        self._chk(lib().lpe_rigid_download_colours(self._h, np_.value, col.ctypes.data_as(_IP),
+                                                   C.byref(n)), "lpe_rigid_download_colours")
+        return col[:np_.value], n.value
 
     # ---- world (resident full tick) -------------------------------------
     def world_set_coupling(self, body_index=None):

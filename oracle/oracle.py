@@ -192,6 +192,20 @@ def position_solver(cfg, bodies, contacts, order=None):
     return b
 
 
+def colour_order(bodies, contacts, npairs):
+    """lpeo_colour_order: (order, pair_colour, ncolours) of the canonical
+    graph-coloured solver order."""
+    L = _rigid_lib()
+    f = L.lpeo_colour_order
+    f.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    b = _bodies(bodies)
+    c = np.ascontiguousarray(contacts, lpe.CONTACT_DTYPE)
+    order = np.zeros(max(len(c), 1), np.int32)
+    col = np.zeros(max(npairs, 1), np.int32)
+    n = f(len(b), b.ctypes.data, len(c), c.ctypes.data, order.ctypes.data, col.ctypes.data, npairs)
+    return order[:len(c)], col[:npairs], n
+
+
 def rigid_update(cfg, bodies, verts):
     b = _bodies(bodies)
     v = np.ascontiguousarray(verts, np.float64)

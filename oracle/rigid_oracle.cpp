@@ -18,7 +18,8 @@
  * its PGS order from std::unordered_map iteration (contact_manager.cpp:
  * 169-245), both platform/structure dependent; every stage here takes an
  * explicit order so fixtures recorded from the reference can be replayed, and
- * the canonical order (pairs sorted by entity id) is what the HIP path runs.
+ * the canonical order (pairs sorted by entity id; solvers in the colour-major
+ * order of lpeo_colour_order) is what the HIP path runs.
  * Arithmetic: IEEE double / float as in the reference, no FMA contraction
  * (build with -ffp-contract=off; g++ on x86-64 emits none by default).
  */
@@ -643,6 +644,93 @@ extern "C" int lpeo_position_solver(const lpe_rigid_config *cfg, int nb, lpe_bod
     return (int)ids.size();
 }
 
+/* The canonical solver order of the device path (lpe_rigid.hip k_pair_colour):
+ * the pairs that produced contacts are edge-coloured so that no two pairs of
+ * one colour share a movable body (finite mass or rotatable), by rounds: every
+ * uncoloured pair claims its movable bodies with the priority (hash(p), p),
+ * the lowest wins a body, and a pair that won all its bodies takes the lowest
+ * colour free on both.  Visiting order: colour-major, pairs ascending inside a colour, each
+ * pair's contacts in narrowphase order.  The reference's PGS order is an
+ * unordered_map's (contact_manager.cpp:169-245); pairs of one colour touch
+ * disjoint movable bodies, so any order inside a colour is bit-identical.
+ * contacts must be grouped by pair (narrowphase order).  Returns the number
+ * of colours, or -1 if more than 64 would be needed. */
+extern "C" int lpeo_colour_order(int nb, const lpe_body *bodies, int nc, const lpe_contact *cs,
+                                 int32_t *order, int32_t *pair_colour, int npairs) {
+    auto dep = [&](int i) {
+        const lpe_body &b = bodies[i];
+        bool inf = (b.flags & LPE_BODY_HAS_MASS) && b.mass > 1e29;
+        bool rot = (b.flags & LPE_BODY_HAS_INERTIA) && b.inertia > 1e-12 && b.inertia < 1e29;
+        return !inf || rot;
+    };
+    /* pairs with contacts: index, bodies, contact range */
+    std::vector<int> pid, pa, pb, ps, pn;
+    for (int k = 0; k < nc; k++) {
+        if (k == 0 || cs[k].pair != cs[k - 1].pair) {
+            pid.push_back(cs[k].pair); pa.push_back(cs[k].a); pb.push_back(cs[k].b);
+            ps.push_back(k); pn.push_back(0);
+        }
+        pn.back()++;
+    }
+    int m = (int)pid.size();
+    std::vector<int> col(m, -2);
+    std::vector<unsigned long long> used(nb, 0ull);
+    const unsigned long long NONE = ~0ull;
+    std::vector<unsigned long long> claim(nb, NONE);
+    auto prio = [&](int p) {
+        uint32_t x = (uint32_t)p;                 /* lpe_rigid.hip colour_hash */
+        x ^= x >> 16; x *= 0x7feb352du;
+        x ^= x >> 15; x *= 0x846ca68bu;
+        x ^= x >> 16;
+        return ((unsigned long long)x << 32) | (uint32_t)p;
+    };
+    for (int left = m; left > 0;) {
+        for (int q = 0; q < m; q++) {
+            if (col[q] != -2) continue;
+            if (dep(pa[q])) claim[pa[q]] = std::min(claim[pa[q]], prio(pid[q]));
+            if (dep(pb[q])) claim[pb[q]] = std::min(claim[pb[q]], prio(pid[q]));
+        }
+        std::vector<int> won;
+        for (int q = 0; q < m; q++) {
+            if (col[q] != -2) continue;
+            int a = dep(pa[q]) ? pa[q] : -1, b = dep(pb[q]) ? pb[q] : -1;
+            if ((a < 0 || claim[a] == prio(pid[q])) && (b < 0 || claim[b] == prio(pid[q]))) {
+                unsigned long long forb = (a >= 0 ? used[a] : 0ull) | (b >= 0 ? used[b] : 0ull);
+                if (forb == ~0ull) return -1;
+                int c = 0;
+                while (forb & (1ull << c)) c++;
+                col[q] = -3 - c;
+                won.push_back(q);
+            }
+        }
+        for (int q = 0; q < m; q++) {
+            if (col[q] == -2 || col[q] <= -3) {
+                if (dep(pa[q])) claim[pa[q]] = NONE;
+                if (dep(pb[q])) claim[pb[q]] = NONE;
+            }
+        }
+        for (int q : won) {
+            int c = -3 - col[q];
+            col[q] = c;
+            if (dep(pa[q])) used[pa[q]] |= 1ull << c;
+            if (dep(pb[q])) used[pb[q]] |= 1ull << c;
+            left--;
+        }
+    }
+    int ncol = 0;
+    for (int q = 0; q < m; q++) ncol = std::max(ncol, col[q] + 1);
+    int t = 0;
+    for (int c = 0; c < ncol; c++)
+        for (int q = 0; q < m; q++)
+            if (col[q] == c)
+                for (int j = 0; j < pn[q]; j++) order[t++] = ps[q] + j;
+    if (pair_colour) {
+        for (int p = 0; p < npairs; p++) pair_colour[p] = -1;
+        for (int q = 0; q < m; q++) if (pid[q] >= 0 && pid[q] < npairs) pair_colour[pid[q]] = col[q];
+    }
+    return ncol;
+}
+
 extern "C" int lpeo_rigid_update(const lpe_rigid_config *cfg, int nb, lpe_body *bodies,
                                  const double *verts, lpeo_rigid_stats *st) {
     std::vector<int32_t> pairs(2 * 1024);
@@ -659,8 +747,11 @@ extern "C" int lpeo_rigid_update(const lpe_rigid_config *cfg, int nb, lpe_body *
     }
     if (st) { st->pairs = np; st->contacts = nc; st->manifolds = 0; st->dynamicBodies = 0; }
     if (nc == 0) return 0;   /* rigid_body_collision.cpp:35-37 */
-    int nd = lpeo_pgs(cfg, nb, bodies, nc, cs.data(), nullptr);
-    lpeo_position_solver(cfg, nb, bodies, nc, cs.data(), nullptr);
+    std::vector<int32_t> order(nc);
+    if (lpeo_colour_order(nb, bodies, nc, cs.data(), order.data(), nullptr, 0) < 0)
+        return -1;
+    int nd = lpeo_pgs(cfg, nb, bodies, nc, cs.data(), order.data());
+    lpeo_position_solver(cfg, nb, bodies, nc, cs.data(), order.data());
     if (st) {
         st->dynamicBodies = nd;
         int m = 0;

@@ -36,9 +36,17 @@ int lpeo_pgs(const lpe_rigid_config *cfg, int nb, lpe_body *bodies, int nc,
 int lpeo_position_solver(const lpe_rigid_config *cfg, int nb, lpe_body *bodies, int nc,
                          const lpe_contact *contacts, const int32_t *order);
 
+/* Canonical solver order (the device's k_pair_colour): colour-major over the
+ * edge-coloured contact pairs, pairs ascending inside a colour, contacts of a
+ * pair in narrowphase order.  order receives nc contact indices; pair_colour
+ * (optional, npairs entries) the colour of each pair (-1: no contact).
+ * Returns the number of colours (-1: more than 64 needed). */
+int lpeo_colour_order(int nb, const lpe_body *bodies, int nc, const lpe_contact *cs,
+                      int32_t *order, int32_t *pair_colour, int npairs);
+
 /* RigidBodyCollisionSystem::update (rigid_body_collision.cpp:24-50) with the
- * canonical orders: pairs by (eid_a, eid_b); PGS manifolds in pair order;
- * position solver in narrowphase order. */
+ * canonical orders: pairs by (eid_a, eid_b); PGS and position solver in the
+ * colour-major order of lpeo_colour_order. */
 int lpeo_rigid_update(const lpe_rigid_config *cfg, int nb, lpe_body *bodies,
                       const double *verts, lpeo_rigid_stats *stats);
 

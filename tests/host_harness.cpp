@@ -1,0 +1,186 @@
+/*
+ * host_harness.cpp — TEST INFRASTRUCTURE ONLY.  Drives the C++ host mirror
+ * (little-physics-engine_amd/host: Systems::FluidSystem and friends, built
+ * against the reference's own headers) through an EnTT registry exactly as
+ * ECSSimulator::tick does (src/sim.cpp:107-114 order, :156-163 loop), so the
+ * tests can check the drop-in systems against the oracle.  Built by
+ * oracle/Makefile.ref (it needs the reference's headers and its
+ * vector_math.cpp, which defines the Position/Vector constructors) into
+ * oracle/_ref/liblpe_host_harness.so.
+ *
+ * BarnesHutSystem (a reference CPU system outside the hot path) is left out:
+ * it returns early for every mass < 1e3 (barnes_hut.cpp:54-70).
+ */
+#include <entt/entt.hpp>
+
+#include <cstring>
+#include <memory>
+#include <unordered_map>
+#include <vector>
+
+#include "entities/entity_components.hpp"
+#include "entities/sim_components.hpp"
+#include "math/polygon.hpp"
+#include "systems/boundary.hpp"
+#include "systems/fluid/fluid.hpp"
+#include "systems/gravity.hpp"
+#include "systems/movement.hpp"
+#include "systems/rigid/rigid_body_collision.hpp"
+#include "systems/rotation.hpp"
+#include "systems/shared_system_config.hpp"
+#include "systems/sleep.hpp"
+
+#include "lpe_backend.hpp"
+
+extern "C" int lpeh_world(int mode, int sync_every, const lpe_rigid_config *rc,
+                          const lpe_fluid_config *fc, double spt, double time_accel, double bta,
+                          double ts, int nb, lpe_body *bodies, const double *verts, int nf,
+                          float *x, float *y, float *vx, float *vy, const float *m, float *rho,
+                          float *p, int nticks, int32_t *fluid_gather, int32_t *rigid_gather,
+                          int32_t *stats) {
+    entt::registry reg;
+    auto se = reg.create();                        /* reset(): SimulatorState first (sim.cpp:93-94) */
+    reg.emplace<Components::SimulatorState>(se, bta, ts);
+    std::vector<entt::entity> bents, fents;
+    for (int i = 0; i < nb; i++) {
+        const lpe_body &b = bodies[i];
+        auto e = reg.create();
+        bents.push_back(e);
+        reg.emplace<Components::Position>(e, b.x, b.y);
+        if (b.flags & LPE_BODY_HAS_VEL) reg.emplace<Components::Velocity>(e, b.vx, b.vy);
+        if (b.flags & LPE_BODY_HAS_MASS) reg.emplace<Components::Mass>(e, b.mass);
+        if (b.flags & LPE_BODY_BOUNDARY) reg.emplace<Components::Boundary>(e, true);
+        if (b.flags & LPE_BODY_HAS_PHASE)
+            reg.emplace<Components::ParticlePhase>(
+                e, (b.flags & LPE_BODY_LIQUID) ? Components::Phase::Liquid : Components::Phase::Solid);
+        if (b.flags & LPE_BODY_HAS_SLEEP) {
+            auto &sl = reg.emplace<Components::Sleep>(e);
+            sl.asleep = (b.flags & LPE_BODY_ASLEEP) != 0;
+            sl.sleepCounter = b.sleep_counter;
+        }
+        if (b.flags & LPE_BODY_CIRCLE) {
+            reg.emplace<CircleShape>(e, CircleShape{b.radius});
+            reg.emplace<Components::Shape>(e, Components::ShapeType::Circle, b.radius);
+        }
+        if (b.flags & LPE_BODY_POLYGON) {
+            PolygonShape poly;
+            poly.type = Components::ShapeType::Polygon;
+            double r = 0;
+            for (int k = 0; k < b.vert_cnt; k++) {
+                double lx = verts[2 * (b.vert_off + k)], ly = verts[2 * (b.vert_off + k) + 1];
+                poly.vertices.emplace_back(lx, ly);
+                r = std::max(r, std::sqrt(lx * lx + ly * ly));
+            }
+            reg.emplace<PolygonShape>(e, poly);
+            reg.emplace<Components::Shape>(e, Components::ShapeType::Polygon, r);
+        }
+        if (b.flags & LPE_BODY_HAS_INERTIA) reg.emplace<Components::Inertia>(e, b.inertia);
+        if (b.flags & LPE_BODY_HAS_ANGPOS) reg.emplace<Components::AngularPosition>(e, b.angle);
+        if (b.flags & LPE_BODY_HAS_ANGVEL) reg.emplace<Components::AngularVelocity>(e, b.omega);
+    }
+    for (int i = 0; i < nf; i++) {                 /* fluid entities (simple_fluid.cpp recipe) */
+        auto e = reg.create();
+        fents.push_back(e);
+        reg.emplace<Components::Position>(e, (double)x[i], (double)y[i]);
+        reg.emplace<Components::Velocity>(e, (double)vx[i], (double)vy[i]);
+        reg.emplace<Components::Mass>(e, (double)m[i]);
+        reg.emplace<Components::ParticlePhase>(e, Components::Phase::Liquid);
+        reg.emplace<Components::SpeedOfSound>(e, 1000.0);
+        auto &t = reg.emplace<Components::SPHTemp>(e);
+        t.density = rho[i];
+        t.pressure = p[i];
+    }
+    /* the gather orders the drop-in FluidSystem will see (fluid.cpp:259-299, :313-435) */
+    {
+        std::unordered_map<uint32_t, int> fidx, bidx;
+        for (int i = 0; i < nf; i++) fidx[(uint32_t)entt::to_integral(fents[i])] = i;
+        for (int i = 0; i < nb; i++) bidx[(uint32_t)entt::to_integral(bents[i])] = i;
+        int k = 0;
+        auto fv = reg.view<Components::Position, Components::Velocity, Components::Mass,
+                           Components::ParticlePhase, Components::SpeedOfSound, Components::SPHTemp>();
+        for (auto e : fv) if (k < nf) fluid_gather[k++] = fidx[(uint32_t)entt::to_integral(e)];
+        k = 0;
+        auto rv = reg.view<Components::Position, Components::Shape>();
+        for (auto e : rv) if (k < nb) rigid_gather[k++] = bidx[(uint32_t)entt::to_integral(e)];
+        for (; k < nb; k++) rigid_gather[k] = -1;
+    }
+
+    SharedSystemConfig sh{};                       /* every field set (no defaults, shared_system_config.hpp:10-20) */
+    sh.UniverseSizeMeters = rc->universeSize;
+    sh.TimeAcceleration = time_accel;
+    sh.MetersPerPixel = rc->metersPerPixel;
+    sh.SecondsPerTick = spt;
+    sh.GravitationalSoftener = 0.0;
+    sh.DragCoeff = 0.0;
+    sh.ParticleDensity = 0.0;
+    sh.GridSize = 50;
+    sh.CellSizePixels = 12.0;
+
+    /* ECSSimulator::createSystems (sim.cpp:103-150), minus BarnesHut */
+    std::vector<std::unique_ptr<Systems::ISystem>> systems;
+    systems.push_back(std::make_unique<Systems::FluidSystem>());
+    systems.push_back(std::make_unique<Systems::BoundarySystem>());
+    systems.push_back(std::make_unique<Systems::BasicGravitySystem>());
+    systems.push_back(std::make_unique<Systems::RigidBodyCollisionSystem>());
+    systems.push_back(std::make_unique<Systems::RotationSystem>());
+    systems.push_back(std::make_unique<Systems::MovementSystem>());
+    systems.push_back(std::make_unique<Systems::SleepSystem>());
+    Systems::FluidConfig fcfg;
+    static_assert(sizeof(fcfg) == sizeof(*fc), "FluidConfig mirrors lpe_fluid_config");
+    std::memcpy(&fcfg, fc, sizeof(fcfg));
+    Systems::BoundaryConfig bc; bc.marginPixels = rc->marginPixels; bc.bounceDamping = rc->bounceDamping;
+    bc.maxSpeed = rc->maxSpeed;
+    Systems::GravityConfig gc; gc.gravitationalAcceleration = rc->gravity;
+    gc.planetaryMassThreshold = rc->planetaryMassThreshold;
+    Systems::RotationConfig roc; roc.angularDamping = rc->angularDamping; roc.maxAngularSpeed = rc->maxAngularSpeed;
+    Systems::SleepConfig sc; sc.linearSleepThreshold = rc->linearSleepThreshold;
+    sc.angularSleepThreshold = rc->angularSleepThreshold; sc.sleepFramesThreshold = rc->sleepFramesThreshold;
+    Systems::RigidBodyCollisionConfig rbc; rbc.pgsIterations = rc->pgsIterations;
+    rbc.frictionCoeff = rc->frictionCoeff; rbc.positionIterations = rc->posIterations;
+    rbc.baumgarte = rc->baumgarte; rbc.slop = rc->slop;
+    for (auto &sys : systems) {                    /* the dynamic_cast chain of sim.cpp:116-149 */
+        sys->setSharedSystemConfig(sh);
+        if (auto *s = dynamic_cast<Systems::FluidSystem *>(sys.get())) s->setSpecificConfig(fcfg);
+        else if (auto *s = dynamic_cast<Systems::BoundarySystem *>(sys.get())) s->setSpecificConfig(bc);
+        else if (auto *s = dynamic_cast<Systems::BasicGravitySystem *>(sys.get())) s->setSpecificConfig(gc);
+        else if (auto *s = dynamic_cast<Systems::RigidBodyCollisionSystem *>(sys.get())) s->setSpecificConfig(rbc);
+        else if (auto *s = dynamic_cast<Systems::RotationSystem *>(sys.get())) s->setSpecificConfig(roc);
+        else if (auto *s = dynamic_cast<Systems::SleepSystem *>(sys.get())) s->setSpecificConfig(sc);
+    }
+    lpe::host::reset();
+    lpe::host::setMode(mode ? lpe::host::Mode::Resident : lpe::host::Mode::Strict, sync_every);
+    for (int t = 0; t < nticks; t++)               /* ECSSimulator::tick (sim.cpp:156-163) */
+        for (auto &sys : systems) sys->update(reg);
+    if (mode) lpe::host::residentSync(reg);
+
+    for (int i = 0; i < nb; i++) {
+        auto e = bents[i];
+        lpe_body &b = bodies[i];
+        const auto &pos = reg.get<Components::Position>(e);
+        b.x = pos.x; b.y = pos.y;
+        if (auto *v = reg.try_get<Components::Velocity>(e)) { b.vx = v->x; b.vy = v->y; }
+        if (auto *a = reg.try_get<Components::AngularPosition>(e)) b.angle = a->angle;
+        if (auto *w = reg.try_get<Components::AngularVelocity>(e)) b.omega = w->omega;
+        if (auto *sl = reg.try_get<Components::Sleep>(e)) {
+            b.sleep_counter = sl->sleepCounter;
+            if (sl->asleep) b.flags |= LPE_BODY_ASLEEP; else b.flags &= ~LPE_BODY_ASLEEP;
+        }
+    }
+    for (int i = 0; i < nf; i++) {
+        auto e = fents[i];
+        const auto &pos = reg.get<Components::Position>(e);
+        const auto &vel = reg.get<Components::Velocity>(e);
+        const auto &t = reg.get<Components::SPHTemp>(e);
+        x[i] = (float)pos.x; y[i] = (float)pos.y;
+        vx[i] = (float)vel.x; vy[i] = (float)vel.y;
+        rho[i] = (float)t.density; p[i] = (float)t.pressure;
+    }
+    auto *fs = dynamic_cast<Systems::FluidSystem *>(systems[0].get());
+    auto *rs = dynamic_cast<Systems::RigidBodyCollisionSystem *>(systems[3].get());
+    stats[0] = lpe::host::lastStatus();
+    stats[1] = fs->lastMaxCellOccupancy();
+    stats[2] = rs->lastPairs();
+    stats[3] = rs->lastContacts();
+    lpe::host::setMode(lpe::host::Mode::Strict, 1);
+    return stats[0];
+}

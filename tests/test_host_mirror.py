@@ -1,0 +1,97 @@
+"""The C++ host mirror (little-physics-engine_amd/host): the reference's system
+plugins Systems::FluidSystem, RigidBodyCollisionSystem, BoundarySystem,
+BasicGravitySystem, RotationSystem, MovementSystem and SleepSystem, re-built
+over the C ABI and compiled against the reference's own headers, driven
+through an EnTT registry in ECSSimulator::tick order (tests/host_harness.cpp).
+
+CPU: the mirror and its harness load and export their entry points.
+GPU: a tick through the drop-in systems equals the whole-tick oracle
+(strict mode: gather/scatter every system, as the reference; resident mode:
+the device owns the state, the ECS is synced at the end)."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, lpe, scenes
+
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "liblpe_host_harness.so")
+SYSTEMS = os.path.join(ROOT, "little-physics-engine_amd", "host", "liblpe_systems.so")
+DT = 1.0 / 120.0
+
+needs_build = pytest.mark.skipif(not os.path.exists(HARNESS),
+                                 reason="host mirror is built only where /root/reference exists")
+
+
+def _harness():
+    L = C.CDLL(HARNESS)
+    f = L.lpeh_world
+    f.argtypes = [C.c_int, C.c_int, C.POINTER(lpe.RigidConfig), C.POINTER(lpe.FluidConfig),
+                  C.c_double, C.c_double, C.c_double, C.c_double, C.c_int, C.c_void_p, C.c_void_p,
+                  C.c_int] + [C.c_void_p] * 7 + [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
+    f.restype = C.c_int
+    return f
+
+
+@needs_build
+def test_host_mirror_exports():
+    L = C.CDLL(HARNESS)
+    assert hasattr(L, "lpeh_world")
+    syms = os.popen(f"nm -D --defined-only {SYSTEMS}").read()
+    for name in ("FluidSystem6update", "RigidBodyCollisionSystem6update", "BoundarySystem6update",
+                 "BasicGravitySystem6update", "RotationSystem6update", "MovementSystem6update",
+                 "SleepSystem6update"):
+        assert name in syms, name
+
+
+def run_world(name, mode, nticks, sync_every=1):
+    s = scenes.scene(name)
+    b, v = scenes.to_bodies(s["bodies"])
+    fl = s["fluid"]
+    n = len(fl["x"])
+    arr = {k: np.ascontiguousarray(fl[k], np.float32).copy()
+           for k in ("x", "y", "vx", "vy", "mass", "density", "pressure")}
+    rc = lpe.rigid_config(universe=s["U"])
+    fc = lpe.default_fluid_config()
+    bodies = np.ascontiguousarray(b).copy()
+    fg = np.zeros(n, np.int32)
+    rg = np.zeros(len(b), np.int32)
+    stats = np.zeros(4, np.int32)
+    st = _harness()(mode, sync_every, C.byref(rc), C.byref(fc), DT, 1.0, 1.0, 1.0, len(b),
+                    bodies.ctypes.data, v.ctypes.data, n,
+                    *[arr[k].ctypes.data for k in ("x", "y", "vx", "vy", "mass", "density", "pressure")],
+                    nticks, fg.ctypes.data, rg.ctypes.data, stats.ctypes.data)
+    assert st == 0, f"host mirror failed with status {st}"
+    return s, b, v, fl, arr, bodies, fg, rg, stats, rc, fc
+
+
+@needs_build
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1], ids=["strict", "resident"])
+def test_host_mirror_tick_matches_oracle(oracle_mod, mode):
+    s, b, v, fl, arr, bodies, fg, rg, stats, rc, fc = run_world("small64_8", mode, 1)
+    # the oracle sees the fluid in the drop-in's gather order (EnTT view order)
+    assert sorted(fg.tolist()) == list(range(len(fg)))
+    p0 = scenes.particles_aos(fl)[fg]
+    couple = rg[rg >= 0].astype(np.int32)
+    p, rb = oracle_mod.world_tick(fc, rc, p0, b, v, couple, DT, 1)
+    for k, col in (("x", 0), ("y", 1), ("vx", 2), ("vy", 3), ("density", 11), ("pressure", 12)):
+        np.testing.assert_array_equal(arr[k][fg], p[:, col], err_msg=k)
+    for k in ("x", "y", "angle"):
+        np.testing.assert_allclose(bodies[k], rb[k], rtol=1e-6, atol=1e-7, err_msg=k)
+    for k in ("vx", "vy", "omega"):
+        np.testing.assert_allclose(bodies[k], rb[k], rtol=1e-5, atol=1e-5, err_msg=k)
+    assert 0 < stats[1] <= 64 or mode == 1
+
+
+@needs_build
+@pytest.mark.gpu
+def test_host_mirror_strict_equals_resident():
+    """Three ticks: per-system ECS round trips (strict) and the device-owned
+    world (resident, ECS synced every 2 ticks and at the end) agree."""
+    _, _, _, _, a0, b0, *_ = run_world("small64_8", 0, 3)
+    _, _, _, _, a1, b1, *_ = run_world("small64_8", 1, 3, sync_every=2)
+    for k in ("x", "y"):
+        np.testing.assert_allclose(a0[k], a1[k], rtol=1e-5, atol=1e-5, err_msg=k)
+        np.testing.assert_allclose(b0[k], b1[k], rtol=1e-5, atol=1e-4, err_msg=k)

@@ -100,6 +100,30 @@ def test_integrators_match_reference(gpu_ctx, path):
          ("x", "y", "angle", "vx", "vy", "omega", "sleep_counter", "flags"))
 
 
+@pytest.mark.parametrize("path", FIXTURES, ids=[os.path.basename(p) for p in FIXTURES])
+def test_colour_order_matches_restatement(gpu_ctx, oracle_mod, path):
+    """The canonical solver order: the device's pair colouring equals the
+    restated one (integer work, bit-exact) and is proper: no movable body
+    appears twice in one colour."""
+    z, cfg = load(path)
+    pre = z["before_rigid"]
+    gpu_ctx.rigid_set_config(cfg)
+    gpu_ctx.rigid_upload(pre, z["verts"])
+    st = gpu_ctx.rigid_step()
+    pairs, cs = gpu_ctx.rigid_contacts()
+    col, ncol = gpu_ctx.rigid_colours()
+    _, ref_col, ref_ncol = oracle_mod.colour_order(pre, cs, len(pairs))
+    np.testing.assert_array_equal(col, ref_col)
+    assert ncol == ref_ncol == st["pgsLevels"]
+    inf = ((pre["flags"] & lpe.BODY_HAS_MASS) != 0) & (pre["mass"] > 1e29)
+    rot = ((pre["flags"] & lpe.BODY_HAS_INERTIA) != 0) & (pre["inertia"] > 1e-12) & (pre["inertia"] < 1e29)
+    movable = ~inf | rot
+    for c in range(ncol):
+        sel = pairs[col == c]
+        ends = np.concatenate([sel[movable[sel[:, 0]], 0], sel[movable[sel[:, 1]], 1]])
+        assert len(np.unique(ends)) == len(ends), f"colour {c} reuses a movable body"
+
+
 def test_c3_pile_canonical(gpu_ctx, oracle_mod):
     """C3-scale pile (4096 polygons + 4 walls, 16 PGS iterations): warm the
     pile on the CPU restatement, then one RigidBodyCollisionSystem::update on
@@ -116,6 +140,7 @@ def test_c3_pile_canonical(gpu_ctx, oracle_mod):
     gpu_ctx.rigid_upload(b, v)
     st = gpu_ctx.rigid_step()
     assert st["pairs"] == rst.pairs and st["contacts"] == rst.contacts and rst.contacts > 1000
+    print(f"C3 pile: {st['pairs']} pairs, {st['contacts']} contacts, {st['pgsLevels']} colours")
     out = gpu_ctx.rigid_download()
     close_state(out, ref)
 
