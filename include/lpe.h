@@ -126,6 +126,11 @@ typedef struct lpe_sph_stats {
     int32_t gridDimX, gridDimY; /* reference grid dims of the last sub-step   */
     int32_t gridMinX, gridMinY;
     float   cellSize;
+    /* diagnostics, counted only while lpe_sph_diag(ctx, 1) is on (sums over
+     * every sub-step since it was switched on): */
+    int32_t nlistOverflow;      /* particles whose neighbour list exceeded 64  */
+    int32_t rigidCandidates;    /* rigids tested by the coupling solvers       */
+    int32_t neighbours;         /* neighbours with r < h found by the density pass */
 } lpe_sph_stats;
 
 /* ------------------------------------------------------------------------ */
@@ -268,6 +273,8 @@ int  lpe_sph_download_aux(lpe_ctx *ctx, float *vxHalf, float *vyHalf,
  * when accum is non-NULL (3 floats per body). */
 int  lpe_sph_download_rigids(lpe_ctx *ctx, lpe_gpu_rigid *rigids, float *accum);
 int  lpe_sph_get_stats(lpe_ctx *ctx, lpe_sph_stats *stats);
+/* Diagnostics counters of lpe_sph_stats on (1, counters reset) or off (0). */
+int  lpe_sph_diag(lpe_ctx *ctx, int on);
 
 /* Parity probe: the reference's assignCells cell index for each particle
  * (fluid_kernels.metal:212-241: cellY*gridDimX + cellX, or -1 if "not

@@ -71,6 +71,7 @@ struct SphDev {
     lpe_fluid_config cfg{};
     bool cfg_set = false;
     bool rig_dirty = true;
+    int diag = 0;                 // count the ST_NL_OVERFLOW / ST_RIGID_CAND / ST_NEIGH stats
 };
 
 // status slots
@@ -79,6 +80,9 @@ enum StatusSlot {
     ST_MAX_OCC = 1,
     ST_NOT_INSERTED = 2,
     ST_LIST_OVERFLOW = 3,
+    ST_NL_OVERFLOW = 4,     // diag: particles whose neighbour list overflowed (forces walk the bins)
+    ST_RIGID_CAND = 5,      // diag: rigid candidates tested by the coupling (sum over particles)
+    ST_NEIGH = 6,           // diag: neighbours (r < h) found by the density pass (sum)
     ST_COUNT = 16
 };
 

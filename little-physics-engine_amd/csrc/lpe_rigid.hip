@@ -642,52 +642,93 @@ k_pair_colour(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict_
         dep[i] = colour_dep(bodies[i]) ? 1 : 0;
     }
     if (threadIdx.x == 0) { s_fault = 0; s_ncol = 0; }
-    // -1: pair without contacts (no item); -2: uncoloured
-    for (int p = threadIdx.x; p < np; p += SOLVE_TPB) pcol[p] = ccount[p] > 0 ? -2 : -1;
     __syncthreads();
+    // Pairs p = tid + k*TPB (k < PK) live in registers for all rounds (a
+    // round is then LDS work only); pairs beyond PK*TPB use global memory.
+    // Colour state: -1 pair without contacts (no item), -2 uncoloured,
+    // <= -3 coloured this round (-3 - colour), >= 0 colour.
+    constexpr int PK = 12;
+    int rab[PK], rc[PK];            // movable bodies packed as two int16 (-1: none)
+#pragma unroll
+    for (int k = 0; k < PK; k++) {
+        const int p = threadIdx.x + k * SOLVE_TPB;
+        rab[k] = -1; rc[k] = -1;
+        if (p < np) {
+            int2 pr = pairs[p];
+            int a = dep[pr.x] ? pr.x : -1, b = dep[pr.y] ? pr.y : -1;
+            rab[k] = (a & 0xffff) | (b << 16);
+            rc[k] = ccount[p] > 0 ? -2 : -1;
+        }
+    }
+    auto A = [](int ab) { return (int)(short)(ab & 0xffff); };
+    auto B = [](int ab) { return ab >> 16; };
+    for (int p = threadIdx.x + PK * SOLVE_TPB; p < np; p += SOLVE_TPB) pcol[p] = ccount[p] > 0 ? -2 : -1;
+    auto prio = [](int p) {
+        return ((unsigned long long)colour_hash((uint32_t)p) << 32) | (uint32_t)p;
+    };
+    auto claimOf = [&](int p, int a, int b, int col) {
+        if (col != -2) return;
+        if (a >= 0) atomicMin(&claim[a], prio(p));
+        if (b >= 0) atomicMin(&claim[b], prio(p));
+    };
+    auto pick = [&](int p, int a, int b, int &col) {
+        if (col != -2) return;
+        const unsigned long long pri = prio(p);
+        if ((a < 0 || claim[a] == pri) && (b < 0 || claim[b] == pri)) {
+            unsigned long long forb = (a >= 0 ? su[a] : 0ull) | (b >= 0 ? su[b] : 0ull);
+            int c = __ffsll((long long)~forb) - 1;
+            if (c < 0 || c >= MAX_COLOURS) { s_fault = 1; c = 0; }
+            col = -3 - c;                                          // coloured this round
+        } else {
+            s_left = 1;
+        }
+    };
+    auto commit = [&](int a, int b, int &col) {
+        if (col == -1 || col >= 0) return;
+        if (col <= -3) {
+            const int c = -3 - col;
+            col = c;
+            if (a >= 0) su[a] |= 1ull << c;                        // one winner per body
+            if (b >= 0) su[b] |= 1ull << c;
+        }
+        if (a >= 0) claim[a] = NONE;
+        if (b >= 0) claim[b] = NONE;
+    };
+    auto gpair = [&](int p, int &a, int &b) {
+        int2 pr = pairs[p];
+        a = dep[pr.x] ? pr.x : -1;
+        b = dep[pr.y] ? pr.y : -1;
+    };
     for (int round = 0;; round++) {
         if (threadIdx.x == 0) s_left = 0;
-        for (int p = threadIdx.x; p < np; p += SOLVE_TPB) {       // claims
-            if (pcol[p] != -2) continue;
-            int2 pr = pairs[p];
-            unsigned long long pri = ((unsigned long long)colour_hash((uint32_t)p) << 32) | (uint32_t)p;
-            if (dep[pr.x]) atomicMin(&claim[pr.x], pri);
-            if (dep[pr.y]) atomicMin(&claim[pr.y], pri);
+#pragma unroll
+        for (int k = 0; k < PK; k++) claimOf(threadIdx.x + k * SOLVE_TPB, A(rab[k]), B(rab[k]), rc[k]);
+        for (int p = threadIdx.x + PK * SOLVE_TPB; p < np; p += SOLVE_TPB) {
+            int a, b; gpair(p, a, b); claimOf(p, a, b, pcol[p]);
         }
         __syncthreads();
-        for (int p = threadIdx.x; p < np; p += SOLVE_TPB) {       // winners pick a colour
-            if (pcol[p] != -2) continue;
-            int2 pr = pairs[p];
-            unsigned long long pri = ((unsigned long long)colour_hash((uint32_t)p) << 32) | (uint32_t)p;
-            int a = dep[pr.x] ? pr.x : -1, b = dep[pr.y] ? pr.y : -1;
-            if ((a < 0 || claim[a] == pri) && (b < 0 || claim[b] == pri)) {
-                unsigned long long forb = (a >= 0 ? su[a] : 0ull) | (b >= 0 ? su[b] : 0ull);
-                int c = __ffsll((long long)~forb) - 1;
-                if (c < 0 || c >= MAX_COLOURS) { s_fault = 1; c = 0; }
-                pcol[p] = -3 - c;                                  // coloured this round
-            } else {
-                s_left = 1;
-            }
+#pragma unroll
+        for (int k = 0; k < PK; k++) pick(threadIdx.x + k * SOLVE_TPB, A(rab[k]), B(rab[k]), rc[k]);
+        for (int p = threadIdx.x + PK * SOLVE_TPB; p < np; p += SOLVE_TPB) {
+            int a, b, col = pcol[p]; gpair(p, a, b); pick(p, a, b, col); pcol[p] = col;
         }
         __syncthreads();
-        for (int p = threadIdx.x; p < np; p += SOLVE_TPB) {       // commit, release claims
-            int v = pcol[p];
-            if (v == -1 || v >= 0) continue;
-            int2 pr = pairs[p];
-            if (v <= -3) {
-                int c = -3 - v;
-                pcol[p] = c;
-                if (dep[pr.x]) su[pr.x] |= 1ull << c;              // one winner per body
-                if (dep[pr.y]) su[pr.y] |= 1ull << c;
-            }
-            if (dep[pr.x]) claim[pr.x] = NONE;
-            if (dep[pr.y]) claim[pr.y] = NONE;
+#pragma unroll
+        for (int k = 0; k < PK; k++) commit(A(rab[k]), B(rab[k]), rc[k]);
+        for (int p = threadIdx.x + PK * SOLVE_TPB; p < np; p += SOLVE_TPB) {
+            int a, b, col = pcol[p]; gpair(p, a, b); commit(a, b, col); pcol[p] = col;
         }
         __syncthreads();
         const bool more = s_left && !s_fault && round < (1 << 20);
         __syncthreads();              // every thread has read s_left before it is reset
         if (!more) break;
     }
+#pragma unroll
+    for (int k = 0; k < PK; k++) {
+        const int p = threadIdx.x + k * SOLVE_TPB;
+        if (p < np) pcol[p] = rc[k];
+    }
+    __syncthreads();
     // colour-major order: rows and pairs per colour -> bases -> pairs placed whole
     if (threadIdx.x < MAX_COLOURS) {
         colCnt[threadIdx.x] = 0; colCur[threadIdx.x] = 0;
@@ -778,25 +819,56 @@ __device__ __forceinline__ void pgs_row_pair(float4 rn, float4 rr, float4 rm, in
     if (ab.y >= 0) { sv[3 * ab.y] = vxB; sv[3 * ab.y + 1] = vyB; sv[3 * ab.y + 2] = wB; }
 }
 
+// A colour step is latency-bound (one workgroup; a pair's rows are a chain),
+// so the global round trips per step are kept to one: colour bases and the
+// coloured pairs' row segments are cached in LDS (when they fit: segLds), and
+// all rows of a pair (up to RB) are loaded before its sequential updates.
+static constexpr int RB = 4;
 __global__ void __launch_bounds__(SOLVE_TPB)
 k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restrict__ cbase,
-             const int2 *__restrict__ seg, const float4 *__restrict__ rowN,
+             const int2 *__restrict__ seg, int segLds, const float4 *__restrict__ rowN,
              const float4 *__restrict__ rowR, const int2 *__restrict__ rowAB,
              const float4 *__restrict__ rowM, float *__restrict__ vel, int iters, float mu,
              float *__restrict__ lamN, float *__restrict__ lamF) {
-    extern __shared__ float sv[];   // 3 floats per body
-    for (int i = threadIdx.x; i < 3 * nb; i += SOLVE_TPB) sv[i] = vel[i];
-    __syncthreads();
+    extern __shared__ float sv[];   // 3 floats per body, then the segment cache
+    int2 *ss = (int2 *)(sv + ((3 * nb + 1) & ~1));
+    __shared__ int scb[MAX_COLOURS + 1];
     const int ncol = counts[8];
+    for (int i = threadIdx.x; i < 3 * nb; i += SOLVE_TPB) sv[i] = vel[i];
+    for (int c = threadIdx.x; c <= ncol; c += SOLVE_TPB) scb[c] = cbase[c];
+    __syncthreads();
+    const int npc = scb[ncol];
+    const bool cached = npc <= segLds;
+    if (cached)
+        for (int q = threadIdx.x; q < npc; q += SOLVE_TPB) ss[q] = seg[q];
+    __syncthreads();
     for (int it = 0; it < iters; it++) {
         for (int c = 0; c < ncol; c++) {
-            const int q1 = cbase[c + 1];
-            for (int q = cbase[c] + threadIdx.x; q < q1; q += SOLVE_TPB) {
-                const int2 sg = seg[q];
-                for (int t = sg.x; t < sg.x + sg.y; t++) {
-                    float ln = it ? lamN[t] : 0.f, lf = it ? lamF[t] : 0.f;
-                    pgs_row_pair(rowN[t], rowR[t], rowM[t], rowAB[t], mu, ln, lf, sv);
-                    lamN[t] = ln; lamF[t] = lf;
+            const int q1 = scb[c + 1];
+            for (int q = scb[c] + threadIdx.x; q < q1; q += SOLVE_TPB) {
+                const int2 sg = cached ? ss[q] : seg[q];
+                float4 n[RB], r[RB], m[RB];
+                int2 ab[RB];
+                float ln[RB], lf[RB];
+#pragma unroll
+                for (int j = 0; j < RB; j++) {
+                    if (j < sg.y) {
+                        const int t = sg.x + j;
+                        n[j] = rowN[t]; r[j] = rowR[t]; m[j] = rowM[t]; ab[j] = rowAB[t];
+                        ln[j] = it ? lamN[t] : 0.f;
+                        lf[j] = it ? lamF[t] : 0.f;
+                    }
+                }
+#pragma unroll
+                for (int j = 0; j < RB; j++)
+                    if (j < sg.y) pgs_row_pair(n[j], r[j], m[j], ab[j], mu, ln[j], lf[j], sv);
+#pragma unroll
+                for (int j = 0; j < RB; j++)
+                    if (j < sg.y) { lamN[sg.x + j] = ln[j]; lamF[sg.x + j] = lf[j]; }
+                for (int t = sg.x + RB; t < sg.x + sg.y; t++) {     // pairs with > RB contacts
+                    float l0 = it ? lamN[t] : 0.f, l1 = it ? lamF[t] : 0.f;
+                    pgs_row_pair(rowN[t], rowR[t], rowM[t], rowAB[t], mu, l0, l1, sv);
+                    lamN[t] = l0; lamF[t] = l1;
                 }
             }
             __syncthreads();
@@ -1098,23 +1170,38 @@ __device__ __forceinline__ void pos_item(const PosRec &q, double *sp) {
 
 __global__ void __launch_bounds__(SOLVE_TPB)
 k_pos_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restrict__ cbase,
-             const int2 *__restrict__ seg, const PosRec *__restrict__ rec,
+             const int2 *__restrict__ seg, int segLds, const PosRec *__restrict__ rec,
              lpe_body *__restrict__ bodies, const double *__restrict__ st,
              const int32_t *__restrict__ inPos, int iters) {
-    extern __shared__ double sp[];   // x, y, angle per body
+    extern __shared__ double sp[];   // x, y, angle per body, then the segment cache
+    int2 *ss = (int2 *)(sp + 3 * nb);
+    __shared__ int scb[MAX_COLOURS + 1];
+    const int ncol = counts[8];
     for (int i = threadIdx.x; i < nb; i += SOLVE_TPB) {
         const lpe_body &b = bodies[i];
         sp[3 * i] = b.x; sp[3 * i + 1] = b.y;
         sp[3 * i + 2] = (b.flags & LPE_BODY_HAS_ANGPOS) ? b.angle : 0.0;
     }
+    for (int c = threadIdx.x; c <= ncol; c += SOLVE_TPB) scb[c] = cbase[c];
     __syncthreads();
-    const int ncol = counts[8];
+    const int npc = scb[ncol];
+    const bool cached = npc <= segLds;
+    if (cached)
+        for (int q = threadIdx.x; q < npc; q += SOLVE_TPB) ss[q] = seg[q];
+    __syncthreads();
     for (int it = 0; it < iters; it++) {
         for (int c = 0; c < ncol; c++) {
-            const int q1 = cbase[c + 1];
-            for (int q = cbase[c] + threadIdx.x; q < q1; q += SOLVE_TPB) {
-                const int2 sg = seg[q];
-                for (int t = sg.x; t < sg.x + sg.y; t++) pos_item(rec[t], sp);
+            const int q1 = scb[c + 1];
+            for (int q = scb[c] + threadIdx.x; q < q1; q += SOLVE_TPB) {
+                const int2 sg = cached ? ss[q] : seg[q];
+                PosRec r[RB];
+#pragma unroll
+                for (int j = 0; j < RB; j++)
+                    if (j < sg.y) r[j] = rec[sg.x + j];
+#pragma unroll
+                for (int j = 0; j < RB; j++)
+                    if (j < sg.y) pos_item(r[j], sp);
+                for (int t = sg.x + RB; t < sg.x + sg.y; t++) pos_item(rec[t], sp);
             }
             __syncthreads();
         }
@@ -1648,14 +1735,21 @@ static int rigid_solve(lpe_ctx *ctx, RigidDev *d, bool colour, const int32_t *pg
     int32_t *inPos = d->inContact + nb;
     if (colour) {
         // canonical order: colour-synchronous sweeps over the colour segments
-        size_t lds = sizeof(float) * 3 * (size_t)nb;
-        LPE_KERNEL(ctx, "k_pgs_colour", k_pgs_colour, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts, d->cbase, d->cseg, d->rowN, d->rowR, d->rowAB, d->rowM, d->vel0, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF);
+        // LDS: body state, then as many pair segments as fit (the coloured
+        // pairs are at most last_np)
+        const size_t ldsMax = 150 * 1024;
+        size_t lds = sizeof(float) * (3 * (size_t)nb + 1);
+        int segLds = (int)std::min<size_t>((size_t)d->last_np, (ldsMax - std::min(ldsMax, lds)) / sizeof(int2));
+        lds += sizeof(int2) * (size_t)segLds + 8;
+        LPE_KERNEL(ctx, "k_pgs_colour", k_pgs_colour, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts, d->cbase, d->cseg, segLds, d->rowN, d->rowR, d->rowAB, d->rowM, d->vel0, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF);
         LPE_KERNEL(ctx, "k_pgs_writeback", k_pgs_writeback, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->inContact);
         LPE_CHECK_LAUNCH(ctx, "pgs");
         LPE_KERNEL(ctx, "k_pos_bodies", k_pos_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->posState);
         LPE_KERNEL(ctx, "k_pos_fill_rows", k_pos_fill_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->order, d->contacts, d->bodies, d->posState, d->posRec, inPos, c.baumgarte, c.slop);
         size_t lds2 = sizeof(double) * 3 * (size_t)nb;
-        LPE_KERNEL(ctx, "k_pos_colour", k_pos_colour, dim3(1), dim3(SOLVE_TPB), lds2, s, nb, d->counts, d->cbase, d->cseg, d->posRec, d->bodies, d->posState, inPos, c.posIterations);
+        int segLds2 = (int)std::min<size_t>((size_t)d->last_np, (ldsMax - std::min(ldsMax, lds2)) / sizeof(int2));
+        lds2 += sizeof(int2) * (size_t)segLds2;
+        LPE_KERNEL(ctx, "k_pos_colour", k_pos_colour, dim3(1), dim3(SOLVE_TPB), lds2, s, nb, d->counts, d->cbase, d->cseg, segLds2, d->posRec, d->bodies, d->posState, inPos, c.posIterations);
         LPE_CHECK_LAUNCH(ctx, "position solver");
     } else {
         // caller-supplied order (reference replay): exact dataflow sweeps

@@ -54,7 +54,8 @@ static constexpr float PI_F = 3.14159265358979323846f;  // metal:17 evaluated in
 static constexpr int TPB = 256;
 static constexpr int SCAN_ELEMS = 1024;   // elements per scan block (256 thr x 4)
 static constexpr int MAX_KICK_BLOCKS = 2048;
-static constexpr int NLIST_CAP = 64;      // neighbours kept per particle (column-major list)
+static constexpr int NLIST_CAP = 128;     // neighbours kept per particle (column-major list)
+static constexpr int DTPB = 128;          // k_density block: its LDS list stage is NLIST_CAP x DTPB int16
 
 // kernel coefficients (metal:19-38), fp32
 __device__ __forceinline__ float poly6Coeff2D(float h) {
@@ -437,7 +438,7 @@ __device__ __forceinline__ float walk_reach(float h, float cs) {
 }
 
 // computeDensity (metal:246-307), one thread per sorted slot
-__global__ void __launch_bounds__(TPB)
+__global__ void __launch_bounds__(DTPB)
 k_density(int n, float h, float eps, float stiffness, float restDensity, int W, int H, int ox, int oy,
           const GridParams *__restrict__ gp, const int32_t *__restrict__ start,
           const float4 *__restrict__ nbA, float2 *__restrict__ nbB,
@@ -445,9 +446,9 @@ k_density(int n, float h, float eps, float stiffness, float restDensity, int W, 
           int32_t *__restrict__ ncount) {
     // neighbour list staged in LDS (column-major per block), written out
     // coalesced at the end: entry = k - s as int16
-    __shared__ int16_t lds_nl[NLIST_CAP * TPB];
-    int lb = xcd_block((n + TPB - 1) / TPB);
-    int s = lb * TPB + threadIdx.x;
+    __shared__ int16_t lds_nl[NLIST_CAP * DTPB];
+    int lb = xcd_block((n + DTPB - 1) / DTPB);
+    int s = lb * DTPB + threadIdx.x;
     if (lb < 0 || s >= n) return;
     const GridParams g = *gp;
     const float cs = g.cellSize;
@@ -472,7 +473,7 @@ k_density(int n, float h, float eps, float stiffness, float restDensity, int W, 
             if (k != s) {
                 int off = k - s;
                 if (cnt < NLIST_CAP && off >= -32768 && off <= 32767)
-                    lds_nl[cnt * TPB + tid] = (int16_t)off;
+                    lds_nl[cnt * DTPB + tid] = (int16_t)off;
                 else
                     cnt = NLIST_CAP;          // overflow: forces walks the bins
                 cnt++;
@@ -481,7 +482,7 @@ k_density(int n, float h, float eps, float stiffness, float restDensity, int W, 
     });
     ncount[s] = cnt;
     const int m = cnt <= NLIST_CAP ? cnt : 0;
-    for (int j = 0; j < m; j++) nlist[(size_t)j * n + s] = lds_nl[j * TPB + tid];
+    for (int j = 0; j < m; j++) nlist[(size_t)j * n + s] = lds_nl[j * DTPB + tid];
     float pres = stiffness * (acc - restDensity);
     if (pres < 0.f) pres = 0.f;
     rho[s] = acc;
@@ -493,6 +494,7 @@ struct SphStepParams {
     int n, W, H, ox, oy;
     float h, eps, dt, hdt;
     float viscosity, minDist, minDens;
+    int diag;                 // count diagnostics into status (lpe_sph_diag)
 };
 
 // computeForces + velocityVerletFinish + impulse + push-out; reads the sorted
@@ -503,7 +505,8 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                 const float4 *__restrict__ nbB, const float *__restrict__ pr,
                 const int16_t *__restrict__ nlist, const int32_t *__restrict__ ncount, PState P,
                 const lpe_gpu_rigid *__restrict__ rig, const int32_t *__restrict__ rbinStart,
-                const int32_t *__restrict__ rbinList, float *__restrict__ accum) {
+                const int32_t *__restrict__ rbinList, float *__restrict__ accum,
+                int32_t *__restrict__ status) {
     int lb = xcd_block((sp.n + TPB - 1) / TPB);
     int s = lb * TPB + threadIdx.x;
     if (lb < 0 || s >= sp.n) return;
@@ -552,6 +555,10 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         sumFy += fy;
     };
     const int cnt = ncount[s];
+    if (sp.diag) {
+        atomicAdd(&status[ST_NEIGH], cnt);
+        if (cnt > NLIST_CAP) atomicAdd(&status[ST_NL_OVERFLOW], 1);
+    }
     if (cnt <= NLIST_CAP) {
         // the density pass's list: the r^2 < h^2 neighbours in canonical
         // order, so the heavy pair math runs only on real neighbours
@@ -568,7 +575,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                 if (j + u < cnt) pair(kk[u], r[u]);
         }
     } else {
-        walk_neighbours<2>(xi, yi, sp.eps, cs, walk_reach(hi, cs), g, sp.W, sp.H, sp.ox, sp.oy, start,
+        walk_neighbours<4>(xi, yi, sp.eps, cs, walk_reach(hi, cs), g, sp.W, sp.H, sp.ox, sp.oy, start,
                            [&](int k) { return Rec{nbA[k], nbB[k]}; }, pair);
     }
     CoupleState st;
@@ -585,6 +592,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         float fby = fminf(fmaxf(floorf(st.y / cp.bcs) - (float)cp.by0, 0.f), (float)(cp.bH - 1));
         int bin = (int)fby * cp.bW + (int)fbx;
         k0 = rbinStart[bin]; k1 = rbinStart[bin + 1];
+        if (sp.diag && k1 > k0) atomicAdd(&status[ST_RIGID_CAND], k1 - k0);
         // impulse solver: dispatched only if R > 0 (fluid.cpp:910)
         couple_impulse(st, cp, sp.dt, rig, rbinList, k0, k1, accum);
     }
@@ -1079,7 +1087,7 @@ static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool pr
 static int sph_density(lpe_ctx *ctx) {
     SphDev &d = ctx->sph;
     const lpe_fluid_config &c = d.cfg;
-    LPE_KERNEL(ctx, "k_density", k_density, dim3(xcd_grid(nblk(d.n))), dim3(TPB), 0, ctx->stream, d.n,
+    LPE_KERNEL(ctx, "k_density", k_density, dim3(xcd_grid(nblk(d.n, DTPB))), dim3(DTPB), 0, ctx->stream, d.n,
                        c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
                        c.restDensity, d.W, d.H, d.ox, d.oy, d.gp, d.start, d.nbA, (float2 *)d.nbB,
                        d.rho, d.pr, d.nlist, d.ncount);
@@ -1108,6 +1116,7 @@ extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
     sp.viscosity = c.viscosity;
     sp.minDist = c.numericalConfig.minDistanceThreshold;
     sp.minDens = c.numericalConfig.minDensityThreshold;
+    sp.diag = d.diag;
     CoupleParams cp;
     sph_couple_params(d, cp);
     for (int step = 0; step < c.numSubSteps; step++) {
@@ -1117,7 +1126,7 @@ extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
         if (st) return st;
         LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(xcd_grid(nblk(d.n))), dim3(TPB), 0, s, sp, cp, d.gp,
                            d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.rbinStart, d.rbinList,
-                           d.accum);
+                           d.accum, d.status);
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
     }
     if (d.nr > 0) {
@@ -1219,6 +1228,19 @@ extern "C" int lpe_sph_get_stats(lpe_ctx *ctx, lpe_sph_stats *out) {
     out->gridDimX = g.gridDimX; out->gridDimY = g.gridDimY;
     out->gridMinX = g.gridMinX; out->gridMinY = g.gridMinY;
     out->cellSize = g.cellSize;
+    out->nlistOverflow = status[ST_NL_OVERFLOW];
+    out->rigidCandidates = status[ST_RIGID_CAND];
+    out->neighbours = status[ST_NEIGH];
+    return LPE_OK;
+}
+
+extern "C" int lpe_sph_diag(lpe_ctx *ctx, int on) {
+    if (!ctx) return LPE_ERR_ARG;
+    SphDev &d = ctx->sph;
+    d.diag = on ? 1 : 0;
+    if (d.status) {
+        LPE_HIP(ctx, hipMemsetAsync(d.status + ST_NL_OVERFLOW, 0, sizeof(int32_t) * 3, ctx->stream));
+    }
     return LPE_OK;
 }
 

@@ -71,7 +71,8 @@ class SphStats(C.Structure):
     _fields_ = [("maxCellOccupancy", C.c_int32), ("notInserted", C.c_int32),
                 ("capacityOverflow", C.c_int32), ("listOverflow", C.c_int32),
                 ("gridDimX", C.c_int32), ("gridDimY", C.c_int32),
-                ("gridMinX", C.c_int32), ("gridMinY", C.c_int32), ("cellSize", C.c_float)]
+                ("gridMinX", C.c_int32), ("gridMinY", C.c_int32), ("cellSize", C.c_float),
+                ("nlistOverflow", C.c_int32), ("rigidCandidates", C.c_int32), ("neighbours", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -166,6 +167,7 @@ SIGNATURES = {
     "lpe_sph_download_aux": ([C.c_void_p] + [_FP] * 4, C.c_int),
     "lpe_sph_download_rigids": ([C.c_void_p, C.c_void_p, _FP], C.c_int),
     "lpe_sph_get_stats": ([C.c_void_p, C.POINTER(SphStats)], C.c_int),
+    "lpe_sph_diag": ([C.c_void_p, C.c_int], C.c_int),
     "lpe_sph_probe_cells": ([C.c_void_p, _IP, C.POINTER(SphStats)], C.c_int),
     "lpe_sph_probe_density": ([C.c_void_p, _FP, _FP], C.c_int),
     "lpe_rigid_config_default": ([C.POINTER(RigidConfig)], C.c_int),
@@ -313,6 +315,9 @@ class Context:
         s = SphStats()
         self._chk(lib().lpe_sph_get_stats(self._h, C.byref(s)), "lpe_sph_get_stats")
         return s.as_dict()
+
+    def sph_diag(self, on=True):
+        self._chk(lib().lpe_sph_diag(self._h, int(on)), "lpe_sph_diag")
 
     def sph_probe_cells(self):
         cells = np.empty(self.n, np.int32)
