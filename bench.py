@@ -86,6 +86,44 @@ def cpu_baseline(scene_name, state=None, budget_s=20.0):
                        f"lpeo_world_tick), 1 thread, -O2")
 
 
+def density_microbench(lpe, scenes, device, side=4096, reps=5):
+    """SURVEY.md §8(d) density microbench: a side x side lattice (16.7M
+    particles at side 4096) in a U = 104 m universe, one density pass from a
+    pre-built grid (lpe_sph_probe_density: hash of the current positions, then
+    the LDS-staged computeDensity), timed with HIP events on the library's
+    stream; algorithmic bytes 24 B/particle + 8 B/cell (§8(d))."""
+    rng = np.random.default_rng(7)
+    U = 104.0
+    x0 = 0.5 * (U - side * scenes.LATTICE_S)
+    fl = scenes.fluid_lattice(rng, side, side, x0, x0)
+    ctx = lpe.Context(device)
+    try:
+        ctx.sph_set_config(lpe.default_fluid_config())
+        ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+        del fl
+        rho, _ = ctx.sph_probe_density()          # warm (code objects, caches)
+        ctx.sph_diag(True)                        # resets the stage-fallback counter
+        ctx.timing(2)
+        ctx.timing_reset()
+        for _ in range(reps):
+            rho, _ = ctx.sph_probe_density()
+        t = ctx.timing_read().get("k_density_staged")
+        ctx.timing(0)
+        st = ctx.sph_stats()
+    finally:
+        ctx.close()
+    n = side * side
+    cells = st["gridDimX"] * st["gridDimY"]
+    avg_s = t[0] / max(t[1], 1) / 1e3
+    b = 24.0 * n + 8.0 * cells
+    ach = b / avg_s / 1e9
+    return dict(kernel="k_density_staged", particles=n, cells=cells, avg_us=round(avg_s * 1e6, 1),
+                algorithmic_bytes=b, achieved=round(ach, 1), unit="GB/s", peak=HBM_PEAK_GBS,
+                frac=round(ach / HBM_PEAK_GBS, 4), launches=t[1],
+                stage_fallback_blocks=st["stageFallback"] // max(reps, 1),
+                mean_density=float(np.mean(rho)), max_cell_occupancy=st["maxCellOccupancy"])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -95,6 +133,7 @@ def main():
     ap.add_argument("--prep", type=int, default=240,
                     help="untimed ticks that settle the scene before warmup (the pile forms)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-density-microbench", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -154,6 +193,8 @@ def main():
     times = ctx.timing_read()
     ctx.timing(False)
     stats = ctx.sph_stats()
+    pairs, contacts = ctx.rigid_contacts()
+    _, ncolours = ctx.rigid_colours()
     out = ctx.sph_download()   # also checks the capacity / overflow flags
     settled = dict(fluid=out, bodies=ctx.rigid_download())
 
@@ -165,8 +206,12 @@ def main():
     assert np.isfinite(out["x"]).all() and np.isfinite(out["vy"]).all()
     n = len(fl["x"])
     cells = stats["gridDimX"] * stats["gridDimY"]
-    dom = max(times.items(), key=lambda kv: kv[1][0])
-    dname, (dms, dcalls) = dom
+    # the roofline kernel: the SPH kernel with the largest share of the tick
+    # (the rigid solvers are latency-bound single-workgroup sweeps with no
+    # byte model; they are reported in kernels_us)
+    modeled = {k: v for k, v in times.items() if kernel_bytes(k, n, cells) is not None}
+    dname, (dms, dcalls) = max(modeled.items(), key=lambda kv: kv[1][0])
+    overall = max(times.items(), key=lambda kv: kv[1][0])[0]
     avg_s = dms / max(dcalls, 1) / 1e3
     b = kernel_bytes(dname, n, cells)
     roof = None
@@ -208,8 +253,12 @@ def main():
         "roofline": roof,
         "roofline_density": roof_d,
         "kernels_us": {k: round(v[0] / max(v[1], 1) * 1e3, 2) for k, v in times.items()},
+        "dominant_kernel": overall,
         "max_cell_occupancy": stats["maxCellOccupancy"],
+        "rigid": {"pairs": int(len(pairs)), "contacts": int(len(contacts)), "colours": int(ncolours)},
     }
+    if world == 1 and not args.no_density_microbench:
+        line["density_microbench"] = density_microbench(lpe, scenes, local)
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.scene, settled)
     print(json.dumps(line))

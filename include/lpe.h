@@ -131,6 +131,8 @@ typedef struct lpe_sph_stats {
     int32_t nlistOverflow;      /* particles whose neighbour list exceeded 64  */
     int32_t rigidCandidates;    /* rigids tested by the coupling solvers       */
     int32_t neighbours;         /* neighbours with r < h found by the density pass */
+    int32_t stageFallback;      /* blocks of the LDS-staged density pass (lpe_sph_probe_density)
+                                   whose neighbourhood did not fit LDS (always counted) */
 } lpe_sph_stats;
 
 /* ------------------------------------------------------------------------ */

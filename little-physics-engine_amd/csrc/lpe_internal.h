@@ -83,6 +83,7 @@ enum StatusSlot {
     ST_NL_OVERFLOW = 4,     // diag: particles whose neighbour list overflowed (forces walk the bins)
     ST_RIGID_CAND = 5,      // diag: rigid candidates tested by the coupling (sum over particles)
     ST_NEIGH = 6,           // diag: neighbours (r < h) found by the density pass (sum)
+    ST_STAGE_FALLBACK = 7,  // staged density blocks whose neighbourhood did not fit LDS
     ST_COUNT = 16
 };
 

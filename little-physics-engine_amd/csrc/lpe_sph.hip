@@ -363,8 +363,8 @@ __device__ __forceinline__ int sel4(int4 v, int i) {
 // The walk issues every bin-boundary load of the (at most 3x3) cells up front
 // and the candidate records U at a time, so a wave has many loads in flight
 // (the loop is latency bound otherwise: one dependent L2 round trip per
-// candidate).  ld(k) loads candidate k's record, f(k, rec) consumes it; f is
-// called in the canonical order.
+// candidate).  ld(k, cy) loads candidate k's record (cy: the absolute cell
+// row being walked), f(k, rec) consumes it; f is called in the canonical order.
 template <int U, class L, class F>
 __device__ __forceinline__ void walk_neighbours(float xi, float yi, float eps, float cs,
                                                 float reach, const GridParams &g, int W, int H,
@@ -410,9 +410,9 @@ __device__ __forceinline__ void walk_neighbours(float xi, float yi, float eps, f
                 int b = sel4(q[dy][dx], i0);
                 int e = (i1 == 4) ? qn[dy][dx] : sel4(q[dy][dx], i1);
                 for (int k = b; k < e; k += U) {
-                    decltype(ld(0)) r[U];
+                    decltype(ld(0, 0)) r[U];
 #pragma unroll
-                    for (int j = 0; j < U; j++) r[j] = ld(min(k + j, e - 1));
+                    for (int j = 0; j < U; j++) r[j] = ld(min(k + j, e - 1), cy);
 #pragma unroll
                     for (int j = 0; j < U; j++)
                         if (k + j < e) f(k + j, r[j]);
@@ -460,7 +460,7 @@ k_density(int n, float h, float eps, float stiffness, float restDensity, int W, 
     float acc = 0.0f;
     int cnt = 0;
     walk_neighbours<4>(xi, yi, eps, cs, walk_reach(h, cs), g, W, H, ox, oy, start,
-                       [&](int k) { return nbA[k]; },
+                       [&](int k, int) { return nbA[k]; },
                        [&](int k, const float4 &o) {
         float dx = xi - o.x, dy = yi - o.y;
         float r2 = dx * dx + dy * dy;
@@ -483,6 +483,142 @@ k_density(int n, float h, float eps, float stiffness, float restDensity, int W, 
     ncount[s] = cnt;
     const int m = cnt <= NLIST_CAP ? cnt : 0;
     for (int j = 0; j < m; j++) nlist[(size_t)j * n + s] = lds_nl[j * DTPB + tid];
+    float pres = stiffness * (acc - restDensity);
+    if (pres < 0.f) pres = 0.f;
+    rho[s] = acc;
+    pr[s] = pres;
+    nbB[2 * s + 1] = make_float2(acc, pres / (acc * acc));   // the p_j / rho_j^2 of metal:370
+}
+
+// ---------------------------------------------------------------------------
+// computeDensity with LDS-staged neighbourhoods (the density probe and the
+// 16M-particle microbench: a pure density pass, no neighbour list).  A block
+// owns SB consecutive sorted slots; in sorted order they cover at most two
+// runs of cells in two adjacent cell rows (unless the fluid is sparse), so
+// every record the block's walks can touch lies in <= 6 contiguous slot
+// ranges: rows cy-1..cy+1 of each run, one cell left and right of it.  The
+// block copies them into LDS with coalesced loads and the walks read LDS
+// instead of L2; the walk itself, and so every sum, is unchanged.  A block
+// whose neighbourhood does not fit reads global memory.
+static constexpr int SB = 128;            // slots per block of the staged kernel
+static constexpr int STAGE_CAP = 1536;    // records staged per block
+
+struct Stage {
+    int ok;                  // neighbourhood staged in LDS
+    int cy0, cy1;            // cell rows of run 0 / run 1 (cy1 == cy0: one run)
+    int cxa[2], cxb[2];      // cell columns of each run
+    int segS[6], segE[6];    // slot range of segment r*3 + (dy+1)
+    int segL[6];             // LDS offset of each segment
+};
+
+__device__ __forceinline__ void cell_xy(float x, float y, float eps, float cs, int &cx, int &cy) {
+    cx = (int)floorf((x + eps) / cs);
+    cy = (int)floorf((y + eps) / cs);
+}
+
+// Plans st (block-uniform) for slots [s0, s1); every thread of the block
+// calls it (it holds barriers).
+__device__ void stage_plan(Stage &st, int s0, int s1, const float4 *__restrict__ nbA, float eps,
+                           float cs, int W, int H, int ox, int oy, const int32_t *__restrict__ start) {
+    const int tid = threadIdx.x;
+    if (tid == 0) {
+        st.ok = 0;
+        if (s1 > s0) {
+            int cx, cy, lx, ly;
+            float4 f = nbA[s0], l = nbA[s1 - 1];
+            cell_xy(f.x, f.y, eps, cs, cx, cy);
+            cell_xy(l.x, l.y, eps, cs, lx, ly);
+            st.cy0 = cy; st.cy1 = ly;
+            st.cxa[0] = cx; st.cxb[0] = -0x7fffffff;
+            st.cxa[1] = 0x7fffffff; st.cxb[1] = lx;
+            st.ok = (ly - cy <= 1) ? 1 : 0;
+        }
+    }
+    __syncthreads();
+    const int s = s0 + tid;
+    if (st.ok && s < s1) {
+        int cx, cy;
+        float4 me = nbA[s];
+        cell_xy(me.x, me.y, eps, cs, cx, cy);
+        if (cy == st.cy0) atomicMax(&st.cxb[0], cx);
+        if (cy == st.cy1 && st.cy1 != st.cy0) atomicMin(&st.cxa[1], cx);
+    }
+    __syncthreads();
+    if (st.ok && tid < 6) {                 // one segment per thread
+        const int r = tid / 3, dy = tid % 3 - 1;
+        int b = 0, e = 0;
+        if (r == 0 || st.cy1 != st.cy0) {
+            const int row = (r ? st.cy1 : st.cy0) + dy - oy;
+            const int kxa = max(st.cxa[r] - 1 - ox, 0), kxb = min(st.cxb[r] + 1 - ox, W - 1);
+            if (row >= 0 && row < H && kxa <= kxb) {
+                b = start[(row * W + kxa) << 2];
+                e = start[((row * W + kxb) << 2) + 4];
+            }
+        }
+        st.segS[tid] = b;
+        st.segE[tid] = e;
+    }
+    __syncthreads();
+    if (tid == 0 && st.ok) {
+        int off = 0;
+        for (int i = 0; i < 6; i++) { st.segL[i] = off; off += st.segE[i] - st.segS[i]; }
+        if (off > STAGE_CAP) st.ok = 0;
+    }
+    __syncthreads();
+}
+
+// LDS index of candidate slot k walked in cell row cyc by a particle of row cyp
+__device__ __forceinline__ int stage_index(const Stage &st, int k, int cyc, int cyp) {
+    const int i = (cyp == st.cy0 ? 0 : 3) + (cyc - cyp + 1);
+    return st.segL[i] + (k - st.segS[i]);
+}
+
+__global__ void __launch_bounds__(SB)
+k_density_staged(int n, float h, float eps, float stiffness, float restDensity, int W, int H, int ox,
+                 int oy, const GridParams *__restrict__ gp, const int32_t *__restrict__ start,
+                 const float4 *__restrict__ nbA, float2 *__restrict__ nbB, float *__restrict__ rho,
+                 float *__restrict__ pr, int32_t *__restrict__ status) {
+    __shared__ Stage st;
+    __shared__ float4 lrec[STAGE_CAP];
+    const int lb = xcd_block((n + SB - 1) / SB);
+    if (lb < 0) return;                                   // whole block idle
+    const int s0 = lb * SB, s1 = min(s0 + SB, n);
+    const GridParams g = *gp;
+    const float cs = g.cellSize;
+    stage_plan(st, s0, s1, nbA, eps, cs, W, H, ox, oy, start);
+    if (st.ok) {
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            const int b = st.segS[i], len = st.segE[i] - b, o = st.segL[i];
+            for (int j = threadIdx.x; j < len; j += SB) lrec[o + j] = nbA[b + j];
+        }
+    }
+    __syncthreads();
+    const int s = s0 + threadIdx.x;
+    if (s >= s1) return;
+    if (!st.ok && threadIdx.x == 0) atomicAdd(&status[ST_STAGE_FALLBACK], 1);
+    const float4 me = nbA[s];
+    const float xi = me.x, yi = me.y;
+    int cxp, cyp;
+    cell_xy(xi, yi, eps, cs, cxp, cyp);
+    const float h2 = h * h;
+    const float poly6 = poly6Coeff2D(h);
+    float acc = 0.0f;
+    auto body = [&](int, const float4 &o) {
+        float dx = xi - o.x, dy = yi - o.y;
+        float r2 = dx * dx + dy * dy;
+        if (r2 < h2) {
+            float diff = h2 - r2;
+            float w = poly6 * diff * diff * diff;
+            acc += o.z * w;
+        }
+    };
+    if (st.ok)
+        walk_neighbours<4>(xi, yi, eps, cs, walk_reach(h, cs), g, W, H, ox, oy, start,
+                           [&](int k, int cyc) { return lrec[stage_index(st, k, cyc, cyp)]; }, body);
+    else
+        walk_neighbours<4>(xi, yi, eps, cs, walk_reach(h, cs), g, W, H, ox, oy, start,
+                           [&](int k, int) { return nbA[k]; }, body);
     float pres = stiffness * (acc - restDensity);
     if (pres < 0.f) pres = 0.f;
     rho[s] = acc;
@@ -576,7 +712,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         }
     } else {
         walk_neighbours<4>(xi, yi, sp.eps, cs, walk_reach(hi, cs), g, sp.W, sp.H, sp.ox, sp.oy, start,
-                           [&](int k) { return Rec{nbA[k], nbB[k]}; }, pair);
+                           [&](int k, int) { return Rec{nbA[k], nbB[k]}; }, pair);
     }
     CoupleState st;
     st.x = xi; st.y = yi;
@@ -1231,6 +1367,7 @@ extern "C" int lpe_sph_get_stats(lpe_ctx *ctx, lpe_sph_stats *out) {
     out->nlistOverflow = status[ST_NL_OVERFLOW];
     out->rigidCandidates = status[ST_RIGID_CAND];
     out->neighbours = status[ST_NEIGH];
+    out->stageFallback = status[ST_STAGE_FALLBACK];
     return LPE_OK;
 }
 
@@ -1239,7 +1376,7 @@ extern "C" int lpe_sph_diag(lpe_ctx *ctx, int on) {
     SphDev &d = ctx->sph;
     d.diag = on ? 1 : 0;
     if (d.status) {
-        LPE_HIP(ctx, hipMemsetAsync(d.status + ST_NL_OVERFLOW, 0, sizeof(int32_t) * 3, ctx->stream));
+        LPE_HIP(ctx, hipMemsetAsync(d.status + ST_NL_OVERFLOW, 0, sizeof(int32_t) * 4, ctx->stream));
     }
     return LPE_OK;
 }
@@ -1269,8 +1406,13 @@ extern "C" int lpe_sph_probe_density(lpe_ctx *ctx, float *density, float *pressu
     (void)hipSetDevice(ctx->device);
     int st = sph_hash(ctx, 0.f, 0.f, false, true);
     if (st) return st;
-    st = sph_density(ctx);
-    if (st) return st;
+    const lpe_fluid_config &c = d.cfg;
+    // computeDensity alone (no neighbour list): the LDS-staged pass
+    LPE_KERNEL(ctx, "k_density_staged", k_density_staged, dim3(xcd_grid(nblk(d.n, SB))), dim3(SB), 0,
+               ctx->stream, d.n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
+               c.restDensity, d.W, d.H, d.ox, d.oy, d.gp, d.start, d.nbA, (float2 *)d.nbB, d.rho,
+               d.pr, d.status);
+    LPE_CHECK_LAUNCH(ctx, "k_density_staged");
     // rho/p are in S slot order here; S.x.. are the unpermute staging buffers,
     // so keep S.id aside in tmpOld first
     LPE_HIP(ctx, hipMemcpyAsync(d.tmpOld, d.S.id, sizeof(int32_t) * d.n, hipMemcpyDeviceToDevice,

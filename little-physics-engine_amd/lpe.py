@@ -72,7 +72,8 @@ class SphStats(C.Structure):
                 ("capacityOverflow", C.c_int32), ("listOverflow", C.c_int32),
                 ("gridDimX", C.c_int32), ("gridDimY", C.c_int32),
                 ("gridMinX", C.c_int32), ("gridMinY", C.c_int32), ("cellSize", C.c_float),
-                ("nlistOverflow", C.c_int32), ("rigidCandidates", C.c_int32), ("neighbours", C.c_int32)]
+                ("nlistOverflow", C.c_int32), ("rigidCandidates", C.c_int32), ("neighbours", C.c_int32),
+                ("stageFallback", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
