@@ -500,8 +500,8 @@ k_density(int n, float h, float eps, float stiffness, float restDensity, int W, 
 // block copies them into LDS with coalesced loads and the walks read LDS
 // instead of L2; the walk itself, and so every sum, is unchanged.  A block
 // whose neighbourhood does not fit reads global memory.
-static constexpr int SB = 128;            // slots per block of the staged kernel
-static constexpr int STAGE_CAP = 1536;    // records staged per block
+static constexpr int SB = 512;            // slots per block of the staged kernel
+static constexpr int STAGE_CAP = 4096;    // records staged per block (64 KB)
 
 struct Stage {
     int ok;                  // neighbourhood staged in LDS
