@@ -28,7 +28,7 @@ build/%.o: $(PKG)/csrc/%.hip $(HIP_HDR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(HIP_OBJ)
-	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -Wl,-rpath,/opt/rocm/lib
+	$(HIPCC) --offload-arch=$(ARCH) -shared -fPIC -o $@ $^ -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 
 build/oracle/%.o: oracle/%.c oracle/*.h include/lpe.h
 	@mkdir -p build/oracle

@@ -364,6 +364,43 @@ int  lpe_world_set_coupling(lpe_ctx *ctx, int nr, const int32_t *body_index);
  * fluid.cpp:496-524 leaves it. */
 int  lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *cfg, int nticks);
 
+/* ---- x-slab decomposition of the SPH step -----------
+ * The reference has one FluidSystem per process (fluid.cpp:958-1021); these
+ * entry points split its particle set over ranks by x slab.  Each rank owns
+ * the particles with x in [x0, x1) (the first slab has no left edge, the last
+ * no right edge) and runs lpe_sph_step on them; per sub-step it receives the
+ * neighbours' particles within `halo` of its edges (ghosts, with their global
+ * ids, so every density/force sum is the single-domain one bit for bit) and,
+ * after the density pass, their owners' density and pressure.  The reference
+ * grid is derived from the all-reduced bbox of all ranks.  Once per tick the
+ * rigid accumulators are all-reduced (rank order) before the write-back and
+ * particles that left the slab move to the neighbour.  halo must cover the
+ * smoothing length plus one tick's drift; ghost_cap bounds the ghosts and
+ * migrants per side (overflow: LPE_ERR_OVERFLOW from the next download). */
+/* Call before lpe_sph_upload (the particle arrays get owned + ghost slots). */
+int  lpe_sph_set_slab(lpe_ctx *ctx, float x0, float x1, float halo, int has_left,
+                      int has_right, int ghost_cap);
+/* Global particle ids of the n uploaded (owned) particles (default 0..n-1). */
+int  lpe_sph_set_ids(lpe_ctx *ctx, int n, const int32_t *ids);
+/* The particles this context owns, in device order, with their global ids
+ * (*n_out = count; LPE_ERR_CAPACITY if it exceeds cap).  Also valid without
+ * a slab (ids 0..n-1 permuted). */
+int  lpe_sph_download_owned(lpe_ctx *ctx, int cap, float *x, float *y, float *vx, float *vy,
+                            float *density, float *pressure, int32_t *ids, int *n_out);
+/* Grow the device grid (fixed absolute cell grid, sized at upload from the
+ * particles) to cover [x0, x1] x [y0, y1]: a slab rank sees particles of the
+ * whole domain only as ghosts and migrants.  Call after lpe_sph_upload. */
+int  lpe_sph_set_domain(lpe_ctx *ctx, double x0, double y0, double x1, double y1);
+/* RCCL transport (one process per GPU, rank r of n, neighbours r-1 / r+1):
+ * rank 0 creates the 128-byte id, every rank passes it to lpe_mg_init_rccl. */
+int  lpe_mg_unique_id(char id[128]);
+int  lpe_mg_init_rccl(lpe_ctx *ctx, int nranks, int rank, const char *id);
+/* In-process transport for tests: n contexts (ranks 0..n-1, any devices)
+ * each advanced nticks by its own host thread — lpe_world_tick(cfg, 1) per
+ * tick when cfg is non-NULL, else lpe_sph_step(dt_tick). */
+int  lpe_mg_loopback_run(int n, lpe_ctx **ctxs, const lpe_world_config *cfg, double dt_tick,
+                         int nticks);
+
 #ifdef __cplusplus
 }
 #endif

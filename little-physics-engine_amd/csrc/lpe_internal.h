@@ -29,6 +29,8 @@ struct PState {
     int32_t *id = nullptr;
 };
 
+struct Shard;
+
 struct SphDev {
     int n = 0, cap_n = 0;
     PState P;                     // primary state (sorted order of the last sub-step)
@@ -72,6 +74,7 @@ struct SphDev {
     bool cfg_set = false;
     bool rig_dirty = true;
     int diag = 0;                 // count the ST_NL_OVERFLOW / ST_RIGID_CAND / ST_NEIGH stats
+    struct Shard *shard = nullptr;// x-slab decomposition state (lpe_sph_set_slab), else single domain
 };
 
 // status slots
@@ -84,6 +87,7 @@ enum StatusSlot {
     ST_RIGID_CAND = 5,      // diag: rigid candidates tested by the coupling (sum over particles)
     ST_NEIGH = 6,           // diag: neighbours (r < h) found by the density pass (sum)
     ST_STAGE_FALLBACK = 7,  // staged density blocks whose neighbourhood did not fit LDS
+    ST_HALO_OVERFLOW = 8,   // slab decomposition: a ghost / migrant buffer overflowed
     ST_COUNT = 16
 };
 
@@ -106,7 +110,10 @@ struct KernelTimer {
 };
 }  // namespace lpe
 
+namespace lpe { struct Transport; }
+
 struct lpe_ctx {
+    lpe::Transport *transport = nullptr;   // slab decomposition (lpe_transport.hip)
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;

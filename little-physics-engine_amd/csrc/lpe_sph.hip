@@ -43,6 +43,7 @@
 // reference's own atomics, metal:892-898).
 #include "lpe_internal.h"
 #include "sph_coupling.h"
+#include "lpe_transport.h"
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -204,7 +205,8 @@ k_scan_reduce(int C, const int32_t *__restrict__ cnt, int32_t *__restrict__ bsum
 __global__ void __launch_bounds__(TPB)
 k_scan_blocks(int nb, int32_t *__restrict__ bsum, int32_t *__restrict__ start_last,
               const float4 *__restrict__ bboxPart, int nparts, float cs,
-              GridParams *__restrict__ gp, int32_t *__restrict__ status) {
+              GridParams *__restrict__ gp, int32_t *__restrict__ status,
+              const float4 *__restrict__ bbG) {
     int carry = 0;
     for (int b0 = 0; b0 < nb; b0 += TPB) {
         int b = b0 + threadIdx.x;
@@ -217,7 +219,13 @@ k_scan_blocks(int nb, int32_t *__restrict__ bsum, int32_t *__restrict__ start_la
     if (threadIdx.x == 0) *start_last = carry;
     if (!gp) return;
     float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
-    for (int p = threadIdx.x; p < nparts; p += TPB) {
+    if (bbG && threadIdx.x == 0) {
+        // slab decomposition: the all-reduced bbox of every rank's particles
+        // (stored as minX, minY, -maxX, -maxY for one MIN all-reduce)
+        float4 b = *bbG;
+        mnx = b.x; mny = b.y; mxx = -b.z; mxy = -b.w;
+    }
+    for (int p = threadIdx.x; p < (bbG ? 0 : nparts); p += TPB) {
         float4 b = bboxPart[p];
         mnx = fminf(mnx, b.x); mxx = fmaxf(mxx, b.y);
         mny = fminf(mny, b.z); mxy = fmaxf(mxy, b.w);
@@ -304,9 +312,9 @@ k_scan_final(int C, int W, int ox, int oy, int32_t *__restrict__ cnt,
 __global__ void __launch_bounds__(TPB)
 k_scatter(int n, const uint32_t *__restrict__ key, const int32_t *__restrict__ id,
           int32_t *__restrict__ cursor, int32_t *__restrict__ tmpId,
-          int32_t *__restrict__ tmpOld) {
+          int32_t *__restrict__ tmpOld, const int32_t *__restrict__ nptr) {
     int i = blockIdx.x * TPB + threadIdx.x;
-    bool active = i < n;
+    bool active = i < (nptr ? *nptr : n);
     uint32_t k = active ? key[i] : 0xFFFFFFFFu;
     int len; bool st;
     int first = wave_runs(k, active, &len, &st);
@@ -328,9 +336,10 @@ __global__ void __launch_bounds__(TPB)
 k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restrict__ start,
                const int32_t *__restrict__ tmpId, const int32_t *__restrict__ tmpOld,
                PState P, PState S, float4 *__restrict__ nbA, float2 *__restrict__ nbB,
-               int probe) {
+               int probe, const int32_t *__restrict__ nptr, int nown, int32_t *__restrict__ inv,
+               int32_t *__restrict__ owned) {
     int s = blockIdx.x * TPB + threadIdx.x;
-    if (s >= n) return;
+    if (s >= (nptr ? *nptr : n)) return;
     int o = tmpOld[s];
     int myid = tmpId[s];
     uint32_t k = key[o];
@@ -342,6 +351,10 @@ k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restric
     nbB[2 * d] = make_float2(P.vx[o], P.vy[o]);
     S.id[d] = myid;
     if (!probe) { S.vhx[d] = P.vhx[o]; S.vhy[d] = P.vhy[o]; }
+    if (inv) {                    // slab decomposition: P slot -> sorted slot, owned flags
+        inv[o] = d;
+        owned[d] = o < nown ? 1 : 0;
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -439,7 +452,8 @@ __device__ __forceinline__ float walk_reach(float h, float cs) {
 
 // computeDensity (metal:246-307), one thread per sorted slot
 __global__ void __launch_bounds__(DTPB)
-k_density(int n, float h, float eps, float stiffness, float restDensity, int W, int H, int ox, int oy,
+k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float eps, float stiffness,
+          float restDensity, int W, int H, int ox, int oy,
           const GridParams *__restrict__ gp, const int32_t *__restrict__ start,
           const float4 *__restrict__ nbA, float2 *__restrict__ nbB,
           float *__restrict__ rho, float *__restrict__ pr, int16_t *__restrict__ nlist,
@@ -449,7 +463,7 @@ k_density(int n, float h, float eps, float stiffness, float restDensity, int W, 
     __shared__ int16_t lds_nl[NLIST_CAP * DTPB];
     int lb = xcd_block((n + DTPB - 1) / DTPB);
     int s = lb * DTPB + threadIdx.x;
-    if (lb < 0 || s >= n) return;
+    if (lb < 0 || s >= (nptr ? *nptr : n)) return;
     const GridParams g = *gp;
     const float cs = g.cellSize;
     const float4 me = nbA[s];
@@ -482,7 +496,7 @@ k_density(int n, float h, float eps, float stiffness, float restDensity, int W, 
     });
     ncount[s] = cnt;
     const int m = cnt <= NLIST_CAP ? cnt : 0;
-    for (int j = 0; j < m; j++) nlist[(size_t)j * n + s] = lds_nl[j * DTPB + tid];
+    for (int j = 0; j < m; j++) nlist[(size_t)j * nstride + s] = lds_nl[j * DTPB + tid];
     float pres = stiffness * (acc - restDensity);
     if (pres < 0.f) pres = 0.f;
     rho[s] = acc;
@@ -627,6 +641,10 @@ k_density_staged(int n, float h, float eps, float stiffness, float restDensity, 
 }
 
 struct SphStepParams {
+    const int32_t *nptr;      // slab decomposition: device slot count (owned + ghosts), else null
+    const int32_t *dst;       // slab decomposition: exclusive scan of the owned flags, else null
+    float *orho, *opr;        // slab decomposition: rho / p of the owned particles in P order
+    int nstride;              // neighbour-list stride (allocated slots)
     int n, W, H, ox, oy;
     float h, eps, dt, hdt;
     float viscosity, minDist, minDens;
@@ -645,7 +663,12 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                 int32_t *__restrict__ status) {
     int lb = xcd_block((sp.n + TPB - 1) / TPB);
     int s = lb * TPB + threadIdx.x;
-    if (lb < 0 || s >= sp.n) return;
+    if (lb < 0 || s >= (sp.nptr ? *sp.nptr : sp.n)) return;
+    int out = s;                              // P slot written
+    if (sp.dst) {                             // ghosts are neighbours only
+        out = sp.dst[s];
+        if (sp.dst[s + 1] == out) return;
+    }
     const GridParams g = *gp;
     const float cs = g.cellSize;
     const float4 meA = nbA[s], meB = nbB[s];
@@ -702,7 +725,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         for (int j = 0; j < cnt; j += U) {
             int kk[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) kk[u] = s + nlist[(size_t)min(j + u, cnt - 1) * sp.n + s];
+            for (int u = 0; u < U; u++) kk[u] = s + nlist[(size_t)min(j + u, cnt - 1) * sp.nstride + s];
             Rec r[U];
 #pragma unroll
             for (int u = 0; u < U; u++) r[u] = Rec{nbA[kk[u]], nbB[kk[u]]};
@@ -733,11 +756,226 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         couple_impulse(st, cp, sp.dt, rig, rbinList, k0, k1, accum);
     }
     couple_position(st, cp, rig, rbinList, k0, k1);
-    P.x[s] = st.x; P.y[s] = st.y;
-    P.vx[s] = st.vx; P.vy[s] = st.vy;
-    P.vhx[s] = st.vhx; P.vhy[s] = st.vhy;
-    P.ax[s] = st.ax; P.ay[s] = st.ay;
-    P.m[s] = st.mass; P.id[s] = S.id[s];
+    P.x[out] = st.x; P.y[out] = st.y;
+    P.vx[out] = st.vx; P.vy[out] = st.vy;
+    P.vhx[out] = st.vhx; P.vhy[out] = st.vhy;
+    P.ax[out] = st.ax; P.ay[out] = st.ay;
+    P.m[out] = st.mass; P.id[out] = S.id[s];
+    if (sp.orho) { sp.orho[out] = rhoi; sp.opr[out] = pi; }
+}
+
+// ---------------------------------------------------------------------------
+// x-slab decomposition.  A rank owns the particles of the
+// slab [x0, x1) (the first/last slab extend to -inf/+inf).  Per sub-step:
+//   kick owned -> all-reduce the bbox (MIN of minX, minY, -maxX, -maxY: the
+//   reference grid is the global one) -> ghosts: owned particles within D of
+//   a slab edge go to that neighbour with their global id (so the canonical
+//   in-bin order, and every sum, is the single-domain one) -> sort owned +
+//   ghosts -> density -> the owners send the ghosts' (rho, p/rho^2) (a ghost's
+//   own density is only right where all its neighbours are present) ->
+//   forces/finish/coupling on owned slots only, compacted back to P.
+// Once per tick: the rigid accumulators are all-reduced (SUM) before the
+// write-back, then particles that left the slab migrate to the neighbour.
+// D must cover h plus the drift of a tick (0.3 m default; ST_HALO_OVERFLOW
+// flags buffers that overflowed).
+static constexpr int GREC = 8;    // floats per ghost record: x, y, vx, vy, m, id, -, -
+static constexpr int MREC = 8;    // floats per migrant: x, y, vx, vy, m, id, rho, p
+static constexpr int HDR = 4;     // header floats of an exchange buffer ([0]: count, int)
+
+struct Shard {
+    float x0 = 0.f, x1 = 0.f, D = 0.f;
+    int hasL = 0, hasR = 0;
+    int cap = 0;                       // ghosts / migrants per side
+    int32_t *ntot = nullptr;           // device: owned + ghosts of the sub-step
+    float *gsL = nullptr, *gsR = nullptr, *grL = nullptr, *grR = nullptr;
+    int32_t *sendSlot = nullptr;       // [2 cap] P slot of each sent ghost
+    float *rsL = nullptr, *rsR = nullptr, *rrL = nullptr, *rrR = nullptr;
+    float *msL = nullptr, *msR = nullptr, *mrL = nullptr, *mrR = nullptr;
+    float4 *bb = nullptr;              // global bbox
+    int cap_slots = 0;                 // per-slot arrays below
+    int32_t *inv = nullptr, *owned = nullptr, *dst = nullptr, *keep = nullptr, *kdst = nullptr;
+    int32_t *obsum = nullptr;
+    float *orho = nullptr, *opr = nullptr;   // rho / p of the owned particles, P order
+};
+
+__global__ void __launch_bounds__(TPB)
+k_bbox_reduce(const float4 *__restrict__ part, int nparts, float4 *__restrict__ bb) {
+    float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
+    for (int p = threadIdx.x; p < nparts; p += TPB) {
+        float4 b = part[p];
+        mnx = fminf(mnx, b.x); mxx = fmaxf(mxx, b.y);
+        mny = fminf(mny, b.z); mxy = fmaxf(mxy, b.w);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        mnx = fminf(mnx, __shfl_xor(mnx, off));
+        mxx = fmaxf(mxx, __shfl_xor(mxx, off));
+        mny = fminf(mny, __shfl_xor(mny, off));
+        mxy = fmaxf(mxy, __shfl_xor(mxy, off));
+    }
+    __shared__ float4 wb[TPB / 64];
+    if (lane_id() == 0) wb[threadIdx.x >> 6] = make_float4(mnx, mxx, mny, mxy);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float4 b = wb[0];
+        for (int w = 1; w < TPB / 64; w++) {
+            b.x = fminf(b.x, wb[w].x); b.y = fmaxf(b.y, wb[w].y);
+            b.z = fminf(b.z, wb[w].z); b.w = fmaxf(b.w, wb[w].w);
+        }
+        *bb = make_float4(b.x, b.z, -b.y, -b.w);
+    }
+}
+
+__device__ __forceinline__ int *hdr(float *buf) { return (int *)buf; }
+__device__ __forceinline__ int rcount(const float *buf, int cap) {
+    return buf ? min(*(const int *)buf, cap) : 0;
+}
+
+__global__ void k_ghost_pack(int n, PState P, float x0, float x1, float D, int hasL, int hasR,
+                             float *__restrict__ sL, float *__restrict__ sR,
+                             int32_t *__restrict__ sendSlot, int cap, int32_t *__restrict__ status) {
+    int i = blockIdx.x * TPB + threadIdx.x;
+    if (i >= n) return;
+    const float x = P.x[i];
+    for (int side = 0; side < 2; side++) {
+        const bool go = side == 0 ? (hasL && x < x0 + D) : (hasR && x >= x1 - D);
+        if (!go) continue;
+        float *buf = side == 0 ? sL : sR;
+        int k = atomicAdd(hdr(buf), 1);
+        if (k >= cap) { atomicOr(&status[ST_HALO_OVERFLOW], 1); continue; }
+        float *r = buf + HDR + (size_t)k * GREC;
+        r[0] = x; r[1] = P.y[i]; r[2] = P.vx[i]; r[3] = P.vy[i];
+        r[4] = P.m[i]; r[5] = __int_as_float(P.id[i]);
+        sendSlot[side * cap + k] = i;
+    }
+}
+
+// ghosts -> P[nown ...] (left ones first), bin key + histogram
+__global__ void k_ghost_unpack(const float *__restrict__ rL, const float *__restrict__ rR, int cap,
+                               int nown, PState P, uint32_t *__restrict__ key,
+                               int32_t *__restrict__ count, float eps, float cs, int ox, int oy,
+                               int W, int H, int32_t *__restrict__ ntot, int32_t *__restrict__ status) {
+    const int t = blockIdx.x * TPB + threadIdx.x;
+    const int gL = rcount(rL, cap), gR = rcount(rR, cap);
+    if (t == 0) *ntot = nown + gL + gR;
+    const float *src;
+    int slot;
+    if (t < cap) {
+        if (t >= gL) return;
+        src = rL + HDR + (size_t)t * GREC;
+        slot = nown + t;
+    } else {
+        const int k = t - cap;
+        if (k >= gR) return;
+        src = rR + HDR + (size_t)k * GREC;
+        slot = nown + gL + k;
+    }
+    const float px = src[0], py = src[1];
+    P.x[slot] = px; P.y[slot] = py; P.vx[slot] = src[2]; P.vy[slot] = src[3];
+    P.vhx[slot] = src[2]; P.vhy[slot] = src[3];
+    P.m[slot] = src[4]; P.id[slot] = __float_as_int(src[5]);
+    float tx = (px + eps) / cs, ty = (py + eps) / cs;      // the key of k_kick_drift
+    int gx = (int)floorf(tx), gy = (int)floorf(ty);
+    int qx = (int)floorf(2.0f * tx) - 2 * gx;
+    int qy = (int)floorf(2.0f * ty) - 2 * gy;
+    int kx = gx - ox, ky = gy - oy;
+    if (kx < 0 || kx >= W || ky < 0 || ky >= H) {
+        atomicOr(&status[ST_CAP_OVERFLOW], 1);
+        kx = min(max(kx, 0), W - 1);
+        ky = min(max(ky, 0), H - 1);
+    }
+    uint32_t k = (((uint32_t)ky * (uint32_t)W + (uint32_t)kx) << 2) | (uint32_t)(qy * 2 + qx);
+    key[slot] = k;
+    atomicAdd(&count[k], 1);
+}
+
+// (rho, p/rho^2) of the ghosts this rank sent, in the order they were sent
+__global__ void k_rho_pack(const int32_t *__restrict__ sendSlot, const float *__restrict__ sL,
+                           const float *__restrict__ sR, const int32_t *__restrict__ inv,
+                           const float4 *__restrict__ nbB, float *__restrict__ rsL,
+                           float *__restrict__ rsR, int cap) {
+    const int t = blockIdx.x * TPB + threadIdx.x;
+    const int side = t < cap ? 0 : 1, k = side ? t - cap : t;
+    const float *sbuf = side ? sR : sL;
+    float *rs = side ? rsR : rsL;
+    if (!sbuf || k >= rcount(sbuf, cap)) return;
+    if (k == 0) *hdr(rs) = rcount(sbuf, cap);
+    const float4 b = nbB[inv[sendSlot[side * cap + k]]];
+    rs[HDR + 2 * k] = b.z;
+    rs[HDR + 2 * k + 1] = b.w;
+}
+
+__global__ void k_rho_unpack(const float *__restrict__ rrL, const float *__restrict__ rrR,
+                             const float *__restrict__ gL, const float *__restrict__ gR, int cap,
+                             int nown, const int32_t *__restrict__ inv, float4 *__restrict__ nbB) {
+    const int t = blockIdx.x * TPB + threadIdx.x;
+    const int nL = rcount(gL, cap), nR = rcount(gR, cap);
+    const float *src;
+    int slot;
+    if (t < cap) {
+        if (t >= nL) return;
+        src = rrL + HDR + 2 * t;
+        slot = nown + t;
+    } else {
+        const int k = t - cap;
+        if (k >= nR) return;
+        src = rrR + HDR + 2 * k;
+        slot = nown + nL + k;
+    }
+    float4 &b = nbB[inv[slot]];
+    b.z = src[0];
+    b.w = src[1];
+}
+
+// particles that left the slab -> migrant buffers; keep flags for the rest
+__global__ void k_mig_pack(int n, PState P, const float *__restrict__ rho, const float *__restrict__ pr,
+                           float x0, float x1, int hasL, int hasR, float *__restrict__ mL,
+                           float *__restrict__ mR, int32_t *__restrict__ keep, int cap,
+                           int32_t *__restrict__ status) {
+    int i = blockIdx.x * TPB + threadIdx.x;
+    if (i >= n) return;
+    const float x = P.x[i];
+    float *buf = nullptr;
+    if (hasL && x < x0) buf = mL;
+    else if (hasR && x >= x1) buf = mR;
+    keep[i] = buf ? 0 : 1;
+    if (!buf) return;
+    int k = atomicAdd(hdr(buf), 1);
+    if (k >= cap) { atomicOr(&status[ST_HALO_OVERFLOW], 1); keep[i] = 1; return; }
+    float *r = buf + HDR + (size_t)k * MREC;
+    r[0] = x; r[1] = P.y[i]; r[2] = P.vx[i]; r[3] = P.vy[i];
+    r[4] = P.m[i]; r[5] = __int_as_float(P.id[i]); r[6] = rho[i]; r[7] = pr[i];
+}
+
+// kept particles -> S[kdst[i]] (rho, p in S.vhx, S.vhy), then received
+// migrants after them; kdst is the exclusive scan of the keep flags (n + 1
+// entries), so particle i is kept iff kdst[i + 1] != kdst[i]
+__global__ void k_mig_compact(int n, const int32_t *__restrict__ kdst, PState P,
+                              const float *__restrict__ rho, const float *__restrict__ pr, PState S) {
+    int i = blockIdx.x * TPB + threadIdx.x;
+    if (i >= n) return;
+    const int d = kdst[i];
+    if (kdst[i + 1] == d) return;
+    S.x[d] = P.x[i]; S.y[d] = P.y[i]; S.vx[d] = P.vx[i]; S.vy[d] = P.vy[i];
+    S.m[d] = P.m[i]; S.id[d] = P.id[i]; S.vhx[d] = rho[i]; S.vhy[d] = pr[i];
+}
+__global__ void k_mig_append(const float *__restrict__ mrL, const float *__restrict__ mrR, int cap,
+                             int base, PState S) {
+    const int t = blockIdx.x * TPB + threadIdx.x;
+    const int nL = rcount(mrL, cap), nR = rcount(mrR, cap);
+    const float *src;
+    int d;
+    if (t < cap) {
+        if (t >= nL) return;
+        src = mrL + HDR + (size_t)t * MREC;
+        d = base + t;
+    } else {
+        const int k = t - cap;
+        if (k >= nR) return;
+        src = mrR + HDR + (size_t)k * MREC;
+        d = base + nL + k;
+    }
+    S.x[d] = src[0]; S.y[d] = src[1]; S.vx[d] = src[2]; S.vy[d] = src[3];
+    S.m[d] = src[4]; S.id[d] = __float_as_int(src[5]); S.vhx[d] = src[6]; S.vhy[d] = src[7];
 }
 
 // ---------------------------------------------------------------------------
@@ -841,6 +1079,7 @@ using namespace lpe;
 // ===========================================================================
 // host side
 static inline int nblk(long n, int t = TPB) { return (int)((n + t - 1) / t); }
+static inline int nblk1(long n, int t = TPB) { return std::max(1, nblk(n, t)); }   // never an empty grid
 
 static void pstate_free(PState &p) {
     void *ptrs[] = {p.x, p.y, p.vx, p.vy, p.vhx, p.vhy, p.ax, p.ay, p.m, p.id};
@@ -848,7 +1087,26 @@ static void pstate_free(PState &p) {
     p = PState();
 }
 
+static void shard_free_slots(Shard *h) {
+    void *ptrs[] = {h->inv, h->owned, h->dst, h->keep, h->kdst, h->obsum, h->orho, h->opr};
+    for (void *p : ptrs) if (p) (void)hipFree(p);
+    h->inv = h->owned = h->dst = h->keep = h->kdst = h->obsum = nullptr;
+    h->orho = h->opr = nullptr;
+    h->cap_slots = 0;
+}
+
+static void shard_free(Shard *h) {
+    if (!h) return;
+    shard_free_slots(h);
+    void *ptrs[] = {h->ntot, h->gsL, h->gsR, h->grL, h->grR, h->sendSlot, h->rsL, h->rsR, h->rrL, h->rrR,
+                    h->msL, h->msR, h->mrL, h->mrR, h->bb};
+    for (void *p : ptrs) if (p) (void)hipFree(p);
+    delete h;
+}
+
 static void sph_free(SphDev &d) {
+    shard_free(d.shard);
+    d.shard = nullptr;
     pstate_free(d.P);
     pstate_free(d.S);
     void *ptrs[] = {d.rho, d.pr, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.count, d.start, d.cursor,
@@ -891,6 +1149,8 @@ extern "C" int lpe_destroy(lpe_ctx *ctx) {
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
     sph_free(ctx->sph);
+    delete ctx->transport;
+    ctx->transport = nullptr;
     lpe_rigid_destroy_internal(ctx);
     lpe_timer_destroy_internal(ctx);
     (void)hipStreamDestroy(ctx->stream);
@@ -995,7 +1255,7 @@ static int sph_plan_grid(lpe_ctx *ctx, const float *x, const float *y, int n) {
 // universe the boundary system keeps every body and particle in)
 int lpe_sph_cover_box(lpe_ctx *ctx, double x0, double y0, double x1, double y1) {
     SphDev &d = ctx->sph;
-    if (d.n <= 0 || d.cs <= 0.f) return LPE_OK;
+    if (d.cs <= 0.f || (d.n <= 0 && !d.shard)) return LPE_OK;
     const double cs = d.cs;
     int gx0 = std::min(d.ox, (int)std::floor(x0 / cs) - 4);
     int gy0 = std::min(d.oy, (int)std::floor(y0 / cs) - 4);
@@ -1016,8 +1276,19 @@ static int pstate_alloc(lpe_ctx *ctx, PState &p, size_t N, bool with_a) {
     return LPE_OK;
 }
 
+static int shard_slots(const Shard &h);
+
+// slots per particle array: n (single domain); owned + ghost slots with room
+// for the owned count to grow through migration (slab decomposition)
 static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     SphDev &d = ctx->sph;
+    Shard *h = d.shard;
+    if (h) {
+        const long want = 2L * n + 4096 + shard_slots(*h);
+        if (want > (1L << 30)) { ctx->err = "slab capacity too large"; return LPE_ERR_CAPACITY; }
+        if (n + shard_slots(*h) <= d.cap_n && d.P.x && h->cap_slots >= d.cap_n) return LPE_OK;
+        n = (int)want;
+    }
     if (n <= d.cap_n && d.P.x) return LPE_OK;
     pstate_free(d.P);
     pstate_free(d.S);
@@ -1039,6 +1310,19 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpOld, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.bboxPart, sizeof(float4) * MAX_KICK_BLOCKS));
     d.cap_n = n;
+    if (h) {
+        shard_free_slots(h);
+        const size_t S1 = N + 1;
+        int32_t **iv[] = {&h->inv, &h->owned, &h->dst, &h->keep, &h->kdst};
+        for (int32_t **q : iv) LPE_HIP(ctx, hipMalloc((void **)q, sizeof(int32_t) * S1));
+        LPE_HIP(ctx, hipMalloc((void **)&h->obsum, sizeof(int32_t) * (S1 / SCAN_ELEMS + 2)));
+        LPE_HIP(ctx, hipMalloc((void **)&h->orho, sizeof(float) * S1));
+        LPE_HIP(ctx, hipMalloc((void **)&h->opr, sizeof(float) * S1));
+        // the scans zero their count arrays after use; they start zeroed
+        LPE_HIP(ctx, hipMemsetAsync(h->owned, 0, sizeof(int32_t) * S1, ctx->stream));
+        LPE_HIP(ctx, hipMemsetAsync(h->keep, 0, sizeof(int32_t) * S1, ctx->stream));
+        h->cap_slots = (int)N;
+    }
     if (!d.gp) {
         LPE_HIP(ctx, hipMalloc((void **)&d.gp, sizeof(GridParams)));
         LPE_HIP(ctx, hipMalloc((void **)&d.status, sizeof(int32_t) * ST_COUNT));
@@ -1142,13 +1426,13 @@ static void sph_couple_params(const SphDev &d, CoupleParams &cp) {
 // exclusive scan of C counts into start/cursor (and, for the fluid bins, the
 // bbox finish + reference grid)
 static int sph_scan(lpe_ctx *ctx, int C, int32_t *cnt, int32_t *start, int32_t *cursor,
-                    int32_t *bsum, int nparts, bool fluid) {
+                    int32_t *bsum, int nparts, bool fluid, const float4 *bbG = nullptr) {
     SphDev &d = ctx->sph;
     int nb = (C + SCAN_ELEMS - 1) / SCAN_ELEMS;
     hipStream_t s = ctx->stream;
     LPE_KERNEL(ctx, "k_scan_reduce", k_scan_reduce, dim3(nb), dim3(TPB), 0, s, C, cnt, bsum);
     LPE_KERNEL(ctx, "k_scan_blocks", k_scan_blocks, dim3(1), dim3(TPB), 0, s, nb, bsum, start + C, d.bboxPart,
-                       nparts, d.cs, fluid ? d.gp : (GridParams *)nullptr, d.status);
+                       nparts, d.cs, fluid ? d.gp : (GridParams *)nullptr, d.status, bbG);
     LPE_KERNEL(ctx, "k_scan_final", k_scan_final, dim3(nb), dim3(TPB), 0, s, C, d.W, d.ox, d.oy, cnt, bsum,
                        start, cursor, d.gp, d.status, fluid ? 1 : 0);
     LPE_CHECK_LAUNCH(ctx, "scan");
@@ -1213,28 +1497,143 @@ static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool pr
     int st = sph_scan(ctx, C, d.count, d.start, d.cursor, d.blocksum, kb, true);
     if (st) return st;
     LPE_KERNEL(ctx, "k_scatter", k_scatter, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.P.id, d.cursor,
-                       d.tmpId, d.tmpOld);
+                       d.tmpId, d.tmpOld, (const int32_t *)nullptr);
     LPE_KERNEL(ctx, "k_rank_permute", k_rank_permute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.start,
-                       d.tmpId, d.tmpOld, d.P, d.S, d.nbA, (float2 *)d.nbB, probe ? 1 : 0);
+                       d.tmpId, d.tmpOld, d.P, d.S, d.nbA, (float2 *)d.nbB, probe ? 1 : 0,
+                       (const int32_t *)nullptr, 0, (int32_t *)nullptr, (int32_t *)nullptr);
     LPE_CHECK_LAUNCH(ctx, "hash");
     return LPE_OK;
 }
 
-static int sph_density(lpe_ctx *ctx) {
+// density over n slots (nptr: device count of the sharded sub-step)
+static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr) {
     SphDev &d = ctx->sph;
     const lpe_fluid_config &c = d.cfg;
-    LPE_KERNEL(ctx, "k_density", k_density, dim3(xcd_grid(nblk(d.n, DTPB))), dim3(DTPB), 0, ctx->stream, d.n,
-                       c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
+    LPE_KERNEL(ctx, "k_density", k_density, dim3(xcd_grid(nblk(n, DTPB))), dim3(DTPB), 0, ctx->stream, n,
+                       nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
                        c.restDensity, d.W, d.H, d.ox, d.oy, d.gp, d.start, d.nbA, (float2 *)d.nbB,
                        d.rho, d.pr, d.nlist, d.ncount);
     LPE_CHECK_LAUNCH(ctx, "k_density");
     return LPE_OK;
 }
 
+// ---- x-slab decomposition (host side of the kernels above) -------------
+static size_t ghost_bytes(int cap) { return sizeof(float) * (HDR + (size_t)cap * GREC); }
+static size_t rho_bytes(int cap) { return sizeof(float) * (HDR + (size_t)cap * 2); }
+static size_t mig_bytes(int cap) { return sizeof(float) * (HDR + (size_t)cap * MREC); }
+static int shard_slots(const Shard &h) { return 2 * h.cap; }   // ghost slots after the owned ones
+
+// the sharded grid hash: kick owned, global bbox, ghost exchange, sort owned + ghosts
+static int sph_hash_shard(lpe_ctx *ctx, float subDt, float halfDt, bool first) {
+    SphDev &d = ctx->sph;
+    Shard &h = *d.shard;
+    Transport *tr = ctx->transport;
+    hipStream_t s = ctx->stream;
+    const int C = 4 * d.W * d.H;
+    const int kb = std::min(MAX_KICK_BLOCKS, std::max(1, nblk(d.n)));
+    const float eps = d.cfg.gridConfig.gridEpsilon;
+    LPE_KERNEL(ctx, "k_kick_drift", k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
+               first ? 1 : 0, 0, eps, d.cs, d.ox, d.oy, d.W, d.H, d.P, d.key, d.count, d.bboxPart, d.status);
+    LPE_KERNEL(ctx, "k_bbox_reduce", k_bbox_reduce, dim3(1), dim3(TPB), 0, s, d.bboxPart, kb, h.bb);
+    LPE_CHECK_LAUNCH(ctx, "shard kick");
+    int st = tr->allreduce(ctx, (float *)h.bb, 4, 1);
+    if (st) return st;
+    LPE_HIP(ctx, hipMemsetAsync(h.gsL, 0, sizeof(float) * HDR, s));
+    LPE_HIP(ctx, hipMemsetAsync(h.gsR, 0, sizeof(float) * HDR, s));
+    LPE_KERNEL(ctx, "k_ghost_pack", k_ghost_pack, dim3(nblk1(d.n)), dim3(TPB), 0, s, d.n, d.P, h.x0, h.x1, h.D,
+               h.hasL, h.hasR, h.gsL, h.gsR, h.sendSlot, h.cap, d.status);
+    LPE_CHECK_LAUNCH(ctx, "k_ghost_pack");
+    st = tr->halo(ctx, h.hasL ? h.gsL : nullptr, h.hasR ? h.gsR : nullptr, h.hasL ? h.grL : nullptr,
+                  h.hasR ? h.grR : nullptr, ghost_bytes(h.cap));
+    if (st) return st;
+    LPE_KERNEL(ctx, "k_ghost_unpack", k_ghost_unpack, dim3(nblk1(2 * h.cap)), dim3(TPB), 0, s,
+               h.hasL ? h.grL : (const float *)nullptr, h.hasR ? h.grR : (const float *)nullptr, h.cap, d.n,
+               d.P, d.key, d.count, eps, d.cs, d.ox, d.oy, d.W, d.H, h.ntot, d.status);
+    LPE_CHECK_LAUNCH(ctx, "k_ghost_unpack");
+    st = sph_scan(ctx, C, d.count, d.start, d.cursor, d.blocksum, kb, true, h.bb);
+    if (st) return st;
+    const int ncap = d.n + shard_slots(h);
+    LPE_KERNEL(ctx, "k_scatter", k_scatter, dim3(nblk1(ncap)), dim3(TPB), 0, s, ncap, d.key, d.P.id, d.cursor,
+               d.tmpId, d.tmpOld, (const int32_t *)h.ntot);
+    LPE_KERNEL(ctx, "k_rank_permute", k_rank_permute, dim3(nblk1(ncap)), dim3(TPB), 0, s, ncap, d.key, d.start,
+               d.tmpId, d.tmpOld, d.P, d.S, d.nbA, (float2 *)d.nbB, 0, (const int32_t *)h.ntot, d.n, h.inv, h.owned);
+    LPE_CHECK_LAUNCH(ctx, "shard hash");
+    return LPE_OK;
+}
+
+// after the density pass: the owners' (rho, p/rho^2) of the ghosts, and the
+// owned-slot compaction map
+static int sph_ghost_density(lpe_ctx *ctx) {
+    SphDev &d = ctx->sph;
+    Shard &h = *d.shard;
+    hipStream_t s = ctx->stream;
+    LPE_KERNEL(ctx, "k_rho_pack", k_rho_pack, dim3(nblk1(2 * h.cap)), dim3(TPB), 0, s, h.sendSlot,
+               h.hasL ? h.gsL : (const float *)nullptr, h.hasR ? h.gsR : (const float *)nullptr, h.inv, d.nbB,
+               h.rsL, h.rsR, h.cap);
+    LPE_CHECK_LAUNCH(ctx, "k_rho_pack");
+    int st = ctx->transport->halo(ctx, h.hasL ? h.rsL : nullptr, h.hasR ? h.rsR : nullptr,
+                                  h.hasL ? h.rrL : nullptr, h.hasR ? h.rrR : nullptr, rho_bytes(h.cap));
+    if (st) return st;
+    LPE_KERNEL(ctx, "k_rho_unpack", k_rho_unpack, dim3(nblk1(2 * h.cap)), dim3(TPB), 0, s,
+               h.hasL ? h.rrL : (const float *)nullptr, h.hasR ? h.rrR : (const float *)nullptr,
+               h.hasL ? h.grL : (const float *)nullptr, h.hasR ? h.grR : (const float *)nullptr, h.cap, d.n,
+               h.inv, d.nbB);
+    LPE_CHECK_LAUNCH(ctx, "k_rho_unpack");
+    const int ncap = d.n + shard_slots(h);
+    return sph_scan(ctx, ncap, h.owned, h.dst, (int32_t *)d.key, h.obsum, 0, false);
+}
+
+// once per tick: particles that left the slab go to the neighbour (one host
+// sync, for the new owned count)
+static int sph_migrate(lpe_ctx *ctx) {
+    SphDev &d = ctx->sph;
+    Shard &h = *d.shard;
+    hipStream_t s = ctx->stream;
+    LPE_HIP(ctx, hipMemsetAsync(h.msL, 0, sizeof(float) * HDR, s));
+    LPE_HIP(ctx, hipMemsetAsync(h.msR, 0, sizeof(float) * HDR, s));
+    LPE_KERNEL(ctx, "k_mig_pack", k_mig_pack, dim3(nblk1(d.n)), dim3(TPB), 0, s, d.n, d.P, h.orho, h.opr, h.x0,
+               h.x1, h.hasL, h.hasR, h.msL, h.msR, h.keep, h.cap, d.status);
+    LPE_CHECK_LAUNCH(ctx, "k_mig_pack");
+    int st = ctx->transport->halo(ctx, h.hasL ? h.msL : nullptr, h.hasR ? h.msR : nullptr,
+                                  h.hasL ? h.mrL : nullptr, h.hasR ? h.mrR : nullptr, mig_bytes(h.cap));
+    if (st) return st;
+    int32_t cnt[4] = {0, 0, 0, 0};
+    if (h.hasL) LPE_HIP(ctx, hipMemcpyAsync(&cnt[0], h.msL, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (h.hasR) LPE_HIP(ctx, hipMemcpyAsync(&cnt[1], h.msR, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (h.hasL) LPE_HIP(ctx, hipMemcpyAsync(&cnt[2], h.mrL, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    if (h.hasR) LPE_HIP(ctx, hipMemcpyAsync(&cnt[3], h.mrR, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    LPE_HIP(ctx, hipStreamSynchronize(s));
+    for (int k = 0; k < 4; k++) cnt[k] = std::min(cnt[k], h.cap);
+    const int kept = d.n - cnt[0] - cnt[1];
+    const int nn = kept + cnt[2] + cnt[3];
+    if (nn + shard_slots(h) > d.cap_n) {
+        ctx->err = "slab decomposition: owned particles exceed the rank's capacity";
+        return LPE_ERR_CAPACITY;
+    }
+    // (the scan leaves the keep flags zeroed; k_mig_pack writes all of them)
+    if (d.n > 0) {
+        st = sph_scan(ctx, d.n, h.keep, h.kdst, (int32_t *)d.key, h.obsum, 0, false);
+        if (st) return st;
+    }
+    LPE_KERNEL(ctx, "k_mig_compact", k_mig_compact, dim3(nblk1(d.n)), dim3(TPB), 0, s, d.n, h.kdst, d.P,
+               h.orho, h.opr, d.S);
+    LPE_KERNEL(ctx, "k_mig_append", k_mig_append, dim3(nblk1(2 * h.cap)), dim3(TPB), 0, s,
+               h.hasL ? h.mrL : (const float *)nullptr, h.hasR ? h.mrR : (const float *)nullptr, h.cap, kept, d.S);
+    LPE_CHECK_LAUNCH(ctx, "migration");
+    const size_t B = sizeof(float) * (size_t)nn;
+    float *dstp[6] = {d.P.x, d.P.y, d.P.vx, d.P.vy, d.P.m, d.rho};
+    float *srcp[6] = {d.S.x, d.S.y, d.S.vx, d.S.vy, d.S.m, d.S.vhx};
+    for (int k = 0; k < 6; k++) LPE_HIP(ctx, hipMemcpyAsync(dstp[k], srcp[k], B, hipMemcpyDeviceToDevice, s));
+    LPE_HIP(ctx, hipMemcpyAsync(d.pr, d.S.vhy, B, hipMemcpyDeviceToDevice, s));
+    LPE_HIP(ctx, hipMemcpyAsync(d.P.id, d.S.id, sizeof(int32_t) * (size_t)nn, hipMemcpyDeviceToDevice, s));
+    d.n = nn;
+    return LPE_OK;
+}
+
 extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
     if (!ctx) return LPE_ERR_ARG;
     SphDev &d = ctx->sph;
-    if (d.n <= 0) return LPE_OK;  // fluid.cpp:969-972
+    if (d.n <= 0 && !d.shard) return LPE_OK;  // fluid.cpp:969-972 (a slab rank joins the exchanges)
     if (!d.P.x) return LPE_ERR_STATE;
     (void)hipSetDevice(ctx->device);
     const lpe_fluid_config &c = d.cfg;
@@ -1253,23 +1652,55 @@ extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
     sp.minDist = c.numericalConfig.minDistanceThreshold;
     sp.minDens = c.numericalConfig.minDensityThreshold;
     sp.diag = d.diag;
+    sp.nptr = nullptr;
+    sp.dst = nullptr;
+    sp.orho = sp.opr = nullptr;
+    sp.nstride = d.cap_n;
+    Shard *sh = d.shard;
+    if (sh && !ctx->transport) {
+        ctx->err = "slab decomposition without a transport (lpe_mg_init_rccl / lpe_mg_loopback_run)";
+        return LPE_ERR_STATE;
+    }
+    if (sh) {
+        sp.n = d.n + shard_slots(*sh);
+        sp.nptr = sh->ntot;
+        sp.dst = sh->dst;
+        sp.orho = sh->orho;
+        sp.opr = sh->opr;
+    }
     CoupleParams cp;
     sph_couple_params(d, cp);
     for (int step = 0; step < c.numSubSteps; step++) {
-        st = sph_hash(ctx, subDt, halfDt, step == 0, false);
+        if (sh) {
+            st = sph_hash_shard(ctx, subDt, halfDt, step == 0);
+            if (st) return st;
+            st = sph_density(ctx, sp.n, sh->ntot);
+            if (st) return st;
+            st = sph_ghost_density(ctx);
+        } else {
+            st = sph_hash(ctx, subDt, halfDt, step == 0, false);
+            if (st) return st;
+            st = sph_density(ctx, d.n, nullptr);
+        }
         if (st) return st;
-        st = sph_density(ctx);
-        if (st) return st;
-        LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(xcd_grid(nblk(d.n))), dim3(TPB), 0, s, sp, cp, d.gp,
+        LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(xcd_grid(nblk(sp.n))), dim3(TPB), 0, s, sp, cp, d.gp,
                            d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.rbinStart, d.rbinList,
                            d.accum, d.status);
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
     }
     if (d.nr > 0) {
+        // slab decomposition: every rank holds its particles' share of the
+        // fluid->rigid impulses; the rigids are replicated, so the shares are
+        // summed (fixed rank order) before the write-back (fluid.cpp:545-562)
+        if (sh) {
+            st = ctx->transport->allreduce(ctx, d.accum, 3 * d.nr, 0);
+            if (st) return st;
+        }
         LPE_KERNEL(ctx, "k_rigid_writeback", k_rigid_writeback, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig,
                            d.accum, d.accum + 3 * d.nr, c.dampingFactor);
         LPE_CHECK_LAUNCH(ctx, "k_rigid_writeback");
     }
+    if (sh) return sph_migrate(ctx);
     return LPE_OK;
 }
 
@@ -1305,6 +1736,10 @@ static int check_status(lpe_ctx *ctx) {
         ctx->err = "the rigid coupling bin list overflowed its capacity bound";
         return LPE_ERR_OVERFLOW;
     }
+    if (status[ST_HALO_OVERFLOW]) {
+        ctx->err = "a slab exchange buffer overflowed (raise ghost_cap of lpe_sph_set_slab)";
+        return LPE_ERR_OVERFLOW;
+    }
     return LPE_OK;
 }
 
@@ -1312,6 +1747,10 @@ extern "C" int lpe_sph_download(lpe_ctx *ctx, float *x, float *y, float *vx, flo
                                 float *density, float *pressure) {
     if (!ctx) return LPE_ERR_ARG;
     SphDev &d = ctx->sph;
+    if (d.shard) {
+        ctx->err = "slab decomposition: the ranks hold global ids, use lpe_sph_download_owned";
+        return LPE_ERR_STATE;
+    }
     if (d.n > 0) {
         const float *src[6] = {d.P.x, d.P.y, d.P.vx, d.P.vy, d.rho, d.pr};
         float *dst[6] = {x, y, vx, vy, density, pressure};
@@ -1420,4 +1859,70 @@ extern "C" int lpe_sph_probe_density(lpe_ctx *ctx, float *density, float *pressu
     const float *src[2] = {d.rho, d.pr};
     float *dst[2] = {density, pressure};
     return sph_unpermute_download(ctx, d.tmpOld, 2, src, dst);
+}
+
+// ---- slab decomposition: configuration and owned-particle I/O -----------
+extern "C" int lpe_sph_set_slab(lpe_ctx *ctx, float x0, float x1, float halo, int has_left, int has_right,
+                                int ghost_cap) {
+    if (!ctx || ghost_cap < 1 || !(halo > 0.f) || (has_left && has_right && !(x1 > x0))) return LPE_ERR_ARG;
+    (void)hipSetDevice(ctx->device);
+    SphDev &d = ctx->sph;
+    LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    shard_free(d.shard);
+    d.shard = nullptr;
+    d.cap_n = 0;                // the particle arrays are re-sized (owned + ghost slots) by the upload
+    Shard *h = new Shard();
+    h->x0 = x0; h->x1 = x1; h->D = halo;
+    h->hasL = has_left ? 1 : 0; h->hasR = has_right ? 1 : 0;
+    h->cap = ghost_cap;
+    d.shard = h;
+    LPE_HIP(ctx, hipMalloc((void **)&h->ntot, sizeof(int32_t)));
+    LPE_HIP(ctx, hipMalloc((void **)&h->bb, sizeof(float4)));
+    LPE_HIP(ctx, hipMalloc((void **)&h->sendSlot, sizeof(int32_t) * 2 * (size_t)ghost_cap));
+    float **gb[] = {&h->gsL, &h->gsR, &h->grL, &h->grR};
+    for (float **q : gb) LPE_HIP(ctx, hipMalloc((void **)q, ghost_bytes(ghost_cap)));
+    float **rb[] = {&h->rsL, &h->rsR, &h->rrL, &h->rrR};
+    for (float **q : rb) LPE_HIP(ctx, hipMalloc((void **)q, rho_bytes(ghost_cap)));
+    float **mb[] = {&h->msL, &h->msR, &h->mrL, &h->mrR};
+    for (float **q : mb) LPE_HIP(ctx, hipMalloc((void **)q, mig_bytes(ghost_cap)));
+    float *all[] = {h->gsL, h->gsR, h->grL, h->grR, h->rsL, h->rsR, h->rrL, h->rrR, h->msL, h->msR, h->mrL, h->mrR};
+    for (float *q : all) LPE_HIP(ctx, hipMemsetAsync(q, 0, sizeof(float) * HDR, ctx->stream));
+    LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LPE_OK;
+}
+
+extern "C" int lpe_sph_set_ids(lpe_ctx *ctx, int n, const int32_t *ids) {
+    if (!ctx || n < 0 || (n > 0 && !ids)) return LPE_ERR_ARG;
+    SphDev &d = ctx->sph;
+    if (n != d.n) return LPE_ERR_ARG;
+    if (n == 0) return LPE_OK;
+    LPE_HIP(ctx, hipMemcpyAsync(d.P.id, ids, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
+    LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LPE_OK;
+}
+
+extern "C" int lpe_sph_download_owned(lpe_ctx *ctx, int cap, float *x, float *y, float *vx, float *vy,
+                                      float *density, float *pressure, int32_t *ids, int *n_out) {
+    if (!ctx || !n_out || cap < 0) return LPE_ERR_ARG;
+    SphDev &d = ctx->sph;
+    *n_out = d.n;
+    if (d.n > cap) return LPE_ERR_CAPACITY;
+    hipStream_t s = ctx->stream;
+    const size_t B = sizeof(float) * (size_t)d.n;
+    if (d.n > 0) {
+        const float *src[6] = {d.P.x, d.P.y, d.P.vx, d.P.vy, d.rho, d.pr};
+        float *dst[6] = {x, y, vx, vy, density, pressure};
+        for (int k = 0; k < 6; k++)
+            if (dst[k]) LPE_HIP(ctx, hipMemcpyAsync(dst[k], src[k], B, hipMemcpyDeviceToHost, s));
+        if (ids) LPE_HIP(ctx, hipMemcpyAsync(ids, d.P.id, sizeof(int32_t) * d.n, hipMemcpyDeviceToHost, s));
+    }
+    LPE_HIP(ctx, hipStreamSynchronize(s));
+    return check_status(ctx);
+}
+
+extern "C" int lpe_sph_set_domain(lpe_ctx *ctx, double x0, double y0, double x1, double y1) {
+    if (!ctx || !(x1 >= x0) || !(y1 >= y0)) return LPE_ERR_ARG;
+    (void)hipSetDevice(ctx->device);
+    if (ctx->sph.cs <= 0.f) return LPE_ERR_STATE;     // after lpe_sph_upload
+    return lpe_sph_cover_box(ctx, x0, y0, x1, y1);
 }

@@ -1,0 +1,197 @@
+// lpe_transport.hip — transports of the x-slab decomposition: RCCL over xGMI
+// (one process per GPU) and an in-process loopback group (tests: several
+// ranks on one GPU, one host thread per rank).
+#include "lpe_transport.h"
+#include <rccl/rccl.h>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <thread>
+#include <vector>
+
+namespace lpe {
+
+// ---------------------------------------------------------------------------
+// RCCL: grouped send/recv with the two slab neighbours, all-reduce in place;
+// everything is enqueued on the context's stream.
+struct RcclTransport : Transport {
+    ncclComm_t comm = nullptr;
+    ~RcclTransport() override {
+        if (comm) ncclCommDestroy(comm);
+    }
+    int halo(lpe_ctx *ctx, const void *sendL, const void *sendR, void *recvL, void *recvR,
+             size_t bytes) override {
+        if (ncclGroupStart() != ncclSuccess) return LPE_ERR_HIP;
+        if (sendL && recvL && rank > 0) {
+            ncclSend(sendL, bytes, ncclChar, rank - 1, comm, ctx->stream);
+            ncclRecv(recvL, bytes, ncclChar, rank - 1, comm, ctx->stream);
+        }
+        if (sendR && recvR && rank < nranks - 1) {
+            ncclSend(sendR, bytes, ncclChar, rank + 1, comm, ctx->stream);
+            ncclRecv(recvR, bytes, ncclChar, rank + 1, comm, ctx->stream);
+        }
+        if (ncclGroupEnd() != ncclSuccess) {
+            ctx->err = "RCCL halo exchange failed";
+            return LPE_ERR_HIP;
+        }
+        return LPE_OK;
+    }
+    int allreduce(lpe_ctx *ctx, float *buf, int n, int op) override {
+        if (nranks == 1 || n <= 0) return LPE_OK;
+        if (ncclAllReduce(buf, buf, (size_t)n, ncclFloat, op ? ncclMin : ncclSum, comm, ctx->stream) !=
+            ncclSuccess) {
+            ctx->err = "RCCL all-reduce failed";
+            return LPE_ERR_HIP;
+        }
+        return LPE_OK;
+    }
+};
+
+int transport_unique_id(char *id) {
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return LPE_ERR_HIP;
+    static_assert(sizeof(u) <= 128, "ncclUniqueId fits 128 bytes");
+    std::memset(id, 0, 128);
+    std::memcpy(id, &u, sizeof(u));
+    return LPE_OK;
+}
+
+Transport *transport_rccl(lpe_ctx *ctx, int nranks, int rank, const char *id, std::string &err) {
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    auto *t = new RcclTransport();
+    t->rank = rank;
+    t->nranks = nranks;
+    (void)hipSetDevice(ctx->device);
+    ncclResult_t r = ncclCommInitRank(&t->comm, nranks, u, rank);
+    if (r != ncclSuccess) {
+        err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r);
+        t->comm = nullptr;
+        delete t;
+        return nullptr;
+    }
+    return t;
+}
+
+// ---------------------------------------------------------------------------
+// Loopback: the ranks are contexts of one process, each driven by its own
+// host thread; an exchange is a barrier, device-to-device copies from the
+// neighbours' send buffers, and a second barrier (so no send buffer is
+// rewritten before every neighbour has copied it).
+struct LoopGroup {
+    int n = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    long gen = 0;
+    bool abort = false;          // a rank failed: every barrier returns at once
+    std::vector<const void *> pL, pR;
+    std::vector<std::vector<float>> red;
+    bool barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        if (abort) return false;
+        long g = gen;
+        if (++arrived == n) {
+            arrived = 0;
+            gen++;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != g || abort; });
+        }
+        return !abort;
+    }
+    void fail() {
+        std::lock_guard<std::mutex> lk(mu);
+        abort = true;
+        cv.notify_all();
+    }
+};
+
+struct LoopTransport : Transport {
+    LoopGroup *g = nullptr;
+    int halo(lpe_ctx *ctx, const void *sendL, const void *sendR, void *recvL, void *recvR,
+             size_t bytes) override {
+        if (hipStreamSynchronize(ctx->stream) != hipSuccess) return LPE_ERR_HIP;
+        g->pL[rank] = sendL;
+        g->pR[rank] = sendR;
+        if (!g->barrier()) return LPE_ERR_STATE;
+        int st = LPE_OK;
+        if (recvL && rank > 0 && g->pR[rank - 1])
+            if (hipMemcpy(recvL, g->pR[rank - 1], bytes, hipMemcpyDeviceToDevice) != hipSuccess) st = LPE_ERR_HIP;
+        if (recvR && rank < nranks - 1 && g->pL[rank + 1])
+            if (hipMemcpy(recvR, g->pL[rank + 1], bytes, hipMemcpyDeviceToDevice) != hipSuccess) st = LPE_ERR_HIP;
+        if (!g->barrier()) return LPE_ERR_STATE;
+        return st;
+    }
+    int allreduce(lpe_ctx *ctx, float *buf, int n, int op) override {
+        if (nranks == 1 || n <= 0) return LPE_OK;
+        std::vector<float> &mine = g->red[rank];
+        mine.resize(n);
+        if (hipMemcpyAsync(mine.data(), buf, sizeof(float) * n, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess)
+            return LPE_ERR_HIP;
+        if (!g->barrier()) return LPE_ERR_STATE;
+        std::vector<float> acc(g->red[0]);             // rank order: deterministic
+        for (int r = 1; r < nranks; r++)
+            for (int i = 0; i < n; i++)
+                acc[i] = op ? (g->red[r][i] < acc[i] ? g->red[r][i] : acc[i]) : acc[i] + g->red[r][i];
+        if (!g->barrier()) return LPE_ERR_STATE;
+        if (hipMemcpy(buf, acc.data(), sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess) return LPE_ERR_HIP;
+        return LPE_OK;
+    }
+};
+
+}  // namespace lpe
+
+using namespace lpe;
+
+extern "C" int lpe_mg_unique_id(char *id) {
+    if (!id) return LPE_ERR_ARG;
+    return transport_unique_id(id);
+}
+
+extern "C" int lpe_mg_init_rccl(lpe_ctx *ctx, int nranks, int rank, const char *id) {
+    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return LPE_ERR_ARG;
+    if (ctx->transport) { delete ctx->transport; ctx->transport = nullptr; }
+    Transport *t = transport_rccl(ctx, nranks, rank, id, ctx->err);
+    if (!t) return LPE_ERR_HIP;
+    ctx->transport = t;
+    return LPE_OK;
+}
+
+extern "C" int lpe_mg_loopback_run(int n, lpe_ctx **ctxs, const lpe_world_config *wc, double dt_tick,
+                                   int nticks) {
+    if (n < 1 || !ctxs || nticks < 0) return LPE_ERR_ARG;
+    for (int r = 0; r < n; r++) if (!ctxs[r]) return LPE_ERR_ARG;
+    LoopGroup g;
+    g.n = n;
+    g.pL.assign(n, nullptr);
+    g.pR.assign(n, nullptr);
+    g.red.resize(n);
+    std::vector<Transport *> saved(n);
+    for (int r = 0; r < n; r++) {
+        auto *t = new LoopTransport();
+        t->g = &g;
+        t->rank = r;
+        t->nranks = n;
+        saved[r] = ctxs[r]->transport;
+        ctxs[r]->transport = t;
+    }
+    std::vector<int> st(n, LPE_OK);
+    std::vector<std::thread> th;
+    for (int r = 0; r < n; r++)
+        th.emplace_back([&, r] {
+            (void)hipSetDevice(ctxs[r]->device);
+            for (int t = 0; t < nticks && st[r] == LPE_OK; t++)
+                st[r] = wc ? lpe_world_tick(ctxs[r], wc, 1) : lpe_sph_step(ctxs[r], dt_tick);
+            if (st[r] == LPE_OK && hipStreamSynchronize(ctxs[r]->stream) != hipSuccess) st[r] = LPE_ERR_HIP;
+            if (st[r] != LPE_OK) g.fail();       // release the ranks waiting on this one
+        });
+    for (auto &t : th) t.join();
+    for (int r = 0; r < n; r++) {
+        delete ctxs[r]->transport;
+        ctxs[r]->transport = saved[r];
+    }
+    for (int r = 0; r < n; r++) if (st[r] != LPE_OK) return st[r];
+    return LPE_OK;
+}

@@ -192,6 +192,16 @@ class WorldConfig(C.Structure):
 SIGNATURES["lpe_world_set_coupling"] = ([C.c_void_p, C.c_int, C.c_void_p], C.c_int)
 SIGNATURES["lpe_world_tick"] = ([C.c_void_p, C.POINTER(WorldConfig), C.c_int], C.c_int)
 
+SIGNATURES["lpe_sph_set_slab"] = ([C.c_void_p, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int],
+                                  C.c_int)
+SIGNATURES["lpe_sph_set_ids"] = ([C.c_void_p, C.c_int, _IP], C.c_int)
+SIGNATURES["lpe_sph_download_owned"] = ([C.c_void_p, C.c_int] + [_FP] * 6 + [_IP, _IP], C.c_int)
+SIGNATURES["lpe_sph_set_domain"] = ([C.c_void_p] + [C.c_double] * 4, C.c_int)
+SIGNATURES["lpe_mg_unique_id"] = ([C.c_char_p], C.c_int)
+SIGNATURES["lpe_mg_init_rccl"] = ([C.c_void_p, C.c_int, C.c_int, C.c_char_p], C.c_int)
+SIGNATURES["lpe_mg_loopback_run"] = ([C.c_int, C.POINTER(C.c_void_p), C.POINTER(WorldConfig), C.c_double,
+                                      C.c_int], C.c_int)
+
 SYS_BOUNDARY, SYS_GRAVITY, SYS_ROTATION, SYS_MOVEMENT, SYS_SLEEP = 1, 2, 4, 8, 16
 
 
@@ -214,6 +224,26 @@ def default_fluid_config() -> FluidConfig:
     cfg = FluidConfig()
     lib().lpe_fluid_config_default(C.byref(cfg))
     return cfg
+
+
+def mg_unique_id() -> bytes:
+    """128-byte RCCL unique id (rank 0 makes it, every rank passes it to mg_init_rccl)."""
+    buf = C.create_string_buffer(128)
+    st = lib().lpe_mg_unique_id(buf)
+    if st != LPE_OK:
+        raise LpeError(f"lpe_mg_unique_id: {STATUS.get(st, st)}")
+    return buf.raw
+
+
+def mg_loopback_run(ctxs, nticks: int, dt_tick: float = 0.0, world: "WorldConfig" = None):
+    """Advance the contexts (ranks 0..n-1 of an in-process slab group) nticks."""
+    arr = (C.c_void_p * len(ctxs))(*[c._h.value for c in ctxs])
+    st = lib().lpe_mg_loopback_run(len(ctxs), arr, C.byref(world) if world is not None else None,
+                                   float(dt_tick), int(nticks))
+    if st != LPE_OK:
+        msgs = [lib().lpe_last_error(c._h) for c in ctxs]
+        raise LpeError(f"lpe_mg_loopback_run: {STATUS.get(st, st)}: "
+                       + "; ".join(m.decode() for m in msgs if m))
 
 
 def device_count() -> int:
@@ -319,6 +349,43 @@ class Context:
 
     def sph_diag(self, on=True):
         self._chk(lib().lpe_sph_diag(self._h, int(on)), "lpe_sph_diag")
+
+    # ---- x-slab decomposition --------------------------------------------
+    def sph_set_slab(self, x0, x1, halo, has_left, has_right, ghost_cap):
+        self._chk(lib().lpe_sph_set_slab(self._h, float(x0), float(x1), float(halo), int(has_left),
+                                         int(has_right), int(ghost_cap)), "lpe_sph_set_slab")
+
+    def sph_set_ids(self, ids):
+        a = np.ascontiguousarray(ids, dtype=np.int32)
+        self._chk(lib().lpe_sph_set_ids(self._h, len(a), a.ctypes.data_as(_IP)), "lpe_sph_set_ids")
+
+    def sph_download_owned(self, cap=None):
+        """{x, y, vx, vy, density, pressure, id} of the particles this context owns."""
+        n = C.c_int(0)
+        cap = int(cap if cap is not None else max(self.n, 1))
+        while True:
+            out = {k: np.empty(cap, np.float32) for k in ("x", "y", "vx", "vy", "density", "pressure")}
+            ids = np.empty(cap, np.int32)
+            st = lib().lpe_sph_download_owned(self._h, cap, *[_fp(out[k]) for k in
+                                              ("x", "y", "vx", "vy", "density", "pressure")],
+                                              ids.ctypes.data_as(_IP), C.byref(n))
+            if st == 4 and n.value > cap:  # LPE_ERR_CAPACITY
+                cap = n.value
+                continue
+            self._chk(st, "lpe_sph_download_owned")
+            break
+        k = n.value
+        out = {key: v[:k] for key, v in out.items()}
+        out["id"] = ids[:k]
+        return out
+
+    def sph_set_domain(self, x0, y0, x1, y1):
+        self._chk(lib().lpe_sph_set_domain(self._h, float(x0), float(y0), float(x1), float(y1)),
+                  "lpe_sph_set_domain")
+
+    def mg_init_rccl(self, nranks: int, rank: int, uid: bytes):
+        assert len(uid) == 128
+        self._chk(lib().lpe_mg_init_rccl(self._h, int(nranks), int(rank), uid), "lpe_mg_init_rccl")
 
     def sph_probe_cells(self):
         cells = np.empty(self.n, np.int32)

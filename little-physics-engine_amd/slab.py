@@ -1,0 +1,124 @@
+"""x-slab decomposition of the SPH step over ranks.
+
+The reference runs one FluidSystem on one device (fluid.cpp:958-1021); here
+the particle set is split by x into one slab per rank and every rank runs
+the same lpe_sph_step on its owned particles, exchanging ghosts with its two
+neighbours each sub-step (include/lpe.h, "x-slab decomposition").  This
+module holds the host side of that split:
+
+  slab_edges      equal-count slab edges (x-quantiles)
+  owners          owning rank of each particle ([x0, x1) per slab)
+  ghost_capacity  exchange-buffer size per side from the initial layout
+  setup_rank      configure + upload one rank's context
+  merge_owned     reassemble the global state from the ranks' owned sets
+  broadcast_uid / gather_owned   the torch.distributed plumbing (RCCL id
+                  exchange, gather of the owned sets to rank 0)
+
+Nothing here runs a physics kernel; the device work is all behind the C ABI.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+FIELDS = ("x", "y", "vx", "vy", "density", "pressure")
+
+
+def slab_edges(x, nranks: int) -> np.ndarray:
+    """nranks + 1 float32 edges [-inf, e1, ..., e_{n-1}, +inf]: inner edges at
+    the x-quantiles of the particles, so every slab starts with ~N/nranks
+    particles.  Deterministic in x, so every rank computes the same edges."""
+    xs = np.sort(np.asarray(x, np.float32))
+    n = len(xs)
+    edges = [np.float32(-np.inf)]
+    for r in range(1, nranks):
+        e = xs[min(n - 1, (n * r) // nranks)] if n else np.float32(r)
+        if e <= edges[-1]:
+            e = np.nextafter(edges[-1], np.float32(np.inf), dtype=np.float32)
+        edges.append(np.float32(e))
+    edges.append(np.float32(np.inf))
+    return np.array(edges, np.float32)
+
+
+def owners(x, edges) -> np.ndarray:
+    """Owning rank of each particle: slab r holds edges[r] <= x < edges[r+1]
+    (the device-side test of k_mig_pack, in float32)."""
+    xf = np.asarray(x, np.float32)
+    return np.searchsorted(np.asarray(edges, np.float32)[1:-1], xf, side="right").astype(np.int32)
+
+
+def ghost_capacity(x, edges, halo: float, factor: float = 4.0, floor: int = 4096) -> int:
+    """Ghost / migrant slots per side: `factor` times the most particles
+    within `halo` of any inner edge at the start, plus `floor`."""
+    xf = np.asarray(x, np.float32)
+    worst = 0
+    for e in np.asarray(edges, np.float32)[1:-1]:
+        worst = max(worst, int(((xf >= e - halo) & (xf < e)).sum()), int(((xf >= e) & (xf < e + halo)).sum()))
+    return int(factor * worst) + floor
+
+
+def default_halo(cfg) -> float:
+    """Ghost width: the smoothing length plus a tick's worth of drift
+    (4h; 0.2 m at the default h = 0.05, SURVEY.md §8(e) "two cells")."""
+    return 4.0 * float(cfg.gridConfig.smoothingLength)
+
+
+def setup_rank(ctx, rank: int, nranks: int, fluid: dict, edges, cfg, rigids=None, halo=None,
+               ghost_cap=None, domain=None):
+    """Configure ctx as slab `rank` and upload the particles it owns (global
+    ids = indices into `fluid`).  Returns the owned global ids."""
+    import lpe  # the in-tree binding (little-physics-engine_amd/lpe.py)
+    halo = default_halo(cfg) if halo is None else halo
+    x = np.asarray(fluid["x"], np.float32)
+    if ghost_cap is None:
+        ghost_cap = ghost_capacity(x, edges, halo)
+    own = np.nonzero(owners(x, edges) == rank)[0].astype(np.int32)
+    x0, x1 = float(edges[rank]), float(edges[rank + 1])
+    ctx.sph_set_config(cfg)
+    ctx.sph_set_slab(x0 if np.isfinite(x0) else 0.0, x1 if np.isfinite(x1) else 0.0, halo,
+                     rank > 0, rank < nranks - 1, ghost_cap)
+    sub = {k: np.asarray(fluid[k])[own] for k in ("x", "y", "vx", "vy", "mass", "density", "pressure")}
+    ctx.sph_upload(sub["x"], sub["y"], sub["vx"], sub["vy"], sub["mass"], sub["density"], sub["pressure"])
+    ctx.sph_set_ids(own)
+    if domain is None:
+        y = np.asarray(fluid["y"], np.float32)
+        pad = 1.0
+        domain = (float(x.min()) - pad, float(y.min()) - pad, float(x.max()) + pad, float(y.max()) + pad)
+    ctx.sph_set_domain(*domain)
+    ctx.sph_upload_rigids(rigids if rigids is not None else np.zeros(0, lpe.RIGID_DTYPE))
+    return own
+
+
+def merge_owned(parts, n_global: int) -> dict:
+    """Global arrays (index = global id) from the ranks' owned sets; every id
+    must appear exactly once."""
+    out = {k: np.zeros(n_global, np.float32) for k in FIELDS}
+    seen = np.zeros(n_global, np.int32)
+    for p in parts:
+        ids = np.asarray(p["id"], np.int64)
+        if len(ids) and (ids.min() < 0 or ids.max() >= n_global):
+            raise ValueError("slab merge: particle id out of range")
+        np.add.at(seen, ids, 1)
+        for k in FIELDS:
+            out[k][ids] = p[k]
+    if not (seen == 1).all():
+        lost, dup = int((seen == 0).sum()), int((seen > 1).sum())
+        raise ValueError(f"slab merge: {lost} particles lost, {dup} duplicated")
+    return out
+
+
+# ---- torch.distributed plumbing (one process per GPU) ---------------------
+def broadcast_uid(uid: bytes | None, rank: int) -> bytes:
+    """Rank 0's 128-byte RCCL id to every rank (over the default process
+    group: gloo or nccl)."""
+    import torch.distributed as dist
+    box = [uid if rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    return box[0]
+
+
+def gather_owned(owned: dict, n_global: int, rank: int, world: int):
+    """The merged global state on rank 0 (None on the others)."""
+    import torch.distributed as dist
+    parts = [None] * world if rank == 0 else None
+    dist.gather_object({k: np.asarray(v) for k, v in owned.items()}, parts, dst=0)
+    return merge_owned(parts, n_global) if rank == 0 else None

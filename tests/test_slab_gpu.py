@@ -1,0 +1,124 @@
+"""GPU parity of the x-slab decomposition against the
+single-domain HIP step, which tests/test_sph_gpu.py pins to the oracle.
+
+Several ranks run on the one GPU of the box through the in-process loopback
+transport (lpe_mg_loopback_run: one host thread per rank, device-to-device
+copies for the halo, host reductions in rank order); the RCCL transport
+differs only in how the same buffers move.  Ghosts carry global ids and the
+reference grid comes from the all-reduced bbox, so without rigid contact the
+merged state is bit-identical to the single-domain run, tick after tick.
+With rigid coupling the fluid is bit-identical in the first tick (rigids are
+frozen during the sub-steps); the rigid accumulators are float atomics
+summed per rank and then across ranks, so they match to summation-order
+ulps (the same bar as the single-domain coupled test)."""
+import numpy as np
+import pytest
+
+from conftest import lpe, scenes
+import importlib.util
+import os
+import sys
+
+pytestmark = pytest.mark.gpu
+DT = 1.0 / 120.0
+
+_spec = importlib.util.spec_from_file_location(
+    "slab", os.path.join(os.path.dirname(lpe.__file__), "slab.py"))
+slab = importlib.util.module_from_spec(_spec)
+sys.modules["slab"] = slab
+_spec.loader.exec_module(slab)
+
+
+def _single(fl, rig, nticks):
+    ctx = lpe.Context(0)
+    try:
+        ctx.sph_set_config(lpe.default_fluid_config())
+        ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+        ctx.sph_upload_rigids(rig)
+        for _ in range(nticks):
+            ctx.sph_step(DT)
+        out = ctx.sph_download()
+        r, acc = ctx.sph_download_rigids()
+        return out, r, acc
+    finally:
+        ctx.close()
+
+
+def _sharded(fl, rig, nticks, edges, ghost_cap=None):
+    n = len(edges) - 1
+    cfg = lpe.default_fluid_config()
+    ctxs = [lpe.Context(0) for _ in range(n)]
+    try:
+        for r, c in enumerate(ctxs):
+            slab.setup_rank(c, r, n, fl, edges, cfg, rig, ghost_cap=ghost_cap)
+        counts0 = [c.n for c in ctxs]
+        lpe.mg_loopback_run(ctxs, nticks, DT)
+        parts = [c.sph_download_owned(cap=len(fl["x"])) for c in ctxs]
+        rigs = [c.sph_download_rigids() for c in ctxs]
+        return slab.merge_owned(parts, len(fl["x"])), rigs, counts0, [len(p["id"]) for p in parts]
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_slab_fluid_bit_exact(nranks):
+    """Dam-break block (walls only, no particle touches them), 3 ticks."""
+    s = scenes.scene("small96_0")
+    fl = s["fluid"]
+    rig = scenes.gather_rigids(s["bodies"])
+    ref, _, _ = _single(fl, rig, 3)
+    edges = slab.slab_edges(fl["x"], nranks)
+    got, _, c0, c1 = _sharded(fl, rig, 3, edges)
+    assert min(c0) > 0
+    for k in slab.FIELDS:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+def test_slab_migration_and_empty_rank():
+    """Edges through the moving fluid (particles cross slab edges and
+    migrate) and a rank that starts empty and receives particles."""
+    s = scenes.scene("small64_0")
+    fl = dict(s["fluid"])
+    n = len(fl["x"])
+    fl["vx"] = np.full(n, 2.0)      # the whole block drifts right 2 m/s
+    rig = np.zeros(0, lpe.RIGID_DTYPE)
+    ref, _, _ = _single(fl, rig, 4)
+    xmax = np.float32(np.max(fl["x"]))
+    edges = np.array([-np.inf, np.median(np.float32(fl["x"])), xmax + np.float32(0.02), np.inf],
+                     np.float32)
+    got, _, c0, c1 = _sharded(fl, rig, 4, edges)
+    assert c0[2] == 0 and c1[2] > 0, (c0, c1)
+    for k in slab.FIELDS:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+def test_slab_coupled_first_tick():
+    """Pentagons sinking into the fluid across a slab edge: the fluid is
+    bit-identical in tick 1, the summed accumulators and rigid velocities
+    within float-atomic summation order."""
+    s = scenes.scene("small96_12")
+    fl = s["fluid"]
+    rig = scenes.gather_rigids(s["bodies"])
+    ref, rref, aref = _single(fl, rig, 1)
+    edges = slab.slab_edges(fl["x"], 2)
+    got, rigs, _, _ = _sharded(fl, rig, 1, edges)
+    assert np.abs(aref).sum() > 0
+    for k in slab.FIELDS:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    for r_out, acc in rigs:                   # every rank holds the summed result
+        for j in range(3):
+            tot = np.abs(aref[:, j]).max()
+            np.testing.assert_allclose(acc[:, j], aref[:, j], rtol=1e-5, atol=1e-6 * tot + 1e-12)
+        for k in ("vx", "vy", "omega"):
+            np.testing.assert_allclose(r_out[k], rref[k], rtol=1e-5, atol=1e-6, err_msg=k)
+    np.testing.assert_array_equal(rigs[0][0]["vx"], rigs[1][0]["vx"])
+
+
+def test_slab_halo_overflow_reported():
+    """A ghost buffer too small for the edge strip fails loudly."""
+    s = scenes.scene("small64_0")
+    fl = s["fluid"]
+    edges = slab.slab_edges(fl["x"], 2)
+    with pytest.raises(lpe.LpeError, match="OVERFLOW|overflow"):
+        _sharded(fl, np.zeros(0, lpe.RIGID_DTYPE), 1, edges, ghost_cap=8)
