@@ -5,9 +5,17 @@
 A step is one tick (ECSSimulator::tick, src/sim.cpp:156-163) of the resident
 device pipeline on the scene BASELINE.json's metric is quoted on: M = 256k SPH
 particles + 4096 pentagons + 4 walls, synthetic seeded input
-already resident in HBM.  For N > 1 (torch.distributed.run, one rank per GPU)
-every rank advances its own replica of the scene (weak scaling, no data-path
-collective); the control plane (barrier, max over ranks) uses gloo.
+already resident in HBM.
+
+For N > 1 (torch.distributed.run, one rank per GPU) the run is weak-scaled
+along the SPH path, the path that shards: scene MW{N} is the
+M pool widened N times (N x 256k particles, the same 4096-pentagon pile in the
+middle, U = 32 N m), its fluid split into N equal-count x-slabs with the RCCL
+halo exchange of include/lpe.h, the rigid pass replicated on every rank (rigid
+accumulators all-reduced once per tick).  Each rank advances one M-sized SPH
+slab per tick, so `value` = N x ticks/s.  MW1 is M.  --replicas runs N
+independent copies of M instead.  The control plane (uid broadcast, barrier,
+max over ranks) uses gloo.
 
 Rank 0 prints ONE JSON line (the driver contract), including the live
 roofline of the dominant kernel (HIP events on the library's stream) and the
@@ -124,6 +132,41 @@ def density_microbench(lpe, scenes, device, side=4096, reps=5):
                 mean_density=float(np.mean(rho)), max_cell_occupancy=st["maxCellOccupancy"])
 
 
+def loopback_check(args, lpe, scenes, slab, device):
+    """K slab ranks of MW{K} on one GPU through the in-process transport:
+    exercises the sharded bench path (scene, slab set-up, world ticks with
+    halo exchange and migration) where only one GPU is available.  Prints one
+    JSON check line (not the metric: K ranks share one GPU)."""
+    K = args.loopback
+    s = scenes.scene(f"MW{K}")
+    fl = s["fluid"]
+    bodies, verts = scenes.to_bodies(s["bodies"])
+    edges = slab.slab_edges(fl["x"], K)
+    ctxs = [lpe.Context(device) for _ in range(K)]
+    try:
+        for r, c in enumerate(ctxs):
+            c.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+            c.rigid_upload(bodies, verts)
+            slab.setup_rank(c, r, K, fl, edges, lpe.default_fluid_config())
+            c.world_set_coupling(None)
+        wc = lpe.WorldConfig(1.0 / 120.0, 1.0, 1.0, 1.0)
+        t0 = time.perf_counter()
+        lpe.mg_loopback_run(ctxs, args.prep + args.warmup + args.steps, world=wc)
+        el = time.perf_counter() - t0
+        parts = [c.sph_download_owned() for c in ctxs]
+        merged = slab.merge_owned(parts, len(fl["x"]))
+        rb = [c.rigid_download() for c in ctxs]
+        same = all(np.array_equal(rb[0][k], r[k]) for r in rb[1:] for k in ("x", "y", "angle"))
+        st = ctxs[0].sph_stats()
+    finally:
+        for c in ctxs:
+            c.close()
+    print(json.dumps({"check": "loopback", "ranks": K, "scene": f"MW{K}", "ticks": args.prep + args.warmup + args.steps,
+                      "seconds": round(el, 3), "owned": [len(p["x"]) for p in parts],
+                      "finite": bool(np.isfinite(merged["x"]).all() and np.isfinite(merged["vy"]).all()),
+                      "rigid_replicas_identical": bool(same), "max_cell_occupancy_rank0": st["maxCellOccupancy"]}))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -134,6 +177,11 @@ def main():
                     help="untimed ticks that settle the scene before warmup (the pile forms)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-density-microbench", action="store_true")
+    ap.add_argument("--replicas", action="store_true",
+                    help="N > 1: independent copies of the scene instead of the slab-sharded MW{N}")
+    ap.add_argument("--loopback", type=int, default=0,
+                    help="validation only: K slab ranks of MW{K} in this process on one GPU "
+                         "(in-process transport); prints a check line, not the metric")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -147,16 +195,27 @@ def main():
 
     lpe = _load("lpe", os.path.join(PKG, "lpe.py"))
     scenes = _load("scenes", os.path.join(PKG, "scenes.py"))
-    s = scenes.scene(args.scene)
+    slab = _load("slab", os.path.join(PKG, "slab.py"))
+    if args.loopback:
+        return loopback_check(args, lpe, scenes, slab, local)
+    sharded = world > 1 and not args.replicas
+    scene_name = f"MW{world}" if sharded and args.scene == "M" else args.scene
+    s = scenes.scene(scene_name)
     fl = s["fluid"]
     bodies, verts = scenes.to_bodies(s["bodies"])
     dt_tick = 1.0 / 120.0
 
     ctx = lpe.Context(local)
-    ctx.sph_set_config(lpe.default_fluid_config())
     ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
     ctx.rigid_upload(bodies, verts)
-    ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+    if sharded:
+        edges = slab.slab_edges(fl["x"], world)
+        slab.setup_rank(ctx, rank, world, fl, edges, lpe.default_fluid_config())
+        uid = slab.broadcast_uid(lpe.mg_unique_id() if rank == 0 else None, rank)
+        ctx.mg_init_rccl(world, rank, uid)
+    else:
+        ctx.sph_set_config(lpe.default_fluid_config())
+        ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
     ctx.world_set_coupling(None)      # every body, reverse insertion (gatherRigidBodies view order)
 
     # scene preparation: the pentagons fall into the pool and settle into a
@@ -195,8 +254,10 @@ def main():
     stats = ctx.sph_stats()
     pairs, contacts = ctx.rigid_contacts()
     _, ncolours = ctx.rigid_colours()
-    out = ctx.sph_download()   # also checks the capacity / overflow flags
+    # (both downloads also check the capacity / overflow flags)
+    out = ctx.sph_download_owned() if sharded else ctx.sph_download()
     settled = dict(fluid=out, bodies=ctx.rigid_download())
+    n_rank = len(out["x"])
 
     if rank != 0:
         if dist is not None:
@@ -204,7 +265,7 @@ def main():
         return
 
     assert np.isfinite(out["x"]).all() and np.isfinite(out["vy"]).all()
-    n = len(fl["x"])
+    n = n_rank                      # particles rank 0 owns (the whole scene unless sharded)
     cells = stats["gridDimX"] * stats["gridDimY"]
     # the roofline kernel: the SPH kernel with the largest share of the tick
     # (the rigid solvers are latency-bound single-workgroup sweeps with no
@@ -227,6 +288,8 @@ def main():
         bd = kernel_bytes("k_density", n, cells)
         roof_d = dict(kernel="k_density", achieved=round(bd / avg_d / 1e9, 1), unit="GB/s",
                       frac=round(bd / avg_d / 1e9 / HBM_PEAK_GBS, 4), avg_us=round(avg_d * 1e6, 2))
+    # weak scaling: every rank advances one M-sized SPH slab (sharded) or one
+    # copy of the scene (replicas) per tick
     value = world * args.steps / elapsed
     line = {
         "metric": "physics steps/sec at 256k SPH + 4k rigids; 1/2/4/8 MI355X vs HBM roofline",
@@ -243,13 +306,16 @@ def main():
         "data": "synthetic (seeded scene generator, SURVEY.md §8(d))",
         "config": {"workload": s["desc"] + f", ticks {args.prep + args.warmup}.."
                                f"{args.prep + args.warmup + args.steps} (settled pile)",
-                   "scene": args.scene, "fluid_particles": n, "prep_ticks": args.prep,
+                   "scene": scene_name, "fluid_particles": len(fl["x"]),
+                   "fluid_particles_rank0": n, "prep_ticks": args.prep,
                    "rigid_bodies": len(bodies), "substeps": 10, "dt": dt_tick,
                    "systems": ["FluidSystem (SPH + coupling)", "Boundary", "Gravity",
                                "RigidBodyCollision (broadphase, GJK/EPA, PGS 10 it, position 10 it)",
                                "Rotation", "Movement", "Sleep"],
                    "mode": "resident (ECS sync skipped inside the timed region)",
-                   "parallelism": f"replica x{world}"},
+                   "parallelism": (f"SPH x-slabs x{world} (RCCL halo + bbox/accumulator all-reduce), "
+                                   f"rigid pass replicated") if sharded else
+                                  ("single GPU" if world == 1 else f"replica x{world}")},
         "roofline": roof,
         "roofline_density": roof_d,
         "kernels_us": {k: round(v[0] / max(v[1], 1) * 1e3, 2) for k, v in times.items()},

@@ -1256,6 +1256,15 @@ static int sph_plan_grid(lpe_ctx *ctx, const float *x, const float *y, int n) {
 int lpe_sph_cover_box(lpe_ctx *ctx, double x0, double y0, double x1, double y1) {
     SphDev &d = ctx->sph;
     if (d.cs <= 0.f || (d.n <= 0 && !d.shard)) return LPE_OK;
+    if (d.shard) {
+        // a slab rank only ever holds particles near its slab: owned ones at
+        // most a tick's drift outside it, ghosts within D of its edges
+        const Shard &h = *d.shard;
+        const double m = 2.0 * h.D + 1.0;
+        if (h.hasL) x0 = std::max(x0, (double)h.x0 - m);
+        if (h.hasR) x1 = std::min(x1, (double)h.x1 + m);
+        if (x1 < x0) x1 = x0;
+    }
     const double cs = d.cs;
     int gx0 = std::min(d.ox, (int)std::floor(x0 / cs) - 4);
     int gy0 = std::min(d.oy, (int)std::floor(y0 / cs) - 4);

@@ -176,7 +176,9 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
     const double dt_fluid = wc->secondsPerTick * wc->timeAcceleration;              // fluid.cpp:592
     const double dt_move = wc->secondsPerTick * wc->timeAcceleration;               // movement.cpp:17
     const double dt_state = wc->secondsPerTick * wc->baseTimeAcceleration * wc->timeScale;  // gravity.cpp:31-33
-    if (d.couple_n == 0 && rd->nb > 0 && d.n > 0) {
+    // a slab rank (lpe_sph_set_slab) joins every fluid step, owned particles or not
+    const bool fluid = d.n > 0 || d.shard;
+    if (d.couple_n == 0 && rd->nb > 0 && fluid) {
         int st = lpe_world_set_coupling(ctx, -1, nullptr);
         if (st) return st;
     }
@@ -190,7 +192,7 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
     }
     for (int t = 0; t < nticks; t++) {
         // 1) FluidSystem::update (fluid.cpp:958-1021)
-        if (d.n > 0) {
+        if (fluid) {
             int nr = d.couple_n;
             if (nr > 0) {
                 LPE_KERNEL(ctx, "k_gather_rigids", k_gather_rigids, dim3(wblk(nr, 128)), dim3(128), 0, s, nr, d.coupleBody, rd->bodies, rd->verts, d.rig);

@@ -208,6 +208,19 @@ def scene(name: str):
         fl = fluid_lattice(rng, 1024, 256, 0.5 * (U - 1024 * LATTICE_S), pool_top)
         return dict(U=U, fluid=fl, bodies=b, seed=seed,
                     desc="M: 1024x256 SPH pool + 4096 pentagons (128x32 @0.24 m), U=32")
+    if name.startswith("MW"):   # M widened N x for weak scaling: N x 256k SPH, the same 4096-pentagon pile
+        nw = int(name[2:] or 1)
+        U, seed = 32.0 * nw, 6
+        rng = np.random.default_rng(seed)
+        b = Bodies()
+        add_walls(b, U)
+        pool_top = U - 0.15 - 256 * LATTICE_S
+        add_pentagon_lattice(b, rng, 128, 32, 0.5 * (U - 127 * 0.24), pool_top - 0.3 - 31 * 0.24,
+                             0.24, lambda i: 0.1)
+        fl = fluid_lattice(rng, 1024 * nw, 256, 0.5 * (U - 1024 * nw * LATTICE_S), pool_top)
+        return dict(U=U, fluid=fl, bodies=b, seed=seed,
+                    desc=f"MW{nw}: {1024 * nw}x256 SPH pool + the M pile of 4096 pentagons "
+                         f"(128x32 @0.24 m, centred), U={U:g}")
     if name.startswith("small"):   # test scenes: small{N} fluid + a few rigids
         parts = name[5:].split("_")
         side = int(parts[0]) if parts and parts[0] else 64

@@ -122,3 +122,74 @@ def test_slab_halo_overflow_reported():
     edges = slab.slab_edges(fl["x"], 2)
     with pytest.raises(lpe.LpeError, match="OVERFLOW|overflow"):
         _sharded(fl, np.zeros(0, lpe.RIGID_DTYPE), 1, edges, ghost_cap=8)
+
+
+def _world_rank(ctx, r, n, s, edges):
+    b, v = scenes.to_bodies(s["bodies"])
+    ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+    ctx.rigid_upload(b, v)
+    if edges is None:
+        fl = s["fluid"]
+        ctx.sph_set_config(lpe.default_fluid_config())
+        ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+    else:
+        slab.setup_rank(ctx, r, n, s["fluid"], edges, lpe.default_fluid_config())
+    ctx.world_set_coupling(np.arange(len(b) - 1, -1, -1, dtype=np.int32))
+
+
+def test_slab_world_tick_replicated_rigids():
+    """Full resident ticks (lpe_world_tick) with the fluid in 2 slabs and the
+    rigid pass replicated: tick 1's fluid is bit-identical to the single
+    domain, the rigid replicas stay identical to each other, and after 3
+    ticks both agree with the single domain at the coupled-test tolerance."""
+    s = scenes.scene("small96_12")
+    n_glob = len(s["fluid"]["x"])
+    for nt in (1, 3):
+        one = lpe.Context(0)
+        try:
+            _world_rank(one, 0, 1, s, None)
+            one.world_tick(DT, nt)
+            ref = one.sph_download()
+            rb_ref = one.rigid_download()
+        finally:
+            one.close()
+        edges = slab.slab_edges(s["fluid"]["x"], 2)
+        ctxs = [lpe.Context(0) for _ in range(2)]
+        try:
+            for r, c in enumerate(ctxs):
+                _world_rank(c, r, 2, s, edges)
+            lpe.mg_loopback_run(ctxs, nt, world=lpe.WorldConfig(DT, 1.0, 1.0, 1.0))
+            got = slab.merge_owned([c.sph_download_owned(cap=n_glob) for c in ctxs], n_glob)
+            rbs = [c.rigid_download() for c in ctxs]
+        finally:
+            for c in ctxs:
+                c.close()
+        for k in ("x", "y", "vx", "vy", "angle", "omega"):
+            np.testing.assert_array_equal(rbs[0][k], rbs[1][k], err_msg=k)
+        if nt == 1:
+            for k in slab.FIELDS:
+                np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+        for k in ("x", "y"):
+            ok = np.isclose(got[k], ref[k], rtol=1e-5, atol=1e-5)
+            assert ok.mean() > 0.99, (nt, k, ok.mean())
+            np.testing.assert_allclose(rbs[0][k], rb_ref[k], rtol=1e-5, atol=1e-4, err_msg=k)
+
+
+def test_rccl_transport_single_rank():
+    """The RCCL transport initialises on the box (world size 1: a slab with no
+    neighbours, so no traffic) and the step matches the single domain."""
+    s = scenes.scene("small64_0")
+    fl = s["fluid"]
+    rig = scenes.gather_rigids(s["bodies"])
+    ref, _, _ = _single(fl, rig, 2)
+    ctx = lpe.Context(0)
+    try:
+        ctx.mg_init_rccl(1, 0, lpe.mg_unique_id())
+        slab.setup_rank(ctx, 0, 1, fl, slab.slab_edges(fl["x"], 1), lpe.default_fluid_config(), rig)
+        ctx.sph_step(DT)
+        ctx.sph_step(DT)
+        got = slab.merge_owned([ctx.sph_download_owned()], len(fl["x"]))
+    finally:
+        ctx.close()
+    for k in slab.FIELDS:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
