@@ -56,7 +56,6 @@ static constexpr int TPB = 256;
 static constexpr int SCAN_ELEMS = 1024;   // elements per scan block (256 thr x 4)
 static constexpr int MAX_KICK_BLOCKS = 2048;
 static constexpr int NLIST_CAP = 128;     // neighbours kept per particle (column-major list)
-static constexpr int DTPB = 128;          // k_density block: its LDS list stage is NLIST_CAP x DTPB int16
 
 // kernel coefficients (metal:19-38), fp32
 __device__ __forceinline__ float poly6Coeff2D(float h) {
@@ -378,11 +377,12 @@ __device__ __forceinline__ int sel4(int4 v, int i) {
 // (the loop is latency bound otherwise: one dependent L2 round trip per
 // candidate).  ld(k, cy) loads candidate k's record (cy: the absolute cell
 // row being walked), f(k, rec) consumes it; f is called in the canonical order.
-template <int U, class L, class F>
-__device__ __forceinline__ void walk_neighbours(float xi, float yi, float eps, float cs,
-                                                float reach, const GridParams &g, int W, int H,
-                                                int ox, int oy, const int32_t *__restrict__ start,
-                                                L ld, F f) {
+// The candidate slot ranges of the walk in canonical order: f(b, e, cy) for
+// each (cell, quadrant row) range [b, e) of absolute cell row cy.
+template <class F>
+__device__ __forceinline__ void walk_ranges(float xi, float yi, float eps, float cs, float reach,
+                                            const GridParams &g, int W, int H, int ox, int oy,
+                                            const int32_t *__restrict__ start, F f) {
     float u = 2.0f * ((xi + eps) / cs), v = 2.0f * ((yi + eps) / cs);
     int bx0 = (int)floorf(u - reach), bx1 = (int)floorf(u + reach);
     int by0 = (int)floorf(v - reach), by1 = (int)floorf(v + reach);
@@ -392,6 +392,7 @@ __device__ __forceinline__ void walk_neighbours(float xi, float yi, float eps, f
     int cxb = min(min(bx1 >> 1, g.gridMinX + g.gridDimX - 1), ox + W - 1);
     int cya = max(max(by0 >> 1, g.gridMinY), oy);
     int cyb = min(min(by1 >> 1, g.gridMinY + g.gridDimY - 1), oy + H - 1);
+    // every bin-boundary load of the (at most 3x3) cells is issued up front
     int4 q[3][3];
     int qn[3][3];
 #pragma unroll
@@ -422,17 +423,32 @@ __device__ __forceinline__ void walk_neighbours(float xi, float yi, float eps, f
                 int i0 = qy * 2 + qxa, i1 = qy * 2 + qxb + 1;
                 int b = sel4(q[dy][dx], i0);
                 int e = (i1 == 4) ? qn[dy][dx] : sel4(q[dy][dx], i1);
-                for (int k = b; k < e; k += U) {
-                    decltype(ld(0, 0)) r[U];
-#pragma unroll
-                    for (int j = 0; j < U; j++) r[j] = ld(min(k + j, e - 1), cy);
-#pragma unroll
-                    for (int j = 0; j < U; j++)
-                        if (k + j < e) f(k + j, r[j]);
-                }
+                if (b < e) f(b, e, cy);
             }
         }
     }
+}
+
+// The walk over every candidate: the candidate records are loaded U at a time
+// so a wave has many loads in flight (the loop is latency bound otherwise:
+// one dependent L2 round trip per candidate).  ld(k, cy) loads candidate k's
+// record (cy: the absolute cell row being walked), f(k, rec) consumes it; f
+// is called once per candidate, in the canonical order.
+template <int U, class L, class F>
+__device__ __forceinline__ void walk_neighbours(float xi, float yi, float eps, float cs,
+                                                float reach, const GridParams &g, int W, int H,
+                                                int ox, int oy, const int32_t *__restrict__ start,
+                                                L ld, F f) {
+    walk_ranges(xi, yi, eps, cs, reach, g, W, H, ox, oy, start, [&](int b, int e, int cy) {
+        for (int k = b; k < e; k += U) {
+            decltype(ld(0, 0)) r[U];
+#pragma unroll
+            for (int j = 0; j < U; j++) r[j] = ld(min(k + j, e - 1), cy);
+#pragma unroll
+            for (int j = 0; j < U; j++)
+                if (k + j < e) f(k + j, r[j]);
+        }
+    });
 }
 
 // XCD-aware block order: hardware block b runs on XCD b % 8; give each XCD a
@@ -448,60 +464,6 @@ __device__ __forceinline__ int xcd_block(int nb) {
 
 __device__ __forceinline__ float walk_reach(float h, float cs) {
     return (2.0f * h / cs) * 1.002f + 2e-3f;
-}
-
-// computeDensity (metal:246-307), one thread per sorted slot
-__global__ void __launch_bounds__(DTPB)
-k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float eps, float stiffness,
-          float restDensity, int W, int H, int ox, int oy,
-          const GridParams *__restrict__ gp, const int32_t *__restrict__ start,
-          const float4 *__restrict__ nbA, float2 *__restrict__ nbB,
-          float *__restrict__ rho, float *__restrict__ pr, int16_t *__restrict__ nlist,
-          int32_t *__restrict__ ncount) {
-    // neighbour list staged in LDS (column-major per block), written out
-    // coalesced at the end: entry = k - s as int16
-    __shared__ int16_t lds_nl[NLIST_CAP * DTPB];
-    int lb = xcd_block((n + DTPB - 1) / DTPB);
-    int s = lb * DTPB + threadIdx.x;
-    if (lb < 0 || s >= (nptr ? *nptr : n)) return;
-    const GridParams g = *gp;
-    const float cs = g.cellSize;
-    const float4 me = nbA[s];
-    const int tid = threadIdx.x;
-    const float xi = me.x, yi = me.y;
-    const float h2 = h * h;
-    const float poly6 = poly6Coeff2D(h);
-    float acc = 0.0f;
-    int cnt = 0;
-    walk_neighbours<4>(xi, yi, eps, cs, walk_reach(h, cs), g, W, H, ox, oy, start,
-                       [&](int k, int) { return nbA[k]; },
-                       [&](int k, const float4 &o) {
-        float dx = xi - o.x, dy = yi - o.y;
-        float r2 = dx * dx + dy * dy;
-        if (r2 < h2) {
-            float diff = h2 - r2;
-            float w = poly6 * diff * diff * diff;
-            acc += o.z * w;
-            // the forces pass sees exactly these neighbours (r^2 < h_ij^2 with
-            // h_ij = h, metal:360-366), in this order
-            if (k != s) {
-                int off = k - s;
-                if (cnt < NLIST_CAP && off >= -32768 && off <= 32767)
-                    lds_nl[cnt * DTPB + tid] = (int16_t)off;
-                else
-                    cnt = NLIST_CAP;          // overflow: forces walks the bins
-                cnt++;
-            }
-        }
-    });
-    ncount[s] = cnt;
-    const int m = cnt <= NLIST_CAP ? cnt : 0;
-    for (int j = 0; j < m; j++) nlist[(size_t)j * nstride + s] = lds_nl[j * DTPB + tid];
-    float pres = stiffness * (acc - restDensity);
-    if (pres < 0.f) pres = 0.f;
-    rho[s] = acc;
-    pr[s] = pres;
-    nbB[2 * s + 1] = make_float2(acc, pres / (acc * acc));   // the p_j / rho_j^2 of metal:370
 }
 
 // ---------------------------------------------------------------------------
@@ -587,16 +549,25 @@ __device__ __forceinline__ int stage_index(const Stage &st, int k, int cyc, int 
     return st.segL[i] + (k - st.segS[i]);
 }
 
+// computeDensity (metal:246-307), one thread per sorted slot, SB slots per
+// block with the neighbourhood staged in LDS.  Besides rho and p it writes
+// the neighbours of the forces pass (r^2 < h^2, not itself: metal:360-366) in
+// the canonical walk order as int16 slot offsets k - s, packed four to a
+// uint2 and column-major [NLIST_CAP / 4][nstride] (one 8-byte store per four
+// neighbours; more than NLIST_CAP: ncount > NLIST_CAP and the forces pass
+// walks the bins).
 __global__ void __launch_bounds__(SB)
-k_density_staged(int n, float h, float eps, float stiffness, float restDensity, int W, int H, int ox,
-                 int oy, const GridParams *__restrict__ gp, const int32_t *__restrict__ start,
-                 const float4 *__restrict__ nbA, float2 *__restrict__ nbB, float *__restrict__ rho,
-                 float *__restrict__ pr, int32_t *__restrict__ status) {
+k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float eps, float stiffness,
+          float restDensity, int W, int H, int ox, int oy, const GridParams *__restrict__ gp,
+          const int32_t *__restrict__ start, const float4 *__restrict__ nbA, float2 *__restrict__ nbB,
+          float *__restrict__ rho, float *__restrict__ pr, uint2 *__restrict__ nlist,
+          int32_t *__restrict__ ncount, int32_t *__restrict__ status) {
     __shared__ Stage st;
     __shared__ float4 lrec[STAGE_CAP];
     const int lb = xcd_block((n + SB - 1) / SB);
     if (lb < 0) return;                                   // whole block idle
-    const int s0 = lb * SB, s1 = min(s0 + SB, n);
+    const int nn = nptr ? *nptr : n;
+    const int s0 = lb * SB, s1 = min(s0 + SB, nn);
     const GridParams g = *gp;
     const float cs = g.cellSize;
     stage_plan(st, s0, s1, nbA, eps, cs, W, H, ox, oy, start);
@@ -618,13 +589,29 @@ k_density_staged(int n, float h, float eps, float stiffness, float restDensity, 
     const float h2 = h * h;
     const float poly6 = poly6Coeff2D(h);
     float acc = 0.0f;
-    auto body = [&](int, const float4 &o) {
+    int cnt = 0;
+    uint32_t pk0 = 0u, pk1 = 0u;                  // the current group of four offsets
+    auto body = [&](int k, const float4 &o) {
         float dx = xi - o.x, dy = yi - o.y;
         float r2 = dx * dx + dy * dy;
         if (r2 < h2) {
             float diff = h2 - r2;
             float w = poly6 * diff * diff * diff;
             acc += o.z * w;
+            if (k != s) {
+                const int off = k - s;
+                if (cnt < NLIST_CAP && off >= -32768 && off <= 32767) {
+                    const uint32_t v = (uint32_t)(off & 0xffff) << (16 * (cnt & 1));
+                    if (cnt & 2) pk1 |= v; else pk0 |= v;
+                    if ((cnt & 3) == 3) {
+                        nlist[(size_t)(cnt >> 2) * nstride + s] = make_uint2(pk0, pk1);
+                        pk0 = pk1 = 0u;
+                    }
+                } else {
+                    cnt = NLIST_CAP;          // overflow: forces walks the bins
+                }
+                cnt++;
+            }
         }
     };
     if (st.ok)
@@ -633,6 +620,8 @@ k_density_staged(int n, float h, float eps, float stiffness, float restDensity, 
     else
         walk_neighbours<4>(xi, yi, eps, cs, walk_reach(h, cs), g, W, H, ox, oy, start,
                            [&](int k, int) { return nbA[k]; }, body);
+    if (cnt <= NLIST_CAP && (cnt & 3)) nlist[(size_t)(cnt >> 2) * nstride + s] = make_uint2(pk0, pk1);
+    ncount[s] = cnt;
     float pres = stiffness * (acc - restDensity);
     if (pres < 0.f) pres = 0.f;
     rho[s] = acc;
@@ -657,7 +646,7 @@ __global__ void __launch_bounds__(TPB)
 k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict__ gp,
                 const int32_t *__restrict__ start, PState S, const float4 *__restrict__ nbA,
                 const float4 *__restrict__ nbB, const float *__restrict__ pr,
-                const int16_t *__restrict__ nlist, const int32_t *__restrict__ ncount, PState P,
+                const uint2 *__restrict__ nlist, const int32_t *__restrict__ ncount, PState P,
                 const lpe_gpu_rigid *__restrict__ rig, const int32_t *__restrict__ rbinStart,
                 const int32_t *__restrict__ rbinList, float *__restrict__ accum,
                 int32_t *__restrict__ status) {
@@ -721,11 +710,17 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     if (cnt <= NLIST_CAP) {
         // the density pass's list: the r^2 < h^2 neighbours in canonical
         // order, so the heavy pair math runs only on real neighbours
-        constexpr int U = 4;
+        constexpr int U = 4;                      // one packed group of four offsets
         for (int j = 0; j < cnt; j += U) {
+            const uint2 g4 = nlist[(size_t)(j >> 2) * sp.nstride + s];
             int kk[U];
+            kk[0] = s + (int)(int16_t)(g4.x & 0xffffu);
+            kk[1] = s + (int)(int16_t)(g4.x >> 16);
+            kk[2] = s + (int)(int16_t)(g4.y & 0xffffu);
+            kk[3] = s + (int)(int16_t)(g4.y >> 16);
 #pragma unroll
-            for (int u = 0; u < U; u++) kk[u] = s + nlist[(size_t)min(j + u, cnt - 1) * sp.nstride + s];
+            for (int u = 1; u < U; u++)
+                if (j + u >= cnt) kk[u] = kk[0];     // unused slots of the last group
             Rec r[U];
 #pragma unroll
             for (int u = 0; u < U; u++) r[u] = Rec{nbA[kk[u]], nbB[kk[u]]};
@@ -1312,7 +1307,7 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     LPE_HIP(ctx, hipMalloc((void **)&d.pr, sizeof(float) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.nbA, sizeof(float4) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.nbB, sizeof(float4) * N));
-    LPE_HIP(ctx, hipMalloc((void **)&d.nlist, sizeof(int16_t) * N * NLIST_CAP));
+    LPE_HIP(ctx, hipMalloc((void **)&d.nlist, sizeof(uint2) * N * (NLIST_CAP / 4)));
     LPE_HIP(ctx, hipMalloc((void **)&d.ncount, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.key, sizeof(uint32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpId, sizeof(int32_t) * N));
@@ -1518,10 +1513,10 @@ static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool pr
 static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr) {
     SphDev &d = ctx->sph;
     const lpe_fluid_config &c = d.cfg;
-    LPE_KERNEL(ctx, "k_density", k_density, dim3(xcd_grid(nblk(n, DTPB))), dim3(DTPB), 0, ctx->stream, n,
+    LPE_KERNEL(ctx, "k_density", k_density, dim3(xcd_grid(nblk(n, SB))), dim3(SB), 0, ctx->stream, n,
                        nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
                        c.restDensity, d.W, d.H, d.ox, d.oy, d.gp, d.start, d.nbA, (float2 *)d.nbB,
-                       d.rho, d.pr, d.nlist, d.ncount);
+                       d.rho, d.pr, d.nlist, d.ncount, d.status);
     LPE_CHECK_LAUNCH(ctx, "k_density");
     return LPE_OK;
 }
@@ -1854,13 +1849,8 @@ extern "C" int lpe_sph_probe_density(lpe_ctx *ctx, float *density, float *pressu
     (void)hipSetDevice(ctx->device);
     int st = sph_hash(ctx, 0.f, 0.f, false, true);
     if (st) return st;
-    const lpe_fluid_config &c = d.cfg;
-    // computeDensity alone (no neighbour list): the LDS-staged pass
-    LPE_KERNEL(ctx, "k_density_staged", k_density_staged, dim3(xcd_grid(nblk(d.n, SB))), dim3(SB), 0,
-               ctx->stream, d.n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
-               c.restDensity, d.W, d.H, d.ox, d.oy, d.gp, d.start, d.nbA, (float2 *)d.nbB, d.rho,
-               d.pr, d.status);
-    LPE_CHECK_LAUNCH(ctx, "k_density_staged");
+    st = sph_density(ctx, d.n, nullptr);           // the tick's density pass, as is
+    if (st) return st;
     // rho/p are in S slot order here; S.x.. are the unpermute staging buffers,
     // so keep S.id aside in tmpOld first
     LPE_HIP(ctx, hipMemcpyAsync(d.tmpOld, d.S.id, sizeof(int32_t) * d.n, hipMemcpyDeviceToDevice,
