@@ -38,7 +38,7 @@ struct SphDev {
     float *rho = nullptr, *pr = nullptr;  // in S/P slot order
     float4 *nbA = nullptr;        // sorted neighbour records (x, y, m, -)
     float4 *nbB = nullptr;        // (vx, vy, rho, p / rho^2)
-    uint2 *nlist = nullptr;       // per-slot neighbour list k - s (int16, 4 per uint2), [cap/4][cap_n]
+    int16_t *nlist = nullptr;     // per-slot neighbour list k - s, column-major [cap][cap_n]
     int32_t *ncount = nullptr;    // neighbours found (> cap: forces walks the bins)
     // counting-sort grid hash over (2h cell, h quadrant) bins
     uint32_t *key = nullptr;      // bin of each P slot
@@ -63,6 +63,8 @@ struct SphDev {
     int32_t *rbinList = nullptr;
     int32_t *rbinCount = nullptr;
     int cap_rbins = 0, cap_rlist = 0;
+    float4 *raabb = nullptr;      // coupling rigids' AABBs (minX, maxX, minY, maxY), per tick
+    int cap_raabb = 0;
     int bx0 = 0, by0 = 0, bW = 0, bH = 0;
     float bcs = 0.25f;
     int rlist_len = 0;

@@ -494,7 +494,7 @@ __device__ __forceinline__ void cell_xy(float x, float y, float eps, float cs, i
 
 // Plans st (block-uniform) for slots [s0, s1); every thread of the block
 // calls it (it holds barriers).
-__device__ void stage_plan(Stage &st, int s0, int s1, const float4 *__restrict__ nbA, float eps,
+__device__ void stage_plan(Stage &st, int cap, int s0, int s1, const float4 *__restrict__ nbA, float eps,
                            float cs, int W, int H, int ox, int oy, const int32_t *__restrict__ start) {
     const int tid = threadIdx.x;
     if (tid == 0) {
@@ -538,7 +538,7 @@ __device__ void stage_plan(Stage &st, int s0, int s1, const float4 *__restrict__
     if (tid == 0 && st.ok) {
         int off = 0;
         for (int i = 0; i < 6; i++) { st.segL[i] = off; off += st.segE[i] - st.segS[i]; }
-        if (off > STAGE_CAP) st.ok = 0;
+        if (off > cap) st.ok = 0;
     }
     __syncthreads();
 }
@@ -552,15 +552,14 @@ __device__ __forceinline__ int stage_index(const Stage &st, int k, int cyc, int 
 // computeDensity (metal:246-307), one thread per sorted slot, SB slots per
 // block with the neighbourhood staged in LDS.  Besides rho and p it writes
 // the neighbours of the forces pass (r^2 < h^2, not itself: metal:360-366) in
-// the canonical walk order as int16 slot offsets k - s, packed four to a
-// uint2 and column-major [NLIST_CAP / 4][nstride] (one 8-byte store per four
-// neighbours; more than NLIST_CAP: ncount > NLIST_CAP and the forces pass
-// walks the bins).
+// the canonical walk order as int16 slot offsets k - s, column-major
+// [NLIST_CAP][nstride] (more than NLIST_CAP: ncount > NLIST_CAP and the
+// forces pass walks the bins).
 __global__ void __launch_bounds__(SB)
 k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float eps, float stiffness,
           float restDensity, int W, int H, int ox, int oy, const GridParams *__restrict__ gp,
           const int32_t *__restrict__ start, const float4 *__restrict__ nbA, float2 *__restrict__ nbB,
-          float *__restrict__ rho, float *__restrict__ pr, uint2 *__restrict__ nlist,
+          float *__restrict__ rho, float *__restrict__ pr, int16_t *__restrict__ nlist,
           int32_t *__restrict__ ncount, int32_t *__restrict__ status) {
     __shared__ Stage st;
     __shared__ float4 lrec[STAGE_CAP];
@@ -570,7 +569,7 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     const int s0 = lb * SB, s1 = min(s0 + SB, nn);
     const GridParams g = *gp;
     const float cs = g.cellSize;
-    stage_plan(st, s0, s1, nbA, eps, cs, W, H, ox, oy, start);
+    stage_plan(st, STAGE_CAP, s0, s1, nbA, eps, cs, W, H, ox, oy, start);
     if (st.ok) {
 #pragma unroll
         for (int i = 0; i < 6; i++) {
@@ -590,7 +589,6 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     const float poly6 = poly6Coeff2D(h);
     float acc = 0.0f;
     int cnt = 0;
-    uint32_t pk0 = 0u, pk1 = 0u;                  // the current group of four offsets
     auto body = [&](int k, const float4 &o) {
         float dx = xi - o.x, dy = yi - o.y;
         float r2 = dx * dx + dy * dy;
@@ -600,16 +598,10 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
             acc += o.z * w;
             if (k != s) {
                 const int off = k - s;
-                if (cnt < NLIST_CAP && off >= -32768 && off <= 32767) {
-                    const uint32_t v = (uint32_t)(off & 0xffff) << (16 * (cnt & 1));
-                    if (cnt & 2) pk1 |= v; else pk0 |= v;
-                    if ((cnt & 3) == 3) {
-                        nlist[(size_t)(cnt >> 2) * nstride + s] = make_uint2(pk0, pk1);
-                        pk0 = pk1 = 0u;
-                    }
-                } else {
+                if (cnt < NLIST_CAP && off >= -32768 && off <= 32767)
+                    nlist[(size_t)cnt * nstride + s] = (int16_t)off;
+                else
                     cnt = NLIST_CAP;          // overflow: forces walks the bins
-                }
                 cnt++;
             }
         }
@@ -620,7 +612,6 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     else
         walk_neighbours<4>(xi, yi, eps, cs, walk_reach(h, cs), g, W, H, ox, oy, start,
                            [&](int k, int) { return nbA[k]; }, body);
-    if (cnt <= NLIST_CAP && (cnt & 3)) nlist[(size_t)(cnt >> 2) * nstride + s] = make_uint2(pk0, pk1);
     ncount[s] = cnt;
     float pres = stiffness * (acc - restDensity);
     if (pres < 0.f) pres = 0.f;
@@ -646,9 +637,10 @@ __global__ void __launch_bounds__(TPB)
 k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict__ gp,
                 const int32_t *__restrict__ start, PState S, const float4 *__restrict__ nbA,
                 const float4 *__restrict__ nbB, const float *__restrict__ pr,
-                const uint2 *__restrict__ nlist, const int32_t *__restrict__ ncount, PState P,
-                const lpe_gpu_rigid *__restrict__ rig, const int32_t *__restrict__ rbinStart,
-                const int32_t *__restrict__ rbinList, float *__restrict__ accum,
+                const int16_t *__restrict__ nlist, const int32_t *__restrict__ ncount, PState P,
+                const lpe_gpu_rigid *__restrict__ rig, const float4 *__restrict__ raabb,
+                const int32_t *__restrict__ rbinStart, const int32_t *__restrict__ rbinList,
+                float *__restrict__ accum,
                 int32_t *__restrict__ status) {
     int lb = xcd_block((sp.n + TPB - 1) / TPB);
     int s = lb * TPB + threadIdx.x;
@@ -710,17 +702,11 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     if (cnt <= NLIST_CAP) {
         // the density pass's list: the r^2 < h^2 neighbours in canonical
         // order, so the heavy pair math runs only on real neighbours
-        constexpr int U = 4;                      // one packed group of four offsets
+        constexpr int U = 4;
         for (int j = 0; j < cnt; j += U) {
-            const uint2 g4 = nlist[(size_t)(j >> 2) * sp.nstride + s];
             int kk[U];
-            kk[0] = s + (int)(int16_t)(g4.x & 0xffffu);
-            kk[1] = s + (int)(int16_t)(g4.x >> 16);
-            kk[2] = s + (int)(int16_t)(g4.y & 0xffffu);
-            kk[3] = s + (int)(int16_t)(g4.y >> 16);
 #pragma unroll
-            for (int u = 1; u < U; u++)
-                if (j + u >= cnt) kk[u] = kk[0];     // unused slots of the last group
+            for (int u = 0; u < U; u++) kk[u] = s + nlist[(size_t)min(j + u, cnt - 1) * sp.nstride + s];
             Rec r[U];
 #pragma unroll
             for (int u = 0; u < U; u++) r[u] = Rec{nbA[kk[u]], nbB[kk[u]]};
@@ -747,10 +733,9 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         int bin = (int)fby * cp.bW + (int)fbx;
         k0 = rbinStart[bin]; k1 = rbinStart[bin + 1];
         if (sp.diag && k1 > k0) atomicAdd(&status[ST_RIGID_CAND], k1 - k0);
-        // impulse solver: dispatched only if R > 0 (fluid.cpp:910)
-        couple_impulse(st, cp, sp.dt, rig, rbinList, k0, k1, accum);
     }
-    couple_position(st, cp, rig, rbinList, k0, k1);
+    // impulse solver: dispatched only if R > 0 (fluid.cpp:910); push-out always
+    couple_both(st, cp, sp.dt, cp.nr > 0, rig, raabb, rbinList, k0, k1, accum);
     P.x[out] = st.x; P.y[out] = st.y;
     P.vx[out] = st.vx; P.vy[out] = st.vy;
     P.vhx[out] = st.vhx; P.vhy[out] = st.vhy;
@@ -980,6 +965,13 @@ __device__ __forceinline__ int bin_of(float v, float bcs, int b0, int nb) {
     t = fminf(fmaxf(t, 0.f), (float)(nb - 1));
     return (int)t;
 }
+// compact AABBs of the coupling rigids: (minX, maxX, minY, maxY)
+__global__ void k_rig_aabb(int nr, const lpe_gpu_rigid *__restrict__ rig, float4 *__restrict__ aabb) {
+    int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nr) return;
+    aabb[r] = make_float4(rig[r].minX, rig[r].maxX, rig[r].minY, rig[r].maxY);
+}
+
 // one wave per rigid, lanes stride over the bins its AABB covers (a wall
 // covers thousands of 0.25 m bins; a thread per rigid serialises on it)
 __global__ void k_rbin_count(int nr, const lpe_gpu_rigid *__restrict__ rig, float bcs,
@@ -1105,7 +1097,7 @@ static void sph_free(SphDev &d) {
     pstate_free(d.P);
     pstate_free(d.S);
     void *ptrs[] = {d.rho, d.pr, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.count, d.start, d.cursor,
-                    d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.accum, d.rbinStart,
+                    d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.raabb, d.accum, d.rbinStart,
                     d.rbinList, d.rbinCount, d.coupleBody};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     d = SphDev();
@@ -1307,7 +1299,7 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     LPE_HIP(ctx, hipMalloc((void **)&d.pr, sizeof(float) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.nbA, sizeof(float4) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.nbB, sizeof(float4) * N));
-    LPE_HIP(ctx, hipMalloc((void **)&d.nlist, sizeof(uint2) * N * (NLIST_CAP / 4)));
+    LPE_HIP(ctx, hipMalloc((void **)&d.nlist, sizeof(int16_t) * N * NLIST_CAP));
     LPE_HIP(ctx, hipMalloc((void **)&d.ncount, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.key, sizeof(uint32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpId, sizeof(int32_t) * N));
@@ -1462,6 +1454,12 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
         d.cap_rbins = B;
     }
     hipStream_t s = ctx->stream;
+    if (d.nr > d.cap_raabb || !d.raabb) {
+        if (d.raabb) (void)hipFree(d.raabb);
+        LPE_HIP(ctx, hipMalloc((void **)&d.raabb, sizeof(float4) * (size_t)d.nr));
+        d.cap_raabb = d.nr;
+    }
+    LPE_KERNEL(ctx, "k_rig_aabb", k_rig_aabb, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig, d.raabb);
     LPE_HIP(ctx, hipMemsetAsync(d.rbinCount, 0, sizeof(int32_t) * B, s));
     LPE_KERNEL(ctx, "k_rbin_count", k_rbin_count, dim3(nblk(d.nr, 4)), dim3(256), 0, s, d.nr, d.rig, d.bcs,
                        d.bx0, d.by0, d.bW, d.bH, d.rbinCount);
@@ -1688,7 +1686,7 @@ extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
         }
         if (st) return st;
         LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(xcd_grid(nblk(sp.n))), dim3(TPB), 0, s, sp, cp, d.gp,
-                           d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.rbinStart, d.rbinList,
+                           d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart, d.rbinList,
                            d.accum, d.status);
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
     }

@@ -73,155 +73,68 @@ struct CoupleState {
     float x, y, vx, vy, vhx, vhy, ax, ay, mass, rho, p;
 };
 
-// rigidFluidImpulseSolver for one particle; adds to the rigid accumulators.
-__device__ __forceinline__ void couple_impulse(CoupleState &st, const CoupleParams &cp, float dt,
-                                               const lpe_gpu_rigid *__restrict__ rig,
-                                               const int32_t *__restrict__ list, int k0, int k1,
-                                               float *__restrict__ accum) {
-    float densityF = st.rho > 0.0f ? st.rho : cp.restDensity;
-    float pressureF = st.p;
-    float tffx = 0.0f, tffy = 0.0f;
-    bool had = false;
-    const float px = st.x, py = st.y;
-    for (int k = k0; k < k1; k++) {
-        const int r = list[k];
-        const lpe_gpu_rigid &rb = rig[r];
-        float rbVelSq = rb.vx * rb.vx + rb.vy * rb.vy + rb.omega * rb.omega;
-        if (rbVelSq > cp.maxSafeVelocitySq) continue;
-        if (px < rb.minX || px > rb.maxX || py < rb.minY || py > rb.maxY) continue;
-        bool inside = false;
-        float pen = 0.0f, relx = 0.f, rely = 0.f, nx = 0.f, ny = 0.f;
-        if (rb.shapeType == 0) {
-            float rx = px - rb.posX, ry = py - rb.posY;
-            float dist2 = rx * rx + ry * ry;
-            float radiusSq = rb.radius * rb.radius;
-            if (dist2 < radiusSq) {
-                inside = true;
-                float dist = sqrtf(dist2);
-                if (dist < cp.minPenetration) dist = cp.minPenetration;
-                pen = rb.radius - dist;
-                if (pen < 0.0f) pen = 0.0f;
-                relx = rx; rely = ry;
-                nx = relx / dist; ny = rely / dist;
-            }
-        } else if (rb.shapeType == 1 && rb.vertCount >= 3) {
-            inside = pointInPolygon(px, py, rb);
-            if (inside) {
-                float cx, cy;
-                closestPointOnPolygon(px, py, rb, cx, cy);
-                float dx = px - cx, dy = py - cy;
-                float d2 = dx * dx + dy * dy;
-                float d = sqrtf(d2);
-                if (d < cp.minPenetration) d = cp.minPenetration;
-                pen = d;
-                if (pen < 0.0f) pen = 0.0f;
-                relx = px - rb.posX; rely = py - rb.posY;
-                nx = dx / d; ny = dy / d;
-            }
-        }
-        if (!inside || pen < cp.minPenetration) continue;
-        had = true;
-        float rotx = -rb.omega * rely, roty = rb.omega * relx;
-        float rvx = rb.vx + rotx, rvy = rb.vy + roty;
-        float relVx = st.vx - rvx, relVy = st.vy - rvy;
-        float depthFactor = lpe_tanhf(cp.depthTransitionRate * pen / cp.depthScale);
-        float normalVel = relVx * nx + relVy * ny;
-        float nvx = nx * normalVel, nvy = ny * normalVel;
-        float tvx = relVx - nvx, tvy = relVy - nvy;
-        float particleVolume = st.mass / densityF;
-        float effectiveArea = lpe_powf(particleVolume, 2.0f / 3.0f);
-        float depth = fminf(py / cp.depthEstimateScale, 1.0f);
-        float hydro = densityF * cp.gravity * depth;
-        float totalPressure = pressureF + hydro;
-        float pressureForce = totalPressure * effectiveArea * depthFactor;
-        float pfm = fminf(pressureForce, cp.maxForce * cp.pressureForceRatio);
-        float pfx = nx * pfm, pfy = ny * pfm;
-        float tangentVelMag = f2len(tvx, tvy);
-        if (tangentVelMag > cp.minRelVelocity) {
-            float tdx = tvx / tangentVelMag, tdy = tvy / tangentVelMag;
-            float viscosityCoef = cp.viscosity * cp.viscosityScale;
-            float viscousForce = viscosityCoef * tangentVelMag * densityF * depthFactor * dt;
-            float vfm = fminf(viscousForce, cp.maxForce * cp.viscousForceRatio);
-            pfx += -tdx * vfm;
-            pfy += -tdy * vfm;
-        }
-        if (rb.mass > 0.1f) {
-            float bxf = 0.0f * cp.buoyancyStrength * pen * effectiveArea * cp.gravity * densityF;
-            float byf = -1.0f * cp.buoyancyStrength * pen * effectiveArea * cp.gravity * densityF;
-            float cbx = pfx + bxf, cby = pfy + byf;
-            if (f2len(cbx, cby) <= cp.maxForce) { pfx = cbx; pfy = cby; }
-        }
-        float tfx = pfx, tfy = pfy;
-        float forceMag = f2len(tfx, tfy);
-        if (forceMag > cp.maxForce) {
-            float sc = cp.maxForce / forceMag;
-            tfx = tfx * sc; tfy = tfy * sc;
-        }
-        float torque = relx * tfy - rely * tfx;
-        torque = fminf(fmaxf(torque, -cp.maxTorque), cp.maxTorque);
-        if (fabsf(rb.omega) > cp.angDampThr) {
-            float sgn = (rb.omega > 0.f) ? 1.f : ((rb.omega < 0.f) ? -1.f : 0.f);
-            torque -= cp.angDampFactor * sgn * fabsf(rb.omega) * rb.inertia;
-        }
-        atomicAdd(&accum[3 * r + 0], tfx);
-        atomicAdd(&accum[3 * r + 1], tfy);
-        atomicAdd(&accum[3 * r + 2], torque);
-        tffx -= tfx * cp.fluidForceScale;
-        tffy -= tfy * cp.fluidForceScale;
+// One rigid's contribution to the impulse solver (metal:792-900), given the
+// penetration, lever arm and normal of the particle inside it.
+__device__ __forceinline__ void impulse_term(const CoupleState &st, const CoupleParams &cp, float dt,
+                                             const lpe_gpu_rigid &rb, int r, float pen, float relx,
+                                             float rely, float nx, float ny, float densityF,
+                                             float pressureF, float *__restrict__ accum, float &tffx,
+                                             float &tffy, bool &had) {
+    had = true;
+    const float py = st.y;
+    float rotx = -rb.omega * rely, roty = rb.omega * relx;
+    float rvx = rb.vx + rotx, rvy = rb.vy + roty;
+    float relVx = st.vx - rvx, relVy = st.vy - rvy;
+    float depthFactor = lpe_tanhf(cp.depthTransitionRate * pen / cp.depthScale);
+    float normalVel = relVx * nx + relVy * ny;
+    float nvx = nx * normalVel, nvy = ny * normalVel;
+    float tvx = relVx - nvx, tvy = relVy - nvy;
+    float particleVolume = st.mass / densityF;
+    float effectiveArea = lpe_powf(particleVolume, 2.0f / 3.0f);
+    float depth = fminf(py / cp.depthEstimateScale, 1.0f);
+    float hydro = densityF * cp.gravity * depth;
+    float totalPressure = pressureF + hydro;
+    float pressureForce = totalPressure * effectiveArea * depthFactor;
+    float pfm = fminf(pressureForce, cp.maxForce * cp.pressureForceRatio);
+    float pfx = nx * pfm, pfy = ny * pfm;
+    float tangentVelMag = f2len(tvx, tvy);
+    if (tangentVelMag > cp.minRelVelocity) {
+        float tdx = tvx / tangentVelMag, tdy = tvy / tangentVelMag;
+        float viscosityCoef = cp.viscosity * cp.viscosityScale;
+        float viscousForce = viscosityCoef * tangentVelMag * densityF * depthFactor * dt;
+        float vfm = fminf(viscousForce, cp.maxForce * cp.viscousForceRatio);
+        pfx += -tdx * vfm;
+        pfy += -tdy * vfm;
     }
-    if (had) {
-        float fm = f2len(tffx, tffy);
-        if (fm > cp.fluidForceMax) {
-            float sc = cp.fluidForceMax / fm;
-            tffx = tffx * sc; tffy = tffy * sc;
-        }
-        float invMass = (st.mass > 0.0001f) ? 1.0f / st.mass : 1.0f;
-        st.ax += tffx * invMass;
-        st.ay += tffy * invMass;
+    if (rb.mass > 0.1f) {
+        float bxf = 0.0f * cp.buoyancyStrength * pen * effectiveArea * cp.gravity * densityF;
+        float byf = -1.0f * cp.buoyancyStrength * pen * effectiveArea * cp.gravity * densityF;
+        float cbx = pfx + bxf, cby = pfy + byf;
+        if (f2len(cbx, cby) <= cp.maxForce) { pfx = cbx; pfy = cby; }
     }
+    float tfx = pfx, tfy = pfy;
+    float forceMag = f2len(tfx, tfy);
+    if (forceMag > cp.maxForce) {
+        float sc = cp.maxForce / forceMag;
+        tfx = tfx * sc; tfy = tfy * sc;
+    }
+    float torque = relx * tfy - rely * tfx;
+    torque = fminf(fmaxf(torque, -cp.maxTorque), cp.maxTorque);
+    if (fabsf(rb.omega) > cp.angDampThr) {
+        float sgn = (rb.omega > 0.f) ? 1.f : ((rb.omega < 0.f) ? -1.f : 0.f);
+        torque -= cp.angDampFactor * sgn * fabsf(rb.omega) * rb.inertia;
+    }
+    atomicAdd(&accum[3 * r + 0], tfx);
+    atomicAdd(&accum[3 * r + 1], tfy);
+    atomicAdd(&accum[3 * r + 2], torque);
+    tffx -= tfx * cp.fluidForceScale;
+    tffy -= tfy * cp.fluidForceScale;
 }
 
-// rigidFluidPositionSolver for one particle (always dispatched, fluid.cpp:929-942).
-__device__ __forceinline__ void couple_position(CoupleState &st, const CoupleParams &cp,
-                                                const lpe_gpu_rigid *__restrict__ rig,
-                                                const int32_t *__restrict__ list, int k0, int k1) {
-    float oldx = st.x, oldy = st.y;
-    float acx = 0.0f, acy = 0.0f;
-    const float px = st.x, py = st.y;
-    bool hadCollision = false;
-    for (int k = k0; k < k1; k++) {
-        const lpe_gpu_rigid &b = rig[list[k]];
-        if (px < b.minX || px > b.maxX || py < b.minY || py > b.maxY) continue;
-        if (b.shapeType == 0) {
-            float dx = px - b.posX, dy = py - b.posY;
-            float dist2 = dx * dx + dy * dy;
-            float radius = b.radius;
-            if (dist2 < radius * radius) {
-                hadCollision = true;
-                float dist = sqrtf(dist2);
-                if (dist < cp.minSafeDistance) { dist = cp.minSafeDistance; dx = 1.0f; dy = 0.0f; }
-                float pen = (radius - dist) + cp.safetyMargin;
-                float dirx = dx / dist, diry = dy / dist;
-                acx -= dirx * pen * cp.relaxFactor;
-                acy -= diry * pen * cp.relaxFactor;
-            }
-        } else if (b.shapeType == 1) {
-            if (b.vertCount < 3) continue;
-            if (pointInPolygon(px, py, b)) {
-                hadCollision = true;
-                float cx, cy;
-                closestPointOnPolygon(px, py, b, cx, cy);
-                float cdx = px - cx, cdy = py - cy;
-                float d2 = cdx * cdx + cdy * cdy;
-                float d = sqrtf(d2);
-                if (d < cp.minSafeDistance) { d = cp.minSafeDistance; cdx = 1.0f; cdy = 0.0f; }
-                float pen = d + cp.safetyMargin;
-                float dirx = cdx / d, diry = cdy / d;
-                acx += dirx * pen * cp.relaxFactor;
-                acy += diry * pen * cp.relaxFactor;
-            }
-        }
-    }
+// The position solver's clamp, move, boundary offset and velocity projection
+// (metal:640-668).
+__device__ __forceinline__ void position_tail(CoupleState &st, const CoupleParams &cp, float oldx, float oldy,
+                                              float acx, float acy, bool hadCollision) {
     float cm = f2len(acx, acy);
     if (cm > cp.maxCorrection) {
         acx = (acx / cm) * cp.maxCorrection;
@@ -247,6 +160,105 @@ __device__ __forceinline__ void couple_position(CoupleState &st, const CouplePar
             }
         }
     }
+}
+
+// rigidFluidImpulseSolver (metal:679-924) followed by rigidFluidPositionSolver
+// (metal:533-668; always dispatched, fluid.cpp:929-942) for one particle, in
+// one pass over its candidate rigids.  The position solver tests exactly the
+// rigids whose AABB holds the particle (the impulse solver additionally skips
+// fast rigids), at the same position (the impulse solver only changes the
+// acceleration), so the containment and closest-point geometry is computed
+// once per (particle, rigid) and each solver accumulates in candidate order
+// exactly as the two separate loops.  aabb[r] = (minX, maxX, minY, maxY) of
+// rig[r]: one 16-B load per candidate, the full record only for AABB hits.
+__device__ __forceinline__ void couple_both(CoupleState &st, const CoupleParams &cp, float dt, bool impulse,
+                                           const lpe_gpu_rigid *__restrict__ rig,
+                                           const float4 *__restrict__ aabb,
+                                           const int32_t *__restrict__ list, int k0, int k1,
+                                           float *__restrict__ accum) {
+    // impulse solver state (metal:679-924)
+    const float densityF = st.rho > 0.0f ? st.rho : cp.restDensity;
+    const float pressureF = st.p;
+    float tffx = 0.0f, tffy = 0.0f;
+    bool had = false;
+    // position solver state (metal:533-668)
+    const float oldx = st.x, oldy = st.y;
+    float acx = 0.0f, acy = 0.0f;
+    bool hadCollision = false;
+    const float px = st.x, py = st.y;
+    auto body = [&](int r) {
+        const lpe_gpu_rigid &rb = rig[r];
+        const bool fast = (rb.vx * rb.vx + rb.vy * rb.vy + rb.omega * rb.omega) > cp.maxSafeVelocitySq;
+        const bool doImp = impulse && !fast;
+        if (rb.shapeType == 0) {
+            const float rx = px - rb.posX, ry = py - rb.posY;
+            const float dist2 = rx * rx + ry * ry;
+            const float radius = rb.radius;
+            if (!(dist2 < radius * radius)) return;
+            const float dist0 = sqrtf(dist2);
+            if (doImp) {
+                float dist = dist0;
+                if (dist < cp.minPenetration) dist = cp.minPenetration;
+                float pen = radius - dist;
+                if (pen < 0.0f) pen = 0.0f;
+                if (!(pen < cp.minPenetration))
+                    impulse_term(st, cp, dt, rb, r, pen, rx, ry, rx / dist, ry / dist, densityF, pressureF,
+                                 accum, tffx, tffy, had);
+            }
+            hadCollision = true;
+            float dist = dist0, dx = rx, dy = ry;
+            if (dist < cp.minSafeDistance) { dist = cp.minSafeDistance; dx = 1.0f; dy = 0.0f; }
+            const float pen = (radius - dist) + cp.safetyMargin;
+            const float dirx = dx / dist, diry = dy / dist;
+            acx -= dirx * pen * cp.relaxFactor;
+            acy -= diry * pen * cp.relaxFactor;
+        } else if (rb.shapeType == 1) {
+            if (rb.vertCount < 3 || !pointInPolygon(px, py, rb)) return;
+            float cx, cy;
+            closestPointOnPolygon(px, py, rb, cx, cy);
+            const float dx = px - cx, dy = py - cy;
+            const float d0 = sqrtf(dx * dx + dy * dy);
+            if (doImp) {
+                float d = d0;
+                if (d < cp.minPenetration) d = cp.minPenetration;
+                float pen = d;
+                if (pen < 0.0f) pen = 0.0f;
+                if (!(pen < cp.minPenetration))
+                    impulse_term(st, cp, dt, rb, r, pen, px - rb.posX, py - rb.posY, dx / d, dy / d, densityF,
+                                 pressureF, accum, tffx, tffy, had);
+            }
+            hadCollision = true;
+            float d = d0, cdx = dx, cdy = dy;
+            if (d < cp.minSafeDistance) { d = cp.minSafeDistance; cdx = 1.0f; cdy = 0.0f; }
+            const float pen = d + cp.safetyMargin;
+            const float dirx = cdx / d, diry = cdy / d;
+            acx += dirx * pen * cp.relaxFactor;
+            acy += diry * pen * cp.relaxFactor;
+        }
+    };
+    constexpr int U = 4;
+    for (int k = k0; k < k1; k += U) {
+        int rr[U];
+        float4 bb[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) rr[u] = list[min(k + u, k1 - 1)];
+#pragma unroll
+        for (int u = 0; u < U; u++) bb[u] = aabb[rr[u]];
+#pragma unroll
+        for (int u = 0; u < U; u++)
+            if (k + u < k1 && !(px < bb[u].x || px > bb[u].y || py < bb[u].z || py > bb[u].w)) body(rr[u]);
+    }
+    if (had) {
+        float fm = f2len(tffx, tffy);
+        if (fm > cp.fluidForceMax) {
+            float sc = cp.fluidForceMax / fm;
+            tffx = tffx * sc; tffy = tffy * sc;
+        }
+        float invMass = (st.mass > 0.0001f) ? 1.0f / st.mass : 1.0f;
+        st.ax += tffx * invMass;
+        st.ay += tffy * invMass;
+    }
+    position_tail(st, cp, oldx, oldy, acx, acy, hadCollision);
 }
 
 }  // namespace lpe
