@@ -61,6 +61,22 @@ def kernel_bytes(name, n, cells):
     return model.get(name)
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC
+    measurement (profiles/r*/pmc_traffic.json, written by
+    profiles/pmc_traffic.py from separate rocprofv3 FETCH_SIZE / WRITE_SIZE
+    passes of this bench on the same scene), or (None, None)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if kernel in d:
+            return d[kernel]["hbm_bytes"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(scene_name, state=None, budget_s=20.0):
     """The oracle (C/C++ restatement of the reference algorithms, 1 thread)
     running the same full tick on the same scene state (`state`: the device
@@ -279,9 +295,12 @@ def main():
     roof = None
     if b is not None:
         ach = b / avg_s / 1e9
+        traffic, tsrc = pmc_traffic(dname) if world == 1 and args.scene == "M" else (None, None)
         roof = dict(kernel=dname, bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS,
-                    unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4), traffic=None,
+                    unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4), traffic=traffic,
                     avg_us=round(avg_s * 1e6, 2), algorithmic_bytes=b)
+        if tsrc:
+            roof["traffic_source"] = tsrc + " (HBM bytes per launch, rocprofv3 PMC, last 5 ticks)"
     dens = times.get("k_density")
     roof_d = None
     if dens:

@@ -38,7 +38,7 @@ struct SphDev {
     float *rho = nullptr, *pr = nullptr;  // in S/P slot order
     float4 *nbA = nullptr;        // sorted neighbour records (x, y, m, -)
     float4 *nbB = nullptr;        // (vx, vy, rho, p / rho^2)
-    int16_t *nlist = nullptr;     // per-slot neighbour list k - s, column-major [cap][cap_n]
+    uint4 *nlist = nullptr;       // per-slot neighbour list k - s (int16, 8 per uint4), [cap/8][cap_n]
     int32_t *ncount = nullptr;    // neighbours found (> cap: forces walks the bins)
     // counting-sort grid hash over (2h cell, h quadrant) bins
     uint32_t *key = nullptr;      // bin of each P slot

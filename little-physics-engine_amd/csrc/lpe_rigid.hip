@@ -632,7 +632,14 @@ k_pair_colour(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict_
     extern __shared__ unsigned long long su[];              // colours used, per body
     unsigned long long *claim = su + nb;                     // best claiming priority, per body
     unsigned char *dep = (unsigned char *)(claim + nb);      // movable body
-    __shared__ int colCnt[MAX_COLOURS], colCur[MAX_COLOURS], colPairs[MAX_COLOURS], colPCur[MAX_COLOURS];
+    // pairs of a colour are placed by row count, largest first, so the waves
+    // of a colour step run pairs of equal length (a wave executes as many
+    // rows as its longest pair); the order inside a colour has no effect on
+    // the result (its pairs share no movable body)
+    constexpr int NCLS = 6;                                  // row-count classes: >= 6, 5, 4, 3, 2, 1
+    __shared__ int colCnt[MAX_COLOURS * NCLS], colCur[MAX_COLOURS * NCLS];
+    __shared__ int colPairs[MAX_COLOURS * NCLS], colPCur[MAX_COLOURS * NCLS];
+    __shared__ int grpQ0[MAX_COLOURS * NCLS], grpRow0[MAX_COLOURS * NCLS];
     __shared__ int s_left, s_fault, s_ncol;
     const unsigned long long NONE = ~0ull;
     const int np = *npptr;
@@ -729,17 +736,23 @@ k_pair_colour(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict_
         if (p < np) pcol[p] = rc[k];
     }
     __syncthreads();
-    // colour-major order: rows and pairs per colour -> bases -> pairs placed whole
-    if (threadIdx.x < MAX_COLOURS) {
-        colCnt[threadIdx.x] = 0; colCur[threadIdx.x] = 0;
-        colPairs[threadIdx.x] = 0; colPCur[threadIdx.x] = 0;
+    // colour-major order, and inside a colour groups of pairs with the same
+    // row count (longest first).  A group of g pairs with n rows stores its
+    // rows transposed, row j of its i-th pair at base + j * g + i, so the
+    // lanes of a wave (consecutive pairs of one group) load row j of their
+    // pairs from consecutive slots; pairs with >= NCLS rows keep theirs
+    // contiguous.  seg[q] = (slot of row 0, n | stride << 8).
+    auto cls = [](int n) { return NCLS - min(n, NCLS); };
+    for (int i = threadIdx.x; i < MAX_COLOURS * NCLS; i += SOLVE_TPB) {
+        colPairs[i] = 0; colPCur[i] = 0; colCnt[i] = 0; colCur[i] = 0;
     }
     __syncthreads();
     for (int p = threadIdx.x; p < np; p += SOLVE_TPB) {
         int c = pcol[p];
         if (c >= 0) {
-            atomicAdd(&colCnt[c], ccount[p]);
-            atomicAdd(&colPairs[c], 1);
+            const int gi = c * NCLS + cls(ccount[p]);
+            atomicAdd(&colCnt[gi], ccount[p]);
+            atomicAdd(&colPairs[gi], 1);
             atomicMax(&s_ncol, c + 1);
         }
     }
@@ -747,10 +760,12 @@ k_pair_colour(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict_
     if (threadIdx.x == 0) {
         int acc = 0, pacc = 0;
         for (int c = 0; c < MAX_COLOURS; c++) {
-            colCur[c] = acc; acc += colCnt[c];
-            colPCur[c] = pacc;
             if (c <= s_ncol) cbase[c] = pacc;
-            pacc += colPairs[c];
+            for (int k = 0; k < NCLS; k++) {
+                const int gi = c * NCLS + k;
+                grpQ0[gi] = pacc; colPCur[gi] = pacc; pacc += colPairs[gi];
+                grpRow0[gi] = acc; colCur[gi] = acc; acc += colCnt[gi];
+            }
         }
         cbase[s_ncol] = pacc;
         counts[8] = s_ncol;
@@ -760,11 +775,18 @@ k_pair_colour(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict_
     for (int p = threadIdx.x; p < np; p += SOLVE_TPB) {
         int c = pcol[p];
         if (c < 0) continue;
-        int n = ccount[p], s0 = cstart[p];
-        int pos = atomicAdd(&colCur[c], n);
-        int q = atomicAdd(&colPCur[c], 1);
-        seg[q] = make_int2(pos, n);
-        for (int j = 0; j < n; j++) order[pos + j] = s0 + j;
+        const int n = ccount[p], s0 = cstart[p], k = cls(n), gi = c * NCLS + k;
+        const int q = atomicAdd(&colPCur[gi], 1);
+        int pos, stride;
+        if (k == 0) {                                   // >= NCLS rows: contiguous
+            pos = atomicAdd(&colCur[gi], n);
+            stride = 1;
+        } else {
+            pos = grpRow0[gi] + (q - grpQ0[gi]);
+            stride = colPairs[gi];
+        }
+        seg[q] = make_int2(pos, n | (stride << 8));
+        for (int j = 0; j < n; j++) order[pos + j * stride] = s0 + j;
     }
 }
 
@@ -847,28 +869,31 @@ k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
             const int q1 = scb[c + 1];
             for (int q = scb[c] + threadIdx.x; q < q1; q += SOLVE_TPB) {
                 const int2 sg = cached ? ss[q] : seg[q];
-                float4 n[RB], r[RB], m[RB];
-                int2 ab[RB];
-                float ln[RB], lf[RB];
+                const int nrow = sg.y & 0xff, stride = sg.y >> 8;   // rows: sg.x + j * stride
+                // the pair's rows in batches of RB, all loads of a batch in flight together
+                for (int j0 = 0; j0 < nrow; j0 += RB) {
+                    const int nb_ = min(RB, nrow - j0);
+                    float4 n[RB], r[RB], m[RB];
+                    int2 ab[RB];
+                    float ln[RB], lf[RB];
 #pragma unroll
-                for (int j = 0; j < RB; j++) {
-                    if (j < sg.y) {
-                        const int t = sg.x + j;
-                        n[j] = rowN[t]; r[j] = rowR[t]; m[j] = rowM[t]; ab[j] = rowAB[t];
-                        ln[j] = it ? lamN[t] : 0.f;
-                        lf[j] = it ? lamF[t] : 0.f;
+                    for (int j = 0; j < RB; j++) {
+                        if (j < nb_) {
+                            const int t = sg.x + (j0 + j) * stride;
+                            n[j] = rowN[t]; r[j] = rowR[t]; m[j] = rowM[t]; ab[j] = rowAB[t];
+                            ln[j] = it ? lamN[t] : 0.f;
+                            lf[j] = it ? lamF[t] : 0.f;
+                        }
                     }
-                }
 #pragma unroll
-                for (int j = 0; j < RB; j++)
-                    if (j < sg.y) pgs_row_pair(n[j], r[j], m[j], ab[j], mu, ln[j], lf[j], sv);
+                    for (int j = 0; j < RB; j++)
+                        if (j < nb_) pgs_row_pair(n[j], r[j], m[j], ab[j], mu, ln[j], lf[j], sv);
 #pragma unroll
-                for (int j = 0; j < RB; j++)
-                    if (j < sg.y) { lamN[sg.x + j] = ln[j]; lamF[sg.x + j] = lf[j]; }
-                for (int t = sg.x + RB; t < sg.x + sg.y; t++) {     // pairs with > RB contacts
-                    float l0 = it ? lamN[t] : 0.f, l1 = it ? lamF[t] : 0.f;
-                    pgs_row_pair(rowN[t], rowR[t], rowM[t], rowAB[t], mu, l0, l1, sv);
-                    lamN[t] = l0; lamF[t] = l1;
+                    for (int j = 0; j < RB; j++)
+                        if (j < nb_) {
+                            const int t = sg.x + (j0 + j) * stride;
+                            lamN[t] = ln[j]; lamF[t] = lf[j];
+                        }
                 }
             }
             __syncthreads();
@@ -1194,14 +1219,17 @@ k_pos_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
             const int q1 = scb[c + 1];
             for (int q = scb[c] + threadIdx.x; q < q1; q += SOLVE_TPB) {
                 const int2 sg = cached ? ss[q] : seg[q];
-                PosRec r[RB];
+                const int nrow = sg.y & 0xff, stride = sg.y >> 8;   // rows: sg.x + j * stride
+                for (int j0 = 0; j0 < nrow; j0 += RB) {              // batches of RB rows
+                    const int nb_ = min(RB, nrow - j0);
+                    PosRec r[RB];
 #pragma unroll
-                for (int j = 0; j < RB; j++)
-                    if (j < sg.y) r[j] = rec[sg.x + j];
+                    for (int j = 0; j < RB; j++)
+                        if (j < nb_) r[j] = rec[sg.x + (j0 + j) * stride];
 #pragma unroll
-                for (int j = 0; j < RB; j++)
-                    if (j < sg.y) pos_item(r[j], sp);
-                for (int t = sg.x + RB; t < sg.x + sg.y; t++) pos_item(rec[t], sp);
+                    for (int j = 0; j < RB; j++)
+                        if (j < nb_) pos_item(r[j], sp);
+                }
             }
             __syncthreads();
         }

@@ -543,23 +543,20 @@ __device__ void stage_plan(Stage &st, int cap, int s0, int s1, const float4 *__r
     __syncthreads();
 }
 
-// LDS index of candidate slot k walked in cell row cyc by a particle of row cyp
-__device__ __forceinline__ int stage_index(const Stage &st, int k, int cyc, int cyp) {
-    const int i = (cyp == st.cy0 ? 0 : 3) + (cyc - cyp + 1);
-    return st.segL[i] + (k - st.segS[i]);
-}
-
 // computeDensity (metal:246-307), one thread per sorted slot, SB slots per
 // block with the neighbourhood staged in LDS.  Besides rho and p it writes
 // the neighbours of the forces pass (r^2 < h^2, not itself: metal:360-366) in
-// the canonical walk order as int16 slot offsets k - s, column-major
-// [NLIST_CAP][nstride] (more than NLIST_CAP: ncount > NLIST_CAP and the
-// forces pass walks the bins).
+// the canonical walk order as int16 slot offsets k - s, eight to a uint4,
+// column-major [NLIST_CAP / 8][nstride]: each thread collects eight offsets
+// in registers and writes them with one 16-byte store (2-byte stores
+// scattered over rows cost ~16 B of write traffic each, PMC WRITE_SIZE).
+// More than NLIST_CAP neighbours: ncount > NLIST_CAP and the forces pass
+// walks the bins.
 __global__ void __launch_bounds__(SB)
 k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float eps, float stiffness,
           float restDensity, int W, int H, int ox, int oy, const GridParams *__restrict__ gp,
           const int32_t *__restrict__ start, const float4 *__restrict__ nbA, float2 *__restrict__ nbB,
-          float *__restrict__ rho, float *__restrict__ pr, int16_t *__restrict__ nlist,
+          float *__restrict__ rho, float *__restrict__ pr, uint4 *__restrict__ nlist,
           int32_t *__restrict__ ncount, int32_t *__restrict__ status) {
     __shared__ Stage st;
     __shared__ float4 lrec[STAGE_CAP];
@@ -589,6 +586,7 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     const float poly6 = poly6Coeff2D(h);
     float acc = 0.0f;
     int cnt = 0;
+    uint32_t w0 = 0u, w1 = 0u, w2 = 0u, w3 = 0u;     // the current group of eight offsets
     auto body = [&](int k, const float4 &o) {
         float dx = xi - o.x, dy = yi - o.y;
         float r2 = dx * dx + dy * dy;
@@ -598,20 +596,42 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
             acc += o.z * w;
             if (k != s) {
                 const int off = k - s;
-                if (cnt < NLIST_CAP && off >= -32768 && off <= 32767)
-                    nlist[(size_t)cnt * nstride + s] = (int16_t)off;
-                else
+                if (cnt < NLIST_CAP && off >= -32768 && off <= 32767) {
+                    const uint32_t v = (uint32_t)(off & 0xffff) << (16 * (cnt & 1));
+                    const int q = (cnt >> 1) & 3;
+                    w0 |= q == 0 ? v : 0u;
+                    w1 |= q == 1 ? v : 0u;
+                    w2 |= q == 2 ? v : 0u;
+                    w3 |= q == 3 ? v : 0u;
+                    if ((cnt & 7) == 7) {
+                        nlist[(size_t)(cnt >> 3) * nstride + s] = make_uint4(w0, w1, w2, w3);
+                        w0 = w1 = w2 = w3 = 0u;
+                    }
+                } else {
                     cnt = NLIST_CAP;          // overflow: forces walks the bins
+                }
                 cnt++;
             }
         }
     };
     if (st.ok)
-        walk_neighbours<4>(xi, yi, eps, cs, walk_reach(h, cs), g, W, H, ox, oy, start,
-                           [&](int k, int cyc) { return lrec[stage_index(st, k, cyc, cyp)]; }, body);
+        walk_ranges(xi, yi, eps, cs, walk_reach(h, cs), g, W, H, ox, oy, start, [&](int b, int e, int cyc) {
+            // the LDS segment of cell row cyc, resolved once per range
+            const int i = (cyp == st.cy0 ? 0 : 3) + (cyc - cyp + 1);
+            const float4 *seg = lrec + (st.segL[i] - st.segS[i]);
+            for (int k = b; k < e; k += 4) {
+                float4 r[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) r[j] = seg[min(k + j, e - 1)];
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (k + j < e) body(k + j, r[j]);
+            }
+        });
     else
         walk_neighbours<4>(xi, yi, eps, cs, walk_reach(h, cs), g, W, H, ox, oy, start,
                            [&](int k, int) { return nbA[k]; }, body);
+    if (cnt <= NLIST_CAP && (cnt & 7)) nlist[(size_t)(cnt >> 3) * nstride + s] = make_uint4(w0, w1, w2, w3);
     ncount[s] = cnt;
     float pres = stiffness * (acc - restDensity);
     if (pres < 0.f) pres = 0.f;
@@ -637,7 +657,7 @@ __global__ void __launch_bounds__(TPB)
 k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict__ gp,
                 const int32_t *__restrict__ start, PState S, const float4 *__restrict__ nbA,
                 const float4 *__restrict__ nbB, const float *__restrict__ pr,
-                const int16_t *__restrict__ nlist, const int32_t *__restrict__ ncount, PState P,
+                const uint4 *__restrict__ nlist, const int32_t *__restrict__ ncount, PState P,
                 const lpe_gpu_rigid *__restrict__ rig, const float4 *__restrict__ raabb,
                 const int32_t *__restrict__ rbinStart, const int32_t *__restrict__ rbinList,
                 float *__restrict__ accum,
@@ -703,16 +723,28 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         // the density pass's list: the r^2 < h^2 neighbours in canonical
         // order, so the heavy pair math runs only on real neighbours
         constexpr int U = 4;
-        for (int j = 0; j < cnt; j += U) {
-            int kk[U];
+        for (int j8 = 0; j8 < cnt; j8 += 8) {
+            const uint4 g8 = nlist[(size_t)(j8 >> 3) * sp.nstride + s];
 #pragma unroll
-            for (int u = 0; u < U; u++) kk[u] = s + nlist[(size_t)min(j + u, cnt - 1) * sp.nstride + s];
-            Rec r[U];
+            for (int h = 0; h < 2; h++) {             // two groups of four offsets
+                const int j = j8 + 4 * h;
+                if (j >= cnt) break;
+                const uint32_t a = h ? g8.z : g8.x, b = h ? g8.w : g8.y;
+                int kk[U];
+                kk[0] = s + (int)(int16_t)(a & 0xffffu);
+                kk[1] = s + (int)(int16_t)(a >> 16);
+                kk[2] = s + (int)(int16_t)(b & 0xffffu);
+                kk[3] = s + (int)(int16_t)(b >> 16);
 #pragma unroll
-            for (int u = 0; u < U; u++) r[u] = Rec{nbA[kk[u]], nbB[kk[u]]};
+                for (int u = 1; u < U; u++)
+                    if (j + u >= cnt) kk[u] = kk[0];   // unused entries of the last group
+                Rec r[U];
 #pragma unroll
-            for (int u = 0; u < U; u++)
-                if (j + u < cnt) pair(kk[u], r[u]);
+                for (int u = 0; u < U; u++) r[u] = Rec{nbA[kk[u]], nbB[kk[u]]};
+#pragma unroll
+                for (int u = 0; u < U; u++)
+                    if (j + u < cnt) pair(kk[u], r[u]);
+            }
         }
     } else {
         walk_neighbours<4>(xi, yi, sp.eps, cs, walk_reach(hi, cs), g, sp.W, sp.H, sp.ox, sp.oy, start,
@@ -1299,7 +1331,7 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     LPE_HIP(ctx, hipMalloc((void **)&d.pr, sizeof(float) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.nbA, sizeof(float4) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.nbB, sizeof(float4) * N));
-    LPE_HIP(ctx, hipMalloc((void **)&d.nlist, sizeof(int16_t) * N * NLIST_CAP));
+    LPE_HIP(ctx, hipMalloc((void **)&d.nlist, sizeof(uint4) * N * (NLIST_CAP / 8)));
     LPE_HIP(ctx, hipMalloc((void **)&d.ncount, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.key, sizeof(uint32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpId, sizeof(int32_t) * N));
