@@ -548,8 +548,8 @@ __device__ void stage_plan(Stage &st, int cap, int s0, int s1, const float4 *__r
 // the neighbours of the forces pass (r^2 < h^2, not itself: metal:360-366) in
 // the canonical walk order as int16 slot offsets k - s, eight to a uint4,
 // column-major [NLIST_CAP / 8][nstride]: each thread collects eight offsets
-// in registers and writes them with one 16-byte store (2-byte stores
-// scattered over rows cost ~16 B of write traffic each, PMC WRITE_SIZE).
+// in its 16-byte LDS slot and writes them with one 16-byte store (2-byte
+// stores scattered over rows cost ~16 B of write traffic each, PMC WRITE_SIZE).
 // More than NLIST_CAP neighbours: ncount > NLIST_CAP and the forces pass
 // walks the bins.
 __global__ void __launch_bounds__(SB)
@@ -560,6 +560,7 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
           int32_t *__restrict__ ncount, int32_t *__restrict__ status) {
     __shared__ Stage st;
     __shared__ float4 lrec[STAGE_CAP];
+    __shared__ uint4 lnl[SB];                             // per thread: the current group of 8 offsets
     const int lb = xcd_block((n + SB - 1) / SB);
     if (lb < 0) return;                                   // whole block idle
     const int nn = nptr ? *nptr : n;
@@ -586,7 +587,7 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     const float poly6 = poly6Coeff2D(h);
     float acc = 0.0f;
     int cnt = 0;
-    uint32_t w0 = 0u, w1 = 0u, w2 = 0u, w3 = 0u;     // the current group of eight offsets
+    int16_t *grp = reinterpret_cast<int16_t *>(&lnl[threadIdx.x]);
     auto body = [&](int k, const float4 &o) {
         float dx = xi - o.x, dy = yi - o.y;
         float r2 = dx * dx + dy * dy;
@@ -597,16 +598,8 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
             if (k != s) {
                 const int off = k - s;
                 if (cnt < NLIST_CAP && off >= -32768 && off <= 32767) {
-                    const uint32_t v = (uint32_t)(off & 0xffff) << (16 * (cnt & 1));
-                    const int q = (cnt >> 1) & 3;
-                    w0 |= q == 0 ? v : 0u;
-                    w1 |= q == 1 ? v : 0u;
-                    w2 |= q == 2 ? v : 0u;
-                    w3 |= q == 3 ? v : 0u;
-                    if ((cnt & 7) == 7) {
-                        nlist[(size_t)(cnt >> 3) * nstride + s] = make_uint4(w0, w1, w2, w3);
-                        w0 = w1 = w2 = w3 = 0u;
-                    }
+                    grp[cnt & 7] = (int16_t)off;
+                    if ((cnt & 7) == 7) nlist[(size_t)(cnt >> 3) * nstride + s] = lnl[threadIdx.x];
                 } else {
                     cnt = NLIST_CAP;          // overflow: forces walks the bins
                 }
@@ -631,7 +624,7 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     else
         walk_neighbours<4>(xi, yi, eps, cs, walk_reach(h, cs), g, W, H, ox, oy, start,
                            [&](int k, int) { return nbA[k]; }, body);
-    if (cnt <= NLIST_CAP && (cnt & 7)) nlist[(size_t)(cnt >> 3) * nstride + s] = make_uint4(w0, w1, w2, w3);
+    if (cnt <= NLIST_CAP && (cnt & 7)) nlist[(size_t)(cnt >> 3) * nstride + s] = lnl[threadIdx.x];
     ncount[s] = cnt;
     float pres = stiffness * (acc - restDensity);
     if (pres < 0.f) pres = 0.f;
