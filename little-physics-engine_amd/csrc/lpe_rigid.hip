@@ -795,12 +795,11 @@ k_pair_colour(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict_
 // barrier.  Equal bit for bit to the sequential sweep in colour-major order.
 // solveLcpPgs (contact_solver.cpp:381-440), rows of buildConstraintRows
 // (:133-197) in fp32, body velocities in LDS.
-__device__ __forceinline__ void pgs_row_pair(float4 rn, float4 rr, float4 rm, int2 ab, float mu,
-                                             float &ln, float &lf, float *sv) {
-    const float imA = rm.x, iiA = rm.y, imB = rm.z, iiB = rm.w;
-    float vxA = 0.f, vyA = 0.f, wA = 0.f, vxB = 0.f, vyB = 0.f, wB = 0.f;
-    if (ab.x >= 0) { vxA = sv[3 * ab.x]; vyA = sv[3 * ab.x + 1]; wA = sv[3 * ab.x + 2]; }
-    if (ab.y >= 0) { vxB = sv[3 * ab.y]; vyB = sv[3 * ab.y + 1]; wB = sv[3 * ab.y + 2]; }
+// one contact row (normal, then friction) on the pair's velocities in registers
+__device__ __forceinline__ void pgs_row_regs(float4 rn, float4 rr, float imA, float iiA, float imB,
+                                             float iiB, bool hasA, bool hasB, float mu, float &ln,
+                                             float &lf, float &vxA, float &vyA, float &wA, float &vxB,
+                                             float &vyB, float &wB) {
 #pragma unroll
     for (int row = 0; row < 2; row++) {
         float dX = row == 0 ? rn.x : -rn.y;
@@ -824,28 +823,28 @@ __device__ __forceinline__ void pgs_row_pair(float4 rn, float4 rr, float4 rm, in
         dl = nl - old;
         if (row == 0) ln = nl; else lf = nl;
         if (fabsf(dl) < 1e-15F) continue;
-        if (ab.x >= 0) {
+        if (hasA) {
             vxA -= dX * (dl * imA);
             vyA -= dY * (dl * imA);
             float crossA = rr.x * dY - rr.y * dX;
             wA -= crossA * dl * iiA;
         }
-        if (ab.y >= 0) {
+        if (hasB) {
             vxB += dX * (dl * imB);
             vyB += dY * (dl * imB);
             float crossB = rr.z * dY - rr.w * dX;
             wB += crossB * dl * iiB;
         }
     }
-    if (ab.x >= 0) { sv[3 * ab.x] = vxA; sv[3 * ab.x + 1] = vyA; sv[3 * ab.x + 2] = wA; }
-    if (ab.y >= 0) { sv[3 * ab.y] = vxB; sv[3 * ab.y + 1] = vyB; sv[3 * ab.y + 2] = wB; }
 }
 
 // A colour step is latency-bound (one workgroup; a pair's rows are a chain),
 // so the global round trips per step are kept to one: colour bases and the
 // coloured pairs' row segments are cached in LDS (when they fit: segLds), and
 // all rows of a pair (up to RB) are loaded before its sequential updates.
-static constexpr int RB = 4;
+// The rows of a pair share its two bodies (and their masses): the bodies'
+// state is read from LDS once per pair and kept in registers across its rows.
+static constexpr int RB = 6;
 __global__ void __launch_bounds__(SOLVE_TPB)
 k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restrict__ cbase,
              const int2 *__restrict__ seg, int segLds, const float4 *__restrict__ rowN,
@@ -870,24 +869,31 @@ k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
             for (int q = scb[c] + threadIdx.x; q < q1; q += SOLVE_TPB) {
                 const int2 sg = cached ? ss[q] : seg[q];
                 const int nrow = sg.y & 0xff, stride = sg.y >> 8;   // rows: sg.x + j * stride
+                const int2 ab = rowAB[sg.x];
+                const float4 m = rowM[sg.x];
+                const bool hasA = ab.x >= 0, hasB = ab.y >= 0;
+                float vxA = 0.f, vyA = 0.f, wA = 0.f, vxB = 0.f, vyB = 0.f, wB = 0.f;
+                if (hasA) { vxA = sv[3 * ab.x]; vyA = sv[3 * ab.x + 1]; wA = sv[3 * ab.x + 2]; }
+                if (hasB) { vxB = sv[3 * ab.y]; vyB = sv[3 * ab.y + 1]; wB = sv[3 * ab.y + 2]; }
                 // the pair's rows in batches of RB, all loads of a batch in flight together
                 for (int j0 = 0; j0 < nrow; j0 += RB) {
                     const int nb_ = min(RB, nrow - j0);
-                    float4 n[RB], r[RB], m[RB];
-                    int2 ab[RB];
+                    float4 n[RB], r[RB];
                     float ln[RB], lf[RB];
 #pragma unroll
                     for (int j = 0; j < RB; j++) {
                         if (j < nb_) {
                             const int t = sg.x + (j0 + j) * stride;
-                            n[j] = rowN[t]; r[j] = rowR[t]; m[j] = rowM[t]; ab[j] = rowAB[t];
+                            n[j] = rowN[t]; r[j] = rowR[t];
                             ln[j] = it ? lamN[t] : 0.f;
                             lf[j] = it ? lamF[t] : 0.f;
                         }
                     }
 #pragma unroll
                     for (int j = 0; j < RB; j++)
-                        if (j < nb_) pgs_row_pair(n[j], r[j], m[j], ab[j], mu, ln[j], lf[j], sv);
+                        if (j < nb_)
+                            pgs_row_regs(n[j], r[j], m.x, m.y, m.z, m.w, hasA, hasB, mu, ln[j], lf[j], vxA, vyA,
+                                         wA, vxB, vyB, wB);
 #pragma unroll
                     for (int j = 0; j < RB; j++)
                         if (j < nb_) {
@@ -895,6 +901,8 @@ k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
                             lamN[t] = ln[j]; lamF[t] = lf[j];
                         }
                 }
+                if (hasA) { sv[3 * ab.x] = vxA; sv[3 * ab.x + 1] = vyA; sv[3 * ab.x + 2] = wA; }
+                if (hasB) { sv[3 * ab.y] = vxB; sv[3 * ab.y + 1] = vyB; sv[3 * ab.y + 2] = wB; }
             }
             __syncthreads();
         }
@@ -1168,6 +1176,33 @@ __global__ void k_pos_fill_rows(const int32_t *__restrict__ ncptr, const int32_t
     rec[u] = q;
 }
 
+// one item on the pair's poses in registers (the colour solver): the items of
+// a pair share its bodies, their inverse masses and rotation flags
+__device__ __forceinline__ void pos_item_regs(double nx, double ny, double corr, double px, double py,
+                                              int flags, double invMA, double invMB, double invIA,
+                                              double invIB, double &xA, double &yA, double &tA,
+                                              double &xB, double &yB, double &tB) {
+    if (flags & 1) return;
+    D2 rA = d2(px - xA, py - yA);
+    D2 rB = d2(px - xB, py - yB);
+    D2 n = d2(nx, ny);
+    double rAn = crs(rA, n), rBn = crs(rB, n);
+    double denom = invMA + invMB + (rAn * rAn) * invIA + (rBn * rBn) * invIB;
+    if (denom < 1e-12) return;
+    double sc = corr / denom;
+    double dx = n.x * sc, dy = n.y * sc;
+    if (invMA != 0.0 || (flags & 2)) {
+        xA -= dx * invMA;
+        yA -= dy * invMA;
+        if (flags & 2) tA -= rAn * sc * invIA;
+    }
+    if (invMB != 0.0 || (flags & 4)) {
+        xB += dx * invMB;
+        yB += dy * invMB;
+        if (flags & 4) tB += rBn * sc * invIB;
+    }
+}
+
 __device__ __forceinline__ void pos_item(const PosRec &q, double *sp) {
     if (q.flags & 1) return;
     const int a = q.a, b = q.b;
@@ -1220,16 +1255,32 @@ k_pos_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
             for (int q = scb[c] + threadIdx.x; q < q1; q += SOLVE_TPB) {
                 const int2 sg = cached ? ss[q] : seg[q];
                 const int nrow = sg.y & 0xff, stride = sg.y >> 8;   // rows: sg.x + j * stride
+                const PosRec &q0 = rec[sg.x];
+                const int a = q0.a, b = q0.b;
+                const double invMA = q0.invMA, invMB = q0.invMB, invIA = q0.invIA, invIB = q0.invIB;
+                double xA = sp[3 * a], yA = sp[3 * a + 1], tA = sp[3 * a + 2];
+                double xB = sp[3 * b], yB = sp[3 * b + 1], tB = sp[3 * b + 2];
                 for (int j0 = 0; j0 < nrow; j0 += RB) {              // batches of RB rows
                     const int nb_ = min(RB, nrow - j0);
-                    PosRec r[RB];
+                    double nx[RB], ny[RB], cr[RB], px[RB], py[RB];
+                    int fl[RB];
 #pragma unroll
                     for (int j = 0; j < RB; j++)
-                        if (j < nb_) r[j] = rec[sg.x + (j0 + j) * stride];
+                        if (j < nb_) {
+                            const PosRec &qr = rec[sg.x + (j0 + j) * stride];
+                            nx[j] = qr.nx; ny[j] = qr.ny; cr[j] = qr.corr; px[j] = qr.px; py[j] = qr.py;
+                            fl[j] = qr.flags;
+                        }
 #pragma unroll
                     for (int j = 0; j < RB; j++)
-                        if (j < nb_) pos_item(r[j], sp);
+                        if (j < nb_)
+                            pos_item_regs(nx[j], ny[j], cr[j], px[j], py[j], fl[j], invMA, invMB, invIA, invIB,
+                                          xA, yA, tA, xB, yB, tB);
                 }
+                // a static body (invM = 0, no rotation) is never written: pairs
+                // of one colour may share it
+                if (invMA != 0.0 || (q0.flags & 2)) { sp[3 * a] = xA; sp[3 * a + 1] = yA; sp[3 * a + 2] = tA; }
+                if (invMB != 0.0 || (q0.flags & 4)) { sp[3 * b] = xB; sp[3 * b + 1] = yB; sp[3 * b + 2] = tB; }
             }
             __syncthreads();
         }
