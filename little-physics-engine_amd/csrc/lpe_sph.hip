@@ -715,29 +715,22 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     if (cnt <= NLIST_CAP) {
         // the density pass's list: the r^2 < h^2 neighbours in canonical
         // order, so the heavy pair math runs only on real neighbours
-        constexpr int U = 4;
-        for (int j8 = 0; j8 < cnt; j8 += 8) {
-            const uint4 g8 = nlist[(size_t)(j8 >> 3) * sp.nstride + s];
+        constexpr int U = 8;                      // one group of eight offsets, all loads in flight
+        for (int j = 0; j < cnt; j += U) {
+            const uint4 g8 = nlist[(size_t)(j >> 3) * sp.nstride + s];
+            const uint32_t w[4] = {g8.x, g8.y, g8.z, g8.w};
+            int kk[U];
 #pragma unroll
-            for (int h = 0; h < 2; h++) {             // two groups of four offsets
-                const int j = j8 + 4 * h;
-                if (j >= cnt) break;
-                const uint32_t a = h ? g8.z : g8.x, b = h ? g8.w : g8.y;
-                int kk[U];
-                kk[0] = s + (int)(int16_t)(a & 0xffffu);
-                kk[1] = s + (int)(int16_t)(a >> 16);
-                kk[2] = s + (int)(int16_t)(b & 0xffffu);
-                kk[3] = s + (int)(int16_t)(b >> 16);
+            for (int u = 0; u < U; u++) kk[u] = s + (int)(int16_t)((w[u >> 1] >> (16 * (u & 1))) & 0xffffu);
 #pragma unroll
-                for (int u = 1; u < U; u++)
-                    if (j + u >= cnt) kk[u] = kk[0];   // unused entries of the last group
-                Rec r[U];
+            for (int u = 1; u < U; u++)
+                if (j + u >= cnt) kk[u] = kk[0];       // unused entries of the last group
+            Rec r[U];
 #pragma unroll
-                for (int u = 0; u < U; u++) r[u] = Rec{nbA[kk[u]], nbB[kk[u]]};
+            for (int u = 0; u < U; u++) r[u] = Rec{nbA[kk[u]], nbB[kk[u]]};
 #pragma unroll
-                for (int u = 0; u < U; u++)
-                    if (j + u < cnt) pair(kk[u], r[u]);
-            }
+            for (int u = 0; u < U; u++)
+                if (j + u < cnt) pair(kk[u], r[u]);
         }
     } else {
         walk_neighbours<4>(xi, yi, sp.eps, cs, walk_reach(hi, cs), g, sp.W, sp.H, sp.ox, sp.oy, start,
