@@ -184,6 +184,36 @@ def loopback_check(args, lpe, scenes, slab, device):
                       "rigid_replicas_identical": bool(same), "max_cell_occupancy_rank0": st["maxCellOccupancy"]}))
 
 
+def rigid_microbench(lpe, device, reps=10):
+    """One RigidBodyCollisionSystem::update (broadphase, narrowphase,
+    colouring, PGS 10 it, position solver 10 it) on the metric scene's settled
+    pile, the committed fixture tests/golden/pile_M_t250.npz, re-uploaded
+    before every repetition: the same ~10k pairs / ~30k contacts every run, so
+    the rigid kernels can be compared across runs (the live pile of the tick
+    bench drifts with float-atomic summation order)."""
+    z = np.load(os.path.join(ROOT, "tests", "golden", "pile_M_t250.npz"))
+    ctx = lpe.Context(device)
+    try:
+        ctx.rigid_set_config(lpe.rigid_config(universe=32.0))
+        ctx.rigid_upload(z["bodies"], z["verts"])
+        st = ctx.rigid_step()                       # warm
+        ctx.timing(1)
+        ctx.timing_reset()
+        for _ in range(reps):
+            ctx.rigid_upload(z["bodies"], z["verts"])
+            ctx.rigid_step(stats=False)
+        t = ctx.timing_read()
+        ctx.timing(0)
+    finally:
+        ctx.close()
+    us = {k: round(v[0] / max(v[1], 1) * 1e3, 1) for k, v in t.items()}
+    step = sum(v[0] for v in t.values()) / reps * 1e3
+    return dict(fixture="tests/golden/pile_M_t250.npz", pairs=st["pairs"], contacts=st["contacts"],
+                colours=st["pgsLevels"], reps=reps, step_kernels_us=round(step, 1),
+                kernels_us={k: us[k] for k in ("k_bp_pairs", "k_narrow", "k_pair_colour", "k_pgs_colour",
+                                               "k_pos_colour") if k in us})
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -345,6 +375,7 @@ def main():
     }
     if world == 1 and not args.no_density_microbench:
         line["density_microbench"] = density_microbench(lpe, scenes, local)
+        line["rigid_microbench"] = rigid_microbench(lpe, local)
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.scene, settled)
     print(json.dumps(line))

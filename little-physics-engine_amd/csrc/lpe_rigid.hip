@@ -859,15 +859,14 @@ k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
     for (int c = threadIdx.x; c <= ncol; c += SOLVE_TPB) scb[c] = cbase[c];
     __syncthreads();
     const int npc = scb[ncol];
-    const bool cached = npc <= segLds;
-    if (cached)
-        for (int q = threadIdx.x; q < npc; q += SOLVE_TPB) ss[q] = seg[q];
+    const int ncached = min(npc, segLds);                  // the first segLds segments live in LDS
+    for (int q = threadIdx.x; q < ncached; q += SOLVE_TPB) ss[q] = seg[q];
     __syncthreads();
     for (int it = 0; it < iters; it++) {
         for (int c = 0; c < ncol; c++) {
             const int q1 = scb[c + 1];
             for (int q = scb[c] + threadIdx.x; q < q1; q += SOLVE_TPB) {
-                const int2 sg = cached ? ss[q] : seg[q];
+                const int2 sg = q < ncached ? ss[q] : seg[q];
                 const int nrow = sg.y & 0xff, stride = sg.y >> 8;   // rows: sg.x + j * stride
                 const int2 ab = rowAB[sg.x];
                 const float4 m = rowM[sg.x];
@@ -1245,15 +1244,14 @@ k_pos_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
     for (int c = threadIdx.x; c <= ncol; c += SOLVE_TPB) scb[c] = cbase[c];
     __syncthreads();
     const int npc = scb[ncol];
-    const bool cached = npc <= segLds;
-    if (cached)
-        for (int q = threadIdx.x; q < npc; q += SOLVE_TPB) ss[q] = seg[q];
+    const int ncached = min(npc, segLds);                  // the first segLds segments live in LDS
+    for (int q = threadIdx.x; q < ncached; q += SOLVE_TPB) ss[q] = seg[q];
     __syncthreads();
     for (int it = 0; it < iters; it++) {
         for (int c = 0; c < ncol; c++) {
             const int q1 = scb[c + 1];
             for (int q = scb[c] + threadIdx.x; q < q1; q += SOLVE_TPB) {
-                const int2 sg = cached ? ss[q] : seg[q];
+                const int2 sg = q < ncached ? ss[q] : seg[q];
                 const int nrow = sg.y & 0xff, stride = sg.y >> 8;   // rows: sg.x + j * stride
                 const PosRec &q0 = rec[sg.x];
                 const int a = q0.a, b = q0.b;
@@ -1816,7 +1814,7 @@ static int rigid_solve(lpe_ctx *ctx, RigidDev *d, bool colour, const int32_t *pg
         // canonical order: colour-synchronous sweeps over the colour segments
         // LDS: body state, then as many pair segments as fit (the coloured
         // pairs are at most last_np)
-        const size_t ldsMax = 150 * 1024;
+        const size_t ldsMax = 159 * 1024;      // of the 160 KB of a CU (the kernels use < 1 KB static)
         size_t lds = sizeof(float) * (3 * (size_t)nb + 1);
         int segLds = (int)std::min<size_t>((size_t)d->last_np, (ldsMax - std::min(ldsMax, lds)) / sizeof(int2));
         lds += sizeof(int2) * (size_t)segLds + 8;

@@ -22,7 +22,8 @@ import pytest
 from conftest import ROOT, lpe, scenes
 
 pytestmark = pytest.mark.gpu
-FIXTURES = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "rigid_*.npz")))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+FIXTURES = sorted(glob.glob(os.path.join(GOLDEN, "rigid_*.npz")))
 DT = 1.0 / 120.0
 
 
@@ -143,6 +144,28 @@ def test_c3_pile_canonical(gpu_ctx, oracle_mod):
     print(f"C3 pile: {st['pairs']} pairs, {st['contacts']} contacts, {st['pgsLevels']} colours")
     out = gpu_ctx.rigid_download()
     close_state(out, ref)
+
+
+def test_metric_pile_canonical(gpu_ctx, oracle_mod):
+    """The metric scene's own settled pile (scene M at tick 250, 4,096
+    pentagons + walls, ~10k pairs / ~30k contacts: tests/golden/pile_M_t250.npz)
+    through one RigidBodyCollisionSystem::update on the device against the
+    restatement: the same broadphase pairs and contacts, the same canonical
+    colouring, and the solved state within the rigid bars."""
+    z = np.load(os.path.join(GOLDEN, "pile_M_t250.npz"))
+    b, v = z["bodies"], z["verts"]
+    cfg = lpe.rigid_config(universe=32.0)
+    ref, rst = oracle_mod.rigid_update(cfg, b, v)
+    gpu_ctx.rigid_set_config(cfg)
+    gpu_ctx.rigid_upload(b, v)
+    st = gpu_ctx.rigid_step()
+    assert st["pairs"] == rst.pairs and st["contacts"] == rst.contacts and rst.contacts > 20000
+    pairs, cs = gpu_ctx.rigid_contacts()
+    col, ncol = gpu_ctx.rigid_colours()
+    _, ref_col, ref_ncol = oracle_mod.colour_order(b, cs, len(pairs))
+    np.testing.assert_array_equal(col, ref_col)
+    assert ncol == ref_ncol
+    close_state(gpu_ctx.rigid_download(), ref)
 
 
 def test_multi_tick_device_matches_restatement(gpu_ctx, oracle_mod):
