@@ -114,7 +114,7 @@ def density_microbench(lpe, scenes, device, side=4096, reps=5):
     """SURVEY.md §8(d) density microbench: a side x side lattice (16.7M
     particles at side 4096) in a U = 104 m universe, one density pass from a
     pre-built grid (lpe_sph_probe_density: hash of the current positions, then
-    the tick's own LDS-staged density kernel, neighbour masks included), timed
+    the tick's own LDS-staged density kernel, neighbour lists included), timed
     with HIP events on the library's stream; algorithmic bytes 24 B/particle +
     8 B/cell (§8(d))."""
     rng = np.random.default_rng(7)
@@ -209,7 +209,7 @@ def rigid_microbench(lpe, device, reps=10):
     us = {k: round(v[0] / max(v[1], 1) * 1e3, 1) for k, v in t.items()}
     step = sum(v[0] for v in t.values()) / reps * 1e3
     return dict(fixture="tests/golden/pile_M_t250.npz", pairs=st["pairs"], contacts=st["contacts"],
-                colours=st["pgsLevels"], reps=reps, step_kernels_us=round(step, 1),
+                colours=st["pgsLevels"], colour_rounds=st["colourRounds"], reps=reps, step_kernels_us=round(step, 1),
                 kernels_us={k: us[k] for k in ("k_bp_pairs", "k_narrow", "k_pair_colour", "k_pgs_colour",
                                                "k_pos_colour") if k in us})
 
@@ -309,6 +309,7 @@ def main():
     if rank != 0:
         if dist is not None:
             dist.barrier()
+        ctx.close()        # RCCL communicator torn down by every rank after the last barrier
         return
 
     assert np.isfinite(out["x"]).all() and np.isfinite(out["vy"]).all()
@@ -381,6 +382,7 @@ def main():
     print(json.dumps(line))
     if dist is not None:
         dist.barrier()
+    ctx.close()
 
 
 if __name__ == "__main__":

@@ -295,7 +295,7 @@ typedef struct lpe_rigid_stats {
     int32_t pgsLevels;      /* dependency levels of one PGS sweep              */
     int32_t posLevels;      /* dependency levels of one position-solver sweep  */
     int32_t overflow;       /* non-zero if a fixed-capacity list overflowed    */
-    int32_t pad;
+    int32_t colourRounds;   /* rounds of the parallel pair colouring           */
 } lpe_rigid_stats;
 
 int  lpe_rigid_config_default(lpe_rigid_config *cfg);

@@ -728,7 +728,10 @@ k_pair_colour(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict_
         __syncthreads();
         const bool more = s_left && !s_fault && round < (1 << 20);
         __syncthreads();              // every thread has read s_left before it is reset
-        if (!more) break;
+        if (!more) {
+            if (threadIdx.x == 0) counts[9] = round + 1;
+            break;
+        }
     }
 #pragma unroll
     for (int k = 0; k < PK; k++) {
@@ -1858,6 +1861,7 @@ static int rigid_solve(lpe_ctx *ctx, RigidDev *d, bool colour, const int32_t *pg
         // colours of the canonical order (0: a caller-supplied order)
         stats->pgsLevels = colour ? hc[8] : 0;
         stats->posLevels = colour ? hc[8] : 0;
+        stats->colourRounds = colour ? hc[9] : 0;
     }
     return LPE_OK;
 }

@@ -61,10 +61,10 @@ class FluidConfig(C.Structure):
 
 class RigidStats(C.Structure):
     _fields_ = [("pairs", C.c_int32), ("contacts", C.c_int32), ("pgsLevels", C.c_int32),
-                ("posLevels", C.c_int32), ("overflow", C.c_int32), ("pad", C.c_int32)]
+                ("posLevels", C.c_int32), ("overflow", C.c_int32), ("colourRounds", C.c_int32)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class SphStats(C.Structure):
