@@ -370,13 +370,15 @@ int  lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *cfg, int nticks);
  * the particles with x in [x0, x1) (the first slab has no left edge, the last
  * no right edge) and runs lpe_sph_step on them; per sub-step it receives the
  * neighbours' particles within `halo` of its edges (ghosts, with their global
- * ids, so every density/force sum is the single-domain one bit for bit) and,
- * after the density pass, their owners' density and pressure.  The reference
+ * ids, so every density/force sum is the single-domain one bit for bit); the
+ * halo is deep enough that every ghost the forces pass reads has all its
+ * neighbours present, so its locally computed density is its owner's.  The reference
  * grid is derived from the all-reduced bbox of all ranks.  Once per tick the
  * rigid accumulators are all-reduced (rank order) before the write-back and
- * particles that left the slab move to the neighbour.  halo must cover the
- * smoothing length plus one tick's drift; ghost_cap bounds the ghosts and
- * migrants per side (overflow: LPE_ERR_OVERFLOW from the next download). */
+ * particles that left the slab move to the neighbour.  halo must cover twice
+ * the smoothing length plus one tick's drift (a particle further outside its
+ * slab raises LPE_ERR_OVERFLOW); ghost_cap bounds the ghosts and migrants per
+ * side (overflow: LPE_ERR_OVERFLOW from the next download). */
 /* Call before lpe_sph_upload (the particle arrays get owned + ghost slots). */
 int  lpe_sph_set_slab(lpe_ctx *ctx, float x0, float x1, float halo, int has_left,
                       int has_right, int ghost_cap);

@@ -90,6 +90,7 @@ enum StatusSlot {
     ST_NEIGH = 6,           // diag: neighbours (r < h) found by the density pass (sum)
     ST_STAGE_FALLBACK = 7,  // staged density blocks whose neighbourhood did not fit LDS
     ST_HALO_OVERFLOW = 8,   // slab decomposition: a ghost / migrant buffer overflowed
+    ST_HALO_DRIFT = 9,      // slab decomposition: an owned particle beyond the halo's reach
     ST_COUNT = 16
 };
 

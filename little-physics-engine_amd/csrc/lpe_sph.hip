@@ -769,13 +769,17 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
 //   reference grid is the global one) -> ghosts: owned particles within D of
 //   a slab edge go to that neighbour with their global id (so the canonical
 //   in-bin order, and every sum, is the single-domain one) -> sort owned +
-//   ghosts -> density -> the owners send the ghosts' (rho, p/rho^2) (a ghost's
-//   own density is only right where all its neighbours are present) ->
-//   forces/finish/coupling on owned slots only, compacted back to P.
+//   ghosts -> density -> forces/finish/coupling on owned slots only,
+//   compacted back to P.
+// Deep halo: an owned particle is at most `drift` = D - 2h outside its slab
+// (checked, ST_HALO_DRIFT), so its neighbours lie within h + drift of the
+// edge and theirs within 2h + drift = D: every ghost the forces pass reads
+// has all its own neighbours present, and its density, computed locally in
+// the canonical order, is bit-identical to its owner's.  One neighbour
+// exchange per sub-step, no second exchange of ghost densities.
 // Once per tick: the rigid accumulators are all-reduced (SUM) before the
 // write-back, then particles that left the slab migrate to the neighbour.
-// D must cover h plus the drift of a tick (0.3 m default; ST_HALO_OVERFLOW
-// flags buffers that overflowed).
+// ST_HALO_OVERFLOW flags exchange buffers that overflowed.
 static constexpr int GREC = 8;    // floats per ghost record: x, y, vx, vy, m, id, -, -
 static constexpr int MREC = 8;    // floats per migrant: x, y, vx, vy, m, id, rho, p
 static constexpr int HDR = 4;     // header floats of an exchange buffer ([0]: count, int)
@@ -786,8 +790,6 @@ struct Shard {
     int cap = 0;                       // ghosts / migrants per side
     int32_t *ntot = nullptr;           // device: owned + ghosts of the sub-step
     float *gsL = nullptr, *gsR = nullptr, *grL = nullptr, *grR = nullptr;
-    int32_t *sendSlot = nullptr;       // [2 cap] P slot of each sent ghost
-    float *rsL = nullptr, *rsR = nullptr, *rrL = nullptr, *rrR = nullptr;
     float *msL = nullptr, *msR = nullptr, *mrL = nullptr, *mrR = nullptr;
     float4 *bb = nullptr;              // global bbox
     int cap_slots = 0;                 // per-slot arrays below
@@ -828,12 +830,14 @@ __device__ __forceinline__ int rcount(const float *buf, int cap) {
     return buf ? min(*(const int *)buf, cap) : 0;
 }
 
-__global__ void k_ghost_pack(int n, PState P, float x0, float x1, float D, int hasL, int hasR,
-                             float *__restrict__ sL, float *__restrict__ sR,
-                             int32_t *__restrict__ sendSlot, int cap, int32_t *__restrict__ status) {
+__global__ void k_ghost_pack(int n, PState P, float x0, float x1, float D, float drift, int hasL, int hasR,
+                             float *__restrict__ sL, float *__restrict__ sR, int cap,
+                             int32_t *__restrict__ status) {
     int i = blockIdx.x * TPB + threadIdx.x;
     if (i >= n) return;
     const float x = P.x[i];
+    if ((hasL && x < x0 - drift) || (hasR && x >= x1 + drift))
+        atomicOr(&status[ST_HALO_DRIFT], 1);       // beyond what the halo covers
     for (int side = 0; side < 2; side++) {
         const bool go = side == 0 ? (hasL && x < x0 + D) : (hasR && x >= x1 - D);
         if (!go) continue;
@@ -843,7 +847,6 @@ __global__ void k_ghost_pack(int n, PState P, float x0, float x1, float D, int h
         float *r = buf + HDR + (size_t)k * GREC;
         r[0] = x; r[1] = P.y[i]; r[2] = P.vx[i]; r[3] = P.vy[i];
         r[4] = P.m[i]; r[5] = __int_as_float(P.id[i]);
-        sendSlot[side * cap + k] = i;
     }
 }
 
@@ -884,44 +887,6 @@ __global__ void k_ghost_unpack(const float *__restrict__ rL, const float *__rest
     uint32_t k = (((uint32_t)ky * (uint32_t)W + (uint32_t)kx) << 2) | (uint32_t)(qy * 2 + qx);
     key[slot] = k;
     atomicAdd(&count[k], 1);
-}
-
-// (rho, p/rho^2) of the ghosts this rank sent, in the order they were sent
-__global__ void k_rho_pack(const int32_t *__restrict__ sendSlot, const float *__restrict__ sL,
-                           const float *__restrict__ sR, const int32_t *__restrict__ inv,
-                           const float4 *__restrict__ nbB, float *__restrict__ rsL,
-                           float *__restrict__ rsR, int cap) {
-    const int t = blockIdx.x * TPB + threadIdx.x;
-    const int side = t < cap ? 0 : 1, k = side ? t - cap : t;
-    const float *sbuf = side ? sR : sL;
-    float *rs = side ? rsR : rsL;
-    if (!sbuf || k >= rcount(sbuf, cap)) return;
-    if (k == 0) *hdr(rs) = rcount(sbuf, cap);
-    const float4 b = nbB[inv[sendSlot[side * cap + k]]];
-    rs[HDR + 2 * k] = b.z;
-    rs[HDR + 2 * k + 1] = b.w;
-}
-
-__global__ void k_rho_unpack(const float *__restrict__ rrL, const float *__restrict__ rrR,
-                             const float *__restrict__ gL, const float *__restrict__ gR, int cap,
-                             int nown, const int32_t *__restrict__ inv, float4 *__restrict__ nbB) {
-    const int t = blockIdx.x * TPB + threadIdx.x;
-    const int nL = rcount(gL, cap), nR = rcount(gR, cap);
-    const float *src;
-    int slot;
-    if (t < cap) {
-        if (t >= nL) return;
-        src = rrL + HDR + 2 * t;
-        slot = nown + t;
-    } else {
-        const int k = t - cap;
-        if (k >= nR) return;
-        src = rrR + HDR + 2 * k;
-        slot = nown + nL + k;
-    }
-    float4 &b = nbB[inv[slot]];
-    b.z = src[0];
-    b.w = src[1];
 }
 
 // particles that left the slab -> migrant buffers; keep flags for the rest
@@ -1103,7 +1068,7 @@ static void shard_free_slots(Shard *h) {
 static void shard_free(Shard *h) {
     if (!h) return;
     shard_free_slots(h);
-    void *ptrs[] = {h->ntot, h->gsL, h->gsR, h->grL, h->grR, h->sendSlot, h->rsL, h->rsR, h->rrL, h->rrR,
+    void *ptrs[] = {h->ntot, h->gsL, h->gsR, h->grL, h->grR,
                     h->msL, h->msR, h->mrL, h->mrR, h->bb};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     delete h;
@@ -1539,7 +1504,6 @@ static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr) {
 
 // ---- x-slab decomposition (host side of the kernels above) -------------
 static size_t ghost_bytes(int cap) { return sizeof(float) * (HDR + (size_t)cap * GREC); }
-static size_t rho_bytes(int cap) { return sizeof(float) * (HDR + (size_t)cap * 2); }
 static size_t mig_bytes(int cap) { return sizeof(float) * (HDR + (size_t)cap * MREC); }
 static int shard_slots(const Shard &h) { return 2 * h.cap; }   // ghost slots after the owned ones
 
@@ -1560,8 +1524,9 @@ static int sph_hash_shard(lpe_ctx *ctx, float subDt, float halfDt, bool first) {
     if (st) return st;
     LPE_HIP(ctx, hipMemsetAsync(h.gsL, 0, sizeof(float) * HDR, s));
     LPE_HIP(ctx, hipMemsetAsync(h.gsR, 0, sizeof(float) * HDR, s));
+    const float drift = h.D - 2.0f * d.cfg.gridConfig.smoothingLength;
     LPE_KERNEL(ctx, "k_ghost_pack", k_ghost_pack, dim3(nblk1(d.n)), dim3(TPB), 0, s, d.n, d.P, h.x0, h.x1, h.D,
-               h.hasL, h.hasR, h.gsL, h.gsR, h.sendSlot, h.cap, d.status);
+               drift, h.hasL, h.hasR, h.gsL, h.gsR, h.cap, d.status);
     LPE_CHECK_LAUNCH(ctx, "k_ghost_pack");
     st = tr->halo(ctx, h.hasL ? h.gsL : nullptr, h.hasR ? h.gsR : nullptr, h.hasL ? h.grL : nullptr,
                   h.hasR ? h.grR : nullptr, ghost_bytes(h.cap));
@@ -1581,24 +1546,11 @@ static int sph_hash_shard(lpe_ctx *ctx, float subDt, float halfDt, bool first) {
     return LPE_OK;
 }
 
-// after the density pass: the owners' (rho, p/rho^2) of the ghosts, and the
-// owned-slot compaction map
-static int sph_ghost_density(lpe_ctx *ctx) {
+// after the density pass: the owned-slot compaction map (exclusive scan of
+// the owned flags of the sorted slots)
+static int sph_owned_map(lpe_ctx *ctx) {
     SphDev &d = ctx->sph;
     Shard &h = *d.shard;
-    hipStream_t s = ctx->stream;
-    LPE_KERNEL(ctx, "k_rho_pack", k_rho_pack, dim3(nblk1(2 * h.cap)), dim3(TPB), 0, s, h.sendSlot,
-               h.hasL ? h.gsL : (const float *)nullptr, h.hasR ? h.gsR : (const float *)nullptr, h.inv, d.nbB,
-               h.rsL, h.rsR, h.cap);
-    LPE_CHECK_LAUNCH(ctx, "k_rho_pack");
-    int st = ctx->transport->halo(ctx, h.hasL ? h.rsL : nullptr, h.hasR ? h.rsR : nullptr,
-                                  h.hasL ? h.rrL : nullptr, h.hasR ? h.rrR : nullptr, rho_bytes(h.cap));
-    if (st) return st;
-    LPE_KERNEL(ctx, "k_rho_unpack", k_rho_unpack, dim3(nblk1(2 * h.cap)), dim3(TPB), 0, s,
-               h.hasL ? h.rrL : (const float *)nullptr, h.hasR ? h.rrR : (const float *)nullptr,
-               h.hasL ? h.grL : (const float *)nullptr, h.hasR ? h.grR : (const float *)nullptr, h.cap, d.n,
-               h.inv, d.nbB);
-    LPE_CHECK_LAUNCH(ctx, "k_rho_unpack");
     const int ncap = d.n + shard_slots(h);
     return sph_scan(ctx, ncap, h.owned, h.dst, (int32_t *)d.key, h.obsum, 0, false);
 }
@@ -1681,6 +1633,10 @@ extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
         ctx->err = "slab decomposition without a transport (lpe_mg_init_rccl / lpe_mg_loopback_run)";
         return LPE_ERR_STATE;
     }
+    if (sh && !(sh->D > 2.0f * c.gridConfig.smoothingLength)) {
+        ctx->err = "slab decomposition: the halo must exceed twice the smoothing length";
+        return LPE_ERR_ARG;
+    }
     if (sh) {
         sp.n = d.n + shard_slots(*sh);
         sp.nptr = sh->ntot;
@@ -1696,7 +1652,7 @@ extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
             if (st) return st;
             st = sph_density(ctx, sp.n, sh->ntot);
             if (st) return st;
-            st = sph_ghost_density(ctx);
+            st = sph_owned_map(ctx);
         } else {
             st = sph_hash(ctx, subDt, halfDt, step == 0, false);
             if (st) return st;
@@ -1754,6 +1710,11 @@ static int check_status(lpe_ctx *ctx) {
     }
     if (status[ST_LIST_OVERFLOW]) {
         ctx->err = "the rigid coupling bin list overflowed its capacity bound";
+        return LPE_ERR_OVERFLOW;
+    }
+    if (status[ST_HALO_DRIFT]) {
+        ctx->err = "slab decomposition: a particle moved further outside its slab than halo - 2h allows "
+                   "(raise the halo of lpe_sph_set_slab)";
         return LPE_ERR_OVERFLOW;
     }
     if (status[ST_HALO_OVERFLOW]) {
@@ -1893,14 +1854,11 @@ extern "C" int lpe_sph_set_slab(lpe_ctx *ctx, float x0, float x1, float halo, in
     d.shard = h;
     LPE_HIP(ctx, hipMalloc((void **)&h->ntot, sizeof(int32_t)));
     LPE_HIP(ctx, hipMalloc((void **)&h->bb, sizeof(float4)));
-    LPE_HIP(ctx, hipMalloc((void **)&h->sendSlot, sizeof(int32_t) * 2 * (size_t)ghost_cap));
     float **gb[] = {&h->gsL, &h->gsR, &h->grL, &h->grR};
     for (float **q : gb) LPE_HIP(ctx, hipMalloc((void **)q, ghost_bytes(ghost_cap)));
-    float **rb[] = {&h->rsL, &h->rsR, &h->rrL, &h->rrR};
-    for (float **q : rb) LPE_HIP(ctx, hipMalloc((void **)q, rho_bytes(ghost_cap)));
     float **mb[] = {&h->msL, &h->msR, &h->mrL, &h->mrR};
     for (float **q : mb) LPE_HIP(ctx, hipMalloc((void **)q, mig_bytes(ghost_cap)));
-    float *all[] = {h->gsL, h->gsR, h->grL, h->grR, h->rsL, h->rsR, h->rrL, h->rrR, h->msL, h->msR, h->mrL, h->mrR};
+    float *all[] = {h->gsL, h->gsR, h->grL, h->grR, h->msL, h->msR, h->mrL, h->mrR};
     for (float *q : all) LPE_HIP(ctx, hipMemsetAsync(q, 0, sizeof(float) * HDR, ctx->stream));
     LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return LPE_OK;

@@ -46,9 +46,10 @@ def owners(x, edges) -> np.ndarray:
     return np.searchsorted(np.asarray(edges, np.float32)[1:-1], xf, side="right").astype(np.int32)
 
 
-def ghost_capacity(x, edges, halo: float, factor: float = 4.0, floor: int = 4096) -> int:
+def ghost_capacity(x, edges, halo: float, factor: float = 3.0, floor: int = 4096) -> int:
     """Ghost / migrant slots per side: `factor` times the most particles
-    within `halo` of any inner edge at the start, plus `floor`."""
+    within `halo` of any inner edge at the start (room for compression), plus
+    `floor`."""
     xf = np.asarray(x, np.float32)
     worst = 0
     for e in np.asarray(edges, np.float32)[1:-1]:
@@ -57,9 +58,12 @@ def ghost_capacity(x, edges, halo: float, factor: float = 4.0, floor: int = 4096
 
 
 def default_halo(cfg) -> float:
-    """Ghost width: the smoothing length plus a tick's worth of drift
-    (4h; 0.2 m at the default h = 0.05, SURVEY.md §8(e) "two cells")."""
-    return 4.0 * float(cfg.gridConfig.smoothingLength)
+    """Ghost width 8h (0.4 m at the default h = 0.05): 2h so that every ghost
+    the forces pass reads has all its own neighbours (no second exchange of
+    ghost densities), plus 6h = 0.3 m of drift per tick, 36 m/s at dt = 1/120 s
+    (fluid struck by the pentagons of the metric scene, which land at ~12 m/s,
+    moves at up to ~25 m/s); beyond it the step fails loudly."""
+    return 8.0 * float(cfg.gridConfig.smoothingLength)
 
 
 def setup_rank(ctx, rank: int, nranks: int, fluid: dict, edges, cfg, rigids=None, halo=None,
