@@ -149,6 +149,26 @@ def density_microbench(lpe, scenes, device, side=4096, reps=5):
                 mean_density=float(np.mean(rho)), max_cell_occupancy=st["maxCellOccupancy"])
 
 
+def render_bench(ctx, U, reps=3):
+    """The screen-space fluid density field (lpe_render_density, SURVEY.md
+    §8(f) rank 3) of the settled scene: the renderer's own parameters
+    (fluid_renderer.cpp:368-388: one cell per pixel at MetersPerPixel = 0.01,
+    origin (0, 0), smoothingRadius 10), over the whole U x U universe."""
+    side = int(round(U / 0.01))
+    ctx.render_density(side, side, 0.01, (0.0, 0.0), 10.0, download=False)      # warm
+    ctx.timing(1)
+    ctx.timing_reset()
+    for _ in range(reps):
+        _, mx = ctx.render_density(side, side, 0.01, (0.0, 0.0), 10.0, download=False)
+    t = ctx.timing_read()
+    ctx.timing(0)
+    keys = ("k_render_density", "k_box_blur", "k_grid_max", "k_normalize_density")
+    frame = sum(t[k][0] for k in t) / reps * 1e3
+    return dict(cells=side * side, kernels_us={k: round(t[k][0] / max(t[k][1], 1) * 1e3, 1) for k in keys if k in t},
+                frame_kernels_us=round(frame, 1), max_density=mx,
+                note="includes the hash of the current positions (k_kick_drift probe, scan, scatter, permute)")
+
+
 def loopback_check(args, lpe, scenes, slab, device):
     """K slab ranks of MW{K} on one GPU through the in-process transport:
     exercises the sharded bench path (scene, slab set-up, world ticks with
@@ -305,6 +325,7 @@ def main():
     out = ctx.sph_download_owned() if sharded else ctx.sph_download()
     settled = dict(fluid=out, bodies=ctx.rigid_download())
     n_rank = len(out["x"])
+    render = render_bench(ctx, s["U"]) if world == 1 and not args.no_density_microbench else None
 
     if rank != 0:
         if dist is not None:
@@ -377,6 +398,7 @@ def main():
     if world == 1 and not args.no_density_microbench:
         line["density_microbench"] = density_microbench(lpe, scenes, local)
         line["rigid_microbench"] = rigid_microbench(lpe, local)
+        line["render_density"] = render
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.scene, settled)
     print(json.dumps(line))

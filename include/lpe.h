@@ -403,6 +403,28 @@ int  lpe_mg_init_rccl(lpe_ctx *ctx, int nranks, int rank, const char *id);
 int  lpe_mg_loopback_run(int n, lpe_ctx **ctxs, const lpe_world_config *cfg, double dt_tick,
                          int nticks);
 
+/* ---- screen-space fluid density field -------- */
+/* GPURenderParams (include/renderers/fluid_renderer_kernels.h:28-41): a
+ * gridW x gridH grid of cellSize-metre cells from (originX, originY);
+ * smoothingRadius is in cells (fluid_renderer.cpp:384-388 sets 10 and
+ * cellSize = metres per pixel, origin (0, 0)). */
+typedef struct lpe_render_params {
+    int32_t gridW, gridH;
+    float cellSize;
+    float originX, originY;
+    float smoothingRadius;
+} lpe_render_params;
+/* Replaces the compute passes of FluidRenderer::render (fluid_renderer.cpp:
+ * 341-465, fluid_renderer_kernels.metal:36-124) on the context's current
+ * fluid: unnormalised poly6 density per cell (h = smoothingRadius *
+ * cellSize), two 5x5 box blurs, the maximum of the blurred grid, and the
+ * normalised grid saturate(d / max) (0 where max <= 1e-12).  normalized
+ * (gridW * gridH floats, row-major, may be NULL) and max_out (may be NULL)
+ * are host pointers; blocks until done.  No fluid: a zero grid (the
+ * reference skips the frame).  Not on a slab rank (LPE_ERR_STATE). */
+int  lpe_render_density(lpe_ctx *ctx, const lpe_render_params *params, float *normalized,
+                        float *max_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -39,6 +39,9 @@ struct SphDev {
     float4 *nbA = nullptr;        // sorted neighbour records (x, y, m, -)
     float4 *nbB = nullptr;        // (vx, vy, rho, p / rho^2)
     uint4 *nlist = nullptr;       // per-slot neighbour list k - s (int16, 8 per uint4), [cap/8][cap_n]
+    float *rgrid = nullptr;       // renderer density grid, two W*H buffers (lpe_render_density)
+    size_t cap_rgrid = 0;
+    uint32_t *rmax = nullptr;     // renderer: max of the blurred grid (float bits)
     int32_t *ncount = nullptr;    // neighbours found (> cap: forces walks the bins)
     // counting-sort grid hash over (2h cell, h quadrant) bins
     uint32_t *key = nullptr;      // bin of each P slot
@@ -173,4 +176,7 @@ static inline int lpe_grow(lpe_ctx *ctx, T **p, int *cap, long want, long elems_
 
 int lpe_rigid_destroy_internal(lpe_ctx *ctx);
 int lpe_sph_cover_box(lpe_ctx *ctx, double x0, double y0, double x1, double y1);
+// sort the CURRENT particle positions into the bins (no integration): the
+// state of lpe_sph_probe_* and of the renderer's density grid
+int lpe_sph_hash_current(lpe_ctx *ctx);
 int lpe_timer_destroy_internal(lpe_ctx *ctx);

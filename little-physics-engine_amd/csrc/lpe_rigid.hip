@@ -67,7 +67,7 @@ __device__ __forceinline__ int r_block_excl(int v, int *total) {
 __global__ void __launch_bounds__(RTPB) k_rscan_reduce(const int32_t *nptr, int ncap,
                                                        const int32_t *__restrict__ cnt,
                                                        int32_t *__restrict__ bsum) {
-    int n = nptr ? *nptr : ncap;
+    int n = nptr ? min(*nptr, ncap) : ncap;   // a count past the capacity (overflow, redone) is clipped
     int base = blockIdx.x * 1024;
     int s = 0;
     for (int k = 0; k < 4; k++) {
@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(RTPB) k_rscan_reduce(const int32_t *nptr, int 
 __global__ void __launch_bounds__(RTPB) k_rscan_blocks(const int32_t *nptr, int ncap,
                                                        int32_t *__restrict__ bsum,
                                                        int32_t *__restrict__ start) {
-    int n = nptr ? *nptr : ncap;
+    int n = nptr ? min(*nptr, ncap) : ncap;   // a count past the capacity (overflow, redone) is clipped
     int nb = (n + 1023) / 1024;
     int carry = 0;
     for (int b0 = 0; b0 < nb; b0 += RTPB) {
@@ -99,7 +99,7 @@ __global__ void __launch_bounds__(RTPB) k_rscan_final(const int32_t *nptr, int n
                                                       const int32_t *__restrict__ bsum,
                                                       int32_t *__restrict__ start,
                                                       int32_t *__restrict__ cursor) {
-    int n = nptr ? *nptr : ncap;
+    int n = nptr ? min(*nptr, ncap) : ncap;   // a count past the capacity (overflow, redone) is clipped
     int base = blockIdx.x * 1024 + threadIdx.x * 4;
     int v[4], s = 0;
     for (int k = 0; k < 4; k++) { int c = base + k; v[k] = (c < n) ? cnt[c] : 0; s += v[k]; }
@@ -381,11 +381,13 @@ __global__ void k_bp_sort(int nb, const int32_t *__restrict__ pstart, int2 *__re
 
 // narrowPhase (narrowphase.cpp:352-420): one thread per pair
 __global__ void __launch_bounds__(128)
-k_narrow(const int32_t *__restrict__ npptr, const int2 *__restrict__ pairs,
+k_narrow(const int32_t *__restrict__ npptr, int cap, const int2 *__restrict__ pairs,
          const lpe_body *__restrict__ bodies, const double *__restrict__ verts,
          lpe_contact *__restrict__ slots, int32_t *__restrict__ ccount) {
     int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= *npptr) return;
+    // the pair count can exceed the buffers when they overflowed (the step
+    // then grows them and redoes the broadphase): never past the capacity
+    if (k >= min(*npptr, cap)) return;
     int2 pr = pairs[k];
     const lpe_body ba = bodies[pr.x], bb = bodies[pr.y];
     DShape A = dshape(ba, verts), B = dshape(bb, verts);
@@ -444,11 +446,11 @@ k_narrow(const int32_t *__restrict__ npptr, const int2 *__restrict__ pairs,
     ccount[k] = cnt;
 }
 
-__global__ void k_compact(const int32_t *__restrict__ npptr, const lpe_contact *__restrict__ slots,
+__global__ void k_compact(const int32_t *__restrict__ npptr, int cap_pairs, const lpe_contact *__restrict__ slots,
                           const int32_t *__restrict__ ccount, const int32_t *__restrict__ cstart,
                           lpe_contact *__restrict__ out, int cap) {
     int k = blockIdx.x * RTPB + threadIdx.x;
-    if (k >= *npptr) return;
+    if (k >= min(*npptr, cap_pairs)) return;
     int s = cstart[k];
     for (int j = 0; j < ccount[k]; j++)
         if (s + j < cap) out[s + j] = slots[(size_t)k * MAXC + j];
@@ -1734,7 +1736,7 @@ static int rigid_detect(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pai
             LPE_KERNEL(ctx, "k_bp_sort", k_bp_sort, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->pstart, d->pairs, d->pairRankB, d->cap_pairs);
             LPE_HIP(ctx, hipMemcpyAsync(d->counts, d->pstart + nb, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
         }
-        LPE_KERNEL(ctx, "k_narrow", k_narrow, dim3(rblk(d->cap_pairs, 128)), dim3(128), 0, s, d->counts, d->pairs, d->bodies, d->verts, d->cslots, d->ccount);
+        LPE_KERNEL(ctx, "k_narrow", k_narrow, dim3(rblk(d->cap_pairs, 128)), dim3(128), 0, s, d->counts, d->cap_pairs, d->pairs, d->bodies, d->verts, d->cslots, d->ccount);
         int st = rscan(ctx, d, d->counts, d->cap_pairs, d->ccount, d->cstart, nullptr);
         if (st) return st;
         int32_t hc[8];
@@ -1757,7 +1759,7 @@ static int rigid_detect(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pai
             if (st) return st;
         }
         LPE_HIP(ctx, hipMemcpyAsync(d->counts + 1, &ncv, sizeof(int32_t), hipMemcpyHostToDevice, s));
-        LPE_KERNEL(ctx, "k_compact", k_compact, dim3(rblk(d->cap_pairs)), dim3(RTPB), 0, s, d->counts, d->cslots, d->ccount, d->cstart, d->contacts, d->cap_contacts);
+        LPE_KERNEL(ctx, "k_compact", k_compact, dim3(rblk(d->cap_pairs)), dim3(RTPB), 0, s, d->counts, d->cap_pairs, d->cslots, d->ccount, d->cstart, d->contacts, d->cap_contacts);
         LPE_CHECK_LAUNCH(ctx, "detect");
         d->last_np = np;
         d->last_nc = ncv;

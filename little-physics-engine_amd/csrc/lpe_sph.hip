@@ -1080,7 +1080,7 @@ static void sph_free(SphDev &d) {
     pstate_free(d.P);
     pstate_free(d.S);
     void *ptrs[] = {d.rho, d.pr, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.count, d.start, d.cursor,
-                    d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.raabb, d.accum, d.rbinStart,
+                    d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.raabb, d.accum, d.rbinStart, d.rgrid, d.rmax,
                     d.rbinList, d.rbinCount, d.coupleBody};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     d = SphDev();
@@ -1799,6 +1799,13 @@ extern "C" int lpe_sph_diag(lpe_ctx *ctx, int on) {
         LPE_HIP(ctx, hipMemsetAsync(d.status + ST_NL_OVERFLOW, 0, sizeof(int32_t) * 4, ctx->stream));
     }
     return LPE_OK;
+}
+
+int lpe_sph_hash_current(lpe_ctx *ctx) {
+    SphDev &d = ctx->sph;
+    if (d.n <= 0) return LPE_OK;
+    LPE_HIP(ctx, hipMemsetAsync(d.status + ST_MAX_OCC, 0, sizeof(int32_t), ctx->stream));
+    return sph_hash(ctx, 0.f, 0.f, false, true);
 }
 
 extern "C" int lpe_sph_probe_cells(lpe_ctx *ctx, int32_t *cell_index, lpe_sph_stats *stats) {

@@ -202,6 +202,13 @@ SIGNATURES["lpe_mg_init_rccl"] = ([C.c_void_p, C.c_int, C.c_int, C.c_char_p], C.
 SIGNATURES["lpe_mg_loopback_run"] = ([C.c_int, C.POINTER(C.c_void_p), C.POINTER(WorldConfig), C.c_double,
                                       C.c_int], C.c_int)
 
+class RenderParams(C.Structure):
+    _fields_ = [("gridW", C.c_int32), ("gridH", C.c_int32), ("cellSize", C.c_float),
+                ("originX", C.c_float), ("originY", C.c_float), ("smoothingRadius", C.c_float)]
+
+
+SIGNATURES["lpe_render_density"] = ([C.c_void_p, C.POINTER(RenderParams), _FP, _FP], C.c_int)
+
 SYS_BOUNDARY, SYS_GRAVITY, SYS_ROTATION, SYS_MOVEMENT, SYS_SLEEP = 1, 2, 4, 8, 16
 
 
@@ -382,6 +389,17 @@ class Context:
     def sph_set_domain(self, x0, y0, x1, y1):
         self._chk(lib().lpe_sph_set_domain(self._h, float(x0), float(y0), float(x1), float(y1)),
                   "lpe_sph_set_domain")
+
+    def render_density(self, grid_w, grid_h, cell_size=0.01, origin=(0.0, 0.0), smoothing_radius=10.0,
+                       download=True):
+        """FluidRenderer's density field: (normalised grid [grid_h, grid_w], max)."""
+        p = RenderParams(int(grid_w), int(grid_h), float(cell_size), float(origin[0]), float(origin[1]),
+                         float(smoothing_radius))
+        out = np.empty((int(grid_h), int(grid_w)), np.float32) if download else None
+        mx = np.zeros(1, np.float32)
+        self._chk(lib().lpe_render_density(self._h, C.byref(p), _fp(out.reshape(-1)) if download else None,
+                                           _fp(mx)), "lpe_render_density")
+        return out, float(mx[0])
 
     def mg_init_rccl(self, nranks: int, rank: int, uid: bytes):
         assert len(uid) == 128

@@ -292,3 +292,21 @@ def world_tick(fcfg, rcfg, particles, bodies, verts, couple, dt, nticks=1):
         f(C.byref(fcfg), C.byref(rcfg), float(dt), 1.0, 1.0, 1.0, p.ctypes.data, p.shape[0],
           b.ctypes.data, len(b), v.ctypes.data, len(c), c.ctypes.data)
     return p, b
+
+
+def render_density(x, y, grid_w, grid_h, cell_size=0.01, origin=(0.0, 0.0), smoothing_radius=10.0):
+    """FluidRenderer's density field restated (oracle/render_oracle.c):
+    dict(density, blurred, max, normalized), grids [grid_h, grid_w]."""
+    L = lib()
+    f = L.lpeo_render_density
+    f.restype = None
+    xs = np.ascontiguousarray(x, np.float32)
+    ys = np.ascontiguousarray(y, np.float32)
+    shape = (int(grid_h), int(grid_w))
+    dens, blur, scratch, norm = (np.empty(shape, np.float32) for _ in range(4))
+    mx = np.zeros(1, np.float32)
+    f(C.c_int(len(xs)), xs.ctypes.data_as(_FP), ys.ctypes.data_as(_FP), C.c_int(shape[1]), C.c_int(shape[0]),
+      C.c_float(cell_size), C.c_float(origin[0]), C.c_float(origin[1]), C.c_float(smoothing_radius),
+      dens.ctypes.data_as(_FP), blur.ctypes.data_as(_FP), scratch.ctypes.data_as(_FP),
+      mx.ctypes.data_as(_FP), norm.ctypes.data_as(_FP))
+    return dict(density=dens, blurred=blur, max=float(mx[0]), normalized=norm)
