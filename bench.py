@@ -230,7 +230,7 @@ def rigid_microbench(lpe, device, reps=10):
     step = sum(v[0] for v in t.values()) / reps * 1e3
     return dict(fixture="tests/golden/pile_M_t250.npz", pairs=st["pairs"], contacts=st["contacts"],
                 colours=st["pgsLevels"], colour_rounds=st["colourRounds"], reps=reps, step_kernels_us=round(step, 1),
-                kernels_us={k: us[k] for k in ("k_bp_pairs", "k_narrow", "k_pair_colour", "k_pgs_colour",
+                kernels_us={k: us[k] for k in ("k_bg_key", "k_bg_pairs", "k_narrow", "k_pair_colour", "k_pgs_colour",
                                                "k_pos_colour") if k in us})
 
 

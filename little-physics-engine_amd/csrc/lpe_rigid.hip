@@ -7,7 +7,7 @@
 //   k_rb_prep       per-body AABB (computeAABB, broadphase.cpp:158-191) and
 //                   the candidate test (Solid + Mass + Phase, inside the
 //                   quadtree root, broadphase.cpp:200-223)
-//   k_bp_pairs      tiled all-pairs AABB test in entity-id order: the pair SET
+//   k_bg_*          uniform-grid broadphase in entity-id order: the pair SET
 //                   of detectCollisions (broadphase.cpp:233-295), which equals
 //                   brute force over the inserted boxes; emitted in canonical
 //                   (eid_a, eid_b) order by count -> scan -> fill -> segment sort
@@ -313,69 +313,160 @@ __global__ void k_rb_prep(int nb, const lpe_body *__restrict__ bodies, const dou
     cand[i] = ok ? 1 : 0;
 }
 
-// tiled all-pairs test in rank (entity id) order; mode 0 counts, 1 fills
-__global__ void __launch_bounds__(RTPB)
-k_bp_pairs(int nb, int mode, const int32_t *__restrict__ byRank, const lpe_body *__restrict__ bodies,
-           const double4 *__restrict__ aabb, const int32_t *__restrict__ cand, double small,
-           int32_t *__restrict__ pcount, const int32_t *__restrict__ pstart,
-           int32_t *__restrict__ pcursor, int2 *__restrict__ pairs, int32_t *__restrict__ pairRankB,
-           int cap_pairs, int32_t *__restrict__ status) {
-    if (blockIdx.y < blockIdx.x) return;
-    __shared__ double4 tb[RTPB];
-    __shared__ int tc[RTPB], ti[RTPB];
-    __shared__ uint32_t tf[RTPB];
-    int rb0 = blockIdx.y * RTPB;
-    {
-        int r = rb0 + threadIdx.x;
-        if (r < nb) {
-            int j = byRank[r];
-            tb[threadIdx.x] = aabb[j]; tc[threadIdx.x] = cand[j]; ti[threadIdx.x] = j;
-            tf[threadIdx.x] = bodies[j].flags;
-        } else {
-            tc[threadIdx.x] = 0;
-        }
-    }
-    __syncthreads();
-    int ra = blockIdx.x * RTPB + threadIdx.x;
-    if (ra >= nb) return;
-    int ia = byRank[ra];
-    if (!cand[ia]) return;
-    double4 A = aabb[ia];
-    bool aB = (bodies[ia].flags & LPE_BODY_BOUNDARY) != 0;
-    double sa = fmax(A.z - A.x, A.w - A.y);
-    int cnt = 0;
-    for (int k = 0; k < RTPB; k++) {
-        int rbk = rb0 + k;
-        if (rbk <= ra || !tc[k]) continue;
-        double4 B = tb[k];
-        if (A.z < B.x || A.x > B.z) continue;                  // boxesOverlap (broadphase.cpp:35-39)
-        if (A.w < B.y || A.y > B.w) continue;
-        bool bB = (tf[k] & LPE_BODY_BOUNDARY) != 0;
-        if (aB && bB) continue;
-        double sb = fmax(B.z - B.x, B.w - B.y);
-        if (sa < small && sb < small) continue;
-        if (mode == 0) {
-            cnt++;
-        } else {
-            int slot = atomicAdd(&pcursor[ra], 1);   // cursor starts at pstart[ra]
-            if (slot < cap_pairs) { pairs[slot] = make_int2(ia, ti[k]); pairRankB[slot] = rbk; }
-            else atomicOr(&status[0], 1);
-        }
-    }
-    if (mode == 0 && cnt) atomicAdd(&pcount[ra], cnt);
-}
-
+// each body's pair list sorted by partner rank; short lists by one thread
+// (insertion sort), lists longer than BP_SHORT by k_bp_sort_long
+static constexpr int BP_SHORT = 32;
+static constexpr int BP_LONG = 4096;       // longest list sorted in LDS (longer: one thread)
 __global__ void k_bp_sort(int nb, const int32_t *__restrict__ pstart, int2 *__restrict__ pairs,
                           int32_t *__restrict__ rk, int cap_pairs) {
     int r = blockIdx.x * RTPB + threadIdx.x;
     if (r >= nb) return;
     int s = pstart[r], e = min(pstart[r + 1], cap_pairs);
+    if (e - s > BP_SHORT && e - s <= BP_LONG) return;
     for (int k = s + 1; k < e; k++) {
         int v = rk[k];
         int2 p = pairs[k];
         int j = k - 1;
         while (j >= s && rk[j] > v) { rk[j + 1] = rk[j]; pairs[j + 1] = pairs[j]; j--; }
         rk[j + 1] = v; pairs[j + 1] = p;
+    }
+}
+
+// one block per body; a list of BP_SHORT < n <= BP_LONG entries (the walls'
+// lists, filled by many threads in arrival order) is bitonic-sorted in LDS
+__global__ void __launch_bounds__(RTPB)
+k_bp_sort_long(int nb, const int32_t *__restrict__ pstart, int2 *__restrict__ pairs,
+               int32_t *__restrict__ rk, int cap_pairs) {
+    const int r = blockIdx.x;
+    if (r >= nb) return;
+    const int s = pstart[r], e = min(pstart[r + 1], cap_pairs), n = e - s;
+    if (n <= BP_SHORT || n > BP_LONG) return;
+    __shared__ int key[BP_LONG];
+    __shared__ int2 val[BP_LONG];
+    int m = 1;
+    while (m < n) m <<= 1;
+    for (int i = threadIdx.x; i < m; i += RTPB) {
+        key[i] = i < n ? rk[s + i] : 0x7fffffff;
+        val[i] = i < n ? pairs[s + i] : make_int2(0, 0);
+    }
+    __syncthreads();
+    for (int size = 2; size <= m; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = threadIdx.x; i < m; i += RTPB) {
+                const int j = i ^ stride;
+                if (j > i) {
+                    const bool up = (i & size) == 0;
+                    if ((key[i] > key[j]) == up) {
+                        const int tk = key[i]; key[i] = key[j]; key[j] = tk;
+                        const int2 tv = val[i]; val[i] = val[j]; val[j] = tv;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    for (int i = threadIdx.x; i < n; i += RTPB) { rk[s + i] = key[i]; pairs[s + i] = val[i]; }
+}
+
+// ---- uniform-grid broadphase --------------------------------------------
+// The reference's pair set (broadphase.cpp:35-295: AABB overlap, not two
+// boundary bodies, not two small particles) in entity-id order (pairs of the
+// lower-ranked body, partners sorted by rank by k_bp_sort), from a uniform
+// grid: a body whose AABB extent is at most the cell size g and whose AABB
+// min corner lies on the grid is keyed by that corner's cell; two such bodies
+// can only overlap if their keys are at most one cell apart.  The others
+// ("special": walls, bodies off the grid) are tested against every candidate.
+__device__ __forceinline__ bool bp_pair_ok(const double4 &A, const double4 &B, bool aB, bool bB, double sa,
+                                           double sb, double small) {
+    if (A.z < B.x || A.x > B.z) return false;               // boxesOverlap (broadphase.cpp:35-39)
+    if (A.w < B.y || A.y > B.w) return false;
+    if (aB && bB) return false;
+    if (sa < small && sb < small) return false;
+    return true;
+}
+
+__global__ void k_bg_key(int nb, const int32_t *__restrict__ byRank, const double4 *__restrict__ aabb,
+                         const int32_t *__restrict__ cand, double org, double g, int G,
+                         int32_t *__restrict__ key, int32_t *__restrict__ cellCount,
+                         int32_t *__restrict__ special, int32_t *__restrict__ nspecial) {
+    int r = blockIdx.x * RTPB + threadIdx.x;
+    if (r >= nb) return;
+    const int ia = byRank[r];
+    int k = -1;                                              // not a candidate
+    if (cand[ia]) {
+        const double4 A = aabb[ia];
+        const double ext = fmax(A.z - A.x, A.w - A.y);
+        const double fx = floor((A.x - org) / g), fy = floor((A.y - org) / g);
+        if (ext <= g && fx >= 0.0 && fy >= 0.0 && fx < (double)G && fy < (double)G) {
+            k = (int)fy * G + (int)fx;
+            atomicAdd(&cellCount[k], 1);
+        } else {
+            k = -2;
+            special[atomicAdd(nspecial, 1)] = r;
+        }
+    }
+    key[r] = k;
+}
+
+__global__ void k_bg_fill(int nb, const int32_t *__restrict__ key, int32_t *__restrict__ cursor,
+                          int32_t *__restrict__ list) {
+    int r = blockIdx.x * RTPB + threadIdx.x;
+    if (r >= nb) return;
+    const int k = key[r];
+    if (k >= 0) list[atomicAdd(&cursor[k], 1)] = r;
+}
+
+// mode 0 counts (pcount of the lower rank), 1 fills (cursor from pstart)
+__global__ void k_bg_pairs(int nb, int mode, const int32_t *__restrict__ byRank,
+                           const lpe_body *__restrict__ bodies, const double4 *__restrict__ aabb,
+                           double small, int G, const int32_t *__restrict__ key,
+                           const int32_t *__restrict__ cellStart, const int32_t *__restrict__ list,
+                           const int32_t *__restrict__ special, const int32_t *__restrict__ nspecial,
+                           int32_t *__restrict__ pcount, int32_t *__restrict__ pcursor,
+                           int2 *__restrict__ pairs, int32_t *__restrict__ pairRankB, int cap_pairs,
+                           int32_t *__restrict__ status) {
+    int r = blockIdx.x * RTPB + threadIdx.x;
+    if (r >= nb) return;
+    const int k = key[r];
+    if (k == -1) return;
+    const int ia = byRank[r];
+    const double4 A = aabb[ia];
+    const bool aB = (bodies[ia].flags & LPE_BODY_BOUNDARY) != 0;
+    const double sa = fmax(A.z - A.x, A.w - A.y);
+    auto emit = [&](int lo, int hi) {                        // ranks: the pair belongs to lo
+        if (mode == 0) {
+            atomicAdd(&pcount[lo], 1);
+        } else {
+            const int slot = atomicAdd(&pcursor[lo], 1);
+            if (slot < cap_pairs) { pairs[slot] = make_int2(byRank[lo], byRank[hi]); pairRankB[slot] = hi; }
+            else atomicOr(&status[0], 1);
+        }
+    };
+    auto test = [&](int rb) {
+        const int ib = byRank[rb];
+        const double4 B = aabb[ib];
+        const bool bB = (bodies[ib].flags & LPE_BODY_BOUNDARY) != 0;
+        return bp_pair_ok(A, B, aB, bB, sa, fmax(B.z - B.x, B.w - B.y), small);
+    };
+    const int ns = *nspecial;
+    if (k >= 0) {
+        const int cx = k % G, cy = k / G;
+        for (int y = max(cy - 1, 0); y <= min(cy + 1, G - 1); y++)
+            for (int x = max(cx - 1, 0); x <= min(cx + 1, G - 1); x++) {
+                const int c = y * G + x;
+                for (int j = cellStart[c]; j < cellStart[c + 1]; j++) {
+                    const int rb = list[j];
+                    if (rb > r && test(rb)) emit(r, rb);
+                }
+            }
+        for (int j = 0; j < ns; j++) {                       // regular - special pairs
+            const int rb = special[j];
+            if (test(rb)) emit(min(r, rb), max(r, rb));
+        }
+    } else {
+        for (int j = 0; j < ns; j++) {                       // special - special pairs
+            const int rb = special[j];
+            if (rb > r && test(rb)) emit(r, rb);
+        }
     }
 }
 
@@ -1524,7 +1615,8 @@ int lpe_rigid_destroy_internal(lpe_ctx *ctx) {
                     d->bsum, d->order, d->rowN, d->rowR, d->rowAB, d->vel0, d->imii, d->inContact,
                     d->posState, d->posRec, d->posKeep, d->posStart, d->rowM, d->sItemA, d->sItemB,
                     d->sVer, d->lamN, d->lamF, d->sBCount, d->sBStart, d->sBCursor, d->sEnt,
-                    d->counts, d->pcol, d->cseg, d->cbase};
+                    d->counts, d->pcol, d->cseg, d->cbase, d->bgCount, d->bgStart, d->bgCursor,
+                    d->bgList, d->bgKey, d->bgSpecial};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     delete d;
     ctx->rigid = nullptr;
@@ -1682,6 +1774,24 @@ extern "C" int lpe_rigid_upload(lpe_ctx *ctx, int nb, const lpe_body *bodies, in
         LPE_HIP(ctx, hipMemcpyAsync(d->bodies, bodies, sizeof(lpe_body) * nb, hipMemcpyHostToDevice, s));
         LPE_HIP(ctx, hipMemcpyAsync(d->rank, rank.data(), sizeof(int32_t) * nb, hipMemcpyHostToDevice, s));
         LPE_HIP(ctx, hipMemcpyAsync(d->byRank, byRank.data(), sizeof(int32_t) * nb, hipMemcpyHostToDevice, s));
+        // broadphase cell: the largest rotation-bounded extent (2 x circumradius)
+        // among bodies of at most 2 m (walls and the like go to the special list)
+        double cell = 0.0;
+        for (int i = 0; i < nb; i++) {
+            const lpe_body &b = bodies[i];
+            double R = 0.0;
+            if (b.flags & LPE_BODY_CIRCLE) R = b.radius;
+            else
+                for (int v = 0; v < b.vert_cnt; v++) {
+                    const double lx = verts[2 * (b.vert_off + v)], ly = verts[2 * (b.vert_off + v) + 1];
+                    R = std::max(R, std::sqrt(lx * lx + ly * ly));
+                }
+            if (2.0 * R <= 2.0) cell = std::max(cell, 2.0 * R);
+        }
+        d->bp_cell = std::max(cell * 1.0001, 0.05);
+        if ((st = rgrow(ctx, &d->bgList, (size_t)nb))) return st;
+        if ((st = rgrow(ctx, &d->bgKey, (size_t)nb))) return st;
+        if ((st = rgrow(ctx, &d->bgSpecial, (size_t)nb))) return st;
         if (nverts > 0)
             LPE_HIP(ctx, hipMemcpyAsync(d->verts, verts, sizeof(double) * 2 * nverts, hipMemcpyHostToDevice, s));
         LPE_HIP(ctx, hipStreamSynchronize(s));
@@ -1728,12 +1838,39 @@ static int rigid_detect(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pai
             double lo = -c.boundaryBuffer, hi = -c.boundaryBuffer + (c.universeSize + 2 * c.boundaryBuffer);
             LPE_KERNEL(ctx, "k_rb_prep", k_rb_prep, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->verts, lo, hi, d->aabb, d->cand);
             LPE_HIP(ctx, hipMemsetAsync(d->pcount, 0, sizeof(int32_t) * nb, s));
-            dim3 g(rblk(nb), rblk(nb));
-            LPE_KERNEL(ctx, "k_bp_pairs", k_bp_pairs, g, dim3(RTPB), 0, s, nb, 0, d->byRank, d->bodies, d->aabb, d->cand, c.smallParticleThreshold, d->pcount, d->pstart, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6);
-            int st = rscan(ctx, d, nullptr, nb, d->pcount, d->pstart, d->pcursor);
+            // grid over the universe plus 1 m (bodies the boundary system lets
+            // stray further, or larger than a cell, are "special")
+            const double org = -1.0, g = d->bp_cell > 0.0 ? d->bp_cell : 1.0;
+            const long G = std::max(1L, (long)std::ceil((c.universeSize + 2.0) / g));
+            if (G * G > (1L << 26)) {
+                ctx->err = "rigid broadphase grid too large (universe / body size)";
+                return LPE_ERR_CAPACITY;
+            }
+            const int cells = (int)(G * G);
+            if (cells > d->cap_bgcells) {
+                int st0 = rgrow(ctx, &d->bgCount, (size_t)cells + 1);
+                if (!st0) st0 = rgrow(ctx, &d->bgStart, (size_t)cells + 1);
+                if (!st0) st0 = rgrow(ctx, &d->bgCursor, (size_t)cells + 1);
+                if (st0) return st0;
+                d->cap_bgcells = cells;
+            }
+            LPE_HIP(ctx, hipMemsetAsync(d->bgCount, 0, sizeof(int32_t) * cells, s));
+            LPE_HIP(ctx, hipMemsetAsync(d->counts + 10, 0, sizeof(int32_t), s));
+            LPE_KERNEL(ctx, "k_bg_key", k_bg_key, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->byRank, d->aabb, d->cand, org, g,
+                       (int)G, d->bgKey, d->bgCount, d->bgSpecial, d->counts + 10);
+            int st = rscan(ctx, d, nullptr, cells, d->bgCount, d->bgStart, d->bgCursor);
             if (st) return st;
-            LPE_KERNEL(ctx, "k_bp_pairs", k_bp_pairs, g, dim3(RTPB), 0, s, nb, 1, d->byRank, d->bodies, d->aabb, d->cand, c.smallParticleThreshold, d->pcount, d->pstart, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6);
+            LPE_KERNEL(ctx, "k_bg_fill", k_bg_fill, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bgKey, d->bgCursor, d->bgList);
+            LPE_KERNEL(ctx, "k_bg_pairs", k_bg_pairs, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, 0, d->byRank, d->bodies, d->aabb,
+                       c.smallParticleThreshold, (int)G, d->bgKey, d->bgStart, d->bgList, d->bgSpecial, d->counts + 10,
+                       d->pcount, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6);
+            st = rscan(ctx, d, nullptr, nb, d->pcount, d->pstart, d->pcursor);
+            if (st) return st;
+            LPE_KERNEL(ctx, "k_bg_pairs", k_bg_pairs, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, 1, d->byRank, d->bodies, d->aabb,
+                       c.smallParticleThreshold, (int)G, d->bgKey, d->bgStart, d->bgList, d->bgSpecial, d->counts + 10,
+                       d->pcount, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6);
             LPE_KERNEL(ctx, "k_bp_sort", k_bp_sort, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->pstart, d->pairs, d->pairRankB, d->cap_pairs);
+            LPE_KERNEL(ctx, "k_bp_sort_long", k_bp_sort_long, dim3(nb), dim3(RTPB), 0, s, nb, d->pstart, d->pairs, d->pairRankB, d->cap_pairs);
             LPE_HIP(ctx, hipMemcpyAsync(d->counts, d->pstart + nb, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
         }
         LPE_KERNEL(ctx, "k_narrow", k_narrow, dim3(rblk(d->cap_pairs, 128)), dim3(128), 0, s, d->counts, d->cap_pairs, d->pairs, d->bodies, d->verts, d->cslots, d->ccount);

@@ -60,11 +60,19 @@ struct RigidDev {
     int4 *sVer = nullptr;                            // rank/cnt on A, rank/cnt on B
     int32_t *sBCount = nullptr, *sBStart = nullptr, *sBCursor = nullptr, *sEnt = nullptr;
     int32_t *counts = nullptr;                // [0]=np [1]=nc [4]=npos [5]=heavy [6]=pair overflow
-                                              // [7]=solver fault [8]=colours
+                                              // [7]=solver fault [8]=colours [9]=colouring rounds
+                                              // [10]=special broadphase bodies
     int32_t *pcol = nullptr;                  // colour per pair (canonical order)
     int2 *cseg = nullptr;                     // (row start, rows) per coloured pair, colour-major
     int32_t *cbase = nullptr;                 // first cseg entry of each colour (+ end)
     int cap_pcol = 0;
+    // uniform-grid broadphase: bodies whose AABB fits a cell are keyed by the
+    // cell of their AABB min corner; the rest ("special": walls, bodies off
+    // the grid) are tested against every candidate
+    double bp_cell = 0.0;                     // cell size (largest bounded body extent)
+    int32_t *bgCount = nullptr, *bgStart = nullptr, *bgCursor = nullptr;   // per cell
+    int32_t *bgList = nullptr, *bgKey = nullptr, *bgSpecial = nullptr;      // per body (rank)
+    long cap_bgcells = 0;
     lpe_rigid_config cfg{};
     bool cfg_set = false;
     int last_np = 0, last_nc = 0;
