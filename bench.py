@@ -77,6 +77,26 @@ def pmc_traffic(kernel):
     return None, None
 
 
+# VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz, one wave64 instruction per 2
+# cycles per SIMD (32 lanes/cycle; MI355X_MICROARCH.md: FP32 vector 157.3 TF =
+# 64 flop/clk/SIMD)
+VALU_PEAK_GINST = 256 * 4 * 2.4 / 2.0
+
+
+def pmc_valu(kernel):
+    """VALU wave-instructions per launch of `kernel` from the newest committed
+    PMC pass (profiles/r*/pmc_valu.json: SQ_INSTS_VALU), or (None, None)."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_valu.json")), reverse=True):
+        try:
+            d = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if kernel in d:
+            return d[kernel]["valu_wave_insts"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def cpu_baseline(scene_name, state=None, budget_s=20.0):
     """The oracle (C/C++ restatement of the reference algorithms, 1 thread)
     running the same full tick on the same scene state (`state`: the device
@@ -353,6 +373,13 @@ def main():
                     avg_us=round(avg_s * 1e6, 2), algorithmic_bytes=b)
         if tsrc:
             roof["traffic_source"] = tsrc + " (HBM bytes per launch, rocprofv3 PMC, last 5 ticks)"
+        vi, vsrc = pmc_valu(dname) if world == 1 and args.scene == "M" else (None, None)
+        if vi:
+            # the compute side of the same launch: VALU instructions (PMC) over
+            # the live duration, against the chip's VALU issue rate
+            roof["valu"] = dict(wave_insts=vi, achieved_ginst_s=round(vi / avg_s / 1e9, 1),
+                                peak_ginst_s=VALU_PEAK_GINST, frac=round(vi / avg_s / 1e9 / VALU_PEAK_GINST, 4),
+                                source=vsrc)
     dens = times.get("k_density")
     roof_d = None
     if dens:
