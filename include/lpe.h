@@ -378,7 +378,9 @@ int  lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *cfg, int nticks);
  * particles that left the slab move to the neighbour.  halo must cover twice
  * the smoothing length plus one tick's drift (a particle further outside its
  * slab raises LPE_ERR_OVERFLOW); ghost_cap bounds the ghosts and migrants per
- * side (overflow: LPE_ERR_OVERFLOW from the next download). */
+ * side (overflow: LPE_ERR_OVERFLOW from the next download).  A slab with two
+ * neighbours must be at least 2 * halo - 2h wide (ghosts come from the two
+ * neighbours only); the host mirror (slab.py:default_halo) picks 2h + 1.5 m. */
 /* Call before lpe_sph_upload (the particle arrays get owned + ghost slots). */
 int  lpe_sph_set_slab(lpe_ctx *ctx, float x0, float x1, float halo, int has_left,
                       int has_right, int ghost_cap);

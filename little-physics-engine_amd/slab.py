@@ -57,13 +57,31 @@ def ghost_capacity(x, edges, halo: float, factor: float = 3.0, floor: int = 4096
     return int(factor * worst) + floor
 
 
-def default_halo(cfg) -> float:
-    """Ghost width 8h (0.4 m at the default h = 0.05): 2h so that every ghost
-    the forces pass reads has all its own neighbours (no second exchange of
-    ghost densities), plus 6h = 0.3 m of drift per tick, 36 m/s at dt = 1/120 s
-    (fluid struck by the pentagons of the metric scene, which land at ~12 m/s,
-    moves at up to ~25 m/s); beyond it the step fails loudly."""
-    return 8.0 * float(cfg.gridConfig.smoothingLength)
+DRIFT_ALLOWANCE = 1.5     # metres an owned particle may travel outside its slab in one tick
+
+
+def default_halo(cfg, edges=None) -> float:
+    """Ghost width D = 2h + DRIFT_ALLOWANCE (1.6 m at the default h = 0.05).
+    2h so that every ghost the forces pass reads has all its own neighbours
+    (no second exchange of ghost densities); the allowance is how far an
+    owned particle may move outside its slab before the once-per-tick
+    migration: 1.5 m, 180 m/s at dt = 1/120 s.  Measured on the metric scenes
+    over 350 ticks (profiles/r01/slab_drift.json): at most 0.69 m per tick
+    (MW2) and 0.62 m (M), speeds up to ~94 m/s (fluid struck by the
+    pentagons).  Beyond the allowance the step fails loudly (ST_HALO_DRIFT).
+
+    A slab between two neighbours must be at least 2D - 2h wide (the ghosts a
+    rank needs come from its neighbours only); with `edges` the halo shrinks
+    to fit the narrowest such slab (the small test scenes)."""
+    h = float(cfg.gridConfig.smoothingLength)
+    D = 2.0 * h + DRIFT_ALLOWANCE
+    if edges is not None:
+        w = np.diff(np.asarray(edges, np.float64))[1:-1]
+        if len(w):
+            D = min(D, (float(w.min()) + 2.0 * h) / 2.0)
+    if not D > 2.0 * h:
+        raise ValueError("slab decomposition: a slab is narrower than the 2h the halo needs")
+    return D
 
 
 def setup_rank(ctx, rank: int, nranks: int, fluid: dict, edges, cfg, rigids=None, halo=None,
@@ -71,7 +89,10 @@ def setup_rank(ctx, rank: int, nranks: int, fluid: dict, edges, cfg, rigids=None
     """Configure ctx as slab `rank` and upload the particles it owns (global
     ids = indices into `fluid`).  Returns the owned global ids."""
     import lpe  # the in-tree binding (little-physics-engine_amd/lpe.py)
-    halo = default_halo(cfg) if halo is None else halo
+    halo = default_halo(cfg, edges) if halo is None else halo
+    w = np.diff(np.asarray(edges, np.float64))[1:-1]
+    if len(w) and 2.0 * halo - 2.0 * float(cfg.gridConfig.smoothingLength) > float(w.min()):
+        raise ValueError("slab decomposition: an inner slab is narrower than 2 * halo - 2h")
     x = np.asarray(fluid["x"], np.float32)
     if ghost_cap is None:
         ghost_cap = ghost_capacity(x, edges, halo)
