@@ -115,11 +115,17 @@ struct LoopTransport : Transport {
         g->pL[rank] = sendL;
         g->pR[rank] = sendR;
         if (!g->barrier()) return LPE_ERR_STATE;
+        // the copies run on this rank's stream and are complete before the
+        // second barrier: the sender may then reuse its buffers, and this
+        // rank's unpack (same stream) sees the data
         int st = LPE_OK;
         if (recvL && rank > 0 && g->pR[rank - 1])
-            if (hipMemcpy(recvL, g->pR[rank - 1], bytes, hipMemcpyDeviceToDevice) != hipSuccess) st = LPE_ERR_HIP;
+            if (hipMemcpyAsync(recvL, g->pR[rank - 1], bytes, hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess)
+                st = LPE_ERR_HIP;
         if (recvR && rank < nranks - 1 && g->pL[rank + 1])
-            if (hipMemcpy(recvR, g->pL[rank + 1], bytes, hipMemcpyDeviceToDevice) != hipSuccess) st = LPE_ERR_HIP;
+            if (hipMemcpyAsync(recvR, g->pL[rank + 1], bytes, hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess)
+                st = LPE_ERR_HIP;
+        if (hipStreamSynchronize(ctx->stream) != hipSuccess) st = LPE_ERR_HIP;
         if (!g->barrier()) return LPE_ERR_STATE;
         return st;
     }
@@ -136,7 +142,9 @@ struct LoopTransport : Transport {
             for (int i = 0; i < n; i++)
                 acc[i] = op ? (g->red[r][i] < acc[i] ? g->red[r][i] : acc[i]) : acc[i] + g->red[r][i];
         if (!g->barrier()) return LPE_ERR_STATE;
-        if (hipMemcpy(buf, acc.data(), sizeof(float) * n, hipMemcpyHostToDevice) != hipSuccess) return LPE_ERR_HIP;
+        if (hipMemcpyAsync(buf, acc.data(), sizeof(float) * n, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess)
+            return LPE_ERR_HIP;
         return LPE_OK;
     }
 };

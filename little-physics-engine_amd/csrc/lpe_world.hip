@@ -137,6 +137,7 @@ extern "C" int lpe_world_set_coupling(lpe_ctx *ctx, int nr, const int32_t *body_
     // rotate keep their AABB extent; the others are bounded by 2 x circumradius
     std::vector<lpe_body> hb(rd->nb);
     std::vector<double> hv(2 * (size_t)std::max(rd->nverts, 1));
+    LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));    // the bodies may still be in flight
     if (rd->nb) LPE_HIP(ctx, hipMemcpy(hb.data(), rd->bodies, sizeof(lpe_body) * rd->nb, hipMemcpyDeviceToHost));
     if (rd->nverts) LPE_HIP(ctx, hipMemcpy(hv.data(), rd->verts, sizeof(double) * 2 * rd->nverts, hipMemcpyDeviceToHost));
     float bcs = std::max(0.25f, d.cs);
