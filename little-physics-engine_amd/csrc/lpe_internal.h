@@ -175,6 +175,10 @@ static inline int lpe_grow(lpe_ctx *ctx, T **p, int *cap, long want, long elems_
 }
 
 int lpe_rigid_destroy_internal(lpe_ctx *ctx);
+// world tick: rigid collision detection overlapped with the fluid step (lpe_rigid.hip)
+int rigid_tick_begin(lpe_ctx *ctx);
+int rigid_tick_boundary(lpe_ctx *ctx);
+int rigid_tick_finish(lpe_ctx *ctx);
 int lpe_sph_cover_box(lpe_ctx *ctx, double x0, double y0, double x1, double y1);
 // sort the CURRENT particle positions into the bins (no integration): the
 // state of lpe_sph_probe_* and of the renderer's density grid

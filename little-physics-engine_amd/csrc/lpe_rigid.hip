@@ -1517,6 +1517,45 @@ __global__ void k_boundary(int nb, lpe_body *__restrict__ bodies, double m, doub
     }
     bodies[i] = b;
 }
+// The world tick splits the boundary system in two so that collision
+// detection can start at the beginning of the tick: the position clamp
+// depends on positions only, which nothing before the boundary system changes
+// (the fluid step and gravity only write velocities; the fluid reads its own
+// gathered copy of the bodies, taken before the clamp), and the velocity part
+// is applied at the boundary system's place in the tick from the recorded
+// bounce bits.  Together they equal k_boundary.
+__global__ void k_boundary_pos(int nb, lpe_body *__restrict__ bodies, double m, double U,
+                               int32_t *__restrict__ bits) {
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb) return;
+    lpe_body &b = bodies[i];
+    int f = 0;
+    const int flags = b.flags;
+    if ((flags & LPE_BODY_HAS_VEL) && !((flags & LPE_BODY_HAS_SLEEP) && (flags & LPE_BODY_ASLEEP))) {
+        const double x = b.x, y = b.y;
+        if (x < m) { b.x = m; f |= 1; }
+        else if (x > U - m) { b.x = U - m; f |= 2; }
+        if (y < m) { b.y = m; f |= 4; }
+        else if (y > U - m) { b.y = U - m; f |= 8; }
+    }
+    bits[i] = f;
+}
+__global__ void k_boundary_vel(int nb, lpe_body *__restrict__ bodies, const int32_t *__restrict__ bits,
+                               double damp, double maxSpeed) {
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb) return;
+    const int f = bits[i];
+    if (!f) return;
+    lpe_body &b = bodies[i];
+    double vx = b.vx, vy = b.vy;
+    if (f & 1) vx = fabs(vx) * damp;
+    else if (f & 2) vx = -fabs(vx) * damp;
+    if (f & 4) vy = fabs(vy) * damp;
+    else if (f & 8) vy = -fabs(vy) * damp;
+    double sp = sqrt(vx * vx + vy * vy);
+    if (sp > maxSpeed) { vx = (vx / sp) * maxSpeed; vy = (vy / sp) * maxSpeed; }
+    b.vx = vx; b.vy = vy;
+}
 __device__ __forceinline__ bool gravity_view(const lpe_body &b) {
     return (b.flags & LPE_BODY_HAS_PHASE) && (b.flags & LPE_BODY_HAS_VEL) &&
            (b.flags & LPE_BODY_HAS_MASS) && !(b.flags & LPE_BODY_BOUNDARY);
@@ -1616,8 +1655,12 @@ int lpe_rigid_destroy_internal(lpe_ctx *ctx) {
                     d->posState, d->posRec, d->posKeep, d->posStart, d->rowM, d->sItemA, d->sItemB,
                     d->sVer, d->lamN, d->lamF, d->sBCount, d->sBStart, d->sBCursor, d->sEnt,
                     d->counts, d->pcol, d->cseg, d->cbase, d->bgCount, d->bgStart, d->bgCursor,
-                    d->bgList, d->bgKey, d->bgSpecial};
+                    d->bgList, d->bgKey, d->bgSpecial, d->bbits};
     for (void *p : ptrs) if (p) (void)hipFree(p);
+    if (d->hc) (void)hipHostFree(d->hc);
+    hipEvent_t evs[] = {d->evStart, d->evDetect, d->evColour};
+    for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
+    if (d->side) (void)hipStreamDestroy(d->side);
     delete d;
     ctx->rigid = nullptr;
     return LPE_OK;
@@ -1662,6 +1705,7 @@ static int rigid_alloc_bodies(lpe_ctx *ctx, RigidDev *d, int nb) {
     if ((st = rgrow(ctx, &d->sBCount, N))) return st;
     if ((st = rgrow(ctx, &d->sBStart, N + 1))) return st;
     if ((st = rgrow(ctx, &d->sBCursor, N))) return st;
+    if ((st = rgrow(ctx, &d->bbits, N))) return st;
     if (!d->counts) {
         if ((st = rgrow(ctx, &d->counts, 16))) return st;
         LPE_HIP(ctx, hipMemsetAsync(d->counts, 0, sizeof(int32_t) * 16, ctx->stream));
@@ -1716,11 +1760,11 @@ static int rigid_alloc_bsum(lpe_ctx *ctx, RigidDev *d, long n) {
 
 // exclusive scan of n (device count nptr or host ncap) ints; start[n] = total
 static int rscan(lpe_ctx *ctx, RigidDev *d, const int32_t *nptr, int ncap, const int32_t *cnt,
-                 int32_t *start, int32_t *cursor) {
+                 int32_t *start, int32_t *cursor, hipStream_t s = nullptr) {
     int st = rigid_alloc_bsum(ctx, d, ncap);
     if (st) return st;
     int nb = ncap / 1024 + 1;
-    hipStream_t s = ctx->stream;
+    if (!s) s = ctx->stream;
     LPE_KERNEL(ctx, "k_rscan_reduce", k_rscan_reduce, dim3(nb), dim3(RTPB), 0, s, nptr, ncap, cnt, d->bsum);
     LPE_KERNEL(ctx, "k_rscan_blocks", k_rscan_blocks, dim3(1), dim3(RTPB), 0, s, nptr, ncap, d->bsum, start);
     LPE_KERNEL(ctx, "k_rscan_final", k_rscan_final, dim3(nb), dim3(RTPB), 0, s, nptr, ncap, cnt, d->bsum, start, cursor);
@@ -1820,87 +1864,109 @@ static int rigid_versions(lpe_ctx *ctx, RigidDev *d, const int32_t *kptr, int kc
 
 // broadphase (canonical) or upload of caller pairs, then narrowphase; syncs
 // once to size the contact list
-static int rigid_detect(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pairs_in) {
-    hipStream_t s = ctx->stream;
+// Collision detection, part 1: broadphase (or the caller's pairs) and
+// narrowphase on stream s, ending with the counts copied to hc (host) —
+// nothing here waits for the host.
+static int detect_launch(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pairs_in, hipStream_t s,
+                         int32_t *hc) {
     const lpe_rigid_config &c = d->cfg;
     int nb = d->nb;
-    for (int attempt = 0; attempt < 4; attempt++) {
-        LPE_HIP(ctx, hipMemsetAsync(d->counts, 0, sizeof(int32_t) * 7, s));   // [7]: solver fault, sticky
-        if (pairs_in) {
-            if (np_in > d->cap_pairs) {
-                int st = rigid_alloc_pairs(ctx, d, np_in + 1024);
-                if (st) return st;
-            }
-            if (np_in > 0)
-                LPE_HIP(ctx, hipMemcpyAsync(d->pairs, pairs_in, sizeof(int32_t) * 2 * np_in, hipMemcpyHostToDevice, s));
-            LPE_HIP(ctx, hipMemcpyAsync(d->counts, &np_in, sizeof(int32_t), hipMemcpyHostToDevice, s));
-        } else {
-            double lo = -c.boundaryBuffer, hi = -c.boundaryBuffer + (c.universeSize + 2 * c.boundaryBuffer);
-            LPE_KERNEL(ctx, "k_rb_prep", k_rb_prep, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->verts, lo, hi, d->aabb, d->cand);
-            LPE_HIP(ctx, hipMemsetAsync(d->pcount, 0, sizeof(int32_t) * nb, s));
-            // grid over the universe plus 1 m (bodies the boundary system lets
-            // stray further, or larger than a cell, are "special")
-            const double org = -1.0, g = d->bp_cell > 0.0 ? d->bp_cell : 1.0;
-            const long G = std::max(1L, (long)std::ceil((c.universeSize + 2.0) / g));
-            if (G * G > (1L << 26)) {
-                ctx->err = "rigid broadphase grid too large (universe / body size)";
-                return LPE_ERR_CAPACITY;
-            }
-            const int cells = (int)(G * G);
-            if (cells > d->cap_bgcells) {
-                int st0 = rgrow(ctx, &d->bgCount, (size_t)cells + 1);
-                if (!st0) st0 = rgrow(ctx, &d->bgStart, (size_t)cells + 1);
-                if (!st0) st0 = rgrow(ctx, &d->bgCursor, (size_t)cells + 1);
-                if (st0) return st0;
-                d->cap_bgcells = cells;
-            }
-            LPE_HIP(ctx, hipMemsetAsync(d->bgCount, 0, sizeof(int32_t) * cells, s));
-            LPE_HIP(ctx, hipMemsetAsync(d->counts + 10, 0, sizeof(int32_t), s));
-            LPE_KERNEL(ctx, "k_bg_key", k_bg_key, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->byRank, d->aabb, d->cand, org, g,
-                       (int)G, d->bgKey, d->bgCount, d->bgSpecial, d->counts + 10);
-            int st = rscan(ctx, d, nullptr, cells, d->bgCount, d->bgStart, d->bgCursor);
+    // [0..3], [6] (counts[4], [5] belong to the solvers / gravity; [7]: solver fault, sticky)
+    LPE_HIP(ctx, hipMemsetAsync(d->counts, 0, sizeof(int32_t) * 4, s));
+    LPE_HIP(ctx, hipMemsetAsync(d->counts + 6, 0, sizeof(int32_t), s));
+    if (pairs_in) {
+        if (np_in > d->cap_pairs) {
+            int st = rigid_alloc_pairs(ctx, d, np_in + 1024);
             if (st) return st;
-            LPE_KERNEL(ctx, "k_bg_fill", k_bg_fill, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bgKey, d->bgCursor, d->bgList);
-            LPE_KERNEL(ctx, "k_bg_pairs", k_bg_pairs, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, 0, d->byRank, d->bodies, d->aabb,
-                       c.smallParticleThreshold, (int)G, d->bgKey, d->bgStart, d->bgList, d->bgSpecial, d->counts + 10,
-                       d->pcount, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6);
-            st = rscan(ctx, d, nullptr, nb, d->pcount, d->pstart, d->pcursor);
-            if (st) return st;
-            LPE_KERNEL(ctx, "k_bg_pairs", k_bg_pairs, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, 1, d->byRank, d->bodies, d->aabb,
-                       c.smallParticleThreshold, (int)G, d->bgKey, d->bgStart, d->bgList, d->bgSpecial, d->counts + 10,
-                       d->pcount, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6);
-            LPE_KERNEL(ctx, "k_bp_sort", k_bp_sort, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->pstart, d->pairs, d->pairRankB, d->cap_pairs);
-            LPE_KERNEL(ctx, "k_bp_sort_long", k_bp_sort_long, dim3(nb), dim3(RTPB), 0, s, nb, d->pstart, d->pairs, d->pairRankB, d->cap_pairs);
-            LPE_HIP(ctx, hipMemcpyAsync(d->counts, d->pstart + nb, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
         }
-        LPE_KERNEL(ctx, "k_narrow", k_narrow, dim3(rblk(d->cap_pairs, 128)), dim3(128), 0, s, d->counts, d->cap_pairs, d->pairs, d->bodies, d->verts, d->cslots, d->ccount);
-        int st = rscan(ctx, d, d->counts, d->cap_pairs, d->ccount, d->cstart, nullptr);
+        if (np_in > 0)
+            LPE_HIP(ctx, hipMemcpyAsync(d->pairs, pairs_in, sizeof(int32_t) * 2 * np_in, hipMemcpyHostToDevice, s));
+        LPE_HIP(ctx, hipMemcpyAsync(d->counts, &np_in, sizeof(int32_t), hipMemcpyHostToDevice, s));
+    } else {
+        double lo = -c.boundaryBuffer, hi = -c.boundaryBuffer + (c.universeSize + 2 * c.boundaryBuffer);
+        LPE_KERNEL(ctx, "k_rb_prep", k_rb_prep, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->verts, lo, hi, d->aabb, d->cand);
+        LPE_HIP(ctx, hipMemsetAsync(d->pcount, 0, sizeof(int32_t) * nb, s));
+        // grid over the universe plus 1 m (bodies the boundary system lets
+        // stray further, or larger than a cell, are "special")
+        const double org = -1.0, g = d->bp_cell > 0.0 ? d->bp_cell : 1.0;
+        const long G = std::max(1L, (long)std::ceil((c.universeSize + 2.0) / g));
+        if (G * G > (1L << 26)) {
+            ctx->err = "rigid broadphase grid too large (universe / body size)";
+            return LPE_ERR_CAPACITY;
+        }
+        const int cells = (int)(G * G);
+        if (cells > d->cap_bgcells) {
+            int st0 = rgrow(ctx, &d->bgCount, (size_t)cells + 1);
+            if (!st0) st0 = rgrow(ctx, &d->bgStart, (size_t)cells + 1);
+            if (!st0) st0 = rgrow(ctx, &d->bgCursor, (size_t)cells + 1);
+            if (st0) return st0;
+            d->cap_bgcells = cells;
+        }
+        LPE_HIP(ctx, hipMemsetAsync(d->bgCount, 0, sizeof(int32_t) * cells, s));
+        LPE_HIP(ctx, hipMemsetAsync(d->counts + 10, 0, sizeof(int32_t), s));
+        LPE_KERNEL(ctx, "k_bg_key", k_bg_key, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->byRank, d->aabb, d->cand, org, g,
+                   (int)G, d->bgKey, d->bgCount, d->bgSpecial, d->counts + 10);
+        int st = rscan(ctx, d, nullptr, cells, d->bgCount, d->bgStart, d->bgCursor, s);
         if (st) return st;
+        LPE_KERNEL(ctx, "k_bg_fill", k_bg_fill, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bgKey, d->bgCursor, d->bgList);
+        LPE_KERNEL(ctx, "k_bg_pairs", k_bg_pairs, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, 0, d->byRank, d->bodies, d->aabb,
+                   c.smallParticleThreshold, (int)G, d->bgKey, d->bgStart, d->bgList, d->bgSpecial, d->counts + 10,
+                   d->pcount, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6);
+        st = rscan(ctx, d, nullptr, nb, d->pcount, d->pstart, d->pcursor, s);
+        if (st) return st;
+        LPE_KERNEL(ctx, "k_bg_pairs", k_bg_pairs, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, 1, d->byRank, d->bodies, d->aabb,
+                   c.smallParticleThreshold, (int)G, d->bgKey, d->bgStart, d->bgList, d->bgSpecial, d->counts + 10,
+                   d->pcount, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6);
+        LPE_KERNEL(ctx, "k_bp_sort", k_bp_sort, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->pstart, d->pairs, d->pairRankB, d->cap_pairs);
+        LPE_KERNEL(ctx, "k_bp_sort_long", k_bp_sort_long, dim3(nb), dim3(RTPB), 0, s, nb, d->pstart, d->pairs, d->pairRankB, d->cap_pairs);
+        LPE_HIP(ctx, hipMemcpyAsync(d->counts, d->pstart + nb, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    }
+    LPE_KERNEL(ctx, "k_narrow", k_narrow, dim3(rblk(d->cap_pairs, 128)), dim3(128), 0, s, d->counts, d->cap_pairs, d->pairs, d->bodies, d->verts, d->cslots, d->ccount);
+    int st = rscan(ctx, d, d->counts, d->cap_pairs, d->ccount, d->cstart, nullptr, s);
+    if (st) return st;
+    LPE_HIP(ctx, hipMemcpyAsync(hc, d->counts, sizeof(int32_t) * 8, hipMemcpyDeviceToHost, s));
+    return LPE_OK;
+}
+
+// Part 2, once hc has arrived: capacity checks (1: the pair buffer
+// overflowed and was grown, run part 1 again) and the contact compaction.
+static int detect_finish(lpe_ctx *ctx, RigidDev *d, hipStream_t s, const int32_t *hc, int *retry) {
+    *retry = 0;
+    int np = hc[0];
+    if (hc[7]) {
+        ctx->err = "rigid solver watchdog fired (a dataflow solve made no progress)";
+        return LPE_ERR_OVERFLOW;
+    }
+    if (hc[6] || np > d->cap_pairs) {   // pair buffer overflow: grow and redo
+        *retry = 1;
+        return rigid_alloc_pairs(ctx, d, std::max(2 * d->cap_pairs, np + 1024));
+    }
+    int32_t ncv = 0;
+    LPE_HIP(ctx, hipMemcpyAsync(&ncv, d->cstart + np, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    LPE_HIP(ctx, hipStreamSynchronize(s));
+    if (ncv > d->cap_contacts) {
+        int st = rigid_alloc_contacts(ctx, d, ncv + 4096);
+        if (st) return st;
+    }
+    LPE_HIP(ctx, hipMemcpyAsync(d->counts + 1, &ncv, sizeof(int32_t), hipMemcpyHostToDevice, s));
+    LPE_KERNEL(ctx, "k_compact", k_compact, dim3(rblk(d->cap_pairs)), dim3(RTPB), 0, s, d->counts, d->cap_pairs, d->cslots, d->ccount, d->cstart, d->contacts, d->cap_contacts);
+    LPE_CHECK_LAUNCH(ctx, "detect");
+    d->last_np = np;
+    d->last_nc = ncv;
+    return LPE_OK;
+}
+
+static int rigid_detect(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pairs_in,
+                        hipStream_t s = nullptr) {
+    if (!s) s = ctx->stream;
+    for (int attempt = 0; attempt < 4; attempt++) {
         int32_t hc[8];
-        LPE_HIP(ctx, hipMemcpyAsync(hc, d->counts, sizeof(int32_t) * 8, hipMemcpyDeviceToHost, s));
-        int32_t ncv = 0;
+        int st = detect_launch(ctx, d, np_in, pairs_in, s, hc);
+        if (st) return st;
         LPE_HIP(ctx, hipStreamSynchronize(s));
-        int np = hc[0];
-        if (hc[7]) {
-            ctx->err = "rigid solver watchdog fired (a dataflow solve made no progress)";
-            return LPE_ERR_OVERFLOW;
-        }
-        if (hc[6] || np > d->cap_pairs) {   // pair buffer overflow: grow and redo
-            st = rigid_alloc_pairs(ctx, d, std::max(2 * d->cap_pairs, np + 1024));
-            if (st) return st;
-            continue;
-        }
-        LPE_HIP(ctx, hipMemcpy(&ncv, d->cstart + np, sizeof(int32_t), hipMemcpyDeviceToHost));
-        if (ncv > d->cap_contacts) {
-            st = rigid_alloc_contacts(ctx, d, ncv + 4096);
-            if (st) return st;
-        }
-        LPE_HIP(ctx, hipMemcpyAsync(d->counts + 1, &ncv, sizeof(int32_t), hipMemcpyHostToDevice, s));
-        LPE_KERNEL(ctx, "k_compact", k_compact, dim3(rblk(d->cap_pairs)), dim3(RTPB), 0, s, d->counts, d->cap_pairs, d->cslots, d->ccount, d->cstart, d->contacts, d->cap_contacts);
-        LPE_CHECK_LAUNCH(ctx, "detect");
-        d->last_np = np;
-        d->last_nc = ncv;
-        return LPE_OK;
+        int retry = 0;
+        st = detect_finish(ctx, d, s, hc, &retry);
+        if (st || !retry) return st;
     }
     ctx->err = "rigid pair buffer kept overflowing";
     return LPE_ERR_OVERFLOW;
@@ -1909,8 +1975,28 @@ static int rigid_detect(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pai
 // colour: canonical mode (colour-major order for both solvers, see
 // k_pair_colour); otherwise pgs_order (NULL = narrowphase order) for the PGS
 // and narrowphase order for the position solver (reference-order replay)
+// the canonical colouring of the pairs (k_pair_colour) on stream s
+static int colour_launch(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
+    int nb = d->nb;
+    if (d->cap_pcol < d->cap_pairs || !d->pcol) {
+        int st0 = rgrow(ctx, &d->pcol, (size_t)d->cap_pairs);
+        if (st0) return st0;
+        st0 = rgrow(ctx, &d->cseg, (size_t)d->cap_pairs);
+        if (st0) return st0;
+        d->cap_pcol = d->cap_pairs;
+    }
+    if (!d->cbase) {
+        int st0 = rgrow(ctx, &d->cbase, (size_t)MAX_COLOURS + 1);
+        if (st0) return st0;
+    }
+    size_t lds = (2 * sizeof(unsigned long long) + 1) * (size_t)nb + 16;
+    LPE_KERNEL(ctx, "k_pair_colour", k_pair_colour, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts, d->pairs, d->ccount, d->cstart, d->bodies, d->pcol, d->order, d->cseg, d->cbase, d->counts);
+    return LPE_OK;
+}
+
+// coloured: the colouring already ran (rigid_tick_finish, side stream)
 static int rigid_solve(lpe_ctx *ctx, RigidDev *d, bool colour, const int32_t *pgs_order,
-                       lpe_rigid_stats *stats) {
+                       lpe_rigid_stats *stats, bool coloured = false) {
     hipStream_t s = ctx->stream;
     const lpe_rigid_config &c = d->cfg;
     int nb = d->nb, nc = d->last_nc;
@@ -1928,19 +2014,10 @@ static int rigid_solve(lpe_ctx *ctx, RigidDev *d, bool colour, const int32_t *pg
     }
     const int32_t *ord = nullptr;
     if (colour) {
-        if (d->cap_pcol < d->cap_pairs || !d->pcol) {
-            int st0 = rgrow(ctx, &d->pcol, (size_t)d->cap_pairs);
-            if (st0) return st0;
-            st0 = rgrow(ctx, &d->cseg, (size_t)d->cap_pairs);
-            if (st0) return st0;
-            d->cap_pcol = d->cap_pairs;
-        }
-        if (!d->cbase) {
-            int st0 = rgrow(ctx, &d->cbase, (size_t)MAX_COLOURS + 1);
+        if (!coloured) {
+            int st0 = colour_launch(ctx, d, s);
             if (st0) return st0;
         }
-        size_t lds = (2 * sizeof(unsigned long long) + 1) * (size_t)nb + 16;
-        LPE_KERNEL(ctx, "k_pair_colour", k_pair_colour, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts, d->pairs, d->ccount, d->cstart, d->bodies, d->pcol, d->order, d->cseg, d->cbase, d->counts);
         ord = d->order;
     } else if (pgs_order) {
         LPE_HIP(ctx, hipMemcpyAsync(d->order, pgs_order, sizeof(int32_t) * nc, hipMemcpyHostToDevice, s));
@@ -2024,6 +2101,71 @@ static int rigid_step_impl(lpe_ctx *ctx, int np, const int32_t *pairs, int nc_or
 
 extern "C" int lpe_rigid_step(lpe_ctx *ctx, lpe_rigid_stats *stats) {
     return rigid_step_impl(ctx, 0, nullptr, 0, nullptr, stats);
+}
+
+// World tick (lpe_world.hip): collision detection and the pair colouring of
+// RigidBodyCollisionSystem run on a side stream while the fluid step runs.
+// Their inputs (poses, shapes, flags) are final once the boundary system's
+// position clamp is applied (k_boundary_pos, at the start of the tick: the
+// fluid step and gravity write only velocities); the solvers, which need the
+// velocities, wait for the colouring on the context stream.
+int rigid_tick_begin(lpe_ctx *ctx) {
+    RigidDev *d = rdev(ctx);
+    d->overlap_pending = false;
+    if (d->nb <= 0) return LPE_OK;
+    const lpe_rigid_config &c = d->cfg;
+    if (!d->side) {
+        LPE_HIP(ctx, hipStreamCreateWithFlags(&d->side, hipStreamNonBlocking));
+        LPE_HIP(ctx, hipEventCreateWithFlags(&d->evStart, hipEventDisableTiming));
+        LPE_HIP(ctx, hipEventCreateWithFlags(&d->evDetect, hipEventDisableTiming));
+        LPE_HIP(ctx, hipEventCreateWithFlags(&d->evColour, hipEventDisableTiming));
+        LPE_HIP(ctx, hipHostMalloc((void **)&d->hc, sizeof(int32_t) * 16, 0));
+    }
+    hipStream_t s = ctx->stream;
+    LPE_KERNEL(ctx, "k_boundary_pos", k_boundary_pos, dim3(rblk(d->nb)), dim3(RTPB), 0, s, d->nb, d->bodies,
+               c.marginPixels * c.metersPerPixel, c.universeSize, d->bbits);
+    LPE_HIP(ctx, hipEventRecord(d->evStart, s));
+    LPE_HIP(ctx, hipStreamWaitEvent(d->side, d->evStart, 0));
+    int st = detect_launch(ctx, d, 0, nullptr, d->side, d->hc);
+    if (st) return st;
+    LPE_HIP(ctx, hipEventRecord(d->evDetect, d->side));
+    d->overlap_pending = true;
+    return LPE_OK;
+}
+
+// the boundary system's velocity part, at its place in the tick
+int rigid_tick_boundary(lpe_ctx *ctx) {
+    RigidDev *d = rdev(ctx);
+    if (d->nb <= 0) return LPE_OK;
+    const lpe_rigid_config &c = d->cfg;
+    LPE_KERNEL(ctx, "k_boundary_vel", k_boundary_vel, dim3(rblk(d->nb)), dim3(RTPB), 0, ctx->stream, d->nb,
+               d->bodies, d->bbits, c.bounceDamping, c.maxSpeed);
+    return LPE_OK;
+}
+
+int rigid_tick_finish(lpe_ctx *ctx) {
+    RigidDev *d = rdev(ctx);
+    if (d->nb <= 0) return LPE_OK;
+    if (!d->overlap_pending) {
+        ctx->err = "rigid_tick_finish without rigid_tick_begin";
+        return LPE_ERR_STATE;
+    }
+    d->overlap_pending = false;
+    LPE_HIP(ctx, hipEventSynchronize(d->evDetect));
+    int retry = 0;
+    int st = detect_finish(ctx, d, d->side, d->hc, &retry);
+    if (st) return st;
+    if (retry) {                     // the pair buffer grew: detect again (rare)
+        st = rigid_detect(ctx, d, 0, nullptr, d->side);
+        if (st) return st;
+    }
+    if (d->last_nc > 0) {
+        st = colour_launch(ctx, d, d->side);
+        if (st) return st;
+    }
+    LPE_HIP(ctx, hipEventRecord(d->evColour, d->side));
+    LPE_HIP(ctx, hipStreamWaitEvent(ctx->stream, d->evColour, 0));
+    return rigid_solve(ctx, d, true, nullptr, nullptr, true);
 }
 
 extern "C" int lpe_rigid_step_ordered(lpe_ctx *ctx, int np, const int32_t *pairs, int nc_order,

@@ -8,6 +8,7 @@
 // back to fp32 (fluid.cpp:283-286).  k_fluid_boundary_gravity performs exactly
 // that: widen, update in double, narrow.
 #include "lpe_internal.h"
+#include <cstdlib>
 #include "rigid_dev.h"
 #include <algorithm>
 #include <cmath>
@@ -191,15 +192,24 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
         int st = lpe_sph_cover_box(ctx, -1.0, -1.0, U + 1.0, U + 1.0);
         if (st) return st;
     }
+    // collision detection overlapped with the fluid step (LPE_SERIAL_TICK=1:
+    // everything on the context stream, in the systems' order)
+    const char *ser = std::getenv("LPE_SERIAL_TICK");
+    const bool serial = ser && std::atoi(ser) != 0;
+    const bool overlap = !serial && rd->nb > 0;
     for (int t = 0; t < nticks; t++) {
         // 1) FluidSystem::update (fluid.cpp:958-1021)
+        int nr = fluid ? d.couple_n : 0;
+        if (nr > 0) {
+            LPE_KERNEL(ctx, "k_gather_rigids", k_gather_rigids, dim3(wblk(nr, 128)), dim3(128), 0, s, nr, d.coupleBody, rd->bodies, rd->verts, d.rig);
+            d.nr = nr;
+            d.rig_dirty = true;
+        }
+        if (overlap) {          // after the gather: the fluid sees the unclamped poses
+            int st = rigid_tick_begin(ctx);
+            if (st) return st;
+        }
         if (fluid) {
-            int nr = d.couple_n;
-            if (nr > 0) {
-                LPE_KERNEL(ctx, "k_gather_rigids", k_gather_rigids, dim3(wblk(nr, 128)), dim3(128), 0, s, nr, d.coupleBody, rd->bodies, rd->verts, d.rig);
-                d.nr = nr;
-                d.rig_dirty = true;
-            }
             int st = lpe_sph_step(ctx, dt_fluid);
             if (st) return st;
             if (nr > 0)
@@ -207,7 +217,13 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
         }
         // 2) BoundarySystem, 3) BasicGravitySystem: bodies and fluid
         // (the planetary-mass check spans bodies and fluid, gravity.cpp:43-51)
-        int st = lpe_rigid_integrate(ctx, 1 | 32, dt_state, dt_move);
+        int st;
+        if (overlap) {
+            st = rigid_tick_boundary(ctx);
+            if (!st) st = lpe_rigid_integrate(ctx, 32, dt_state, dt_move);
+        } else {
+            st = lpe_rigid_integrate(ctx, 1 | 32, dt_state, dt_move);
+        }
         if (st) return st;
         if (d.n > 0) {
             LPE_KERNEL(ctx, "k_fluid_boundary_gravity", k_fluid_boundary_gravity, dim3(wblk(d.n)), dim3(256), 0, s, d.n, d.P, rc.marginPixels * rc.metersPerPixel, rc.universeSize, rc.bounceDamping, rc.maxSpeed, rc.gravity, dt_state, rd->nb > 0 ? rd->counts + 5 : (const int32_t *)nullptr, d.fluid_heavy ? 1 : 0);
@@ -215,7 +231,7 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
         st = lpe_rigid_integrate(ctx, 2, dt_state, dt_move);
         if (st) return st;
         // 4) RigidBodyCollisionSystem
-        st = lpe_rigid_step(ctx, nullptr);
+        st = overlap ? rigid_tick_finish(ctx) : lpe_rigid_step(ctx, nullptr);
         if (st) return st;
         // 5) BarnesHut (early out), 6) Rotation, 7) Movement, 8) Sleep
         st = lpe_rigid_integrate(ctx, 4 | 8 | 16, dt_state, dt_move);

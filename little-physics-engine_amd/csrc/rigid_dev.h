@@ -76,6 +76,13 @@ struct RigidDev {
     lpe_rigid_config cfg{};
     bool cfg_set = false;
     int last_np = 0, last_nc = 0;
+    // world tick: collision detection and colouring run on a side stream
+    // while the fluid step runs (rigid_tick_begin / rigid_tick_finish)
+    int32_t *bbits = nullptr;                 // per body: boundary bounce bits of the tick
+    int32_t *hc = nullptr;                    // pinned: detection counts read by the host
+    hipStream_t side = nullptr;
+    hipEvent_t evStart = nullptr, evDetect = nullptr, evColour = nullptr;
+    bool overlap_pending = false;
 };
 
 

@@ -59,3 +59,72 @@ def test_world_multi_tick(gpu_ctx, oracle_mod):
     for k in ("x", "y"):
         np.testing.assert_allclose(bodies[k], rb[k], rtol=1e-5, atol=1e-4, err_msg=k)
     assert np.isfinite(out["vx"]).all() and np.isfinite(bodies["vx"]).all()
+
+
+def _bounce_bodies(b):
+    """Bodies of small64_8 moved past the boundary margin (0.15 m) towards
+    the walls, so the boundary system clamps and reflects them in the tick."""
+    b = b.copy()
+    b["x"][4], b["vx"][4] = 0.08, -0.5          # left margin, against the left wall
+    b["y"][5], b["vy"][5] = 5.95, 0.8           # top margin
+    b["x"][6], b["vx"][6] = 5.9, 0.3            # right margin
+    return b
+
+
+def _rigid_only_run(b, v, rcfg, nticks, serial):
+    import os
+    os.environ["LPE_SERIAL_TICK"] = "1" if serial else "0"
+    try:
+        ctx = lpe.Context(0)
+        try:
+            ctx.rigid_set_config(rcfg)
+            ctx.rigid_upload(b, v)
+            ctx.world_tick(DT, nticks)
+            return ctx.rigid_download()
+        finally:
+            ctx.close()
+    finally:
+        os.environ.pop("LPE_SERIAL_TICK", None)
+
+
+def test_world_overlap_equals_serial_with_bounces():
+    """The world tick runs collision detection and colouring on a side stream
+    during the fluid step, with the boundary clamp moved to the start of the
+    tick (k_boundary_pos / k_boundary_vel); a rigid-only run (deterministic)
+    must equal the serial systems order bit for bit, bounces included."""
+    s = scenes.scene("small64_8")
+    b, v = scenes.to_bodies(s["bodies"])
+    b = _bounce_bodies(b)
+    rcfg = lpe.rigid_config(universe=s["U"])
+    a = _rigid_only_run(b, v, rcfg, 30, serial=False)
+    r = _rigid_only_run(b, v, rcfg, 30, serial=True)
+    for k in ("x", "y", "angle", "vx", "vy", "omega", "flags"):
+        np.testing.assert_array_equal(a[k], r[k], err_msg=k)
+    assert a["x"][4] >= 0.15 - 1e-12 and a["y"][5] <= 6.0 - 0.15 + 1e-12
+
+
+def test_world_one_tick_bounces(gpu_ctx, oracle_mod):
+    """One full tick with fluid, coupling and bodies inside the boundary
+    margin against the whole-tick oracle (tolerances of test_world_one_tick)."""
+    s = scenes.scene("small64_8")
+    fl = s["fluid"]
+    b, v = scenes.to_bodies(s["bodies"])
+    b = _bounce_bodies(b)
+    rcfg = lpe.rigid_config(universe=s["U"])
+    fcfg = lpe.default_fluid_config()
+    gpu_ctx.sph_set_config(fcfg)
+    gpu_ctx.rigid_set_config(rcfg)
+    gpu_ctx.rigid_upload(b, v)
+    gpu_ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+    couple = np.arange(len(b) - 1, -1, -1, dtype=np.int32)
+    gpu_ctx.world_set_coupling(couple)
+    gpu_ctx.world_tick(DT, 1)
+    out = gpu_ctx.sph_download()
+    bodies = gpu_ctx.rigid_download()
+    p, rb = oracle_mod.world_tick(fcfg, rcfg, scenes.particles_aos(fl), b, v, couple, DT, 1)
+    for k, col in (("x", 0), ("y", 1), ("vx", 2), ("vy", 3)):
+        np.testing.assert_array_equal(out[k], p[:, col], err_msg=k)
+    for k in ("x", "y", "angle"):
+        np.testing.assert_allclose(bodies[k], rb[k], rtol=1e-6, atol=1e-7, err_msg=k)
+    for k in ("vx", "vy", "omega"):
+        np.testing.assert_allclose(bodies[k], rb[k], rtol=1e-5, atol=1e-5, err_msg=k)
