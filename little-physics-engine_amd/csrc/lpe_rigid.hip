@@ -958,49 +958,91 @@ k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
     const int ncached = min(npc, segLds);                  // the first segLds segments live in LDS
     for (int q = threadIdx.x; q < ncached; q += SOLVE_TPB) ss[q] = seg[q];
     __syncthreads();
-    for (int it = 0; it < iters; it++) {
-        for (int c = 0; c < ncol; c++) {
-            const int q1 = scb[c + 1];
-            for (int q = scb[c] + threadIdx.x; q < q1; q += SOLVE_TPB) {
-                const int2 sg = q < ncached ? ss[q] : seg[q];
-                const int nrow = sg.y & 0xff, stride = sg.y >> 8;   // rows: sg.x + j * stride
-                const int2 ab = rowAB[sg.x];
-                const float4 m = rowM[sg.x];
-                const bool hasA = ab.x >= 0, hasB = ab.y >= 0;
-                float vxA = 0.f, vyA = 0.f, wA = 0.f, vxB = 0.f, vyB = 0.f, wB = 0.f;
-                if (hasA) { vxA = sv[3 * ab.x]; vyA = sv[3 * ab.x + 1]; wA = sv[3 * ab.x + 2]; }
-                if (hasB) { vxB = sv[3 * ab.y]; vyB = sv[3 * ab.y + 1]; wB = sv[3 * ab.y + 2]; }
-                // the pair's rows in batches of RB, all loads of a batch in flight together
-                for (int j0 = 0; j0 < nrow; j0 += RB) {
-                    const int nb_ = min(RB, nrow - j0);
-                    float4 n[RB], r[RB];
-                    float ln[RB], lf[RB];
+    // One item per thread and colour step is software-pipelined: the global
+    // loads of the thread's first pair of the NEXT step (segment, bodies,
+    // masses, its first PF rows and their multipliers) are issued before the
+    // current pair is solved, so they arrive during the solve and the
+    // barrier.  Row data are constant during the solve; a pair's multipliers
+    // are written only by the thread that owns it (static q -> thread map),
+    // and the next step's pair differs from the current one unless there is
+    // a single colour (then they are read at use).  Rows in canonical order,
+    // arithmetic unchanged: bit-identical to the unpipelined sweep.
+    constexpr int PF = 2;
+    struct Pf {
+        int2 sg, ab;
+        float4 m, n[PF], r[PF];
+        float ln[PF], lf[PF];
+    };
+    auto load = [&](int q, int it, bool lam, Pf &f) {
+        f.sg = q < ncached ? ss[q] : seg[q];
+        f.ab = rowAB[f.sg.x];
+        f.m = rowM[f.sg.x];
+        const int nrow = f.sg.y & 0xff, stride = f.sg.y >> 8;
 #pragma unroll
-                    for (int j = 0; j < RB; j++) {
-                        if (j < nb_) {
-                            const int t = sg.x + (j0 + j) * stride;
-                            n[j] = rowN[t]; r[j] = rowR[t];
-                            ln[j] = it ? lamN[t] : 0.f;
-                            lf[j] = it ? lamF[t] : 0.f;
-                        }
-                    }
-#pragma unroll
-                    for (int j = 0; j < RB; j++)
-                        if (j < nb_)
-                            pgs_row_regs(n[j], r[j], m.x, m.y, m.z, m.w, hasA, hasB, mu, ln[j], lf[j], vxA, vyA,
-                                         wA, vxB, vyB, wB);
-#pragma unroll
-                    for (int j = 0; j < RB; j++)
-                        if (j < nb_) {
-                            const int t = sg.x + (j0 + j) * stride;
-                            lamN[t] = ln[j]; lamF[t] = lf[j];
-                        }
-                }
-                if (hasA) { sv[3 * ab.x] = vxA; sv[3 * ab.x + 1] = vyA; sv[3 * ab.x + 2] = wA; }
-                if (hasB) { sv[3 * ab.y] = vxB; sv[3 * ab.y + 1] = vyB; sv[3 * ab.y + 2] = wB; }
+        for (int j = 0; j < PF; j++)
+            if (j < nrow) {
+                const int t = f.sg.x + j * stride;
+                f.n[j] = rowN[t]; f.r[j] = rowR[t];
+                f.ln[j] = (it && lam) ? lamN[t] : 0.f;
+                f.lf[j] = (it && lam) ? lamF[t] : 0.f;
             }
-            __syncthreads();
+    };
+    auto solve = [&](Pf &f, int it, bool lam) {
+        const int nrow = f.sg.y & 0xff, stride = f.sg.y >> 8;   // rows: sg.x + j * stride
+        const int2 ab = f.ab;
+        const float4 m = f.m;
+        const bool hasA = ab.x >= 0, hasB = ab.y >= 0;
+        float vxA = 0.f, vyA = 0.f, wA = 0.f, vxB = 0.f, vyB = 0.f, wB = 0.f;
+        if (hasA) { vxA = sv[3 * ab.x]; vyA = sv[3 * ab.x + 1]; wA = sv[3 * ab.x + 2]; }
+        if (hasB) { vxB = sv[3 * ab.y]; vyB = sv[3 * ab.y + 1]; wB = sv[3 * ab.y + 2]; }
+#pragma unroll
+        for (int j = 0; j < PF; j++)
+            if (j < nrow) {
+                const int t = f.sg.x + j * stride;
+                if (!lam && it) { f.ln[j] = lamN[t]; f.lf[j] = lamF[t]; }
+                pgs_row_regs(f.n[j], f.r[j], m.x, m.y, m.z, m.w, hasA, hasB, mu, f.ln[j], f.lf[j], vxA, vyA,
+                             wA, vxB, vyB, wB);
+                lamN[t] = f.ln[j]; lamF[t] = f.lf[j];
+            }
+        for (int j = PF; j < nrow; j++) {                     // longer pairs: on demand
+            const int t = f.sg.x + j * stride;
+            float ln = it ? lamN[t] : 0.f, lf = it ? lamF[t] : 0.f;
+            pgs_row_regs(rowN[t], rowR[t], m.x, m.y, m.z, m.w, hasA, hasB, mu, ln, lf, vxA, vyA, wA, vxB,
+                         vyB, wB);
+            lamN[t] = ln; lamF[t] = lf;
         }
+        if (hasA) { sv[3 * ab.x] = vxA; sv[3 * ab.x + 1] = vyA; sv[3 * ab.x + 2] = wA; }
+        if (hasB) { sv[3 * ab.y] = vxB; sv[3 * ab.y + 1] = vyB; sv[3 * ab.y + 2] = wB; }
+    };
+    const int total = iters * ncol;
+    const bool lamPf = ncol > 1;
+    Pf cur{}, nxt{};
+    bool hcur = false;
+    if (total > 0) {
+        const int q = scb[0] + threadIdx.x;
+        hcur = q < scb[1];
+        if (hcur) load(q, 0, lamPf, cur);
+    }
+    for (int step = 0, it = 0, c = 0; step < total; step++) {
+        int it1 = it, c1 = c + 1;
+        if (c1 == ncol) { c1 = 0; it1++; }
+        bool hnxt = false;
+        if (step + 1 < total) {
+            const int q = scb[c1] + threadIdx.x;
+            hnxt = q < scb[c1 + 1];
+            if (hnxt) load(q, it1, lamPf, nxt);
+        }
+        if (hcur) solve(cur, it, lamPf);
+        for (int q = scb[c] + threadIdx.x + SOLVE_TPB; q < scb[c + 1]; q += SOLVE_TPB) {
+            Pf f;
+            load(q, it, true, f);
+            solve(f, it, true);
+        }
+        __syncthreads();
+        cur = nxt;
+        hcur = hnxt;
+        it = it1;
+        c = c1;
     }
     for (int i = threadIdx.x; i < 3 * nb; i += SOLVE_TPB) vel[i] = sv[i];
 }
@@ -1343,41 +1385,77 @@ k_pos_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
     const int ncached = min(npc, segLds);                  // the first segLds segments live in LDS
     for (int q = threadIdx.x; q < ncached; q += SOLVE_TPB) ss[q] = seg[q];
     __syncthreads();
-    for (int it = 0; it < iters; it++) {
-        for (int c = 0; c < ncol; c++) {
-            const int q1 = scb[c + 1];
-            for (int q = scb[c] + threadIdx.x; q < q1; q += SOLVE_TPB) {
-                const int2 sg = q < ncached ? ss[q] : seg[q];
-                const int nrow = sg.y & 0xff, stride = sg.y >> 8;   // rows: sg.x + j * stride
-                const PosRec &q0 = rec[sg.x];
-                const int a = q0.a, b = q0.b;
-                const double invMA = q0.invMA, invMB = q0.invMB, invIA = q0.invIA, invIB = q0.invIB;
-                double xA = sp[3 * a], yA = sp[3 * a + 1], tA = sp[3 * a + 2];
-                double xB = sp[3 * b], yB = sp[3 * b + 1], tB = sp[3 * b + 2];
-                for (int j0 = 0; j0 < nrow; j0 += RB) {              // batches of RB rows
-                    const int nb_ = min(RB, nrow - j0);
-                    double nx[RB], ny[RB], cr[RB], px[RB], py[RB];
-                    int fl[RB];
+    // software-pipelined like k_pgs_colour: the next step's first pair
+    // (segment, bodies, masses, its first PF rows) is loaded before the
+    // current one is solved; the records are constant during the solve
+    constexpr int PF = 2;
+    struct Pf {
+        int2 sg;
+        int a, b, fl0;
+        double invMA, invMB, invIA, invIB;
+        double nx[PF], ny[PF], cr[PF], px[PF], py[PF];
+        int fl[PF];
+    };
+    auto load = [&](int q, Pf &f) {
+        f.sg = q < ncached ? ss[q] : seg[q];
+        const int nrow = f.sg.y & 0xff, stride = f.sg.y >> 8;
+        const PosRec &q0 = rec[f.sg.x];
+        f.a = q0.a; f.b = q0.b; f.fl0 = q0.flags;
+        f.invMA = q0.invMA; f.invMB = q0.invMB; f.invIA = q0.invIA; f.invIB = q0.invIB;
 #pragma unroll
-                    for (int j = 0; j < RB; j++)
-                        if (j < nb_) {
-                            const PosRec &qr = rec[sg.x + (j0 + j) * stride];
-                            nx[j] = qr.nx; ny[j] = qr.ny; cr[j] = qr.corr; px[j] = qr.px; py[j] = qr.py;
-                            fl[j] = qr.flags;
-                        }
-#pragma unroll
-                    for (int j = 0; j < RB; j++)
-                        if (j < nb_)
-                            pos_item_regs(nx[j], ny[j], cr[j], px[j], py[j], fl[j], invMA, invMB, invIA, invIB,
-                                          xA, yA, tA, xB, yB, tB);
-                }
-                // a static body (invM = 0, no rotation) is never written: pairs
-                // of one colour may share it
-                if (invMA != 0.0 || (q0.flags & 2)) { sp[3 * a] = xA; sp[3 * a + 1] = yA; sp[3 * a + 2] = tA; }
-                if (invMB != 0.0 || (q0.flags & 4)) { sp[3 * b] = xB; sp[3 * b + 1] = yB; sp[3 * b + 2] = tB; }
+        for (int j = 0; j < PF; j++)
+            if (j < nrow) {
+                const PosRec &qr = rec[f.sg.x + j * stride];
+                f.nx[j] = qr.nx; f.ny[j] = qr.ny; f.cr[j] = qr.corr; f.px[j] = qr.px; f.py[j] = qr.py;
+                f.fl[j] = qr.flags;
             }
-            __syncthreads();
+    };
+    auto solve = [&](const Pf &f) {
+        const int nrow = f.sg.y & 0xff, stride = f.sg.y >> 8;   // rows: sg.x + j * stride
+        const int a = f.a, b = f.b;
+        double xA = sp[3 * a], yA = sp[3 * a + 1], tA = sp[3 * a + 2];
+        double xB = sp[3 * b], yB = sp[3 * b + 1], tB = sp[3 * b + 2];
+#pragma unroll
+        for (int j = 0; j < PF; j++)
+            if (j < nrow)
+                pos_item_regs(f.nx[j], f.ny[j], f.cr[j], f.px[j], f.py[j], f.fl[j], f.invMA, f.invMB, f.invIA,
+                              f.invIB, xA, yA, tA, xB, yB, tB);
+        for (int j = PF; j < nrow; j++) {                     // longer pairs: on demand
+            const PosRec &qr = rec[f.sg.x + j * stride];
+            pos_item_regs(qr.nx, qr.ny, qr.corr, qr.px, qr.py, qr.flags, f.invMA, f.invMB, f.invIA, f.invIB,
+                          xA, yA, tA, xB, yB, tB);
         }
+        // a static body (invM = 0, no rotation) is never written: pairs
+        // of one colour may share it
+        if (f.invMA != 0.0 || (f.fl0 & 2)) { sp[3 * a] = xA; sp[3 * a + 1] = yA; sp[3 * a + 2] = tA; }
+        if (f.invMB != 0.0 || (f.fl0 & 4)) { sp[3 * b] = xB; sp[3 * b + 1] = yB; sp[3 * b + 2] = tB; }
+    };
+    const int total = iters * ncol;
+    Pf cur{}, nxt{};
+    bool hcur = false;
+    if (total > 0) {
+        const int q = scb[0] + threadIdx.x;
+        hcur = q < scb[1];
+        if (hcur) load(q, cur);
+    }
+    for (int step = 0, c = 0; step < total; step++) {
+        int c1 = c + 1 == ncol ? 0 : c + 1;
+        bool hnxt = false;
+        if (step + 1 < total) {
+            const int q = scb[c1] + threadIdx.x;
+            hnxt = q < scb[c1 + 1];
+            if (hnxt) load(q, nxt);
+        }
+        if (hcur) solve(cur);
+        for (int q = scb[c] + threadIdx.x + SOLVE_TPB; q < scb[c + 1]; q += SOLVE_TPB) {
+            Pf f;
+            load(q, f);
+            solve(f);
+        }
+        __syncthreads();
+        cur = nxt;
+        hcur = hnxt;
+        c = c1;
     }
     // storeBodyData (:176-197)
     for (int i = threadIdx.x; i < nb; i += SOLVE_TPB) {
