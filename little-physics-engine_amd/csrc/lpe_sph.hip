@@ -646,7 +646,10 @@ struct SphStepParams {
 
 // computeForces + velocityVerletFinish + impulse + push-out; reads the sorted
 // records, writes P
-__global__ void __launch_bounds__(TPB)
+#ifndef LPE_FORCES_MINW
+#define LPE_FORCES_MINW 1
+#endif
+__global__ void __launch_bounds__(TPB, LPE_FORCES_MINW)
 k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict__ gp,
                 const int32_t *__restrict__ start, PState S, const float4 *__restrict__ nbA,
                 const float4 *__restrict__ nbB, const float *__restrict__ pr,

@@ -13,7 +13,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "liblpe_hip.so")
+LIB_PATH = os.environ.get("LPE_LIB") or os.path.join(HERE, "liblpe_hip.so")   # LPE_LIB: an alternative build (A/B runs)
 
 LPE_OK = 0
 STATUS = {0: "OK", 1: "ERR_HIP", 2: "ERR_ARG", 3: "ERR_STATE", 4: "ERR_CAPACITY",
