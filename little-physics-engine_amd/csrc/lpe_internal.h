@@ -78,6 +78,12 @@ struct SphDev {
     lpe_fluid_config cfg{};
     bool cfg_set = false;
     bool rig_dirty = true;
+    // world tick: sub-step 0's kick/hash/density of the next tick, launched on
+    // a side stream while the rigid solvers run (sph_prelaunch)
+    hipStream_t pside = nullptr;
+    hipEvent_t preReady = nullptr, preDone = nullptr;
+    bool pre = false;
+    double pre_dt = 0.0;
     int diag = 0;                 // count the ST_NL_OVERFLOW / ST_RIGID_CAND / ST_NEIGH stats
     struct Shard *shard = nullptr;// x-slab decomposition state (lpe_sph_set_slab), else single domain
 };
@@ -179,6 +185,7 @@ int lpe_rigid_destroy_internal(lpe_ctx *ctx);
 int rigid_tick_begin(lpe_ctx *ctx);
 int rigid_tick_boundary(lpe_ctx *ctx);
 int rigid_tick_finish(lpe_ctx *ctx);
+int sph_prelaunch(lpe_ctx *ctx, double dt_tick);
 int lpe_sph_cover_box(lpe_ctx *ctx, double x0, double y0, double x1, double y1);
 // sort the CURRENT particle positions into the bins (no integration): the
 // state of lpe_sph_probe_* and of the renderer's density grid

@@ -892,19 +892,25 @@ k_pair_colour(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict_
 // solveLcpPgs (contact_solver.cpp:381-440), rows of buildConstraintRows
 // (:133-197) in fp32, body velocities in LDS.
 // one contact row (normal, then friction) on the pair's velocities in registers
+typedef float pk2 __attribute__((ext_vector_type(2)));
+// The x/y halves of the row are computed as packed fp32 pairs (v_pk_mul_f32 /
+// v_pk_add_f32: each lane of a packed op is the IEEE scalar op, unfused), so
+// the results are the scalar code's bit for bit with fewer VALU issues.
 __device__ __forceinline__ void pgs_row_regs(float4 rn, float4 rr, float imA, float iiA, float imB,
                                              float iiB, bool hasA, bool hasB, float mu, float &ln,
                                              float &lf, float &vxA, float &vyA, float &wA, float &vxB,
                                              float &vyB, float &wB) {
+    pk2 vA = {vxA, vyA}, vB = {vxB, vyB};
+    const pk2 lA = {-rr.y, rr.x}, lB = {-rr.w, rr.z};
 #pragma unroll
     for (int row = 0; row < 2; row++) {
-        float dX = row == 0 ? rn.x : -rn.y;
-        float dY = row == 0 ? rn.y : rn.x;
+        const pk2 d = row == 0 ? pk2{rn.x, rn.y} : pk2{-rn.y, rn.x};
         float eff = row == 0 ? rn.z : rn.w;
-        float ax = vxA - wA * rr.y, ay = vyA + wA * rr.x;
-        float bx = vxB - wB * rr.w, by = vyB + wB * rr.z;
-        float relX = bx - ax, relY = by - ay;
-        float vrel = relX * dX + relY * dY;
+        // a = vA + wA * (-rA.y, rA.x): x - w*ry == x + w*(-ry) exactly
+        const pk2 a = vA + lA * wA, b = vB + lB * wB;
+        const pk2 rel = b - a;
+        const pk2 pr = rel * d;
+        float vrel = pr.x + pr.y;
         float old, lo, hi;
         if (row == 0) { old = ln; lo = 0.0f; hi = 1e20f; }
         else {
@@ -920,18 +926,17 @@ __device__ __forceinline__ void pgs_row_regs(float4 rn, float4 rr, float imA, fl
         if (row == 0) ln = nl; else lf = nl;
         if (fabsf(dl) < 1e-15F) continue;
         if (hasA) {
-            vxA -= dX * (dl * imA);
-            vyA -= dY * (dl * imA);
-            float crossA = rr.x * dY - rr.y * dX;
+            vA -= d * (dl * imA);
+            float crossA = rr.x * d.y - rr.y * d.x;
             wA -= crossA * dl * iiA;
         }
         if (hasB) {
-            vxB += dX * (dl * imB);
-            vyB += dY * (dl * imB);
-            float crossB = rr.z * dY - rr.w * dX;
+            vB += d * (dl * imB);
+            float crossB = rr.z * d.y - rr.w * d.x;
             wB += crossB * dl * iiB;
         }
     }
+    vxA = vA.x; vyA = vA.y; vxB = vB.x; vyB = vB.y;
 }
 
 // A colour step is latency-bound (one workgroup; a pair's rows are a chain),

@@ -1086,6 +1086,10 @@ static void sph_free(SphDev &d) {
                     d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.raabb, d.accum, d.rbinStart, d.rgrid, d.rmax,
                     d.rbinList, d.rbinCount, d.coupleBody};
     for (void *p : ptrs) if (p) (void)hipFree(p);
+    if (d.pside) (void)hipStreamSynchronize(d.pside);
+    hipEvent_t evs[] = {d.preReady, d.preDone};
+    for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
+    if (d.pside) (void)hipStreamDestroy(d.pside);
     d = SphDev();
 }
 
@@ -1605,6 +1609,49 @@ static int sph_migrate(lpe_ctx *ctx) {
     return LPE_OK;
 }
 
+// World tick (lpe_world.hip): sub-step 0's kick-drift, grid hash and density
+// of the NEXT tick read only the fluid state, which is final once this tick's
+// fluid boundary/gravity kernel has run; they are launched on a side stream
+// then, so they run while the rigid solvers (one CU) run, and that tick's
+// lpe_sph_step starts at the forces (single domain; the slab path's exchanges
+// stay on the context stream).
+static constexpr int PRE_FREE_CUS = 16;
+int sph_prelaunch(lpe_ctx *ctx, double dt_tick) {
+    SphDev &d = ctx->sph;
+    d.pre = false;
+    if (d.shard || d.n <= 0 || !d.P.x) return LPE_OK;
+    if (!d.pside) {
+        // the side stream leaves a few CUs out of its mask: the solvers on
+        // the context stream are one workgroup that needs a whole CU's LDS,
+        // and would otherwise wait for the density blocks to drain
+        hipDeviceProp_t prop;
+        LPE_HIP(ctx, hipGetDeviceProperties(&prop, ctx->device));
+        const int ncu = prop.multiProcessorCount;
+        const int keep = std::max(1, ncu - PRE_FREE_CUS);
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int i = 0; i < keep; i++) mask[i / 32] |= 1u << (i % 32);
+        LPE_HIP(ctx, hipExtStreamCreateWithCUMask(&d.pside, (uint32_t)mask.size(), mask.data()));
+        LPE_HIP(ctx, hipEventCreateWithFlags(&d.preReady, hipEventDisableTiming));
+        LPE_HIP(ctx, hipEventCreateWithFlags(&d.preDone, hipEventDisableTiming));
+    }
+    LPE_HIP(ctx, hipEventRecord(d.preReady, ctx->stream));
+    LPE_HIP(ctx, hipStreamWaitEvent(d.pside, d.preReady, 0));
+    const lpe_fluid_config &c = d.cfg;
+    const float subDt = (float)dt_tick / (float)c.numSubSteps;
+    const float halfDt = 0.5f * subDt;
+    hipStream_t main = ctx->stream;
+    ctx->stream = d.pside;                       // the hash / density helpers launch on ctx->stream
+    int st = hipMemsetAsync(d.status + ST_MAX_OCC, 0, sizeof(int32_t), d.pside) == hipSuccess ? LPE_OK : LPE_ERR_HIP;
+    if (!st) st = sph_hash(ctx, subDt, halfDt, true, false);
+    if (!st) st = sph_density(ctx, d.n, nullptr);
+    if (!st && hipEventRecord(d.preDone, d.pside) != hipSuccess) st = LPE_ERR_HIP;
+    ctx->stream = main;
+    if (st) return st;
+    d.pre = true;
+    d.pre_dt = dt_tick;
+    return LPE_OK;
+}
+
 extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
     if (!ctx) return LPE_ERR_ARG;
     SphDev &d = ctx->sph;
@@ -1616,9 +1663,16 @@ extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
     float subDt = dt / (float)c.numSubSteps;         // fluid.cpp:593
     float halfDt = 0.5f * subDt;
     hipStream_t s = ctx->stream;
+    // sub-step 0 up to the forces already launched (sph_prelaunch)?
+    const bool pre = d.pre && !d.shard;
+    d.pre = false;
+    if (pre && d.pre_dt != dt_tick) {
+        ctx->err = "lpe_sph_step: the prelaunched sub-step was for another time step";
+        return LPE_ERR_STATE;
+    }
     int st = sph_build_rigid_bins(ctx);
     if (st) return st;
-    LPE_HIP(ctx, hipMemsetAsync(d.status + ST_MAX_OCC, 0, sizeof(int32_t), s));
+    if (!pre) LPE_HIP(ctx, hipMemsetAsync(d.status + ST_MAX_OCC, 0, sizeof(int32_t), s));
     SphStepParams sp;
     sp.n = d.n; sp.W = d.W; sp.H = d.H; sp.ox = d.ox; sp.oy = d.oy;
     sp.h = c.gridConfig.smoothingLength; sp.eps = c.gridConfig.gridEpsilon;
@@ -1656,6 +1710,8 @@ extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
             st = sph_density(ctx, sp.n, sh->ntot);
             if (st) return st;
             st = sph_owned_map(ctx);
+        } else if (step == 0 && pre) {
+            st = hipStreamWaitEvent(s, d.preDone, 0) == hipSuccess ? LPE_OK : LPE_ERR_HIP;
         } else {
             st = sph_hash(ctx, subDt, halfDt, step == 0, false);
             if (st) return st;

@@ -197,6 +197,7 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
     const char *ser = std::getenv("LPE_SERIAL_TICK");
     const bool serial = ser && std::atoi(ser) != 0;
     const bool overlap = !serial && rd->nb > 0;
+    d.pre = false;              // a prelaunch left by a failed call is void
     for (int t = 0; t < nticks; t++) {
         // 1) FluidSystem::update (fluid.cpp:958-1021)
         int nr = fluid ? d.couple_n : 0;
@@ -230,6 +231,12 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
         }
         st = lpe_rigid_integrate(ctx, 2, dt_state, dt_move);
         if (st) return st;
+        // the fluid state is final for this tick: the next tick's first
+        // sub-step (up to its forces) runs beside the rigid solvers
+        if (!serial && fluid && !d.shard && t + 1 < nticks) {
+            st = sph_prelaunch(ctx, dt_fluid);
+            if (st) return st;
+        }
         // 4) RigidBodyCollisionSystem
         st = overlap ? rigid_tick_finish(ctx) : lpe_rigid_step(ctx, nullptr);
         if (st) return st;
