@@ -61,7 +61,8 @@ struct SphDev {
     // rigid coupling
     int nr = 0, cap_nr = 0;
     lpe_gpu_rigid *rig = nullptr;
-    float *accum = nullptr;       // [3R] running + [3R] last tick
+    float *accum = nullptr;       // [3R] the last tick's accumulators (rounded, before the write-back)
+    unsigned long long *acq = nullptr;  // [3R][XACC_LIMBS] exact running sums (sph_coupling.h)
     int32_t *rbinStart = nullptr; // rigid bins (absolute grid of bin size bcs)
     int32_t *rbinList = nullptr;
     int32_t *rbinCount = nullptr;
@@ -100,6 +101,7 @@ enum StatusSlot {
     ST_STAGE_FALLBACK = 7,  // staged density blocks whose neighbourhood did not fit LDS
     ST_HALO_OVERFLOW = 8,   // slab decomposition: a ghost / migrant buffer overflowed
     ST_HALO_DRIFT = 9,      // slab decomposition: an owned particle beyond the halo's reach
+    ST_XACC_RANGE = 10,     // a rigid coupling force outside the exact accumulator's range (|f| >= 2^64)
     ST_COUNT = 16
 };
 
@@ -187,6 +189,8 @@ int rigid_tick_boundary(lpe_ctx *ctx);
 int rigid_tick_finish(lpe_ctx *ctx);
 int sph_prelaunch(lpe_ctx *ctx, double dt_tick);
 int lpe_sph_cover_box(lpe_ctx *ctx, double x0, double y0, double x1, double y1);
+// coupling rigids' device arrays (rig, accum, acq) for n rigids (grow-only)
+int sph_alloc_rigids(lpe_ctx *ctx, int n);
 // sort the CURRENT particle positions into the bins (no integration): the
 // state of lpe_sph_probe_* and of the renderer's density grid
 int lpe_sph_hash_current(lpe_ctx *ctx);

@@ -38,9 +38,10 @@
 //
 // Numerics: fp32, no FMA contraction (-ffp-contract=off), correctly rounded
 // division and sqrt, tanh/pow via fp64 rounded once; with the canonical orders
-// above the fluid state is bit-identical to the oracle.  Only the rigid
-// accumulators use float atomics (order-dependent in the last bits, as the
-// reference's own atomics, metal:892-898).
+// above the fluid state is bit-identical to the oracle.  The rigid
+// accumulators (float atomics in the reference, metal:892-898) are exact
+// fixed-point sums rounded once (sph_coupling.h): deterministic, and equal
+// to the oracle's bit for bit.
 #include "lpe_internal.h"
 #include "sph_coupling.h"
 #include "lpe_transport.h"
@@ -656,7 +657,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                 const uint4 *__restrict__ nlist, const int32_t *__restrict__ ncount, PState P,
                 const lpe_gpu_rigid *__restrict__ rig, const float4 *__restrict__ raabb,
                 const int32_t *__restrict__ rbinStart, const int32_t *__restrict__ rbinList,
-                float *__restrict__ accum,
+                unsigned long long *__restrict__ acq,
                 int32_t *__restrict__ status) {
     int lb = xcd_block((sp.n + TPB - 1) / TPB);
     int s = lb * TPB + threadIdx.x;
@@ -756,7 +757,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         if (sp.diag && k1 > k0) atomicAdd(&status[ST_RIGID_CAND], k1 - k0);
     }
     // impulse solver: dispatched only if R > 0 (fluid.cpp:910); push-out always
-    couple_both(st, cp, sp.dt, cp.nr > 0, rig, raabb, rbinList, k0, k1, accum);
+    couple_both(st, cp, sp.dt, cp.nr > 0, rig, raabb, rbinList, k0, k1, acq, status);
     P.x[out] = st.x; P.y[out] = st.y;
     P.vx[out] = st.vx; P.vy[out] = st.vy;
     P.vhx[out] = st.vhx; P.vhy[out] = st.vhy;
@@ -1000,14 +1001,17 @@ __global__ void k_rbin_sort(int B, int32_t *__restrict__ start, int32_t *__restr
     }
 }
 
-// writeBackRigidBodies arithmetic (fluid.cpp:545-562), once per tick
+// writeBackRigidBodies arithmetic (fluid.cpp:545-562), once per tick: the
+// exact sums rounded to fp32 (kept in accum_out for download), then zeroed
 __global__ void k_rigid_writeback(int nr, lpe_gpu_rigid *__restrict__ rig,
-                                  float *__restrict__ accum, float *__restrict__ accum_out,
+                                  unsigned long long *__restrict__ acq, float *__restrict__ accum_out,
                                   float damping) {
     int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nr) return;
     lpe_gpu_rigid &rb = rig[r];
-    float fx = accum[3 * r], fy = accum[3 * r + 1], tq = accum[3 * r + 2];
+    unsigned long long *a = acq + (size_t)r * (3 * XACC_LIMBS);
+    const float fx = xacc_round(a), fy = xacc_round(a + XACC_LIMBS), tq = xacc_round(a + 2 * XACC_LIMBS);
+    for (int k = 0; k < 3 * XACC_LIMBS; k++) a[k] = 0ull;
     accum_out[3 * r] = fx; accum_out[3 * r + 1] = fy; accum_out[3 * r + 2] = tq;
     float invMass = (rb.mass > 1e-12f) ? (1.f / rb.mass) : 0.f;
     float invInertia = (rb.inertia > 1e-12f) ? (1.f / rb.inertia) : 0.f;
@@ -1018,7 +1022,6 @@ __global__ void k_rigid_writeback(int nr, lpe_gpu_rigid *__restrict__ rig,
     rb.omega += tq * invInertia;
     rb.omega *= damping;
     rb.accumFx = 0.f; rb.accumFy = 0.f; rb.accumTorque = 0.f;
-    accum[3 * r] = 0.f; accum[3 * r + 1] = 0.f; accum[3 * r + 2] = 0.f;
 }
 
 // reference cell index (metal:224-236) of each particle, written at its id
@@ -1083,7 +1086,7 @@ static void sph_free(SphDev &d) {
     pstate_free(d.P);
     pstate_free(d.S);
     void *ptrs[] = {d.rho, d.pr, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.count, d.start, d.cursor,
-                    d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.raabb, d.accum, d.rbinStart, d.rgrid, d.rmax,
+                    d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.raabb, d.accum, d.acq, d.rbinStart, d.rgrid, d.rmax,
                     d.rbinList, d.rbinCount, d.coupleBody};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     if (d.pside) (void)hipStreamSynchronize(d.pside);
@@ -1358,24 +1361,36 @@ extern "C" int lpe_sph_upload(lpe_ctx *ctx, int n, const float *x, const float *
     return LPE_OK;
 }
 
+int sph_alloc_rigids(lpe_ctx *ctx, int n) {
+    SphDev &d = ctx->sph;
+    if (n <= d.cap_nr && d.rig) return LPE_OK;
+    const size_t R = (size_t)std::max(n, 1);
+    void *ptrs[] = {d.rig, d.accum, d.acq};
+    for (void *p : ptrs) if (p) (void)hipFree(p);
+    d.rig = nullptr; d.accum = nullptr; d.acq = nullptr;
+    LPE_HIP(ctx, hipMalloc((void **)&d.rig, sizeof(lpe_gpu_rigid) * R));
+    LPE_HIP(ctx, hipMalloc((void **)&d.accum, sizeof(float) * 3 * R));
+    LPE_HIP(ctx, hipMalloc((void **)&d.acq, sizeof(unsigned long long) * 3 * XACC_LIMBS * R));
+    LPE_HIP(ctx, hipMemsetAsync(d.accum, 0, sizeof(float) * 3 * R, ctx->stream));
+    LPE_HIP(ctx, hipMemsetAsync(d.acq, 0, sizeof(unsigned long long) * 3 * XACC_LIMBS * R, ctx->stream));
+    d.cap_nr = (int)R;
+    return LPE_OK;
+}
+
 extern "C" int lpe_sph_upload_rigids(lpe_ctx *ctx, int r, const lpe_gpu_rigid *rigids) {
     if (!ctx || r < 0 || (r > 0 && !rigids)) return LPE_ERR_ARG;
     (void)hipSetDevice(ctx->device);
     SphDev &d = ctx->sph;
-    if (r > d.cap_nr || !d.rig) {
-        if (d.rig) (void)hipFree(d.rig);
-        if (d.accum) (void)hipFree(d.accum);
-        LPE_HIP(ctx, hipMalloc((void **)&d.rig, sizeof(lpe_gpu_rigid) * (size_t)std::max(r, 1)));
-        LPE_HIP(ctx, hipMalloc((void **)&d.accum, sizeof(float) * 6 * (size_t)std::max(r, 1)));
-        d.cap_nr = std::max(r, 1);
-    }
+    int st = sph_alloc_rigids(ctx, r);
+    if (st) return st;
     d.nr = r;
     if (r > 0) {
         std::vector<lpe_gpu_rigid> tmp(rigids, rigids + r);
         for (auto &b : tmp) b.accumFx = b.accumFy = b.accumTorque = 0.f;
         LPE_HIP(ctx, hipMemcpyAsync(d.rig, tmp.data(), sizeof(lpe_gpu_rigid) * r,
                                     hipMemcpyHostToDevice, ctx->stream));
-        LPE_HIP(ctx, hipMemsetAsync(d.accum, 0, sizeof(float) * 6 * r, ctx->stream));
+        LPE_HIP(ctx, hipMemsetAsync(d.accum, 0, sizeof(float) * 3 * r, ctx->stream));
+        LPE_HIP(ctx, hipMemsetAsync(d.acq, 0, sizeof(unsigned long long) * 3 * XACC_LIMBS * r, ctx->stream));
         LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
     }
     d.rig_dirty = true;
@@ -1720,19 +1735,20 @@ extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
         if (st) return st;
         LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(xcd_grid(nblk(sp.n))), dim3(TPB), 0, s, sp, cp, d.gp,
                            d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart, d.rbinList,
-                           d.accum, d.status);
+                           d.acq, d.status);
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
     }
     if (d.nr > 0) {
         // slab decomposition: every rank holds its particles' share of the
         // fluid->rigid impulses; the rigids are replicated, so the shares are
-        // summed (fixed rank order) before the write-back (fluid.cpp:545-562)
+        // summed before the write-back (fluid.cpp:545-562): the exact limbs
+        // add as int64, so the result is the single domain's bit for bit
         if (sh) {
-            st = ctx->transport->allreduce(ctx, d.accum, 3 * d.nr, 0);
+            st = ctx->transport->allreduce_i64(ctx, (long long *)d.acq, 3 * XACC_LIMBS * d.nr);
             if (st) return st;
         }
         LPE_KERNEL(ctx, "k_rigid_writeback", k_rigid_writeback, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig,
-                           d.accum, d.accum + 3 * d.nr, c.dampingFactor);
+                           d.acq, d.accum, c.dampingFactor);
         LPE_CHECK_LAUNCH(ctx, "k_rigid_writeback");
     }
     if (sh) return sph_migrate(ctx);
@@ -1774,6 +1790,10 @@ static int check_status(lpe_ctx *ctx) {
     if (status[ST_HALO_DRIFT]) {
         ctx->err = "slab decomposition: a particle moved further outside its slab than halo - 2h allows "
                    "(raise the halo of lpe_sph_set_slab)";
+        return LPE_ERR_OVERFLOW;
+    }
+    if (status[ST_XACC_RANGE]) {
+        ctx->err = "a rigid coupling force left the exact accumulator's range (|f| >= 2^64 or not finite)";
         return LPE_ERR_OVERFLOW;
     }
     if (status[ST_HALO_OVERFLOW]) {
@@ -1819,7 +1839,7 @@ extern "C" int lpe_sph_download_rigids(lpe_ctx *ctx, lpe_gpu_rigid *rigids, floa
             LPE_HIP(ctx, hipMemcpyAsync(rigids, d.rig, sizeof(lpe_gpu_rigid) * d.nr,
                                         hipMemcpyDeviceToHost, s));
         if (accum)
-            LPE_HIP(ctx, hipMemcpyAsync(accum, d.accum + 3 * d.nr, sizeof(float) * 3 * d.nr,
+            LPE_HIP(ctx, hipMemcpyAsync(accum, d.accum, sizeof(float) * 3 * d.nr,
                                         hipMemcpyDeviceToHost, s));
     }
     LPE_HIP(ctx, hipStreamSynchronize(s));

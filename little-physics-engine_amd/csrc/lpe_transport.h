@@ -21,6 +21,9 @@ struct Transport {
                      size_t bytes) = 0;
     // in-place all-reduce of n floats on the device; op 0 = sum, 1 = min
     virtual int allreduce(lpe_ctx *ctx, float *buf, int n, int op) = 0;
+    // in-place SUM all-reduce of n int64 on the device (exact: the rigid
+    // accumulators' fixed-point limbs)
+    virtual int allreduce_i64(lpe_ctx *ctx, long long *buf, int n) = 0;
 };
 
 Transport *transport_rccl(lpe_ctx *ctx, int nranks, int rank, const char *id, std::string &err);

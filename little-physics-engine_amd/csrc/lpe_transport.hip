@@ -22,16 +22,28 @@ struct RcclTransport : Transport {
     int halo(lpe_ctx *ctx, const void *sendL, const void *sendR, void *recvL, void *recvR,
              size_t bytes) override {
         if (ncclGroupStart() != ncclSuccess) return LPE_ERR_HIP;
+        ncclResult_t r = ncclSuccess;
+        auto keep = [&r](ncclResult_t x) { if (r == ncclSuccess) r = x; };
         if (sendL && recvL && rank > 0) {
-            ncclSend(sendL, bytes, ncclChar, rank - 1, comm, ctx->stream);
-            ncclRecv(recvL, bytes, ncclChar, rank - 1, comm, ctx->stream);
+            keep(ncclSend(sendL, bytes, ncclChar, rank - 1, comm, ctx->stream));
+            keep(ncclRecv(recvL, bytes, ncclChar, rank - 1, comm, ctx->stream));
         }
         if (sendR && recvR && rank < nranks - 1) {
-            ncclSend(sendR, bytes, ncclChar, rank + 1, comm, ctx->stream);
-            ncclRecv(recvR, bytes, ncclChar, rank + 1, comm, ctx->stream);
+            keep(ncclSend(sendR, bytes, ncclChar, rank + 1, comm, ctx->stream));
+            keep(ncclRecv(recvR, bytes, ncclChar, rank + 1, comm, ctx->stream));
         }
-        if (ncclGroupEnd() != ncclSuccess) {
-            ctx->err = "RCCL halo exchange failed";
+        const ncclResult_t e = ncclGroupEnd();     // always closes the group
+        if (r != ncclSuccess || e != ncclSuccess) {
+            ctx->err = std::string("RCCL halo exchange failed: ") +
+                       ncclGetErrorString(r != ncclSuccess ? r : e);
+            return LPE_ERR_HIP;
+        }
+        return LPE_OK;
+    }
+    int allreduce_i64(lpe_ctx *ctx, long long *buf, int n) override {
+        if (nranks == 1 || n <= 0) return LPE_OK;
+        if (ncclAllReduce(buf, buf, (size_t)n, ncclInt64, ncclSum, comm, ctx->stream) != ncclSuccess) {
+            ctx->err = "RCCL all-reduce (int64) failed";
             return LPE_ERR_HIP;
         }
         return LPE_OK;
@@ -87,6 +99,7 @@ struct LoopGroup {
     bool abort = false;          // a rank failed: every barrier returns at once
     std::vector<const void *> pL, pR;
     std::vector<std::vector<float>> red;
+    std::vector<std::vector<long long>> redi;
     bool barrier() {
         std::unique_lock<std::mutex> lk(mu);
         if (abort) return false;
@@ -147,6 +160,26 @@ struct LoopTransport : Transport {
             return LPE_ERR_HIP;
         return LPE_OK;
     }
+    int allreduce_i64(lpe_ctx *ctx, long long *buf, int n) override {
+        if (nranks == 1 || n <= 0) return LPE_OK;
+        std::vector<long long> &mine = g->redi[rank];
+        mine.resize(n);
+        if (hipMemcpyAsync(mine.data(), buf, sizeof(long long) * n, hipMemcpyDeviceToHost, ctx->stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess)
+            return LPE_ERR_HIP;
+        if (!g->barrier()) return LPE_ERR_STATE;
+        std::vector<long long> acc(g->redi[0]);
+        for (int r = 1; r < nranks; r++)
+            for (int i = 0; i < n; i++)     // two's complement wrap-around, as the device limbs
+                acc[i] = (long long)((unsigned long long)acc[i] + (unsigned long long)g->redi[r][i]);
+        if (!g->barrier()) return LPE_ERR_STATE;
+        if (hipMemcpyAsync(buf, acc.data(), sizeof(long long) * n, hipMemcpyHostToDevice, ctx->stream) !=
+                hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess)
+            return LPE_ERR_HIP;
+        return LPE_OK;
+    }
 };
 
 }  // namespace lpe
@@ -176,6 +209,7 @@ extern "C" int lpe_mg_loopback_run(int n, lpe_ctx **ctxs, const lpe_world_config
     g.pL.assign(n, nullptr);
     g.pR.assign(n, nullptr);
     g.red.resize(n);
+    g.redi.resize(n);
     std::vector<Transport *> saved(n);
     for (int r = 0; r < n; r++) {
         auto *t = new LoopTransport();

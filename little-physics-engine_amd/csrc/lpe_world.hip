@@ -10,6 +10,7 @@
 #include "lpe_internal.h"
 #include <cstdlib>
 #include "rigid_dev.h"
+#include "sph_coupling.h"
 #include <algorithm>
 #include <cmath>
 #include <vector>
@@ -122,16 +123,12 @@ extern "C" int lpe_world_set_coupling(lpe_ctx *ctx, int nr, const int32_t *body_
         LPE_HIP(ctx, hipMalloc((void **)&d.coupleBody, sizeof(int32_t) * std::max(n, 1)));
         d.cap_couple = n;
     }
-    if (n > d.cap_nr || !d.rig) {
-        if (d.rig) (void)hipFree(d.rig);
-        if (d.accum) (void)hipFree(d.accum);
-        LPE_HIP(ctx, hipMalloc((void **)&d.rig, sizeof(lpe_gpu_rigid) * (size_t)std::max(n, 1)));
-        LPE_HIP(ctx, hipMalloc((void **)&d.accum, sizeof(float) * 6 * (size_t)std::max(n, 1)));
-        d.cap_nr = std::max(n, 1);
-    }
+    int st0 = sph_alloc_rigids(ctx, n);
+    if (st0) return st0;
     if (n > 0) {
         LPE_HIP(ctx, hipMemcpyAsync(d.coupleBody, idx.data(), sizeof(int32_t) * n, hipMemcpyHostToDevice, ctx->stream));
-        LPE_HIP(ctx, hipMemsetAsync(d.accum, 0, sizeof(float) * 6 * n, ctx->stream));
+        LPE_HIP(ctx, hipMemsetAsync(d.accum, 0, sizeof(float) * 3 * n, ctx->stream));
+        LPE_HIP(ctx, hipMemsetAsync(d.acq, 0, sizeof(unsigned long long) * 3 * XACC_LIMBS * n, ctx->stream));
     }
     d.couple_n = n;
     // bin-list capacity bound without a host sync per tick: bodies that cannot

@@ -73,12 +73,75 @@ struct CoupleState {
     float x, y, vx, vy, vhx, vhy, ax, ay, mass, rho, p;
 };
 
+// ---------------------------------------------------------------------------
+// Rigid accumulators (accumFx, accumFy, accumTorque).  The reference adds the
+// per-particle forces with float atomics (metal:892-898), in no defined
+// order.  Here every accumulator is an EXACT fixed-point sum: 8 limbs of 32
+// bits (held in 64-bit words, so carries can wait) covering 2^-160 .. 2^96,
+// i.e. every fp32 value below 2^64 (denormals included) lands exactly; after
+// the sub-steps the sum is rounded once, to nearest even, to fp32.  The
+// result is the correctly rounded sum, which every order of float additions
+// approximates: independent of thread scheduling, of the sort order, and of
+// how the particles are split over slab ranks (the limbs all-reduce exactly
+// as int64).  oracle/sph_oracle.c restates the same arithmetic.
+static constexpr int XACC_LIMBS = 8;      // limb k holds bits [32k, 32k + 32) of the value * 2^160
+static constexpr int XACC_BIAS = 160;
+
+__device__ __forceinline__ void xacc_add(unsigned long long *__restrict__ acc, float f,
+                                         int32_t *__restrict__ status, int range_slot) {
+    const uint32_t u = __float_as_uint(f);
+    const uint32_t e = (u >> 23) & 0xffu, m = u & 0x7fffffu;
+    if (e == 0u && m == 0u) return;                              // +-0
+    if (e >= 127u + 64u) { atomicOr(&status[range_slot], 1); return; }   // |f| >= 2^64, inf, nan
+    const uint32_t M = e ? (m | 0x800000u) : m;
+    const int pos = (e ? (int)e - 150 : -149) + XACC_BIAS;     // bit index of M's lsb, >= 11
+    const unsigned long long v = (unsigned long long)M << (pos & 31);
+    unsigned long long lo = v & 0xffffffffull, hi = v >> 32;
+    if (u >> 31) { lo = 0ull - lo; hi = 0ull - hi; }             // two's complement limbs
+    if (lo) atomicAdd(&acc[pos >> 5], lo);
+    if (hi) atomicAdd(&acc[(pos >> 5) + 1], hi);
+}
+
+// The exact sum rounded to nearest even.
+__host__ __device__ __forceinline__ float xacc_round(const unsigned long long *acc) {
+    uint32_t d[XACC_LIMBS];
+    long long carry = 0;
+    for (int i = 0; i < XACC_LIMBS; i++) {
+        const long long t = (long long)acc[i] + carry;
+        d[i] = (uint32_t)((unsigned long long)t & 0xffffffffull);
+        carry = t >> 32;                                         // floor division
+    }
+    const bool neg = carry < 0;
+    if (neg) {                                                   // magnitude of the 256-bit value
+        unsigned long long c = 1;
+        for (int i = 0; i < XACC_LIMBS; i++) {
+            const unsigned long long t = (unsigned long long)(uint32_t)~d[i] + c;
+            d[i] = (uint32_t)t;
+            c = t >> 32;
+        }
+    }
+    int b = -1;
+    for (int i = XACC_LIMBS - 1; i >= 0 && b < 0; i--)
+        if (d[i]) b = i * 32 + 31 - __builtin_clz(d[i]);
+    if (b < 0) return 0.0f;
+    const int p = b - 23 > 11 ? b - 23 : 11;                      // lsb kept; bit 11 is 2^-149
+    uint32_t kept = 0;
+    for (int k = b; k >= p; k--) kept = (kept << 1) | ((d[k >> 5] >> (k & 31)) & 1u);
+    const uint32_t guard = (d[(p - 1) >> 5] >> ((p - 1) & 31)) & 1u;
+    bool sticky = false;
+    for (int k = 0; k < p - 1; k++) sticky |= ((d[k >> 5] >> (k & 31)) & 1u) != 0u;
+    if (guard && (sticky || (kept & 1u))) kept++;
+    const float r = ldexpf((float)kept, p - XACC_BIAS);          // exact
+    return neg ? -r : r;
+}
+
 // One rigid's contribution to the impulse solver (metal:792-900), given the
 // penetration, lever arm and normal of the particle inside it.
 __device__ __forceinline__ void impulse_term(const CoupleState &st, const CoupleParams &cp, float dt,
                                              const lpe_gpu_rigid &rb, int r, float pen, float relx,
                                              float rely, float nx, float ny, float densityF,
-                                             float pressureF, float *__restrict__ accum, float &tffx,
+                                             float pressureF, unsigned long long *__restrict__ acq,
+                                             int32_t *__restrict__ status, float &tffx,
                                              float &tffy, bool &had) {
     had = true;
     const float py = st.y;
@@ -124,9 +187,10 @@ __device__ __forceinline__ void impulse_term(const CoupleState &st, const Couple
         float sgn = (rb.omega > 0.f) ? 1.f : ((rb.omega < 0.f) ? -1.f : 0.f);
         torque -= cp.angDampFactor * sgn * fabsf(rb.omega) * rb.inertia;
     }
-    atomicAdd(&accum[3 * r + 0], tfx);
-    atomicAdd(&accum[3 * r + 1], tfy);
-    atomicAdd(&accum[3 * r + 2], torque);
+    unsigned long long *a = acq + (size_t)r * (3 * XACC_LIMBS);
+    xacc_add(a, tfx, status, ST_XACC_RANGE);
+    xacc_add(a + XACC_LIMBS, tfy, status, ST_XACC_RANGE);
+    xacc_add(a + 2 * XACC_LIMBS, torque, status, ST_XACC_RANGE);
     tffx -= tfx * cp.fluidForceScale;
     tffy -= tfy * cp.fluidForceScale;
 }
@@ -175,7 +239,8 @@ __device__ __forceinline__ void couple_both(CoupleState &st, const CoupleParams 
                                            const lpe_gpu_rigid *__restrict__ rig,
                                            const float4 *__restrict__ aabb,
                                            const int32_t *__restrict__ list, int k0, int k1,
-                                           float *__restrict__ accum) {
+                                           unsigned long long *__restrict__ acq,
+                                           int32_t *__restrict__ status) {
     // impulse solver state (metal:679-924)
     const float densityF = st.rho > 0.0f ? st.rho : cp.restDensity;
     const float pressureF = st.p;
@@ -203,7 +268,7 @@ __device__ __forceinline__ void couple_both(CoupleState &st, const CoupleParams 
                 if (pen < 0.0f) pen = 0.0f;
                 if (!(pen < cp.minPenetration))
                     impulse_term(st, cp, dt, rb, r, pen, rx, ry, rx / dist, ry / dist, densityF, pressureF,
-                                 accum, tffx, tffy, had);
+                                 acq, status, tffx, tffy, had);
             }
             hadCollision = true;
             float dist = dist0, dx = rx, dy = ry;
@@ -225,7 +290,7 @@ __device__ __forceinline__ void couple_both(CoupleState &st, const CoupleParams 
                 if (pen < 0.0f) pen = 0.0f;
                 if (!(pen < cp.minPenetration))
                     impulse_term(st, cp, dt, rb, r, pen, px - rb.posX, py - rb.posY, dx / d, dy / d, densityF,
-                                 pressureF, accum, tffx, tffy, had);
+                                 pressureF, acq, status, tffx, tffy, had);
             }
             hadCollision = true;
             float d = d0, cdx = dx, cdy = dy;

@@ -96,6 +96,16 @@ def density(p, cfg=None):
     return p[:, 11].copy(), p[:, 12].copy(), g, st
 
 
+def xacc_sum(values):
+    """Exact sum of float32 values rounded once to nearest even (the rigid
+    coupling accumulators' arithmetic, sph_oracle.c xacc_*)."""
+    v = np.ascontiguousarray(values, np.float32)
+    f = lib().lpeo_xacc_sum
+    f.argtypes = [_FP, C.c_int]
+    f.restype = C.c_float
+    return np.float32(f(v.ctypes.data_as(_FP), len(v)))
+
+
 def fluid_tick(p, rigids, dt_tick, cfg=None):
     """FluidSystem::update minus the ECS: returns (particles, rigids, accum, stats)."""
     cfg = cfg or default_config()

@@ -12,8 +12,10 @@
  * reference's non-deterministic orders replaced by canonical ones:
  *   - grid cell lists: ascending particle index (the reference inserts in
  *     atomic arrival order, fluid_kernels.metal:237);
- *   - rigid accumulators: ascending particle index (reference: float atomics,
- *     fluid_kernels.metal:892-898).
+ *   - rigid accumulators (reference: float atomics, fluid_kernels.metal:
+ *     892-898, no defined order): the exact sum of the fp32 contributions,
+ *     rounded once to nearest even (xacc_* below) -- the order-independent
+ *     value that every sequence of float additions approximates.
  * Arithmetic is IEEE fp32 with no FMA contraction (build with
  * -ffp-contract=off); the reference compiles Metal with fast-math, which has
  * no single defined result.
@@ -96,6 +98,70 @@ static float f2len(float x, float y) { return sqrtf(x * x + y * y); }
  * rounded fp32 result except in ~2^-29 of cases. */
 static float lpe_tanhf(float x) { return (float)tanh((double)x); }
 static float lpe_powf(float x, float e) { return (float)pow((double)x, (double)e); }
+
+/* Exact accumulation of the rigid coupling forces.  A sum is 8 limbs of 32
+ * bits (int64 containers, carries deferred) of the value * 2^160: every fp32
+ * below 2^64 in magnitude, denormals included, is added exactly; the total is
+ * rounded once to nearest even.  Independent restatement of the device's
+ * xacc_add / xacc_round (little-physics-engine_amd/csrc/sph_coupling.h). */
+#define XACC_LIMBS 8
+#define XACC_BIAS 160
+static int xacc_range_error = 0;
+
+static void xacc_add(uint64_t *acc, float f) {
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    uint32_t e = (u >> 23) & 0xffu, m = u & 0x7fffffu;
+    if (e == 0 && m == 0) return;
+    if (e >= 127u + 64u) { xacc_range_error = 1; return; }
+    uint32_t M = e ? (m | 0x800000u) : m;
+    int pos = (e ? (int)e - 150 : -149) + XACC_BIAS;
+    uint64_t v = (uint64_t)M << (pos & 31);
+    uint64_t lo = v & 0xffffffffull, hi = v >> 32;
+    if (u >> 31) { lo = 0ull - lo; hi = 0ull - hi; }
+    acc[pos >> 5] += lo;
+    acc[(pos >> 5) + 1] += hi;
+}
+
+static float xacc_round(const uint64_t *acc) {
+    uint32_t d[XACC_LIMBS];
+    int64_t carry = 0;
+    for (int i = 0; i < XACC_LIMBS; i++) {
+        int64_t t = (int64_t)acc[i] + carry;
+        d[i] = (uint32_t)((uint64_t)t & 0xffffffffull);
+        carry = (t - (int64_t)d[i]) / 4294967296LL;      /* exact: t - low is a multiple of 2^32 */
+    }
+    int neg = carry < 0;
+    if (neg) {
+        uint64_t c = 1;
+        for (int i = 0; i < XACC_LIMBS; i++) {
+            uint64_t t = (uint64_t)(uint32_t)~d[i] + c;
+            d[i] = (uint32_t)t;
+            c = t >> 32;
+        }
+    }
+    int b = -1;
+    for (int i = XACC_LIMBS - 1; i >= 0 && b < 0; i--)
+        if (d[i]) for (int k = 31; k >= 0; k--) if ((d[i] >> k) & 1u) { b = i * 32 + k; break; }
+    if (b < 0) return 0.0f;
+    int p = b - 23 > 11 ? b - 23 : 11;
+    uint32_t kept = 0;
+    for (int k = b; k >= p; k--) kept = (kept << 1) | ((d[k >> 5] >> (k & 31)) & 1u);
+    uint32_t guard = (d[(p - 1) >> 5] >> ((p - 1) & 31)) & 1u;
+    int sticky = 0;
+    for (int k = 0; k < p - 1; k++) sticky |= (int)((d[k >> 5] >> (k & 31)) & 1u);
+    if (guard && (sticky || (kept & 1u))) kept++;
+    float r = ldexpf((float)kept, p - XACC_BIAS);
+    return neg ? -r : r;
+}
+
+/* Test hook: the exact, once-rounded sum of n floats (-1e30f on a range error). */
+float lpeo_xacc_sum(const float *v, int n) {
+    uint64_t acc[XACC_LIMBS] = {0};
+    xacc_range_error = 0;
+    for (int i = 0; i < n; i++) xacc_add(acc, v[i]);
+    return xacc_range_error ? -1e30f : xacc_round(acc);
+}
 
 /* Grid of the reference: fluid.cpp:717-752 (host, fp32). */
 void lpeo_grid_from_bbox(const lpeo_particle *p, int n, float smoothingLength,
@@ -288,10 +354,9 @@ static void forces_one(const lpeo_particle *p, int n, int i, const lpeo_grid *g,
 }
 
 /* rigidFluidImpulseSolver (fluid_kernels.metal:679-924) for particle i;
- * rigid accumulators are summed in ascending particle order by the caller's
- * loop order (canonical for the reference's float atomics). */
-static void impulse_one(lpeo_particle *fpp, lpe_gpu_rigid *rigids, int rigidCount,
-                        const lpe_fluid_config *cfg, float dt) {
+ * the rigid accumulators are exact sums (xacc, 3 x XACC_LIMBS per rigid). */
+static void impulse_one(lpeo_particle *fpp, const lpe_gpu_rigid *rigids, int rigidCount,
+                        const lpe_fluid_config *cfg, float dt, uint64_t *acq) {
     const float GRAVITY = cfg->gravity;
     const float WATER_DENSITY = cfg->restDensity;
     const float MAX_FORCE = cfg->impulseSolver.maxForce;
@@ -317,7 +382,7 @@ static void impulse_one(lpeo_particle *fpp, lpe_gpu_rigid *rigids, int rigidCoun
     float tffx = 0.0f, tffy = 0.0f;
     int hadInteraction = 0;
     for (int r = 0; r < rigidCount; r++) {
-        lpe_gpu_rigid *rb = &rigids[r];
+        const lpe_gpu_rigid *rb = &rigids[r];
         float rbVelSq = rb->vx * rb->vx + rb->vy * rb->vy + rb->omega * rb->omega;
         if (rbVelSq > MAX_SAFE_VELOCITY_SQ) continue;
         if (fp.x < rb->minX || fp.x > rb->maxX || fp.y < rb->minY || fp.y > rb->maxY) continue;
@@ -395,9 +460,9 @@ static void impulse_one(lpeo_particle *fpp, lpe_gpu_rigid *rigids, int rigidCoun
             float sgn = (rb->omega > 0.f) ? 1.f : ((rb->omega < 0.f) ? -1.f : 0.f);
             torque -= ANGULAR_DAMPING_FACTOR * sgn * fabsf(rb->omega) * rb->inertia;
         }
-        rb->accumFx += tfx;
-        rb->accumFy += tfy;
-        rb->accumTorque += torque;
+        xacc_add(acq + (size_t)r * 3 * XACC_LIMBS, tfx);
+        xacc_add(acq + (size_t)r * 3 * XACC_LIMBS + XACC_LIMBS, tfy);
+        xacc_add(acq + (size_t)r * 3 * XACC_LIMBS + 2 * XACC_LIMBS, torque);
         tffx -= tfx * FLUID_FORCE_SCALE;
         tffy -= tfy * FLUID_FORCE_SCALE;
     }
@@ -523,6 +588,8 @@ int lpeo_fluid_tick(const lpe_fluid_config *cfg, double dt_tick,
     float *ay = (float *)malloc(sizeof(float) * (size_t)n);
     float *rho = (float *)malloc(sizeof(float) * (size_t)n);
     float *pr = (float *)malloc(sizeof(float) * (size_t)n);
+    uint64_t *acq = (uint64_t *)calloc((size_t)(nr > 0 ? nr : 1) * 3 * XACC_LIMBS, sizeof(uint64_t));
+    xacc_range_error = 0;
     for (int step = 0; step < cfg->numSubSteps; step++) {
         /* velocityVerletHalf (fluid_kernels.metal:408-423) */
         for (int i = 0; i < n; i++) {
@@ -550,13 +617,16 @@ int lpeo_fluid_tick(const lpe_fluid_config *cfg, double dt_tick,
             p[i].vy = p[i].vyHalf + halfDt * p[i].ay;
         }
         if (nr > 0)
-            for (int i = 0; i < n; i++) impulse_one(&p[i], rigids, nr, cfg, subDt);
+            for (int i = 0; i < n; i++) impulse_one(&p[i], rigids, nr, cfg, subDt, acq);
         for (int i = 0; i < n; i++) position_one(&p[i], rigids, nr, cfg);
         free_cells(&cl);
     }
     /* writeBackRigidBodies arithmetic (fluid.cpp:545-562) */
     for (int r = 0; r < nr; r++) {
         lpe_gpu_rigid *rb = &rigids[r];
+        rb->accumFx = xacc_round(acq + (size_t)r * 3 * XACC_LIMBS);
+        rb->accumFy = xacc_round(acq + (size_t)r * 3 * XACC_LIMBS + XACC_LIMBS);
+        rb->accumTorque = xacc_round(acq + (size_t)r * 3 * XACC_LIMBS + 2 * XACC_LIMBS);
         if (accum_out) {
             accum_out[3 * r + 0] = rb->accumFx;
             accum_out[3 * r + 1] = rb->accumFy;
@@ -572,8 +642,8 @@ int lpeo_fluid_tick(const lpe_fluid_config *cfg, double dt_tick,
         rb->omega *= cfg->dampingFactor;
         rb->accumFx = rb->accumFy = rb->accumTorque = 0.f;
     }
-    free(ax); free(ay); free(rho); free(pr);
-    return 0;
+    free(ax); free(ay); free(rho); free(pr); free(acq);
+    return xacc_range_error ? 2 : 0;
 }
 
 void lpeo_fluid_config_default(lpe_fluid_config *c) {

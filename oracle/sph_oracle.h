@@ -36,6 +36,10 @@ int lpeo_fluid_tick(const lpe_fluid_config *cfg, double dt_tick,
                     lpeo_particle *p, int n, lpe_gpu_rigid *rigids, int nr,
                     float *accum_out, lpeo_tick_stats *st);
 
+/* Exact sum of n floats rounded once to nearest even (the coupling
+ * accumulators' arithmetic); -1e30f if a value is outside the range. */
+float lpeo_xacc_sum(const float *v, int n);
+
 #ifdef __cplusplus
 }
 #endif

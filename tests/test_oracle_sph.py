@@ -134,3 +134,51 @@ def test_tick_invariants(oracle_mod):
     assert (out[:, 0] >= 0).all() and (out[:, 1] >= 0).all()   # push-out clamp
     # walls have mass 1e30 -> write-back v += F * 1e-30 keeps them ~at rest
     assert np.abs(rout["vx"][:4]).max() < 1e-20
+
+
+def _round_f32_exact(fr):
+    """Nearest float32 to the rational fr, ties to even (independent of the
+    oracle: candidates around float64(fr), compared exactly)."""
+    from fractions import Fraction
+    c = np.float32(float(fr))
+    best = None
+    for cand in (np.nextafter(c, f32(-np.inf)), c, np.nextafter(c, f32(np.inf))):
+        err = abs(Fraction(float(cand)) - fr)
+        key = (err, int(np.frombuffer(np.float32(cand).tobytes(), np.uint32)[0]) & 1)
+        if best is None or key < best[0]:
+            best = (key, cand)
+    return f32(best[1])
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_xacc_sum_is_correctly_rounded(oracle_mod, seed):
+    """The rigid accumulators' exact sum (sph_oracle.c xacc_*): equal to the
+    correctly rounded rational sum, for mixed signs, magnitudes from
+    denormals to 1e6, and massive cancellation; order does not matter."""
+    from fractions import Fraction
+    rng = np.random.default_rng(seed)
+    n = 2000
+    mag = 10.0 ** rng.uniform(-44, 6, n)
+    v = (rng.choice([-1.0, 1.0], n) * mag).astype(np.float32)
+    v[:10] = np.array([1e-45, -1e-45, 3e-39, 0.15, -0.15, 0.1, 1e6, -1e6, 0.0, -0.0], np.float32)
+    exact = sum((Fraction(float(x)) for x in v), Fraction(0))
+    want = _round_f32_exact(exact)
+    got = oracle_mod.xacc_sum(v)
+    assert got == want, (got, want)
+    assert oracle_mod.xacc_sum(v[::-1]) == got
+    assert oracle_mod.xacc_sum(rng.permutation(v)) == got
+
+
+def test_xacc_sum_cancellation_and_ties(oracle_mod):
+    one = f32(1.0)
+    eps = np.float32(2.0 ** -24)
+    # 1 + 2^-24 is a tie between 1 and 1 + 2^-23: rounds to even (1.0)
+    assert oracle_mod.xacc_sum(np.array([one, eps], np.float32)) == one
+    # 1 + 2^-24 + 2^-40 is above the tie: rounds up
+    assert oracle_mod.xacc_sum(np.array([one, eps, 2.0 ** -40], np.float32)) == np.nextafter(one, f32(2))
+    # huge cancellation leaves the tiny term exactly
+    v = np.array([1e6, 3e-30, -1e6], np.float32)
+    assert oracle_mod.xacc_sum(v) == f32(3e-30)
+    assert oracle_mod.xacc_sum(np.array([-0.5, -0.25], np.float32)) == f32(-0.75)
+    assert oracle_mod.xacc_sum(np.zeros(0, np.float32)) == f32(0)
+    assert oracle_mod.xacc_sum(np.array([2.0 ** 64], np.float32)) == f32(-1e30)   # range error

@@ -7,10 +7,9 @@ copies for the halo, host reductions in rank order); the RCCL transport
 differs only in how the same buffers move.  Ghosts carry global ids and the
 reference grid comes from the all-reduced bbox, so without rigid contact the
 merged state is bit-identical to the single-domain run, tick after tick.
-With rigid coupling the fluid is bit-identical in the first tick (rigids are
-frozen during the sub-steps); the rigid accumulators are float atomics
-summed per rank and then across ranks, so they match to summation-order
-ulps (the same bar as the single-domain coupled test)."""
+With rigid coupling too: the rigid accumulators are exact fixed-point sums
+whose limbs are all-reduced as int64, so the split over ranks cannot change a
+bit, and full world ticks stay bit-identical to the single domain.""" 
 import numpy as np
 import pytest
 
@@ -107,12 +106,9 @@ def test_slab_coupled_first_tick():
     for k in slab.FIELDS:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
     for r_out, acc in rigs:                   # every rank holds the summed result
-        for j in range(3):
-            tot = np.abs(aref[:, j]).max()
-            np.testing.assert_allclose(acc[:, j], aref[:, j], rtol=1e-5, atol=1e-6 * tot + 1e-12)
+        np.testing.assert_array_equal(acc, aref)
         for k in ("vx", "vy", "omega"):
-            np.testing.assert_allclose(r_out[k], rref[k], rtol=1e-5, atol=1e-6, err_msg=k)
-    np.testing.assert_array_equal(rigs[0][0]["vx"], rigs[1][0]["vx"])
+            np.testing.assert_array_equal(r_out[k], rref[k], err_msg=k)
 
 
 def test_slab_halo_overflow_reported():
@@ -139,12 +135,11 @@ def _world_rank(ctx, r, n, s, edges):
 
 def test_slab_world_tick_replicated_rigids():
     """Full resident ticks (lpe_world_tick) with the fluid in 2 slabs and the
-    rigid pass replicated: tick 1's fluid is bit-identical to the single
-    domain, the rigid replicas stay identical to each other, and after 3
-    ticks both agree with the single domain at the coupled-test tolerance."""
+    rigid pass replicated: fluid and bodies bit-identical to the single domain
+    after 1 and 5 ticks, the rigid replicas identical to each other."""
     s = scenes.scene("small96_12")
     n_glob = len(s["fluid"]["x"])
-    for nt in (1, 3):
+    for nt in (1, 5):
         one = lpe.Context(0)
         try:
             _world_rank(one, 0, 1, s, None)
@@ -166,13 +161,10 @@ def test_slab_world_tick_replicated_rigids():
                 c.close()
         for k in ("x", "y", "vx", "vy", "angle", "omega"):
             np.testing.assert_array_equal(rbs[0][k], rbs[1][k], err_msg=k)
-        if nt == 1:
-            for k in slab.FIELDS:
-                np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
-        for k in ("x", "y"):
-            ok = np.isclose(got[k], ref[k], rtol=1e-5, atol=1e-5)
-            assert ok.mean() > 0.99, (nt, k, ok.mean())
-            np.testing.assert_allclose(rbs[0][k], rb_ref[k], rtol=1e-5, atol=1e-4, err_msg=k)
+        for k in slab.FIELDS:
+            np.testing.assert_array_equal(got[k], ref[k], err_msg=(nt, k))
+        for k in ("x", "y", "angle", "vx", "vy", "omega"):
+            np.testing.assert_array_equal(rbs[0][k], rb_ref[k], err_msg=(nt, k))
 
 
 def test_rccl_transport_single_rank():

@@ -1,11 +1,11 @@
 """GPU parity of the SPH path (HIP, through the C ABI) against the CPU oracle.
 
 Bar (BASELINE.json north_star): bit-exact reference grid-cell indices; fp32
-state within 1e-5 relative.  Without rigid contact the HIP path is expected to
-be bit-identical to oracle/sph_oracle.c (same canonical orders, no FMA
-contraction, correctly rounded div/sqrt); with rigid coupling the device
-tanhf/powf and the float-atomic rigid accumulators allow ulp-level drift, so
-those cases use the 1e-5 relative bar (scaled by the field's magnitude).
+state within 1e-5 relative.  The HIP path is in fact held to bit-identity with
+oracle/sph_oracle.c (same canonical orders, no FMA contraction, correctly
+rounded div/sqrt, tanh/pow via fp64 rounded once), the rigid accumulators
+included: both sides sum the fluid->rigid forces exactly and round once
+(sph_coupling.h xacc_*; the reference's float atomics have no defined order).
 """
 import numpy as np
 import pytest
@@ -93,9 +93,8 @@ def lpe_max_per_cell():
 @pytest.mark.parametrize("name", ["small64_8", "small96_12"])
 def test_tick_coupled(gpu_ctx, oracle_mod, name):
     """One tick with pentagons sinking into the fluid: impulse + push-out.
-    The fluid state is bit-identical (canonical orders, fp64-rounded tanh/pow);
-    the rigid accumulators are float atomics on the GPU (the reference uses
-    float atomics too, metal:892-898), so they match to summation-order ulps."""
+    The fluid state, the rigid accumulators (exact sums rounded once) and the
+    written-back rigid velocities are bit-identical to the oracle."""
     s = scenes.scene(name)
     rig = scenes.gather_rigids(s["bodies"])
     _upload(gpu_ctx, s["fluid"], rig)
@@ -107,11 +106,33 @@ def test_tick_coupled(gpu_ctx, oracle_mod, name):
     for k, col in (("x", 0), ("y", 1), ("vx", 2), ("vy", 3), ("vxHalf", 4), ("vyHalf", 5),
                    ("ax", 6), ("ay", 7), ("density", 11), ("pressure", 12)):
         np.testing.assert_array_equal(out[k], ref[:, col], err_msg=k)
-    for j in range(3):
-        tot = np.abs(racc[:, j]).max()
-        np.testing.assert_allclose(acc[:, j], racc[:, j], rtol=1e-5, atol=1e-6 * tot + 1e-12)
+    np.testing.assert_array_equal(acc, racc)
     for k in ("vx", "vy", "omega"):
-        np.testing.assert_allclose(r_out[k], rref[k], rtol=1e-5, atol=1e-6, err_msg=k)
+        np.testing.assert_array_equal(r_out[k], rref[k], err_msg=k)
+
+
+def test_tick_coupled_deterministic(oracle_mod):
+    """Two runs of several coupled ticks give the same bits (no float atomics
+    left on the path: the accumulators are exact sums)."""
+    s = scenes.scene("small96_12")
+    rig = scenes.gather_rigids(s["bodies"])
+    outs = []
+    for _ in range(2):
+        ctx = lpe.Context(0)
+        try:
+            _upload(ctx, s["fluid"], rig)
+            for _ in range(4):
+                ctx.sph_step(DT)
+            out = ctx.sph_download()
+            r_out, acc = ctx.sph_download_rigids()
+            outs.append((out, r_out, acc))
+        finally:
+            ctx.close()
+    (a, ra, aa), (b, rb, ab) = outs
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    np.testing.assert_array_equal(aa, ab)
+    np.testing.assert_array_equal(ra.view(np.uint8), rb.view(np.uint8))
 
 
 def test_multi_tick_invariants(gpu_ctx):
