@@ -10,7 +10,7 @@ HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -ffp-contract=off \
             -Wall -Wno-unused-function
 CC       ?= gcc
 CXX      ?= g++
-OFLAGS   := -O2 -fPIC -ffp-contract=off -Wall
+OFLAGS   := -O2 -fPIC -ffp-contract=off -Wall -fopenmp
 
 HIP_SRC  := $(wildcard $(PKG)/csrc/*.hip)
 HIP_HDR  := $(wildcard $(PKG)/csrc/*.h) include/lpe.h
@@ -39,7 +39,7 @@ build/oracle/%.opp: oracle/%.cpp oracle/*.h include/lpe.h
 	$(CXX) -std=c++17 $(OFLAGS) -c $< -o $@
 
 $(ORACLE): $(patsubst oracle/%.c,build/oracle/%.o,$(ORC_SRC)) $(patsubst oracle/%.cpp,build/oracle/%.opp,$(ORX_SRC))
-	$(CXX) -shared -fPIC -o $@ $^ -lm
+	$(CXX) -shared -fPIC -fopenmp -o $@ $^ -lm
 
 # C++ host mirror of the reference's system plugins (Systems::FluidSystem,
 # RigidBodyCollisionSystem, the integrator systems) over the C ABI.  It is the

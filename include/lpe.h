@@ -133,6 +133,13 @@ typedef struct lpe_sph_stats {
     int32_t neighbours;         /* neighbours with r < h found by the density pass */
     int32_t stageFallback;      /* blocks of the LDS-staged density pass (lpe_sph_probe_density)
                                    whose neighbourhood did not fit LDS (always counted) */
+    /* reference cells holding more than LPE_REF_MAX_PER_CELL particles,
+     * summed over the sub-steps of the last lpe_sph_step (any mode): where
+     * this is non-zero the reference drops inserts and reads across cells */
+    int32_t overCapCells;
+    /* LPE_SPH_MODE_REF_CELL_CAP read past the last cell of the grid (the
+     * reference reads stale or out-of-bounds memory there: undefined) */
+    int32_t refUndefined;
 } lpe_sph_stats;
 
 /* ------------------------------------------------------------------------ */
@@ -277,6 +284,22 @@ int  lpe_sph_download_rigids(lpe_ctx *ctx, lpe_gpu_rigid *rigids, float *accum);
 int  lpe_sph_get_stats(lpe_ctx *ctx, lpe_sph_stats *stats);
 /* Diagnostics counters of lpe_sph_stats on (1, counters reset) or off (0). */
 int  lpe_sph_diag(lpe_ctx *ctx, int on);
+
+/* SPH modes (flags, default 0).
+ * LPE_SPH_MODE_REF_CELL_CAP: the reference's fixed-capacity grid semantics.
+ *   Its GPUGridCell holds a count and 64 indices (GPU_MAX_PER_CELL,
+ *   fluid.hpp:56); assignCells keeps incrementing count past 64 but stores no
+ *   more indices (fluid_kernels.metal:237-240), and computeDensity /
+ *   computeForces loop c < count unclamped (:281-283, :349-351), reading the
+ *   next cells' count and indices as particle ids (values >= N skipped).  In
+ *   this mode the device reproduces exactly that, with the canonical
+ *   insertion order (cell quadrants row-major, ascending particle index) in
+ *   place of the reference's atomic order; where no cell exceeds 64 it equals
+ *   the default mode bit for bit.  Default (0): unbounded cell lists (the
+ *   counting sort has no capacity), i.e. the reference's intent.  Not
+ *   available on a slab rank (LPE_ERR_STATE). */
+#define LPE_SPH_MODE_REF_CELL_CAP 1
+int  lpe_sph_set_mode(lpe_ctx *ctx, int flags);
 
 /* Parity probe: the reference's assignCells cell index for each particle
  * (fluid_kernels.metal:212-241: cellY*gridDimX + cellX, or -1 if "not

@@ -36,6 +36,7 @@ struct SphDev {
     PState P;                     // primary state (sorted order of the last sub-step)
     PState S;                     // permutation target of the current sub-step
     float *rho = nullptr, *pr = nullptr;  // in S/P slot order
+    float *rhoN = nullptr, *prN = nullptr;// the prelaunched sub-step's (swapped in when it is consumed)
     float4 *nbA = nullptr;        // sorted neighbour records (x, y, m, -)
     float4 *nbB = nullptr;        // (vx, vy, rho, p / rho^2)
     uint4 *nlist = nullptr;       // per-slot neighbour list k - s (int16, 8 per uint4), [cap/8][cap_n]
@@ -56,8 +57,11 @@ struct SphDev {
     // absolute device grid: origin (cells) and dims, fixed per upload
     int ox = 0, oy = 0, W = 0, H = 0;
     float cs = 0.1f;
-    GridParams *gp = nullptr;     // device copy of the reference grid
-    int32_t *status = nullptr;    // [16] flags / stats
+    GridParams *gp = nullptr;     // device copy of the reference grid; [1]: the prelaunched sub-step's
+    int32_t *status = nullptr;    // [ST_COUNT] flags / stats; [ST_COUNT..2 ST_COUNT): the prelaunch's
+    GridParams *gp_cur = nullptr; // where the hash / density launches write (gp, or gp + 1 in sph_prelaunch)
+    int32_t *stat_cur = nullptr;  // likewise status / status + ST_COUNT
+    float *stage = nullptr;       // download staging (with S.x, S.y, S.vx, S.vy, S.m)
     // rigid coupling
     int nr = 0, cap_nr = 0;
     lpe_gpu_rigid *rig = nullptr;
@@ -80,12 +84,17 @@ struct SphDev {
     bool cfg_set = false;
     bool rig_dirty = true;
     // world tick: sub-step 0's kick/hash/density of the next tick, launched on
-    // a side stream while the rigid solvers run (sph_prelaunch)
+    // a side stream while the rigid solvers run (sph_prelaunch).  It writes
+    // only scratch (kicked state, bins, sorted records, gp[1], status[1]),
+    // never P, so it can be voided at any time (sph_void_prelaunch) and may
+    // outlive the lpe_world_tick call that launched it
     hipStream_t pside = nullptr;
     hipEvent_t preReady = nullptr, preDone = nullptr;
     bool pre = false;
     double pre_dt = 0.0;
     int diag = 0;                 // count the ST_NL_OVERFLOW / ST_RIGID_CAND / ST_NEIGH stats
+    int mode = 0;                 // LPE_SPH_MODE_* (lpe_sph_set_mode)
+    int32_t *refInv = nullptr;    // reference cell-capacity mode: sorted slot of each particle id
     struct Shard *shard = nullptr;// x-slab decomposition state (lpe_sph_set_slab), else single domain
 };
 
@@ -102,6 +111,8 @@ enum StatusSlot {
     ST_HALO_OVERFLOW = 8,   // slab decomposition: a ghost / migrant buffer overflowed
     ST_HALO_DRIFT = 9,      // slab decomposition: an owned particle beyond the halo's reach
     ST_XACC_RANGE = 10,     // a rigid coupling force outside the exact accumulator's range (|f| >= 2^64)
+    ST_OVER_CAP = 11,       // reference cells over GPU_MAX_PER_CELL, summed over the tick's sub-steps
+    ST_REF_UB = 12,         // reference cell-capacity mode read past the last cell (undefined in the reference)
     ST_COUNT = 16
 };
 

@@ -96,11 +96,19 @@ __device__ __forceinline__ int wave_runs(uint32_t k, bool active, int *runlen, b
 }
 
 // ---------------------------------------------------------------------------
+// The kicked half-step state (x, y, vh after velocityVerletHalf) lives in
+// scratch arrays (the S staging arrays x, y, vx, vy, dead inside a sub-step)
+// until the permute copies it into the sorted records; P itself is rewritten
+// only by the forces pass.  So the primary state is untouched until a
+// sub-step's forces run: a sub-step prelaunched up to its density can be
+// discarded at any time (sph_void_prelaunch).
+struct KState { float *x, *y, *vhx, *vhy; };
+
 // k_kick_drift: velocityVerletHalf + bin key + histogram + bbox partials.
 // first != 0: first sub-step of a tick; the gather set a = 0 (fluid.cpp:289-290).
 __global__ void __launch_bounds__(TPB)
 k_kick_drift(int n, float dt, float hdt, int first, int probe, float eps, float cs,
-             int ox, int oy, int W, int H, PState P, uint32_t *__restrict__ key,
+             int ox, int oy, int W, int H, PState P, KState K, uint32_t *__restrict__ key,
              int32_t *__restrict__ count, float4 *__restrict__ bboxPart,
              int32_t *__restrict__ status) {
     float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
@@ -121,8 +129,9 @@ k_kick_drift(int n, float dt, float hdt, int first, int probe, float eps, float 
                 float hy = P.vy[i] + hdt * a_y;
                 px = P.x[i] + hx * dt;
                 py = P.y[i] + hy * dt;
-                P.x[i] = px; P.y[i] = py; P.vhx[i] = hx; P.vhy[i] = hy;
+                K.vhx[i] = hx; K.vhy[i] = hy;
             }
+            K.x[i] = px; K.y[i] = py;
             float tx = (px + eps) / cs, ty = (py + eps) / cs;
             int gx = (int)floorf(tx), gy = (int)floorf(ty);
             int qx = (int)floorf(2.0f * tx) - 2 * gx;
@@ -272,8 +281,8 @@ k_scan_final(int C, int W, int ox, int oy, int32_t *__restrict__ cnt,
              const int32_t *__restrict__ bsum, int32_t *__restrict__ start,
              int32_t *__restrict__ cursor, const GridParams *__restrict__ gp,
              int32_t *__restrict__ status, int do_stats) {
-    __shared__ int s_max, s_out;
-    if (threadIdx.x == 0) { s_max = 0; s_out = 0; }
+    __shared__ int s_max, s_out, s_over;
+    if (threadIdx.x == 0) { s_max = 0; s_out = 0; s_over = 0; }
     __syncthreads();
     GridParams g{};
     if (do_stats) g = *gp;
@@ -293,6 +302,7 @@ k_scan_final(int C, int W, int ox, int oy, int32_t *__restrict__ cnt,
         bool in = gx >= g.gridMinX && gx < g.gridMinX + g.gridDimX &&
                   gy >= g.gridMinY && gy < g.gridMinY + g.gridDimY;
         if (in) atomicMax(&s_max, s); else atomicAdd(&s_out, s);
+        if (in && s > LPE_REF_MAX_PER_CELL) atomicAdd(&s_over, 1);
     }
     int tot;
     int ex = block_excl_scan(s, &tot) + bsum[blockIdx.x];
@@ -305,6 +315,7 @@ k_scan_final(int C, int W, int ox, int oy, int32_t *__restrict__ cnt,
     if (threadIdx.x == 0) {
         if (s_max) atomicMax(&status[ST_MAX_OCC], s_max);
         if (s_out) atomicAdd(&status[ST_NOT_INSERTED], s_out);
+        if (s_over) atomicAdd(&status[ST_OVER_CAP], s_over);
     }
 }
 
@@ -335,9 +346,9 @@ k_scatter(int n, const uint32_t *__restrict__ key, const int32_t *__restrict__ i
 __global__ void __launch_bounds__(TPB)
 k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restrict__ start,
                const int32_t *__restrict__ tmpId, const int32_t *__restrict__ tmpOld,
-               PState P, PState S, float4 *__restrict__ nbA, float2 *__restrict__ nbB,
+               PState P, KState K, PState S, float4 *__restrict__ nbA, float2 *__restrict__ nbB,
                int probe, const int32_t *__restrict__ nptr, int nown, int32_t *__restrict__ inv,
-               int32_t *__restrict__ owned) {
+               int32_t *__restrict__ owned, int32_t *__restrict__ refInv) {
     int s = blockIdx.x * TPB + threadIdx.x;
     if (s >= (nptr ? *nptr : n)) return;
     int o = tmpOld[s];
@@ -347,10 +358,11 @@ k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restric
     int rank = 0;
     for (int j = b; j < e; j++) rank += (tmpId[j] < myid) ? 1 : 0;
     int d = b + rank;
-    nbA[d] = make_float4(P.x[o], P.y[o], P.m[o], 0.f);
+    nbA[d] = make_float4(K.x[o], K.y[o], P.m[o], 0.f);
     nbB[2 * d] = make_float2(P.vx[o], P.vy[o]);
     S.id[d] = myid;
-    if (!probe) { S.vhx[d] = P.vhx[o]; S.vhy[d] = P.vhy[o]; }
+    if (refInv) refInv[myid] = d;         // reference cell-capacity mode: id -> sorted slot
+    if (!probe) { S.vhx[d] = K.vhx[o]; S.vhy[d] = K.vhy[o]; }
     if (inv) {                    // slab decomposition: P slot -> sorted slot, owned flags
         inv[o] = d;
         owned[d] = o < nown ? 1 : 0;
@@ -468,6 +480,79 @@ __device__ __forceinline__ float walk_reach(float h, float cs) {
 }
 
 // ---------------------------------------------------------------------------
+// Reference cell-capacity mode (LPE_SPH_MODE_REF_CELL_CAP, include/lpe.h).
+// The reference's grid buffer is, per reference cell c, 65 ints {count,
+// indices[64]} (fluid.hpp:56-61), zeroed every sub-step (fluid.cpp:821-824):
+// count is the cell's full population, indices its first 64 inserts
+// (metal:237-240).  Our sorted slots ARE the canonical insertion order, so the
+// buffer never needs to exist: its int at flat position 65 c + j is count(c)
+// for j = 0, the id of the (j-1)-th slot of c for j - 1 < min(count, 64),
+// else 0.  The readers loop k < count(c) over position 65 c + 1 + k
+// unclamped (metal:281-283, :349-351), so past 64 they read the following
+// cells' words, skipping values >= N.  A particle none of whose 3x3 cells
+// exceeds 64 sees exactly its cells' members and takes the default walk
+// (bit-identical); the others take this literal walk.
+__device__ __forceinline__ int ref_cell_base(int c, const GridParams &g, int W, int ox, int oy) {
+    const int cy = c / g.gridDimX, cx = c - cy * g.gridDimX;
+    return (((cy + g.gridMinY - oy) * W) + (cx + g.gridMinX - ox)) << 2;
+}
+
+// does any of the particle's 3x3 reference cells hold more than 64?
+__device__ __forceinline__ bool ref_cap_slow(float xi, float yi, float eps, const GridParams &g, int W, int ox,
+                                             int oy, const int32_t *__restrict__ start) {
+    const int cellX = (int)floorf((xi + eps) / g.cellSize) - g.gridMinX;
+    const int cellY = (int)floorf((yi + eps) / g.cellSize) - g.gridMinY;
+    bool over = false;
+    for (int ny = -1; ny <= 1; ny++)
+        for (int nx = -1; nx <= 1; nx++) {
+            const int cx = cellX + nx, cy = cellY + ny;
+            if (cx < 0 || cx >= g.gridDimX || cy < 0 || cy >= g.gridDimY) continue;
+            const int b = ref_cell_base(cy * g.gridDimX + cx, g, W, ox, oy);
+            over |= start[b + 4] - start[b] > LPE_REF_MAX_PER_CELL;
+        }
+    return over;
+}
+
+// the reference's neighbour loop over its grid buffer: f(slot, id) for every
+// value read that is < n, in the reference's order (metal:272-291)
+template <class F>
+__device__ void ref_cap_walk(float xi, float yi, float eps, const GridParams &g, int W, int ox, int oy,
+                             const int32_t *__restrict__ start, const int32_t *__restrict__ sid,
+                             const int32_t *__restrict__ refInv, int n, int32_t *__restrict__ status, F f) {
+    constexpr int CI = LPE_REF_MAX_PER_CELL + 1;
+    const int cellX = (int)floorf((xi + eps) / g.cellSize) - g.gridMinX;
+    const int cellY = (int)floorf((yi + eps) / g.cellSize) - g.gridMinY;
+    const long C = (long)g.gridDimX * g.gridDimY;
+    for (int ny = -1; ny <= 1; ny++)
+        for (int nx = -1; nx <= 1; nx++) {
+            const int cx = cellX + nx, cy = cellY + ny;
+            if (cx < 0 || cx >= g.gridDimX || cy < 0 || cy >= g.gridDimY) continue;
+            const int c = cy * g.gridDimX + cx;
+            const int b0 = ref_cell_base(c, g, W, ox, oy);
+            const int count = start[b0 + 4] - start[b0];
+            for (int k = 0; k < count; k++) {
+                const long pos = (long)CI * c + 1 + k;
+                const long cc = pos / CI;
+                const int j = (int)(pos - cc * CI);
+                int slot = -1, id;
+                if (cc >= C) {                            // past the buffer: undefined
+                    atomicOr(&status[ST_REF_UB], 1);
+                    id = 0;
+                } else {
+                    const int bb = ref_cell_base((int)cc, g, W, ox, oy);
+                    const int cnt = start[bb + 4] - start[bb];
+                    if (j == 0) id = cnt;                              // the next cell's count
+                    else if (j - 1 < min(cnt, LPE_REF_MAX_PER_CELL)) { slot = start[bb] + (j - 1); id = sid[slot]; }
+                    else id = 0;                                        // memset slot
+                }
+                if (id >= n) continue;
+                if (slot < 0) slot = refInv[id];
+                f(slot, id);
+            }
+        }
+}
+
+// ---------------------------------------------------------------------------
 // computeDensity with LDS-staged neighbourhoods (the density probe and the
 // 16M-particle microbench: a pure density pass, no neighbour list).  A block
 // owns SB consecutive sorted slots; in sorted order they cover at most two
@@ -558,7 +643,8 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
           float restDensity, int W, int H, int ox, int oy, const GridParams *__restrict__ gp,
           const int32_t *__restrict__ start, const float4 *__restrict__ nbA, float2 *__restrict__ nbB,
           float *__restrict__ rho, float *__restrict__ pr, uint4 *__restrict__ nlist,
-          int32_t *__restrict__ ncount, int32_t *__restrict__ status) {
+          int32_t *__restrict__ ncount, int32_t *__restrict__ status, const int32_t *__restrict__ sid,
+          const int32_t *__restrict__ refInv) {
     __shared__ Stage st;
     __shared__ float4 lrec[STAGE_CAP];
     __shared__ uint4 lnl[SB];                             // per thread: the current group of 8 offsets
@@ -608,7 +694,22 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
             }
         }
     };
-    if (st.ok)
+    if (refInv && ref_cap_slow(xi, yi, eps, g, W, ox, oy, start)) {
+        // reference cell-capacity mode, an over-full cell in reach: the
+        // reference's literal loop (no neighbour list; the forces pass walks
+        // the same way)
+        ref_cap_walk(xi, yi, eps, g, W, ox, oy, start, sid, refInv, nn, status, [&](int k, int) {
+            const float4 o = nbA[k];
+            float dx = xi - o.x, dy = yi - o.y;
+            float r2 = dx * dx + dy * dy;
+            if (r2 < h2) {
+                float diff = h2 - r2;
+                float w = poly6 * diff * diff * diff;
+                acc += o.z * w;
+            }
+        });
+        cnt = NLIST_CAP + 1;
+    } else if (st.ok)
         walk_ranges(xi, yi, eps, cs, walk_reach(h, cs), g, W, H, ox, oy, start, [&](int b, int e, int cyc) {
             // the LDS segment of cell row cyc, resolved once per range
             const int i = (cyp == st.cy0 ? 0 : 3) + (cyc - cyp + 1);
@@ -643,6 +744,7 @@ struct SphStepParams {
     float h, eps, dt, hdt;
     float viscosity, minDist, minDens;
     int diag;                 // count diagnostics into status (lpe_sph_diag)
+    const int32_t *refInv;    // reference cell-capacity mode: id -> slot (else null)
 };
 
 // computeForces + velocityVerletFinish + impulse + push-out; reads the sorted
@@ -716,7 +818,12 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         atomicAdd(&status[ST_NEIGH], cnt);
         if (cnt > NLIST_CAP) atomicAdd(&status[ST_NL_OVERFLOW], 1);
     }
-    if (cnt <= NLIST_CAP) {
+    if (sp.refInv && ref_cap_slow(xi, yi, sp.eps, g, sp.W, sp.ox, sp.oy, start)) {
+        // reference cell-capacity mode: the reference's literal loop
+        // (metal:345-351; the j == i skip is the slot test in pair)
+        ref_cap_walk(xi, yi, sp.eps, g, sp.W, sp.ox, sp.oy, start, S.id, sp.refInv, sp.n, status,
+                     [&](int k, int) { pair(k, Rec{nbA[k], nbB[k]}); });
+    } else if (cnt <= NLIST_CAP) {
         // the density pass's list: the r^2 < h^2 neighbours in canonical
         // order, so the heavy pair math runs only on real neighbours
         constexpr int U = 8;                      // one group of eight offsets, all loads in flight
@@ -834,12 +941,12 @@ __device__ __forceinline__ int rcount(const float *buf, int cap) {
     return buf ? min(*(const int *)buf, cap) : 0;
 }
 
-__global__ void k_ghost_pack(int n, PState P, float x0, float x1, float D, float drift, int hasL, int hasR,
-                             float *__restrict__ sL, float *__restrict__ sR, int cap,
+__global__ void k_ghost_pack(int n, PState P, KState K, float x0, float x1, float D, float drift, int hasL,
+                             int hasR, float *__restrict__ sL, float *__restrict__ sR, int cap,
                              int32_t *__restrict__ status) {
     int i = blockIdx.x * TPB + threadIdx.x;
     if (i >= n) return;
-    const float x = P.x[i];
+    const float x = K.x[i];                      // the kicked position of this sub-step
     if ((hasL && x < x0 - drift) || (hasR && x >= x1 + drift))
         atomicOr(&status[ST_HALO_DRIFT], 1);       // beyond what the halo covers
     for (int side = 0; side < 2; side++) {
@@ -849,14 +956,14 @@ __global__ void k_ghost_pack(int n, PState P, float x0, float x1, float D, float
         int k = atomicAdd(hdr(buf), 1);
         if (k >= cap) { atomicOr(&status[ST_HALO_OVERFLOW], 1); continue; }
         float *r = buf + HDR + (size_t)k * GREC;
-        r[0] = x; r[1] = P.y[i]; r[2] = P.vx[i]; r[3] = P.vy[i];
+        r[0] = x; r[1] = K.y[i]; r[2] = P.vx[i]; r[3] = P.vy[i];
         r[4] = P.m[i]; r[5] = __int_as_float(P.id[i]);
     }
 }
 
 // ghosts -> P[nown ...] (left ones first), bin key + histogram
 __global__ void k_ghost_unpack(const float *__restrict__ rL, const float *__restrict__ rR, int cap,
-                               int nown, PState P, uint32_t *__restrict__ key,
+                               int nown, PState P, KState K, uint32_t *__restrict__ key,
                                int32_t *__restrict__ count, float eps, float cs, int ox, int oy,
                                int W, int H, int32_t *__restrict__ ntot, int32_t *__restrict__ status) {
     const int t = blockIdx.x * TPB + threadIdx.x;
@@ -875,8 +982,8 @@ __global__ void k_ghost_unpack(const float *__restrict__ rL, const float *__rest
         slot = nown + gL + k;
     }
     const float px = src[0], py = src[1];
-    P.x[slot] = px; P.y[slot] = py; P.vx[slot] = src[2]; P.vy[slot] = src[3];
-    P.vhx[slot] = src[2]; P.vhy[slot] = src[3];
+    K.x[slot] = px; K.y[slot] = py; P.vx[slot] = src[2]; P.vy[slot] = src[3];
+    K.vhx[slot] = src[2]; K.vhy[slot] = src[3];
     P.m[slot] = src[4]; P.id[slot] = __float_as_int(src[5]);
     float tx = (px + eps) / cs, ty = (py + eps) / cs;      // the key of k_kick_drift
     int gx = (int)floorf(tx), gy = (int)floorf(ty);
@@ -1048,6 +1155,18 @@ __global__ void k_unpermute(int n, const int32_t *__restrict__ id, int nf, Field
     for (int k = 0; k < nf; k++) f.dst[k][d] = f.src[k][i];
 }
 
+// the prelaunched sub-step's stats (status[1]) into the step's (status[0])
+__global__ void k_merge_prestats(int32_t *__restrict__ st, int32_t *__restrict__ pre) {
+    if (threadIdx.x != 0) return;
+    st[ST_CAP_OVERFLOW] |= pre[ST_CAP_OVERFLOW];
+    st[ST_MAX_OCC] = max(st[ST_MAX_OCC], pre[ST_MAX_OCC]);
+    st[ST_NOT_INSERTED] = pre[ST_NOT_INSERTED];
+    st[ST_STAGE_FALLBACK] += pre[ST_STAGE_FALLBACK];
+    st[ST_OVER_CAP] += pre[ST_OVER_CAP];
+    st[ST_REF_UB] |= pre[ST_REF_UB];
+    for (int k = 0; k < ST_COUNT; k++) pre[k] = 0;
+}
+
 }  // namespace lpe
 
 using namespace lpe;
@@ -1056,6 +1175,38 @@ using namespace lpe;
 // host side
 static inline int nblk(long n, int t = TPB) { return (int)((n + t - 1) / t); }
 static inline int nblk1(long n, int t = TPB) { return std::max(1, nblk(n, t)); }   // never an empty grid
+
+// the id -> slot map of the reference cell-capacity mode, or null (mode off)
+static inline int32_t *sph_ref_inv(const SphDev &d) {
+    return (d.mode & LPE_SPH_MODE_REF_CELL_CAP) ? d.refInv : nullptr;
+}
+
+// per-step stats (max occupancy, over-capacity cells, undefined reads)
+static int sph_reset_step_stats(lpe_ctx *ctx, hipStream_t s, int32_t *status) {
+    LPE_HIP(ctx, hipMemsetAsync(status + ST_MAX_OCC, 0, sizeof(int32_t), s));
+    LPE_HIP(ctx, hipMemsetAsync(status + ST_OVER_CAP, 0, 2 * sizeof(int32_t), s));
+    return LPE_OK;
+}
+
+// the kicked-state scratch (the S staging arrays, dead inside a sub-step)
+static inline KState sph_kstate(const SphDev &d) { return KState{d.S.x, d.S.y, d.S.vx, d.S.vy}; }
+
+// A pending prelaunch (sph_prelaunch) only wrote scratch: voiding it orders
+// the context stream after it (its buffers are reused next) and forgets it.
+static int sph_void_prelaunch(lpe_ctx *ctx) {
+    SphDev &d = ctx->sph;
+    if (!d.pre) return LPE_OK;
+    d.pre = false;
+    LPE_HIP(ctx, hipStreamWaitEvent(ctx->stream, d.preDone, 0));
+    return LPE_OK;
+}
+// order the context stream after a pending prelaunch, which stays valid
+// (downloads stage through arrays the prelaunched sub-step no longer needs)
+static int sph_join_prelaunch(lpe_ctx *ctx) {
+    SphDev &d = ctx->sph;
+    if (d.pre) LPE_HIP(ctx, hipStreamWaitEvent(ctx->stream, d.preDone, 0));
+    return LPE_OK;
+}
 
 static void pstate_free(PState &p) {
     void *ptrs[] = {p.x, p.y, p.vx, p.vy, p.vhx, p.vhy, p.ax, p.ay, p.m, p.id};
@@ -1081,15 +1232,16 @@ static void shard_free(Shard *h) {
 }
 
 static void sph_free(SphDev &d) {
+    if (d.pside) (void)hipStreamSynchronize(d.pside);   // a prelaunch may still use the buffers
+    d.pre = false;
     shard_free(d.shard);
     d.shard = nullptr;
     pstate_free(d.P);
     pstate_free(d.S);
-    void *ptrs[] = {d.rho, d.pr, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.count, d.start, d.cursor,
+    void *ptrs[] = {d.rho, d.pr, d.rhoN, d.prN, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.refInv, d.stage, d.count, d.start, d.cursor,
                     d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.raabb, d.accum, d.acq, d.rbinStart, d.rgrid, d.rmax,
                     d.rbinList, d.rbinCount, d.coupleBody};
     for (void *p : ptrs) if (p) (void)hipFree(p);
-    if (d.pside) (void)hipStreamSynchronize(d.pside);
     hipEvent_t evs[] = {d.preReady, d.preDone};
     for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
     if (d.pside) (void)hipStreamDestroy(d.pside);
@@ -1176,6 +1328,8 @@ extern "C" int lpe_fluid_config_default(lpe_fluid_config *c) {
 extern "C" int lpe_sph_set_config(lpe_ctx *ctx, const lpe_fluid_config *cfg) {
     if (!ctx || !cfg) return LPE_ERR_ARG;
     if (cfg->numSubSteps < 0) return LPE_ERR_ARG;
+    int st = sph_void_prelaunch(ctx);
+    if (st) return st;
     ctx->sph.cfg = *cfg;
     ctx->sph.cfg_set = true;
     ctx->sph.rig_dirty = true;
@@ -1192,6 +1346,8 @@ static float ref_cell_size(const lpe_fluid_config &c) {
 // absolute device grid [gx0, gx1] x [gy0, gy1] (reference cells)
 static int sph_set_grid(lpe_ctx *ctx, int gx0, int gy0, int gx1, int gy1) {
     SphDev &d = ctx->sph;
+    if (d.pside) LPE_HIP(ctx, hipStreamSynchronize(d.pside));   // the bins may be re-allocated
+    d.pre = false;
     d.ox = gx0; d.oy = gy0;
     d.W = gx1 - gx0 + 1; d.H = gy1 - gy0 + 1;
     long C = 4L * d.W * d.H;
@@ -1281,7 +1437,8 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     if (n <= d.cap_n && d.P.x) return LPE_OK;
     pstate_free(d.P);
     pstate_free(d.S);
-    void *ptrs[] = {d.rho, d.pr, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.bboxPart};
+    void *ptrs[] = {d.rho, d.pr, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.bboxPart, d.refInv,
+                    d.stage, d.rhoN, d.prN};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     size_t N = (size_t)std::max(n, 1);
     int st = pstate_alloc(ctx, d.P, N, true);
@@ -1290,6 +1447,8 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     if (st) return st;
     LPE_HIP(ctx, hipMalloc((void **)&d.rho, sizeof(float) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.pr, sizeof(float) * N));
+    LPE_HIP(ctx, hipMalloc((void **)&d.rhoN, sizeof(float) * N));
+    LPE_HIP(ctx, hipMalloc((void **)&d.prN, sizeof(float) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.nbA, sizeof(float4) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.nbB, sizeof(float4) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.nlist, sizeof(uint4) * N * (NLIST_CAP / 8)));
@@ -1297,6 +1456,8 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     LPE_HIP(ctx, hipMalloc((void **)&d.key, sizeof(uint32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpId, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpOld, sizeof(int32_t) * N));
+    LPE_HIP(ctx, hipMalloc((void **)&d.refInv, sizeof(int32_t) * N));
+    LPE_HIP(ctx, hipMalloc((void **)&d.stage, sizeof(float) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.bboxPart, sizeof(float4) * MAX_KICK_BLOCKS));
     d.cap_n = n;
     if (h) {
@@ -1313,10 +1474,13 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
         h->cap_slots = (int)N;
     }
     if (!d.gp) {
-        LPE_HIP(ctx, hipMalloc((void **)&d.gp, sizeof(GridParams)));
-        LPE_HIP(ctx, hipMalloc((void **)&d.status, sizeof(int32_t) * ST_COUNT));
-        LPE_HIP(ctx, hipMemsetAsync(d.gp, 0, sizeof(GridParams), ctx->stream));
+        LPE_HIP(ctx, hipMalloc((void **)&d.gp, 2 * sizeof(GridParams)));
+        LPE_HIP(ctx, hipMalloc((void **)&d.status, sizeof(int32_t) * 2 * ST_COUNT));
+        LPE_HIP(ctx, hipMemsetAsync(d.gp, 0, 2 * sizeof(GridParams), ctx->stream));
+        LPE_HIP(ctx, hipMemsetAsync(d.status, 0, sizeof(int32_t) * 2 * ST_COUNT, ctx->stream));
     }
+    d.gp_cur = d.gp;
+    d.stat_cur = d.status;
     return LPE_OK;
 }
 
@@ -1327,6 +1491,8 @@ extern "C" int lpe_sph_upload(lpe_ctx *ctx, int n, const float *x, const float *
     if (n > 0 && (!x || !y || !vx || !vy || !mass)) return LPE_ERR_ARG;
     (void)hipSetDevice(ctx->device);
     SphDev &d = ctx->sph;
+    if (d.pside) LPE_HIP(ctx, hipStreamSynchronize(d.pside));   // buffers may be re-allocated
+    d.pre = false;
     int st = sph_alloc_particles(ctx, n);
     if (st) return st;
     d.n = n;
@@ -1433,9 +1599,9 @@ static int sph_scan(lpe_ctx *ctx, int C, int32_t *cnt, int32_t *start, int32_t *
     hipStream_t s = ctx->stream;
     LPE_KERNEL(ctx, "k_scan_reduce", k_scan_reduce, dim3(nb), dim3(TPB), 0, s, C, cnt, bsum);
     LPE_KERNEL(ctx, "k_scan_blocks", k_scan_blocks, dim3(1), dim3(TPB), 0, s, nb, bsum, start + C, d.bboxPart,
-                       nparts, d.cs, fluid ? d.gp : (GridParams *)nullptr, d.status, bbG);
+                       nparts, d.cs, fluid ? d.gp_cur : (GridParams *)nullptr, d.stat_cur, bbG);
     LPE_KERNEL(ctx, "k_scan_final", k_scan_final, dim3(nb), dim3(TPB), 0, s, C, d.W, d.ox, d.oy, cnt, bsum,
-                       start, cursor, d.gp, d.status, fluid ? 1 : 0);
+                       start, cursor, d.gp_cur, d.stat_cur, fluid ? 1 : 0);
     LPE_CHECK_LAUNCH(ctx, "scan");
     return LPE_OK;
 }
@@ -1499,27 +1665,27 @@ static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool pr
     int kb = std::min(MAX_KICK_BLOCKS, std::max(1, nblk(d.n)));
     LPE_KERNEL(ctx, "k_kick_drift", k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
                        first ? 1 : 0, probe ? 1 : 0, d.cfg.gridConfig.gridEpsilon, d.cs, d.ox,
-                       d.oy, d.W, d.H, d.P, d.key, d.count, d.bboxPart, d.status);
+                       d.oy, d.W, d.H, d.P, sph_kstate(d), d.key, d.count, d.bboxPart, d.stat_cur);
     LPE_CHECK_LAUNCH(ctx, "k_kick_drift");
     int st = sph_scan(ctx, C, d.count, d.start, d.cursor, d.blocksum, kb, true);
     if (st) return st;
     LPE_KERNEL(ctx, "k_scatter", k_scatter, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.P.id, d.cursor,
                        d.tmpId, d.tmpOld, (const int32_t *)nullptr);
     LPE_KERNEL(ctx, "k_rank_permute", k_rank_permute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.start,
-                       d.tmpId, d.tmpOld, d.P, d.S, d.nbA, (float2 *)d.nbB, probe ? 1 : 0,
-                       (const int32_t *)nullptr, 0, (int32_t *)nullptr, (int32_t *)nullptr);
+                       d.tmpId, d.tmpOld, d.P, sph_kstate(d), d.S, d.nbA, (float2 *)d.nbB, probe ? 1 : 0,
+                       (const int32_t *)nullptr, 0, (int32_t *)nullptr, (int32_t *)nullptr, sph_ref_inv(d));
     LPE_CHECK_LAUNCH(ctx, "hash");
     return LPE_OK;
 }
 
 // density over n slots (nptr: device count of the sharded sub-step)
-static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr) {
+static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr, float *rho, float *pr) {
     SphDev &d = ctx->sph;
     const lpe_fluid_config &c = d.cfg;
     LPE_KERNEL(ctx, "k_density", k_density, dim3(xcd_grid(nblk(n, SB))), dim3(SB), 0, ctx->stream, n,
                        nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
-                       c.restDensity, d.W, d.H, d.ox, d.oy, d.gp, d.start, d.nbA, (float2 *)d.nbB,
-                       d.rho, d.pr, d.nlist, d.ncount, d.status);
+                       c.restDensity, d.W, d.H, d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)d.nbB,
+                       rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d));
     LPE_CHECK_LAUNCH(ctx, "k_density");
     return LPE_OK;
 }
@@ -1539,7 +1705,8 @@ static int sph_hash_shard(lpe_ctx *ctx, float subDt, float halfDt, bool first) {
     const int kb = std::min(MAX_KICK_BLOCKS, std::max(1, nblk(d.n)));
     const float eps = d.cfg.gridConfig.gridEpsilon;
     LPE_KERNEL(ctx, "k_kick_drift", k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
-               first ? 1 : 0, 0, eps, d.cs, d.ox, d.oy, d.W, d.H, d.P, d.key, d.count, d.bboxPart, d.status);
+               first ? 1 : 0, 0, eps, d.cs, d.ox, d.oy, d.W, d.H, d.P, sph_kstate(d), d.key, d.count, d.bboxPart,
+               d.status);
     LPE_KERNEL(ctx, "k_bbox_reduce", k_bbox_reduce, dim3(1), dim3(TPB), 0, s, d.bboxPart, kb, h.bb);
     LPE_CHECK_LAUNCH(ctx, "shard kick");
     int st = tr->allreduce(ctx, (float *)h.bb, 4, 1);
@@ -1547,7 +1714,8 @@ static int sph_hash_shard(lpe_ctx *ctx, float subDt, float halfDt, bool first) {
     LPE_HIP(ctx, hipMemsetAsync(h.gsL, 0, sizeof(float) * HDR, s));
     LPE_HIP(ctx, hipMemsetAsync(h.gsR, 0, sizeof(float) * HDR, s));
     const float drift = h.D - 2.0f * d.cfg.gridConfig.smoothingLength;
-    LPE_KERNEL(ctx, "k_ghost_pack", k_ghost_pack, dim3(nblk1(d.n)), dim3(TPB), 0, s, d.n, d.P, h.x0, h.x1, h.D,
+    LPE_KERNEL(ctx, "k_ghost_pack", k_ghost_pack, dim3(nblk1(d.n)), dim3(TPB), 0, s, d.n, d.P, sph_kstate(d), h.x0,
+               h.x1, h.D,
                drift, h.hasL, h.hasR, h.gsL, h.gsR, h.cap, d.status);
     LPE_CHECK_LAUNCH(ctx, "k_ghost_pack");
     st = tr->halo(ctx, h.hasL ? h.gsL : nullptr, h.hasR ? h.gsR : nullptr, h.hasL ? h.grL : nullptr,
@@ -1555,7 +1723,7 @@ static int sph_hash_shard(lpe_ctx *ctx, float subDt, float halfDt, bool first) {
     if (st) return st;
     LPE_KERNEL(ctx, "k_ghost_unpack", k_ghost_unpack, dim3(nblk1(2 * h.cap)), dim3(TPB), 0, s,
                h.hasL ? h.grL : (const float *)nullptr, h.hasR ? h.grR : (const float *)nullptr, h.cap, d.n,
-               d.P, d.key, d.count, eps, d.cs, d.ox, d.oy, d.W, d.H, h.ntot, d.status);
+               d.P, sph_kstate(d), d.key, d.count, eps, d.cs, d.ox, d.oy, d.W, d.H, h.ntot, d.status);
     LPE_CHECK_LAUNCH(ctx, "k_ghost_unpack");
     st = sph_scan(ctx, C, d.count, d.start, d.cursor, d.blocksum, kb, true, h.bb);
     if (st) return st;
@@ -1563,7 +1731,9 @@ static int sph_hash_shard(lpe_ctx *ctx, float subDt, float halfDt, bool first) {
     LPE_KERNEL(ctx, "k_scatter", k_scatter, dim3(nblk1(ncap)), dim3(TPB), 0, s, ncap, d.key, d.P.id, d.cursor,
                d.tmpId, d.tmpOld, (const int32_t *)h.ntot);
     LPE_KERNEL(ctx, "k_rank_permute", k_rank_permute, dim3(nblk1(ncap)), dim3(TPB), 0, s, ncap, d.key, d.start,
-               d.tmpId, d.tmpOld, d.P, d.S, d.nbA, (float2 *)d.nbB, 0, (const int32_t *)h.ntot, d.n, h.inv, h.owned);
+               d.tmpId, d.tmpOld, d.P, sph_kstate(d), d.S, d.nbA, (float2 *)d.nbB, 0, (const int32_t *)h.ntot, d.n,
+               h.inv, h.owned,
+               (int32_t *)nullptr);
     LPE_CHECK_LAUNCH(ctx, "shard hash");
     return LPE_OK;
 }
@@ -1655,13 +1825,25 @@ int sph_prelaunch(lpe_ctx *ctx, double dt_tick) {
     const float subDt = (float)dt_tick / (float)c.numSubSteps;
     const float halfDt = 0.5f * subDt;
     hipStream_t main = ctx->stream;
-    ctx->stream = d.pside;                       // the hash / density helpers launch on ctx->stream
-    int st = hipMemsetAsync(d.status + ST_MAX_OCC, 0, sizeof(int32_t), d.pside) == hipSuccess ? LPE_OK : LPE_ERR_HIP;
+    // the hash / density helpers launch on ctx->stream and write gp_cur /
+    // stat_cur: here the side stream and the prelaunch's own slots
+    ctx->stream = d.pside;
+    d.gp_cur = d.gp + 1;
+    d.stat_cur = d.status + ST_COUNT;
+    int st = hipMemsetAsync(d.stat_cur, 0, sizeof(int32_t) * ST_COUNT, d.pside) == hipSuccess ? LPE_OK : LPE_ERR_HIP;
     if (!st) st = sph_hash(ctx, subDt, halfDt, true, false);
-    if (!st) st = sph_density(ctx, d.n, nullptr);
-    if (!st && hipEventRecord(d.preDone, d.pside) != hipSuccess) st = LPE_ERR_HIP;
+    if (!st) st = sph_density(ctx, d.n, nullptr, d.rhoN, d.prN);   // P-order rho / p stay the tick's
     ctx->stream = main;
-    if (st) return st;
+    d.gp_cur = d.gp;
+    d.stat_cur = d.status;
+    // recorded even after a failed launch, so whoever voids it waits on
+    // everything that reached the side stream
+    const bool rec = hipEventRecord(d.preDone, d.pside) == hipSuccess;
+    if (st || !rec) {
+        (void)hipStreamSynchronize(d.pside);
+        ctx->err = st ? ctx->err : "hipEventRecord (prelaunch)";
+        return st ? st : LPE_ERR_HIP;
+    }
     d.pre = true;
     d.pre_dt = dt_tick;
     return LPE_OK;
@@ -1678,16 +1860,24 @@ extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
     float subDt = dt / (float)c.numSubSteps;         // fluid.cpp:593
     float halfDt = 0.5f * subDt;
     hipStream_t s = ctx->stream;
-    // sub-step 0 up to the forces already launched (sph_prelaunch)?
-    const bool pre = d.pre && !d.shard;
-    d.pre = false;
-    if (pre && d.pre_dt != dt_tick) {
-        ctx->err = "lpe_sph_step: the prelaunched sub-step was for another time step";
-        return LPE_ERR_STATE;
+    // sub-step 0 up to the forces already launched (sph_prelaunch)?  One for
+    // another time step is discarded (it never touched P)
+    if (d.pre && (d.shard || d.pre_dt != dt_tick)) {
+        int st0 = sph_void_prelaunch(ctx);
+        if (st0) return st0;
     }
+    const bool pre = d.pre;
+    d.pre = false;
     int st = sph_build_rigid_bins(ctx);
     if (st) return st;
-    if (!pre) LPE_HIP(ctx, hipMemsetAsync(d.status + ST_MAX_OCC, 0, sizeof(int32_t), s));
+    st = sph_reset_step_stats(ctx, s, d.status);
+    if (st) return st;
+    if (pre) {
+        std::swap(d.rho, d.rhoN);                     // sub-step 0's density is the prelaunch's
+        std::swap(d.pr, d.prN);
+        LPE_HIP(ctx, hipStreamWaitEvent(s, d.preDone, 0));
+        LPE_KERNEL(ctx, "k_merge_prestats", k_merge_prestats, dim3(1), dim3(64), 0, s, d.status, d.status + ST_COUNT);
+    }
     SphStepParams sp;
     sp.n = d.n; sp.W = d.W; sp.H = d.H; sp.ox = d.ox; sp.oy = d.oy;
     sp.h = c.gridConfig.smoothingLength; sp.eps = c.gridConfig.gridEpsilon;
@@ -1696,6 +1886,7 @@ extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
     sp.minDist = c.numericalConfig.minDistanceThreshold;
     sp.minDens = c.numericalConfig.minDensityThreshold;
     sp.diag = d.diag;
+    sp.refInv = sph_ref_inv(d);
     sp.nptr = nullptr;
     sp.dst = nullptr;
     sp.orho = sp.opr = nullptr;
@@ -1722,18 +1913,19 @@ extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
         if (sh) {
             st = sph_hash_shard(ctx, subDt, halfDt, step == 0);
             if (st) return st;
-            st = sph_density(ctx, sp.n, sh->ntot);
+            st = sph_density(ctx, sp.n, sh->ntot, d.rho, d.pr);
             if (st) return st;
             st = sph_owned_map(ctx);
         } else if (step == 0 && pre) {
-            st = hipStreamWaitEvent(s, d.preDone, 0) == hipSuccess ? LPE_OK : LPE_ERR_HIP;
+            st = LPE_OK;                              // waited for above
         } else {
             st = sph_hash(ctx, subDt, halfDt, step == 0, false);
             if (st) return st;
-            st = sph_density(ctx, d.n, nullptr);
+            st = sph_density(ctx, d.n, nullptr, d.rho, d.pr);
         }
         if (st) return st;
-        LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(xcd_grid(nblk(sp.n))), dim3(TPB), 0, s, sp, cp, d.gp,
+        LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(xcd_grid(nblk(sp.n))), dim3(TPB), 0, s, sp, cp,
+                           (step == 0 && pre) ? d.gp + 1 : d.gp,
                            d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart, d.rbinList,
                            d.acq, d.status);
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
@@ -1761,7 +1953,11 @@ static int sph_unpermute_download(lpe_ctx *ctx, const int32_t *id, int nf, const
                                   float **host) {
     SphDev &d = ctx->sph;
     hipStream_t s = ctx->stream;
-    float *stage[6] = {d.S.x, d.S.y, d.S.vx, d.S.vy, d.S.vhx, d.S.vhy};
+    // staging: arrays a pending prelaunch no longer needs (it keeps S.vhx,
+    // S.vhy, S.id, the records and the bins)
+    int st0 = sph_join_prelaunch(ctx);
+    if (st0) return st0;
+    float *stage[6] = {d.S.x, d.S.y, d.S.vx, d.S.vy, d.S.m, d.stage};
     Fields6 f{};
     for (int k = 0; k < nf; k++) { f.src[k] = src[k]; f.dst[k] = stage[k]; }
     LPE_KERNEL(ctx, "k_unpermute", k_unpermute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, id, nf, f);
@@ -1867,6 +2063,21 @@ extern "C" int lpe_sph_get_stats(lpe_ctx *ctx, lpe_sph_stats *out) {
     out->rigidCandidates = status[ST_RIGID_CAND];
     out->neighbours = status[ST_NEIGH];
     out->stageFallback = status[ST_STAGE_FALLBACK];
+    out->overCapCells = status[ST_OVER_CAP];
+    out->refUndefined = status[ST_REF_UB];
+    return LPE_OK;
+}
+
+extern "C" int lpe_sph_set_mode(lpe_ctx *ctx, int flags) {
+    if (!ctx || (flags & ~LPE_SPH_MODE_REF_CELL_CAP)) return LPE_ERR_ARG;
+    SphDev &d = ctx->sph;
+    if ((flags & LPE_SPH_MODE_REF_CELL_CAP) && d.shard) {
+        ctx->err = "the reference cell-capacity mode is single-domain only (not on a slab rank)";
+        return LPE_ERR_STATE;
+    }
+    int st = sph_void_prelaunch(ctx);        // a prelaunched sub-step ran in the old mode
+    if (st) return st;
+    d.mode = flags;
     return LPE_OK;
 }
 
@@ -1883,7 +2094,10 @@ extern "C" int lpe_sph_diag(lpe_ctx *ctx, int on) {
 int lpe_sph_hash_current(lpe_ctx *ctx) {
     SphDev &d = ctx->sph;
     if (d.n <= 0) return LPE_OK;
-    LPE_HIP(ctx, hipMemsetAsync(d.status + ST_MAX_OCC, 0, sizeof(int32_t), ctx->stream));
+    int st = sph_void_prelaunch(ctx);           // the probe's hash reuses the prelaunch's buffers
+    if (st) return st;
+    st = sph_reset_step_stats(ctx, ctx->stream, d.status);
+    if (st) return st;
     return sph_hash(ctx, 0.f, 0.f, false, true);
 }
 
@@ -1892,8 +2106,11 @@ extern "C" int lpe_sph_probe_cells(lpe_ctx *ctx, int32_t *cell_index, lpe_sph_st
     SphDev &d = ctx->sph;
     if (d.n <= 0) return LPE_OK;
     (void)hipSetDevice(ctx->device);
-    LPE_HIP(ctx, hipMemsetAsync(d.status + ST_MAX_OCC, 0, sizeof(int32_t), ctx->stream));
-    int st = sph_hash(ctx, 0.f, 0.f, false, true);
+    int st = sph_void_prelaunch(ctx);           // the probe's hash reuses the prelaunch's buffers
+    if (st) return st;
+    st = sph_reset_step_stats(ctx, ctx->stream, d.status);
+    if (st) return st;
+    st = sph_hash(ctx, 0.f, 0.f, false, true);
     if (st) return st;
     LPE_KERNEL(ctx, "k_ref_cells", k_ref_cells, dim3(nblk(d.n)), dim3(TPB), 0, ctx->stream, d.n,
                        d.cfg.gridConfig.gridEpsilon, d.P.x, d.P.y, d.P.id, d.gp, d.tmpId);
@@ -1910,9 +2127,13 @@ extern "C" int lpe_sph_probe_density(lpe_ctx *ctx, float *density, float *pressu
     SphDev &d = ctx->sph;
     if (d.n <= 0) return LPE_OK;
     (void)hipSetDevice(ctx->device);
-    int st = sph_hash(ctx, 0.f, 0.f, false, true);
+    int st = sph_void_prelaunch(ctx);           // the probe's hash reuses the prelaunch's buffers
     if (st) return st;
-    st = sph_density(ctx, d.n, nullptr);           // the tick's density pass, as is
+    st = sph_reset_step_stats(ctx, ctx->stream, d.status);
+    if (st) return st;
+    st = sph_hash(ctx, 0.f, 0.f, false, true);
+    if (st) return st;
+    st = sph_density(ctx, d.n, nullptr, d.rho, d.pr);   // the tick's density pass, as is
     if (st) return st;
     // rho/p are in S slot order here; S.x.. are the unpermute staging buffers,
     // so keep S.id aside in tmpOld first
@@ -1929,6 +2150,12 @@ extern "C" int lpe_sph_set_slab(lpe_ctx *ctx, float x0, float x1, float halo, in
     if (!ctx || ghost_cap < 1 || !(halo > 0.f) || (has_left && has_right && !(x1 > x0))) return LPE_ERR_ARG;
     (void)hipSetDevice(ctx->device);
     SphDev &d = ctx->sph;
+    if (d.mode & LPE_SPH_MODE_REF_CELL_CAP) {
+        ctx->err = "the reference cell-capacity mode is single-domain only (not on a slab rank)";
+        return LPE_ERR_STATE;
+    }
+    if (d.pside) LPE_HIP(ctx, hipStreamSynchronize(d.pside));
+    d.pre = false;
     LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
     shard_free(d.shard);
     d.shard = nullptr;
@@ -1955,6 +2182,8 @@ extern "C" int lpe_sph_set_ids(lpe_ctx *ctx, int n, const int32_t *ids) {
     SphDev &d = ctx->sph;
     if (n != d.n) return LPE_ERR_ARG;
     if (n == 0) return LPE_OK;
+    int st = sph_void_prelaunch(ctx);          // it sorted by the old ids
+    if (st) return st;
     LPE_HIP(ctx, hipMemcpyAsync(d.P.id, ids, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
     LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
     return LPE_OK;
@@ -1967,6 +2196,8 @@ extern "C" int lpe_sph_download_owned(lpe_ctx *ctx, int cap, float *x, float *y,
     *n_out = d.n;
     if (d.n > cap) return LPE_ERR_CAPACITY;
     hipStream_t s = ctx->stream;
+    int st0 = sph_join_prelaunch(ctx);
+    if (st0) return st0;
     const size_t B = sizeof(float) * (size_t)d.n;
     if (d.n > 0) {
         const float *src[6] = {d.P.x, d.P.y, d.P.vx, d.P.vy, d.rho, d.pr};

@@ -194,7 +194,6 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
     const char *ser = std::getenv("LPE_SERIAL_TICK");
     const bool serial = ser && std::atoi(ser) != 0;
     const bool overlap = !serial && rd->nb > 0;
-    d.pre = false;              // a prelaunch left by a failed call is void
     for (int t = 0; t < nticks; t++) {
         // 1) FluidSystem::update (fluid.cpp:958-1021)
         int nr = fluid ? d.couple_n : 0;
@@ -229,8 +228,10 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
         st = lpe_rigid_integrate(ctx, 2, dt_state, dt_move);
         if (st) return st;
         // the fluid state is final for this tick: the next tick's first
-        // sub-step (up to its forces) runs beside the rigid solvers
-        if (!serial && fluid && !d.shard && t + 1 < nticks) {
+        // sub-step (up to its forces) runs beside the rigid solvers -- also
+        // after the last tick of this call, for the next call (it writes only
+        // scratch, so downloads and state changes in between are safe)
+        if (!serial && fluid && !d.shard) {
             st = sph_prelaunch(ctx, dt_fluid);
             if (st) return st;
         }

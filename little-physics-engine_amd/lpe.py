@@ -73,7 +73,7 @@ class SphStats(C.Structure):
                 ("gridDimX", C.c_int32), ("gridDimY", C.c_int32),
                 ("gridMinX", C.c_int32), ("gridMinY", C.c_int32), ("cellSize", C.c_float),
                 ("nlistOverflow", C.c_int32), ("rigidCandidates", C.c_int32), ("neighbours", C.c_int32),
-                ("stageFallback", C.c_int32)]
+                ("stageFallback", C.c_int32), ("overCapCells", C.c_int32), ("refUndefined", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -169,6 +169,7 @@ SIGNATURES = {
     "lpe_sph_download_rigids": ([C.c_void_p, C.c_void_p, _FP], C.c_int),
     "lpe_sph_get_stats": ([C.c_void_p, C.POINTER(SphStats)], C.c_int),
     "lpe_sph_diag": ([C.c_void_p, C.c_int], C.c_int),
+    "lpe_sph_set_mode": ([C.c_void_p, C.c_int], C.c_int),
     "lpe_sph_probe_cells": ([C.c_void_p, _IP, C.POINTER(SphStats)], C.c_int),
     "lpe_sph_probe_density": ([C.c_void_p, _FP, _FP], C.c_int),
     "lpe_rigid_config_default": ([C.POINTER(RigidConfig)], C.c_int),
@@ -210,6 +211,7 @@ class RenderParams(C.Structure):
 SIGNATURES["lpe_render_density"] = ([C.c_void_p, C.POINTER(RenderParams), _FP, _FP], C.c_int)
 
 SYS_BOUNDARY, SYS_GRAVITY, SYS_ROTATION, SYS_MOVEMENT, SYS_SLEEP = 1, 2, 4, 8, 16
+SPH_MODE_REF_CELL_CAP = 1       # LPE_SPH_MODE_REF_CELL_CAP (include/lpe.h)
 
 
 def lib():
@@ -353,6 +355,10 @@ class Context:
         s = SphStats()
         self._chk(lib().lpe_sph_get_stats(self._h, C.byref(s)), "lpe_sph_get_stats")
         return s.as_dict()
+
+    def sph_set_mode(self, flags: int):
+        """LPE_SPH_MODE_* flags (SPH_MODE_REF_CELL_CAP: the reference's 64-slot cells)."""
+        self._chk(lib().lpe_sph_set_mode(self._h, int(flags)), "lpe_sph_set_mode")
 
     def sph_diag(self, on=True):
         self._chk(lib().lpe_sph_diag(self._h, int(on)), "lpe_sph_diag")

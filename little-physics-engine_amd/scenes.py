@@ -208,6 +208,14 @@ def scene(name: str):
         fl = fluid_lattice(rng, 1024, 256, 0.5 * (U - 1024 * LATTICE_S), pool_top)
         return dict(U=U, fluid=fl, bodies=b, seed=seed,
                     desc="M: 1024x256 SPH pool + 4096 pentagons (128x32 @0.24 m), U=32")
+    if name == "C5":     # 2M SPH for the 8-GPU strong-scaling config: 2048 x 1024 lattice + 4 walls, U = 64 m
+        U, seed = 64.0, 5
+        rng = np.random.default_rng(seed)
+        b = Bodies()
+        add_walls(b, U)
+        fl = fluid_lattice(rng, 2048, 1024, 0.5 * (U - 2048 * LATTICE_S), U - 0.15 - 1024 * LATTICE_S)
+        return dict(U=U, fluid=fl, bodies=b, seed=seed,
+                    desc="C5: 2048x1024 SPH (51.2 x 25.6 m) + 4 walls, U=64")
     if name.startswith("MW"):   # M widened N x for weak scaling: N x 256k SPH, the same 4096-pentagon pile
         nw = int(name[2:] or 1)
         U, seed = 32.0 * nw, 6

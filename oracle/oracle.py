@@ -35,11 +35,11 @@ class Grid(C.Structure):
 
 
 class SubStats(C.Structure):
-    _fields_ = [("maxOcc", C.c_int), ("notInserted", C.c_int)]
+    _fields_ = [("maxOcc", C.c_int), ("notInserted", C.c_int), ("overCap", C.c_int)]
 
 
 class TickStats(C.Structure):
-    _fields_ = [("maxOcc", C.c_int), ("notInserted", C.c_int), ("grid", Grid)]
+    _fields_ = [("maxOcc", C.c_int), ("notInserted", C.c_int), ("grid", Grid), ("overCap", C.c_int)]
 
 
 _lib = None
@@ -94,6 +94,26 @@ def density(p, cfg=None):
     st = SubStats()
     lib().lpeo_density(p.ctypes.data, p.shape[0], C.byref(cfg), C.byref(g), C.byref(st))
     return p[:, 11].copy(), p[:, 12].copy(), g, st
+
+
+def set_threads(n: int):
+    """OpenMP threads of the oracle's particle loops (<= 0: all); the results
+    do not depend on it."""
+    lib().lpeo_set_threads(int(n))
+
+
+def get_threads() -> int:
+    return int(lib().lpeo_get_threads())
+
+
+def set_ref_cell_cap(on: bool):
+    """The reference's GPU_MAX_PER_CELL = 64 grid semantics (sph_oracle.c):
+    inserts past 64 dropped, readers loop to the unclamped count."""
+    lib().lpeo_set_ref_cell_cap(1 if on else 0)
+
+
+def ref_undefined() -> bool:
+    return bool(lib().lpeo_ref_undefined())
 
 
 def xacc_sum(values):

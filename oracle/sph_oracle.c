@@ -113,14 +113,16 @@ static void xacc_add(uint64_t *acc, float f) {
     memcpy(&u, &f, 4);
     uint32_t e = (u >> 23) & 0xffu, m = u & 0x7fffffu;
     if (e == 0 && m == 0) return;
-    if (e >= 127u + 64u) { xacc_range_error = 1; return; }
+    if (e >= 127u + 64u) { __atomic_store_n(&xacc_range_error, 1, __ATOMIC_RELAXED); return; }
     uint32_t M = e ? (m | 0x800000u) : m;
     int pos = (e ? (int)e - 150 : -149) + XACC_BIAS;
     uint64_t v = (uint64_t)M << (pos & 31);
     uint64_t lo = v & 0xffffffffull, hi = v >> 32;
     if (u >> 31) { lo = 0ull - lo; hi = 0ull - hi; }
-    acc[pos >> 5] += lo;
-    acc[(pos >> 5) + 1] += hi;
+    /* atomic: the oracle's particle loops run on OpenMP threads; integer
+     * adds commute, so the sum is the same in any order */
+    __atomic_fetch_add(&acc[pos >> 5], lo, __ATOMIC_RELAXED);
+    __atomic_fetch_add(&acc[(pos >> 5) + 1], hi, __ATOMIC_RELAXED);
 }
 
 static float xacc_round(const uint64_t *acc) {
@@ -153,6 +155,26 @@ static float xacc_round(const uint64_t *acc) {
     if (guard && (sticky || (kept & 1u))) kept++;
     float r = ldexpf((float)kept, p - XACC_BIAS);
     return neg ? -r : r;
+}
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+/* Threads of the per-particle loops (<= 0: OpenMP's default).  Every particle
+ * is computed exactly as in the serial loop, so results do not depend on it. */
+void lpeo_set_threads(int n) {
+#ifdef _OPENMP
+    omp_set_num_threads(n > 0 ? n : omp_get_num_procs());
+#else
+    (void)n;
+#endif
+}
+int lpeo_get_threads(void) {
+#ifdef _OPENMP
+    return omp_get_max_threads();
+#else
+    return 1;
+#endif
 }
 
 /* Test hook: the exact, once-rounded sum of n floats (-1e30f on a range error). */
@@ -220,7 +242,36 @@ void lpeo_assign_cells(const lpeo_particle *p, int n, const lpeo_grid *g,
  * cells, metal:272-283) visits each cell's list in that order.  The quadrant
  * of a particle is floor(2t) - 2 floor(t) with t = (x + eps) / cellSize, so it
  * is consistent with the cell index bit for bit. start has C+1 entries. */
-typedef struct { int32_t *start; int32_t *idx; int C; int maxOcc; int notIns; } cells_t;
+typedef struct {
+    int32_t *start; int32_t *idx; int C; int maxOcc; int notIns;
+    int overCap;          /* cells holding more than GPU_MAX_PER_CELL particles  */
+    int32_t *F;           /* reference cell-capacity mode: the grid buffer      */
+} cells_t;
+
+/* Reference cell-capacity mode (lpeo_set_ref_cell_cap).  The reference's grid
+ * is an array of GPUGridCell {int count; int indices[64];} (fluid.hpp:56-61,
+ * 65 ints per cell), memset to 0 every sub-step (fluid.cpp:821-824).
+ * assignCells increments count for every particle but stores only the first
+ * 64 indices (fluid_kernels.metal:237-240); the readers loop c < count
+ * UNCLAMPED over indices[c] (:281-283, :349-351), so past 64 they read the
+ * next cell's count and indices (a flat 65-int stride), skipping values
+ * >= particleCount.  Insertion order is the canonical cell order above (the
+ * reference's is atomic arrival order).  F is that buffer, read exactly as
+ * the kernels read it; a read past the last cell (undefined in the
+ * reference: stale or out-of-bounds memory) sets lpeo_ref_undefined. */
+#define REF_MAX_PER_CELL 64
+#define REF_CELL_INTS (REF_MAX_PER_CELL + 1)
+static int ref_cap_mode = 0;
+static int ref_undefined = 0;
+void lpeo_set_ref_cell_cap(int on) { ref_cap_mode = on ? 1 : 0; }
+int lpeo_ref_undefined(void) { return ref_undefined; }
+
+/* indices[k] of cell c as the reference kernels read it (k may exceed 63) */
+static int ref_index(const cells_t *cl, int c, int k) {
+    long pos = (long)REF_CELL_INTS * c + 1 + k;
+    if (pos >= (long)REF_CELL_INTS * cl->C) { __atomic_store_n(&ref_undefined, 1, __ATOMIC_RELAXED); return 0; }
+    return cl->F[pos];
+}
 
 static int quad_of(const lpeo_grid *g, float eps, float x, float y) {
     float tx = (x + eps) / g->cellSize, ty = (y + eps) / g->cellSize;
@@ -259,8 +310,21 @@ static void build_cells(const lpeo_particle *p, int n, const lpeo_grid *g,
     free(cur);
     free(bstart);
     free(bin);
+    cl->overCap = 0;
+    cl->F = NULL;
+    for (int c = 0; c < C; c++)
+        if (cl->start[c + 1] - cl->start[c] > REF_MAX_PER_CELL) cl->overCap++;
+    if (ref_cap_mode) {                 /* assignCells into the memset grid buffer */
+        cl->F = (int32_t *)calloc((size_t)REF_CELL_INTS * (C > 0 ? C : 1), sizeof(int32_t));
+        for (int c = 0; c < C; c++) {
+            int cnt = cl->start[c + 1] - cl->start[c];
+            cl->F[(size_t)REF_CELL_INTS * c] = cnt;
+            for (int k = 0; k < cnt && k < REF_MAX_PER_CELL; k++)
+                cl->F[(size_t)REF_CELL_INTS * c + 1 + k] = cl->idx[cl->start[c] + k];
+        }
+    }
 }
-static void free_cells(cells_t *cl) { free(cl->start); free(cl->idx); }
+static void free_cells(cells_t *cl) { free(cl->start); free(cl->idx); free(cl->F); }
 
 /* computeDensity (fluid_kernels.metal:246-307) for particle i. */
 static void density_one(lpeo_particle *p, int n, int i, const lpeo_grid *g,
@@ -280,8 +344,10 @@ static void density_one(lpeo_particle *p, int n, int i, const lpeo_grid *g,
             int cx = cellX + nx, cy = cellY + ny;
             if (cx < 0 || cx >= g->gridDimX || cy < 0 || cy >= g->gridDimY) continue;
             int c = cy * g->gridDimX + cx;
-            for (int k = cl->start[c]; k < cl->start[c + 1]; k++) {
-                int j = cl->idx[k];
+            int kb = cl->start[c], ke = cl->start[c + 1];
+            if (cl->F) { kb = 0; ke = cl->F[(size_t)REF_CELL_INTS * c]; }     /* count */
+            for (int k = kb; k < ke; k++) {
+                int j = cl->F ? ref_index(cl, c, k) : cl->idx[k];
                 if (j >= n) continue;
                 float dx = xi - p[j].x, dy = yi - p[j].y;
                 float r2 = dx * dx + dy * dy;
@@ -315,8 +381,10 @@ static void forces_one(const lpeo_particle *p, int n, int i, const lpeo_grid *g,
             int cx = cellX + nx, cy = cellY + ny;
             if (cx < 0 || cx >= g->gridDimX || cy < 0 || cy >= g->gridDimY) continue;
             int c = cy * g->gridDimX + cx;
-            for (int k = cl->start[c]; k < cl->start[c + 1]; k++) {
-                int j = cl->idx[k];
+            int kb = cl->start[c], ke = cl->start[c + 1];
+            if (cl->F) { kb = 0; ke = cl->F[(size_t)REF_CELL_INTS * c]; }
+            for (int k = kb; k < ke; k++) {
+                int j = cl->F ? ref_index(cl, c, k) : cl->idx[k];
                 if (j == i || j >= n) continue;
                 const lpeo_particle nb = p[j];
                 float dx = xi - nb.x, dy = yi - nb.y;
@@ -561,9 +629,10 @@ void lpeo_density(lpeo_particle *p, int n, const lpe_fluid_config *cfg, lpeo_gri
     build_cells(p, n, &g, cfg->gridConfig.gridEpsilon, &cl);
     float *rho = (float *)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
     float *pr = (float *)malloc(sizeof(float) * (size_t)(n > 0 ? n : 1));
+    #pragma omp parallel for schedule(dynamic, 1024)
     for (int i = 0; i < n; i++) density_one(p, n, i, &g, &cl, cfg, &rho[i], &pr[i]);
     for (int i = 0; i < n; i++) { p[i].density = rho[i]; p[i].pressure = pr[i]; }
-    if (st) { st->maxOcc = cl.maxOcc; st->notInserted = cl.notIns; }
+    if (st) { st->maxOcc = cl.maxOcc; st->notInserted = cl.notIns; st->overCap = cl.overCap; }
     if (g_out) *g_out = g;
     free(rho); free(pr);
     free_cells(&cl);
@@ -590,6 +659,7 @@ int lpeo_fluid_tick(const lpe_fluid_config *cfg, double dt_tick,
     float *pr = (float *)malloc(sizeof(float) * (size_t)n);
     uint64_t *acq = (uint64_t *)calloc((size_t)(nr > 0 ? nr : 1) * 3 * XACC_LIMBS, sizeof(uint64_t));
     xacc_range_error = 0;
+    ref_undefined = 0;
     for (int step = 0; step < cfg->numSubSteps; step++) {
         /* velocityVerletHalf (fluid_kernels.metal:408-423) */
         for (int i = 0; i < n; i++) {
@@ -605,10 +675,13 @@ int lpeo_fluid_tick(const lpe_fluid_config *cfg, double dt_tick,
         if (st) {
             if (cl.maxOcc > st->maxOcc) st->maxOcc = cl.maxOcc;
             st->notInserted = cl.notIns;
+            st->overCap += cl.overCap;
             st->grid = g;
         }
+        #pragma omp parallel for schedule(dynamic, 1024)
         for (int i = 0; i < n; i++) density_one(p, n, i, &g, &cl, cfg, &rho[i], &pr[i]);
         for (int i = 0; i < n; i++) { p[i].density = rho[i]; p[i].pressure = pr[i]; }
+        #pragma omp parallel for schedule(dynamic, 1024)
         for (int i = 0; i < n; i++) forces_one(p, n, i, &g, &cl, cfg, &ax[i], &ay[i]);
         for (int i = 0; i < n; i++) { p[i].ax = ax[i]; p[i].ay = ay[i]; }
         /* velocityVerletFinish (fluid_kernels.metal:428-441) */
@@ -617,7 +690,9 @@ int lpeo_fluid_tick(const lpe_fluid_config *cfg, double dt_tick,
             p[i].vy = p[i].vyHalf + halfDt * p[i].ay;
         }
         if (nr > 0)
+            #pragma omp parallel for schedule(dynamic, 1024)
             for (int i = 0; i < n; i++) impulse_one(&p[i], rigids, nr, cfg, subDt, acq);
+        #pragma omp parallel for schedule(dynamic, 1024)
         for (int i = 0; i < n; i++) position_one(&p[i], rigids, nr, cfg);
         free_cells(&cl);
     }

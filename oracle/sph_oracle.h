@@ -20,8 +20,9 @@ typedef struct lpeo_grid {
     float bbox[4]; /* minX, maxX, minY, maxY of the particles */
 } lpeo_grid;
 
-typedef struct lpeo_sub_stats { int maxOcc; int notInserted; } lpeo_sub_stats;
-typedef struct lpeo_tick_stats { int maxOcc; int notInserted; lpeo_grid grid; } lpeo_tick_stats;
+typedef struct lpeo_sub_stats { int maxOcc; int notInserted; int overCap; } lpeo_sub_stats;
+/* overCap: cells over GPU_MAX_PER_CELL, summed over the sub-steps */
+typedef struct lpeo_tick_stats { int maxOcc; int notInserted; lpeo_grid grid; int overCap; } lpeo_tick_stats;
 
 void lpeo_fluid_config_default(lpe_fluid_config *c);
 void lpeo_grid_from_bbox(const lpeo_particle *p, int n, float smoothingLength, lpeo_grid *g);
@@ -39,6 +40,14 @@ int lpeo_fluid_tick(const lpe_fluid_config *cfg, double dt_tick,
 /* Exact sum of n floats rounded once to nearest even (the coupling
  * accumulators' arithmetic); -1e30f if a value is outside the range. */
 float lpeo_xacc_sum(const float *v, int n);
+/* Reference cell-capacity semantics on (1) / off (0, default: unbounded cell
+ * lists); see sph_oracle.c.  lpeo_ref_undefined() reports a read past the
+ * last cell since the last tick started (undefined in the reference). */
+void lpeo_set_ref_cell_cap(int on);
+/* OpenMP threads of the particle loops (results are independent of it). */
+void lpeo_set_threads(int n);
+int lpeo_get_threads(void);
+int lpeo_ref_undefined(void);
 
 #ifdef __cplusplus
 }

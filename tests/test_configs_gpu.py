@@ -1,0 +1,140 @@
+"""Full-size parity at BASELINE.json's configs.
+
+C2 (64k SPH dam break), C4 (256k SPH + 512 pentagons) and the metric scene M
+(256k SPH + 4096 pentagons) are advanced on the device until they are in
+motion (C2: the dam has broken; C4, M: the pentagons are in the fluid and M's
+pile has settled), then ONE full world tick (lpe_world_tick: every system of
+sim.cpp:107-114) from that exact state runs on the device and on the oracle
+(OpenMP over particles; results are thread-count independent).  The fluid
+must be bit-identical, the bodies within the fp64-transcendental bar of
+tests/test_world_gpu.py.
+
+The reference cell-capacity mode (LPE_SPH_MODE_REF_CELL_CAP) is the
+reference's own grid semantics; M's settled pool compresses cells past the
+reference's 64 slots, so there the check covers the reference's dropped
+inserts and cross-cell reads, and the default (unbounded) mode is checked
+too.  C5 (2M particles, the 8-GPU config) is checked as 8 slab ranks through
+the in-process transport against the single domain."""
+import importlib.util
+import os
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import lpe, scenes
+
+pytestmark = pytest.mark.gpu
+DT = 1.0 / 120.0
+
+_spec = importlib.util.spec_from_file_location(
+    "slab", os.path.join(os.path.dirname(lpe.__file__), "slab.py"))
+slab = importlib.util.module_from_spec(_spec)
+sys.modules["slab"] = slab
+_spec.loader.exec_module(slab)
+
+
+def _world_ctx(U, fl, bodies, verts, mode=0):
+    ctx = lpe.Context(0)
+    ctx.sph_set_config(lpe.default_fluid_config())
+    ctx.rigid_set_config(lpe.rigid_config(universe=U))
+    ctx.rigid_upload(bodies, verts)
+    ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+    ctx.world_set_coupling(np.arange(len(bodies) - 1, -1, -1, dtype=np.int32))
+    ctx.sph_set_mode(mode)
+    return ctx
+
+
+_STATE = {}
+
+
+def _advanced(name, prep):
+    """The scene after `prep` device ticks (cached per session)."""
+    key = (name, prep)
+    if key not in _STATE:
+        s = scenes.scene(name)
+        b, v = scenes.to_bodies(s["bodies"])
+        ctx = _world_ctx(s["U"], s["fluid"], b, v)
+        try:
+            ctx.world_tick(DT, prep)
+            out = ctx.sph_download()
+            fl = dict(x=out["x"], y=out["y"], vx=out["vx"], vy=out["vy"], mass=s["fluid"]["mass"],
+                      density=out["density"], pressure=out["pressure"])
+            _STATE[key] = (s, fl, ctx.rigid_download(), v)
+        finally:
+            ctx.close()
+    return _STATE[key]
+
+
+@pytest.mark.parametrize("name,prep,mode", [
+    ("C2", 30, lpe.SPH_MODE_REF_CELL_CAP),
+    ("C4", 90, lpe.SPH_MODE_REF_CELL_CAP),
+    ("M", 240, lpe.SPH_MODE_REF_CELL_CAP),
+    ("M", 240, 0),
+])
+def test_config_world_tick_bit_exact(oracle_mod, name, prep, mode):
+    s, fl, bodies, verts = _advanced(name, prep)
+    ctx = _world_ctx(s["U"], fl, bodies, verts, mode)
+    try:
+        ctx.world_tick(DT, 1)
+        out = ctx.sph_download()
+        got_b = ctx.rigid_download()
+        st = ctx.sph_stats()
+    finally:
+        ctx.close()
+    oracle_mod.set_threads(0)
+    oracle_mod.set_ref_cell_cap(bool(mode))
+    try:
+        couple = np.arange(len(bodies) - 1, -1, -1, dtype=np.int32)
+        p, rb = oracle_mod.world_tick(lpe.default_fluid_config(), lpe.rigid_config(universe=s["U"]),
+                                      scenes.particles_aos(fl), bodies, verts, couple, DT, 1)
+        assert not oracle_mod.ref_undefined()
+    finally:
+        oracle_mod.set_ref_cell_cap(False)
+    assert st["refUndefined"] == 0
+    if name == "M":                  # the metric config is outside the reference's 64-slot envelope
+        assert st["overCapCells"] > 0 and st["maxCellOccupancy"] > 64
+    for k, col in (("x", 0), ("y", 1), ("vx", 2), ("vy", 3), ("density", 11), ("pressure", 12)):
+        np.testing.assert_array_equal(out[k], p[:, col], err_msg=(name, k, st))
+    for k in ("x", "y", "angle"):
+        np.testing.assert_allclose(got_b[k], rb[k], rtol=1e-9, atol=1e-12, err_msg=(name, k))
+    for k in ("vx", "vy", "omega"):
+        np.testing.assert_allclose(got_b[k], rb[k], rtol=1e-5, atol=1e-6, err_msg=(name, k))
+
+
+def test_c5_eight_slab_ranks_bit_exact():
+    """C5 (2,097,152 particles): 8 x-slab ranks (in-process transport, one
+    GPU) against the single domain, 2 full world ticks: every particle and
+    wall bit for bit."""
+    s = scenes.scene("C5")
+    fl = s["fluid"]
+    n = len(fl["x"])
+    b, v = scenes.to_bodies(s["bodies"])
+    one = _world_ctx(s["U"], fl, b, v)
+    try:
+        one.world_tick(DT, 2)
+        ref = one.sph_download()
+        rb_ref = one.rigid_download()
+    finally:
+        one.close()
+    edges = slab.slab_edges(fl["x"], 8)
+    ctxs = [lpe.Context(0) for _ in range(8)]
+    try:
+        for r, c in enumerate(ctxs):
+            c.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+            c.rigid_upload(b, v)
+            slab.setup_rank(c, r, 8, fl, edges, lpe.default_fluid_config())
+            c.world_set_coupling(np.arange(len(b) - 1, -1, -1, dtype=np.int32))
+        lpe.mg_loopback_run(ctxs, 2, world=lpe.WorldConfig(DT, 1.0, 1.0, 1.0))
+        parts = [c.sph_download_owned(cap=n) for c in ctxs]
+        rbs = [c.rigid_download() for c in ctxs]
+    finally:
+        for c in ctxs:
+            c.close()
+    assert min(len(p["id"]) for p in parts) > 0
+    got = slab.merge_owned(parts, n)
+    for k in slab.FIELDS:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    for r in rbs:
+        for k in ("x", "y", "vx", "vy"):
+            np.testing.assert_array_equal(r[k], rb_ref[k], err_msg=k)

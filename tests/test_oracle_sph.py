@@ -182,3 +182,109 @@ def test_xacc_sum_cancellation_and_ties(oracle_mod):
     assert oracle_mod.xacc_sum(np.array([-0.5, -0.25], np.float32)) == f32(-0.75)
     assert oracle_mod.xacc_sum(np.zeros(0, np.float32)) == f32(0)
     assert oracle_mod.xacc_sum(np.array([2.0 ** 64], np.float32)) == f32(-1e30)   # range error
+
+
+def compressed_scene(extra=90, seed=3):
+    """A 16 x 16 lattice (16 particles per 2h cell) plus `extra` particles
+    squeezed into one cell: that cell exceeds GPU_MAX_PER_CELL = 64."""
+    rng = np.random.default_rng(seed)
+    s = scenes.LATTICE_S
+    gx, gy = np.meshgrid(np.arange(16), np.arange(16))
+    x = 1.0 + (gx.ravel() + 0.5) * s + rng.uniform(-0.1, 0.1, 256) * s
+    y = 1.0 + (gy.ravel() + 0.5) * s + rng.uniform(-0.1, 0.1, 256) * s
+    cx, cy = 1.2 + 0.05, 1.2 + 0.05                       # inside cell (12, 12) of the 0.1 m grid
+    x = np.concatenate([x, cx + rng.uniform(-0.045, 0.045, extra)])
+    y = np.concatenate([y, cy + rng.uniform(-0.045, 0.045, extra)])
+    n = len(x)
+    return dict(x=x, y=y, vx=rng.uniform(-0.1, 0.1, n), vy=rng.uniform(-0.1, 0.1, n),
+                mass=np.full(n, scenes.FLUID_MASS), density=np.zeros(n), pressure=np.zeros(n))
+
+
+def ref_cap_density_numpy(p):
+    """computeDensity (metal:246-307) over the reference's GPUGridCell buffer
+    (count + 64 indices per cell, memset each sub-step, fluid.hpp:56-61,
+    fluid.cpp:821-824; inserts past 64 dropped, metal:237-240), read with the
+    unclamped loop (metal:281-283), insertion order = cell quadrant then
+    index.  Plain numpy fp32, independent of the oracle."""
+    cells, (gmx, gmy, dx, dy) = ref_cells_numpy(p)
+    n = len(p)
+    cs = f32(0.1)
+    eps = f32(1e-6)
+    C = dx * dy
+    buf = np.zeros(65 * C, np.int64)
+    quad = []
+    for i in range(n):
+        tx = (p[i, 0] + eps) / cs
+        ty = (p[i, 1] + eps) / cs
+        qx = int(np.floor(f32(2) * tx)) - 2 * int(np.floor(tx))
+        qy = int(np.floor(f32(2) * ty)) - 2 * int(np.floor(ty))
+        quad.append(qy * 2 + qx)
+    for c in range(C):
+        mem = sorted((quad[i], i) for i in np.nonzero(cells == c)[0])
+        buf[65 * c] = len(mem)
+        for k, (_, i) in enumerate(mem[:64]):
+            buf[65 * c + 1 + k] = i
+    h = f32(0.05)
+    h2 = h * h
+    h4 = h2 * h2
+    poly6 = f32(4.0) / (PI_F * (h4 * h4))
+    rho = np.zeros(n, np.float32)
+    for i in range(n):
+        xi, yi = p[i, 0], p[i, 1]
+        cX = int(np.floor((xi + eps) / cs)) - gmx
+        cY = int(np.floor((yi + eps) / cs)) - gmy
+        acc = f32(0)
+        for ny in (-1, 0, 1):
+            for nx in (-1, 0, 1):
+                cx, cy = cX + nx, cY + ny
+                if cx < 0 or cx >= dx or cy < 0 or cy >= dy:
+                    continue
+                c = cy * dx + cx
+                for k in range(int(buf[65 * c])):
+                    pos = 65 * c + 1 + k
+                    assert pos < 65 * C
+                    j = int(buf[pos])
+                    if j >= n:
+                        continue
+                    ddx = xi - p[j, 0]
+                    ddy = yi - p[j, 1]
+                    r2 = ddx * ddx + ddy * ddy
+                    if r2 < h2:
+                        diff = h2 - r2
+                        acc = f32(acc + p[j, 8] * (poly6 * diff * diff * diff))
+        rho[i] = acc
+    return rho
+
+
+def test_ref_cell_cap_density_known_answer(oracle_mod):
+    """The oracle's reference cell-capacity mode equals the literal numpy
+    restatement bit for bit on a scene with an over-full cell, and differs
+    from the unbounded default there (the reference drops and mis-reads)."""
+    fl = compressed_scene()
+    p = scenes.particles_aos(fl)
+    want = ref_cap_density_numpy(p)
+    oracle_mod.set_ref_cell_cap(True)
+    try:
+        rho, pr, g, st = oracle_mod.density(p)
+    finally:
+        oracle_mod.set_ref_cell_cap(False)
+    assert st.overCap == 1 and st.maxOcc > 64
+    np.testing.assert_array_equal(rho, want)
+    rho0, _, _, _ = oracle_mod.density(p)
+    assert (rho0 != rho).sum() > 0
+
+
+def test_ref_cell_cap_is_default_below_64(oracle_mod):
+    """Without an over-full cell the capacity mode is the default, bit for bit."""
+    s = scenes.scene("small64_8")
+    p = scenes.particles_aos(s["fluid"])
+    rig = scenes.gather_rigids(s["bodies"])
+    a = oracle_mod.fluid_tick(p, rig, 1.0 / 120.0)
+    oracle_mod.set_ref_cell_cap(True)
+    try:
+        b = oracle_mod.fluid_tick(p, rig, 1.0 / 120.0)
+    finally:
+        oracle_mod.set_ref_cell_cap(False)
+    assert b[3].overCap == 0
+    np.testing.assert_array_equal(a[0], b[0])
+    np.testing.assert_array_equal(a[2], b[2])

@@ -148,3 +148,86 @@ def test_multi_tick_invariants(gpu_ctx):
     st = gpu_ctx.sph_stats()
     assert st["capacityOverflow"] == 0
     assert 0 < st["maxCellOccupancy"] <= 64
+
+
+# ---- reference cell-capacity mode (LPE_SPH_MODE_REF_CELL_CAP) ----------------
+from test_oracle_sph import compressed_scene  # noqa: E402
+
+
+def _crowd_rigids():
+    """Walls of a 3 m universe and two pentagons over the crowded region."""
+    b = scenes.Bodies()
+    scenes.add_walls(b, 3.0)
+    for (x, y, r) in ((1.12, 1.1, 0.08), (1.3, 1.33, 0.1)):
+        v = scenes.regular_polygon(5, r)
+        b.add(x=x, y=y, vx=0.1, vy=0.3, mass=5.0, verts=v, has_angvel=True, has_inertia=True,
+              inertia=scenes.polygon_inertia(v, 5.0), omega=0.5)
+    return scenes.gather_rigids(b)
+
+
+def test_ref_cell_cap_density_bit_exact(gpu_ctx, oracle_mod):
+    """An over-full cell (> 64): the device's literal reference walk equals
+    the oracle's 65-int grid buffer read, bit for bit."""
+    fl = compressed_scene()
+    _upload(gpu_ctx, fl)
+    gpu_ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP)
+    try:
+        rho, p = gpu_ctx.sph_probe_density()
+        st = gpu_ctx.sph_stats()
+    finally:
+        gpu_ctx.sph_set_mode(0)
+    oracle_mod.set_ref_cell_cap(True)
+    try:
+        rrho, rp, g, ost = oracle_mod.density(scenes.particles_aos(fl))
+    finally:
+        oracle_mod.set_ref_cell_cap(False)
+    assert st["overCapCells"] == ost.overCap == 1 and st["refUndefined"] == 0
+    np.testing.assert_array_equal(rho, rrho)
+    np.testing.assert_array_equal(p, rp)
+    rho0, _ = gpu_ctx.sph_probe_density()             # default mode: unbounded lists
+    assert (rho0 != rho).sum() > 0
+
+
+@pytest.mark.parametrize("extra", [90, 300])
+def test_ref_cell_cap_tick_bit_exact(gpu_ctx, oracle_mod, extra):
+    """One coupled tick (10 sub-steps) in the capacity mode with an over-full
+    cell (300 extra: the unclamped read runs several cells ahead)."""
+    fl = compressed_scene(extra=extra)
+    rig = _crowd_rigids()
+    _upload(gpu_ctx, fl, rig)
+    gpu_ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP)
+    try:
+        gpu_ctx.sph_step(DT)
+        out = gpu_ctx.sph_download()
+        r_out, acc = gpu_ctx.sph_download_rigids()
+        st = gpu_ctx.sph_stats()
+    finally:
+        gpu_ctx.sph_set_mode(0)
+    oracle_mod.set_ref_cell_cap(True)
+    try:
+        ref, rref, racc, ost = oracle_mod.fluid_tick(scenes.particles_aos(fl), rig, DT)
+        assert not oracle_mod.ref_undefined()
+    finally:
+        oracle_mod.set_ref_cell_cap(False)
+    assert st["overCapCells"] == ost.overCap > 0
+    assert np.abs(racc).sum() > 0
+    for k, col in (("x", 0), ("y", 1), ("vx", 2), ("vy", 3), ("vxHalf", 4), ("vyHalf", 5),
+                   ("ax", 6), ("ay", 7), ("density", 11), ("pressure", 12)):
+        np.testing.assert_array_equal(out[k], ref[:, col], err_msg=k)
+    np.testing.assert_array_equal(acc, racc)
+
+
+def test_ref_cell_cap_equals_default_below_64(gpu_ctx, oracle_mod):
+    s = scenes.scene("small64_8")
+    rig = scenes.gather_rigids(s["bodies"])
+    _upload(gpu_ctx, s["fluid"], rig)
+    gpu_ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP)
+    try:
+        gpu_ctx.sph_step(DT)
+        out = gpu_ctx.sph_download()
+        assert gpu_ctx.sph_stats()["overCapCells"] == 0
+    finally:
+        gpu_ctx.sph_set_mode(0)
+    ref, _, _, _ = oracle_mod.fluid_tick(scenes.particles_aos(s["fluid"]), rig, DT)
+    for k, col in (("x", 0), ("y", 1), ("vx", 2), ("vy", 3), ("density", 11)):
+        np.testing.assert_array_equal(out[k], ref[:, col], err_msg=k)

@@ -167,3 +167,88 @@ def test_world_one_tick_bounces(gpu_ctx, oracle_mod):
         np.testing.assert_allclose(bodies[k], rb[k], rtol=1e-9, atol=1e-12, err_msg=k)
     for k in ("vx", "vy", "omega"):
         np.testing.assert_allclose(bodies[k], rb[k], rtol=1e-5, atol=1e-6, err_msg=k)
+
+
+def test_world_one_tick_calls_equal_multi_tick(oracle_mod):
+    """The drop-in path calls lpe_world_tick once per ECSSimulator::tick; the
+    next tick's first sub-step is prelaunched at the end of every call (it
+    writes only scratch), so downloads, stats and a probe between the calls
+    see the end-of-tick state, and 5 one-tick calls equal one 5-tick call
+    bit for bit."""
+    s = scenes.scene("small64_8")
+    fl = s["fluid"]
+    b, v = scenes.to_bodies(s["bodies"])
+    runs = []
+    for mode in ("loop", "one"):
+        ctx = lpe.Context(0)
+        try:
+            ctx.sph_set_config(lpe.default_fluid_config())
+            ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+            ctx.rigid_upload(b, v)
+            ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+            ctx.world_set_coupling(np.arange(len(b) - 1, -1, -1, dtype=np.int32))
+            if mode == "loop":
+                mids = []
+                for t in range(5):
+                    ctx.world_tick(DT, 1)
+                    mids.append(ctx.sph_download())        # joins the pending prelaunch
+                    ctx.sph_stats()
+                # the state after tick 1 is the oracle's after one tick
+                p1, _ = oracle_mod.world_tick(lpe.default_fluid_config(), lpe.rigid_config(universe=s["U"]),
+                                              scenes.particles_aos(fl), b, v,
+                                              np.arange(len(b) - 1, -1, -1, dtype=np.int32), DT, 1)
+                np.testing.assert_array_equal(mids[0]["x"], p1[:, 0])
+                np.testing.assert_array_equal(mids[0]["vy"], p1[:, 3])
+            else:
+                ctx.world_tick(DT, 5)
+            runs.append((ctx.sph_download(), ctx.rigid_download()))
+        finally:
+            ctx.close()
+    (fa, ba), (fb, bb) = runs
+    for k in ("x", "y", "vx", "vy", "density", "pressure"):
+        np.testing.assert_array_equal(fa[k], fb[k], err_msg=k)
+    for k in ("x", "y", "angle", "vx", "vy", "omega"):
+        np.testing.assert_array_equal(ba[k], bb[k], err_msg=k)
+
+
+def test_prelaunch_voided_by_probe_and_upload(gpu_ctx):
+    """A probe (its own hash) and a re-upload between world ticks discard the
+    pending prelaunch; the following ticks equal a fresh run's."""
+    s = scenes.scene("small64_0")
+    fl = s["fluid"]
+    b, v = scenes.to_bodies(s["bodies"])
+
+    def fresh(nt):
+        ctx = lpe.Context(0)
+        try:
+            ctx.sph_set_config(lpe.default_fluid_config())
+            ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+            ctx.rigid_upload(b, v)
+            ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+            ctx.world_set_coupling(np.arange(len(b) - 1, -1, -1, dtype=np.int32))
+            ctx.world_tick(DT, nt)
+            return ctx.sph_download()
+        finally:
+            ctx.close()
+    want = fresh(3)
+    ctx = lpe.Context(0)
+    try:
+        ctx.sph_set_config(lpe.default_fluid_config())
+        ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+        ctx.rigid_upload(b, v)
+        ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+        ctx.world_set_coupling(np.arange(len(b) - 1, -1, -1, dtype=np.int32))
+        ctx.world_tick(DT, 2)
+        ctx.sph_probe_density()                  # voids the prelaunch
+        ctx.world_tick(DT, 1)
+        got = ctx.sph_download()
+        # a re-upload of the start state voids it too: 3 ticks again
+        ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+        ctx.rigid_upload(b, v)
+        ctx.world_tick(DT, 3)
+        again = ctx.sph_download()
+    finally:
+        ctx.close()
+    for k in ("x", "y", "vx", "vy", "density"):
+        np.testing.assert_array_equal(got[k], want[k], err_msg=k)
+        np.testing.assert_array_equal(again[k], want[k], err_msg=k)
