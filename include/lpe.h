@@ -339,6 +339,14 @@ int  lpe_rigid_upload(lpe_ctx *ctx, int nb, const lpe_body *bodies, int nverts,
  * unordered_map's order, contact_manager.cpp:169-245).  stats->pgsLevels and
  * posLevels report the colour count. */
 int  lpe_rigid_step(lpe_ctx *ctx, lpe_rigid_stats *stats);
+/* Pre-size the pair and contact buffers of lpe_rigid_step (re-allocated at
+ * exactly these capacities; the defaults are 16 pairs and 64 contacts per
+ * body).  A step whose pairs or contacts exceed them grows them and redoes
+ * its detection (never a truncated list); lpe_rigid_buffer_info reports the
+ * capacities and how often that happened.  Replaces the grow-only sizing of
+ * the reference's per-pair std::vectors (narrowphase.cpp:352-420). */
+int  lpe_rigid_reserve(lpe_ctx *ctx, int pairs, int contacts);
+int  lpe_rigid_buffer_info(lpe_ctx *ctx, int *pairs, int *contacts, int *regrows);
 /* Colour of each pair of the last lpe_rigid_step (-1: pair without contacts),
  * for the parity harness; cap entries at most, *ncolours the colour count. */
 int  lpe_rigid_download_colours(lpe_ctx *ctx, int cap, int32_t *pair_colour, int32_t *ncolours);

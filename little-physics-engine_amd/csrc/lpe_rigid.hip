@@ -474,7 +474,7 @@ __global__ void k_bg_pairs(int nb, int mode, const int32_t *__restrict__ byRank,
 __global__ void __launch_bounds__(128)
 k_narrow(const int32_t *__restrict__ npptr, int cap, const int2 *__restrict__ pairs,
          const lpe_body *__restrict__ bodies, const double *__restrict__ verts,
-         lpe_contact *__restrict__ slots, int32_t *__restrict__ ccount) {
+         lpe_contact *__restrict__ slots, int32_t *__restrict__ ccount, int32_t *__restrict__ counts) {
     int k = blockIdx.x * blockDim.x + threadIdx.x;
     // the pair count can exceed the buffers when they overflowed (the step
     // then grows them and redoes the broadphase): never past the capacity
@@ -526,6 +526,9 @@ k_narrow(const int32_t *__restrict__ npptr, int cap, const int2 *__restrict__ pa
                 int m2 = clip_face(t1, m1, edge, dot(edge, v2), t2);
                 int m3 = clip_face(t2, m2, botN, dot(botN, v1), t1);
                 double planeOff = dot(refN, v1);
+                // at most nbv + 3 <= 35 < MAXC clipped points (MAXV = 32):
+                // never truncated, but a truncation would be reported
+                if (m3 > MAXC) atomicOr(&counts[11], 1);
                 for (int q = 0; q < m3 && cnt < MAXC; q++) {
                     c.pen = -(dot(refN, t1[q]) - planeOff);
                     c.px = t1[q].x; c.py = t1[q].y;
@@ -1732,6 +1735,8 @@ static int rgrow(lpe_ctx *ctx, T **p, size_t n) {
 int lpe_rigid_destroy_internal(lpe_ctx *ctx) {
     RigidDev *d = (RigidDev *)ctx->rigid;
     if (!d) return LPE_OK;
+    if (d->side) (void)hipStreamSynchronize(d->side);      // nothing may still use the buffers
+    if (d->psolve) (void)hipStreamSynchronize(d->psolve);
     void *ptrs[] = {d->bodies, d->verts, d->rank, d->byRank, d->aabb, d->cand, d->pcount, d->pstart,
                     d->pcursor, d->pairs, d->pairRankB, d->cslots, d->ccount, d->cstart, d->contacts,
                     d->bsum, d->order, d->rowN, d->rowR, d->rowAB, d->vel0, d->imii, d->inContact,
@@ -1741,9 +1746,10 @@ int lpe_rigid_destroy_internal(lpe_ctx *ctx) {
                     d->bgList, d->bgKey, d->bgSpecial, d->bbits};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     if (d->hc) (void)hipHostFree(d->hc);
-    hipEvent_t evs[] = {d->evStart, d->evDetect, d->evColour};
+    hipEvent_t evs[] = {d->evStart, d->evDetect, d->evColour, d->evFork, d->evJoin};
     for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
     if (d->side) (void)hipStreamDestroy(d->side);
+    if (d->psolve) (void)hipStreamDestroy(d->psolve);
     delete d;
     ctx->rigid = nullptr;
     return LPE_OK;
@@ -1957,6 +1963,7 @@ static int detect_launch(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pa
     // [0..3], [6] (counts[4], [5] belong to the solvers / gravity; [7]: solver fault, sticky)
     LPE_HIP(ctx, hipMemsetAsync(d->counts, 0, sizeof(int32_t) * 4, s));
     LPE_HIP(ctx, hipMemsetAsync(d->counts + 6, 0, sizeof(int32_t), s));
+    LPE_HIP(ctx, hipMemsetAsync(d->counts + 11, 0, sizeof(int32_t), s));
     if (pairs_in) {
         if (np_in > d->cap_pairs) {
             int st = rigid_alloc_pairs(ctx, d, np_in + 1024);
@@ -2004,10 +2011,10 @@ static int detect_launch(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pa
         LPE_KERNEL(ctx, "k_bp_sort_long", k_bp_sort_long, dim3(nb), dim3(RTPB), 0, s, nb, d->pstart, d->pairs, d->pairRankB, d->cap_pairs);
         LPE_HIP(ctx, hipMemcpyAsync(d->counts, d->pstart + nb, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
     }
-    LPE_KERNEL(ctx, "k_narrow", k_narrow, dim3(rblk(d->cap_pairs, 128)), dim3(128), 0, s, d->counts, d->cap_pairs, d->pairs, d->bodies, d->verts, d->cslots, d->ccount);
+    LPE_KERNEL(ctx, "k_narrow", k_narrow, dim3(rblk(d->cap_pairs, 128)), dim3(128), 0, s, d->counts, d->cap_pairs, d->pairs, d->bodies, d->verts, d->cslots, d->ccount, d->counts);
     int st = rscan(ctx, d, d->counts, d->cap_pairs, d->ccount, d->cstart, nullptr, s);
     if (st) return st;
-    LPE_HIP(ctx, hipMemcpyAsync(hc, d->counts, sizeof(int32_t) * 8, hipMemcpyDeviceToHost, s));
+    LPE_HIP(ctx, hipMemcpyAsync(hc, d->counts, sizeof(int32_t) * 12, hipMemcpyDeviceToHost, s));
     return LPE_OK;
 }
 
@@ -2022,12 +2029,18 @@ static int detect_finish(lpe_ctx *ctx, RigidDev *d, hipStream_t s, const int32_t
     }
     if (hc[6] || np > d->cap_pairs) {   // pair buffer overflow: grow and redo
         *retry = 1;
+        d->regrows++;
         return rigid_alloc_pairs(ctx, d, std::max(2 * d->cap_pairs, np + 1024));
+    }
+    if (hc[11]) {
+        ctx->err = "narrowphase: a pair produced more contacts than a pair slot holds (MAXC)";
+        return LPE_ERR_OVERFLOW;
     }
     int32_t ncv = 0;
     LPE_HIP(ctx, hipMemcpyAsync(&ncv, d->cstart + np, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     LPE_HIP(ctx, hipStreamSynchronize(s));
     if (ncv > d->cap_contacts) {
+        d->regrows++;
         int st = rigid_alloc_contacts(ctx, d, ncv + 4096);
         if (st) return st;
     }
@@ -2043,7 +2056,7 @@ static int rigid_detect(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pai
                         hipStream_t s = nullptr) {
     if (!s) s = ctx->stream;
     for (int attempt = 0; attempt < 4; attempt++) {
-        int32_t hc[8];
+        int32_t hc[12];
         int st = detect_launch(ctx, d, np_in, pairs_in, s, hc);
         if (st) return st;
         LPE_HIP(ctx, hipStreamSynchronize(s));
@@ -2115,21 +2128,37 @@ static int rigid_solve(lpe_ctx *ctx, RigidDev *d, bool colour, const int32_t *pg
     if (colour) {
         // canonical order: colour-synchronous sweeps over the colour segments
         // LDS: body state, then as many pair segments as fit (the coloured
-        // pairs are at most last_np)
+        // pairs are at most last_np).
+        // The two solvers run CONCURRENTLY, one workgroup each: the position
+        // solver (position_solver.cpp:299-325) reads poses, masses and the
+        // narrowphase contacts, never a velocity, and the PGS
+        // (contact_solver.cpp:449-543) writes only v and omega and reads the
+        // poses before the position solver moves them (k_pgs_rows, below, is
+        // done before the fork).  The reference runs them one after the
+        // other; the results are the same bits.
         const size_t ldsMax = 159 * 1024;      // of the 160 KB of a CU (the kernels use < 1 KB static)
+        LPE_KERNEL(ctx, "k_pos_bodies", k_pos_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->posState);
+        LPE_KERNEL(ctx, "k_pos_fill_rows", k_pos_fill_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->order, d->contacts, d->bodies, d->posState, d->posRec, inPos, c.baumgarte, c.slop);
+        if (!d->psolve) {
+            LPE_HIP(ctx, hipStreamCreateWithFlags(&d->psolve, hipStreamNonBlocking));
+            LPE_HIP(ctx, hipEventCreateWithFlags(&d->evFork, hipEventDisableTiming));
+            LPE_HIP(ctx, hipEventCreateWithFlags(&d->evJoin, hipEventDisableTiming));
+        }
+        LPE_HIP(ctx, hipEventRecord(d->evFork, s));
+        LPE_HIP(ctx, hipStreamWaitEvent(d->psolve, d->evFork, 0));
+        size_t lds2 = sizeof(double) * 3 * (size_t)nb;
+        int segLds2 = (int)std::min<size_t>((size_t)d->last_np, (ldsMax - std::min(ldsMax, lds2)) / sizeof(int2));
+        lds2 += sizeof(int2) * (size_t)segLds2;
+        LPE_KERNEL(ctx, "k_pos_colour", k_pos_colour, dim3(1), dim3(SOLVE_TPB), lds2, d->psolve, nb, d->counts, d->cbase, d->cseg, segLds2, d->posRec, d->bodies, d->posState, inPos, c.posIterations);
+        LPE_CHECK_LAUNCH(ctx, "position solver");
+        LPE_HIP(ctx, hipEventRecord(d->evJoin, d->psolve));
         size_t lds = sizeof(float) * (3 * (size_t)nb + 1);
         int segLds = (int)std::min<size_t>((size_t)d->last_np, (ldsMax - std::min(ldsMax, lds)) / sizeof(int2));
         lds += sizeof(int2) * (size_t)segLds + 8;
         LPE_KERNEL(ctx, "k_pgs_colour", k_pgs_colour, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts, d->cbase, d->cseg, segLds, d->rowN, d->rowR, d->rowAB, d->rowM, d->vel0, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF);
         LPE_KERNEL(ctx, "k_pgs_writeback", k_pgs_writeback, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->inContact);
         LPE_CHECK_LAUNCH(ctx, "pgs");
-        LPE_KERNEL(ctx, "k_pos_bodies", k_pos_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->posState);
-        LPE_KERNEL(ctx, "k_pos_fill_rows", k_pos_fill_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->order, d->contacts, d->bodies, d->posState, d->posRec, inPos, c.baumgarte, c.slop);
-        size_t lds2 = sizeof(double) * 3 * (size_t)nb;
-        int segLds2 = (int)std::min<size_t>((size_t)d->last_np, (ldsMax - std::min(ldsMax, lds2)) / sizeof(int2));
-        lds2 += sizeof(int2) * (size_t)segLds2;
-        LPE_KERNEL(ctx, "k_pos_colour", k_pos_colour, dim3(1), dim3(SOLVE_TPB), lds2, s, nb, d->counts, d->cbase, d->cseg, segLds2, d->posRec, d->bodies, d->posState, inPos, c.posIterations);
-        LPE_CHECK_LAUNCH(ctx, "position solver");
+        LPE_HIP(ctx, hipStreamWaitEvent(s, d->evJoin, 0));
     } else {
         // caller-supplied order (reference replay): exact dataflow sweeps
         int st = rigid_versions(ctx, d, d->counts + 1, nc);
@@ -2180,6 +2209,28 @@ static int rigid_step_impl(lpe_ctx *ctx, int np, const int32_t *pairs, int nc_or
     }
     if (stats) { stats->pairs = d->last_np; stats->contacts = d->last_nc; }
     return rigid_solve(ctx, d, pairs == nullptr, pgs_order, stats);
+}
+
+extern "C" int lpe_rigid_reserve(lpe_ctx *ctx, int pairs, int contacts) {
+    if (!ctx || pairs < 1 || contacts < 1) return LPE_ERR_ARG;
+    (void)hipSetDevice(ctx->device);
+    RigidDev *d = rdev(ctx);
+    if (d->side) LPE_HIP(ctx, hipStreamSynchronize(d->side));
+    LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    d->cap_pairs = 0;                     // re-allocated at exactly the requested sizes
+    d->cap_contacts = 0;
+    int st = rigid_alloc_pairs(ctx, d, pairs);
+    if (!st) st = rigid_alloc_contacts(ctx, d, contacts);
+    return st;
+}
+
+extern "C" int lpe_rigid_buffer_info(lpe_ctx *ctx, int *pairs, int *contacts, int *regrows) {
+    if (!ctx) return LPE_ERR_ARG;
+    RigidDev *d = rdev(ctx);
+    if (pairs) *pairs = d->cap_pairs;
+    if (contacts) *contacts = d->cap_contacts;
+    if (regrows) *regrows = d->regrows;
+    return LPE_OK;
 }
 
 extern "C" int lpe_rigid_step(lpe_ctx *ctx, lpe_rigid_stats *stats) {

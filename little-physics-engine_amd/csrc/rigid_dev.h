@@ -61,7 +61,7 @@ struct RigidDev {
     int32_t *sBCount = nullptr, *sBStart = nullptr, *sBCursor = nullptr, *sEnt = nullptr;
     int32_t *counts = nullptr;                // [0]=np [1]=nc [4]=npos [5]=heavy [6]=pair overflow
                                               // [7]=solver fault [8]=colours [9]=colouring rounds
-                                              // [10]=special broadphase bodies
+                                              // [10]=special broadphase bodies [11]=contact truncation
     int32_t *pcol = nullptr;                  // colour per pair (canonical order)
     int2 *cseg = nullptr;                     // (row start, rows) per coloured pair, colour-major
     int32_t *cbase = nullptr;                 // first cseg entry of each colour (+ end)
@@ -76,6 +76,7 @@ struct RigidDev {
     lpe_rigid_config cfg{};
     bool cfg_set = false;
     int last_np = 0, last_nc = 0;
+    int regrows = 0;                          // detections redone / contact buffer grown (lpe_rigid_buffer_info)
     // world tick: collision detection and colouring run on a side stream
     // while the fluid step runs (rigid_tick_begin / rigid_tick_finish)
     int32_t *bbits = nullptr;                 // per body: boundary bounce bits of the tick
@@ -83,6 +84,9 @@ struct RigidDev {
     hipStream_t side = nullptr;
     hipEvent_t evStart = nullptr, evDetect = nullptr, evColour = nullptr;
     bool overlap_pending = false;
+    // the position solver runs beside the PGS on its own stream (rigid_solve)
+    hipStream_t psolve = nullptr;
+    hipEvent_t evFork = nullptr, evJoin = nullptr;
 };
 
 

@@ -183,6 +183,8 @@ SIGNATURES = {
     "lpe_rigid_download_contacts": ([C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
                                      _IP, _IP], C.c_int),
     "lpe_rigid_download_colours": ([C.c_void_p, C.c_int, _IP, _IP], C.c_int),
+    "lpe_rigid_reserve": ([C.c_void_p, C.c_int, C.c_int], C.c_int),
+    "lpe_rigid_buffer_info": ([C.c_void_p, _IP, _IP, _IP], C.c_int),
 }
 
 class WorldConfig(C.Structure):
@@ -443,6 +445,15 @@ class Context:
                                              C.byref(st) if stats else None)
         self._chk(r, "lpe_rigid_step")
         return st.as_dict()
+
+    def rigid_reserve(self, pairs: int, contacts: int):
+        self._chk(lib().lpe_rigid_reserve(self._h, int(pairs), int(contacts)), "lpe_rigid_reserve")
+
+    def rigid_buffer_info(self) -> dict:
+        p, c, r = C.c_int32(0), C.c_int32(0), C.c_int32(0)
+        self._chk(lib().lpe_rigid_buffer_info(self._h, C.byref(p), C.byref(c), C.byref(r)),
+                  "lpe_rigid_buffer_info")
+        return dict(pairs=p.value, contacts=c.value, regrows=r.value)
 
     def rigid_integrate(self, systems, dt_state, dt_move=None):
         self._chk(lib().lpe_rigid_integrate(self._h, int(systems), float(dt_state),

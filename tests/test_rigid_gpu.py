@@ -185,3 +185,51 @@ def test_multi_tick_device_matches_restatement(gpu_ctx, oracle_mod):
     out = gpu_ctx.rigid_download()
     close_state(out, ref)
     same(out, ref, ("sleep_counter", "flags"))
+
+
+def test_pair_buffer_grow_and_redo(oracle_mod):
+    """Regression for the pair-buffer overflow fixed in round 1 (an
+    out-of-bounds write on the first step of a larger pile): with the buffers
+    deliberately sized for 16 pairs / 64 contacts, the step on the metric
+    pile (~10k pairs) must grow them, redo its detection and still match the
+    restatement exactly as test_metric_pile_canonical does."""
+    z = np.load(os.path.join(GOLDEN, "pile_M_t250.npz"))
+    b, v = z["bodies"], z["verts"]
+    cfg = lpe.rigid_config(universe=32.0)
+    ref, rst = oracle_mod.rigid_update(cfg, b, v)
+    ctx = lpe.Context(0)
+    try:
+        ctx.rigid_set_config(cfg)
+        ctx.rigid_upload(b, v)
+        ctx.rigid_reserve(16, 64)
+        assert ctx.rigid_buffer_info()["pairs"] == 16
+        st = ctx.rigid_step()
+        info = ctx.rigid_buffer_info()
+        out = ctx.rigid_download()
+    finally:
+        ctx.close()
+    assert info["regrows"] >= 2 and info["pairs"] >= rst.pairs and info["contacts"] >= rst.contacts, info
+    assert st["pairs"] == rst.pairs and st["contacts"] == rst.contacts
+    close_state(out, ref)
+
+
+def test_pair_buffer_grow_in_world_tick():
+    """The same overflow inside the world tick (detection on the side stream,
+    rigid_tick_finish redoes it): bodies equal a run with roomy buffers."""
+    z = np.load(os.path.join(GOLDEN, "pile_M_t250.npz"))
+    b, v = z["bodies"], z["verts"]
+    outs = []
+    for tiny in (True, False):
+        ctx = lpe.Context(0)
+        try:
+            ctx.rigid_set_config(lpe.rigid_config(universe=32.0))
+            ctx.rigid_upload(b, v)
+            if tiny:
+                ctx.rigid_reserve(8, 32)
+            ctx.world_tick(DT, 3)
+            outs.append((ctx.rigid_download(), ctx.rigid_buffer_info()))
+        finally:
+            ctx.close()
+    assert outs[0][1]["regrows"] >= 1
+    for k in ("x", "y", "angle", "vx", "vy", "omega", "flags"):
+        np.testing.assert_array_equal(outs[0][0][k], outs[1][0][k], err_msg=k)
