@@ -19,7 +19,13 @@ max over ranks) uses gloo.
 
 Rank 0 prints ONE JSON line (the driver contract), including the live
 roofline of the dominant kernel (HIP events on the library's stream) and the
-CPU baseline (the oracle, 1 thread, on a bounded sample of the same workload).
+CPU baseline (the oracle on 1 thread and on all cores, on a bounded sample of
+the same workload).  Besides the contract window of exactly K ticks (`value`)
+the line carries SURVEY.md §8(d)'s methodology: the median of >= 5 windows of
+>= 2 s (`windows`), the one-tick-per-call rate of the drop-in path, strict
+mode (ECS sync every tick), the BASELINE configs C1-C4 beside the reference's
+own measured anchors, and whether the timed window stayed inside the
+reference's 64-particle cell capacity.
 """
 from __future__ import annotations
 
@@ -97,10 +103,22 @@ def pmc_valu(kernel):
     return None, None
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(scene_name, state=None, budget_s=20.0):
-    """The oracle (C/C++ restatement of the reference algorithms, 1 thread)
-    running the same full tick on the same scene state (`state`: the device
-    state at the end of the timed window, so the CPU ticks the settled pile)."""
+    """The oracle (C/C++ restatement of the reference algorithms, -O2) running
+    the same full tick on the same scene state (`state`: the device state at
+    the end of the timed window, so the CPU ticks the settled pile), on one
+    thread (the reference's execution model) and on every host core (OpenMP
+    over particles; bit-identical results)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle  # noqa: E402  (checker / baseline only)
     lpe = _load("lpe", os.path.join(PKG, "lpe.py"))
@@ -111,23 +129,36 @@ def cpu_baseline(scene_name, state=None, budget_s=20.0):
     if state is not None:
         fl.update({k: state["fluid"][k] for k in ("x", "y", "vx", "vy", "density", "pressure")})
         b = state["bodies"]
-    p = scenes.particles_aos(fl)
+    p0 = scenes.particles_aos(fl)
     couple = np.arange(len(b) - 1, -1, -1, dtype=np.int32)
     fcfg = lpe.default_fluid_config()
     rcfg = lpe.rigid_config(universe=s["U"])
-    ticks = 0
-    t0 = time.perf_counter()
-    while True:
-        p, b = oracle.world_tick(fcfg, rcfg, p, b, v, couple, 1.0 / 120.0, 1)
-        ticks += 1
-        el = time.perf_counter() - t0
-        if el > budget_s or el / ticks * (ticks + 1) > budget_s * 1.5:
-            break
-    return dict(value=ticks / el, unit="ticks/s", cores=1, kind="port",
-                sample=f"{ticks} full tick(s) of scene {scene_name}"
-                       f"{' (settled state from the device)' if state is not None else ''} ({len(p)} SPH particles, "
-                       f"{len(b)} bodies) through oracle/ (sph_oracle.c + rigid_oracle.cpp "
-                       f"lpeo_world_tick), 1 thread, -O2")
+    nproc = os.cpu_count() or 1
+    # the box exports OMP_NUM_THREADS (its CPU share); os.cpu_count() is the whole machine
+    allc = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or nproc
+
+    def run(threads, budget):
+        oracle.set_threads(threads)
+        p, bb = p0, b
+        ticks = 0
+        t0 = time.perf_counter()
+        while True:
+            p, bb = oracle.world_tick(fcfg, rcfg, p, bb, v, couple, 1.0 / 120.0, 1)
+            ticks += 1
+            el = time.perf_counter() - t0
+            if el > budget or el / ticks * (ticks + 1) > budget * 1.5:
+                break
+        return ticks / el, ticks
+
+    one, n1 = run(1, budget_s)
+    many, nm = run(allc, budget_s / 2)
+    oracle.set_threads(0)
+    return dict(value=one, unit="ticks/s", cores=1, kind="port",
+                all_cores=dict(value=many, cores=allc, ticks=nm),
+                nproc=nproc, cpu_model=cpu_model(),
+                sample=f"{n1} full tick(s) (1 thread) and {nm} (all {allc} threads) of scene {scene_name}"
+                       f"{' from the settled device state' if state is not None else ''} ({len(p0)} SPH particles, "
+                       f"{len(b)} bodies) through oracle/ (sph_oracle.c + rigid_oracle.cpp lpeo_world_tick), -O2")
 
 
 def density_microbench(lpe, scenes, device, side=4096, reps=5):
@@ -254,6 +285,116 @@ def rigid_microbench(lpe, device, reps=10):
                                                "k_pos_colour") if k in us})
 
 
+def timed_windows(ctx, dt_tick, rate_hint, nwin=5, min_s=2.0, min_ticks=50):
+    """>= nwin windows of >= min_s each, back to back."""
+    per = max(min_ticks, int(rate_hint * min_s) + 1)
+    rates = []
+    for _ in range(nwin):
+        ctx.sync()
+        t0 = time.perf_counter()
+        ctx.world_tick(dt_tick, per)
+        ctx.sync()
+        rates.append(per / (time.perf_counter() - t0))
+    return dict(median=round(float(np.median(rates)), 2), rates=[round(r, 2) for r in rates],
+                ticks_per_window=per, windows=nwin)
+
+
+def one_tick_calls(ctx, dt_tick, n):
+    """The drop-in path: one lpe_world_tick call per ECSSimulator::tick (the
+    host mirror's IntegratorSystems, host/src/systems/integrators.cpp)."""
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        ctx.world_tick(dt_tick, 1)
+    ctx.sync()
+    return n / (time.perf_counter() - t0)
+
+
+def strict_mode(ctx, dt_tick, fl, n=10):
+    """Strict mode: the ECS is synchronised every tick -- the fluid and the
+    bodies go host -> device before the tick and device -> host after it
+    (fluid.cpp:250-302 gather, :496-524 write-back), as the reference's
+    FluidSystem does every tick.  PCIe-inclusive; not the headline."""
+    out = ctx.sph_download()
+    bodies = ctx.rigid_download()
+    verts = ctx._rkeep[1]
+    mass = np.asarray(fl["mass"], np.float32)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        ctx.sph_upload(out["x"], out["y"], out["vx"], out["vy"], mass, out["density"], out["pressure"])
+        ctx.rigid_upload(bodies, verts)
+        ctx.world_tick(dt_tick, 1)
+        out = ctx.sph_download()
+        bodies = ctx.rigid_download()
+    return n / (time.perf_counter() - t0)
+
+
+def config_lines(lpe, scenes, device, dt_tick, with_ref):
+    """Device tick rates at BASELINE.json's other configs,
+    each after the scene is in motion, over a window of >= 2 s; the rigid
+    configs beside the reference's own rigid path (oracle/_ref, compiled from
+    /root/reference by oracle/Makefile.ref; its PGS is the restatement, the
+    reference's needs NEON) on this host's single core, and BASELINE.md's
+    anchors measured in the build container."""
+    out = {}
+    for name, prep in (("C2", 30), ("C4", 90)):
+        s = scenes.scene(name)
+        fl = s["fluid"]
+        b, v = scenes.to_bodies(s["bodies"])
+        ctx = lpe.Context(device)
+        try:
+            ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+            ctx.rigid_upload(b, v)
+            ctx.sph_set_config(lpe.default_fluid_config())
+            ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+            ctx.world_set_coupling(None)
+            ctx.world_tick(dt_tick, prep)
+            w = timed_windows(ctx, dt_tick, 500.0, nwin=3, min_s=1.0)
+            st = ctx.sph_stats()
+        finally:
+            ctx.close()
+        out[name] = dict(desc=s["desc"], ticks_per_s=w["median"], windows=w, fluid_particles=len(fl["x"]),
+                         bodies=len(b), max_cell_occupancy=st["maxCellOccupancy"],
+                         cells_over_64=st["overCapCells"])
+    anchors = {"C1": (555.0, 600), "C3": (12.1, 240)}
+    for name in ("C1", "C3"):
+        s = scenes.rigid_scene(name)
+        b, v = scenes.to_bodies(s["bodies"])
+        cfg = lpe.rigid_config(universe=s["U"], pgs_iterations=s["pgs_iterations"])
+        ctx = lpe.Context(device)
+        try:
+            ctx.rigid_set_config(cfg)
+            ctx.rigid_upload(b, v)
+            ctx.world_tick(dt_tick, 240 if name == "C3" else 60)       # the pile forms / the stack settles
+            warm = ctx.rigid_download()
+            w = timed_windows(ctx, dt_tick, 1000.0, nwin=3, min_s=1.0)
+            pairs, contacts = ctx.rigid_contacts()
+        finally:
+            ctx.close()
+        line = dict(desc=s["desc"], ticks_per_s=w["median"], windows=w, bodies=len(b), pgs_iterations=s["pgs_iterations"],
+                    pairs=int(len(pairs)), contacts=int(len(contacts)),
+                    reference_anchor=dict(ticks_per_s=anchors[name][0], where="BASELINE.md §2: the reference's own "
+                                          "rigid path, -O2, 1 core of the build container's Xeon"))
+        if with_ref:
+            sys.path.insert(0, os.path.join(ROOT, "oracle"))
+            import oracle  # noqa: E402  (baseline only)
+            if oracle.ref_available():
+                nt = 1
+                t0 = time.perf_counter()
+                while True:                     # bounded sample: >= 1 s of the reference
+                    oracle.ref_rigid_ticks(cfg, warm, v, nt, dt_tick)
+                    el = time.perf_counter() - t0
+                    if el > 1.0 or nt >= 512:
+                        break
+                    nt *= 2
+                    t0 = time.perf_counter()
+                line["reference_this_host"] = dict(ticks_per_s=round(nt / el, 2), ticks=nt, cores=1,
+                                                   kind="reference", cpu_model=cpu_model())
+        out[name] = line
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -263,6 +404,8 @@ def main():
     ap.add_argument("--prep", type=int, default=240,
                     help="untimed ticks that settle the scene before warmup (the pile forms)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the >=2 s windows, one-tick calls, strict mode and the C1-C4 lines")
     ap.add_argument("--no-density-microbench", action="store_true")
     ap.add_argument("--replicas", action="store_true",
                     help="N > 1: independent copies of the scene instead of the slab-sharded MW{N}")
@@ -316,6 +459,7 @@ def main():
         if dist is not None:
             dist.barrier()
 
+    ctx.sph_diag(False)               # restart the window totals (cells over the reference's 64)
     barrier()
     ctx.sync()
     t0 = time.perf_counter()
@@ -324,11 +468,25 @@ def main():
     t1 = time.perf_counter()
     barrier()
     elapsed = t1 - t0
+    wstats = ctx.sph_stats()
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    extras = {}
+    if world == 1 and not args.no_extras:
+        rate = args.steps / elapsed
+        extras["windows"] = timed_windows(ctx, dt_tick, rate)
+        n1 = max(50, int(rate * 2.0))
+        r1 = one_tick_calls(ctx, dt_tick, n1)
+        extras["one_tick_calls"] = dict(ticks_per_s=round(r1, 2), ticks=n1,
+                                        vs_multi_tick=round(r1 / extras["windows"]["median"], 4),
+                                        note="lpe_world_tick(ctx, wc, 1) in a loop: the drop-in path "
+                                             "(one call per ECSSimulator::tick)")
+        extras["strict"] = dict(ticks_per_s=round(strict_mode(ctx, dt_tick, fl), 2),
+                                note="ECS sync every tick: fluid + bodies uploaded before and downloaded "
+                                     "after each tick (PCIe-inclusive, fluid.cpp:250-302 / :496-524)")
     # per-kernel durations: start/stop events carried by every launch on the
     # library's stream (hipExtLaunchKernelGGL), over a second window of the
     # same length (the event bookkeeping adds host work per launch, so it is
@@ -420,8 +578,25 @@ def main():
         "kernels_us": {k: round(v[0] / max(v[1], 1) * 1e3, 2) for k, v in times.items()},
         "dominant_kernel": overall,
         "max_cell_occupancy": stats["maxCellOccupancy"],
+        "reference_envelope": {
+            "max_cell_occupancy_window": wstats["maxCellOccupancyTotal"],
+            "cells_over_64_window": wstats["overCapCellsTotal"],
+            "inside": wstats["overCapCellsTotal"] == 0,
+            "note": "reference cells (2h) holding more than GPU_MAX_PER_CELL = 64 particles, summed over the "
+                    "sub-steps of the timed window: where non-zero the reference drops inserts and reads "
+                    "across cells (fluid.hpp:56, fluid_kernels.metal:237-240, :281-283); the headline runs "
+                    "the unbounded lists, and LPE_SPH_MODE_REF_CELL_CAP reproduces the reference's behaviour "
+                    "exactly (tests/test_configs_gpu.py checks both at this scene)"},
         "rigid": {"pairs": int(len(pairs)), "contacts": int(len(contacts)), "colours": int(ncolours)},
     }
+    line.update(extras)
+    if world == 1 and not args.no_extras:
+        # the same scene in the reference's own 64-slot cell mode
+        ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP)
+        w = timed_windows(ctx, dt_tick, args.steps / elapsed, nwin=3, min_s=1.0)
+        ctx.sph_set_mode(0)
+        line["ref_cell_cap_mode"] = dict(ticks_per_s=w["median"], windows=w)
+        line["configs"] = config_lines(lpe, scenes, local, dt_tick, not args.no_cpu_baseline)
     if world == 1 and not args.no_density_microbench:
         line["density_microbench"] = density_microbench(lpe, scenes, local)
         line["rigid_microbench"] = rigid_microbench(lpe, local)

@@ -140,6 +140,10 @@ typedef struct lpe_sph_stats {
     /* LPE_SPH_MODE_REF_CELL_CAP read past the last cell of the grid (the
      * reference reads stale or out-of-bounds memory there: undefined) */
     int32_t refUndefined;
+    /* overCapCells summed, and maxCellOccupancy maximised, over every step
+     * since the last lpe_sph_diag call (a bench window) */
+    int32_t overCapCellsTotal;
+    int32_t maxCellOccupancyTotal;
 } lpe_sph_stats;
 
 /* ------------------------------------------------------------------------ */
@@ -282,7 +286,9 @@ int  lpe_sph_download_aux(lpe_ctx *ctx, float *vxHalf, float *vyHalf,
  * when accum is non-NULL (3 floats per body). */
 int  lpe_sph_download_rigids(lpe_ctx *ctx, lpe_gpu_rigid *rigids, float *accum);
 int  lpe_sph_get_stats(lpe_ctx *ctx, lpe_sph_stats *stats);
-/* Diagnostics counters of lpe_sph_stats on (1, counters reset) or off (0). */
+/* Diagnostics counters of lpe_sph_stats on (1, counters reset) or off (0);
+ * either way the window totals (overCapCellsTotal, maxCellOccupancyTotal)
+ * restart. */
 int  lpe_sph_diag(lpe_ctx *ctx, int on);
 
 /* SPH modes (flags, default 0).

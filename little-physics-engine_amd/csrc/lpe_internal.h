@@ -113,6 +113,8 @@ enum StatusSlot {
     ST_XACC_RANGE = 10,     // a rigid coupling force outside the exact accumulator's range (|f| >= 2^64)
     ST_OVER_CAP = 11,       // reference cells over GPU_MAX_PER_CELL, summed over the tick's sub-steps
     ST_REF_UB = 12,         // reference cell-capacity mode read past the last cell (undefined in the reference)
+    ST_OVER_CAP_TOTAL = 13, // ST_OVER_CAP summed since the last lpe_sph_diag call (bench windows)
+    ST_MAX_OCC_TOTAL = 14,  // ST_MAX_OCC maximum since the last lpe_sph_diag call
     ST_COUNT = 16
 };
 
@@ -197,7 +199,10 @@ int lpe_rigid_destroy_internal(lpe_ctx *ctx);
 // world tick: rigid collision detection overlapped with the fluid step (lpe_rigid.hip)
 int rigid_tick_begin(lpe_ctx *ctx);
 int rigid_tick_boundary(lpe_ctx *ctx);
+int rigid_tick_detect(lpe_ctx *ctx);   // host half of the detection + colouring launch
 int rigid_tick_finish(lpe_ctx *ctx);
+// lpe_sph_step with a host callback after the forces of sub-step `after`
+int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int after, int (*hook)(lpe_ctx *));
 int sph_prelaunch(lpe_ctx *ctx, double dt_tick);
 int lpe_sph_cover_box(lpe_ctx *ctx, double x0, double y0, double x1, double y1);
 // coupling rigids' device arrays (rig, accum, acq) for n rigids (grow-only)

@@ -2246,6 +2246,7 @@ extern "C" int lpe_rigid_step(lpe_ctx *ctx, lpe_rigid_stats *stats) {
 int rigid_tick_begin(lpe_ctx *ctx) {
     RigidDev *d = rdev(ctx);
     d->overlap_pending = false;
+    d->colour_pending = false;
     if (d->nb <= 0) return LPE_OK;
     const lpe_rigid_config &c = d->cfg;
     if (!d->side) {
@@ -2277,11 +2278,16 @@ int rigid_tick_boundary(lpe_ctx *ctx) {
     return LPE_OK;
 }
 
-int rigid_tick_finish(lpe_ctx *ctx) {
+// The host half of the detection (its counts decide whether the pair buffer
+// must grow and how many contacts there are), then the colouring on the side
+// stream.  The world tick calls this from inside the fluid step, after its
+// first sub-steps are queued, so the host waits on the detection while the
+// device is busy with the fluid and the colouring runs beside the rest of it.
+int rigid_tick_detect(lpe_ctx *ctx) {
     RigidDev *d = rdev(ctx);
-    if (d->nb <= 0) return LPE_OK;
+    if (d->nb <= 0 || d->colour_pending) return LPE_OK;
     if (!d->overlap_pending) {
-        ctx->err = "rigid_tick_finish without rigid_tick_begin";
+        ctx->err = "rigid_tick_detect without rigid_tick_begin";
         return LPE_ERR_STATE;
     }
     d->overlap_pending = false;
@@ -2298,6 +2304,16 @@ int rigid_tick_finish(lpe_ctx *ctx) {
         if (st) return st;
     }
     LPE_HIP(ctx, hipEventRecord(d->evColour, d->side));
+    d->colour_pending = true;
+    return LPE_OK;
+}
+
+int rigid_tick_finish(lpe_ctx *ctx) {
+    RigidDev *d = rdev(ctx);
+    if (d->nb <= 0) return LPE_OK;
+    int st = rigid_tick_detect(ctx);          // (already done inside the fluid step)
+    if (st) return st;
+    d->colour_pending = false;
     LPE_HIP(ctx, hipStreamWaitEvent(ctx->stream, d->evColour, 0));
     return rigid_solve(ctx, d, true, nullptr, nullptr, true);
 }

@@ -313,9 +313,9 @@ k_scan_final(int C, int W, int ox, int oy, int32_t *__restrict__ cnt,
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        if (s_max) atomicMax(&status[ST_MAX_OCC], s_max);
+        if (s_max) { atomicMax(&status[ST_MAX_OCC], s_max); atomicMax(&status[ST_MAX_OCC_TOTAL], s_max); }
         if (s_out) atomicAdd(&status[ST_NOT_INSERTED], s_out);
-        if (s_over) atomicAdd(&status[ST_OVER_CAP], s_over);
+        if (s_over) { atomicAdd(&status[ST_OVER_CAP], s_over); atomicAdd(&status[ST_OVER_CAP_TOTAL], s_over); }
     }
 }
 
@@ -553,181 +553,223 @@ __device__ void ref_cap_walk(float xi, float yi, float eps, const GridParams &g,
 }
 
 // ---------------------------------------------------------------------------
-// computeDensity with LDS-staged neighbourhoods (the density probe and the
-// 16M-particle microbench: a pure density pass, no neighbour list).  A block
-// owns SB consecutive sorted slots; in sorted order they cover at most two
-// runs of cells in two adjacent cell rows (unless the fluid is sparse), so
-// every record the block's walks can touch lies in <= 6 contiguous slot
-// ranges: rows cy-1..cy+1 of each run, one cell left and right of it.  The
-// block copies them into LDS with coalesced loads and the walks read LDS
-// instead of L2; the walk itself, and so every sum, is unchanged.  A block
-// whose neighbourhood does not fit reads global memory.
-static constexpr int SB = 512;            // slots per block of the staged kernel
-static constexpr int STAGE_CAP = 4096;    // records staged per block (64 KB)
-
-struct Stage {
-    int ok;                  // neighbourhood staged in LDS
-    int cy0, cy1;            // cell rows of run 0 / run 1 (cy1 == cy0: one run)
-    int cxa[2], cxb[2];      // cell columns of each run
-    int segS[6], segE[6];    // slot range of segment r*3 + (dy+1)
-    int segL[6];             // LDS offset of each segment
-};
+// LDS-staged neighbourhoods.  A block owns HB consecutive sorted slots; in
+// sorted order they cover one run of cells of one cell row, or the end of one
+// row and the start of the next (unless the fluid is sparse).  Every record a
+// walk of the block can touch then lies in <= 6 contiguous slot ranges ("row
+// segments": rows cy-1..cy+1 of each run, one cell left and right of it).
+// The block copies them into LDS with coalesced loads, together with the
+// quadrant boundaries of every cell of those segments rebased to LDS offsets,
+// so a walk reads nothing but LDS: the walk itself, and so every sum, is the
+// canonical one.  The plan is computed by every wave from block-uniform loads
+// (no serial section, one barrier).  A block whose neighbourhood does not fit
+// walks global memory instead.
+static constexpr int HB = 256;            // slots (threads) per staged block
+static constexpr int HCAP = 1792;         // records staged per block (28 KB of float4: 4 blocks per CU)
+static constexpr int HCELLS = 320;        // staged cells per block (4 boundaries each)
 
 __device__ __forceinline__ void cell_xy(float x, float y, float eps, float cs, int &cx, int &cy) {
     cx = (int)floorf((x + eps) / cs);
     cy = (int)floorf((y + eps) / cs);
 }
 
-// Plans st (block-uniform) for slots [s0, s1); every thread of the block
-// calls it (it holds barriers).
-__device__ void stage_plan(Stage &st, int cap, int s0, int s1, const float4 *__restrict__ nbA, float eps,
-                           float cs, int W, int H, int ox, int oy, const int32_t *__restrict__ start) {
-    const int tid = threadIdx.x;
-    if (tid == 0) {
-        st.ok = 0;
-        if (s1 > s0) {
-            int cx, cy, lx, ly;
-            float4 f = nbA[s0], l = nbA[s1 - 1];
-            cell_xy(f.x, f.y, eps, cs, cx, cy);
-            cell_xy(l.x, l.y, eps, cs, lx, ly);
-            st.cy0 = cy; st.cy1 = ly;
-            st.cxa[0] = cx; st.cxb[0] = -0x7fffffff;
-            st.cxa[1] = 0x7fffffff; st.cxb[1] = lx;
-            st.ok = (ly - cy <= 1) ? 1 : 0;
+struct Hood {
+    bool ok;
+    int nrun, cy0;            // runs (1 or 2: rows cy0, cy0 + 1)
+    int ca[6], ss[6], se[6];  // per segment r * 3 + dy + 1: first cell column, global slot range
+    int l[6], bo[6];          // LDS record offset; boundary-table entry of the first cell
+    int ncell[6];             // cells in the segment (0: none)
+};
+
+// the plan for slots [s0, s1) (s1 > s0); cells of the device grid [ox, ox+W) x [oy, oy+H)
+__device__ __forceinline__ void hood_plan(Hood &hd, int s0, int s1, const float4 *__restrict__ nbA, float eps,
+                                          float cs, int W, int H, int ox, int oy,
+                                          const int32_t *__restrict__ start) {
+    const float4 f = nbA[s0], l = nbA[s1 - 1];
+    int cx0, cy0, cx1, cy1;
+    cell_xy(f.x, f.y, eps, cs, cx0, cy0);
+    cell_xy(l.x, l.y, eps, cs, cx1, cy1);
+    int xa[2] = {cx0, 0}, xb[2] = {cx1, 0};
+    hd.ok = true;
+    hd.cy0 = cy0;
+    if (cy1 == cy0) {
+        hd.nrun = 1;
+    } else if (cy1 == cy0 + 1 && cy1 - oy >= 0 && cy1 - oy < H) {
+        hd.nrun = 2;
+        const int rs = start[((cy1 - oy) * W) << 2];        // first slot of row cy1 (> s0)
+        const float4 e0 = nbA[rs - 1], b1 = nbA[rs];
+        int t;
+        cell_xy(e0.x, e0.y, eps, cs, xb[0], t);
+        cell_xy(b1.x, b1.y, eps, cs, xa[1], t);
+        xb[1] = cx1;
+    } else {
+        hd.ok = false;
+        return;
+    }
+    int L = 0, B = 0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        const int r = i / 3, row = cy0 + r + (i % 3) - 1;
+        const int ca = max(xa[r] - 1, ox), cb = min(xb[r] + 1, ox + W - 1);
+        hd.l[i] = L;
+        hd.bo[i] = B;
+        hd.ca[i] = ca;
+        hd.ncell[i] = 0;
+        hd.ss[i] = hd.se[i] = 0;
+        if (r < hd.nrun && row >= oy && row < oy + H && ca <= cb) {
+            const int base = (row - oy) * W - ox;
+            hd.ss[i] = start[(base + ca) << 2];
+            hd.se[i] = start[((base + cb) << 2) + 4];
+            hd.ncell[i] = cb - ca + 1;
+            L += hd.se[i] - hd.ss[i];
+            B += cb - ca + 2;                                // + the end sentinel
         }
     }
-    __syncthreads();
-    const int s = s0 + tid;
-    if (st.ok && s < s1) {
-        int cx, cy;
-        float4 me = nbA[s];
-        cell_xy(me.x, me.y, eps, cs, cx, cy);
-        if (cy == st.cy0) atomicMax(&st.cxb[0], cx);
-        if (cy == st.cy1 && st.cy1 != st.cy0) atomicMin(&st.cxa[1], cx);
-    }
-    __syncthreads();
-    if (st.ok && tid < 6) {                 // one segment per thread
-        const int r = tid / 3, dy = tid % 3 - 1;
-        int b = 0, e = 0;
-        if (r == 0 || st.cy1 != st.cy0) {
-            const int row = (r ? st.cy1 : st.cy0) + dy - oy;
-            const int kxa = max(st.cxa[r] - 1 - ox, 0), kxb = min(st.cxb[r] + 1 - ox, W - 1);
-            if (row >= 0 && row < H && kxa <= kxb) {
-                b = start[(row * W + kxa) << 2];
-                e = start[((row * W + kxb) << 2) + 4];
-            }
-        }
-        st.segS[tid] = b;
-        st.segE[tid] = e;
-    }
-    __syncthreads();
-    if (tid == 0 && st.ok) {
-        int off = 0;
-        for (int i = 0; i < 6; i++) { st.segL[i] = off; off += st.segE[i] - st.segS[i]; }
-        if (off > cap) st.ok = 0;
-    }
-    __syncthreads();
+    hd.ok = L <= HCAP && B <= HCELLS;
 }
 
-// computeDensity (metal:246-307), one thread per sorted slot, SB slots per
-// block with the neighbourhood staged in LDS.  Besides rho and p it writes
-// the neighbours of the forces pass (r^2 < h^2, not itself: metal:360-366) in
-// the canonical walk order as int16 slot offsets k - s, eight to a uint4,
-// column-major [NLIST_CAP / 8][nstride]: each thread collects eight offsets
-// in its 16-byte LDS slot and writes them with one 16-byte store (2-byte
-// stores scattered over rows cost ~16 B of write traffic each, PMC WRITE_SIZE).
-// More than NLIST_CAP neighbours: ncount > NLIST_CAP and the forces pass
-// walks the bins.
-__global__ void __launch_bounds__(SB)
+// copies the planned records (rec[k] -> lrec) and the cells' quadrant starts
+// (rebased to LDS offsets, 4 per cell + the segment end) into LDS
+template <typename R, class Ld>
+__device__ __forceinline__ void hood_stage(const Hood &hd, R *lrec, int *lbnd, int W, int ox, int oy,
+                                           const int32_t *__restrict__ start, Ld ld) {
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+        if (!hd.ncell[i]) continue;
+        const int b = hd.ss[i], len = hd.se[i] - b, o = hd.l[i];
+        for (int j = threadIdx.x; j < len; j += HB) lrec[o + j] = ld(b + j);
+        const int row = hd.cy0 + i / 3 + (i % 3) - 1;
+        const int g0 = (((row - oy) * W) + hd.ca[i] - ox) << 2;   // first boundary of the segment
+        const int nb = 4 * hd.ncell[i] + 1;
+        const int shift = o - b;
+        for (int j = threadIdx.x; j < nb; j += HB) lbnd[4 * hd.bo[i] + j] = start[g0 + j] + shift;
+    }
+}
+
+// The canonical walk (walk_ranges) over the staged neighbourhood: f(b, e)
+// for each (cell, quadrant row) range [b, e) of LDS records, in the order of
+// walk_ranges.  (cxp, cyp): the particle's cell.
+template <class F>
+__device__ __forceinline__ void hood_ranges(const Hood &hd, const int *lbnd, float xi, float yi, float eps,
+                                            float cs, float reach, int cyp, const GridParams &g, F f) {
+    const float u = 2.0f * ((xi + eps) / cs), v = 2.0f * ((yi + eps) / cs);
+    const int bx0 = (int)floorf(u - reach), bx1 = (int)floorf(u + reach);
+    const int by0 = (int)floorf(v - reach), by1 = (int)floorf(v + reach);
+    const int cxa = max(bx0 >> 1, g.gridMinX), cxb = min(bx1 >> 1, g.gridMinX + g.gridDimX - 1);
+    const int cya = max(by0 >> 1, g.gridMinY), cyb = min(by1 >> 1, g.gridMinY + g.gridDimY - 1);
+    const int r3 = (cyp == hd.cy0) ? 0 : 3;
+    for (int cy = cya; cy <= cyb; cy++) {
+        const int i = r3 + cy - cyp + 1;                      // segment of this cell row
+        const int qya = max(by0 - 2 * cy, 0), qyb = min(by1 - 2 * cy, 1);
+        const int shift = hd.ss[i] - hd.l[i];                 // LDS index -> global slot
+        for (int cx = cxa; cx <= cxb; cx++) {
+            const int qxa = max(bx0 - 2 * cx, 0), qxb = min(bx1 - 2 * cx, 1);
+            const int *cb = lbnd + 4 * (hd.bo[i] + cx - hd.ca[i]);
+            for (int qy = qya; qy <= qyb; qy++) {
+                const int b = cb[qy * 2 + qxa], e = cb[qy * 2 + qxb + 1];   // [4] is the next cell's start
+                f(b, e, shift);
+            }
+        }
+    }
+}
+
+// computeDensity (metal:246-307), one thread per sorted slot, HB slots per
+// block with the neighbourhood staged in LDS.  NL: also write the neighbours
+// of the forces pass (r^2 < h^2, not itself: metal:360-366) in the canonical
+// walk order as int16 slot offsets k - s, eight to a uint4, column-major
+// [NLIST_CAP / 8][nstride]: each thread collects eight offsets in its 16-byte
+// LDS slot and writes them with one 16-byte store.  More than NLIST_CAP
+// neighbours: ncount > NLIST_CAP and the forces pass walks the bins.
+template <bool NL>
+__global__ void __launch_bounds__(HB)
 k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float eps, float stiffness,
           float restDensity, int W, int H, int ox, int oy, const GridParams *__restrict__ gp,
           const int32_t *__restrict__ start, const float4 *__restrict__ nbA, float2 *__restrict__ nbB,
           float *__restrict__ rho, float *__restrict__ pr, uint4 *__restrict__ nlist,
           int32_t *__restrict__ ncount, int32_t *__restrict__ status, const int32_t *__restrict__ sid,
           const int32_t *__restrict__ refInv) {
-    __shared__ Stage st;
-    __shared__ float4 lrec[STAGE_CAP];
-    __shared__ uint4 lnl[SB];                             // per thread: the current group of 8 offsets
-    const int lb = xcd_block((n + SB - 1) / SB);
+    __shared__ float4 lrec[HCAP + 1];                     // + 1: the pair-unrolled walk reads one past a range
+    __shared__ int lbnd[4 * HCELLS];
+    __shared__ uint4 lnl[NL ? HB : 1];                    // per thread: the current group of 8 offsets
+    const int lb = xcd_block((n + HB - 1) / HB);
     if (lb < 0) return;                                   // whole block idle
     const int nn = nptr ? *nptr : n;
-    const int s0 = lb * SB, s1 = min(s0 + SB, nn);
+    const int s0 = lb * HB, s1 = min(s0 + HB, nn);
+    if (s0 >= s1) return;
     const GridParams g = *gp;
     const float cs = g.cellSize;
-    stage_plan(st, STAGE_CAP, s0, s1, nbA, eps, cs, W, H, ox, oy, start);
-    if (st.ok) {
-#pragma unroll
-        for (int i = 0; i < 6; i++) {
-            const int b = st.segS[i], len = st.segE[i] - b, o = st.segL[i];
-            for (int j = threadIdx.x; j < len; j += SB) lrec[o + j] = nbA[b + j];
-        }
+    __shared__ Hood hd;                                   // (LDS: the walks index it per lane)
+    {
+        Hood p;
+        hood_plan(p, s0, s1, nbA, eps, cs, W, H, ox, oy, start);
+        if (p.ok) hood_stage(p, lrec, lbnd, W, ox, oy, start, [&](int k) { return nbA[k]; });
+        if (threadIdx.x == 0) hd = p;
     }
     __syncthreads();
     const int s = s0 + threadIdx.x;
     if (s >= s1) return;
-    if (!st.ok && threadIdx.x == 0) atomicAdd(&status[ST_STAGE_FALLBACK], 1);
+    if (!hd.ok && threadIdx.x == 0) atomicAdd(&status[ST_STAGE_FALLBACK], 1);
     const float4 me = nbA[s];
     const float xi = me.x, yi = me.y;
     int cxp, cyp;
     cell_xy(xi, yi, eps, cs, cxp, cyp);
     const float h2 = h * h;
     const float poly6 = poly6Coeff2D(h);
+    const float reach = walk_reach(h, cs);
     float acc = 0.0f;
     int cnt = 0;
-    int16_t *grp = reinterpret_cast<int16_t *>(&lnl[threadIdx.x]);
-    auto body = [&](int k, const float4 &o) {
-        float dx = xi - o.x, dy = yi - o.y;
-        float r2 = dx * dx + dy * dy;
-        if (r2 < h2) {
-            float diff = h2 - r2;
-            float w = poly6 * diff * diff * diff;
-            acc += o.z * w;
-            if (k != s) {
-                const int off = k - s;
-                if (cnt < NLIST_CAP && off >= -32768 && off <= 32767) {
-                    grp[cnt & 7] = (int16_t)off;
-                    if ((cnt & 7) == 7) nlist[(size_t)(cnt >> 3) * nstride + s] = lnl[threadIdx.x];
-                } else {
-                    cnt = NLIST_CAP;          // overflow: forces walks the bins
-                }
-                cnt++;
-            }
+    int16_t *grp = reinterpret_cast<int16_t *>(&lnl[NL ? threadIdx.x : 0]);
+    // one candidate: r^2 < h^2 adds m * poly6 (h^2 - r^2)^3; otherwise +0,
+    // which leaves the non-negative sum unchanged bit for bit
+    auto term = [&](const float4 &o, bool valid) {
+        const float dx = xi - o.x, dy = yi - o.y;
+        const float r2 = dx * dx + dy * dy;
+        const float diff = h2 - r2;
+        const float w = poly6 * diff * diff * diff;
+        const float t = o.z * w;
+        const bool in = valid && r2 < h2;
+        acc += in ? t : 0.0f;
+        return in;
+    };
+    auto emit = [&](int k) {                              // a neighbour for the forces pass
+        if (k == s) return;
+        const int off = k - s;
+        if (cnt < NLIST_CAP && off >= -32768 && off <= 32767) {
+            grp[cnt & 7] = (int16_t)off;
+            if ((cnt & 7) == 7) nlist[(size_t)(cnt >> 3) * nstride + s] = lnl[threadIdx.x];
+        } else {
+            cnt = NLIST_CAP;                              // overflow: forces walks the bins
         }
+        cnt++;
     };
     if (refInv && ref_cap_slow(xi, yi, eps, g, W, ox, oy, start)) {
         // reference cell-capacity mode, an over-full cell in reach: the
         // reference's literal loop (no neighbour list; the forces pass walks
         // the same way)
-        ref_cap_walk(xi, yi, eps, g, W, ox, oy, start, sid, refInv, nn, status, [&](int k, int) {
-            const float4 o = nbA[k];
-            float dx = xi - o.x, dy = yi - o.y;
-            float r2 = dx * dx + dy * dy;
-            if (r2 < h2) {
-                float diff = h2 - r2;
-                float w = poly6 * diff * diff * diff;
-                acc += o.z * w;
-            }
-        });
+        ref_cap_walk(xi, yi, eps, g, W, ox, oy, start, sid, refInv, nn, status,
+                     [&](int k, int) { (void)term(nbA[k], true); });
         cnt = NLIST_CAP + 1;
-    } else if (st.ok)
-        walk_ranges(xi, yi, eps, cs, walk_reach(h, cs), g, W, H, ox, oy, start, [&](int b, int e, int cyc) {
-            // the LDS segment of cell row cyc, resolved once per range
-            const int i = (cyp == st.cy0 ? 0 : 3) + (cyc - cyp + 1);
-            const float4 *seg = lrec + (st.segL[i] - st.segS[i]);
-            for (int k = b; k < e; k += 4) {
-                float4 r[4];
-#pragma unroll
-                for (int j = 0; j < 4; j++) r[j] = seg[min(k + j, e - 1)];
-#pragma unroll
-                for (int j = 0; j < 4; j++)
-                    if (k + j < e) body(k + j, r[j]);
+    } else if (hd.ok) {
+        hood_ranges(hd, lbnd, xi, yi, eps, cs, reach, cyp, g, [&](int b, int e, int shift) {
+            for (int k = b; k < e; k += 2) {              // two candidates per trip, the second masked
+                const float4 r0 = lrec[k], r1 = lrec[k + 1];
+                const bool n0 = term(r0, true);
+                const bool n1 = term(r1, k + 1 < e);
+                if (NL) {
+                    if (n0) emit(k + shift);
+                    if (n1) emit(k + 1 + shift);
+                }
             }
         });
-    else
-        walk_neighbours<4>(xi, yi, eps, cs, walk_reach(h, cs), g, W, H, ox, oy, start,
-                           [&](int k, int) { return nbA[k]; }, body);
-    if (cnt <= NLIST_CAP && (cnt & 7)) nlist[(size_t)(cnt >> 3) * nstride + s] = lnl[threadIdx.x];
-    ncount[s] = cnt;
+    } else {
+        walk_neighbours<4>(xi, yi, eps, cs, reach, g, W, H, ox, oy, start,
+                           [&](int k, int) { return nbA[k]; },
+                           [&](int k, const float4 &o) { if (term(o, true) && NL) emit(k); });
+    }
+    if (NL) {
+        if (cnt <= NLIST_CAP && (cnt & 7)) nlist[(size_t)(cnt >> 3) * nstride + s] = lnl[threadIdx.x];
+        ncount[s] = cnt;
+    }
     float pres = stiffness * (acc - restDensity);
     if (pres < 0.f) pres = 0.f;
     rho[s] = acc;
@@ -1164,6 +1206,8 @@ __global__ void k_merge_prestats(int32_t *__restrict__ st, int32_t *__restrict__
     st[ST_STAGE_FALLBACK] += pre[ST_STAGE_FALLBACK];
     st[ST_OVER_CAP] += pre[ST_OVER_CAP];
     st[ST_REF_UB] |= pre[ST_REF_UB];
+    st[ST_OVER_CAP_TOTAL] += pre[ST_OVER_CAP_TOTAL];
+    st[ST_MAX_OCC_TOTAL] = max(st[ST_MAX_OCC_TOTAL], pre[ST_MAX_OCC_TOTAL]);
     for (int k = 0; k < ST_COUNT; k++) pre[k] = 0;
 }
 
@@ -1678,14 +1722,22 @@ static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool pr
     return LPE_OK;
 }
 
-// density over n slots (nptr: device count of the sharded sub-step)
-static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr, float *rho, float *pr) {
+// density over n slots (nptr: device count of the sharded sub-step); nl:
+// also the neighbour lists of the forces pass (the tick), else density only
+// (the probe / microbench)
+static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr, float *rho, float *pr, bool nl = true) {
     SphDev &d = ctx->sph;
     const lpe_fluid_config &c = d.cfg;
-    LPE_KERNEL(ctx, "k_density", k_density, dim3(xcd_grid(nblk(n, SB))), dim3(SB), 0, ctx->stream, n,
-                       nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
-                       c.restDensity, d.W, d.H, d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)d.nbB,
-                       rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d));
+    if (nl)
+        LPE_KERNEL(ctx, "k_density", k_density<true>, dim3(xcd_grid(nblk(n, HB))), dim3(HB), 0, ctx->stream, n,
+                   nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
+                   c.restDensity, d.W, d.H, d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)d.nbB,
+                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d));
+    else
+        LPE_KERNEL(ctx, "k_density", k_density<false>, dim3(xcd_grid(nblk(n, HB))), dim3(HB), 0, ctx->stream, n,
+                   nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
+                   c.restDensity, d.W, d.H, d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)d.nbB,
+                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d));
     LPE_CHECK_LAUNCH(ctx, "k_density");
     return LPE_OK;
 }
@@ -1850,6 +1902,10 @@ int sph_prelaunch(lpe_ctx *ctx, double dt_tick) {
 }
 
 extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
+    return sph_step_hooked(ctx, dt_tick, -1, nullptr);
+}
+
+int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int after, int (*hook)(lpe_ctx *)) {
     if (!ctx) return LPE_ERR_ARG;
     SphDev &d = ctx->sph;
     if (d.n <= 0 && !d.shard) return LPE_OK;  // fluid.cpp:969-972 (a slab rank joins the exchanges)
@@ -1929,6 +1985,15 @@ extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
                            d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart, d.rbinList,
                            d.acq, d.status);
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
+        if (hook && (step == after || (step + 1 == c.numSubSteps && after >= step))) {
+            st = hook(ctx);
+            if (st) return st;
+            hook = nullptr;
+        }
+    }
+    if (hook) {                                      // no sub-steps ran
+        st = hook(ctx);
+        if (st) return st;
     }
     if (d.nr > 0) {
         // slab decomposition: every rank holds its particles' share of the
@@ -2065,6 +2130,8 @@ extern "C" int lpe_sph_get_stats(lpe_ctx *ctx, lpe_sph_stats *out) {
     out->stageFallback = status[ST_STAGE_FALLBACK];
     out->overCapCells = status[ST_OVER_CAP];
     out->refUndefined = status[ST_REF_UB];
+    out->overCapCellsTotal = status[ST_OVER_CAP_TOTAL];
+    out->maxCellOccupancyTotal = status[ST_MAX_OCC_TOTAL];
     return LPE_OK;
 }
 
@@ -2087,6 +2154,7 @@ extern "C" int lpe_sph_diag(lpe_ctx *ctx, int on) {
     d.diag = on ? 1 : 0;
     if (d.status) {
         LPE_HIP(ctx, hipMemsetAsync(d.status + ST_NL_OVERFLOW, 0, sizeof(int32_t) * 4, ctx->stream));
+        LPE_HIP(ctx, hipMemsetAsync(d.status + ST_OVER_CAP_TOTAL, 0, sizeof(int32_t) * 2, ctx->stream));
     }
     return LPE_OK;
 }
@@ -2133,7 +2201,7 @@ extern "C" int lpe_sph_probe_density(lpe_ctx *ctx, float *density, float *pressu
     if (st) return st;
     st = sph_hash(ctx, 0.f, 0.f, false, true);
     if (st) return st;
-    st = sph_density(ctx, d.n, nullptr, d.rho, d.pr);   // the tick's density pass, as is
+    st = sph_density(ctx, d.n, nullptr, d.rho, d.pr, false);   // the tick's density kernel, no neighbour lists
     if (st) return st;
     // rho/p are in S slot order here; S.x.. are the unpermute staging buffers,
     // so keep S.id aside in tmpOld first

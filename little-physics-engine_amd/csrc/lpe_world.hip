@@ -207,7 +207,9 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
             if (st) return st;
         }
         if (fluid) {
-            int st = lpe_sph_step(ctx, dt_fluid);
+            // the detection's host half and the colouring launch after the
+            // second sub-step's forces (rigid_tick_detect)
+            int st = sph_step_hooked(ctx, dt_fluid, 1, overlap ? rigid_tick_detect : nullptr);
             if (st) return st;
             if (nr > 0)
                 LPE_KERNEL(ctx, "k_scatter_rigid_vel", k_scatter_rigid_vel, dim3(wblk(nr, 128)), dim3(128), 0, s, nr, d.coupleBody, d.rig, rd->bodies);

@@ -83,7 +83,8 @@ struct RigidDev {
     int32_t *hc = nullptr;                    // pinned: detection counts read by the host
     hipStream_t side = nullptr;
     hipEvent_t evStart = nullptr, evDetect = nullptr, evColour = nullptr;
-    bool overlap_pending = false;
+    bool overlap_pending = false;             // detection queued on the side stream
+    bool colour_pending = false;              // ... finished by the host, colouring queued
     // the position solver runs beside the PGS on its own stream (rigid_solve)
     hipStream_t psolve = nullptr;
     hipEvent_t evFork = nullptr, evJoin = nullptr;

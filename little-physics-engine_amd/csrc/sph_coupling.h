@@ -125,11 +125,16 @@ __host__ __device__ __forceinline__ float xacc_round(const unsigned long long *a
         if (d[i]) b = i * 32 + 31 - __builtin_clz(d[i]);
     if (b < 0) return 0.0f;
     const int p = b - 23 > 11 ? b - 23 : 11;                      // lsb kept; bit 11 is 2^-149
-    uint32_t kept = 0;
-    for (int k = b; k >= p; k--) kept = (kept << 1) | ((d[k >> 5] >> (k & 31)) & 1u);
-    const uint32_t guard = (d[(p - 1) >> 5] >> ((p - 1) & 31)) & 1u;
-    bool sticky = false;
-    for (int k = 0; k < p - 1; k++) sticky |= ((d[k >> 5] >> (k & 31)) & 1u) != 0u;
+    // kept = bits [p, b] (<= 24 bits, inside the 64-bit window of limbs
+    // p/32 and p/32 + 1); guard = bit p - 1; sticky = any bit below it
+    const int li = p >> 5;
+    const unsigned long long win =
+        (unsigned long long)d[li] | (li + 1 < XACC_LIMBS ? (unsigned long long)d[li + 1] << 32 : 0ull);
+    uint32_t kept = (uint32_t)((win >> (p & 31)) & ((1ull << (b - p + 1)) - 1ull));
+    const int gb = p - 1;
+    const uint32_t guard = (d[gb >> 5] >> (gb & 31)) & 1u;
+    bool sticky = (d[gb >> 5] & ((1u << (gb & 31)) - 1u)) != 0u;
+    for (int i = 0; i < (gb >> 5); i++) sticky |= d[i] != 0u;
     if (guard && (sticky || (kept & 1u))) kept++;
     const float r = ldexpf((float)kept, p - XACC_BIAS);          // exact
     return neg ? -r : r;

@@ -73,7 +73,8 @@ class SphStats(C.Structure):
                 ("gridDimX", C.c_int32), ("gridDimY", C.c_int32),
                 ("gridMinX", C.c_int32), ("gridMinY", C.c_int32), ("cellSize", C.c_float),
                 ("nlistOverflow", C.c_int32), ("rigidCandidates", C.c_int32), ("neighbours", C.c_int32),
-                ("stageFallback", C.c_int32), ("overCapCells", C.c_int32), ("refUndefined", C.c_int32)]
+                ("stageFallback", C.c_int32), ("overCapCells", C.c_int32), ("refUndefined", C.c_int32),
+                ("overCapCellsTotal", C.c_int32), ("maxCellOccupancyTotal", C.c_int32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

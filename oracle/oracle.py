@@ -280,6 +280,8 @@ def ref_rigid_ticks(cfg, bodies, verts, nticks, dt):
     """Runs the reference systems for nticks; returns the final bodies and the
     stage outputs of the last tick (pairs in quadtree order, contacts in
     narrowphase order, PGS contact order, snapshots)."""
+    # the driver's rigid_oracle.o resolves lpeo_fluid_tick from the oracle library
+    C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
     L = C.CDLL(REF_PATH)
     f = L.lpref_rigid_ticks
     f.argtypes = [C.POINTER(lpe.RigidConfig), C.c_double, C.c_double, C.c_double, C.c_double,
