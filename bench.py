@@ -401,7 +401,7 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--scene", default="M")
-    ap.add_argument("--prep", type=int, default=240,
+    ap.add_argument("--prep", type=int, default=3000,
                     help="untimed ticks that settle the scene before warmup (the pile forms)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",

@@ -568,23 +568,29 @@ __global__ void k_mark_contacts(const int32_t *__restrict__ ncptr, const lpe_con
     inContact[cs[k].b] = 1;
 }
 
+// loading the solver's bodies (contact_solver.cpp:480-507): what & 1 the
+// inverse masses (constant during the tick), what & 2 the velocities
 __global__ void k_pgs_bodies(int nb, const lpe_body *__restrict__ bodies, float *__restrict__ vel0,
-                             float *__restrict__ imii) {
+                             float *__restrict__ imii, int what) {
     int i = blockIdx.x * RTPB + threadIdx.x;
     if (i >= nb) return;
     const lpe_body b = bodies[i];
-    double m = b.mass;
-    float im = (m > 1e29) ? 0.f : (float)(1.0 / m);
-    float iv = 0.f;
     bool cr = can_rotate(b);
-    if (cr) {
-        double I = b.inertia;
-        if (I > 1e-12 && I < 1e29) iv = (float)(1.0 / I);
+    if (what & 1) {
+        double m = b.mass;
+        float im = (m > 1e29) ? 0.f : (float)(1.0 / m);
+        float iv = 0.f;
+        if (cr) {
+            double I = b.inertia;
+            if (I > 1e-12 && I < 1e29) iv = (float)(1.0 / I);
+        }
+        imii[2 * i] = im; imii[2 * i + 1] = iv;
     }
-    imii[2 * i] = im; imii[2 * i + 1] = iv;
-    vel0[3 * i] = (float)b.vx;
-    vel0[3 * i + 1] = (float)b.vy;
-    vel0[3 * i + 2] = cr ? (float)b.omega : 0.f;
+    if (what & 2) {
+        vel0[3 * i] = (float)b.vx;
+        vel0[3 * i + 1] = (float)b.vy;
+        vel0[3 * i + 2] = cr ? (float)b.omega : 0.f;
+    }
 }
 
 __device__ __forceinline__ float cross2f(float ax, float ay, float bx, float by) {
@@ -2090,9 +2096,80 @@ static int colour_launch(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     return LPE_OK;
 }
 
-// coloured: the colouring already ran (rigid_tick_finish, side stream)
+// ---- canonical-order solve (graph-coloured, see k_pair_colour), in three
+// launches groups.  The position solver (position_solver.cpp:299-325) reads
+// poses, masses and the narrowphase contacts, never a velocity; the PGS
+// (contact_solver.cpp:449-543) writes only v and omega, and its rows take the
+// lever arms from the poses BEFORE the position solver moves them
+// (contact_solver.cpp:133-197).  So everything except the PGS sweeps is
+// velocity independent and runs as soon as the contacts are coloured:
+//   colour_prep  contact marks, inverse masses, PGS rows, position items
+//   colour_pos   the position solver (one workgroup, poses in LDS)
+//   colour_pgs   the velocities (final only after the fluid and gravity
+//                systems have run) and the PGS sweeps
+// The reference runs PGS then the position solver; the results are the same
+// bits in any of these arrangements.
+static size_t colour_lds_cap() { return 159 * 1024; }   // of a CU's 160 KB (the kernels use < 1 KB static)
+
+static int colour_prep(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
+    const lpe_rigid_config &c = d->cfg;
+    const int nb = d->nb, nc = d->last_nc;
+    int32_t *inPos = d->inContact + nb;
+    LPE_HIP(ctx, hipMemsetAsync(d->inContact, 0, sizeof(int32_t) * 2 * nb, s));
+    LPE_KERNEL(ctx, "k_mark_contacts", k_mark_contacts, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->contacts, d->inContact);
+    LPE_KERNEL(ctx, "k_pgs_bodies", k_pgs_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->imii, 1);
+    LPE_KERNEL(ctx, "k_pgs_rows", k_pgs_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->order, d->contacts, d->bodies, d->imii, d->rowN, d->rowR, d->rowAB, d->rowM, d->sItemA, d->sItemB);
+    LPE_KERNEL(ctx, "k_pos_bodies", k_pos_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->posState);
+    LPE_KERNEL(ctx, "k_pos_fill_rows", k_pos_fill_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->order, d->contacts, d->bodies, d->posState, d->posRec, inPos, c.baumgarte, c.slop);
+    LPE_CHECK_LAUNCH(ctx, "solver preparation");
+    return LPE_OK;
+}
+
+static int colour_pos(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
+    const lpe_rigid_config &c = d->cfg;
+    const int nb = d->nb;
+    size_t lds2 = sizeof(double) * 3 * (size_t)nb;
+    const size_t ldsMax = colour_lds_cap();
+    int segLds2 = (int)std::min<size_t>((size_t)d->last_np, (ldsMax - std::min(ldsMax, lds2)) / sizeof(int2));
+    lds2 += sizeof(int2) * (size_t)segLds2;
+    LPE_KERNEL(ctx, "k_pos_colour", k_pos_colour, dim3(1), dim3(SOLVE_TPB), lds2, s, nb, d->counts, d->cbase, d->cseg, segLds2, d->posRec, d->bodies, d->posState, d->inContact + nb, c.posIterations);
+    LPE_CHECK_LAUNCH(ctx, "position solver");
+    return LPE_OK;
+}
+
+static int colour_pgs(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
+    const lpe_rigid_config &c = d->cfg;
+    const int nb = d->nb;
+    LPE_KERNEL(ctx, "k_pgs_bodies", k_pgs_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->imii, 2);
+    size_t lds = sizeof(float) * (3 * (size_t)nb + 1);
+    const size_t ldsMax = colour_lds_cap();
+    int segLds = (int)std::min<size_t>((size_t)d->last_np, (ldsMax - std::min(ldsMax, lds)) / sizeof(int2));
+    lds += sizeof(int2) * (size_t)segLds + 8;
+    LPE_KERNEL(ctx, "k_pgs_colour", k_pgs_colour, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts, d->cbase, d->cseg, segLds, d->rowN, d->rowR, d->rowAB, d->rowM, d->vel0, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF);
+    LPE_KERNEL(ctx, "k_pgs_writeback", k_pgs_writeback, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->inContact);
+    LPE_CHECK_LAUNCH(ctx, "pgs");
+    return LPE_OK;
+}
+
+static int solver_streams(lpe_ctx *ctx, RigidDev *d) {
+    if (d->psolve) return LPE_OK;
+    LPE_HIP(ctx, hipStreamCreateWithFlags(&d->psolve, hipStreamNonBlocking));
+    LPE_HIP(ctx, hipEventCreateWithFlags(&d->evFork, hipEventDisableTiming));
+    LPE_HIP(ctx, hipEventCreateWithFlags(&d->evJoin, hipEventDisableTiming));
+    return LPE_OK;
+}
+
+static int solver_lds_check(lpe_ctx *ctx, RigidDev *d) {
+    if ((size_t)d->nb * (3 * sizeof(double) + sizeof(int)) > 160 * 1024) {
+        ctx->err = "rigid solver: too many bodies for the LDS-resident solve (max 5851)";
+        return LPE_ERR_CAPACITY;
+    }
+    return LPE_OK;
+}
+
+// coloured: the colouring already ran (side stream)
 static int rigid_solve(lpe_ctx *ctx, RigidDev *d, bool colour, const int32_t *pgs_order,
-                       lpe_rigid_stats *stats, bool coloured = false) {
+                       lpe_rigid_stats *stats) {
     hipStream_t s = ctx->stream;
     const lpe_rigid_config &c = d->cfg;
     int nb = d->nb, nc = d->last_nc;
@@ -2104,64 +2181,36 @@ static int rigid_solve(lpe_ctx *ctx, RigidDev *d, bool colour, const int32_t *pg
         }
         return LPE_OK;
     }
-    if ((size_t)nb * (3 * sizeof(double) + sizeof(int)) > 160 * 1024) {
-        ctx->err = "rigid solver: too many bodies for the LDS-resident solve (max 5851)";
-        return LPE_ERR_CAPACITY;
-    }
-    const int32_t *ord = nullptr;
+    int st = solver_lds_check(ctx, d);
+    if (st) return st;
     if (colour) {
-        if (!coloured) {
-            int st0 = colour_launch(ctx, d, s);
-            if (st0) return st0;
-        }
-        ord = d->order;
-    } else if (pgs_order) {
-        LPE_HIP(ctx, hipMemcpyAsync(d->order, pgs_order, sizeof(int32_t) * nc, hipMemcpyHostToDevice, s));
-        ord = d->order;
-    }
-    // ---- PGS
-    LPE_HIP(ctx, hipMemsetAsync(d->inContact, 0, sizeof(int32_t) * 2 * nb, s));
-    LPE_KERNEL(ctx, "k_mark_contacts", k_mark_contacts, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->contacts, d->inContact);
-    LPE_KERNEL(ctx, "k_pgs_bodies", k_pgs_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->imii);
-    LPE_KERNEL(ctx, "k_pgs_rows", k_pgs_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, ord, d->contacts, d->bodies, d->imii, d->rowN, d->rowR, d->rowAB, d->rowM, d->sItemA, d->sItemB);
-    int32_t *inPos = d->inContact + nb;
-    if (colour) {
-        // canonical order: colour-synchronous sweeps over the colour segments
-        // LDS: body state, then as many pair segments as fit (the coloured
-        // pairs are at most last_np).
-        // The two solvers run CONCURRENTLY, one workgroup each: the position
-        // solver (position_solver.cpp:299-325) reads poses, masses and the
-        // narrowphase contacts, never a velocity, and the PGS
-        // (contact_solver.cpp:449-543) writes only v and omega and reads the
-        // poses before the position solver moves them (k_pgs_rows, below, is
-        // done before the fork).  The reference runs them one after the
-        // other; the results are the same bits.
-        const size_t ldsMax = 159 * 1024;      // of the 160 KB of a CU (the kernels use < 1 KB static)
-        LPE_KERNEL(ctx, "k_pos_bodies", k_pos_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->posState);
-        LPE_KERNEL(ctx, "k_pos_fill_rows", k_pos_fill_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->order, d->contacts, d->bodies, d->posState, d->posRec, inPos, c.baumgarte, c.slop);
-        if (!d->psolve) {
-            LPE_HIP(ctx, hipStreamCreateWithFlags(&d->psolve, hipStreamNonBlocking));
-            LPE_HIP(ctx, hipEventCreateWithFlags(&d->evFork, hipEventDisableTiming));
-            LPE_HIP(ctx, hipEventCreateWithFlags(&d->evJoin, hipEventDisableTiming));
-        }
+        // canonical order: colour, prepare, then the two solvers concurrently
+        // (one workgroup each) on the context stream and the solver stream
+        st = colour_launch(ctx, d, s);
+        if (!st) st = colour_prep(ctx, d, s);
+        if (!st) st = solver_streams(ctx, d);
+        if (st) return st;
         LPE_HIP(ctx, hipEventRecord(d->evFork, s));
         LPE_HIP(ctx, hipStreamWaitEvent(d->psolve, d->evFork, 0));
-        size_t lds2 = sizeof(double) * 3 * (size_t)nb;
-        int segLds2 = (int)std::min<size_t>((size_t)d->last_np, (ldsMax - std::min(ldsMax, lds2)) / sizeof(int2));
-        lds2 += sizeof(int2) * (size_t)segLds2;
-        LPE_KERNEL(ctx, "k_pos_colour", k_pos_colour, dim3(1), dim3(SOLVE_TPB), lds2, d->psolve, nb, d->counts, d->cbase, d->cseg, segLds2, d->posRec, d->bodies, d->posState, inPos, c.posIterations);
-        LPE_CHECK_LAUNCH(ctx, "position solver");
+        st = colour_pos(ctx, d, d->psolve);
+        if (st) return st;
         LPE_HIP(ctx, hipEventRecord(d->evJoin, d->psolve));
-        size_t lds = sizeof(float) * (3 * (size_t)nb + 1);
-        int segLds = (int)std::min<size_t>((size_t)d->last_np, (ldsMax - std::min(ldsMax, lds)) / sizeof(int2));
-        lds += sizeof(int2) * (size_t)segLds + 8;
-        LPE_KERNEL(ctx, "k_pgs_colour", k_pgs_colour, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts, d->cbase, d->cseg, segLds, d->rowN, d->rowR, d->rowAB, d->rowM, d->vel0, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF);
-        LPE_KERNEL(ctx, "k_pgs_writeback", k_pgs_writeback, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->inContact);
-        LPE_CHECK_LAUNCH(ctx, "pgs");
+        st = colour_pgs(ctx, d, s);
+        if (st) return st;
         LPE_HIP(ctx, hipStreamWaitEvent(s, d->evJoin, 0));
     } else {
         // caller-supplied order (reference replay): exact dataflow sweeps
-        int st = rigid_versions(ctx, d, d->counts + 1, nc);
+        const int32_t *ord = nullptr;
+        if (pgs_order) {
+            LPE_HIP(ctx, hipMemcpyAsync(d->order, pgs_order, sizeof(int32_t) * nc, hipMemcpyHostToDevice, s));
+            ord = d->order;
+        }
+        LPE_HIP(ctx, hipMemsetAsync(d->inContact, 0, sizeof(int32_t) * 2 * nb, s));
+        LPE_KERNEL(ctx, "k_mark_contacts", k_mark_contacts, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->contacts, d->inContact);
+        LPE_KERNEL(ctx, "k_pgs_bodies", k_pgs_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->imii, 3);
+        LPE_KERNEL(ctx, "k_pgs_rows", k_pgs_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, ord, d->contacts, d->bodies, d->imii, d->rowN, d->rowR, d->rowAB, d->rowM, d->sItemA, d->sItemB);
+        int32_t *inPos = d->inContact + nb;
+        st = rigid_versions(ctx, d, d->counts + 1, nc);
         if (st) return st;
         size_t lds = (sizeof(float) * 3 + sizeof(int)) * (size_t)nb;
         LPE_KERNEL(ctx, "k_pgs_flow", k_pgs_flow, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts + 1, d->rowN, d->rowR, d->rowAB, d->rowM, d->sVer, d->vel0, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF, d->counts + 7);
@@ -2299,11 +2348,17 @@ int rigid_tick_detect(lpe_ctx *ctx) {
         st = rigid_detect(ctx, d, 0, nullptr, d->side);
         if (st) return st;
     }
+    st = solver_streams(ctx, d);
+    if (st) return st;
     if (d->last_nc > 0) {
-        st = colour_launch(ctx, d, d->side);
+        // the velocity-independent preparation runs here, beside the fluid
+        // step: colouring, contact marks, PGS rows, position items
+        st = solver_lds_check(ctx, d);
+        if (!st) st = colour_launch(ctx, d, d->side);
+        if (!st) st = colour_prep(ctx, d, d->side);
         if (st) return st;
     }
-    LPE_HIP(ctx, hipEventRecord(d->evColour, d->side));
+    LPE_HIP(ctx, hipEventRecord(d->evColour, d->side));   // everything on the side stream
     d->colour_pending = true;
     return LPE_OK;
 }
@@ -2314,8 +2369,29 @@ int rigid_tick_finish(lpe_ctx *ctx) {
     int st = rigid_tick_detect(ctx);          // (already done inside the fluid step)
     if (st) return st;
     d->colour_pending = false;
-    LPE_HIP(ctx, hipStreamWaitEvent(ctx->stream, d->evColour, 0));
-    return rigid_solve(ctx, d, true, nullptr, nullptr, true);
+    hipStream_t s = ctx->stream;
+    if (d->last_nc == 0) {                    // early out (rigid_body_collision.cpp:35-37)
+        LPE_HIP(ctx, hipStreamWaitEvent(s, d->evColour, 0));
+        if (d->pcol && d->last_np > 0)
+            LPE_HIP(ctx, hipMemsetAsync(d->pcol, 0xff, sizeof(int32_t) * d->last_np, s));
+        LPE_HIP(ctx, hipMemsetAsync(d->counts + 8, 0, sizeof(int32_t), s));
+        return LPE_OK;
+    }
+    // the two solvers, concurrently: the PGS after the fluid, boundary and
+    // gravity systems set the velocities, the position solver (solver
+    // stream) beside it.  (Run during the fluid step instead, the
+    // one-workgroup position solver slows the full-chip fluid kernels by more
+    // than it saves.)
+    LPE_HIP(ctx, hipStreamWaitEvent(s, d->evColour, 0));
+    LPE_HIP(ctx, hipEventRecord(d->evFork, s));
+    LPE_HIP(ctx, hipStreamWaitEvent(d->psolve, d->evFork, 0));
+    st = colour_pos(ctx, d, d->psolve);
+    if (st) return st;
+    LPE_HIP(ctx, hipEventRecord(d->evJoin, d->psolve));
+    st = colour_pgs(ctx, d, s);
+    if (st) return st;
+    LPE_HIP(ctx, hipStreamWaitEvent(s, d->evJoin, 0));
+    return LPE_OK;
 }
 
 extern "C" int lpe_rigid_step_ordered(lpe_ctx *ctx, int np, const int32_t *pairs, int nc_order,

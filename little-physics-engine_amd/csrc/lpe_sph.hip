@@ -565,8 +565,17 @@ __device__ void ref_cap_walk(float xi, float yi, float eps, const GridParams &g,
 // (no serial section, one barrier).  A block whose neighbourhood does not fit
 // walks global memory instead.
 static constexpr int HB = 256;            // slots (threads) per staged block
-static constexpr int HCAP = 1792;         // records staged per block (28 KB of float4: 4 blocks per CU)
+static constexpr int HCAP = 1536;         // records staged per block (the forces pass stages 32 B each)
 static constexpr int HCELLS = 320;        // staged cells per block (4 boundaries each)
+// The forces pass stages the density pass's neighbourhood too (its neighbour
+// lists then hold LDS indices) or gathers from global memory (slot offsets).
+#ifndef LPE_FORCES_STAGED
+#define LPE_FORCES_STAGED 0
+#endif
+static constexpr bool FSTAGE = LPE_FORCES_STAGED != 0;
+#ifndef LPE_DEXP
+#define LPE_DEXP 0
+#endif
 
 __device__ __forceinline__ void cell_xy(float x, float y, float eps, float cs, int &cx, int &cy) {
     cx = (int)floorf((x + eps) / cs);
@@ -673,6 +682,40 @@ __device__ __forceinline__ void hood_ranges(const Hood &hd, const int *lbnd, flo
     }
 }
 
+// The walk of hood_ranges as one contiguous LDS span per cell row: from the
+// first walked quadrant of the row's first cell to the end of the last
+// walked quadrant of its last cell.  Slots are cell-major and quadrant-major
+// inside a cell, so the span visits the walked candidates in the canonical
+// order; the quadrants in between that the walk skips lie outside the reach
+// box (more than h * 1.002 away in x or y), so their r^2 >= h^2: they add +0
+// to a density sum and are never neighbours.  Rows the particle does not
+// reach get empty spans.  Span r covers [b[r], e[r]); shift[r] maps an LDS
+// index to its global slot.
+__device__ __forceinline__ void hood_spans(const Hood &hd, const int *lbnd, float xi, float yi, float eps,
+                                           float cs, float reach, int cyp, const GridParams &g, int b[3],
+                                           int e[3], int shift[3]) {
+    const float u = 2.0f * ((xi + eps) / cs), v = 2.0f * ((yi + eps) / cs);
+    const int bx0 = (int)floorf(u - reach), bx1 = (int)floorf(u + reach);
+    const int by0 = (int)floorf(v - reach), by1 = (int)floorf(v + reach);
+    const int cxa = max(bx0 >> 1, g.gridMinX), cxb = min(bx1 >> 1, g.gridMinX + g.gridDimX - 1);
+    const int cya = max(by0 >> 1, g.gridMinY), cyb = min(by1 >> 1, g.gridMinY + g.gridDimY - 1);
+    const int r3 = (cyp == hd.cy0) ? 0 : 3;
+    const int qa = max(bx0 - 2 * cxa, 0), qb = min(bx1 - 2 * cxb, 1);
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        const int cy = cyp - 1 + r;
+        b[r] = e[r] = shift[r] = 0;
+        if (cy < cya || cy > cyb || cxa > cxb) continue;
+        const int i = r3 + r;                                 // segment of this cell row
+        const int qya = max(by0 - 2 * cy, 0), qyb = min(by1 - 2 * cy, 1);
+        const int *ca = lbnd + 4 * (hd.bo[i] + cxa - hd.ca[i]);
+        const int *cb = lbnd + 4 * (hd.bo[i] + cxb - hd.ca[i]);
+        b[r] = ca[qya * 2 + qa];
+        e[r] = cb[qyb * 2 + qb + 1];                          // [4] is the next cell's start
+        shift[r] = hd.ss[i] - hd.l[i];
+    }
+}
+
 // computeDensity (metal:246-307), one thread per sorted slot, HB slots per
 // block with the neighbourhood staged in LDS.  NL: also write the neighbours
 // of the forces pass (r^2 < h^2, not itself: metal:360-366) in the canonical
@@ -688,7 +731,7 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
           float *__restrict__ rho, float *__restrict__ pr, uint4 *__restrict__ nlist,
           int32_t *__restrict__ ncount, int32_t *__restrict__ status, const int32_t *__restrict__ sid,
           const int32_t *__restrict__ refInv) {
-    __shared__ float4 lrec[HCAP + 1];                     // + 1: the pair-unrolled walk reads one past a range
+    __shared__ float4 lrec[HCAP + 4];                     // + 4: the span walk reads up to 3 past a span
     __shared__ int lbnd[4 * HCELLS];
     __shared__ uint4 lnl[NL ? HB : 1];                    // per thread: the current group of 8 offsets
     const int lb = xcd_block((n + HB - 1) / HB);
@@ -731,11 +774,12 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
         acc += in ? t : 0.0f;
         return in;
     };
-    auto emit = [&](int k) {                              // a neighbour for the forces pass
-        if (k == s) return;
-        const int off = k - s;
-        if (cnt < NLIST_CAP && off >= -32768 && off <= 32767) {
-            grp[cnt & 7] = (int16_t)off;
+    // a neighbour for the forces pass: its index in the staged LDS image
+    // (the forces pass stages the same neighbourhood: same blocks, same plan)
+    // or, for an unstaged block, its slot offset k - s
+    auto emit = [&](int code, bool ok) {
+        if (cnt < NLIST_CAP && ok) {
+            grp[cnt & 7] = (int16_t)code;
             if ((cnt & 7) == 7) nlist[(size_t)(cnt >> 3) * nstride + s] = lnl[threadIdx.x];
         } else {
             cnt = NLIST_CAP;                              // overflow: forces walks the bins
@@ -749,22 +793,39 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
         ref_cap_walk(xi, yi, eps, g, W, ox, oy, start, sid, refInv, nn, status,
                      [&](int k, int) { (void)term(nbA[k], true); });
         cnt = NLIST_CAP + 1;
+    } else if (LPE_DEXP == 1) {
     } else if (hd.ok) {
-        hood_ranges(hd, lbnd, xi, yi, eps, cs, reach, cyp, g, [&](int b, int e, int shift) {
-            for (int k = b; k < e; k += 2) {              // two candidates per trip, the second masked
-                const float4 r0 = lrec[k], r1 = lrec[k + 1];
-                const bool n0 = term(r0, true);
-                const bool n1 = term(r1, k + 1 < e);
-                if (NL) {
-                    if (n0) emit(k + shift);
-                    if (n1) emit(k + 1 + shift);
+        // one span per cell row (hood_spans), four candidates per trip with
+        // a wave-uniform trip count: LDS reads at immediate offsets, the
+        // lanes past their span masked
+        int sb[3], se[3], sh[3];
+        hood_spans(hd, lbnd, xi, yi, eps, cs, reach, cyp, g, sb, se, sh);
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            const int b = sb[r], len = se[r] - b;
+            for (int t = 0; __any(t < len); t += 4) {
+                const int a = min(b + t, HCAP);               // past every span: reads the pad, masked
+                float4 o[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) o[j] = lrec[a + j];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const bool in = term(o[j], t + j < len);
+                    if (NL) {                                 // (not itself: metal:360-366)
+                        const int k = b + t + j;
+                        const int oc = FSTAGE ? k : k + sh[r] - s;
+                        if (in && k + sh[r] != s) emit(oc, FSTAGE || (oc >= -32768 && oc <= 32767));
+                    }
                 }
             }
-        });
+        }
     } else {
         walk_neighbours<4>(xi, yi, eps, cs, reach, g, W, H, ox, oy, start,
                            [&](int k, int) { return nbA[k]; },
-                           [&](int k, const float4 &o) { if (term(o, true) && NL) emit(k); });
+                           [&](int k, const float4 &o) {
+                               if (term(o, true) && NL && k != s)
+                                   emit(k - s, k - s >= -32768 && k - s <= 32767);
+                           });
     }
     if (NL) {
         if (cnt <= NLIST_CAP && (cnt & 7)) nlist[(size_t)(cnt >> 3) * nstride + s] = lnl[threadIdx.x];
@@ -790,11 +851,16 @@ struct SphStepParams {
 };
 
 // computeForces + velocityVerletFinish + impulse + push-out; reads the sorted
-// records, writes P
+// records, writes P.  The block stages the same neighbourhood as the density
+// pass (same HB-slot blocks, same plan), now with both records of every
+// slot, so the neighbour list's LDS indices address the staged image and the
+// gathers never leave the CU.
 #ifndef LPE_FORCES_MINW
 #define LPE_FORCES_MINW 1
 #endif
-__global__ void __launch_bounds__(TPB, LPE_FORCES_MINW)
+struct FRec { float4 a, b; };        // nbA (x, y, m, -), nbB (vx, vy, rho, p / rho^2)
+
+__global__ void __launch_bounds__(HB, LPE_FORCES_MINW)
 k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict__ gp,
                 const int32_t *__restrict__ start, PState S, const float4 *__restrict__ nbA,
                 const float4 *__restrict__ nbB, const float *__restrict__ pr,
@@ -803,16 +869,34 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                 const int32_t *__restrict__ rbinStart, const int32_t *__restrict__ rbinList,
                 unsigned long long *__restrict__ acq,
                 int32_t *__restrict__ status) {
-    int lb = xcd_block((sp.n + TPB - 1) / TPB);
-    int s = lb * TPB + threadIdx.x;
-    if (lb < 0 || s >= (sp.nptr ? *sp.nptr : sp.n)) return;
+    __shared__ FRec lrec[FSTAGE ? HCAP + 1 : 1];
+    __shared__ int lbnd[FSTAGE ? 4 * HCELLS : 1];
+    __shared__ Hood hd;
+    const int lb = xcd_block((sp.n + HB - 1) / HB);
+    if (lb < 0) return;                                   // whole block idle
+    const int nn = sp.nptr ? *sp.nptr : sp.n;
+    const int s0 = lb * HB, s1 = min(s0 + HB, nn);
+    if (s0 >= s1) return;
+    const GridParams g = *gp;
+    const float cs = g.cellSize;
+    if (FSTAGE) {
+        Hood p;
+        hood_plan(p, s0, s1, nbA, sp.eps, cs, sp.W, sp.H, sp.ox, sp.oy, start);
+        if (p.ok)
+            hood_stage(p, lrec, lbnd, sp.W, sp.ox, sp.oy, start, [&](int k) { return FRec{nbA[k], nbB[k]}; });
+        if (threadIdx.x == 0) hd = p;
+        __syncthreads();
+    } else if (threadIdx.x == 0) {
+        hd.ok = false;
+    }
+    if (!FSTAGE) __syncthreads();
+    const int s = s0 + threadIdx.x;
+    if (s >= s1) return;
     int out = s;                              // P slot written
     if (sp.dst) {                             // ghosts are neighbours only
         out = sp.dst[s];
         if (sp.dst[s + 1] == out) return;
     }
-    const GridParams g = *gp;
-    const float cs = g.cellSize;
     const float4 meA = nbA[s], meB = nbB[s];
     const float xi = meA.x, yi = meA.y;
     const float vxi = meB.x, vyi = meB.y;
@@ -829,25 +913,24 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     const float pti = meB.w;                      // pi / (rhoi * rhoi)
     const bool rhoi_ok = !(rhoi < sp.minDens);
     float sumFx = 0.f, sumFy = 0.f;
-    struct Rec { float4 a, b; };
-    auto pair = [&](int k, const Rec &o) {
-        if (k == s) return;
-        float dx = xi - o.a.x, dy = yi - o.a.y;
+    // one neighbour j != i (metal:352-399)
+    auto pair = [&](const float4 &oa, const float4 &ob) {
+        float dx = xi - oa.x, dy = yi - oa.y;
         float r2 = dx * dx + dy * dy;
         if (r2 < sp.minDist) return;
         if (r2 >= h_ij2) return;
         float r = sqrtf(r2);
-        float rhoj = o.b.z;
+        float rhoj = ob.z;
         if (rhoj < sp.minDens || !rhoi_ok) return;
-        float mj = o.a.z;
-        float term = pti + o.b.w;
+        float mj = oa.z;
+        float term = pti + ob.w;
         float diff = (h_ij - r);
         float wSpiky = spF * (diff * diff);
         float rx = dx / r, ry = dy / r;
         float fxPress = -mj * term * wSpiky;
         float fx = fxPress * rx;
         float fy = fxPress * ry;
-        float vx_ij = vxi - o.b.x, vy_ij = vyi - o.b.y;
+        float vx_ij = vxi - ob.x, vy_ij = vyi - ob.y;
         float wVisc = lapC * diff;
         float fVisc = sp.viscosity * mj * (wVisc / rhoj);
         fx -= fVisc * vx_ij;
@@ -862,32 +945,48 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     }
     if (sp.refInv && ref_cap_slow(xi, yi, sp.eps, g, sp.W, sp.ox, sp.oy, start)) {
         // reference cell-capacity mode: the reference's literal loop
-        // (metal:345-351; the j == i skip is the slot test in pair)
+        // (metal:345-351; nbrID == globalID is skipped)
         ref_cap_walk(xi, yi, sp.eps, g, sp.W, sp.ox, sp.oy, start, S.id, sp.refInv, sp.n, status,
-                     [&](int k, int) { pair(k, Rec{nbA[k], nbB[k]}); });
+                     [&](int k, int) { if (k != s) pair(nbA[k], nbB[k]); });
     } else if (cnt <= NLIST_CAP) {
         // the density pass's list: the r^2 < h^2 neighbours in canonical
-        // order, so the heavy pair math runs only on real neighbours
-        constexpr int U = 8;                      // one group of eight offsets, all loads in flight
+        // order, so the heavy pair math runs only on real neighbours; staged
+        // blocks hold LDS indices, the others slot offsets
+        const bool staged = FSTAGE && hd.ok;
+        constexpr int U = 8;                      // one group of eight entries
         for (int j = 0; j < cnt; j += U) {
             const uint4 g8 = nlist[(size_t)(j >> 3) * sp.nstride + s];
             const uint32_t w[4] = {g8.x, g8.y, g8.z, g8.w};
             int kk[U];
 #pragma unroll
-            for (int u = 0; u < U; u++) kk[u] = s + (int)(int16_t)((w[u >> 1] >> (16 * (u & 1))) & 0xffffu);
+            for (int u = 0; u < U; u++) kk[u] = (int)(int16_t)((w[u >> 1] >> (16 * (u & 1))) & 0xffffu);
+            if (staged) {
 #pragma unroll
-            for (int u = 1; u < U; u++)
-                if (j + u >= cnt) kk[u] = kk[0];       // unused entries of the last group
-            Rec r[U];
+                for (int u = 0; u < U; u++)
+                    if (j + u < cnt) pair(lrec[kk[u]].a, lrec[kk[u]].b);
+            } else {
 #pragma unroll
-            for (int u = 0; u < U; u++) r[u] = Rec{nbA[kk[u]], nbB[kk[u]]};
+                for (int u = 0; u < U; u++) kk[u] = s + (j + u < cnt ? kk[u] : 0);
+                FRec r[U];
 #pragma unroll
-            for (int u = 0; u < U; u++)
-                if (j + u < cnt) pair(kk[u], r[u]);
+                for (int u = 0; u < U; u++) r[u] = FRec{nbA[kk[u]], nbB[kk[u]]};
+#pragma unroll
+                for (int u = 0; u < U; u++)
+                    if (j + u < cnt) pair(r[u].a, r[u].b);
+            }
         }
+    } else if (FSTAGE && hd.ok) {
+        // more than NLIST_CAP neighbours: the canonical walk over the staged image
+        int cxp, cyp;
+        cell_xy(xi, yi, sp.eps, cs, cxp, cyp);
+        hood_ranges(hd, lbnd, xi, yi, sp.eps, cs, walk_reach(hi, cs), cyp, g, [&](int b, int e, int shift) {
+            for (int k = b; k < e; k++)
+                if (k + shift != s) pair(lrec[k].a, lrec[k].b);
+        });
     } else {
         walk_neighbours<4>(xi, yi, sp.eps, cs, walk_reach(hi, cs), g, sp.W, sp.H, sp.ox, sp.oy, start,
-                           [&](int k, int) { return Rec{nbA[k], nbB[k]}; }, pair);
+                           [&](int k, int) { return FRec{nbA[k], nbB[k]}; },
+                           [&](int k, const FRec &o) { if (k != s) pair(o.a, o.b); });
     }
     CoupleState st;
     st.x = xi; st.y = yi;
@@ -1980,7 +2079,7 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int after, int (*hook)(lpe_ctx
             st = sph_density(ctx, d.n, nullptr, d.rho, d.pr);
         }
         if (st) return st;
-        LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(xcd_grid(nblk(sp.n))), dim3(TPB), 0, s, sp, cp,
+        LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(xcd_grid(nblk(sp.n, HB))), dim3(HB), 0, s, sp, cp,
                            (step == 0 && pre) ? d.gp + 1 : d.gp,
                            d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart, d.rbinList,
                            d.acq, d.status);
