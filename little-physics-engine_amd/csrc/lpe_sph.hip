@@ -564,15 +564,9 @@ __device__ void ref_cap_walk(float xi, float yi, float eps, const GridParams &g,
 // canonical one.  The plan is computed by every wave from block-uniform loads
 // (no serial section, one barrier).  A block whose neighbourhood does not fit
 // walks global memory instead.
-static constexpr int HB = 256;            // slots (threads) per staged block
-static constexpr int HCAP = 1536;         // records staged per block (the forces pass stages 32 B each)
-static constexpr int HCELLS = 320;        // staged cells per block (4 boundaries each)
-// The forces pass stages the density pass's neighbourhood too (its neighbour
-// lists then hold LDS indices) or gathers from global memory (slot offsets).
-#ifndef LPE_FORCES_STAGED
-#define LPE_FORCES_STAGED 0
-#endif
-static constexpr bool FSTAGE = LPE_FORCES_STAGED != 0;
+static constexpr int HB = 256;            // slots (threads) per staged block (4 waves: hood_stage)
+static constexpr int HCAP = 1536;         // records staged per block (6 per thread)
+static constexpr int HBND = 1280;         // staged cell boundaries per block (5 per thread)
 #ifndef LPE_DEXP
 #define LPE_DEXP 0
 #endif
@@ -585,8 +579,10 @@ __device__ __forceinline__ void cell_xy(float x, float y, float eps, float cs, i
 struct Hood {
     bool ok;
     int nrun, cy0;            // runs (1 or 2: rows cy0, cy0 + 1)
-    int ca[6], ss[6], se[6];  // per segment r * 3 + dy + 1: first cell column, global slot range
-    int l[6], bo[6];          // LDS record offset; boundary-table entry of the first cell
+    int L, NB;                // records, boundaries staged
+    int ca[6], ss[6];         // per segment r * 3 + dy + 1: first cell column, first global slot
+    int l[6], bb[6];          // LDS record offset; LDS offset of the first cell's boundaries
+    int g0[6];                // global index of the first cell's first boundary
     int ncell[6];             // cells in the segment (0: none)
 };
 
@@ -604,6 +600,8 @@ __device__ __forceinline__ void hood_plan(Hood &hd, int s0, int s1, const float4
     if (cy1 == cy0) {
         hd.nrun = 1;
     } else if (cy1 == cy0 + 1 && cy1 - oy >= 0 && cy1 - oy < H) {
+        // two runs: row cy0 from cx0 to the cell of the last slot before row
+        // cy1, row cy1 from the cell of its first slot to cx1
         hd.nrun = 2;
         const int rs = start[((cy1 - oy) * W) << 2];        // first slot of row cy1 (> s0)
         const float4 e0 = nbA[rs - 1], b1 = nbA[rs];
@@ -615,82 +613,97 @@ __device__ __forceinline__ void hood_plan(Hood &hd, int s0, int s1, const float4
         hd.ok = false;
         return;
     }
-    int L = 0, B = 0;
+    int L = 0, NB = 0;
 #pragma unroll
     for (int i = 0; i < 6; i++) {
         const int r = i / 3, row = cy0 + r + (i % 3) - 1;
         const int ca = max(xa[r] - 1, ox), cb = min(xb[r] + 1, ox + W - 1);
         hd.l[i] = L;
-        hd.bo[i] = B;
+        hd.bb[i] = NB;
         hd.ca[i] = ca;
         hd.ncell[i] = 0;
-        hd.ss[i] = hd.se[i] = 0;
+        hd.ss[i] = hd.g0[i] = 0;
         if (r < hd.nrun && row >= oy && row < oy + H && ca <= cb) {
-            const int base = (row - oy) * W - ox;
-            hd.ss[i] = start[(base + ca) << 2];
-            hd.se[i] = start[((base + cb) << 2) + 4];
+            const int g0 = (((row - oy) * W) + ca - ox) << 2;
+            const int ss = start[g0], se = start[((((row - oy) * W) + cb - ox) << 2) + 4];
+            hd.ss[i] = ss;
+            hd.g0[i] = g0;
             hd.ncell[i] = cb - ca + 1;
-            L += hd.se[i] - hd.ss[i];
-            B += cb - ca + 2;                                // + the end sentinel
+            L += se - ss;
+            NB += 4 * (cb - ca + 1) + 1;                     // + the end sentinel
         }
     }
-    hd.ok = L <= HCAP && B <= HCELLS;
+    hd.L = L;
+    hd.NB = NB;
+    hd.ok = L <= HCAP && NB <= HBND;
 }
 
-// copies the planned records (rec[k] -> lrec) and the cells' quadrant starts
-// (rebased to LDS offsets, 4 per cell + the segment end) into LDS
-template <typename R, class Ld>
-__device__ __forceinline__ void hood_stage(const Hood &hd, R *lrec, int *lbnd, int W, int ox, int oy,
-                                           const int32_t *__restrict__ start, Ld ld) {
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void glb_void_t;
+
+// Copies the planned records and the cells' quadrant starts into LDS in one
+// pass of asynchronous global -> LDS loads (global_load_lds: each lane's
+// source address is its own, the destination the wave's base + lane * size):
+// the records form one flat LDS array (segment i at l[i]), the boundaries
+// another (segment i's cells at bb[i], 4 per cell + the segment end), kept
+// as global slot numbers (a reader adds l[i] - ss[i]).  Every load of the
+// block is in flight at once; the caller's __syncthreads() retires them.
+// (Per-segment chunks of 64 instead of the flat index: fewer VALU per load
+// but three times the SALU, measured slower.)
+__device__ __forceinline__ void hood_stage(const Hood &hd, float4 *lrec, int *lbnd,
+                                           const float4 *__restrict__ nbA,
+                                           const int32_t *__restrict__ start, int s0) {
+    const int wbase = threadIdx.x & ~63;
 #pragma unroll
-    for (int i = 0; i < 6; i++) {
-        if (!hd.ncell[i]) continue;
-        const int b = hd.ss[i], len = hd.se[i] - b, o = hd.l[i];
-        for (int j = threadIdx.x; j < len; j += HB) lrec[o + j] = ld(b + j);
-        const int row = hd.cy0 + i / 3 + (i % 3) - 1;
-        const int g0 = (((row - oy) * W) + hd.ca[i] - ox) << 2;   // first boundary of the segment
-        const int nb = 4 * hd.ncell[i] + 1;
-        const int shift = o - b;
-        for (int j = threadIdx.x; j < nb; j += HB) lbnd[4 * hd.bo[i] + j] = start[g0 + j] + shift;
+    for (int u = 0; u < HCAP / HB; u++) {
+        const int f0 = u * HB;
+        if (f0 >= hd.L) break;
+        const int f = f0 + threadIdx.x;
+        int d = hd.ss[0] - hd.l[0];
+#pragma unroll
+        for (int i = 1; i < 6; i++)
+            if (f >= hd.l[i]) d = hd.ss[i] - hd.l[i];
+        const int src = f < hd.L ? f + d : s0;            // lanes past the end copy a valid record
+        __builtin_amdgcn_global_load_lds((glb_void_t *)(nbA + src), (lds_void_t *)(lrec + f0 + wbase), 16, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < HBND / HB; u++) {
+        const int f0 = u * HB;
+        if (f0 >= hd.NB) break;
+        const int f = f0 + threadIdx.x;
+        int d = hd.g0[0] - hd.bb[0];
+#pragma unroll
+        for (int i = 1; i < 6; i++)
+            if (f >= hd.bb[i]) d = hd.g0[i] - hd.bb[i];
+        const int src = f < hd.NB ? f + d : 0;
+        __builtin_amdgcn_global_load_lds((glb_void_t *)(start + src), (lds_void_t *)(lbnd + f0 + wbase), 4, 0, 0);
     }
 }
 
-// The canonical walk (walk_ranges) over the staged neighbourhood: f(b, e)
-// for each (cell, quadrant row) range [b, e) of LDS records, in the order of
-// walk_ranges.  (cxp, cyp): the particle's cell.
-template <class F>
-__device__ __forceinline__ void hood_ranges(const Hood &hd, const int *lbnd, float xi, float yi, float eps,
-                                            float cs, float reach, int cyp, const GridParams &g, F f) {
-    const float u = 2.0f * ((xi + eps) / cs), v = 2.0f * ((yi + eps) / cs);
-    const int bx0 = (int)floorf(u - reach), bx1 = (int)floorf(u + reach);
-    const int by0 = (int)floorf(v - reach), by1 = (int)floorf(v + reach);
-    const int cxa = max(bx0 >> 1, g.gridMinX), cxb = min(bx1 >> 1, g.gridMinX + g.gridDimX - 1);
-    const int cya = max(by0 >> 1, g.gridMinY), cyb = min(by1 >> 1, g.gridMinY + g.gridDimY - 1);
-    const int r3 = (cyp == hd.cy0) ? 0 : 3;
-    for (int cy = cya; cy <= cyb; cy++) {
-        const int i = r3 + cy - cyp + 1;                      // segment of this cell row
-        const int qya = max(by0 - 2 * cy, 0), qyb = min(by1 - 2 * cy, 1);
-        const int shift = hd.ss[i] - hd.l[i];                 // LDS index -> global slot
-        for (int cx = cxa; cx <= cxb; cx++) {
-            const int qxa = max(bx0 - 2 * cx, 0), qxb = min(bx1 - 2 * cx, 1);
-            const int *cb = lbnd + 4 * (hd.bo[i] + cx - hd.ca[i]);
-            for (int qy = qya; qy <= qyb; qy++) {
-                const int b = cb[qy * 2 + qxa], e = cb[qy * 2 + qxb + 1];   // [4] is the next cell's start
-                f(b, e, shift);
-            }
-        }
+// min and max of v (0 <= v < 65536) over the wave, as wave-uniform values
+// (every lane active): one xor-shuffle tree on the pair (v, 65535 - v)
+typedef unsigned short ushort2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void wave_minmax(int v, int &mn, int &mx) {
+    ushort2v p = {(unsigned short)v, (unsigned short)(0xffff - v)};
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        unsigned u = __builtin_bit_cast(unsigned, p);
+        unsigned o = (unsigned)__shfl_xor((int)u, m);
+        p = __builtin_elementwise_max(p, __builtin_bit_cast(ushort2v, o));
     }
+    mx = __builtin_amdgcn_readfirstlane((int)p.x);
+    mn = __builtin_amdgcn_readfirstlane(0xffff - (int)p.y);
 }
 
-// The walk of hood_ranges as one contiguous LDS span per cell row: from the
-// first walked quadrant of the row's first cell to the end of the last
-// walked quadrant of its last cell.  Slots are cell-major and quadrant-major
-// inside a cell, so the span visits the walked candidates in the canonical
-// order; the quadrants in between that the walk skips lie outside the reach
-// box (more than h * 1.002 away in x or y), so their r^2 >= h^2: they add +0
-// to a density sum and are never neighbours.  Rows the particle does not
-// reach get empty spans.  Span r covers [b[r], e[r]); shift[r] maps an LDS
-// index to its global slot.
+// The canonical walk over the staged neighbourhood, as one contiguous LDS
+// span per cell row: from the first walked quadrant of the row's first cell
+// to the end of the last walked quadrant of its last cell.  Slots are
+// cell-major and quadrant-major inside a cell, so the span visits the walked
+// candidates (walk_ranges) in the canonical order; the quadrants in between
+// that the walk skips lie outside the reach box (more than h * 1.002 away in
+// x or y), so their r^2 >= h^2: they add +0 to a density sum and are never
+// neighbours.  Rows the particle does not reach get empty spans.  Span r
+// covers LDS records [b[r], e[r]); shift[r] maps an LDS index to its slot.
 __device__ __forceinline__ void hood_spans(const Hood &hd, const int *lbnd, float xi, float yi, float eps,
                                            float cs, float reach, int cyp, const GridParams &g, int b[3],
                                            int e[3], int shift[3]) {
@@ -708,11 +721,12 @@ __device__ __forceinline__ void hood_spans(const Hood &hd, const int *lbnd, floa
         if (cy < cya || cy > cyb || cxa > cxb) continue;
         const int i = r3 + r;                                 // segment of this cell row
         const int qya = max(by0 - 2 * cy, 0), qyb = min(by1 - 2 * cy, 1);
-        const int *ca = lbnd + 4 * (hd.bo[i] + cxa - hd.ca[i]);
-        const int *cb = lbnd + 4 * (hd.bo[i] + cxb - hd.ca[i]);
-        b[r] = ca[qya * 2 + qa];
-        e[r] = cb[qyb * 2 + qb + 1];                          // [4] is the next cell's start
-        shift[r] = hd.ss[i] - hd.l[i];
+        const int *c0 = lbnd + hd.bb[i] + 4 * (cxa - hd.ca[i]);
+        const int *c1 = lbnd + hd.bb[i] + 4 * (cxb - hd.ca[i]);
+        const int rebase = hd.l[i] - hd.ss[i];               // global slot -> LDS index
+        b[r] = c0[qya * 2 + qa] + rebase;
+        e[r] = c1[qyb * 2 + qb + 1] + rebase;                 // [4] is the next cell's start
+        shift[r] = -rebase;
     }
 }
 
@@ -732,7 +746,7 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
           int32_t *__restrict__ ncount, int32_t *__restrict__ status, const int32_t *__restrict__ sid,
           const int32_t *__restrict__ refInv) {
     __shared__ float4 lrec[HCAP + 4];                     // + 4: the span walk reads up to 3 past a span
-    __shared__ int lbnd[4 * HCELLS];
+    __shared__ int lbnd[HBND];
     __shared__ uint4 lnl[NL ? HB : 1];                    // per thread: the current group of 8 offsets
     const int lb = xcd_block((n + HB - 1) / HB);
     if (lb < 0) return;                                   // whole block idle
@@ -745,14 +759,17 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     {
         Hood p;
         hood_plan(p, s0, s1, nbA, eps, cs, W, H, ox, oy, start);
-        if (p.ok) hood_stage(p, lrec, lbnd, W, ox, oy, start, [&](int k) { return nbA[k]; });
+        if (p.ok) hood_stage(p, lrec, lbnd, nbA, start, s0);
         if (threadIdx.x == 0) hd = p;
     }
     __syncthreads();
+    // every lane stays to the end (the span walk's trip counts are wave
+    // reductions); lanes past the block's last slot walk nothing
     const int s = s0 + threadIdx.x;
-    if (s >= s1) return;
+    const bool live = s < s1;
+    const int sl = live ? s : s1 - 1;
     if (!hd.ok && threadIdx.x == 0) atomicAdd(&status[ST_STAGE_FALLBACK], 1);
-    const float4 me = nbA[s];
+    const float4 me = nbA[sl];
     const float xi = me.x, yi = me.y;
     int cxp, cyp;
     cell_xy(xi, yi, eps, cs, cxp, cyp);
@@ -774,9 +791,16 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
         acc += in ? t : 0.0f;
         return in;
     };
-    // a neighbour for the forces pass: its index in the staged LDS image
-    // (the forces pass stages the same neighbourhood: same blocks, same plan)
-    // or, for an unstaged block, its slot offset k - s
+    // the same sum without the neighbour test: max(h^2 - r^2, 0) is h^2 - r^2
+    // inside and +0 outside, where the term is then m * (+0) = +0
+    auto term0 = [&](const float4 &o, bool valid) {
+        const float dx = xi - o.x, dy = yi - o.y;
+        const float r2 = dx * dx + dy * dy;
+        const float diff = fmaxf(h2 - r2, 0.0f);
+        const float t = o.z * (poly6 * diff * diff * diff);
+        acc += valid ? t : 0.0f;
+    };
+    // a neighbour for the forces pass: its slot offset k - s
     auto emit = [&](int code, bool ok) {
         if (cnt < NLIST_CAP && ok) {
             grp[cnt & 7] = (int16_t)code;
@@ -786,40 +810,57 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
         }
         cnt++;
     };
-    if (refInv && ref_cap_slow(xi, yi, eps, g, W, ox, oy, start)) {
-        // reference cell-capacity mode, an over-full cell in reach: the
-        // reference's literal loop (no neighbour list; the forces pass walks
-        // the same way)
-        ref_cap_walk(xi, yi, eps, g, W, ox, oy, start, sid, refInv, nn, status,
-                     [&](int k, int) { (void)term(nbA[k], true); });
-        cnt = NLIST_CAP + 1;
-    } else if (LPE_DEXP == 1) {
+    // reference cell-capacity mode, an over-full cell in reach: the
+    // reference's literal loop (no neighbour list; the forces pass walks the
+    // same way)
+    const bool slow = live && refInv && ref_cap_slow(xi, yi, eps, g, W, ox, oy, start);
+    if (LPE_DEXP == 1) {
     } else if (hd.ok) {
-        // one span per cell row (hood_spans), four candidates per trip with
-        // a wave-uniform trip count: LDS reads at immediate offsets, the
-        // lanes past their span masked
+        // one span per cell row (hood_spans), the non-empty ones first; four
+        // candidates per trip, trip counts wave-uniform: unmasked trips up to
+        // the wave's shortest span, masked ones up to its longest.  LDS reads
+        // at immediate offsets.
         int sb[3], se[3], sh[3];
         hood_spans(hd, lbnd, xi, yi, eps, cs, reach, cyp, g, sb, se, sh);
 #pragma unroll
+        for (int r = 0; r < 3; r++)
+            if (!live || slow) sb[r] = se[r] = 0;
+#pragma unroll
+        for (int pass = 0; pass < 2; pass++)
+#pragma unroll
+            for (int r = 0; r < 2; r++)
+                if (se[r] == sb[r]) {
+                    sb[r] = sb[r + 1]; se[r] = se[r + 1]; sh[r] = sh[r + 1];
+                    sb[r + 1] = se[r + 1] = 0;
+                }
+#pragma unroll
         for (int r = 0; r < 3; r++) {
             const int b = sb[r], len = se[r] - b;
-            for (int t = 0; __any(t < len); t += 4) {
-                const int a = min(b + t, HCAP);               // past every span: reads the pad, masked
+            int lmin, lmax;
+            wave_minmax(len, lmin, lmax);
+            if (lmax == 0) break;                         // (later spans are empty too)
+            auto trip = [&](int t, bool masked) {
+                const int a = min(b + t, HCAP);           // past every span: reads the pad, masked
                 float4 o[4];
 #pragma unroll
                 for (int j = 0; j < 4; j++) o[j] = lrec[a + j];
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
-                    const bool in = term(o[j], t + j < len);
-                    if (NL) {                                 // (not itself: metal:360-366)
-                        const int k = b + t + j;
-                        const int oc = FSTAGE ? k : k + sh[r] - s;
-                        if (in && k + sh[r] != s) emit(oc, FSTAGE || (oc >= -32768 && oc <= 32767));
+                    const bool valid = !masked || t + j < len;
+                    if (NL) {
+                        const bool in = term(o[j], valid);
+                        const int oc = b + t + j + sh[r] - s;
+                        if (in && oc != 0) emit(oc, oc >= -32768 && oc <= 32767);   // (not itself: metal:360-366)
+                    } else {
+                        term0(o[j], valid);
                     }
                 }
-            }
+            };
+            int t = 0;
+            for (; t + 4 <= lmin; t += 4) trip(t, false);
+            for (; t < lmax; t += 4) trip(t, true);
         }
-    } else {
+    } else if (live && !slow) {
         walk_neighbours<4>(xi, yi, eps, cs, reach, g, W, H, ox, oy, start,
                            [&](int k, int) { return nbA[k]; },
                            [&](int k, const float4 &o) {
@@ -827,6 +868,12 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
                                    emit(k - s, k - s >= -32768 && k - s <= 32767);
                            });
     }
+    if (slow) {
+        ref_cap_walk(xi, yi, eps, g, W, ox, oy, start, sid, refInv, nn, status,
+                     [&](int k, int) { (void)term(nbA[k], true); });
+        cnt = NLIST_CAP + 1;
+    }
+    if (!live) return;
     if (NL) {
         if (cnt <= NLIST_CAP && (cnt & 7)) nlist[(size_t)(cnt >> 3) * nstride + s] = lnl[threadIdx.x];
         ncount[s] = cnt;
@@ -869,9 +916,6 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                 const int32_t *__restrict__ rbinStart, const int32_t *__restrict__ rbinList,
                 unsigned long long *__restrict__ acq,
                 int32_t *__restrict__ status) {
-    __shared__ FRec lrec[FSTAGE ? HCAP + 1 : 1];
-    __shared__ int lbnd[FSTAGE ? 4 * HCELLS : 1];
-    __shared__ Hood hd;
     const int lb = xcd_block((sp.n + HB - 1) / HB);
     if (lb < 0) return;                                   // whole block idle
     const int nn = sp.nptr ? *sp.nptr : sp.n;
@@ -879,17 +923,6 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     if (s0 >= s1) return;
     const GridParams g = *gp;
     const float cs = g.cellSize;
-    if (FSTAGE) {
-        Hood p;
-        hood_plan(p, s0, s1, nbA, sp.eps, cs, sp.W, sp.H, sp.ox, sp.oy, start);
-        if (p.ok)
-            hood_stage(p, lrec, lbnd, sp.W, sp.ox, sp.oy, start, [&](int k) { return FRec{nbA[k], nbB[k]}; });
-        if (threadIdx.x == 0) hd = p;
-        __syncthreads();
-    } else if (threadIdx.x == 0) {
-        hd.ok = false;
-    }
-    if (!FSTAGE) __syncthreads();
     const int s = s0 + threadIdx.x;
     if (s >= s1) return;
     int out = s;                              // P slot written
@@ -950,9 +983,8 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                      [&](int k, int) { if (k != s) pair(nbA[k], nbB[k]); });
     } else if (cnt <= NLIST_CAP) {
         // the density pass's list: the r^2 < h^2 neighbours in canonical
-        // order, so the heavy pair math runs only on real neighbours; staged
-        // blocks hold LDS indices, the others slot offsets
-        const bool staged = FSTAGE && hd.ok;
+        // order as slot offsets, so the heavy pair math runs only on real
+        // neighbours
         constexpr int U = 8;                      // one group of eight entries
         for (int j = 0; j < cnt; j += U) {
             const uint4 g8 = nlist[(size_t)(j >> 3) * sp.nstride + s];
@@ -960,29 +992,15 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
             int kk[U];
 #pragma unroll
             for (int u = 0; u < U; u++) kk[u] = (int)(int16_t)((w[u >> 1] >> (16 * (u & 1))) & 0xffffu);
-            if (staged) {
 #pragma unroll
-                for (int u = 0; u < U; u++)
-                    if (j + u < cnt) pair(lrec[kk[u]].a, lrec[kk[u]].b);
-            } else {
+            for (int u = 0; u < U; u++) kk[u] = s + (j + u < cnt ? kk[u] : 0);
+            FRec r[U];
 #pragma unroll
-                for (int u = 0; u < U; u++) kk[u] = s + (j + u < cnt ? kk[u] : 0);
-                FRec r[U];
+            for (int u = 0; u < U; u++) r[u] = FRec{nbA[kk[u]], nbB[kk[u]]};
 #pragma unroll
-                for (int u = 0; u < U; u++) r[u] = FRec{nbA[kk[u]], nbB[kk[u]]};
-#pragma unroll
-                for (int u = 0; u < U; u++)
-                    if (j + u < cnt) pair(r[u].a, r[u].b);
-            }
+            for (int u = 0; u < U; u++)
+                if (j + u < cnt) pair(r[u].a, r[u].b);
         }
-    } else if (FSTAGE && hd.ok) {
-        // more than NLIST_CAP neighbours: the canonical walk over the staged image
-        int cxp, cyp;
-        cell_xy(xi, yi, sp.eps, cs, cxp, cyp);
-        hood_ranges(hd, lbnd, xi, yi, sp.eps, cs, walk_reach(hi, cs), cyp, g, [&](int b, int e, int shift) {
-            for (int k = b; k < e; k++)
-                if (k + shift != s) pair(lrec[k].a, lrec[k].b);
-        });
     } else {
         walk_neighbours<4>(xi, yi, sp.eps, cs, walk_reach(hi, cs), g, sp.W, sp.H, sp.ox, sp.oy, start,
                            [&](int k, int) { return FRec{nbA[k], nbB[k]}; },
