@@ -567,9 +567,6 @@ __device__ void ref_cap_walk(float xi, float yi, float eps, const GridParams &g,
 static constexpr int HB = 256;            // slots (threads) per staged block (4 waves: hood_stage)
 static constexpr int HCAP = 1536;         // records staged per block (6 per thread)
 static constexpr int HBND = 1280;         // staged cell boundaries per block (5 per thread)
-#ifndef LPE_DEXP
-#define LPE_DEXP 0
-#endif
 
 __device__ __forceinline__ void cell_xy(float x, float y, float eps, float cs, int &cx, int &cy) {
     cx = (int)floorf((x + eps) / cs);
@@ -814,8 +811,7 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     // reference's literal loop (no neighbour list; the forces pass walks the
     // same way)
     const bool slow = live && refInv && ref_cap_slow(xi, yi, eps, g, W, ox, oy, start);
-    if (LPE_DEXP == 1) {
-    } else if (hd.ok) {
+    if (hd.ok) {
         // one span per cell row (hood_spans), the non-empty ones first; four
         // candidates per trip, trip counts wave-uniform: unmasked trips up to
         // the wave's shortest span, masked ones up to its longest.  LDS reads
@@ -903,9 +899,10 @@ struct SphStepParams {
 // slot, so the neighbour list's LDS indices address the staged image and the
 // gathers never leave the CU.
 #ifndef LPE_FORCES_MINW
-#define LPE_FORCES_MINW 1
+#define LPE_FORCES_MINW 4
 #endif
 struct FRec { float4 a, b; };        // nbA (x, y, m, -), nbB (vx, vy, rho, p / rho^2)
+static constexpr int PAIR_CAP = 1024;   // coupling pairs shared by a block (k_forces_couple)
 
 __global__ void __launch_bounds__(HB, LPE_FORCES_MINW)
 k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict__ gp,
@@ -923,18 +920,21 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     if (s0 >= s1) return;
     const GridParams g = *gp;
     const float cs = g.cellSize;
+    // every lane stays to the end (the coupling pairs are shared by the
+    // block); lanes past the last slot and ghost slots only join the barriers
     const int s = s0 + threadIdx.x;
-    if (s >= s1) return;
+    bool live = s < s1;
     int out = s;                              // P slot written
-    if (sp.dst) {                             // ghosts are neighbours only
+    if (live && sp.dst) {                     // ghosts are neighbours only
         out = sp.dst[s];
-        if (sp.dst[s + 1] == out) return;
+        if (sp.dst[s + 1] == out) live = false;
     }
-    const float4 meA = nbA[s], meB = nbB[s];
+    const int sl = live ? s : s0;
+    const float4 meA = nbA[sl], meB = nbB[sl];
     const float xi = meA.x, yi = meA.y;
     const float vxi = meB.x, vyi = meB.y;
     const float rhoi = meB.z;
-    const float pi = pr[s];
+    const float pi = pr[sl];
     const float hi = sp.h;
     // all particles carry h = smoothingLength (fluid.cpp:287-292): the pair
     // smoothing length and its kernel coefficients are per-launch constants
@@ -971,12 +971,13 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         sumFx += fx;
         sumFy += fy;
     };
-    const int cnt = ncount[s];
-    if (sp.diag) {
+    const int cnt = live ? ncount[s] : 0;
+    if (sp.diag && live) {
         atomicAdd(&status[ST_NEIGH], cnt);
         if (cnt > NLIST_CAP) atomicAdd(&status[ST_NL_OVERFLOW], 1);
     }
-    if (sp.refInv && ref_cap_slow(xi, yi, sp.eps, g, sp.W, sp.ox, sp.oy, start)) {
+    if (!live) {
+    } else if (sp.refInv && ref_cap_slow(xi, yi, sp.eps, g, sp.W, sp.ox, sp.oy, start)) {
         // reference cell-capacity mode: the reference's literal loop
         // (metal:345-351; nbrID == globalID is skipped)
         ref_cap_walk(xi, yi, sp.eps, g, sp.W, sp.ox, sp.oy, start, S.id, sp.refInv, sp.n, status,
@@ -1008,22 +1009,60 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     }
     CoupleState st;
     st.x = xi; st.y = yi;
-    st.vhx = S.vhx[s]; st.vhy = S.vhy[s];
+    st.vhx = S.vhx[sl]; st.vhy = S.vhy[sl];
     st.ax = sumFx; st.ay = sumFy;
     // velocityVerletFinish (metal:428-441)
     st.vx = st.vhx + sp.hdt * st.ax;
     st.vy = st.vhy + sp.hdt * st.ay;
     st.mass = meA.z; st.rho = rhoi; st.p = pi;
     int k0 = 0, k1 = 0;
-    if (cp.nr > 0) {
+    if (cp.nr > 0 && live) {
         float fbx = fminf(fmaxf(floorf(st.x / cp.bcs) - (float)cp.bx0, 0.f), (float)(cp.bW - 1));
         float fby = fminf(fmaxf(floorf(st.y / cp.bcs) - (float)cp.by0, 0.f), (float)(cp.bH - 1));
         int bin = (int)fby * cp.bW + (int)fbx;
         k0 = rbinStart[bin]; k1 = rbinStart[bin + 1];
         if (sp.diag && k1 > k0) atomicAdd(&status[ST_RIGID_CAND], k1 - k0);
     }
-    // impulse solver: dispatched only if R > 0 (fluid.cpp:910); push-out always
-    couple_both(st, cp, sp.dt, cp.nr > 0, rig, raabb, rbinList, k0, k1, acq, status);
+    // Coupling (impulse solver only if R > 0, fluid.cpp:910; push-out
+    // always).  The (particle, rigid) pairs whose AABB test passes are few
+    // and clustered (particles in and around the rigid pile), so they are
+    // spread over the whole block: each particle's pairs get consecutive
+    // slots (block scan of the hit counts), every thread computes pairs round
+    // robin into LDS, then each particle folds its own pairs in candidate
+    // (ascending rigid) order.  A block with more than PAIR_CAP pairs couples
+    // per thread instead (same arithmetic).
+    const CoupleIn cin = couple_in(st, cp);
+    int nh = 0;
+    for (int k = k0; k < k1; k++) nh += aabb_holds(raabb[rbinList[k]], cin.x, cin.y) ? 1 : 0;
+    int total;
+    const int off = block_excl_scan(nh, &total);       // (HB == TPB)
+    if (total > PAIR_CAP) {
+        if (live) couple_both(st, cp, sp.dt, cp.nr > 0, rig, raabb, rbinList, k0, k1, acq, status);
+    } else {
+        __shared__ int pRig[PAIR_CAP];
+        __shared__ unsigned char pOwn[PAIR_CAP], pFlag[PAIR_CAP];
+        __shared__ PairTerm pTerm[PAIR_CAP];
+        __shared__ CoupleIn lIn[HB];
+        lIn[threadIdx.x] = cin;
+        for (int k = k0, q = off; k < k1; k++) {
+            const int r = rbinList[k];
+            if (aabb_holds(raabb[r], cin.x, cin.y)) { pRig[q] = r; pOwn[q] = (unsigned char)threadIdx.x; q++; }
+        }
+        __syncthreads();
+        for (int q = threadIdx.x; q < total; q += HB) {
+            const int r = pRig[q];
+            PairTerm t;
+            pFlag[q] = (unsigned char)couple_pair(lIn[pOwn[q]], cp, sp.dt, cp.nr > 0, rig[r], r, acq, status, t);
+            pTerm[q] = t;
+        }
+        __syncthreads();
+        if (live) {
+            CoupleAcc a;
+            for (int q = off; q < off + nh; q++) a.fold(pTerm[q], pFlag[q]);
+            couple_finish(st, cp, a);
+        }
+    }
+    if (!live) return;
     P.x[out] = st.x; P.y[out] = st.y;
     P.vx[out] = st.vx; P.vy[out] = st.vy;
     P.vhx[out] = st.vhx; P.vhy[out] = st.vhy;

@@ -146,9 +146,8 @@ __device__ __forceinline__ void impulse_term(const CoupleState &st, const Couple
                                              const lpe_gpu_rigid &rb, int r, float pen, float relx,
                                              float rely, float nx, float ny, float densityF,
                                              float pressureF, unsigned long long *__restrict__ acq,
-                                             int32_t *__restrict__ status, float &tffx,
-                                             float &tffy, bool &had) {
-    had = true;
+                                             int32_t *__restrict__ status, float &tfx_out,
+                                             float &tfy_out) {
     const float py = st.y;
     float rotx = -rb.omega * rely, roty = rb.omega * relx;
     float rvx = rb.vx + rotx, rvy = rb.vy + roty;
@@ -196,8 +195,8 @@ __device__ __forceinline__ void impulse_term(const CoupleState &st, const Couple
     xacc_add(a, tfx, status, ST_XACC_RANGE);
     xacc_add(a + XACC_LIMBS, tfy, status, ST_XACC_RANGE);
     xacc_add(a + 2 * XACC_LIMBS, torque, status, ST_XACC_RANGE);
-    tffx -= tfx * cp.fluidForceScale;
-    tffy -= tfy * cp.fluidForceScale;
+    tfx_out = tfx;
+    tfy_out = tfy;
 }
 
 // The position solver's clamp, move, boundary offset and velocity projection
@@ -231,6 +230,126 @@ __device__ __forceinline__ void position_tail(CoupleState &st, const CoupleParam
     }
 }
 
+// One (particle, rigid) pair of the two coupling solvers, for a rigid whose
+// AABB holds the particle: the terms the particle's accumulators take from
+// it.  Both solvers accumulate in ascending rigid order; a term is stored
+// with its sign so that the fold is an addition (x - y is x + (-y) in IEEE
+// arithmetic, so folding the signed terms is bit-identical to the
+// reference's -= / +=).  flags: PT_COLL the particle is inside (position
+// solver term in ax, ay), PT_IMP the impulse solver ran (fluid force term in
+// fx, fy; rigid accumulators already added).
+struct PairTerm { float ax, ay, fx, fy; };
+static constexpr int PT_COLL = 1, PT_IMP = 2;
+
+// the particle's inputs of the pair computation
+struct CoupleIn {
+    float x, y, vx, vy, mass, densityF, pressureF;
+};
+
+__device__ __forceinline__ int couple_pair(const CoupleIn &in, const CoupleParams &cp, float dt, bool impulse,
+                                           const lpe_gpu_rigid &rb, int r, unsigned long long *__restrict__ acq,
+                                           int32_t *__restrict__ status, PairTerm &t) {
+    const float px = in.x, py = in.y;
+    CoupleState st;                    // the fields impulse_term reads
+    st.x = px; st.y = py; st.vx = in.vx; st.vy = in.vy; st.mass = in.mass;
+    st.vhx = st.vhy = st.ax = st.ay = st.rho = st.p = 0.f;
+    const bool fast = (rb.vx * rb.vx + rb.vy * rb.vy + rb.omega * rb.omega) > cp.maxSafeVelocitySq;
+    const bool doImp = impulse && !fast;
+    int flags = 0;
+    float tfx = 0.f, tfy = 0.f;
+    if (rb.shapeType == 0) {
+        const float rx = px - rb.posX, ry = py - rb.posY;
+        const float dist2 = rx * rx + ry * ry;
+        const float radius = rb.radius;
+        if (!(dist2 < radius * radius)) return 0;
+        const float dist0 = sqrtf(dist2);
+        if (doImp) {
+            float dist = dist0;
+            if (dist < cp.minPenetration) dist = cp.minPenetration;
+            float pen = radius - dist;
+            if (pen < 0.0f) pen = 0.0f;
+            if (!(pen < cp.minPenetration)) {
+                impulse_term(st, cp, dt, rb, r, pen, rx, ry, rx / dist, ry / dist, in.densityF, in.pressureF,
+                             acq, status, tfx, tfy);
+                flags |= PT_IMP;
+            }
+        }
+        float dist = dist0, dx = rx, dy = ry;
+        if (dist < cp.minSafeDistance) { dist = cp.minSafeDistance; dx = 1.0f; dy = 0.0f; }
+        const float pen = (radius - dist) + cp.safetyMargin;
+        const float dirx = dx / dist, diry = dy / dist;
+        t.ax = -(dirx * pen * cp.relaxFactor);                 // acx -= ...
+        t.ay = -(diry * pen * cp.relaxFactor);
+    } else if (rb.shapeType == 1) {
+        if (rb.vertCount < 3 || !pointInPolygon(px, py, rb)) return 0;
+        float cx, cy;
+        closestPointOnPolygon(px, py, rb, cx, cy);
+        const float dx = px - cx, dy = py - cy;
+        const float d0 = sqrtf(dx * dx + dy * dy);
+        if (doImp) {
+            float d = d0;
+            if (d < cp.minPenetration) d = cp.minPenetration;
+            float pen = d;
+            if (pen < 0.0f) pen = 0.0f;
+            if (!(pen < cp.minPenetration)) {
+                impulse_term(st, cp, dt, rb, r, pen, px - rb.posX, py - rb.posY, dx / d, dy / d, in.densityF,
+                             in.pressureF, acq, status, tfx, tfy);
+                flags |= PT_IMP;
+            }
+        }
+        float d = d0, cdx = dx, cdy = dy;
+        if (d < cp.minSafeDistance) { d = cp.minSafeDistance; cdx = 1.0f; cdy = 0.0f; }
+        const float pen = d + cp.safetyMargin;
+        const float dirx = cdx / d, diry = cdy / d;
+        t.ax = dirx * pen * cp.relaxFactor;                    // acx += ...
+        t.ay = diry * pen * cp.relaxFactor;
+    } else {
+        return 0;
+    }
+    t.fx = -(tfx * cp.fluidForceScale);                        // tffx -= tfx * fluidForceScale
+    t.fy = -(tfy * cp.fluidForceScale);
+    return flags | PT_COLL;
+}
+
+// the per-particle accumulators of the two solvers
+struct CoupleAcc {
+    float tffx = 0.f, tffy = 0.f, acx = 0.f, acy = 0.f;
+    bool had = false, hadCollision = false;
+    __device__ __forceinline__ void fold(const PairTerm &t, int flags) {
+        if (!(flags & PT_COLL)) return;
+        if (flags & PT_IMP) { tffx = tffx + t.fx; tffy = tffy + t.fy; had = true; }
+        hadCollision = true;
+        acx = acx + t.ax;
+        acy = acy + t.ay;
+    }
+};
+
+__device__ __forceinline__ CoupleIn couple_in(const CoupleState &st, const CoupleParams &cp) {
+    CoupleIn in;
+    in.x = st.x; in.y = st.y; in.vx = st.vx; in.vy = st.vy; in.mass = st.mass;
+    in.densityF = st.rho > 0.0f ? st.rho : cp.restDensity;
+    in.pressureF = st.p;
+    return in;
+}
+
+// the impulse solver's fluid force on the particle and the position solver's
+// move (metal:900-924, :640-668), after every pair was folded
+__device__ __forceinline__ void couple_finish(CoupleState &st, const CoupleParams &cp, const CoupleAcc &a) {
+    const float oldx = st.x, oldy = st.y;
+    if (a.had) {
+        float tffx = a.tffx, tffy = a.tffy;
+        float fm = f2len(tffx, tffy);
+        if (fm > cp.fluidForceMax) {
+            float sc = cp.fluidForceMax / fm;
+            tffx = tffx * sc; tffy = tffy * sc;
+        }
+        float invMass = (st.mass > 0.0001f) ? 1.0f / st.mass : 1.0f;
+        st.ax += tffx * invMass;
+        st.ay += tffy * invMass;
+    }
+    position_tail(st, cp, oldx, oldy, a.acx, a.acy, a.hadCollision);
+}
+
 // rigidFluidImpulseSolver (metal:679-924) followed by rigidFluidPositionSolver
 // (metal:533-668; always dispatched, fluid.cpp:929-942) for one particle, in
 // one pass over its candidate rigids.  The position solver tests exactly the
@@ -240,72 +359,17 @@ __device__ __forceinline__ void position_tail(CoupleState &st, const CoupleParam
 // once per (particle, rigid) and each solver accumulates in candidate order
 // exactly as the two separate loops.  aabb[r] = (minX, maxX, minY, maxY) of
 // rig[r]: one 16-B load per candidate, the full record only for AABB hits.
+__device__ __forceinline__ bool aabb_holds(const float4 &bb, float px, float py) {
+    return !(px < bb.x || px > bb.y || py < bb.z || py > bb.w);
+}
 __device__ __forceinline__ void couple_both(CoupleState &st, const CoupleParams &cp, float dt, bool impulse,
                                            const lpe_gpu_rigid *__restrict__ rig,
                                            const float4 *__restrict__ aabb,
                                            const int32_t *__restrict__ list, int k0, int k1,
                                            unsigned long long *__restrict__ acq,
                                            int32_t *__restrict__ status) {
-    // impulse solver state (metal:679-924)
-    const float densityF = st.rho > 0.0f ? st.rho : cp.restDensity;
-    const float pressureF = st.p;
-    float tffx = 0.0f, tffy = 0.0f;
-    bool had = false;
-    // position solver state (metal:533-668)
-    const float oldx = st.x, oldy = st.y;
-    float acx = 0.0f, acy = 0.0f;
-    bool hadCollision = false;
-    const float px = st.x, py = st.y;
-    auto body = [&](int r) {
-        const lpe_gpu_rigid &rb = rig[r];
-        const bool fast = (rb.vx * rb.vx + rb.vy * rb.vy + rb.omega * rb.omega) > cp.maxSafeVelocitySq;
-        const bool doImp = impulse && !fast;
-        if (rb.shapeType == 0) {
-            const float rx = px - rb.posX, ry = py - rb.posY;
-            const float dist2 = rx * rx + ry * ry;
-            const float radius = rb.radius;
-            if (!(dist2 < radius * radius)) return;
-            const float dist0 = sqrtf(dist2);
-            if (doImp) {
-                float dist = dist0;
-                if (dist < cp.minPenetration) dist = cp.minPenetration;
-                float pen = radius - dist;
-                if (pen < 0.0f) pen = 0.0f;
-                if (!(pen < cp.minPenetration))
-                    impulse_term(st, cp, dt, rb, r, pen, rx, ry, rx / dist, ry / dist, densityF, pressureF,
-                                 acq, status, tffx, tffy, had);
-            }
-            hadCollision = true;
-            float dist = dist0, dx = rx, dy = ry;
-            if (dist < cp.minSafeDistance) { dist = cp.minSafeDistance; dx = 1.0f; dy = 0.0f; }
-            const float pen = (radius - dist) + cp.safetyMargin;
-            const float dirx = dx / dist, diry = dy / dist;
-            acx -= dirx * pen * cp.relaxFactor;
-            acy -= diry * pen * cp.relaxFactor;
-        } else if (rb.shapeType == 1) {
-            if (rb.vertCount < 3 || !pointInPolygon(px, py, rb)) return;
-            float cx, cy;
-            closestPointOnPolygon(px, py, rb, cx, cy);
-            const float dx = px - cx, dy = py - cy;
-            const float d0 = sqrtf(dx * dx + dy * dy);
-            if (doImp) {
-                float d = d0;
-                if (d < cp.minPenetration) d = cp.minPenetration;
-                float pen = d;
-                if (pen < 0.0f) pen = 0.0f;
-                if (!(pen < cp.minPenetration))
-                    impulse_term(st, cp, dt, rb, r, pen, px - rb.posX, py - rb.posY, dx / d, dy / d, densityF,
-                                 pressureF, acq, status, tffx, tffy, had);
-            }
-            hadCollision = true;
-            float d = d0, cdx = dx, cdy = dy;
-            if (d < cp.minSafeDistance) { d = cp.minSafeDistance; cdx = 1.0f; cdy = 0.0f; }
-            const float pen = d + cp.safetyMargin;
-            const float dirx = cdx / d, diry = cdy / d;
-            acx += dirx * pen * cp.relaxFactor;
-            acy += diry * pen * cp.relaxFactor;
-        }
-    };
+    const CoupleIn in = couple_in(st, cp);
+    CoupleAcc a;
     constexpr int U = 4;
     for (int k = k0; k < k1; k += U) {
         int rr[U];
@@ -316,19 +380,13 @@ __device__ __forceinline__ void couple_both(CoupleState &st, const CoupleParams 
         for (int u = 0; u < U; u++) bb[u] = aabb[rr[u]];
 #pragma unroll
         for (int u = 0; u < U; u++)
-            if (k + u < k1 && !(px < bb[u].x || px > bb[u].y || py < bb[u].z || py > bb[u].w)) body(rr[u]);
+            if (k + u < k1 && aabb_holds(bb[u], in.x, in.y)) {
+                PairTerm t;
+                const int f = couple_pair(in, cp, dt, impulse, rig[rr[u]], rr[u], acq, status, t);
+                a.fold(t, f);
+            }
     }
-    if (had) {
-        float fm = f2len(tffx, tffy);
-        if (fm > cp.fluidForceMax) {
-            float sc = cp.fluidForceMax / fm;
-            tffx = tffx * sc; tffy = tffy * sc;
-        }
-        float invMass = (st.mass > 0.0001f) ? 1.0f / st.mass : 1.0f;
-        st.ax += tffx * invMass;
-        st.ay += tffy * invMass;
-    }
-    position_tail(st, cp, oldx, oldy, acx, acy, hadCollision);
+    couple_finish(st, cp, a);
 }
 
 }  // namespace lpe
