@@ -954,7 +954,13 @@ __device__ __forceinline__ void pgs_row_regs(float4 rn, float4 rr, float imA, fl
 // all rows of a pair (up to RB) are loaded before its sequential updates.
 // The rows of a pair share its two bodies (and their masses): the bodies'
 // state is read from LDS once per pair and kept in registers across its rows.
-static constexpr int RB = 6;
+
+#ifndef LPE_PGS_PF
+#define LPE_PGS_PF 2
+#endif
+#ifndef LPE_POS_PF
+#define LPE_POS_PF 2
+#endif
 __global__ void __launch_bounds__(SOLVE_TPB)
 k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restrict__ cbase,
              const int2 *__restrict__ seg, int segLds, const float4 *__restrict__ rowN,
@@ -981,7 +987,7 @@ k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
     // and the next step's pair differs from the current one unless there is
     // a single colour (then they are read at use).  Rows in canonical order,
     // arithmetic unchanged: bit-identical to the unpipelined sweep.
-    constexpr int PF = 2;
+    constexpr int PF = LPE_PGS_PF;
     struct Pf {
         int2 sg, ab;
         float4 m, n[PF], r[PF];
@@ -1402,7 +1408,7 @@ k_pos_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
     // software-pipelined like k_pgs_colour: the next step's first pair
     // (segment, bodies, masses, its first PF rows) is loaded before the
     // current one is solved; the records are constant during the solve
-    constexpr int PF = 2;
+    constexpr int PF = LPE_POS_PF;
     struct Pf {
         int2 sg;
         int a, b, fl0;

@@ -902,7 +902,14 @@ struct SphStepParams {
 #define LPE_FORCES_MINW 4
 #endif
 struct FRec { float4 a, b; };        // nbA (x, y, m, -), nbB (vx, vy, rho, p / rho^2)
-static constexpr int PAIR_CAP = 1024;   // coupling pairs shared by a block (k_forces_couple)
+static constexpr int PAIR_CAP = 1024;
+#ifdef LPE_FTRACE
+__device__ unsigned long long g_ftrace[4096 * 8];
+__device__ int g_ftrace_on;
+#define FTR(k) do { if (g_ftrace_on && threadIdx.x == 0) g_ftrace[lb * 8 + (k)] = wall_clock64(); } while (0)
+#else
+#define FTR(k) do {} while (0)
+#endif   // coupling pairs shared by a block (k_forces_couple)
 
 __global__ void __launch_bounds__(HB, LPE_FORCES_MINW)
 k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict__ gp,
@@ -911,13 +918,17 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                 const uint4 *__restrict__ nlist, const int32_t *__restrict__ ncount, PState P,
                 const lpe_gpu_rigid *__restrict__ rig, const float4 *__restrict__ raabb,
                 const int32_t *__restrict__ rbinStart, const int32_t *__restrict__ rbinList,
+                const float4 *__restrict__ rbinAabb,
                 unsigned long long *__restrict__ acq,
                 int32_t *__restrict__ status) {
-    const int lb = xcd_block((sp.n + HB - 1) / HB);
-    if (lb < 0) return;                                   // whole block idle
+    // plain block order (blocks go round robin over the XCDs): the costly
+    // blocks, the particles in and around the rigid pile, are one spatial
+    // run that an XCD-contiguous mapping (xcd_block) would put on one XCD
+    const int lb = (int)blockIdx.x;
     const int nn = sp.nptr ? *sp.nptr : sp.n;
     const int s0 = lb * HB, s1 = min(s0 + HB, nn);
     if (s0 >= s1) return;
+    FTR(0);
     const GridParams g = *gp;
     const float cs = g.cellSize;
     // every lane stays to the end (the coupling pairs are shared by the
@@ -1007,6 +1018,12 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                            [&](int k, int) { return FRec{nbA[k], nbB[k]}; },
                            [&](int k, const FRec &o) { if (k != s) pair(o.a, o.b); });
     }
+#ifdef LPE_FTRACE
+    if (g_ftrace_on) {
+        atomicMax(&g_ftrace[lb * 8 + 5], wall_clock64());
+        atomicMax(&g_ftrace[lb * 8 + 6], (unsigned long long)cnt);
+    }
+#endif
     CoupleState st;
     st.x = xi; st.y = yi;
     st.vhx = S.vhx[sl]; st.vhy = S.vhy[sl];
@@ -1022,6 +1039,9 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         int bin = (int)fby * cp.bW + (int)fbx;
         k0 = rbinStart[bin]; k1 = rbinStart[bin + 1];
         if (sp.diag && k1 > k0) atomicAdd(&status[ST_RIGID_CAND], k1 - k0);
+#ifdef LPE_FTRACE
+        if (g_ftrace_on) atomicMax(&g_ftrace[lb * 8 + 7], (unsigned long long)(k1 - k0));
+#endif
     }
     // Coupling (impulse solver only if R > 0, fluid.cpp:910; push-out
     // always).  The (particle, rigid) pairs whose AABB test passes are few
@@ -1031,31 +1051,53 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     // robin into LDS, then each particle folds its own pairs in candidate
     // (ascending rigid) order.  A block with more than PAIR_CAP pairs couples
     // per thread instead (same arithmetic).
-    const CoupleIn cin = couple_in(st, cp);
+    // AABB hits among the bin's candidates (bin-ordered AABBs, 8 loads in
+    // flight); the first 64 candidates' hits kept as a mask
     int nh = 0;
-    for (int k = k0; k < k1; k++) nh += aabb_holds(raabb[rbinList[k]], cin.x, cin.y) ? 1 : 0;
+    unsigned long long hitm = 0ull;
+    for (int k = k0; k < k1; k += 8) {
+        float4 bb[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) bb[u] = rbinAabb[min(k + u, k1 - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+            if (k + u < k1 && aabb_holds(bb[u], st.x, st.y)) {
+                nh++;
+                if (k + u - k0 < 64) hitm |= 1ull << (k + u - k0);
+            }
+    }
+    const CoupleIn cin = couple_in(st, cp, cp.nr > 0 && nh > 0);
+    const float4 *rc = raabb + cp.nr;                 // the compact records (k_rig_couple)
     int total;
     const int off = block_excl_scan(nh, &total);       // (HB == TPB)
+    FTR(1);
+#ifdef LPE_FTRACE
+    if (g_ftrace_on && threadIdx.x == 0) g_ftrace[lb * 8 + 4] = total;
+#endif
     if (total > PAIR_CAP) {
-        if (live) couple_both(st, cp, sp.dt, cp.nr > 0, rig, raabb, rbinList, k0, k1, acq, status);
+        if (live) couple_both(st, cp, sp.dt, cp.nr > 0, rc, rbinAabb, rbinList, k0, k1, acq, status);
     } else {
         __shared__ int pRig[PAIR_CAP];
         __shared__ unsigned char pOwn[PAIR_CAP], pFlag[PAIR_CAP];
         __shared__ PairTerm pTerm[PAIR_CAP];
         __shared__ CoupleIn lIn[HB];
         lIn[threadIdx.x] = cin;
-        for (int k = k0, q = off; k < k1; k++) {
-            const int r = rbinList[k];
-            if (aabb_holds(raabb[r], cin.x, cin.y)) { pRig[q] = r; pOwn[q] = (unsigned char)threadIdx.x; q++; }
+        int q = off;
+        for (unsigned long long m = hitm; m; m &= m - 1ull, q++) {
+            pRig[q] = rbinList[k0 + __ffsll((long long)m) - 1];
+            pOwn[q] = (unsigned char)threadIdx.x;
         }
+        for (int k = k0 + 64; k < k1; k++)                 // (a bin of more than 64 candidates)
+            if (aabb_holds(rbinAabb[k], cin.x, cin.y)) { pRig[q] = rbinList[k]; pOwn[q] = (unsigned char)threadIdx.x; q++; }
         __syncthreads();
         for (int q = threadIdx.x; q < total; q += HB) {
             const int r = pRig[q];
             PairTerm t;
-            pFlag[q] = (unsigned char)couple_pair(lIn[pOwn[q]], cp, sp.dt, cp.nr > 0, rig[r], r, acq, status, t);
+            pFlag[q] = (unsigned char)couple_pair(lIn[pOwn[q]], cp, sp.dt, cp.nr > 0, rc, r, acq, status, t);
             pTerm[q] = t;
         }
         __syncthreads();
+        FTR(2);
         if (live) {
             CoupleAcc a;
             for (int q = off; q < off + nh; q++) a.fold(pTerm[q], pFlag[q]);
@@ -1069,7 +1111,18 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     P.ax[out] = st.ax; P.ay[out] = st.ay;
     P.m[out] = st.mass; P.id[out] = S.id[s];
     if (sp.orho) { sp.orho[out] = rhoi; sp.opr[out] = pi; }
+#ifdef LPE_FTRACE
+    if (g_ftrace_on) atomicMax(&g_ftrace[lb * 8 + 3], wall_clock64());
+#endif
 }
+#ifdef LPE_FTRACE
+extern "C" int lpe_ftrace(int on, unsigned long long *host, int n) {
+    if (host) (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ftrace), sizeof(unsigned long long) * n);
+    unsigned long long z[4096 * 8] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_ftrace), z, sizeof(z));
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_ftrace_on), &on, sizeof(int)) == hipSuccess ? 0 : 1;
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // x-slab decomposition.  A rank owns the particles of the
@@ -1258,10 +1311,22 @@ __device__ __forceinline__ int bin_of(float v, float bcs, int b0, int nb) {
     return (int)t;
 }
 // compact AABBs of the coupling rigids: (minX, maxX, minY, maxY)
-__global__ void k_rig_aabb(int nr, const lpe_gpu_rigid *__restrict__ rig, float4 *__restrict__ aabb) {
+// and their compact coupling records (sph_coupling.h RigC), nr after them
+__global__ void k_rig_couple(int nr, const lpe_gpu_rigid *__restrict__ rig, float maxSafeVelocitySq,
+                             float4 *__restrict__ aabb) {
     int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nr) return;
-    aabb[r] = make_float4(rig[r].minX, rig[r].maxX, rig[r].minY, rig[r].maxY);
+    const lpe_gpu_rigid &b = rig[r];
+    aabb[r] = make_float4(b.minX, b.maxX, b.minY, b.maxY);
+    float4 *q = aabb + nr + (size_t)r * RIGC_F4;
+    const bool fast = (b.vx * b.vx + b.vy * b.vy + b.omega * b.omega) > maxSafeVelocitySq;
+    const int nv = min(max(b.vertCount, 0), LPE_MAX_POLY_VERTS);
+    const int fl = (b.shapeType & 0xff) | ((b.shapeType == 1 ? nv : 0) << 8) | ((fast ? 1 : 0) << 16);
+    q[0] = make_float4(b.posX, b.posY, b.radius, __int_as_float(b.shapeType == 0 || b.shapeType == 1 ? fl : 0xff));
+    q[1] = make_float4(b.vx, b.vy, b.omega, b.mass);
+    q[2] = make_float4(b.inertia, 0.f, 0.f, 0.f);
+    for (int k = 0; k < LPE_MAX_POLY_VERTS / 2; k++)
+        q[3 + k] = make_float4(b.vertsX[2 * k], b.vertsY[2 * k], b.vertsX[2 * k + 1], b.vertsY[2 * k + 1]);
 }
 
 // one wave per rigid, lanes stride over the bins its AABB covers (a wall
@@ -1293,8 +1358,11 @@ __global__ void k_rbin_fill(int nr, const lpe_gpu_rigid *__restrict__ rig, float
         else atomicOr(&status[ST_LIST_OVERFLOW], 1);
     }
 }
-// insertion sort of each bin's list -> ascending rigid index
-__global__ void k_rbin_sort(int B, int32_t *__restrict__ start, int32_t *__restrict__ list, int cap) {
+// insertion sort of each bin's list -> ascending rigid index; then the
+// entries' AABBs in list order (the coupling's candidate walk reads them
+// contiguously instead of through the index)
+__global__ void k_rbin_sort(int B, int32_t *__restrict__ start, int32_t *__restrict__ list, int cap,
+                            const float4 *__restrict__ aabb, float4 *__restrict__ baabb) {
     int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     int s = min(start[b], cap), e = min(start[b + 1], cap);
@@ -1304,6 +1372,7 @@ __global__ void k_rbin_sort(int B, int32_t *__restrict__ start, int32_t *__restr
         while (j >= s && list[j] > v) { list[j + 1] = list[j]; j--; }
         list[j + 1] = v;
     }
+    for (int k = s; k < e; k++) baabb[k] = aabb[list[k]];
 }
 
 // writeBackRigidBodies arithmetic (fluid.cpp:545-562), once per tick: the
@@ -1374,6 +1443,12 @@ using namespace lpe;
 // ===========================================================================
 // host side
 static inline int nblk(long n, int t = TPB) { return (int)((n + t - 1) / t); }
+// the rigid bin list buffer: cap ints, then cap float4 AABBs (16-B aligned)
+static inline size_t rbin_list_pad(int cap) { return ((sizeof(int32_t) * (size_t)cap + 15) / 16) * 16; }
+static inline size_t rbin_bytes(int cap) { return rbin_list_pad(cap) + sizeof(float4) * (size_t)cap; }
+static inline float4 *rbin_aabb(const SphDev &d) {
+    return d.rbinList ? (float4 *)((char *)d.rbinList + rbin_list_pad(d.cap_rlist)) : nullptr;
+}
 static inline int nblk1(long n, int t = TPB) { return std::max(1, nblk(n, t)); }   // never an empty grid
 
 // the id -> slot map of the reference cell-capacity mode, or null (mode off)
@@ -1827,10 +1902,11 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
     hipStream_t s = ctx->stream;
     if (d.nr > d.cap_raabb || !d.raabb) {
         if (d.raabb) (void)hipFree(d.raabb);
-        LPE_HIP(ctx, hipMalloc((void **)&d.raabb, sizeof(float4) * (size_t)d.nr));
+        LPE_HIP(ctx, hipMalloc((void **)&d.raabb, sizeof(float4) * (size_t)d.nr * (1 + RIGC_F4)));
         d.cap_raabb = d.nr;
     }
-    LPE_KERNEL(ctx, "k_rig_aabb", k_rig_aabb, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig, d.raabb);
+    LPE_KERNEL(ctx, "k_rig_couple", k_rig_couple, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig,
+               d.cfg.impulseSolver.maxSafeVelocitySq, d.raabb);
     LPE_HIP(ctx, hipMemsetAsync(d.rbinCount, 0, sizeof(int32_t) * B, s));
     LPE_KERNEL(ctx, "k_rbin_count", k_rbin_count, dim3(nblk(d.nr, 4)), dim3(256), 0, s, d.nr, d.rig, d.bcs,
                        d.bx0, d.by0, d.bW, d.bH, d.rbinCount);
@@ -1845,13 +1921,15 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
     }
     if (total > d.cap_rlist || !d.rbinList) {
         if (d.rbinList) (void)hipFree(d.rbinList);
-        LPE_HIP(ctx, hipMalloc((void **)&d.rbinList, sizeof(int32_t) * std::max(total, 1)));
+        // the list, then its entries' AABBs (float4, bin order: rbin_aabb)
+        LPE_HIP(ctx, hipMalloc((void **)&d.rbinList, rbin_bytes(std::max(total, 1))));
         d.cap_rlist = std::max(total, 1);
     }
     d.rlist_len = total;
     LPE_KERNEL(ctx, "k_rbin_fill", k_rbin_fill, dim3(nblk(d.nr, 4)), dim3(256), 0, s, d.nr, d.rig, d.bcs,
                        d.bx0, d.by0, d.bW, d.bH, cursor, d.rbinList, d.cap_rlist, d.status);
-    LPE_KERNEL(ctx, "k_rbin_sort", k_rbin_sort, dim3(nblk(B, 128)), dim3(128), 0, s, B, d.rbinStart, d.rbinList, d.cap_rlist);
+    LPE_KERNEL(ctx, "k_rbin_sort", k_rbin_sort, dim3(nblk(B, 128)), dim3(128), 0, s, B, d.rbinStart, d.rbinList, d.cap_rlist,
+               d.raabb, rbin_aabb(d));
     LPE_CHECK_LAUNCH(ctx, "rbin");
     d.rig_dirty = false;
     return LPE_OK;
@@ -2136,9 +2214,10 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int after, int (*hook)(lpe_ctx
             st = sph_density(ctx, d.n, nullptr, d.rho, d.pr);
         }
         if (st) return st;
-        LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(xcd_grid(nblk(sp.n, HB))), dim3(HB), 0, s, sp, cp,
+        LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(nblk1(sp.n, HB)), dim3(HB), 0, s, sp, cp,
                            (step == 0 && pre) ? d.gp + 1 : d.gp,
                            d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart, d.rbinList,
+                           rbin_aabb(d),
                            d.acq, d.status);
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
         if (hook && (step == after || (step + 1 == c.numSubSteps && after >= step))) {

@@ -50,6 +50,79 @@ __device__ __forceinline__ void closestPointOnPolygon(float px, float py, const 
 
 __device__ __forceinline__ float f2len(float x, float y) { return sqrtf(x * x + y * y); }
 
+// The coupling's view of a rigid, rebuilt once per tick (k_rig_couple):
+// 16-B aligned, so a (particle, rigid) pair loads everything it may need in
+// one round of wide loads instead of a chain of scalar field loads.
+//   h = (posX, posY, radius, flags: shapeType | vertCount << 8 | fast << 16)
+//   v = (vx, vy, omega, mass), w = (inertia, -, -, -)
+//   vt[k] = (x_2k, y_2k, x_2k+1, y_2k+1): the polygon, interleaved
+// fast = the impulse solver's velocity test (metal:705-709), same arithmetic.
+static constexpr int RIGC_F4 = 3 + LPE_MAX_POLY_VERTS / 2;   // float4s per record
+struct RigC {
+    float px, py, radius;
+    int shape, nv;
+    bool fast;
+    float vx, vy, omega, mass, inertia;
+};
+
+// the compact record of rigid r (k_rig_couple); the polygon stays in the
+// record (vert(i) reads it, L1-resident)
+__device__ __forceinline__ const float4 *rigc_load(const float4 *__restrict__ rc, int r, RigC &b) {
+    const float4 *q = rc + (size_t)r * RIGC_F4;
+    const float4 h = q[0], v = q[1], w = q[2];
+    const int fl = __float_as_int(h.w);
+    b.px = h.x; b.py = h.y; b.radius = h.z;
+    b.shape = fl & 0xff; b.nv = (fl >> 8) & 0xff; b.fast = (fl >> 16) & 1;
+    b.vx = v.x; b.vy = v.y; b.omega = v.z; b.mass = v.w; b.inertia = w.x;
+    return q + 3;
+}
+__device__ __forceinline__ float2 rigc_vert(const float4 *__restrict__ vt, int i) {
+    const float4 p = vt[i >> 1];
+    return (i & 1) ? make_float2(p.z, p.w) : make_float2(p.x, p.y);
+}
+
+// pointInPolygon / closestPointOnPolygon (above) on the compact record's
+// vertices (n <= LPE_MAX_POLY_VERTS), each edge's vertices loaded once.  The
+// parity test's toggles commute; the closest-point scan keeps the original
+// edge order (first minimum wins).
+__device__ __forceinline__ bool pip_rec(float px, float py, int n, const float4 *__restrict__ vt) {
+    if (n < 3) return false;
+    bool inside = false;
+    float2 pj = rigc_vert(vt, n - 1);
+    for (int i = 0; i < n; i++) {
+        const float2 pi = rigc_vert(vt, i);
+        const float xi = pi.x, yi = pi.y, xj = pj.x, yj = pj.y;
+        const bool intersect = ((yi > py) != (yj > py)) && (px < (xj - xi) * (py - yi) / (yj - yi) + xi);
+        if (intersect) inside = !inside;
+        pj = pi;
+    }
+    return inside;
+}
+__device__ __forceinline__ void closest_rec(float px, float py, int n, const float4 *__restrict__ vt,
+                                            float &ox, float &oy) {
+    ox = px; oy = py;
+    if (n < 2) return;
+    float minDistSq = 1e12f;
+    const float2 p0 = rigc_vert(vt, 0);
+    float2 p1 = p0;
+    for (int i = 0; i < n; i++) {
+        const float2 p2 = i + 1 < n ? rigc_vert(vt, i + 1) : p0;
+        float x1 = p1.x, y1 = p1.y, x2 = p2.x, y2 = p2.y;
+        p1 = p2;
+        float ex = x2 - x1, ey = y2 - y1;
+        float eLenSq = ex * ex + ey * ey;
+        if (eLenSq < 1e-16f) continue;
+        float dx = px - x1, dy = py - y1;
+        float t = (dx * ex + dy * ey) / eLenSq;
+        if (t < 0.f) t = 0.f;
+        if (t > 1.f) t = 1.f;
+        float cx = x1 + t * ex, cy = y1 + t * ey;
+        float cdx = px - cx, cdy = py - cy;
+        float distSq = cdx * cdx + cdy * cdy;
+        if (distSq < minDistSq) { minDistSq = distSq; ox = cx; oy = cy; }
+    }
+}
+
 // tanh / pow of the impulse solver (metal:810, :822): fp64 rounded once to
 // fp32, the same definition as oracle/sph_oracle.c.
 __device__ __forceinline__ float lpe_tanhf(float x) { return (float)tanh((double)x); }
@@ -141,9 +214,10 @@ __host__ __device__ __forceinline__ float xacc_round(const unsigned long long *a
 }
 
 // One rigid's contribution to the impulse solver (metal:792-900), given the
-// penetration, lever arm and normal of the particle inside it.
+// penetration, lever arm and normal of the particle inside it;
+// effectiveArea = pow(m / densityF, 2/3), a per-particle value (couple_in).
 __device__ __forceinline__ void impulse_term(const CoupleState &st, const CoupleParams &cp, float dt,
-                                             const lpe_gpu_rigid &rb, int r, float pen, float relx,
+                                             const RigC &rb, float effectiveArea, int r, float pen, float relx,
                                              float rely, float nx, float ny, float densityF,
                                              float pressureF, unsigned long long *__restrict__ acq,
                                              int32_t *__restrict__ status, float &tfx_out,
@@ -156,8 +230,6 @@ __device__ __forceinline__ void impulse_term(const CoupleState &st, const Couple
     float normalVel = relVx * nx + relVy * ny;
     float nvx = nx * normalVel, nvy = ny * normalVel;
     float tvx = relVx - nvx, tvy = relVy - nvy;
-    float particleVolume = st.mass / densityF;
-    float effectiveArea = lpe_powf(particleVolume, 2.0f / 3.0f);
     float depth = fminf(py / cp.depthEstimateScale, 1.0f);
     float hydro = densityF * cp.gravity * depth;
     float totalPressure = pressureF + hydro;
@@ -243,22 +315,24 @@ static constexpr int PT_COLL = 1, PT_IMP = 2;
 
 // the particle's inputs of the pair computation
 struct CoupleIn {
-    float x, y, vx, vy, mass, densityF, pressureF;
+    float x, y, vx, vy, mass, densityF, pressureF, effArea;
 };
 
 __device__ __forceinline__ int couple_pair(const CoupleIn &in, const CoupleParams &cp, float dt, bool impulse,
-                                           const lpe_gpu_rigid &rb, int r, unsigned long long *__restrict__ acq,
-                                           int32_t *__restrict__ status, PairTerm &t) {
+                                           const float4 *__restrict__ rc, int r,
+                                           unsigned long long *__restrict__ acq, int32_t *__restrict__ status,
+                                           PairTerm &t) {
+    RigC rb;
+    const float4 *vt = rigc_load(rc, r, rb);
     const float px = in.x, py = in.y;
     CoupleState st;                    // the fields impulse_term reads
     st.x = px; st.y = py; st.vx = in.vx; st.vy = in.vy; st.mass = in.mass;
     st.vhx = st.vhy = st.ax = st.ay = st.rho = st.p = 0.f;
-    const bool fast = (rb.vx * rb.vx + rb.vy * rb.vy + rb.omega * rb.omega) > cp.maxSafeVelocitySq;
-    const bool doImp = impulse && !fast;
+    const bool doImp = impulse && !rb.fast;
     int flags = 0;
     float tfx = 0.f, tfy = 0.f;
-    if (rb.shapeType == 0) {
-        const float rx = px - rb.posX, ry = py - rb.posY;
+    if (rb.shape == 0) {
+        const float rx = px - rb.px, ry = py - rb.py;
         const float dist2 = rx * rx + ry * ry;
         const float radius = rb.radius;
         if (!(dist2 < radius * radius)) return 0;
@@ -269,8 +343,8 @@ __device__ __forceinline__ int couple_pair(const CoupleIn &in, const CoupleParam
             float pen = radius - dist;
             if (pen < 0.0f) pen = 0.0f;
             if (!(pen < cp.minPenetration)) {
-                impulse_term(st, cp, dt, rb, r, pen, rx, ry, rx / dist, ry / dist, in.densityF, in.pressureF,
-                             acq, status, tfx, tfy);
+                impulse_term(st, cp, dt, rb, in.effArea, r, pen, rx, ry, rx / dist, ry / dist, in.densityF,
+                             in.pressureF, acq, status, tfx, tfy);
                 flags |= PT_IMP;
             }
         }
@@ -280,10 +354,10 @@ __device__ __forceinline__ int couple_pair(const CoupleIn &in, const CoupleParam
         const float dirx = dx / dist, diry = dy / dist;
         t.ax = -(dirx * pen * cp.relaxFactor);                 // acx -= ...
         t.ay = -(diry * pen * cp.relaxFactor);
-    } else if (rb.shapeType == 1) {
-        if (rb.vertCount < 3 || !pointInPolygon(px, py, rb)) return 0;
+    } else if (rb.shape == 1) {
+        if (rb.nv < 3 || !pip_rec(px, py, rb.nv, vt)) return 0;
         float cx, cy;
-        closestPointOnPolygon(px, py, rb, cx, cy);
+        closest_rec(px, py, rb.nv, vt, cx, cy);
         const float dx = px - cx, dy = py - cy;
         const float d0 = sqrtf(dx * dx + dy * dy);
         if (doImp) {
@@ -292,8 +366,8 @@ __device__ __forceinline__ int couple_pair(const CoupleIn &in, const CoupleParam
             float pen = d;
             if (pen < 0.0f) pen = 0.0f;
             if (!(pen < cp.minPenetration)) {
-                impulse_term(st, cp, dt, rb, r, pen, px - rb.posX, py - rb.posY, dx / d, dy / d, in.densityF,
-                             in.pressureF, acq, status, tfx, tfy);
+                impulse_term(st, cp, dt, rb, in.effArea, r, pen, px - rb.px, py - rb.py, dx / d, dy / d,
+                             in.densityF, in.pressureF, acq, status, tfx, tfy);
                 flags |= PT_IMP;
             }
         }
@@ -324,11 +398,13 @@ struct CoupleAcc {
     }
 };
 
-__device__ __forceinline__ CoupleIn couple_in(const CoupleState &st, const CoupleParams &cp) {
+// area: the particle has impulse-solver candidates (pow only then)
+__device__ __forceinline__ CoupleIn couple_in(const CoupleState &st, const CoupleParams &cp, bool area) {
     CoupleIn in;
     in.x = st.x; in.y = st.y; in.vx = st.vx; in.vy = st.vy; in.mass = st.mass;
     in.densityF = st.rho > 0.0f ? st.rho : cp.restDensity;
     in.pressureF = st.p;
+    in.effArea = area ? lpe_powf(st.mass / in.densityF, 2.0f / 3.0f) : 0.f;   // metal:818-822
     return in;
 }
 
@@ -357,18 +433,18 @@ __device__ __forceinline__ void couple_finish(CoupleState &st, const CoupleParam
 // fast rigids), at the same position (the impulse solver only changes the
 // acceleration), so the containment and closest-point geometry is computed
 // once per (particle, rigid) and each solver accumulates in candidate order
-// exactly as the two separate loops.  aabb[r] = (minX, maxX, minY, maxY) of
-// rig[r]: one 16-B load per candidate, the full record only for AABB hits.
+// exactly as the two separate loops.  aabb[k] = (minX, maxX, minY, maxY) of
+// candidate list[k] (bin order): one 16-B load per candidate, the compact
+// record only for AABB hits.
 __device__ __forceinline__ bool aabb_holds(const float4 &bb, float px, float py) {
     return !(px < bb.x || px > bb.y || py < bb.z || py > bb.w);
 }
 __device__ __forceinline__ void couple_both(CoupleState &st, const CoupleParams &cp, float dt, bool impulse,
-                                           const lpe_gpu_rigid *__restrict__ rig,
-                                           const float4 *__restrict__ aabb,
+                                           const float4 *__restrict__ rc, const float4 *__restrict__ aabb,
                                            const int32_t *__restrict__ list, int k0, int k1,
                                            unsigned long long *__restrict__ acq,
                                            int32_t *__restrict__ status) {
-    const CoupleIn in = couple_in(st, cp);
+    const CoupleIn in = couple_in(st, cp, impulse && k1 > k0);
     CoupleAcc a;
     constexpr int U = 4;
     for (int k = k0; k < k1; k += U) {
@@ -377,12 +453,12 @@ __device__ __forceinline__ void couple_both(CoupleState &st, const CoupleParams 
 #pragma unroll
         for (int u = 0; u < U; u++) rr[u] = list[min(k + u, k1 - 1)];
 #pragma unroll
-        for (int u = 0; u < U; u++) bb[u] = aabb[rr[u]];
+        for (int u = 0; u < U; u++) bb[u] = aabb[min(k + u, k1 - 1)];   // bin-ordered AABBs
 #pragma unroll
         for (int u = 0; u < U; u++)
             if (k + u < k1 && aabb_holds(bb[u], in.x, in.y)) {
                 PairTerm t;
-                const int f = couple_pair(in, cp, dt, impulse, rig[rr[u]], rr[u], acq, status, t);
+                const int f = couple_pair(in, cp, dt, impulse, rc, rr[u], acq, status, t);
                 a.fold(t, f);
             }
     }
