@@ -313,23 +313,36 @@ __global__ void k_rb_prep(int nb, const lpe_body *__restrict__ bodies, const dou
     cand[i] = ok ? 1 : 0;
 }
 
-// each body's pair list sorted by partner rank; short lists by one thread
-// (insertion sort), lists longer than BP_SHORT by k_bp_sort_long
-static constexpr int BP_SHORT = 32;
+// each body's pair list sorted by partner rank (the ranks in a list are
+// distinct): lists of up to BP_SHORT entries by one wave each, in registers
+// (an entry's place is the number of smaller keys), longer ones by
+// k_bp_sort_long
+static constexpr int BP_SHORT = 64;
 static constexpr int BP_LONG = 4096;       // longest list sorted in LDS (longer: one thread)
-__global__ void k_bp_sort(int nb, const int32_t *__restrict__ pstart, int2 *__restrict__ pairs,
-                          int32_t *__restrict__ rk, int cap_pairs) {
-    int r = blockIdx.x * RTPB + threadIdx.x;
-    if (r >= nb) return;
-    int s = pstart[r], e = min(pstart[r + 1], cap_pairs);
-    if (e - s > BP_SHORT && e - s <= BP_LONG) return;
-    for (int k = s + 1; k < e; k++) {
-        int v = rk[k];
-        int2 p = pairs[k];
-        int j = k - 1;
-        while (j >= s && rk[j] > v) { rk[j + 1] = rk[j]; pairs[j + 1] = pairs[j]; j--; }
-        rk[j + 1] = v; pairs[j + 1] = p;
+__global__ void __launch_bounds__(RTPB)
+k_bp_sort(int nb, const int32_t *__restrict__ pstart, int2 *__restrict__ pairs,
+          int32_t *__restrict__ rk, int cap_pairs) {
+    const int r = blockIdx.x * (RTPB / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= nb) return;                                     // (whole wave)
+    const int s = pstart[r], e = min(pstart[r + 1], cap_pairs), n = e - s;
+    if (n <= 1 || (n > BP_SHORT && n <= BP_LONG)) return;
+    if (n > BP_LONG) {                                       // (never expected) one lane, in place
+        if (lane == 0)
+            for (int k = s + 1; k < e; k++) {
+                int v = rk[k];
+                int2 p = pairs[k];
+                int j = k - 1;
+                while (j >= s && rk[j] > v) { rk[j + 1] = rk[j]; pairs[j + 1] = pairs[j]; j--; }
+                rk[j + 1] = v; pairs[j + 1] = p;
+            }
+        return;
     }
+    const int key = lane < n ? rk[s + lane] : 0x7fffffff;
+    const int2 val = lane < n ? pairs[s + lane] : make_int2(0, 0);
+    int rank = 0;
+    for (int j = 0; j < n; j++) rank += __shfl(key, j) < key ? 1 : 0;
+    if (lane < n) { rk[s + rank] = key; pairs[s + rank] = val; }
 }
 
 // one block per body; a list of BP_SHORT < n <= BP_LONG entries (the walls'
@@ -415,17 +428,24 @@ __global__ void k_bg_fill(int nb, const int32_t *__restrict__ key, int32_t *__re
     if (k >= 0) list[atomicAdd(&cursor[k], 1)] = r;
 }
 
-// mode 0 counts (pcount of the lower rank), 1 fills (cursor from pstart)
-__global__ void k_bg_pairs(int nb, int mode, const int32_t *__restrict__ byRank,
-                           const lpe_body *__restrict__ bodies, const double4 *__restrict__ aabb,
-                           double small, int G, const int32_t *__restrict__ key,
-                           const int32_t *__restrict__ cellStart, const int32_t *__restrict__ list,
-                           const int32_t *__restrict__ special, const int32_t *__restrict__ nspecial,
-                           int32_t *__restrict__ pcount, int32_t *__restrict__ pcursor,
-                           int2 *__restrict__ pairs, int32_t *__restrict__ pairRankB, int cap_pairs,
-                           int32_t *__restrict__ status) {
-    int r = blockIdx.x * RTPB + threadIdx.x;
-    if (r >= nb) return;
+// mode 0 counts (pcount of the lower rank), 1 fills (cursor from pstart).
+// One wave per body rank: the lanes take the candidates of its (up to 3x3)
+// cells as one flat index space, then the special bodies, so a body's tests
+// run in parallel instead of as a chain of dependent loads.  The emission
+// order is free (each body's list is sorted by partner rank afterwards).
+static constexpr int BG_WAVES = RTPB / 64;                 // bodies per block
+__global__ void __launch_bounds__(RTPB)
+k_bg_pairs(int nb, int mode, const int32_t *__restrict__ byRank,
+           const lpe_body *__restrict__ bodies, const double4 *__restrict__ aabb,
+           double small, int G, const int32_t *__restrict__ key,
+           const int32_t *__restrict__ cellStart, const int32_t *__restrict__ list,
+           const int32_t *__restrict__ special, const int32_t *__restrict__ nspecial,
+           int32_t *__restrict__ pcount, int32_t *__restrict__ pcursor,
+           int2 *__restrict__ pairs, int32_t *__restrict__ pairRankB, int cap_pairs,
+           int32_t *__restrict__ status) {
+    const int r = blockIdx.x * BG_WAVES + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (r >= nb) return;                                     // (whole wave)
     const int k = key[r];
     if (k == -1) return;
     const int ia = byRank[r];
@@ -450,20 +470,34 @@ __global__ void k_bg_pairs(int nb, int mode, const int32_t *__restrict__ byRank,
     const int ns = *nspecial;
     if (k >= 0) {
         const int cx = k % G, cy = k / G;
-        for (int y = max(cy - 1, 0); y <= min(cy + 1, G - 1); y++)
-            for (int x = max(cx - 1, 0); x <= min(cx + 1, G - 1); x++) {
+        int cs[9], pre[10];                                  // cell starts, flat prefix
+        pre[0] = 0;
+#pragma unroll
+        for (int i = 0; i < 9; i++) {
+            const int x = cx - 1 + i % 3, y = cy - 1 + i / 3;
+            int b0 = 0, n = 0;
+            if (x >= 0 && x < G && y >= 0 && y < G) {
                 const int c = y * G + x;
-                for (int j = cellStart[c]; j < cellStart[c + 1]; j++) {
-                    const int rb = list[j];
-                    if (rb > r && test(rb)) emit(r, rb);
-                }
+                b0 = cellStart[c];
+                n = cellStart[c + 1] - b0;
             }
-        for (int j = 0; j < ns; j++) {                       // regular - special pairs
+            cs[i] = b0;
+            pre[i + 1] = pre[i] + n;
+        }
+        for (int t = lane; t < pre[9]; t += 64) {
+            int j = 0;
+#pragma unroll
+            for (int i = 0; i < 9; i++)
+                if (t >= pre[i] && t < pre[i + 1]) j = cs[i] + (t - pre[i]);
+            const int rb = list[j];
+            if (rb > r && test(rb)) emit(r, rb);
+        }
+        for (int j = lane; j < ns; j += 64) {                // regular - special pairs
             const int rb = special[j];
             if (test(rb)) emit(min(r, rb), max(r, rb));
         }
     } else {
-        for (int j = 0; j < ns; j++) {                       // special - special pairs
+        for (int j = lane; j < ns; j += 64) {                // special - special pairs
             const int rb = special[j];
             if (rb > r && test(rb)) emit(r, rb);
         }
@@ -961,6 +995,27 @@ __device__ __forceinline__ void pgs_row_regs(float4 rn, float4 rr, float imA, fl
 #ifndef LPE_POS_PF
 #define LPE_POS_PF 2
 #endif
+// A colour step's barrier: the step's LDS writes (velocities / poses) are
+// visible to every wave after it; outstanding global loads (the next step's
+// prefetch) stay in flight across it (__syncthreads() would drain them).
+// Global data written inside the sweeps (the PGS multipliers) is re-read only
+// by the thread that wrote it (static pair -> thread map).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+#ifdef LPE_PTRACE
+__device__ unsigned long long g_ptrace[2][2048];
+extern "C" int lpe_ptrace(unsigned long long *host) {
+    if (host) (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ptrace), sizeof(unsigned long long) * 2 * 2048);
+    return 0;
+}
+#define PTR(w, k) do { if (threadIdx.x == 0 && (k) < 2048) g_ptrace[w][k] = wall_clock64(); } while (0)
+#else
+#define PTR(w, k) do {} while (0)
+#endif
 __global__ void __launch_bounds__(SOLVE_TPB)
 k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restrict__ cbase,
              const int2 *__restrict__ seg, int segLds, const float4 *__restrict__ rowN,
@@ -1036,6 +1091,10 @@ k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
     };
     const int total = iters * ncol;
     const bool lamPf = ncol > 1;
+    PTR(0, 0);
+#ifdef LPE_PTRACE
+    if (threadIdx.x <= ncol) g_ptrace[1][1024 + threadIdx.x] = scb[threadIdx.x];
+#endif
     Pf cur{}, nxt{};
     bool hcur = false;
     if (total > 0) {
@@ -1058,7 +1117,8 @@ k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
             load(q, it, true, f);
             solve(f, it, true);
         }
-        __syncthreads();
+        lds_barrier();
+        PTR(0, step + 1);
         cur = nxt;
         hcur = hnxt;
         it = it1;
@@ -1451,6 +1511,7 @@ k_pos_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
         if (f.invMB != 0.0 || (f.fl0 & 4)) { sp[3 * b] = xB; sp[3 * b + 1] = yB; sp[3 * b + 2] = tB; }
     };
     const int total = iters * ncol;
+    PTR(1, 0);
     Pf cur{}, nxt{};
     bool hcur = false;
     if (total > 0) {
@@ -1472,7 +1533,8 @@ k_pos_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
             load(q, f);
             solve(f);
         }
-        __syncthreads();
+        lds_barrier();
+        PTR(1, step + 1);
         cur = nxt;
         hcur = hnxt;
         c = c1;
@@ -1780,6 +1842,7 @@ extern "C" int lpe_rigid_config_default(lpe_rigid_config *c) {
 }
 
 extern "C" int lpe_rigid_set_config(lpe_ctx *ctx, const lpe_rigid_config *cfg) {
+    if (ctx) rdev(ctx)->heavy_valid = false;
     if (!ctx || !cfg) return LPE_ERR_ARG;
     RigidDev *d = rdev(ctx);
     d->cfg = *cfg;
@@ -1875,6 +1938,7 @@ static int rscan(lpe_ctx *ctx, RigidDev *d, const int32_t *nptr, int ncap, const
 
 extern "C" int lpe_rigid_upload(lpe_ctx *ctx, int nb, const lpe_body *bodies, int nverts,
                                 const double *verts) {
+    if (ctx) rdev(ctx)->heavy_valid = false;
     if (!ctx || nb < 0 || nverts < 0 || (nb > 0 && !bodies) || (nverts > 0 && !verts))
         return LPE_ERR_ARG;
     (void)hipSetDevice(ctx->device);
@@ -2011,15 +2075,15 @@ static int detect_launch(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pa
         int st = rscan(ctx, d, nullptr, cells, d->bgCount, d->bgStart, d->bgCursor, s);
         if (st) return st;
         LPE_KERNEL(ctx, "k_bg_fill", k_bg_fill, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bgKey, d->bgCursor, d->bgList);
-        LPE_KERNEL(ctx, "k_bg_pairs", k_bg_pairs, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, 0, d->byRank, d->bodies, d->aabb,
+        LPE_KERNEL(ctx, "k_bg_pairs", k_bg_pairs, dim3((nb + BG_WAVES - 1) / BG_WAVES), dim3(RTPB), 0, s, nb, 0, d->byRank, d->bodies, d->aabb,
                    c.smallParticleThreshold, (int)G, d->bgKey, d->bgStart, d->bgList, d->bgSpecial, d->counts + 10,
                    d->pcount, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6);
         st = rscan(ctx, d, nullptr, nb, d->pcount, d->pstart, d->pcursor, s);
         if (st) return st;
-        LPE_KERNEL(ctx, "k_bg_pairs", k_bg_pairs, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, 1, d->byRank, d->bodies, d->aabb,
+        LPE_KERNEL(ctx, "k_bg_pairs", k_bg_pairs, dim3((nb + BG_WAVES - 1) / BG_WAVES), dim3(RTPB), 0, s, nb, 1, d->byRank, d->bodies, d->aabb,
                    c.smallParticleThreshold, (int)G, d->bgKey, d->bgStart, d->bgList, d->bgSpecial, d->counts + 10,
                    d->pcount, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6);
-        LPE_KERNEL(ctx, "k_bp_sort", k_bp_sort, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->pstart, d->pairs, d->pairRankB, d->cap_pairs);
+        LPE_KERNEL(ctx, "k_bp_sort", k_bp_sort, dim3((nb + RTPB / 64 - 1) / (RTPB / 64)), dim3(RTPB), 0, s, nb, d->pstart, d->pairs, d->pairRankB, d->cap_pairs);
         LPE_KERNEL(ctx, "k_bp_sort_long", k_bp_sort_long, dim3(nb), dim3(RTPB), 0, s, nb, d->pstart, d->pairs, d->pairRankB, d->cap_pairs);
         LPE_HIP(ctx, hipMemcpyAsync(d->counts, d->pstart + nb, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
     }
@@ -2416,8 +2480,14 @@ extern "C" int lpe_rigid_integrate(lpe_ctx *ctx, int systems, double dt_state, d
     if (systems & 1)
         LPE_KERNEL(ctx, "k_boundary", k_boundary, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.marginPixels * c.metersPerPixel, c.universeSize, c.bounceDamping, c.maxSpeed);
     if (systems & (2 | 32)) {   // 32: planetary-mass check only (world tick)
-        LPE_HIP(ctx, hipMemsetAsync(d->counts + 5, 0, sizeof(int32_t), s));
-        LPE_KERNEL(ctx, "k_gravity_check", k_gravity_check, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.planetaryMassThreshold, d->counts + 5);
+        // gravity.cpp:43-51 scans every tick; its inputs (gravity view flags,
+        // masses) change only by lpe_rigid_upload / lpe_rigid_set_config, so
+        // the result is kept until then
+        if (!d->heavy_valid) {
+            LPE_HIP(ctx, hipMemsetAsync(d->counts + 5, 0, sizeof(int32_t), s));
+            LPE_KERNEL(ctx, "k_gravity_check", k_gravity_check, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.planetaryMassThreshold, d->counts + 5);
+            d->heavy_valid = true;
+        }
     }
     if (systems & 2) {
         LPE_KERNEL(ctx, "k_gravity", k_gravity, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.gravity, dt_state, d->counts + 5);

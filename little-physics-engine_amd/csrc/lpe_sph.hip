@@ -1358,21 +1358,39 @@ __global__ void k_rbin_fill(int nr, const lpe_gpu_rigid *__restrict__ rig, float
         else atomicOr(&status[ST_LIST_OVERFLOW], 1);
     }
 }
-// insertion sort of each bin's list -> ascending rigid index; then the
-// entries' AABBs in list order (the coupling's candidate walk reads them
-// contiguously instead of through the index)
-__global__ void k_rbin_sort(int B, int32_t *__restrict__ start, int32_t *__restrict__ list, int cap,
-                            const float4 *__restrict__ aabb, float4 *__restrict__ baabb) {
-    int b = blockIdx.x * blockDim.x + threadIdx.x;
-    if (b >= B) return;
-    int s = min(start[b], cap), e = min(start[b + 1], cap);
-    for (int k = s + 1; k < e; k++) {
-        int v = list[k];
-        int j = k - 1;
-        while (j >= s && list[j] > v) { list[j + 1] = list[j]; j--; }
-        list[j + 1] = v;
+// each bin's list -> ascending rigid index (indices in a list are distinct):
+// one wave per bin, an entry's place is the number of smaller indices (bins
+// of more than 64 entries: one lane, insertion sort); then the entries'
+// AABBs in list order (the coupling's candidate walk reads them contiguously
+// instead of through the index)
+static constexpr int RBS_WAVES = 4;                        // bins per 256-thread block
+__global__ void __launch_bounds__(256)
+k_rbin_sort(int B, int32_t *__restrict__ start, int32_t *__restrict__ list, int cap,
+            const float4 *__restrict__ aabb, float4 *__restrict__ baabb) {
+    const int b = blockIdx.x * RBS_WAVES + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (b >= B) return;                                     // (whole wave)
+    const int s = min(start[b], cap), e = min(start[b + 1], cap), n = e - s;
+    if (n <= 0) return;
+    if (n > 64) {
+        if (lane == 0) {
+            for (int k = s + 1; k < e; k++) {
+                int v = list[k];
+                int j = k - 1;
+                while (j >= s && list[j] > v) { list[j + 1] = list[j]; j--; }
+                list[j + 1] = v;
+            }
+            for (int k = s; k < e; k++) baabb[k] = aabb[list[k]];
+        }
+        return;
     }
-    for (int k = s; k < e; k++) baabb[k] = aabb[list[k]];
+    const int v = lane < n ? list[s + lane] : 0x7fffffff;
+    int rank = 0;
+    for (int j = 0; j < n; j++) rank += __shfl(v, j) < v ? 1 : 0;
+    if (lane < n) {
+        list[s + rank] = v;
+        baabb[s + rank] = aabb[v];
+    }
 }
 
 // writeBackRigidBodies arithmetic (fluid.cpp:545-562), once per tick: the
@@ -1928,7 +1946,7 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
     d.rlist_len = total;
     LPE_KERNEL(ctx, "k_rbin_fill", k_rbin_fill, dim3(nblk(d.nr, 4)), dim3(256), 0, s, d.nr, d.rig, d.bcs,
                        d.bx0, d.by0, d.bW, d.bH, cursor, d.rbinList, d.cap_rlist, d.status);
-    LPE_KERNEL(ctx, "k_rbin_sort", k_rbin_sort, dim3(nblk(B, 128)), dim3(128), 0, s, B, d.rbinStart, d.rbinList, d.cap_rlist,
+    LPE_KERNEL(ctx, "k_rbin_sort", k_rbin_sort, dim3((B + RBS_WAVES - 1) / RBS_WAVES), dim3(256), 0, s, B, d.rbinStart, d.rbinList, d.cap_rlist,
                d.raabb, rbin_aabb(d));
     LPE_CHECK_LAUNCH(ctx, "rbin");
     d.rig_dirty = false;

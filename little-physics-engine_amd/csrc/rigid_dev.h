@@ -60,6 +60,8 @@ struct RigidDev {
     int4 *sVer = nullptr;                            // rank/cnt on A, rank/cnt on B
     int32_t *sBCount = nullptr, *sBStart = nullptr, *sBCursor = nullptr, *sEnt = nullptr;
     int32_t *counts = nullptr;                // [0]=np [1]=nc [4]=npos [5]=heavy [6]=pair overflow
+    bool heavy_valid = false;                 // counts[5] holds the planetary-mass check of the bodies
+                                              // (masses and flags change only by upload / config)
                                               // [7]=solver fault [8]=colours [9]=colouring rounds
                                               // [10]=special broadphase bodies [11]=contact truncation
     int32_t *pcol = nullptr;                  // colour per pair (canonical order)
