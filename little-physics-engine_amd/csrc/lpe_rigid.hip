@@ -989,12 +989,6 @@ __device__ __forceinline__ void pgs_row_regs(float4 rn, float4 rr, float imA, fl
 // The rows of a pair share its two bodies (and their masses): the bodies'
 // state is read from LDS once per pair and kept in registers across its rows.
 
-#ifndef LPE_PGS_PF
-#define LPE_PGS_PF 2
-#endif
-#ifndef LPE_POS_PF
-#define LPE_POS_PF 2
-#endif
 // A colour step's barrier: the step's LDS writes (velocities / poses) are
 // visible to every wave after it; outstanding global loads (the next step's
 // prefetch) stay in flight across it (__syncthreads() would drain them).
@@ -1042,7 +1036,7 @@ k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
     // and the next step's pair differs from the current one unless there is
     // a single colour (then they are read at use).  Rows in canonical order,
     // arithmetic unchanged: bit-identical to the unpipelined sweep.
-    constexpr int PF = LPE_PGS_PF;
+    constexpr int PF = 2;
     struct Pf {
         int2 sg, ab;
         float4 m, n[PF], r[PF];
@@ -1468,7 +1462,7 @@ k_pos_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
     // software-pipelined like k_pgs_colour: the next step's first pair
     // (segment, bodies, masses, its first PF rows) is loaded before the
     // current one is solved; the records are constant during the solve
-    constexpr int PF = LPE_POS_PF;
+    constexpr int PF = 2;
     struct Pf {
         int2 sg;
         int a, b, fl0;

@@ -194,20 +194,29 @@ __host__ __device__ __forceinline__ float xacc_round(const unsigned long long *a
         }
     }
     int b = -1;
-    for (int i = XACC_LIMBS - 1; i >= 0 && b < 0; i--)
-        if (d[i]) b = i * 32 + 31 - __builtin_clz(d[i]);
+#pragma unroll
+    for (int i = XACC_LIMBS - 1; i >= 0; i--)
+        if (b < 0 && d[i]) b = i * 32 + 31 - __builtin_clz(d[i]);
     if (b < 0) return 0.0f;
     const int p = b - 23 > 11 ? b - 23 : 11;                      // lsb kept; bit 11 is 2^-149
     // kept = bits [p, b] (<= 24 bits, inside the 64-bit window of limbs
-    // p/32 and p/32 + 1); guard = bit p - 1; sticky = any bit below it
+    // p/32 and p/32 + 1); guard = bit p - 1; sticky = any bit below it.
+    // The limbs are picked by unrolled compares (no dynamic register index).
     const int li = p >> 5;
-    const unsigned long long win =
-        (unsigned long long)d[li] | (li + 1 < XACC_LIMBS ? (unsigned long long)d[li + 1] << 32 : 0ull);
+    const int gb = p - 1, gl = gb >> 5;
+    uint32_t wlo = 0u, whi = 0u, gw = 0u;
+    bool sticky = false;
+#pragma unroll
+    for (int i = 0; i < XACC_LIMBS; i++) {
+        if (i == li) wlo = d[i];
+        if (i == li + 1) whi = d[i];
+        if (i == gl) gw = d[i];
+        if (i < gl) sticky |= d[i] != 0u;
+    }
+    const unsigned long long win = (unsigned long long)wlo | ((unsigned long long)whi << 32);
     uint32_t kept = (uint32_t)((win >> (p & 31)) & ((1ull << (b - p + 1)) - 1ull));
-    const int gb = p - 1;
-    const uint32_t guard = (d[gb >> 5] >> (gb & 31)) & 1u;
-    bool sticky = (d[gb >> 5] & ((1u << (gb & 31)) - 1u)) != 0u;
-    for (int i = 0; i < (gb >> 5); i++) sticky |= d[i] != 0u;
+    const uint32_t guard = (gw >> (gb & 31)) & 1u;
+    sticky |= (gw & ((1u << (gb & 31)) - 1u)) != 0u;
     if (guard && (sticky || (kept & 1u))) kept++;
     const float r = ldexpf((float)kept, p - XACC_BIAS);          // exact
     return neg ? -r : r;
