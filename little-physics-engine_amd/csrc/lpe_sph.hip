@@ -2101,25 +2101,18 @@ static int sph_migrate(lpe_ctx *ctx) {
 // World tick (lpe_world.hip): sub-step 0's kick-drift, grid hash and density
 // of the NEXT tick read only the fluid state, which is final once this tick's
 // fluid boundary/gravity kernel has run; they are launched on a side stream
-// then, so they run while the rigid solvers (one CU) run, and that tick's
-// lpe_sph_step starts at the forces (single domain; the slab path's exchanges
-// stay on the context stream).
-static constexpr int PRE_FREE_CUS = 16;
+// then, so they run while the rigid solvers (one CU each) run, and that
+// tick's lpe_sph_step starts at the forces (single domain; the slab path's
+// exchanges stay on the context stream).  The side stream is a plain one: a
+// CU-masked queue (round 1 kept 16 CUs free for the solvers) cost a third of
+// the tick rate on MI355X (396 vs 554 ticks/s on the settled metric scene),
+// while the solvers start promptly without it.
 int sph_prelaunch(lpe_ctx *ctx, double dt_tick) {
     SphDev &d = ctx->sph;
     d.pre = false;
     if (d.shard || d.n <= 0 || !d.P.x) return LPE_OK;
     if (!d.pside) {
-        // the side stream leaves a few CUs out of its mask: the solvers on
-        // the context stream are one workgroup that needs a whole CU's LDS,
-        // and would otherwise wait for the density blocks to drain
-        hipDeviceProp_t prop;
-        LPE_HIP(ctx, hipGetDeviceProperties(&prop, ctx->device));
-        const int ncu = prop.multiProcessorCount;
-        const int keep = std::max(1, ncu - PRE_FREE_CUS);
-        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-        for (int i = 0; i < keep; i++) mask[i / 32] |= 1u << (i % 32);
-        LPE_HIP(ctx, hipExtStreamCreateWithCUMask(&d.pside, (uint32_t)mask.size(), mask.data()));
+        LPE_HIP(ctx, hipStreamCreateWithFlags(&d.pside, hipStreamNonBlocking));
         LPE_HIP(ctx, hipEventCreateWithFlags(&d.preReady, hipEventDisableTiming));
         LPE_HIP(ctx, hipEventCreateWithFlags(&d.preDone, hipEventDisableTiming));
     }
