@@ -200,9 +200,10 @@ int lpe_rigid_destroy_internal(lpe_ctx *ctx);
 int rigid_tick_begin(lpe_ctx *ctx);
 int rigid_tick_boundary(lpe_ctx *ctx);
 int rigid_tick_detect(lpe_ctx *ctx);   // host half of the detection + colouring launch
+int rigid_tick_hook(lpe_ctx *ctx, int step);   // fluid-step hook (after each sub-step's forces)
 int rigid_tick_finish(lpe_ctx *ctx);
 // lpe_sph_step with a host callback after the forces of sub-step `after`
-int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int after, int (*hook)(lpe_ctx *));
+int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int));
 int sph_prelaunch(lpe_ctx *ctx, double dt_tick);
 int lpe_sph_cover_box(lpe_ctx *ctx, double x0, double y0, double x1, double y1);
 // coupling rigids' device arrays (rig, accum, acq) for n rigids (grow-only)

@@ -2373,12 +2373,36 @@ int rigid_tick_begin(lpe_ctx *ctx) {
     LPE_KERNEL(ctx, "k_boundary_pos", k_boundary_pos, dim3(rblk(d->nb)), dim3(RTPB), 0, s, d->nb, d->bodies,
                c.marginPixels * c.metersPerPixel, c.universeSize, d->bbits);
     LPE_HIP(ctx, hipEventRecord(d->evStart, s));
+    d->detect_launched = false;
+    d->overlap_pending = true;
+    return LPE_OK;
+}
+
+// The detection's launches on the side stream (after the boundary clamp).
+// Issued from the fluid step's hook once its first sub-step is enqueued: the
+// ~25 calls take the host ~150 us, and issued first they left the context
+// stream without work for that long at every tick start.
+static int rigid_tick_launch(lpe_ctx *ctx, RigidDev *d) {
+    if (d->detect_launched) return LPE_OK;
     LPE_HIP(ctx, hipStreamWaitEvent(d->side, d->evStart, 0));
     int st = detect_launch(ctx, d, 0, nullptr, d->side, d->hc);
     if (st) return st;
     LPE_HIP(ctx, hipEventRecord(d->evDetect, d->side));
-    d->overlap_pending = true;
+    d->detect_launched = true;
     return LPE_OK;
+}
+
+// Fluid-step hook, after each sub-step's forces are enqueued: the detection
+// launches after sub-step 0, its host half and the colouring after sub-step
+// 2 (the detection has finished on the device by then, so the host does not
+// wait); step < 0: everything at once.
+int rigid_tick_hook(lpe_ctx *ctx, int step) {
+    RigidDev *d = rdev(ctx);
+    if (d->nb <= 0 || !d->overlap_pending) return LPE_OK;
+    int st = rigid_tick_launch(ctx, d);
+    if (st) return st;
+    if (step < 0 || step >= 2) st = rigid_tick_detect(ctx);
+    return st;
 }
 
 // the boundary system's velocity part, at its place in the tick
@@ -2403,6 +2427,8 @@ int rigid_tick_detect(lpe_ctx *ctx) {
         ctx->err = "rigid_tick_detect without rigid_tick_begin";
         return LPE_ERR_STATE;
     }
+    int st0 = rigid_tick_launch(ctx, d);
+    if (st0) return st0;
     d->overlap_pending = false;
     LPE_HIP(ctx, hipEventSynchronize(d->evDetect));
     int retry = 0;
@@ -2442,16 +2468,17 @@ int rigid_tick_finish(lpe_ctx *ctx) {
         return LPE_OK;
     }
     // the two solvers, concurrently: the PGS after the fluid, boundary and
-    // gravity systems set the velocities, the position solver (solver
-    // stream) beside it.  (Run during the fluid step instead, the
-    // one-workgroup position solver slows the full-chip fluid kernels by more
-    // than it saves.)
+    // gravity systems set the velocities, the position solver beside it on
+    // the detection stream (idle by now; the solver stream shares a hardware
+    // queue with the next tick's prelaunch, which then delayed it).  (Run
+    // during the fluid step instead, the one-workgroup position solver slows
+    // the full-chip fluid kernels by more than it saves.)
     LPE_HIP(ctx, hipStreamWaitEvent(s, d->evColour, 0));
     LPE_HIP(ctx, hipEventRecord(d->evFork, s));
-    LPE_HIP(ctx, hipStreamWaitEvent(d->psolve, d->evFork, 0));
-    st = colour_pos(ctx, d, d->psolve);
+    LPE_HIP(ctx, hipStreamWaitEvent(d->side, d->evFork, 0));
+    st = colour_pos(ctx, d, d->side);
     if (st) return st;
-    LPE_HIP(ctx, hipEventRecord(d->evJoin, d->psolve));
+    LPE_HIP(ctx, hipEventRecord(d->evJoin, d->side));
     st = colour_pgs(ctx, d, s);
     if (st) return st;
     LPE_HIP(ctx, hipStreamWaitEvent(s, d->evJoin, 0));

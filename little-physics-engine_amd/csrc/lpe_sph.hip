@@ -2147,10 +2147,10 @@ int sph_prelaunch(lpe_ctx *ctx, double dt_tick) {
 }
 
 extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
-    return sph_step_hooked(ctx, dt_tick, -1, nullptr);
+    return sph_step_hooked(ctx, dt_tick, nullptr);
 }
 
-int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int after, int (*hook)(lpe_ctx *)) {
+int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
     if (!ctx) return LPE_ERR_ARG;
     SphDev &d = ctx->sph;
     if (d.n <= 0 && !d.shard) return LPE_OK;  // fluid.cpp:969-972 (a slab rank joins the exchanges)
@@ -2231,14 +2231,13 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int after, int (*hook)(lpe_ctx
                            rbin_aabb(d),
                            d.acq, d.status);
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
-        if (hook && (step == after || (step + 1 == c.numSubSteps && after >= step))) {
-            st = hook(ctx);
+        if (hook) {                                  // (lpe_world_tick: the rigid detection)
+            st = hook(ctx, step);
             if (st) return st;
-            hook = nullptr;
         }
     }
-    if (hook) {                                      // no sub-steps ran
-        st = hook(ctx);
+    if (hook) {                                      // after the sub-steps: whatever is still pending
+        st = hook(ctx, -1);
         if (st) return st;
     }
     if (d.nr > 0) {

@@ -207,9 +207,9 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
             if (st) return st;
         }
         if (fluid) {
-            // the detection's host half and the colouring launch after the
-            // second sub-step's forces (rigid_tick_detect)
-            int st = sph_step_hooked(ctx, dt_fluid, 1, overlap ? rigid_tick_detect : nullptr);
+            // the detection launches after the first sub-step, its host half
+            // and the colouring after the third (rigid_tick_hook)
+            int st = sph_step_hooked(ctx, dt_fluid, overlap ? rigid_tick_hook : nullptr);
             if (st) return st;
             if (nr > 0)
                 LPE_KERNEL(ctx, "k_scatter_rigid_vel", k_scatter_rigid_vel, dim3(wblk(nr, 128)), dim3(128), 0, s, nr, d.coupleBody, d.rig, rd->bodies);

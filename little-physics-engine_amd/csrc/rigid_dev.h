@@ -60,6 +60,7 @@ struct RigidDev {
     int4 *sVer = nullptr;                            // rank/cnt on A, rank/cnt on B
     int32_t *sBCount = nullptr, *sBStart = nullptr, *sBCursor = nullptr, *sEnt = nullptr;
     int32_t *counts = nullptr;                // [0]=np [1]=nc [4]=npos [5]=heavy [6]=pair overflow
+    bool detect_launched = false;             // this tick's detection is on the side stream
     bool heavy_valid = false;                 // counts[5] holds the planetary-mass check of the bodies
                                               // (masses and flags change only by upload / config)
                                               // [7]=solver fault [8]=colours [9]=colouring rounds
