@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 namespace lpe {
@@ -935,6 +936,9 @@ k_pair_colour(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict_
 // solveLcpPgs (contact_solver.cpp:381-440), rows of buildConstraintRows
 // (:133-197) in fp32, body velocities in LDS.
 // one contact row (normal, then friction) on the pair's velocities in registers
+#ifndef PGS_BRANCHLESS
+#define PGS_BRANCHLESS 0
+#endif
 typedef float pk2 __attribute__((ext_vector_type(2)));
 // The x/y halves of the row are computed as packed fp32 pairs (v_pk_mul_f32 /
 // v_pk_add_f32: each lane of a packed op is the IEEE scalar op, unfused), so
@@ -967,6 +971,18 @@ __device__ __forceinline__ void pgs_row_regs(float4 rn, float4 rr, float imA, fl
         if (nl > hi) nl = hi;
         dl = nl - old;
         if (row == 0) ln = nl; else lf = nl;
+#if PGS_BRANCHLESS
+        // the skipped / absent-body cases as selects of the unchanged values
+        // (bit-identical to the branches; keeps exec-mask updates and their
+        // VALU -> SALU hazards out of the row chain)
+        const bool apply = !(fabsf(dl) < 1e-15F);
+        const float crossA = rr.x * d.y - rr.y * d.x, crossB = rr.z * d.y - rr.w * d.x;
+        const pk2 nvA = vA - d * (dl * imA), nvB = vB + d * (dl * imB);
+        const float nwA = wA - crossA * dl * iiA, nwB = wB + crossB * dl * iiB;
+        const bool uA = apply && hasA, uB = apply && hasB;
+        vA.x = uA ? nvA.x : vA.x; vA.y = uA ? nvA.y : vA.y; wA = uA ? nwA : wA;
+        vB.x = uB ? nvB.x : vB.x; vB.y = uB ? nvB.y : vB.y; wB = uB ? nwB : wB;
+#else
         if (fabsf(dl) < 1e-15F) continue;
         if (hasA) {
             vA -= d * (dl * imA);
@@ -978,6 +994,7 @@ __device__ __forceinline__ void pgs_row_regs(float4 rn, float4 rr, float imA, fl
             float crossB = rr.z * d.y - rr.w * d.x;
             wB += crossB * dl * iiB;
         }
+#endif
     }
     vxA = vA.x; vyA = vA.y; vxB = vB.x; vyB = vB.y;
 }
@@ -994,6 +1011,33 @@ __device__ __forceinline__ void pgs_row_regs(float4 rn, float4 rr, float imA, fl
 // prefetch) stay in flight across it (__syncthreads() would drain them).
 // Global data written inside the sweeps (the PGS multipliers) is re-read only
 // by the thread that wrote it (static pair -> thread map).
+// Buffer loads / stores with a 32-bit byte offset (one address VGPR per
+// operation instead of two); descriptors built from kernel arguments only,
+// so they stay in SGPRs.  No range limit beyond the 32-bit offset.
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *p) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+// A lane without work passes ok = false: its offset is out of range, so the
+// load returns zeros without touching memory while the wave keeps a fixed
+// count of memory operations (what lets the compiler's waits stay partial).
+static constexpr uint32_t BOOB = 0x80000000u;
+__device__ __forceinline__ float4 bld_f4(__amdgpu_buffer_rsrc_t r, uint32_t i, bool ok = true) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(ok ? i * 16u : BOOB), 0, 0);
+    return make_float4(__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w));
+}
+__device__ __forceinline__ int2 bld_i2(__amdgpu_buffer_rsrc_t r, uint32_t i, bool ok = true) {
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(ok ? i * 8u : BOOB), 0, 0);
+    return make_int2((int)v.x, (int)v.y);
+}
+__device__ __forceinline__ float bld_f(__amdgpu_buffer_rsrc_t r, uint32_t i, bool ok = true) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (int)(ok ? i * 4u : BOOB), 0, 0));
+}
+__device__ __forceinline__ void bst_f(__amdgpu_buffer_rsrc_t r, uint32_t i, float v, bool ok = true) {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, (int)(ok ? i * 4u : BOOB), 0, 0);
+}
+
 __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     __builtin_amdgcn_s_barrier();
@@ -1010,113 +1054,180 @@ extern "C" int lpe_ptrace(unsigned long long *host) {
 #else
 #define PTR(w, k) do {} while (0)
 #endif
+#ifndef PGS_PF
+#define PGS_PF 2    // rows of a pair prefetched with it
+#endif
+#ifndef PGS_TL
+#define PGS_TL 1    // further rows loaded at the start of its slot (waves with longer pairs)
+#endif
+#ifndef PGS_ILV
+#define PGS_ILV 1   // the next slot's rows loaded between the current pair's rows
+#endif
 __global__ void __launch_bounds__(SOLVE_TPB)
 k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restrict__ cbase,
              const int2 *__restrict__ seg, int segLds, const float4 *__restrict__ rowN,
              const float4 *__restrict__ rowR, const int2 *__restrict__ rowAB,
              const float4 *__restrict__ rowM, float *__restrict__ vel, int iters, float mu,
              float *__restrict__ lamN, float *__restrict__ lamF) {
-    extern __shared__ float sv[];   // 3 floats per body, then the segment cache
-    int2 *ss = (int2 *)(sv + ((3 * nb + 1) & ~1));
+    extern __shared__ float sv[];   // 3 floats per body
     __shared__ int scb[MAX_COLOURS + 1];
     const int ncol = counts[8];
     for (int i = threadIdx.x; i < 3 * nb; i += SOLVE_TPB) sv[i] = vel[i];
     for (int c = threadIdx.x; c <= ncol; c += SOLVE_TPB) scb[c] = cbase[c];
     __syncthreads();
-    const int npc = scb[ncol];
-    const int ncached = min(npc, segLds);                  // the first segLds segments live in LDS
-    for (int q = threadIdx.x; q < ncached; q += SOLVE_TPB) ss[q] = seg[q];
-    __syncthreads();
-    // One item per thread and colour step is software-pipelined: the global
-    // loads of the thread's first pair of the NEXT step (segment, bodies,
-    // masses, its first PF rows and their multipliers) are issued before the
-    // current pair is solved, so they arrive during the solve and the
-    // barrier.  Row data are constant during the solve; a pair's multipliers
-    // are written only by the thread that owns it (static q -> thread map),
-    // and the next step's pair differs from the current one unless there is
-    // a single colour (then they are read at use).  Rows in canonical order,
-    // arithmetic unchanged: bit-identical to the unpipelined sweep.
-    constexpr int PF = 2;
+    (void)segLds;
+    // Slots: a colour's pairs are split into ceil(n / SOLVE_TPB) slots of at
+    // most one pair per thread (pairs of one colour share no movable body,
+    // so any split is the same sweep); the barrier follows a colour's last
+    // slot.  Slots are software-pipelined: the global loads of the thread's
+    // pair of the NEXT slot (bodies, masses, its first PF rows and their
+    // multipliers) are issued before the current pair is solved, and the
+    // segment of the slot after that one slot earlier still, so they arrive
+    // during the solve and the barrier.  The two slot buffers alternate (no
+    // register copy, which would wait for the loads), and every prefetch and
+    // every store of the first PF rows is issued unconditionally (a thread
+    // without a next pair, or a pair with fewer rows, reads out of range:
+    // zeros, no memory traffic; a pair with fewer rows re-stores its last
+    // row), so the counts of memory operations in flight are static and each
+    // wait covers only the buffer it needs.  Row data are constant
+    // during the solve; a pair's multipliers are written only by the thread
+    // that owns it (static q -> thread map), and the next slot's pair
+    // differs from the current one (an iteration has at least two slots).
+    // Rows in canonical order, arithmetic unchanged: bit-identical to the
+    // unpipelined sweep.
+    constexpr int PF = PGS_PF, TL = PGS_TL;
+    constexpr bool ILV = PGS_ILV;
+    struct Row { float4 n, r; float ln, lf; };
     struct Pf {
         int2 sg, ab;
-        float4 m, n[PF], r[PF];
-        float ln[PF], lf[PF];
+        float4 m;
+        Row r[PF];
     };
-    auto load = [&](int q, int it, bool lam, Pf &f) {
-        f.sg = q < ncached ? ss[q] : seg[q];
-        f.ab = rowAB[f.sg.x];
-        f.m = rowM[f.sg.x];
-        const int nrow = f.sg.y & 0xff, stride = f.sg.y >> 8;
-#pragma unroll
-        for (int j = 0; j < PF; j++)
-            if (j < nrow) {
-                const int t = f.sg.x + j * stride;
-                f.n[j] = rowN[t]; f.r[j] = rowR[t];
-                f.ln[j] = (it && lam) ? lamN[t] : 0.f;
-                f.lf[j] = (it && lam) ? lamF[t] : 0.f;
-            }
+    const auto rN = brsrc(rowN), rR = brsrc(rowR), rAB = brsrc(rowAB), rM = brsrc(rowM);
+    const auto rLN = brsrc(lamN), rLF = brsrc(lamF), rSeg = brsrc(seg);
+    auto ldrow = [&](int t, bool ok, Row &w) {
+        w.n = bld_f4(rN, t, ok); w.r = bld_f4(rR, t, ok);
+        w.ln = bld_f(rLN, t, ok); w.lf = bld_f(rLF, t, ok);
     };
-    auto solve = [&](Pf &f, int it, bool lam) {
-        const int nrow = f.sg.y & 0xff, stride = f.sg.y >> 8;   // rows: sg.x + j * stride
-        const int2 ab = f.ab;
-        const float4 m = f.m;
-        const bool hasA = ab.x >= 0, hasB = ab.y >= 0;
-        float vxA = 0.f, vyA = 0.f, wA = 0.f, vxB = 0.f, vyB = 0.f, wB = 0.f;
-        if (hasA) { vxA = sv[3 * ab.x]; vyA = sv[3 * ab.x + 1]; wA = sv[3 * ab.x + 2]; }
-        if (hasB) { vxB = sv[3 * ab.y]; vyB = sv[3 * ab.y + 1]; wB = sv[3 * ab.y + 2]; }
-#pragma unroll
-        for (int j = 0; j < PF; j++)
-            if (j < nrow) {
-                const int t = f.sg.x + j * stride;
-                if (!lam && it) { f.ln[j] = lamN[t]; f.lf[j] = lamF[t]; }
-                pgs_row_regs(f.n[j], f.r[j], m.x, m.y, m.z, m.w, hasA, hasB, mu, f.ln[j], f.lf[j], vxA, vyA,
-                             wA, vxB, vyB, wB);
-                lamN[t] = f.ln[j]; lamF[t] = f.lf[j];
-            }
-        for (int j = PF; j < nrow; j++) {                     // longer pairs: on demand
-            const int t = f.sg.x + j * stride;
-            float ln = it ? lamN[t] : 0.f, lf = it ? lamF[t] : 0.f;
-            pgs_row_regs(rowN[t], rowR[t], m.x, m.y, m.z, m.w, hasA, hasB, mu, ln, lf, vxA, vyA, wA, vxB,
-                         vyB, wB);
-            lamN[t] = ln; lamF[t] = lf;
-        }
-        if (hasA) { sv[3 * ab.x] = vxA; sv[3 * ab.x + 1] = vyA; sv[3 * ab.x + 2] = wA; }
-        if (hasB) { sv[3 * ab.y] = vxB; sv[3 * ab.y + 1] = vyB; sv[3 * ab.y + 2] = wB; }
+    // row j of the pair with segment sg (rows past its last: clamped to it,
+    // not loaded; no pair: an out-of-range segment, nrow 0)
+    auto ldrow_j = [&](int2 sg, int j, Row &w) {
+        const int nrow = sg.y & 0xff, stride = sg.y >> 8;
+        ldrow(sg.x + min(j, max(nrow - 1, 0)) * stride, j < nrow, w);
     };
-    const int total = iters * ncol;
-    const bool lamPf = ncol > 1;
+    auto ldpair = [&](int2 sg, Pf &f) {
+        f.sg = sg;
+        const bool ok = (sg.y & 0xff) > 0;
+        f.ab = bld_i2(rAB, sg.x, ok);
+        f.m = bld_f4(rM, sg.x, ok);
+    };
+    auto ucb = [&](int c) { return __builtin_amdgcn_readfirstlane(scb[c]); };
+    auto nslot0 = [&](int c) { return (ucb(c + 1) - ucb(c) + SOLVE_TPB - 1) / SOLVE_TPB; };
+    int S = 0;
+    for (int c = 0; c < ncol; c++) S += nslot0(c);
+    // an iteration of one slot gets an empty second slot: the multipliers
+    // prefetched for the next iteration are then loaded after this one's
+    // stores (the prefetch is always valid)
+    const int pad = S == 1 ? 1 : 0;
+    auto nslot = [&](int c) { return nslot0(c) + pad; };
+    const int total = iters * (S + pad);
     PTR(0, 0);
 #ifdef LPE_PTRACE
     if (threadIdx.x <= ncol) g_ptrace[1][1024 + threadIdx.x] = scb[threadIdx.x];
 #endif
-    Pf cur{}, nxt{};
-    bool hcur = false;
+    // slot positions (colour, slot of the colour, iteration) of slots s, s+1, s+2
+    struct SP { int c, k, it; };
+    auto adv = [&](SP p) {
+        if (++p.k == nslot(p.c)) { p.k = 0; if (++p.c == ncol) { p.c = 0; p.it++; } }
+        return p;
+    };
+    auto seg_of = [&](SP p) {
+        const int q = ucb(p.c) + threadIdx.x + p.k * SOLVE_TPB;
+        return bld_i2(rSeg, q, q < ucb(p.c + 1) && p.it < iters);
+    };
+    SP p0{0, 0, 0}, p1 = adv(p0), p2 = adv(p1);
+    // one slot: [the current pairs' rows PF.. PF+TL-1 when the wave has
+    // longer pairs] [segment of slot s+2 into sgZ] [bodies, masses of slot
+    // s+1 into Y], then the current pair X row by row, each row followed by
+    // the load of Y's row of that index (the next slot's data streams in
+    // during the solve instead of stalling the wave's issue at its start),
+    // barrier after the colour's last slot.  The multipliers are stored for
+    // every row slot, out of range where there is none.
+    auto slot = [&](auto tail, Pf &X, Pf &Y, int2 sgY, int2 &sgZ) {
+        constexpr bool TAIL = decltype(tail)::value;
+        const int it = p0.it;
+        const int nrow = X.sg.y & 0xff, stride = X.sg.y >> 8;
+        const bool hx = nrow > 0;
+        Row T[TL > 0 ? TL : 1];
+        if constexpr (TAIL) {
+#pragma unroll
+            for (int j = 0; j < TL; j++) ldrow_j(X.sg, PF + j, T[j]);
+        }
+        sgZ = seg_of(p2);
+        ldpair(sgY, Y);
+        if constexpr (!ILV) {
+#pragma unroll
+            for (int j = 0; j < PF; j++) ldrow_j(sgY, j, Y.r[j]);
+        }
+        const int2 ab = X.ab;
+        const float4 m = X.m;
+        const bool hasA = hx && ab.x >= 0, hasB = hx && ab.y >= 0;
+        float vxA = 0.f, vyA = 0.f, wA = 0.f, vxB = 0.f, vyB = 0.f, wB = 0.f;
+        if (hasA) { vxA = sv[3 * ab.x]; vyA = sv[3 * ab.x + 1]; wA = sv[3 * ab.x + 2]; }
+        if (hasB) { vxB = sv[3 * ab.y]; vyB = sv[3 * ab.y + 1]; wB = sv[3 * ab.y + 2]; }
+        auto row = [&](int j, Row &w) {
+            float ln = it ? w.ln : 0.f, lf = it ? w.lf : 0.f;
+            if (j < nrow)
+                pgs_row_regs(w.n, w.r, m.x, m.y, m.z, m.w, hasA, hasB, mu, ln, lf, vxA, vyA, wA, vxB, vyB, wB);
+            const int t = X.sg.x + min(j, max(nrow - 1, 0)) * stride;
+            bst_f(rLN, t, ln, j < nrow); bst_f(rLF, t, lf, j < nrow);
+        };
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            row(j, X.r[j]);
+            if constexpr (ILV) {
+                __builtin_amdgcn_sched_barrier(0);
+                ldrow_j(sgY, j, Y.r[j]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if constexpr (TAIL) {
+#pragma unroll
+            for (int j = 0; j < TL; j++) row(PF + j, T[j]);
+        }
+        for (int j = TAIL ? PF + TL : PF; j < nrow; j++) {   // longer pairs: on demand
+            Row w;
+            ldrow(X.sg.x + j * stride, true, w);
+            row(j, w);
+        }
+        if (hasA) { sv[3 * ab.x] = vxA; sv[3 * ab.x + 1] = vyA; sv[3 * ab.x + 2] = wA; }
+        if (hasB) { sv[3 * ab.y] = vxB; sv[3 * ab.y + 1] = vyB; sv[3 * ab.y + 2] = wB; }
+        if (p1.k == 0) {
+            lds_barrier();
+            PTR(0, p0.it * ncol + p0.c + 1);
+        }
+        p0 = p1; p1 = p2; p2 = adv(p2);
+    };
+    auto step = [&](Pf &X, Pf &Y, int2 sgY, int2 &sgZ) {
+        if (TL > 0 && __builtin_amdgcn_ballot_w64((X.sg.y & 0xff) > PF) != 0)
+            slot(std::true_type{}, X, Y, sgY, sgZ);
+        else
+            slot(std::false_type{}, X, Y, sgY, sgZ);
+    };
+    Pf bufA{}, bufB{};
+    int2 sgA = make_int2(0, 0), sgB = make_int2(0, 0);
     if (total > 0) {
-        const int q = scb[0] + threadIdx.x;
-        hcur = q < scb[1];
-        if (hcur) load(q, 0, lamPf, cur);
+        const int2 sg0 = seg_of(p0);
+        ldpair(sg0, bufA);
+#pragma unroll
+        for (int j = 0; j < PF; j++) ldrow_j(sg0, j, bufA.r[j]);
+        sgB = seg_of(p1);
     }
-    for (int step = 0, it = 0, c = 0; step < total; step++) {
-        int it1 = it, c1 = c + 1;
-        if (c1 == ncol) { c1 = 0; it1++; }
-        bool hnxt = false;
-        if (step + 1 < total) {
-            const int q = scb[c1] + threadIdx.x;
-            hnxt = q < scb[c1 + 1];
-            if (hnxt) load(q, it1, lamPf, nxt);
-        }
-        if (hcur) solve(cur, it, lamPf);
-        for (int q = scb[c] + threadIdx.x + SOLVE_TPB; q < scb[c + 1]; q += SOLVE_TPB) {
-            Pf f;
-            load(q, it, true, f);
-            solve(f, it, true);
-        }
-        lds_barrier();
-        PTR(0, step + 1);
-        cur = nxt;
-        hcur = hnxt;
-        it = it1;
-        c = c1;
+    // slot s solves the buffer of s's parity and fills the other; the
+    // segment registers hold slot s+1's (parity of s+1) and s+2's
+    for (int s = 0; s < total; s += 2) {
+        step(bufA, bufB, sgB, sgA);
+        if (s + 1 < total) step(bufB, bufA, sgA, sgB);
     }
     for (int i = threadIdx.x; i < 3 * nb; i += SOLVE_TPB) vel[i] = sv[i];
 }
@@ -1357,17 +1468,24 @@ __global__ void k_pos_fill(const int32_t *__restrict__ ncptr, const int32_t *__r
 // (non-kept contacts become skipped items), so the colour segments of the PGS
 // apply unchanged; colour-synchronous sweeps (see k_pgs_colour), body poses
 // in LDS (fp64).  solvePositionContactsOnce (position_solver.cpp:215-290).
+// The rows are stored as arrays (44 bytes a row, the pair's bodies and
+// masses with each row and read from its first), carved from posRec's
+// allocation: lanes of a wave read consecutive 16-byte pieces.
+struct PosRows {
+    double2 *n, *c, *m, *i;    // (nx, ny), (corr, px), (invMA, invMB), (invIA, invIB)
+    double *py;
+    int2 *ab;                  // bodies
+    int32_t *fl;               // 1 skipped, 2 A rotates, 4 B rotates
+};
 __global__ void k_pos_fill_rows(const int32_t *__restrict__ ncptr, const int32_t *__restrict__ order,
                                 const lpe_contact *__restrict__ cs, const lpe_body *__restrict__ bodies,
-                                const double *__restrict__ st, PosRec *__restrict__ rec,
+                                const double *__restrict__ st, PosRows out,
                                 int32_t *__restrict__ inPos, double baumgarte, double slop) {
     int u = blockIdx.x * RTPB + threadIdx.x;
     if (u >= *ncptr) return;
     const lpe_contact c = cs[order[u]];
     const bool kept = solid_body(bodies[c.a]) || solid_body(bodies[c.b]);   // gatherPositionData (:67-120)
     int fa = (int)st[3 * c.a + 2], fb = (int)st[3 * c.b + 2];
-    PosRec q;
-    q.a = c.a; q.b = c.b;
     int fl = kept ? 0 : 1;
     if (kept) { inPos[c.a] = 1; inPos[c.b] = 1; }
     if (!(fa & 2) || !(fb & 2)) fl |= 1;
@@ -1377,14 +1495,13 @@ __global__ void k_pos_fill_rows(const int32_t *__restrict__ ncptr, const int32_t
     if (fa & 1) fl |= 2;
     if (fb & 1) fl |= 4;
     D2 n = nrm(d2(c.nx, c.ny));
-    q.nx = n.x; q.ny = n.y;
-    q.corr = baumgarte * pen;
-    q.px = c.px; q.py = c.py;
-    q.invMA = st[3 * c.a]; q.invMB = st[3 * c.b];
-    q.invIA = st[3 * c.a + 1]; q.invIB = st[3 * c.b + 1];
-    q.flags = fl;
-    q.pad = 0;
-    rec[u] = q;
+    out.n[u] = make_double2(n.x, n.y);
+    out.c[u] = make_double2(baumgarte * pen, c.px);
+    out.py[u] = c.py;
+    out.fl[u] = fl;
+    out.m[u] = make_double2(st[3 * c.a], st[3 * c.b]);
+    out.i[u] = make_double2(st[3 * c.a + 1], st[3 * c.b + 1]);
+    out.ab[u] = make_int2(c.a, c.b);
 }
 
 // one item on the pair's poses in registers (the colour solver): the items of
@@ -1439,13 +1556,40 @@ __device__ __forceinline__ void pos_item(const PosRec &q, double *sp) {
     }
 }
 
+#ifndef POS_PF
+#define POS_PF 1    // rows of a pair prefetched with it
+#endif
+#ifndef POS_TL
+#define POS_TL 2    // further rows loaded at the start of its slot (waves with longer pairs)
+#endif
+#ifndef POS_ILV
+#define POS_ILV 0   // the next slot's rows loaded between the current pair's rows
+#endif
+__device__ __forceinline__ double2 bld_d2(__amdgpu_buffer_rsrc_t r, uint32_t i, bool ok = true) {
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)(ok ? i * 16u : BOOB), 0, 0);
+    return make_double2(__hiloint2double((int)v.y, (int)v.x), __hiloint2double((int)v.w, (int)v.z));
+}
+__device__ __forceinline__ double bld_d(__amdgpu_buffer_rsrc_t r, uint32_t i, bool ok = true) {
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, (int)(ok ? i * 8u : BOOB), 0, 0);
+    return __hiloint2double((int)v.y, (int)v.x);
+}
+__device__ __forceinline__ int bld_i(__amdgpu_buffer_rsrc_t r, uint32_t i, bool ok = true) {
+    return (int)__builtin_amdgcn_raw_buffer_load_b32(r, (int)(ok ? i * 4u : BOOB), 0, 0);
+}
+// Slot-pipelined like k_pgs_colour (see there): a colour's pairs in slots of
+// at most one pair per thread, the next slot's pair (bodies, masses, first
+// POS_PF rows) prefetched into the other buffer, the segment of the slot
+// after it one slot earlier, idle lanes reading out of range.  A wave whose
+// current pairs have more rows loads rows POS_PF.. POS_PF+POS_TL-1 at the
+// start of the slot (before the prefetch, so each wait stays exact); rows
+// beyond those are read on demand.  Rows in canonical order, arithmetic
+// unchanged: bit-identical to the sequential sweep in colour-major order.
 __global__ void __launch_bounds__(SOLVE_TPB)
 k_pos_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restrict__ cbase,
-             const int2 *__restrict__ seg, int segLds, const PosRec *__restrict__ rec,
+             const int2 *__restrict__ seg, PosRows rows,
              lpe_body *__restrict__ bodies, const double *__restrict__ st,
              const int32_t *__restrict__ inPos, int iters) {
-    extern __shared__ double sp[];   // x, y, angle per body, then the segment cache
-    int2 *ss = (int2 *)(sp + 3 * nb);
+    extern __shared__ double sp[];   // x, y, angle per body
     __shared__ int scb[MAX_COLOURS + 1];
     const int ncol = counts[8];
     for (int i = threadIdx.x; i < nb; i += SOLVE_TPB) {
@@ -1455,84 +1599,129 @@ k_pos_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
     }
     for (int c = threadIdx.x; c <= ncol; c += SOLVE_TPB) scb[c] = cbase[c];
     __syncthreads();
-    const int npc = scb[ncol];
-    const int ncached = min(npc, segLds);                  // the first segLds segments live in LDS
-    for (int q = threadIdx.x; q < ncached; q += SOLVE_TPB) ss[q] = seg[q];
-    __syncthreads();
-    // software-pipelined like k_pgs_colour: the next step's first pair
-    // (segment, bodies, masses, its first PF rows) is loaded before the
-    // current one is solved; the records are constant during the solve
-    constexpr int PF = 2;
+    const auto rN = brsrc(rows.n), rC = brsrc(rows.c), rMm = brsrc(rows.m), rI = brsrc(rows.i);
+    const auto rPy = brsrc(rows.py), rAB = brsrc(rows.ab), rF = brsrc(rows.fl), rSeg = brsrc(seg);
+    constexpr int PF = POS_PF, TL = POS_TL;
+    constexpr bool ILV = POS_ILV;
+    struct Row { double nx, ny, cr, px, py; int fl; };
     struct Pf {
         int2 sg;
-        int a, b, fl0;
-        double invMA, invMB, invIA, invIB;
-        double nx[PF], ny[PF], cr[PF], px[PF], py[PF];
-        int fl[PF];
+        int a, b;
+        double iMA, iMB, iIA, iIB;
+        Row r[PF];
     };
-    auto load = [&](int q, Pf &f) {
-        f.sg = q < ncached ? ss[q] : seg[q];
-        const int nrow = f.sg.y & 0xff, stride = f.sg.y >> 8;
-        const PosRec &q0 = rec[f.sg.x];
-        f.a = q0.a; f.b = q0.b; f.fl0 = q0.flags;
-        f.invMA = q0.invMA; f.invMB = q0.invMB; f.invIA = q0.invIA; f.invIB = q0.invIB;
-#pragma unroll
-        for (int j = 0; j < PF; j++)
-            if (j < nrow) {
-                const PosRec &qr = rec[f.sg.x + j * stride];
-                f.nx[j] = qr.nx; f.ny[j] = qr.ny; f.cr[j] = qr.corr; f.px[j] = qr.px; f.py[j] = qr.py;
-                f.fl[j] = qr.flags;
-            }
+    auto ldrow = [&](int t, bool ok, Row &w) {
+        const double2 n = bld_d2(rN, t, ok), c = bld_d2(rC, t, ok);
+        w.nx = n.x; w.ny = n.y; w.cr = c.x; w.px = c.y;
+        w.py = bld_d(rPy, t, ok);
+        w.fl = bld_i(rF, t, ok);
     };
-    auto solve = [&](const Pf &f) {
-        const int nrow = f.sg.y & 0xff, stride = f.sg.y >> 8;   // rows: sg.x + j * stride
-        const int a = f.a, b = f.b;
-        double xA = sp[3 * a], yA = sp[3 * a + 1], tA = sp[3 * a + 2];
-        double xB = sp[3 * b], yB = sp[3 * b + 1], tB = sp[3 * b + 2];
-#pragma unroll
-        for (int j = 0; j < PF; j++)
-            if (j < nrow)
-                pos_item_regs(f.nx[j], f.ny[j], f.cr[j], f.px[j], f.py[j], f.fl[j], f.invMA, f.invMB, f.invIA,
-                              f.invIB, xA, yA, tA, xB, yB, tB);
-        for (int j = PF; j < nrow; j++) {                     // longer pairs: on demand
-            const PosRec &qr = rec[f.sg.x + j * stride];
-            pos_item_regs(qr.nx, qr.ny, qr.corr, qr.px, qr.py, qr.flags, f.invMA, f.invMB, f.invIA, f.invIB,
-                          xA, yA, tA, xB, yB, tB);
-        }
-        // a static body (invM = 0, no rotation) is never written: pairs
-        // of one colour may share it
-        if (f.invMA != 0.0 || (f.fl0 & 2)) { sp[3 * a] = xA; sp[3 * a + 1] = yA; sp[3 * a + 2] = tA; }
-        if (f.invMB != 0.0 || (f.fl0 & 4)) { sp[3 * b] = xB; sp[3 * b + 1] = yB; sp[3 * b + 2] = tB; }
+    // row j of the pair with segment sg (rows past its last: clamped to it,
+    // not loaded; no pair: an out-of-range segment, nrow 0)
+    auto ldrow_j = [&](int2 sg, int j, Row &w) {
+        const int nrow = sg.y & 0xff, stride = sg.y >> 8;
+        ldrow(sg.x + min(j, max(nrow - 1, 0)) * stride, j < nrow, w);
     };
-    const int total = iters * ncol;
+    auto ldpair = [&](int2 sg, Pf &f) {
+        f.sg = sg;
+        const bool ok = (sg.y & 0xff) > 0;
+        const int2 ab = bld_i2(rAB, sg.x, ok);
+        f.a = ab.x; f.b = ab.y;
+        const double2 m = bld_d2(rMm, sg.x, ok), ii = bld_d2(rI, sg.x, ok);
+        f.iMA = m.x; f.iMB = m.y; f.iIA = ii.x; f.iIB = ii.y;
+    };
+    auto ucb = [&](int c) { return __builtin_amdgcn_readfirstlane(scb[c]); };
+    auto nslot0 = [&](int c) { return (ucb(c + 1) - ucb(c) + SOLVE_TPB - 1) / SOLVE_TPB; };
+    int S = 0;
+    for (int c = 0; c < ncol; c++) S += nslot0(c);
+    const int total = iters * S;
+    struct SP { int c, k, it; };
+    auto adv = [&](SP p) {
+        if (++p.k == nslot0(p.c)) { p.k = 0; if (++p.c == ncol) { p.c = 0; p.it++; } }
+        return p;
+    };
+    auto seg_of = [&](SP p) {
+        const int q = ucb(p.c) + threadIdx.x + p.k * SOLVE_TPB;
+        return bld_i2(rSeg, q, q < ucb(p.c + 1) && p.it < iters);
+    };
+    SP p0{0, 0, 0}, p1 = adv(p0), p2 = adv(p1);
     PTR(1, 0);
-    Pf cur{}, nxt{};
-    bool hcur = false;
+    // one slot, laid out as k_pgs_colour's
+    auto slot = [&](auto tail, Pf &X, Pf &Y, int2 sgY, int2 &sgZ) {
+        constexpr bool TAIL = decltype(tail)::value;
+        const int nrow = X.sg.y & 0xff, stride = X.sg.y >> 8;
+        const bool hx = nrow > 0;
+        Row T[TL > 0 ? TL : 1];
+        if constexpr (TAIL) {
+#pragma unroll
+            for (int j = 0; j < TL; j++) ldrow_j(X.sg, PF + j, T[j]);
+        }
+        sgZ = seg_of(p2);
+        ldpair(sgY, Y);
+        if constexpr (!ILV) {
+#pragma unroll
+            for (int j = 0; j < PF; j++) ldrow_j(sgY, j, Y.r[j]);
+        }
+        const int a = X.a, b = X.b;
+        double xA = 0.0, yA = 0.0, tA = 0.0, xB = 0.0, yB = 0.0, tB = 0.0;
+        if (hx) {
+            xA = sp[3 * a]; yA = sp[3 * a + 1]; tA = sp[3 * a + 2];
+            xB = sp[3 * b]; yB = sp[3 * b + 1]; tB = sp[3 * b + 2];
+        }
+        auto row = [&](int j, const Row &w) {
+            if (j < nrow)
+                pos_item_regs(w.nx, w.ny, w.cr, w.px, w.py, w.fl, X.iMA, X.iMB, X.iIA, X.iIB, xA, yA, tA, xB,
+                              yB, tB);
+        };
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            row(j, X.r[j]);
+            if constexpr (ILV) {
+                __builtin_amdgcn_sched_barrier(0);
+                ldrow_j(sgY, j, Y.r[j]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        if constexpr (TAIL) {
+#pragma unroll
+            for (int j = 0; j < TL; j++) row(PF + j, T[j]);
+        }
+        for (int j = TAIL ? PF + TL : PF; j < nrow; j++) {   // longer pairs: on demand
+            Row w;
+            ldrow(X.sg.x + j * stride, true, w);
+            row(j, w);
+        }
+        // a static body (invM = 0, no rotation) is never written: pairs of
+        // one colour may share it
+        const int fl0 = X.r[0].fl;
+        if (hx && (X.iMA != 0.0 || (fl0 & 2))) { sp[3 * a] = xA; sp[3 * a + 1] = yA; sp[3 * a + 2] = tA; }
+        if (hx && (X.iMB != 0.0 || (fl0 & 4))) { sp[3 * b] = xB; sp[3 * b + 1] = yB; sp[3 * b + 2] = tB; }
+        if (p1.k == 0) {
+            lds_barrier();
+            PTR(1, p0.it * ncol + p0.c + 1);
+        }
+        p0 = p1; p1 = p2; p2 = adv(p2);
+    };
+    auto step = [&](Pf &X, Pf &Y, int2 sgY, int2 &sgZ) {
+        if (TL > 0 && __builtin_amdgcn_ballot_w64((X.sg.y & 0xff) > PF) != 0)
+            slot(std::true_type{}, X, Y, sgY, sgZ);
+        else
+            slot(std::false_type{}, X, Y, sgY, sgZ);
+    };
+    Pf bufA{}, bufB{};
+    int2 sgA = make_int2(0, 0), sgB = make_int2(0, 0);
     if (total > 0) {
-        const int q = scb[0] + threadIdx.x;
-        hcur = q < scb[1];
-        if (hcur) load(q, cur);
+        const int2 sg0 = seg_of(p0);
+        ldpair(sg0, bufA);
+#pragma unroll
+        for (int j = 0; j < PF; j++) ldrow_j(sg0, j, bufA.r[j]);
+        sgB = seg_of(p1);
     }
-    for (int step = 0, c = 0; step < total; step++) {
-        int c1 = c + 1 == ncol ? 0 : c + 1;
-        bool hnxt = false;
-        if (step + 1 < total) {
-            const int q = scb[c1] + threadIdx.x;
-            hnxt = q < scb[c1 + 1];
-            if (hnxt) load(q, nxt);
-        }
-        if (hcur) solve(cur);
-        for (int q = scb[c] + threadIdx.x + SOLVE_TPB; q < scb[c + 1]; q += SOLVE_TPB) {
-            Pf f;
-            load(q, f);
-            solve(f);
-        }
-        lds_barrier();
-        PTR(1, step + 1);
-        cur = nxt;
-        hcur = hnxt;
-        c = c1;
+    for (int s = 0; s < total; s += 2) {
+        step(bufA, bufB, sgB, sgA);
+        if (s + 1 < total) step(bufB, bufA, sgA, sgB);
     }
+    __syncthreads();
     // storeBodyData (:176-197)
     for (int i = threadIdx.x; i < nb; i += SOLVE_TPB) {
         if (!inPos[i]) continue;
@@ -2175,6 +2364,21 @@ static int colour_launch(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
 // bits in any of these arrangements.
 static size_t colour_lds_cap() { return 159 * 1024; }   // of a CU's 160 KB (the kernels use < 1 KB static)
 
+// the colour-order position rows, carved from posRec's allocation
+// (cap_contacts records of 88 bytes hold the arrays' 84 bytes a row)
+static PosRows pos_rows(RigidDev *d) {
+    static_assert(sizeof(PosRec) >= 4 * sizeof(double2) + sizeof(double) + sizeof(int2) + sizeof(int32_t),
+                  "position rows must fit in posRec");
+    const size_t K = (size_t)d->cap_contacts;
+    PosRows r;
+    double2 *base = (double2 *)d->posRec;
+    r.n = base; r.c = base + K; r.m = base + 2 * K; r.i = base + 3 * K;
+    r.py = (double *)(base + 4 * K);
+    r.ab = (int2 *)(r.py + K);
+    r.fl = (int32_t *)(r.ab + K);
+    return r;
+}
+
 static int colour_prep(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     const lpe_rigid_config &c = d->cfg;
     const int nb = d->nb, nc = d->last_nc;
@@ -2184,7 +2388,7 @@ static int colour_prep(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     LPE_KERNEL(ctx, "k_pgs_bodies", k_pgs_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->imii, 1);
     LPE_KERNEL(ctx, "k_pgs_rows", k_pgs_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->order, d->contacts, d->bodies, d->imii, d->rowN, d->rowR, d->rowAB, d->rowM, d->sItemA, d->sItemB);
     LPE_KERNEL(ctx, "k_pos_bodies", k_pos_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->posState);
-    LPE_KERNEL(ctx, "k_pos_fill_rows", k_pos_fill_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->order, d->contacts, d->bodies, d->posState, d->posRec, inPos, c.baumgarte, c.slop);
+    LPE_KERNEL(ctx, "k_pos_fill_rows", k_pos_fill_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->order, d->contacts, d->bodies, d->posState, pos_rows(d), inPos, c.baumgarte, c.slop);
     LPE_CHECK_LAUNCH(ctx, "solver preparation");
     return LPE_OK;
 }
@@ -2192,11 +2396,8 @@ static int colour_prep(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
 static int colour_pos(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     const lpe_rigid_config &c = d->cfg;
     const int nb = d->nb;
-    size_t lds2 = sizeof(double) * 3 * (size_t)nb;
-    const size_t ldsMax = colour_lds_cap();
-    int segLds2 = (int)std::min<size_t>((size_t)d->last_np, (ldsMax - std::min(ldsMax, lds2)) / sizeof(int2));
-    lds2 += sizeof(int2) * (size_t)segLds2;
-    LPE_KERNEL(ctx, "k_pos_colour", k_pos_colour, dim3(1), dim3(SOLVE_TPB), lds2, s, nb, d->counts, d->cbase, d->cseg, segLds2, d->posRec, d->bodies, d->posState, d->inContact + nb, c.posIterations);
+    const size_t lds2 = sizeof(double) * 3 * (size_t)nb;
+    LPE_KERNEL(ctx, "k_pos_colour", k_pos_colour, dim3(1), dim3(SOLVE_TPB), lds2, s, nb, d->counts, d->cbase, d->cseg, pos_rows(d), d->bodies, d->posState, d->inContact + nb, c.posIterations);
     LPE_CHECK_LAUNCH(ctx, "position solver");
     return LPE_OK;
 }
@@ -2205,11 +2406,8 @@ static int colour_pgs(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     const lpe_rigid_config &c = d->cfg;
     const int nb = d->nb;
     LPE_KERNEL(ctx, "k_pgs_bodies", k_pgs_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->imii, 2);
-    size_t lds = sizeof(float) * (3 * (size_t)nb + 1);
-    const size_t ldsMax = colour_lds_cap();
-    int segLds = (int)std::min<size_t>((size_t)d->last_np, (ldsMax - std::min(ldsMax, lds)) / sizeof(int2));
-    lds += sizeof(int2) * (size_t)segLds + 8;
-    LPE_KERNEL(ctx, "k_pgs_colour", k_pgs_colour, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts, d->cbase, d->cseg, segLds, d->rowN, d->rowR, d->rowAB, d->rowM, d->vel0, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF);
+    const size_t lds = sizeof(float) * 3 * (size_t)nb;
+    LPE_KERNEL(ctx, "k_pgs_colour", k_pgs_colour, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts, d->cbase, d->cseg, 0, d->rowN, d->rowR, d->rowAB, d->rowM, d->vel0, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF);
     LPE_KERNEL(ctx, "k_pgs_writeback", k_pgs_writeback, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->inContact);
     LPE_CHECK_LAUNCH(ctx, "pgs");
     return LPE_OK;
