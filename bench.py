@@ -221,12 +221,13 @@ def render_bench(ctx, U, reps=3):
 
 
 def loopback_check(args, lpe, scenes, slab, device):
-    """K slab ranks of MW{K} on one GPU through the in-process transport:
+    """K slab ranks of MW{K} (or of C5 with --scene C5) on one GPU through the in-process transport:
     exercises the sharded bench path (scene, slab set-up, world ticks with
     halo exchange and migration) where only one GPU is available.  Prints one
     JSON check line (not the metric: K ranks share one GPU)."""
     K = args.loopback
-    s = scenes.scene(f"MW{K}")
+    name = "C5" if args.scene == "C5" else f"MW{K}"
+    s = scenes.scene(name)
     fl = s["fluid"]
     bodies, verts = scenes.to_bodies(s["bodies"])
     edges = slab.slab_edges(fl["x"], K)
@@ -249,8 +250,10 @@ def loopback_check(args, lpe, scenes, slab, device):
     finally:
         for c in ctxs:
             c.close()
-    print(json.dumps({"check": "loopback", "ranks": K, "scene": f"MW{K}", "ticks": args.prep + args.warmup + args.steps,
-                      "seconds": round(el, 3), "owned": [len(p["x"]) for p in parts],
+    print(json.dumps({"check": "loopback", "ranks": K, "scene": name, "ticks": args.prep + args.warmup + args.steps,
+                      "seconds": round(el, 3), "ticks_per_s_all_ranks_on_one_gpu":
+                          round((args.prep + args.warmup + args.steps) / el, 2),
+                      "owned": [len(p["x"]) for p in parts],
                       "finite": bool(np.isfinite(merged["x"]).all() and np.isfinite(merged["vy"]).all()),
                       "rigid_replicas_identical": bool(same), "max_cell_occupancy_rank0": st["maxCellOccupancy"]}))
 
@@ -401,8 +404,9 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--scene", default="M")
-    ap.add_argument("--prep", type=int, default=3000,
-                    help="untimed ticks that settle the scene before warmup (the pile forms)")
+    ap.add_argument("--prep", type=int, default=None,
+                    help="untimed ticks that settle the scene before warmup (the pile forms); "
+                         "default 3000 for M, 240 for the fluid-only C5")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the >=2 s windows, one-tick calls, strict mode and the C1-C4 lines")
@@ -413,6 +417,8 @@ def main():
                     help="validation only: K slab ranks of MW{K} in this process on one GPU "
                          "(in-process transport); prints a check line, not the metric")
     args = ap.parse_args()
+    if args.prep is None:
+        args.prep = 240 if args.scene == "C5" else 3000
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -546,8 +552,10 @@ def main():
         roof_d = dict(kernel="k_density", achieved=round(bd / avg_d / 1e9, 1), unit="GB/s",
                       frac=round(bd / avg_d / 1e9 / HBM_PEAK_GBS, 4), avg_us=round(avg_d * 1e6, 2))
     # weak scaling: every rank advances one M-sized SPH slab (sharded) or one
-    # copy of the scene (replicas) per tick
-    value = world * args.steps / elapsed
+    # copy of the scene (replicas) per tick; strong scaling (C5, SURVEY.md
+    # §8(d)): the one fixed 2M-particle scene, split over the ranks
+    strong = args.scene == "C5" and not args.replicas
+    value = (1 if strong else world) * args.steps / elapsed
     line = {
         "metric": "physics steps/sec at 256k SPH + 4k rigids; 1/2/4/8 MI355X vs HBM roofline",
         "value": round(value, 2),
@@ -557,7 +565,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f32 (SPH), f64+f32 (rigid: fp64 geometry, fp32 PGS as the reference)",
         "data": "synthetic (seeded scene generator, SURVEY.md §8(d))",
@@ -601,7 +609,7 @@ def main():
         line["density_microbench"] = density_microbench(lpe, scenes, local)
         line["rigid_microbench"] = rigid_microbench(lpe, local)
         line["render_density"] = render
-    if world == 1 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline and args.scene == "M":
         line["cpu_baseline"] = cpu_baseline(args.scene, settled)
     print(json.dumps(line))
     if dist is not None:

@@ -22,7 +22,7 @@ def per_kernel(path, counter, last):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        m = re.match(r"(?:lpe::)?(\w+)", r["Kernel_Name"])
+        m = re.match(r"(?:void )?(?:lpe::)?(\w+)", r["Kernel_Name"])
         rows[m.group(1)].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
     out = {}
     for k, v in rows.items():
