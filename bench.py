@@ -163,11 +163,12 @@ def cpu_baseline(scene_name, state=None, budget_s=20.0):
 
 def density_microbench(lpe, scenes, device, side=4096, reps=5):
     """SURVEY.md §8(d) density microbench: a side x side lattice (16.7M
-    particles at side 4096) in a U = 104 m universe, one density pass from a
-    pre-built grid (lpe_sph_probe_density: hash of the current positions, then
-    the tick's own LDS-staged density kernel, neighbour lists included), timed
-    with HIP events on the library's stream; algorithmic bytes 24 B/particle +
-    8 B/cell (§8(d))."""
+    particles at side 4096) in a U = 104 m universe, one pure density pass
+    (computeDensity, no neighbour list) from a pre-built grid
+    (lpe_sph_probe_density: hash of the current positions, then
+    k_density_plan + k_density_pair, two particles per lane; avg_us is the SUM
+    of both launches), timed with HIP events on the library's stream;
+    algorithmic bytes 24 B/particle + 8 B/cell (§8(d))."""
     rng = np.random.default_rng(7)
     U = 104.0
     x0 = 0.5 * (U - side * scenes.LATTICE_S)
@@ -183,17 +184,21 @@ def density_microbench(lpe, scenes, device, side=4096, reps=5):
         ctx.timing_reset()
         for _ in range(reps):
             rho, _ = ctx.sph_probe_density()
-        t = ctx.timing_read().get("k_density")
+        tr = ctx.timing_read()
         ctx.timing(0)
         st = ctx.sph_stats()
     finally:
         ctx.close()
+    t = tr.get("k_density")
+    tp = tr.get("k_density_plan", (0.0, 0))       # the pass's per-tile staging plans (its own launch)
     n = side * side
     cells = st["gridDimX"] * st["gridDimY"]
-    avg_s = t[0] / max(t[1], 1) / 1e3
+    avg_s = (t[0] + tp[0]) / max(t[1], 1) / 1e3
     b = 24.0 * n + 8.0 * cells
     ach = b / avg_s / 1e9
     return dict(kernel="k_density", particles=n, cells=cells, avg_us=round(avg_s * 1e6, 1),
+                kernels_us={"k_density_plan": round(tp[0] / max(tp[1], 1) * 1e3, 1),
+                            "k_density": round(t[0] / max(t[1], 1) * 1e3, 1)},
                 algorithmic_bytes=b, achieved=round(ach, 1), unit="GB/s", peak=HBM_PEAK_GBS,
                 frac=round(ach / HBM_PEAK_GBS, 4), launches=t[1],
                 stage_fallback_blocks=st["stageFallback"] // max(reps, 1),

@@ -464,6 +464,45 @@ typedef struct lpe_render_params {
 int  lpe_render_density(lpe_ctx *ctx, const lpe_render_params *params, float *normalized,
                         float *max_out);
 
+/* ---- Barnes-Hut gravity ----------------------- */
+/* BarnesHutConfig (include/systems/barnes_hut.hpp:19-25) plus the
+ * SharedSystemConfig fields BarnesHutSystem::update reads: UniverseSizeMeters
+ * (root box, barnes_hut.cpp:110-112, :123-124), GravitationalSoftener (:261)
+ * and SimulatorConstants::RealG (:277). */
+typedef struct lpe_bh_config {
+    double theta;                 /* 0.5 */
+    double small_mass_threshold;  /* 1e3; <= 0 disables the early exit and the small-node skip */
+    double universe_size;         /* root box [0, U) x [0, U) */
+    double softener;              /* added as softener^2 to every distance^2 */
+    double G;                     /* 6.674e-11 (src/core/constants.cpp:8) */
+} lpe_bh_config;
+typedef struct lpe_bh_stats {
+    int32_t skipped;              /* 1: every mass below the threshold, nothing done (:55-71) */
+    int32_t inserted;             /* bodies inside the universe, inserted into the tree */
+    int32_t nodes;                /* quadtree nodes (the reference's nodePool_ use) */
+    int32_t depth;                /* deepest level an insert reached (root = 0) */
+} lpe_bh_stats;
+/* Safety cap on the tree depth (LPE_ERR_OVERFLOW past it).  fp64 never gets
+ * there: coincident bodies are dropped by the child's contains() test once the
+ * box is below their ulp (depth ~55 for coordinates ~10 in a 64 m universe),
+ * as in the reference. */
+#define LPE_BH_MAX_DEPTH 128
+int  lpe_bh_config_default(lpe_bh_config *cfg);
+/* The bodies: the entities of view<Position, Mass>(exclude<Boundary>) in that
+ * view's iteration order, which is buildTree's insertion order (:117-128);
+ * has_vel[i] != 0 where the entity also has a Velocity (bodyView, :89; NULL:
+ * all).  Host arrays, copied to the device. */
+int  lpe_bh_upload(lpe_ctx *ctx, int n, const double *x, const double *y, const double *vx,
+                   const double *vy, const double *mass, const uint8_t *has_vel);
+/* One BarnesHutSystem::update (barnes_hut.cpp:50-99) on the uploaded bodies:
+ * the small-mass early exit, the quadtree (same nodes, same centre-of-mass
+ * fold order as the sequential insertion) and the force walk of every body
+ * with a velocity, vel += a * dt in the reference's child order.
+ * dt = SecondsPerTick * baseTimeAcceleration * timeScale (:284).  stats may
+ * be NULL.  Blocks until done. */
+int  lpe_bh_step(lpe_ctx *ctx, const lpe_bh_config *cfg, double dt, lpe_bh_stats *stats);
+int  lpe_bh_download(lpe_ctx *ctx, double *vx, double *vy);
+
 #ifdef __cplusplus
 }
 #endif

@@ -95,6 +95,8 @@ struct SphDev {
     int diag = 0;                 // count the ST_NL_OVERFLOW / ST_RIGID_CAND / ST_NEIGH stats
     int mode = 0;                 // LPE_SPH_MODE_* (lpe_sph_set_mode)
     int32_t *refInv = nullptr;    // reference cell-capacity mode: sorted slot of each particle id
+    void *plans = nullptr;        // pure density pass: per-tile staging plans (lpe_sph.hip Hood)
+    size_t cap_plans = 0;
     struct Shard *shard = nullptr;// x-slab decomposition state (lpe_sph_set_slab), else single domain
 };
 
@@ -146,6 +148,7 @@ struct lpe_ctx {
     std::string err;
     lpe::SphDev sph;
     void *rigid = nullptr;  // lpe::RigidDev*, owned by lpe_rigid.hip
+    void *bh = nullptr;     // lpe::BhDev*, owned by lpe_bh.hip (Barnes-Hut)
     lpe::KernelTimer timer;
 };
 
@@ -212,3 +215,4 @@ int sph_alloc_rigids(lpe_ctx *ctx, int n);
 // state of lpe_sph_probe_* and of the renderer's density grid
 int lpe_sph_hash_current(lpe_ctx *ctx);
 int lpe_timer_destroy_internal(lpe_ctx *ctx);
+int lpe_bh_destroy_internal(lpe_ctx *ctx);

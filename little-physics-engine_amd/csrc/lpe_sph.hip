@@ -348,7 +348,7 @@ k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restric
                const int32_t *__restrict__ tmpId, const int32_t *__restrict__ tmpOld,
                PState P, KState K, PState S, float4 *__restrict__ nbA, float2 *__restrict__ nbB,
                int probe, const int32_t *__restrict__ nptr, int nown, int32_t *__restrict__ inv,
-               int32_t *__restrict__ owned, int32_t *__restrict__ refInv) {
+               int32_t *__restrict__ owned, int32_t *__restrict__ refInv, int W) {
     int s = blockIdx.x * TPB + threadIdx.x;
     if (s >= (nptr ? *nptr : n)) return;
     int o = tmpOld[s];
@@ -358,7 +358,10 @@ k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restric
     int rank = 0;
     for (int j = b; j < e; j++) rank += (tmpId[j] < myid) ? 1 : 0;
     int d = b + rank;
-    nbA[d] = make_float4(K.x[o], K.y[o], P.m[o], 0.f);
+    // .w: the bin's (cell row - oy) << 17 | (cell column - ox) << 2 | quadrant
+    // (the density pass reads a slot's cell and quadrant row from it)
+    const uint32_t cl = k >> 2, cyr = cl / (uint32_t)W, cxr = cl - cyr * (uint32_t)W;
+    nbA[d] = make_float4(K.x[o], K.y[o], P.m[o], __int_as_float((int)((cyr << 17) | (cxr << 2) | (k & 3))));
     nbB[2 * d] = make_float2(P.vx[o], P.vy[o]);
     S.id[d] = myid;
     if (refInv) refInv[myid] = d;         // reference cell-capacity mode: id -> sorted slot
@@ -586,7 +589,7 @@ struct Hood {
 // the plan for slots [s0, s1) (s1 > s0); cells of the device grid [ox, ox+W) x [oy, oy+H)
 __device__ __forceinline__ void hood_plan(Hood &hd, int s0, int s1, const float4 *__restrict__ nbA, float eps,
                                           float cs, int W, int H, int ox, int oy,
-                                          const int32_t *__restrict__ start) {
+                                          const int32_t *__restrict__ start, int cap = HCAP, int bcap = HBND) {
     const float4 f = nbA[s0], l = nbA[s1 - 1];
     int cx0, cy0, cx1, cy1;
     cell_xy(f.x, f.y, eps, cs, cx0, cy0);
@@ -632,7 +635,7 @@ __device__ __forceinline__ void hood_plan(Hood &hd, int s0, int s1, const float4
     }
     hd.L = L;
     hd.NB = NB;
-    hd.ok = L <= HCAP && NB <= HBND;
+    hd.ok = L <= cap && NB <= bcap;
 }
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -647,13 +650,14 @@ typedef __attribute__((address_space(1))) const void glb_void_t;
 // block is in flight at once; the caller's __syncthreads() retires them.
 // (Per-segment chunks of 64 instead of the flat index: fewer VALU per load
 // but three times the SALU, measured slower.)
+template <int NT = HB, int CAP = HCAP, int BCAP = HBND>
 __device__ __forceinline__ void hood_stage(const Hood &hd, float4 *lrec, int *lbnd,
                                            const float4 *__restrict__ nbA,
                                            const int32_t *__restrict__ start, int s0) {
     const int wbase = threadIdx.x & ~63;
 #pragma unroll
-    for (int u = 0; u < HCAP / HB; u++) {
-        const int f0 = u * HB;
+    for (int u = 0; u < CAP / NT; u++) {
+        const int f0 = u * NT;
         if (f0 >= hd.L) break;
         const int f = f0 + threadIdx.x;
         int d = hd.ss[0] - hd.l[0];
@@ -664,8 +668,8 @@ __device__ __forceinline__ void hood_stage(const Hood &hd, float4 *lrec, int *lb
         __builtin_amdgcn_global_load_lds((glb_void_t *)(nbA + src), (lds_void_t *)(lrec + f0 + wbase), 16, 0, 0);
     }
 #pragma unroll
-    for (int u = 0; u < HBND / HB; u++) {
-        const int f0 = u * HB;
+    for (int u = 0; u < BCAP / NT; u++) {
+        const int f0 = u * NT;
         if (f0 >= hd.NB) break;
         const int f = f0 + threadIdx.x;
         int d = hd.g0[0] - hd.bb[0];
@@ -880,6 +884,237 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     pr[s] = pres;
     nbB[2 * s + 1] = make_float2(acc, pres / (acc * acc));   // the p_j / rho_j^2 of metal:370
 }
+
+// ---------------------------------------------------------------------------
+// Pure density pass with two particles per lane (lpe_sph_probe_density and
+// the density microbench: computeDensity, metal:246-307, without the
+// forces pass's neighbour list).  A block of DT_NT threads owns DT_TILE =
+// 2 DT_NT consecutive sorted slots and stages their neighbourhood once
+// (hood_plan / hood_stage, as k_density); lane t takes slots s0 + 2t and
+// s0 + 2t + 1.  The pair walks ONE set of row spans: per cell row, the union
+// of its two particles' spans.  A superset of a particle's canonical walk, in
+// canonical order, leaves its sum unchanged bit for bit: the extra candidates
+// lie beyond h * 1.002 in x or y (skipped quadrants, later or earlier cells
+// of the row), so max(h^2 - r^2, 0) = +0, m * +0 = +0 and acc + 0 = acc.  So
+// every LDS record read serves both particles, and the two sums advance in
+// one packed fp32 pipe (v_pk_add_f32 / v_pk_mul_f32 round lane-wise exactly
+// like the scalar ops; no FMA contraction).  A pair that straddles the tile's
+// two row runs walks its particles one after the other, the other one parked
+// at +inf (r^2 = inf: its terms are +0).
+static constexpr int DT_NT = 256;
+static constexpr int DT_TILE = 2 * DT_NT;
+static constexpr int DT_CAP = 2048;       // records staged per tile (32 KB of LDS)
+static constexpr int DT_BND = 1536;       // cell boundaries staged per tile (6 KB)
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// one canonical pass over <= 3 row spans for the lane's two particles
+// (X, Y): four records per trip, trip counts wave-uniform (unmasked up to the
+// wave's shortest span, masked - mass forced to +0 - up to its longest)
+__device__ __forceinline__ void pair_pass(int sb[3], int se[3], const float4 *lrec, f2v X, f2v Y, float h2,
+                                          float poly6, f2v &acc) {
+#pragma unroll
+    for (int pass = 0; pass < 2; pass++)
+#pragma unroll
+        for (int r = 0; r < 2; r++)
+            if (se[r] == sb[r]) {
+                sb[r] = sb[r + 1]; se[r] = se[r + 1];
+                sb[r + 1] = se[r + 1] = 0;
+            }
+    const f2v H2 = {h2, h2}, P6 = {poly6, poly6}, Z = {0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 3; r++) {
+        const int b = sb[r], len = se[r] - b;
+        int lmin, lmax;
+        wave_minmax(len, lmin, lmax);
+        if (lmax == 0) break;
+        auto trip = [&](int t, bool masked) {
+            const int a = min(b + t, DT_CAP);
+            float4 o[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) o[j] = lrec[a + j];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const float m = (!masked || t + j < len) ? o[j].z : 0.0f;
+                const f2v dx = X - o[j].x, dy = Y - o[j].y;
+                const f2v r2 = dx * dx + dy * dy;
+                const f2v diff = __builtin_elementwise_max(H2 - r2, Z);
+                const f2v w = P6 * diff * diff * diff;
+                acc += m * w;
+            }
+        };
+        int t = 0;
+        for (; t + 4 <= lmin; t += 4) trip(t, false);
+        for (; t < lmax; t += 4) trip(t, true);
+    }
+}
+
+// The lane's two slots of tile [s0, s1) (staged in lrec / lbnd per hd):
+// their densities, or the global walk when the neighbourhood did not fit
+__device__ __forceinline__ f2v pair_tile(const Hood &hd, const float4 *lrec, const int *lbnd, int s0, int s1,
+                                         int pair, float h, float eps, const GridParams &g, int W, int H, int ox, int oy,
+                                         const int32_t *__restrict__ start, const float4 *__restrict__ nbA,
+                                         int32_t *__restrict__ status) {
+    const float cs = g.cellSize;
+    const int sa = s0 + 2 * pair, sb = sa + 1;
+    const bool la = sa < s1, lv = sb < s1;
+    const float4 pa = nbA[la ? sa : s1 - 1];
+    const float4 pb = nbA[lv ? sb : s1 - 1];
+    const float h2 = h * h;
+    const float poly6 = poly6Coeff2D(h);
+    const float reach = walk_reach(h, cs);
+    const float INF = __builtin_inff();
+    f2v acc = {0.0f, 0.0f};
+    if (hd.ok) {
+        const int cya = oy + (int)((unsigned)__float_as_int(pa.w) >> 17);   // the bin's cell row (k_rank_permute)
+        const int cyb = oy + (int)((unsigned)__float_as_int(pb.w) >> 17);
+        int Ab[3], Ae[3], Bb[3], Be[3], sh[3];
+        hood_spans(hd, lbnd, pa.x, pa.y, eps, cs, reach, cya, g, Ab, Ae, sh);
+        hood_spans(hd, lbnd, pb.x, pb.y, eps, cs, reach, cyb, g, Bb, Be, sh);
+        const bool strad = la && lv && cya != cyb;           // one pair per tile at most
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            if (!la) Ab[r] = Ae[r] = 0;
+            if (!lv) Bb[r] = Be[r] = 0;
+        }
+        int Pb[3], Pe[3];
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            const bool ea = Ae[r] == Ab[r], eb = Be[r] == Bb[r];
+            if (strad) {
+                Pb[r] = Ab[r]; Pe[r] = Ae[r];
+            } else {
+                Pb[r] = ea ? Bb[r] : (eb ? Ab[r] : min(Ab[r], Bb[r]));
+                Pe[r] = ea ? Be[r] : (eb ? Ae[r] : max(Ae[r], Be[r]));
+            }
+        }
+        const f2v X = {pa.x, strad ? INF : pb.x}, Y = {pa.y, pb.y};
+        pair_pass(Pb, Pe, lrec, X, Y, h2, poly6, acc);
+        if (__any(strad)) {
+#pragma unroll
+            for (int r = 0; r < 3; r++) {
+                Pb[r] = strad ? Bb[r] : 0;
+                Pe[r] = strad ? Be[r] : 0;
+            }
+            const f2v X2 = {INF, pb.x};
+            pair_pass(Pb, Pe, lrec, X2, Y, h2, poly6, acc);
+        }
+    } else {
+        if (threadIdx.x == 0) atomicAdd(&status[ST_STAGE_FALLBACK], 1);
+        auto one = [&](const float4 &me, float &out) {
+            walk_neighbours<4>(me.x, me.y, eps, cs, reach, g, W, H, ox, oy, start,
+                               [&](int k, int) { return nbA[k]; },
+                               [&](int, const float4 &o) {
+                                   const float dx = me.x - o.x, dy = me.y - o.y;
+                                   const float r2 = dx * dx + dy * dy;
+                                   const float diff = fmaxf(h2 - r2, 0.0f);
+                                   out += o.z * (poly6 * diff * diff * diff);
+                               });
+        };
+        float ra = 0.0f, rb = 0.0f;
+        if (la) one(pa, ra);
+        if (lv) one(pb, rb);
+        acc = f2v{ra, rb};
+    }
+    return acc;
+}
+
+// density / pressure / nbB write-back of one slot (metal:299-306)
+__device__ __forceinline__ void density_out(int s, float a, float stiffness, float restDensity,
+                                            float *__restrict__ rho, float *__restrict__ pr,
+                                            float2 *__restrict__ nbB) {
+    float pres = stiffness * (a - restDensity);
+    if (pres < 0.f) pres = 0.f;
+    rho[s] = a;
+    pr[s] = pres;
+    nbB[2 * s + 1] = make_float2(a, pres / (a * a));   // the p_j / rho_j^2 of metal:370
+}
+
+// A plan (sizeof(Hood) bytes) copied global -> LDS by wave 0, asynchronously
+// (global_load_lds, one dword per lane; retired by the next barrier)
+static constexpr int HOOD_WORDS = (int)(sizeof(Hood) / 4);
+static_assert(sizeof(Hood) % 4 == 0 && HOOD_WORDS <= 64, "a plan is at most one wave of dwords");
+__device__ __forceinline__ void hood_fetch(const Hood *__restrict__ plans, int t, int *dst) {
+    if (threadIdx.x < HOOD_WORDS) {
+        const int *src = reinterpret_cast<const int *>(plans + t) + threadIdx.x;
+        __builtin_amdgcn_global_load_lds((glb_void_t *)src, (lds_void_t *)dst, 4, 0, 0);
+    }
+}
+
+// One tile per block.  The tile's staging plan comes precomputed
+// (k_density_plan, fetched into LDS by wave 0) instead of being derived by
+// every lane.  Lanes are grouped by the quadrant row of their pair's first
+// particle (upper quadrants first): a pair's span lengths depend mostly on
+// which q-row of its cell it sits in (one q-row of the row above vs of the
+// row below), so grouping them keeps a wave's lanes on equal trip counts
+// (fewer masked trips).  Results go to the pair's own slots, so the lane
+// order changes nothing in the sums.
+__global__ void __launch_bounds__(DT_NT)
+k_density_pair(int n, const int32_t *__restrict__ nptr, float h, float eps, float stiffness, float restDensity,
+               int W, int H, int ox, int oy, const GridParams *__restrict__ gp, const int32_t *__restrict__ start,
+               const float4 *__restrict__ nbA, float2 *__restrict__ nbB, float *__restrict__ rho,
+               float *__restrict__ pr, int32_t *__restrict__ status, const Hood *__restrict__ plans) {
+    __shared__ float4 lrec[DT_CAP + 4];                   // + 4: a trip reads up to 3 past a span
+    __shared__ int lbnd[DT_BND];
+    __shared__ int hraw[64];
+    __shared__ int nup[DT_NT / 64];
+    const int lb = xcd_block((n + DT_TILE - 1) / DT_TILE);
+    if (lb < 0) return;
+    const int nn = nptr ? *nptr : n;
+    const int s0 = lb * DT_TILE, s1 = min(s0 + DT_TILE, nn);
+    if (s0 >= s1) return;
+    const GridParams g = *gp;
+    hood_fetch(plans, lb, hraw);
+    // the pair's quadrant row: bit 1 of the bin's quadrant (nbA.w, k_rank_permute)
+    const int sp = s0 + 2 * (int)threadIdx.x;
+    const int up = (sp < s1) ? ((__float_as_int(nbA[sp].w) & 2) ? 0 : 1) : 0;
+    const unsigned long long bal = __ballot(up);
+    const int lane = (int)threadIdx.x & 63, wv = (int)threadIdx.x >> 6;
+    const int below = __popcll(bal & ((1ull << lane) - 1));
+    if (lane == 0) nup[wv] = __popcll(bal);
+    __syncthreads();                                      // the plan, nup
+    const Hood &hd = *reinterpret_cast<const Hood *>(hraw);
+    if (hd.ok) hood_stage<DT_NT, DT_CAP, DT_BND>(hd, lrec, lbnd, nbA, start, s0);
+    int ubefore = 0, utot = 0;
+#pragma unroll
+    for (int w = 0; w < DT_NT / 64; w++) {
+        ubefore += (w < wv) ? nup[w] : 0;
+        utot += nup[w];
+    }
+    // lane position of this pair: upper pairs first, each group in tile order
+    const int pos = up ? (ubefore + below) : (utot + (wv * 64 + lane - ubefore - below));
+    __shared__ short perm[DT_NT];
+    perm[pos] = (short)threadIdx.x;
+    __syncthreads();                                      // staged records, perm
+    const int pair = perm[threadIdx.x];
+    const f2v acc = pair_tile(hd, lrec, lbnd, s0, s1, pair, h, eps, g, W, H, ox, oy, start, nbA, status);
+    const int sa = s0 + 2 * pair;
+    if (sa < s1) density_out(sa, acc.x, stiffness, restDensity, rho, pr, nbB);
+    if (sa + 1 < s1) density_out(sa + 1, acc.y, stiffness, restDensity, rho, pr, nbB);
+}
+
+// The tiles' staging plans, one thread per tile (the persistent pass reads
+// them a tile ahead instead of computing them between its walks).  nrun = -1:
+// an empty tile (the sharded slot count ended before it).
+__global__ void __launch_bounds__(TPB)
+k_density_plan(int n, const int32_t *__restrict__ nptr, float eps, int W, int H, int ox, int oy,
+               const GridParams *__restrict__ gp, const int32_t *__restrict__ start,
+               const float4 *__restrict__ nbA, Hood *__restrict__ plans) {
+    const int t = blockIdx.x * TPB + threadIdx.x;
+    if (t >= (n + DT_TILE - 1) / DT_TILE) return;
+    const int nn = nptr ? *nptr : n;
+    const int s0 = t * DT_TILE, s1 = min(s0 + DT_TILE, nn);
+    Hood p;
+    if (s0 >= s1) {
+        p.ok = false;
+        p.nrun = -1;
+    } else {
+        hood_plan(p, s0, s1, nbA, eps, gp->cellSize, W, H, ox, oy, start, DT_CAP, DT_BND);
+        if (!p.ok) p.nrun = 0;                            // (left unset on the >2-run early out)
+    }
+    plans[t] = p;
+}
+
 
 struct SphStepParams {
     const int32_t *nptr;      // slab decomposition: device slot count (owned + ghosts), else null
@@ -1533,7 +1768,7 @@ static void sph_free(SphDev &d) {
     pstate_free(d.S);
     void *ptrs[] = {d.rho, d.pr, d.rhoN, d.prN, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.refInv, d.stage, d.count, d.start, d.cursor,
                     d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.raabb, d.accum, d.acq, d.rbinStart, d.rgrid, d.rmax,
-                    d.rbinList, d.rbinCount, d.coupleBody};
+                    d.rbinList, d.rbinCount, d.coupleBody, d.plans};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     hipEvent_t evs[] = {d.preReady, d.preDone};
     for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
@@ -1577,6 +1812,7 @@ extern "C" int lpe_destroy(lpe_ctx *ctx) {
     delete ctx->transport;
     ctx->transport = nullptr;
     lpe_rigid_destroy_internal(ctx);
+    lpe_bh_destroy_internal(ctx);
     lpe_timer_destroy_internal(ctx);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -1969,7 +2205,7 @@ static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool pr
                        d.tmpId, d.tmpOld, (const int32_t *)nullptr);
     LPE_KERNEL(ctx, "k_rank_permute", k_rank_permute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.start,
                        d.tmpId, d.tmpOld, d.P, sph_kstate(d), d.S, d.nbA, (float2 *)d.nbB, probe ? 1 : 0,
-                       (const int32_t *)nullptr, 0, (int32_t *)nullptr, (int32_t *)nullptr, sph_ref_inv(d));
+                       (const int32_t *)nullptr, 0, (int32_t *)nullptr, (int32_t *)nullptr, sph_ref_inv(d), d.W);
     LPE_CHECK_LAUNCH(ctx, "hash");
     return LPE_OK;
 }
@@ -1977,10 +2213,38 @@ static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool pr
 // density over n slots (nptr: device count of the sharded sub-step); nl:
 // also the neighbour lists of the forces pass (the tick), else density only
 // (the probe / microbench)
+static int sph_cu_count(lpe_ctx *ctx) {
+    static int cus = 0;
+    if (!cus) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || v <= 0)
+            v = 256;
+        cus = v;
+    }
+    return cus;
+}
+
 static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr, float *rho, float *pr, bool nl = true) {
     SphDev &d = ctx->sph;
     const lpe_fluid_config &c = d.cfg;
-    if (nl)
+    static const bool v1 = getenv("LPE_DENSITY_V1") != nullptr;   // A/B switch: the one-particle-per-lane pass
+    const int ntiles = (n + DT_TILE - 1) / DT_TILE;
+    if (!nl && !v1 && !sph_ref_inv(d)) {
+        if ((size_t)ntiles > d.cap_plans) {
+            if (d.plans) (void)hipFree(d.plans);
+            d.plans = nullptr;
+            d.cap_plans = 0;
+            LPE_HIP(ctx, hipMalloc(&d.plans, sizeof(Hood) * (size_t)ntiles));
+            d.cap_plans = (size_t)ntiles;
+        }
+        LPE_KERNEL(ctx, "k_density_plan", k_density_plan, dim3(nblk(ntiles)), dim3(TPB), 0, ctx->stream, n, nptr,
+                   c.gridConfig.gridEpsilon, d.W, d.H, d.ox, d.oy, d.gp_cur, d.start, d.nbA, (Hood *)d.plans);
+        LPE_KERNEL(ctx, "k_density", k_density_pair, dim3(xcd_grid(ntiles)), dim3(DT_NT), 0, ctx->stream, n, nptr,
+                   c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness, c.restDensity, d.W, d.H,
+                   d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)d.nbB, rho, pr, d.stat_cur,
+                   (const Hood *)d.plans);
+    }
+    else if (nl)
         LPE_KERNEL(ctx, "k_density", k_density<true>, dim3(xcd_grid(nblk(n, HB))), dim3(HB), 0, ctx->stream, n,
                    nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
                    c.restDensity, d.W, d.H, d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)d.nbB,
@@ -2037,7 +2301,7 @@ static int sph_hash_shard(lpe_ctx *ctx, float subDt, float halfDt, bool first) {
     LPE_KERNEL(ctx, "k_rank_permute", k_rank_permute, dim3(nblk1(ncap)), dim3(TPB), 0, s, ncap, d.key, d.start,
                d.tmpId, d.tmpOld, d.P, sph_kstate(d), d.S, d.nbA, (float2 *)d.nbB, 0, (const int32_t *)h.ntot, d.n,
                h.inv, h.owned,
-               (int32_t *)nullptr);
+               (int32_t *)nullptr, d.W);
     LPE_CHECK_LAUNCH(ctx, "shard hash");
     return LPE_OK;
 }

@@ -9,7 +9,7 @@ namespace lpe {
 // bottleneck and the events then time the device idling between launches)
 bool KernelTimer::wants(const char *name) const {
     if (on == 1) return true;
-    static const char *hot[] = {"k_density", "k_forces_couple", "k_pgs_flow", "k_pos_flow", "k_pair_colour",
+    static const char *hot[] = {"k_density", "k_density_plan", "k_forces_couple", "k_pgs_flow", "k_pos_flow", "k_pair_colour",
                                 "k_narrow", "k_bg_pairs"};
     for (const char *h : hot)
         if (std::strcmp(h, name) == 0) return true;

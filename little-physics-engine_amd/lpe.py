@@ -213,6 +213,37 @@ class RenderParams(C.Structure):
 
 SIGNATURES["lpe_render_density"] = ([C.c_void_p, C.POINTER(RenderParams), _FP, _FP], C.c_int)
 
+class BhConfig(C.Structure):
+    """lpe_bh_config: BarnesHutConfig (barnes_hut.hpp:19-25) + the shared fields it reads."""
+    _fields_ = [("theta", C.c_double), ("small_mass_threshold", C.c_double), ("universe_size", C.c_double),
+                ("softener", C.c_double), ("G", C.c_double)]
+
+
+class BhStats(C.Structure):
+    _fields_ = [("skipped", C.c_int32), ("inserted", C.c_int32), ("nodes", C.c_int32), ("depth", C.c_int32)]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+_DP = C.POINTER(C.c_double)
+SIGNATURES["lpe_bh_config_default"] = ([C.POINTER(BhConfig)], C.c_int)
+SIGNATURES["lpe_bh_upload"] = ([C.c_void_p, C.c_int] + [_DP] * 5 + [C.c_void_p], C.c_int)
+SIGNATURES["lpe_bh_step"] = ([C.c_void_p, C.POINTER(BhConfig), C.c_double, C.POINTER(BhStats)], C.c_int)
+SIGNATURES["lpe_bh_download"] = ([C.c_void_p, _DP, _DP], C.c_int)
+
+
+def bh_config(universe: float, theta: float = 0.5, small_mass_threshold: float = 1e3,
+              softener: float = 0.0) -> BhConfig:
+    cfg = BhConfig()
+    lib().lpe_bh_config_default(C.byref(cfg))
+    cfg.universe_size = universe
+    cfg.theta = theta
+    cfg.small_mass_threshold = small_mass_threshold
+    cfg.softener = softener
+    return cfg
+
+
 SYS_BOUNDARY, SYS_GRAVITY, SYS_ROTATION, SYS_MOVEMENT, SYS_SLEEP = 1, 2, 4, 8, 16
 SPH_MODE_REF_CELL_CAP = 1       # LPE_SPH_MODE_REF_CELL_CAP (include/lpe.h)
 
@@ -510,3 +541,26 @@ class Context:
         p = np.empty(self.n, np.float32)
         self._chk(lib().lpe_sph_probe_density(self._h, _fp(rho), _fp(p)), "lpe_sph_probe_density")
         return rho, p
+
+    # ---- Barnes-Hut (lpe_bh_*) ----
+    def bh_upload(self, x, y, vx, vy, m, has_vel=None):
+        """Bodies in buildTree's insertion order (barnes_hut.cpp:117-128)."""
+        a = [np.ascontiguousarray(v, np.float64) for v in (x, y, vx, vy, m)]
+        hv = None if has_vel is None else np.ascontiguousarray(has_vel, np.uint8)
+        self._bh_keep = (a, hv)
+        self.nbh = len(a[0])
+        dp = [v.ctypes.data_as(_DP) for v in a]
+        self._chk(lib().lpe_bh_upload(self._h, self.nbh, *dp, None if hv is None else hv.ctypes.data),
+                  "lpe_bh_upload")
+
+    def bh_step(self, cfg: "BhConfig", dt: float) -> dict:
+        st = BhStats()
+        self._chk(lib().lpe_bh_step(self._h, C.byref(cfg), float(dt), C.byref(st)), "lpe_bh_step")
+        return st.as_dict()
+
+    def bh_download(self):
+        vx = np.zeros(self.nbh, np.float64)
+        vy = np.zeros(self.nbh, np.float64)
+        self._chk(lib().lpe_bh_download(self._h, vx.ctypes.data_as(_DP), vy.ctypes.data_as(_DP)),
+                  "lpe_bh_download")
+        return vx, vy

@@ -371,3 +371,50 @@ def particles_aos(fl) -> np.ndarray:
     p[:, 11] = fl["density"].astype(np.float32)
     p[:, 12] = fl["pressure"].astype(np.float32)
     return p
+
+
+# ---------------------------------------------------------------------------
+# Barnes-Hut scenes.  The reference's BH scenario is
+# KeplerianDiskScenario (src/scenarios/keplerian_disk.cpp:16-31, :45-140,
+# include/scenarios/keplerian_disk.hpp:15-42): a 1e36 kg central body at the
+# centre of a U = 600 px * 1e7 m/px universe, disk bodies between 100 px and
+# 240 px (ScreenLength / outerRadiusFactor) with ~1e22 kg masses falling off as
+# (r_min / r)^0.5 and Keplerian speeds, softener 2e7 m.  Seeded synthetic
+# version (the reference seeds with time(nullptr)); `n` bodies in total.
+BH_MPP = 1e7
+BH_U = 600 * BH_MPP
+BH_SOFT = 2e7
+BH_G = 6.674e-11
+
+
+def bh_disk(n: int = 1000, seed: int = 11, central_mass: float = 1e36, thin: float = 0.02):
+    rng = np.random.default_rng(seed)
+    cx = cy = 0.5 * BH_U
+    rmin, rmax = 100 * BH_MPP, 240 * BH_MPP
+    k = n - 1
+    r = rmin + (rmax - rmin) * np.sqrt(rng.random(k))
+    ang = rng.random(k) * 2 * math.pi
+    x = cx + r * np.cos(ang)
+    y = cy + r * np.sin(ang) + rng.normal(0.0, thin * r)
+    speed = np.sqrt(BH_G * central_mass / r) * rng.normal(1.0, 0.01, k)
+    vx = -speed * np.sin(ang)
+    vy = speed * np.cos(ang)
+    m = rng.normal((rmin / r) ** 0.5 * 1e22, 1e21)
+    return dict(x=np.concatenate([[cx], x]), y=np.concatenate([[cy], y]),
+                vx=np.concatenate([[0.0], vx]), vy=np.concatenate([[0.0], vy]),
+                m=np.concatenate([[central_mass], m]), U=BH_U, softener=BH_SOFT)
+
+
+def bh_clustered(n: int = 4096, seed: int = 3, U: float = 1.0e6):
+    """Gaussian clusters (deep, unbalanced subtrees), a few bodies outside
+    [0, U) (not inserted, still attracted), masses spanning the small-mass
+    threshold (1e3) so that all-small nodes are skipped."""
+    rng = np.random.default_rng(seed)
+    centres = rng.random((8, 2)) * U
+    c = rng.integers(0, 8, n)
+    pts = centres[c] + rng.normal(0.0, U * 0.01, (n, 2)) * rng.choice([1.0, 0.05], (n, 1))
+    pts[: max(1, n // 200)] = rng.random((max(1, n // 200), 2)) * U * 1.5 - 0.25 * U
+    m = 10.0 ** rng.uniform(1.0, 9.0, n)
+    v = rng.normal(0.0, 1.0, (n, 2))
+    return dict(x=pts[:, 0].copy(), y=pts[:, 1].copy(), vx=v[:, 0].copy(), vy=v[:, 1].copy(), m=m, U=U,
+                softener=0.0)

@@ -309,6 +309,45 @@ def ref_rigid_ticks(cfg, bodies, verts, nticks, dt):
                 contacts=cs[:nc.value].copy(), pgs_order=order[:nc.value].copy())
 
 
+def bh_step(cfg, x, y, vx, vy, m, dt, has_vel=None):
+    """oracle/bh_oracle.c: one BarnesHutSystem::update; returns (vx, vy, stats)."""
+    L = lib()
+    f = L.lpeo_bh_step
+    f.argtypes = [C.POINTER(lpe.BhConfig), C.c_int] + [C.c_void_p] * 6 + [C.c_double, C.POINTER(lpe.BhStats)]
+    f.restype = C.c_int
+    a = [np.ascontiguousarray(v, np.float64) for v in (x, y, m)]
+    wx = np.array(vx, np.float64, copy=True)
+    wy = np.array(vy, np.float64, copy=True)
+    hv = None if has_vel is None else np.ascontiguousarray(has_vel, np.uint8)
+    st = lpe.BhStats()
+    rc = f(C.byref(cfg), len(a[0]), a[0].ctypes.data, a[1].ctypes.data, wx.ctypes.data, wy.ctypes.data,
+           a[2].ctypes.data, None if hv is None else hv.ctypes.data, float(dt), C.byref(st))
+    if rc != 0:
+        raise RuntimeError("lpeo_bh_step: tree deeper than LPE_BH_MAX_DEPTH")
+    return wx, wy, st.as_dict()
+
+
+def ref_barnes_hut(cfg, x, y, vx, vy, m, spt, bta=1.0, ts=1.0, has_vel=None):
+    """The reference's BarnesHutSystem::update (oracle/_ref); bodies created in
+    array order.  Returns (vx, vy, order): order = body indices in the
+    insertion order of buildTree (view<Position, Mass> iteration)."""
+    C.CDLL(LIB_PATH, mode=C.RTLD_GLOBAL)
+    L = C.CDLL(REF_PATH)
+    f = L.lpref_barnes_hut
+    f.argtypes = [C.c_double] * 7 + [C.c_int] + [C.c_void_p] * 7
+    f.restype = C.c_int
+    a = [np.ascontiguousarray(v, np.float64) for v in (x, y, m)]
+    n = len(a[0])
+    wx = np.array(vx, np.float64, copy=True)
+    wy = np.array(vy, np.float64, copy=True)
+    hv = None if has_vel is None else np.ascontiguousarray(has_vel, np.uint8)
+    order = np.zeros(n, np.int32)
+    f(cfg.theta, cfg.small_mass_threshold, cfg.universe_size, cfg.softener, float(spt), float(bta), float(ts),
+      n, a[0].ctypes.data, a[1].ctypes.data, wx.ctypes.data, wy.ctypes.data, a[2].ctypes.data,
+      None if hv is None else hv.ctypes.data, order.ctypes.data)
+    return wx, wy, order
+
+
 def world_tick(fcfg, rcfg, particles, bodies, verts, couple, dt, nticks=1):
     """lpeo_world_tick: full ticks with fluid + bodies (canonical orders)."""
     L = _rigid_lib()

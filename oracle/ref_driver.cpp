@@ -23,6 +23,7 @@
 #include "entities/entity_components.hpp"
 #include "entities/sim_components.hpp"
 #include "math/polygon.hpp"
+#include "systems/barnes_hut.hpp"
 #include "systems/boundary.hpp"
 #include "systems/gravity.hpp"
 #include "systems/movement.hpp"
@@ -224,5 +225,59 @@ extern "C" int lpref_rigid_ticks(const lpe_rigid_config *cfg, double spt, double
         sleep.update(s.reg);
     }
     extract(s, nb, tmpl.data(), bodies);
+    return 0;
+}
+
+/* BarnesHutSystem::update (src/systems/barnes_hut.cpp:50-99), the reference's
+ * own code, on n bodies with Position + Mass (+ Velocity where has_vel[i]):
+ * vx/vy updated in place (body index order); order_out[k] = the body index of
+ * the k-th entity of view<Position, Mass>(exclude<Boundary>), buildTree's
+ * insertion order (:117-128), which the oracle and the device take as their
+ * input order.  Returns 0. */
+extern "C" int lpref_barnes_hut(double theta, double small_mass, double universe, double softener,
+                                double spt, double bta, double ts, int n, const double *x,
+                                const double *y, double *vx, double *vy, const double *m,
+                                const unsigned char *has_vel, int32_t *order_out) {
+    entt::registry reg;
+    auto st = reg.create();
+    reg.emplace<Components::SimulatorState>(st, bta, ts);
+    std::vector<entt::entity> ents(n);
+    for (int i = 0; i < n; i++) {
+        auto e = reg.create();
+        ents[i] = e;
+        reg.emplace<Components::Position>(e, x[i], y[i]);
+        if (!has_vel || has_vel[i]) reg.emplace<Components::Velocity>(e, vx[i], vy[i]);
+        reg.emplace<Components::Mass>(e, m[i]);
+    }
+    auto body_index = [&](entt::entity e) {
+        for (int i = 0; i < n; i++) if (ents[i] == e) return i;
+        return -1;
+    };
+    int k = 0;
+    for (auto e : reg.view<Components::Position, Components::Mass>(entt::exclude<Components::Boundary>))
+        order_out[k++] = body_index(e);
+    SharedSystemConfig sh{};
+    sh.UniverseSizeMeters = universe;
+    sh.SecondsPerTick = spt;
+    sh.GravitationalSoftener = softener;
+    sh.TimeAcceleration = 1.0;
+    sh.MetersPerPixel = 1.0;
+    sh.DragCoeff = 0.0;
+    sh.ParticleDensity = 0.0;
+    sh.GridSize = 50;
+    sh.CellSizePixels = 12.0;
+    Systems::BarnesHutSystem bh;
+    Systems::BarnesHutConfig bc;
+    bc.theta = theta;
+    bc.smallMassThreshold = small_mass;
+    bh.setSpecificConfig(bc);
+    bh.setSharedSystemConfig(sh);
+    bh.update(reg);
+    for (int i = 0; i < n; i++)
+        if (!has_vel || has_vel[i]) {
+            const auto &v = reg.get<Components::Velocity>(ents[i]);
+            vx[i] = v.x;
+            vy[i] = v.y;
+        }
     return 0;
 }

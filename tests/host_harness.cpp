@@ -21,6 +21,7 @@
 #include "entities/entity_components.hpp"
 #include "entities/sim_components.hpp"
 #include "math/polygon.hpp"
+#include "systems/barnes_hut.hpp"
 #include "systems/boundary.hpp"
 #include "systems/fluid/fluid.hpp"
 #include "systems/gravity.hpp"
@@ -183,4 +184,43 @@ extern "C" int lpeh_world(int mode, int sync_every, const lpe_rigid_config *rc,
     stats[3] = rs->lastContacts();
     lpe::host::setMode(lpe::host::Mode::Strict, 1);
     return stats[0];
+}
+
+/* The drop-in Systems::BarnesHutSystem (host/src/systems/barnes_hut.cpp) on
+ * a registry built exactly like oracle/ref_driver.cpp lpref_barnes_hut
+ * (entities in array order, Velocity where has_vel): vx/vy updated in place. */
+extern "C" int lpeh_barnes_hut(double theta, double small_mass, double universe, double softener,
+                               double spt, double bta, double ts, int n, const double *x, const double *y,
+                               double *vx, double *vy, const double *m, const unsigned char *has_vel) {
+    entt::registry reg;
+    auto st = reg.create();
+    reg.emplace<Components::SimulatorState>(st, bta, ts);
+    std::vector<entt::entity> ents(n);
+    for (int i = 0; i < n; i++) {
+        auto e = reg.create();
+        ents[i] = e;
+        reg.emplace<Components::Position>(e, x[i], y[i]);
+        if (!has_vel || has_vel[i]) reg.emplace<Components::Velocity>(e, vx[i], vy[i]);
+        reg.emplace<Components::Mass>(e, m[i]);
+    }
+    SharedSystemConfig sh{};
+    sh.UniverseSizeMeters = universe;
+    sh.SecondsPerTick = spt;
+    sh.GravitationalSoftener = softener;
+    Systems::BarnesHutSystem bh;
+    Systems::BarnesHutConfig bc;
+    bc.theta = theta;
+    bc.smallMassThreshold = small_mass;
+    bh.setSpecificConfig(bc);
+    bh.setSharedSystemConfig(sh);
+    lpe::host::reset();
+    lpe::host::setMode(lpe::host::Mode::Strict, 1);
+    bh.update(reg);
+    for (int i = 0; i < n; i++)
+        if (!has_vel || has_vel[i]) {
+            const auto &v = reg.get<Components::Velocity>(ents[i]);
+            vx[i] = v.x;
+            vy[i] = v.y;
+        }
+    return lpe::host::lastStatus();
 }

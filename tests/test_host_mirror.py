@@ -41,7 +41,7 @@ def test_host_mirror_exports():
     syms = os.popen(f"nm -D --defined-only {SYSTEMS}").read()
     for name in ("FluidSystem6update", "RigidBodyCollisionSystem6update", "BoundarySystem6update",
                  "BasicGravitySystem6update", "RotationSystem6update", "MovementSystem6update",
-                 "SleepSystem6update"):
+                 "SleepSystem6update", "BarnesHutSystem6update"):
         assert name in syms, name
 
 
@@ -95,3 +95,25 @@ def test_host_mirror_strict_equals_resident():
     for k in ("x", "y"):
         np.testing.assert_allclose(a0[k], a1[k], rtol=1e-5, atol=1e-5, err_msg=k)
         np.testing.assert_allclose(b0[k], b1[k], rtol=1e-5, atol=1e-4, err_msg=k)
+
+
+@needs_build
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["disk150", "clustered150", "clustered210"])
+def test_host_mirror_barnes_hut_matches_reference(name):
+    """The drop-in BarnesHutSystem through a real EnTT registry (its own view
+    order) reproduces the reference's velocities bit for bit
+    (tests/golden/bh_*.npz, recorded from the reference's barnes_hut.cpp)."""
+    z = dict(np.load(os.path.join(ROOT, "tests", "golden", f"bh_{name}.npz")))
+    L = C.CDLL(HARNESS)
+    f = L.lpeh_barnes_hut
+    f.argtypes = [C.c_double] * 7 + [C.c_int] + [C.c_void_p] * 6
+    f.restype = C.c_int
+    vx, vy = z["vx0"].copy(), z["vy0"].copy()
+    bta = float(z["dt"]) / DT
+    st = f(float(z["theta"]), float(z["small_mass_threshold"]), float(z["universe"]), float(z["softener"]),
+           DT, bta, 1.0, len(vx), z["x"].ctypes.data, z["y"].ctypes.data, vx.ctypes.data, vy.ctypes.data,
+           z["m"].ctypes.data, z["has_vel"].ctypes.data)
+    assert st == 0
+    np.testing.assert_array_equal(vx, z["vx"])
+    np.testing.assert_array_equal(vy, z["vy"])

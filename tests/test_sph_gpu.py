@@ -69,6 +69,30 @@ def test_density_bit_exact(gpu_ctx, oracle_mod, name):
     np.testing.assert_array_equal(p, rp)
 
 
+@pytest.mark.parametrize("kind", ["C2", "jitter", "jitter_wide"])
+def test_density_pair_kernel_staged_bit_exact(gpu_ctx, oracle_mod, kind):
+    """The two-particles-per-lane pure density pass (k_density_pair) on wide
+    fluids, where its 512-slot tiles stage their neighbourhoods (no fallback):
+    the C2 dam break, and a jittered lattice with uneven cells (pairs that
+    straddle quadrants, cells and the tiles' two row runs)."""
+    if kind == "C2":
+        fl = scenes.scene("C2")["fluid"]
+    else:
+        rng = np.random.default_rng(12)
+        # jitter_wide: ~1,560 tiles, several per block of the persistent pass
+        fl = scenes.fluid_lattice(rng, *((1600, 500) if kind == "jitter_wide" else (700, 60)), 1.0, 1.0)
+        fl["x"] = (fl["x"] + rng.uniform(-0.006, 0.006, len(fl["x"])))
+        fl["y"] = (fl["y"] + rng.uniform(-0.006, 0.006, len(fl["y"])))
+    _upload(gpu_ctx, fl)
+    gpu_ctx.sph_diag(True)
+    rho, p = gpu_ctx.sph_probe_density()
+    st = gpu_ctx.sph_stats()
+    rrho, rp, g, _ = oracle_mod.density(scenes.particles_aos(fl))
+    np.testing.assert_array_equal(rho, rrho)
+    np.testing.assert_array_equal(p, rp)
+    assert st["stageFallback"] == 0
+
+
 def test_tick_walls_only_bit_exact(gpu_ctx, oracle_mod):
     """One full tick (10 sub-steps) with only the 4 walls (R > 0 dispatches the
     impulse kernel, but no particle touches a wall)."""
