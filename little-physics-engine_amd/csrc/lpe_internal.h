@@ -117,7 +117,11 @@ enum StatusSlot {
     ST_REF_UB = 12,         // reference cell-capacity mode read past the last cell (undefined in the reference)
     ST_OVER_CAP_TOTAL = 13, // ST_OVER_CAP summed since the last lpe_sph_diag call (bench windows)
     ST_MAX_OCC_TOTAL = 14,  // ST_MAX_OCC maximum since the last lpe_sph_diag call
-    ST_COUNT = 16
+    ST_RX_GHOST_L = 16,     // slab decomposition: most ghosts the left / right neighbour packed for this
+    ST_RX_GHOST_R = 17,     //   rank in a sub-step of the current tick (sizes the next tick's exchange)
+    ST_RX_MIG_L = 18,       // most migrants received from the left / right neighbour so far
+    ST_RX_MIG_R = 19,
+    ST_COUNT = 20
 };
 
 }  // namespace lpe

@@ -20,17 +20,17 @@ struct RcclTransport : Transport {
         if (comm) ncclCommDestroy(comm);
     }
     int halo(lpe_ctx *ctx, const void *sendL, const void *sendR, void *recvL, void *recvR,
-             size_t bytes) override {
+             size_t sbL, size_t sbR, size_t rbL, size_t rbR) override {
         if (ncclGroupStart() != ncclSuccess) return LPE_ERR_HIP;
         ncclResult_t r = ncclSuccess;
         auto keep = [&r](ncclResult_t x) { if (r == ncclSuccess) r = x; };
         if (sendL && recvL && rank > 0) {
-            keep(ncclSend(sendL, bytes, ncclChar, rank - 1, comm, ctx->stream));
-            keep(ncclRecv(recvL, bytes, ncclChar, rank - 1, comm, ctx->stream));
+            keep(ncclSend(sendL, sbL, ncclChar, rank - 1, comm, ctx->stream));
+            keep(ncclRecv(recvL, rbL, ncclChar, rank - 1, comm, ctx->stream));
         }
         if (sendR && recvR && rank < nranks - 1) {
-            keep(ncclSend(sendR, bytes, ncclChar, rank + 1, comm, ctx->stream));
-            keep(ncclRecv(recvR, bytes, ncclChar, rank + 1, comm, ctx->stream));
+            keep(ncclSend(sendR, sbR, ncclChar, rank + 1, comm, ctx->stream));
+            keep(ncclRecv(recvR, rbR, ncclChar, rank + 1, comm, ctx->stream));
         }
         const ncclResult_t e = ncclGroupEnd();     // always closes the group
         if (r != ncclSuccess || e != ncclSuccess) {
@@ -98,6 +98,7 @@ struct LoopGroup {
     long gen = 0;
     bool abort = false;          // a rank failed: every barrier returns at once
     std::vector<const void *> pL, pR;
+    std::vector<size_t> szL, szR;          // the send sizes of each rank (checked by the receivers)
     std::vector<std::vector<float>> red;
     std::vector<std::vector<long long>> redi;
     bool barrier() {
@@ -123,21 +124,33 @@ struct LoopGroup {
 struct LoopTransport : Transport {
     LoopGroup *g = nullptr;
     int halo(lpe_ctx *ctx, const void *sendL, const void *sendR, void *recvL, void *recvR,
-             size_t bytes) override {
+             size_t sbL, size_t sbR, size_t rbL, size_t rbR) override {
         if (hipStreamSynchronize(ctx->stream) != hipSuccess) return LPE_ERR_HIP;
         g->pL[rank] = sendL;
         g->pR[rank] = sendR;
+        g->szL[rank] = sbL;
+        g->szR[rank] = sbR;
         if (!g->barrier()) return LPE_ERR_STATE;
         // the copies run on this rank's stream and are complete before the
         // second barrier: the sender may then reuse its buffers, and this
-        // rank's unpack (same stream) sees the data
+        // rank's unpack (same stream) sees the data.  A size that differs
+        // from the neighbour's send is a protocol error (RCCL would hang or
+        // truncate): fail loudly.
         int st = LPE_OK;
-        if (recvL && rank > 0 && g->pR[rank - 1])
-            if (hipMemcpyAsync(recvL, g->pR[rank - 1], bytes, hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess)
+        if (recvL && rank > 0 && g->pR[rank - 1]) {
+            if (g->szR[rank - 1] != rbL) {
+                ctx->err = "loopback halo: receive size differs from the left neighbour's send";
+                st = LPE_ERR_STATE;
+            } else if (hipMemcpyAsync(recvL, g->pR[rank - 1], rbL, hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess)
                 st = LPE_ERR_HIP;
-        if (recvR && rank < nranks - 1 && g->pL[rank + 1])
-            if (hipMemcpyAsync(recvR, g->pL[rank + 1], bytes, hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess)
+        }
+        if (recvR && rank < nranks - 1 && g->pL[rank + 1]) {
+            if (g->szL[rank + 1] != rbR) {
+                ctx->err = "loopback halo: receive size differs from the right neighbour's send";
+                st = LPE_ERR_STATE;
+            } else if (hipMemcpyAsync(recvR, g->pL[rank + 1], rbR, hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess)
                 st = LPE_ERR_HIP;
+        }
         if (hipStreamSynchronize(ctx->stream) != hipSuccess) st = LPE_ERR_HIP;
         if (!g->barrier()) return LPE_ERR_STATE;
         return st;
@@ -207,6 +220,8 @@ extern "C" int lpe_mg_loopback_run(int n, lpe_ctx **ctxs, const lpe_world_config
     LoopGroup g;
     g.n = n;
     g.pL.assign(n, nullptr);
+    g.szL.assign(n, 0);
+    g.szR.assign(n, 0);
     g.pR.assign(n, nullptr);
     g.red.resize(n);
     g.redi.resize(n);

@@ -74,10 +74,11 @@ class SphStats(C.Structure):
                 ("gridMinX", C.c_int32), ("gridMinY", C.c_int32), ("cellSize", C.c_float),
                 ("nlistOverflow", C.c_int32), ("rigidCandidates", C.c_int32), ("neighbours", C.c_int32),
                 ("stageFallback", C.c_int32), ("overCapCells", C.c_int32), ("refUndefined", C.c_int32),
-                ("overCapCellsTotal", C.c_int32), ("maxCellOccupancyTotal", C.c_int32)]
+                ("overCapCellsTotal", C.c_int32), ("maxCellOccupancyTotal", C.c_int32),
+                ("haloWire", C.c_int32 * 2)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        return {k: (list(getattr(self, k)) if k == "haloWire" else getattr(self, k)) for k, _ in self._fields_}
 
 
 # numpy mirror of lpe_gpu_rigid / Systems::GPURigidBody (fluid.hpp:94-125), 200 B

@@ -111,6 +111,37 @@ def test_slab_coupled_first_tick():
             np.testing.assert_array_equal(r_out[k], rref[k], err_msg=k)
 
 
+def test_slab_wire_sized_by_fill():
+    """After the first tick each direction's exchange carries the receiver's
+    request (1.5x its largest ghost receive + 512), not the capacity; the
+    merged state stays bit-identical to the single domain over 5 ticks with
+    particles migrating across the edges."""
+    s = scenes.scene("small96_0")
+    fl = dict(s["fluid"])
+    fl["vx"] = np.full(len(fl["x"]), 0.8)
+    rig = np.zeros(0, lpe.RIGID_DTYPE)
+    ref, _, _ = _single(fl, rig, 5)
+    edges = slab.slab_edges(fl["x"], 3)
+    cfg = lpe.default_fluid_config()
+    ctxs = [lpe.Context(0) for _ in range(3)]
+    try:
+        caps = [slab.ghost_capacity(np.asarray(fl["x"], np.float32), edges, slab.default_halo(cfg))] * 3
+        for r, c in enumerate(ctxs):
+            slab.setup_rank(c, r, 3, fl, edges, cfg, rig)
+        lpe.mg_loopback_run(ctxs, 5, DT)
+        wires = [c.sph_stats()["haloWire"] for c in ctxs]
+        parts = [c.sph_download_owned(cap=len(fl["x"])) for c in ctxs]
+    finally:
+        for c in ctxs:
+            c.close()
+    got = slab.merge_owned(parts, len(fl["x"]))
+    for k in slab.FIELDS:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    assert wires[0][0] == 0 and wires[2][1] == 0            # no neighbour there
+    for w in (wires[0][1], wires[1][0], wires[1][1], wires[2][0]):
+        assert 512 < w < caps[0], (wires, caps)
+
+
 def test_slab_halo_overflow_reported():
     """A ghost buffer too small for the edge strip fails loudly."""
     s = scenes.scene("small64_0")
