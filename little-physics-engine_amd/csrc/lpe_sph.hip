@@ -104,6 +104,64 @@ __device__ __forceinline__ int wave_runs(uint32_t k, bool active, int *runlen, b
 // discarded at any time (sph_void_prelaunch).
 struct KState { float *x, *y, *vhx, *vhy; };
 
+// velocityVerletHalf (metal:408-423) of one particle from its state, and the
+// bin key of the kicked position ((cell, quadrant) of the device grid)
+__device__ __forceinline__ void kick_one(float x, float y, float vx, float vy, float ax, float ay, float dt,
+                                         float hdt, float &px, float &py, float &hx, float &hy) {
+    hx = vx + hdt * ax;
+    hy = vy + hdt * ay;
+    px = x + hx * dt;
+    py = y + hy * dt;
+}
+__device__ __forceinline__ uint32_t bin_key(float px, float py, float eps, float cs, int ox, int oy, int W, int H,
+                                            int32_t *__restrict__ status) {
+    float tx = (px + eps) / cs, ty = (py + eps) / cs;
+    int gx = (int)floorf(tx), gy = (int)floorf(ty);
+    int qx = (int)floorf(2.0f * tx) - 2 * gx;
+    int qy = (int)floorf(2.0f * ty) - 2 * gy;
+    int kx = gx - ox, ky = gy - oy;
+    if (kx < 0 || kx >= W || ky < 0 || ky >= H) {
+        atomicOr(&status[ST_CAP_OVERFLOW], 1);
+        kx = min(max(kx, 0), W - 1);
+        ky = min(max(ky, 0), H - 1);
+    }
+    return (((uint32_t)ky * (uint32_t)W + (uint32_t)kx) << 2) | (uint32_t)(qy * 2 + qx);
+}
+// the block's bbox partial (exact: min/max are order independent); every
+// thread of the TPB-thread block calls it
+__device__ __forceinline__ void bbox_partial(float mnx, float mxx, float mny, float mxy, float4 *__restrict__ out) {
+    for (int off = 32; off > 0; off >>= 1) {
+        mnx = fminf(mnx, __shfl_xor(mnx, off));
+        mxx = fmaxf(mxx, __shfl_xor(mxx, off));
+        mny = fminf(mny, __shfl_xor(mny, off));
+        mxy = fmaxf(mxy, __shfl_xor(mxy, off));
+    }
+    __shared__ float4 wb[TPB / 64];
+    if (lane_id() == 0) wb[threadIdx.x >> 6] = make_float4(mnx, mxx, mny, mxy);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float4 b = wb[0];
+        for (int w = 1; w < TPB / 64; w++) {
+            b.x = fminf(b.x, wb[w].x); b.y = fmaxf(b.y, wb[w].y);
+            b.z = fminf(b.z, wb[w].z); b.w = fmaxf(b.w, wb[w].w);
+        }
+        *out = b;
+    }
+}
+
+// The next sub-step's kick, fused into the forces pass of the current one
+// (sub-steps 1..numSubSteps-1 of a single-domain tick): the finished state
+// of a particle is exactly what k_kick_drift would read back from P.
+struct KickNext {
+    int on;
+    float dt, hdt, eps, cs;
+    int ox, oy, W, H;
+    float *kx, *ky, *kvhx, *kvhy;     // KState
+    uint32_t *key;
+    int32_t *count;
+    float4 *bboxPart;                 // one partial per forces block
+};
+
 // k_kick_drift: velocityVerletHalf + bin key + histogram + bbox partials.
 // first != 0: first sub-step of a tick; the gather set a = 0 (fluid.cpp:289-290).
 __global__ void __launch_bounds__(TPB)
@@ -123,26 +181,13 @@ k_kick_drift(int n, float dt, float hdt, int first, int probe, float eps, float 
             if (probe) {
                 px = P.x[i]; py = P.y[i];
             } else {
-                float a_x = first ? 0.f : P.ax[i];
-                float a_y = first ? 0.f : P.ay[i];
-                float hx = P.vx[i] + hdt * a_x;
-                float hy = P.vy[i] + hdt * a_y;
-                px = P.x[i] + hx * dt;
-                py = P.y[i] + hy * dt;
+                float hx, hy;
+                kick_one(P.x[i], P.y[i], P.vx[i], P.vy[i], first ? 0.f : P.ax[i], first ? 0.f : P.ay[i], dt, hdt,
+                         px, py, hx, hy);
                 K.vhx[i] = hx; K.vhy[i] = hy;
             }
             K.x[i] = px; K.y[i] = py;
-            float tx = (px + eps) / cs, ty = (py + eps) / cs;
-            int gx = (int)floorf(tx), gy = (int)floorf(ty);
-            int qx = (int)floorf(2.0f * tx) - 2 * gx;
-            int qy = (int)floorf(2.0f * ty) - 2 * gy;
-            int kx = gx - ox, ky = gy - oy;
-            if (kx < 0 || kx >= W || ky < 0 || ky >= H) {
-                atomicOr(&status[ST_CAP_OVERFLOW], 1);
-                kx = min(max(kx, 0), W - 1);
-                ky = min(max(ky, 0), H - 1);
-            }
-            k = (((uint32_t)ky * (uint32_t)W + (uint32_t)kx) << 2) | (uint32_t)(qy * 2 + qx);
+            k = bin_key(px, py, eps, cs, ox, oy, W, H, status);
             key[i] = k;
             mnx = fminf(mnx, px); mxx = fmaxf(mxx, px);
             mny = fminf(mny, py); mxy = fmaxf(mxy, py);
@@ -151,24 +196,7 @@ k_kick_drift(int n, float dt, float hdt, int first, int probe, float eps, float 
         (void)wave_runs(k, active, &len, &st);
         if (st) atomicAdd(&count[k], len);
     }
-    // block bbox partial (exact: min/max are order independent)
-    for (int off = 32; off > 0; off >>= 1) {
-        mnx = fminf(mnx, __shfl_xor(mnx, off));
-        mxx = fmaxf(mxx, __shfl_xor(mxx, off));
-        mny = fminf(mny, __shfl_xor(mny, off));
-        mxy = fmaxf(mxy, __shfl_xor(mxy, off));
-    }
-    __shared__ float4 wb[TPB / 64];
-    if (lane_id() == 0) wb[threadIdx.x >> 6] = make_float4(mnx, mxx, mny, mxy);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        float4 b = wb[0];
-        for (int w = 1; w < TPB / 64; w++) {
-            b.x = fminf(b.x, wb[w].x); b.y = fmaxf(b.y, wb[w].y);
-            b.z = fminf(b.z, wb[w].z); b.w = fmaxf(b.w, wb[w].w);
-        }
-        bboxPart[blockIdx.x] = b;
-    }
+    bbox_partial(mnx, mxx, mny, mxy, bboxPart + blockIdx.x);
 }
 
 // ---------------------------------------------------------------------------
@@ -1155,14 +1183,17 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                 const int32_t *__restrict__ rbinStart, const int32_t *__restrict__ rbinList,
                 const float4 *__restrict__ rbinAabb,
                 unsigned long long *__restrict__ acq,
-                int32_t *__restrict__ status) {
+                int32_t *__restrict__ status, KickNext kn) {
     // plain block order (blocks go round robin over the XCDs): the costly
     // blocks, the particles in and around the rigid pile, are one spatial
     // run that an XCD-contiguous mapping (xcd_block) would put on one XCD
     const int lb = (int)blockIdx.x;
     const int nn = sp.nptr ? *sp.nptr : sp.n;
     const int s0 = lb * HB, s1 = min(s0 + HB, nn);
-    if (s0 >= s1) return;
+    if (s0 >= s1) {
+        if (kn.on && threadIdx.x == 0) kn.bboxPart[lb] = make_float4(1e30f, -1e30f, 1e30f, -1e30f);
+        return;
+    }
     FTR(0);
     const GridParams g = *gp;
     const float cs = g.cellSize;
@@ -1339,13 +1370,32 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
             couple_finish(st, cp, a);
         }
     }
-    if (!live) return;
-    P.x[out] = st.x; P.y[out] = st.y;
-    P.vx[out] = st.vx; P.vy[out] = st.vy;
-    P.vhx[out] = st.vhx; P.vhy[out] = st.vhy;
-    P.ax[out] = st.ax; P.ay[out] = st.ay;
-    P.m[out] = st.mass; P.id[out] = S.id[s];
-    if (sp.orho) { sp.orho[out] = rhoi; sp.opr[out] = pi; }
+    if (live) {
+        P.x[out] = st.x; P.y[out] = st.y;
+        P.vx[out] = st.vx; P.vy[out] = st.vy;
+        P.vhx[out] = st.vhx; P.vhy[out] = st.vhy;
+        P.ax[out] = st.ax; P.ay[out] = st.ay;
+        P.m[out] = st.mass; P.id[out] = S.id[s];
+        if (sp.orho) { sp.orho[out] = rhoi; sp.opr[out] = pi; }
+    }
+    if (kn.on) {            // the next sub-step's k_kick_drift for this particle (block-uniform)
+        float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
+        uint32_t k = 0xFFFFFFFFu;
+        if (live) {
+            float px, py, hx, hy;
+            kick_one(st.x, st.y, st.vx, st.vy, st.ax, st.ay, kn.dt, kn.hdt, px, py, hx, hy);
+            kn.kvhx[out] = hx; kn.kvhy[out] = hy;
+            kn.kx[out] = px; kn.ky[out] = py;
+            k = bin_key(px, py, kn.eps, kn.cs, kn.ox, kn.oy, kn.W, kn.H, status);
+            kn.key[out] = k;
+            mnx = mxx = px;
+            mny = mxy = py;
+        }
+        int len; bool stt;
+        (void)wave_runs(k, live, &len, &stt);
+        if (stt) atomicAdd(&kn.count[k], len);
+        bbox_partial(mnx, mxx, mny, mxy, kn.bboxPart + lb);
+    }
 #ifdef LPE_FTRACE
     if (g_ftrace_on) atomicMax(&g_ftrace[lb * 8 + 3], wall_clock64());
 #endif
@@ -2034,7 +2084,8 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpOld, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.refInv, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.stage, sizeof(float) * N));
-    LPE_HIP(ctx, hipMalloc((void **)&d.bboxPart, sizeof(float4) * MAX_KICK_BLOCKS));
+    // bbox partials: the kick's blocks, or the forces pass's when it kicks the next sub-step
+    LPE_HIP(ctx, hipMalloc((void **)&d.bboxPart, sizeof(float4) * std::max<size_t>(MAX_KICK_BLOCKS, (N + HB - 1) / HB)));
     d.cap_n = n;
     if (h) {
         shard_free_slots(h);
@@ -2238,15 +2289,20 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
 }
 
 // one grid hash: kick (unless probe) + histogram + scan + scatter + rank/permute
-static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool probe) {
+// kicked > 0: the previous forces pass already kicked this sub-step (KickNext)
+// and left `kicked` bbox partials
+static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool probe, int kicked = 0) {
     SphDev &d = ctx->sph;
     hipStream_t s = ctx->stream;
     int C = 4 * d.W * d.H;
-    int kb = std::min(MAX_KICK_BLOCKS, std::max(1, nblk(d.n)));
-    LPE_KERNEL(ctx, "k_kick_drift", k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
-                       first ? 1 : 0, probe ? 1 : 0, d.cfg.gridConfig.gridEpsilon, d.cs, d.ox,
-                       d.oy, d.W, d.H, d.P, sph_kstate(d), d.key, d.count, d.bboxPart, d.stat_cur);
-    LPE_CHECK_LAUNCH(ctx, "k_kick_drift");
+    int kb = kicked;
+    if (!kicked) {
+        kb = std::min(MAX_KICK_BLOCKS, std::max(1, nblk(d.n)));
+        LPE_KERNEL(ctx, "k_kick_drift", k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
+                   first ? 1 : 0, probe ? 1 : 0, d.cfg.gridConfig.gridEpsilon, d.cs, d.ox,
+                   d.oy, d.W, d.H, d.P, sph_kstate(d), d.key, d.count, d.bboxPart, d.stat_cur);
+        LPE_CHECK_LAUNCH(ctx, "k_kick_drift");
+    }
     int st = sph_scan(ctx, C, d.count, d.start, d.cursor, d.blocksum, kb, true);
     if (st) return st;
     LPE_KERNEL(ctx, "k_scatter", k_scatter, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.P.id, d.cursor,
@@ -2537,6 +2593,12 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
     }
     CoupleParams cp;
     sph_couple_params(d, cp);
+    // single domain: each forces pass but the last also kicks the next
+    // sub-step (KickNext), so its hash starts at the scan (LPE_NO_KICK_FUSION=1: off)
+    static const bool nofuse = getenv("LPE_NO_KICK_FUSION") != nullptr;
+    const bool fuse = !sh && !nofuse;
+    const int fblocks = nblk1(sp.n, HB);
+    int kicked = 0;
     for (int step = 0; step < c.numSubSteps; step++) {
         if (sh) {
             st = sph_hash_shard(ctx, subDt, halfDt, step == 0);
@@ -2547,16 +2609,26 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
         } else if (step == 0 && pre) {
             st = LPE_OK;                              // waited for above
         } else {
-            st = sph_hash(ctx, subDt, halfDt, step == 0, false);
+            st = sph_hash(ctx, subDt, halfDt, step == 0, false, kicked);
             if (st) return st;
             st = sph_density(ctx, d.n, nullptr, d.rho, d.pr);
         }
         if (st) return st;
-        LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(nblk1(sp.n, HB)), dim3(HB), 0, s, sp, cp,
+        KickNext kn{};
+        kn.on = fuse && step + 1 < c.numSubSteps;
+        if (kn.on) {
+            kn.dt = subDt; kn.hdt = halfDt; kn.eps = c.gridConfig.gridEpsilon; kn.cs = d.cs;
+            kn.ox = d.ox; kn.oy = d.oy; kn.W = d.W; kn.H = d.H;
+            const KState K = sph_kstate(d);
+            kn.kx = K.x; kn.ky = K.y; kn.kvhx = K.vhx; kn.kvhy = K.vhy;
+            kn.key = d.key; kn.count = d.count; kn.bboxPart = d.bboxPart;
+        }
+        kicked = kn.on ? fblocks : 0;
+        LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(fblocks), dim3(HB), 0, s, sp, cp,
                            (step == 0 && pre) ? d.gp + 1 : d.gp,
                            d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart, d.rbinList,
                            rbin_aabb(d),
-                           d.acq, d.status);
+                           d.acq, d.status, kn);
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
         if (hook) {                                  // (lpe_world_tick: the rigid detection)
             st = hook(ctx, step);
