@@ -200,6 +200,26 @@ k_kick_drift(int n, float dt, float hdt, int first, int probe, float eps, float 
 }
 
 // ---------------------------------------------------------------------------
+// the reference grid from the particle bbox (fluid.cpp:440-494, :717-752)
+__device__ __forceinline__ GridParams grid_from_bbox(float minX, float maxX, float minY, float maxY, float cs) {
+    if (minX > maxX) { float t = minX; minX = maxX; maxX = t; }
+    if (minY > maxY) { float t = minY; minY = maxY; maxY = t; }
+    minX -= 1e-6f;
+    minY -= 1e-6f;
+    GridParams g;
+    g.cellSize = cs;
+    g.gridMinX = (int)floorf(minX / cs);
+    g.gridMinY = (int)floorf(minY / cs);
+    g.gridMaxX = (int)floorf(maxX / cs);
+    g.gridMaxY = (int)floorf(maxY / cs);
+    g.gridDimX = g.gridMaxX - g.gridMinX + 1;
+    g.gridDimY = g.gridMaxY - g.gridMinY + 1;
+    if (g.gridDimX < 1) g.gridDimX = 1;
+    if (g.gridDimY < 1) g.gridDimY = 1;
+    return g;
+}
+
+// ---------------------------------------------------------------------------
 // scan
 __device__ __forceinline__ int wave_incl_scan(int v) {
     int lane = lane_id();
@@ -225,7 +245,8 @@ __device__ __forceinline__ int block_excl_scan(int v, int *total) {
 }
 
 __global__ void __launch_bounds__(TPB)
-k_scan_reduce(int C, const int32_t *__restrict__ cnt, int32_t *__restrict__ bsum) {
+k_scan_reduce(int C, const int32_t *__restrict__ cnt, int32_t *__restrict__ bsum, int32_t *__restrict__ status) {
+    if (status && blockIdx.x == 0 && threadIdx.x == 0) status[ST_NOT_INSERTED] = 0;   // (fused scan)
     int base = blockIdx.x * SCAN_ELEMS;
     int s = 0;
     for (int k = 0; k < 4; k++) {
@@ -282,38 +303,75 @@ k_scan_blocks(int nb, int32_t *__restrict__ bsum, int32_t *__restrict__ start_la
             b.x = fminf(b.x, wb[w].x); b.y = fmaxf(b.y, wb[w].y);
             b.z = fminf(b.z, wb[w].z); b.w = fmaxf(b.w, wb[w].w);
         }
-        float minX = b.x, maxX = b.y, minY = b.z, maxY = b.w;
-        if (minX > maxX) { float t = minX; minX = maxX; maxX = t; }
-        if (minY > maxY) { float t = minY; minY = maxY; maxY = t; }
-        minX -= 1e-6f;
-        minY -= 1e-6f;
-        GridParams g;
-        g.cellSize = cs;
-        g.gridMinX = (int)floorf(minX / cs);
-        g.gridMinY = (int)floorf(minY / cs);
-        g.gridMaxX = (int)floorf(maxX / cs);
-        g.gridMaxY = (int)floorf(maxY / cs);
-        g.gridDimX = g.gridMaxX - g.gridMinX + 1;
-        g.gridDimY = g.gridMaxY - g.gridMinY + 1;
-        if (g.gridDimX < 1) g.gridDimX = 1;
-        if (g.gridDimY < 1) g.gridDimY = 1;
-        *gp = g;
+        *gp = grid_from_bbox(b.x, b.y, b.z, b.w, cs);
         status[ST_NOT_INSERTED] = 0;
     }
 }
 
 // final scan pass; one thread = 4 consecutive bins = one reference cell when
 // the bins are the (cell, quadrant) bins of the fluid (do_stats).
+// fused (the fluid hash, few tiles): bsum holds the raw tile totals and each
+// block derives its own prefix, the total and the reference grid from the
+// bbox partials itself (what k_scan_blocks computes once), block 0 storing
+// gp and start[C] for the kernels after it: one launch fewer per sub-step
 __global__ void __launch_bounds__(TPB)
 k_scan_final(int C, int W, int ox, int oy, int32_t *__restrict__ cnt,
              const int32_t *__restrict__ bsum, int32_t *__restrict__ start,
-             int32_t *__restrict__ cursor, const GridParams *__restrict__ gp,
-             int32_t *__restrict__ status, int do_stats) {
+             int32_t *__restrict__ cursor, GridParams *__restrict__ gp,
+             int32_t *__restrict__ status, int do_stats, int fused, const float4 *__restrict__ bboxPart,
+             int nparts, float gcs) {
     __shared__ int s_max, s_out, s_over;
     if (threadIdx.x == 0) { s_max = 0; s_out = 0; s_over = 0; }
-    __syncthreads();
     GridParams g{};
-    if (do_stats) g = *gp;
+    int prefix = 0;
+    if (fused) {
+        const int nb = (C + SCAN_ELEMS - 1) / SCAN_ELEMS;
+        int pre = 0, all = 0;
+        for (int i = threadIdx.x; i < nb; i += TPB) {
+            const int v = bsum[i];
+            pre += i < (int)blockIdx.x ? v : 0;
+            all += v;
+        }
+        float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
+        for (int p = threadIdx.x; p < nparts; p += TPB) {
+            const float4 b = bboxPart[p];
+            mnx = fminf(mnx, b.x); mxx = fmaxf(mxx, b.y);
+            mny = fminf(mny, b.z); mxy = fmaxf(mxy, b.w);
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            pre += __shfl_xor(pre, off);
+            all += __shfl_xor(all, off);
+            mnx = fminf(mnx, __shfl_xor(mnx, off));
+            mxx = fmaxf(mxx, __shfl_xor(mxx, off));
+            mny = fminf(mny, __shfl_xor(mny, off));
+            mxy = fmaxf(mxy, __shfl_xor(mxy, off));
+        }
+        __shared__ int wp[TPB / 64], wa[TPB / 64];
+        __shared__ float4 wb[TPB / 64];
+        if (lane_id() == 0) {
+            wp[threadIdx.x >> 6] = pre;
+            wa[threadIdx.x >> 6] = all;
+            wb[threadIdx.x >> 6] = make_float4(mnx, mxx, mny, mxy);
+        }
+        __syncthreads();
+        float4 b = wb[0];
+        pre = wp[0]; all = wa[0];
+        for (int w = 1; w < TPB / 64; w++) {
+            pre += wp[w]; all += wa[w];
+            b.x = fminf(b.x, wb[w].x); b.y = fmaxf(b.y, wb[w].y);
+            b.z = fminf(b.z, wb[w].z); b.w = fmaxf(b.w, wb[w].w);
+        }
+        g = grid_from_bbox(b.x, b.y, b.z, b.w, gcs);
+        prefix = pre;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            *gp = g;
+            start[C] = all;
+        }
+    } else {
+        __syncthreads();
+        if (do_stats) g = *gp;
+        prefix = bsum[blockIdx.x];
+    }
     int base = blockIdx.x * SCAN_ELEMS + threadIdx.x * 4;
     int v[4];
     int s = 0;
@@ -333,7 +391,7 @@ k_scan_final(int C, int W, int ox, int oy, int32_t *__restrict__ cnt,
         if (in && s > LPE_REF_MAX_PER_CELL) atomicAdd(&s_over, 1);
     }
     int tot;
-    int ex = block_excl_scan(s, &tot) + bsum[blockIdx.x];
+    int ex = block_excl_scan(s, &tot) + prefix;
     for (int k = 0; k < 4; k++) {
         int c = base + k;
         if (c < C) { start[c] = ex; cursor[c] = ex; cnt[c] = 0; }
@@ -2225,11 +2283,18 @@ static int sph_scan(lpe_ctx *ctx, int C, int32_t *cnt, int32_t *start, int32_t *
     SphDev &d = ctx->sph;
     int nb = (C + SCAN_ELEMS - 1) / SCAN_ELEMS;
     hipStream_t s = ctx->stream;
-    LPE_KERNEL(ctx, "k_scan_reduce", k_scan_reduce, dim3(nb), dim3(TPB), 0, s, C, cnt, bsum);
-    LPE_KERNEL(ctx, "k_scan_blocks", k_scan_blocks, dim3(1), dim3(TPB), 0, s, nb, bsum, start + C, d.bboxPart,
-                       nparts, d.cs, fluid ? d.gp_cur : (GridParams *)nullptr, d.stat_cur, bbG);
+    // the fluid hash with few tiles: k_scan_blocks' work folded into every
+    // k_scan_final block (LPE_NO_SCAN_FUSION=1: off)
+    static const bool nofuse = getenv("LPE_NO_SCAN_FUSION") != nullptr;
+    const bool fused = fluid && !bbG && nb <= 1024 && !nofuse;
+    LPE_KERNEL(ctx, "k_scan_reduce", k_scan_reduce, dim3(nb), dim3(TPB), 0, s, C, cnt, bsum,
+               fused ? d.stat_cur : (int32_t *)nullptr);
+    if (!fused)
+        LPE_KERNEL(ctx, "k_scan_blocks", k_scan_blocks, dim3(1), dim3(TPB), 0, s, nb, bsum, start + C, d.bboxPart,
+                   nparts, d.cs, fluid ? d.gp_cur : (GridParams *)nullptr, d.stat_cur, bbG);
     LPE_KERNEL(ctx, "k_scan_final", k_scan_final, dim3(nb), dim3(TPB), 0, s, C, d.W, d.ox, d.oy, cnt, bsum,
-                       start, cursor, d.gp_cur, d.stat_cur, fluid ? 1 : 0);
+               start, cursor, d.gp_cur, d.stat_cur, fluid ? 1 : 0, fused ? 1 : 0, (const float4 *)d.bboxPart,
+               nparts, d.cs);
     LPE_CHECK_LAUNCH(ctx, "scan");
     return LPE_OK;
 }
