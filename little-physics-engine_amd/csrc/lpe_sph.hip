@@ -791,12 +791,21 @@ __device__ __forceinline__ void wave_minmax(int v, int &mn, int &mx) {
 // x or y), so their r^2 >= h^2: they add +0 to a density sum and are never
 // neighbours.  Rows the particle does not reach get empty spans.  Span r
 // covers LDS records [b[r], e[r]); shift[r] maps an LDS index to its slot.
+// The quadrant ranges come from u = 2 (x + eps) / cs by a multiply with the
+// rounded reciprocal, widened by a bound on its error (|u| 2^-20 + 1e-5 covers
+// the product's rounding against the correctly rounded quotient): the walk is
+// then a superset of walk_ranges' quadrants, which is bit-identical (every
+// extra quadrant lies beyond h * 1.002, its terms are +0 and never
+// neighbours), and costs no division.  A quadrant column of the superset is
+// at most one past the exact one, so it stays inside the staged cells.
 __device__ __forceinline__ void hood_spans(const Hood &hd, const int *lbnd, float xi, float yi, float eps,
                                            float cs, float reach, int cyp, const GridParams &g, int b[3],
                                            int e[3], int shift[3]) {
-    const float u = 2.0f * ((xi + eps) / cs), v = 2.0f * ((yi + eps) / cs);
-    const int bx0 = (int)floorf(u - reach), bx1 = (int)floorf(u + reach);
-    const int by0 = (int)floorf(v - reach), by1 = (int)floorf(v + reach);
+    const float rcs = 2.0f / cs;
+    const float u = (xi + eps) * rcs, v = (yi + eps) * rcs;
+    const float wu = reach + fabsf(u) * 0x1p-20f + 1e-5f, wv = reach + fabsf(v) * 0x1p-20f + 1e-5f;
+    const int bx0 = (int)floorf(u - wu), bx1 = (int)floorf(u + wu);
+    const int by0 = (int)floorf(v - wv), by1 = (int)floorf(v + wv);
     const int cxa = max(bx0 >> 1, g.gridMinX), cxb = min(bx1 >> 1, g.gridMinX + g.gridDimX - 1);
     const int cya = max(by0 >> 1, g.gridMinY), cyb = min(by1 >> 1, g.gridMinY + g.gridDimY - 1);
     const int r3 = (cyp == hd.cy0) ? 0 : 3;
@@ -858,8 +867,7 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     if (!hd.ok && threadIdx.x == 0) atomicAdd(&status[ST_STAGE_FALLBACK], 1);
     const float4 me = nbA[sl];
     const float xi = me.x, yi = me.y;
-    int cxp, cyp;
-    cell_xy(xi, yi, eps, cs, cxp, cyp);
+    const int cyp = oy + (int)((unsigned)__float_as_int(me.w) >> 17);   // the bin's cell row (k_rank_permute)
     const float h2 = h * h;
     const float poly6 = poly6Coeff2D(h);
     const float reach = walk_reach(h, cs);
