@@ -433,8 +433,8 @@ __global__ void __launch_bounds__(TPB)
 k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restrict__ start,
                const int32_t *__restrict__ tmpId, const int32_t *__restrict__ tmpOld,
                PState P, KState K, PState S, float4 *__restrict__ nbA, float2 *__restrict__ nbB,
-               int probe, const int32_t *__restrict__ nptr, int nown, int32_t *__restrict__ inv,
-               int32_t *__restrict__ owned, int32_t *__restrict__ refInv, int W) {
+               int probe, const int32_t *__restrict__ nptr, int32_t *__restrict__ src,
+               int32_t *__restrict__ refInv, int W) {
     int s = blockIdx.x * TPB + threadIdx.x;
     if (s >= (nptr ? *nptr : n)) return;
     int o = tmpOld[s];
@@ -452,10 +452,7 @@ k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restric
     S.id[d] = myid;
     if (refInv) refInv[myid] = d;         // reference cell-capacity mode: id -> sorted slot
     if (!probe) { S.vhx[d] = K.vhx[o]; S.vhy[d] = K.vhy[o]; }
-    if (inv) {                    // slab decomposition: P slot -> sorted slot, owned flags
-        inv[o] = d;
-        owned[d] = o < nown ? 1 : 0;
-    }
+    if (src) src[d] = o;          // slab decomposition: sorted slot -> P slot (ghosts: >= the owned count)
 }
 
 // ---------------------------------------------------------------------------
@@ -1212,7 +1209,9 @@ k_density_plan(int n, const int32_t *__restrict__ nptr, float eps, int W, int H,
 
 struct SphStepParams {
     const int32_t *nptr;      // slab decomposition: device slot count (owned + ghosts), else null
-    const int32_t *dst;       // slab decomposition: exclusive scan of the owned flags, else null
+    const int32_t *oldSlot;   // slab decomposition: the P slot of each sorted slot (tmpOld), else null;
+    int nown;                 //   P slots >= nown are ghosts (neighbours only).  Owned particles are
+                              //   written back to their own P slot: P keeps its order on a rank
     float *orho, *opr;        // slab decomposition: rho / p of the owned particles in P order
     int nstride;              // neighbour-list stride (allocated slots)
     int n, W, H, ox, oy;
@@ -1268,9 +1267,9 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     const int s = s0 + threadIdx.x;
     bool live = s < s1;
     int out = s;                              // P slot written
-    if (live && sp.dst) {                     // ghosts are neighbours only
-        out = sp.dst[s];
-        if (sp.dst[s + 1] == out) live = false;
+    if (live && sp.oldSlot) {                 // ghosts are neighbours only
+        out = sp.oldSlot[s];
+        if (out >= sp.nown) live = false;
     }
     const int sl = live ? s : s0;
     const float4 meA = nbA[sl], meB = nbB[sl];
@@ -1512,7 +1511,8 @@ struct Shard {
     float *msL = nullptr, *msR = nullptr, *mrL = nullptr, *mrR = nullptr;
     float4 *bb = nullptr;              // global bbox
     int cap_slots = 0;                 // per-slot arrays below
-    int32_t *inv = nullptr, *owned = nullptr, *dst = nullptr, *keep = nullptr, *kdst = nullptr;
+    int32_t *keep = nullptr, *kdst = nullptr;
+    int32_t *src = nullptr;            // the P slot of each sorted slot (k_rank_permute), for the forces pass
     int32_t *obsum = nullptr;
     float *orho = nullptr, *opr = nullptr;   // rho / p of the owned particles, P order
 };
@@ -1522,8 +1522,15 @@ static inline void shard_reset_wire(Shard &h) {
     h.wmsL = h.wmsR = h.wmrL = h.wmrR = h.cap;
 }
 
+// (also clears the ghost send headers for the pack that follows: two
+// memset launches fewer per sub-step)
 __global__ void __launch_bounds__(TPB)
-k_bbox_reduce(const float4 *__restrict__ part, int nparts, float4 *__restrict__ bb) {
+k_bbox_reduce(const float4 *__restrict__ part, int nparts, float4 *__restrict__ bb, float *__restrict__ sL,
+              float *__restrict__ sR) {
+    if (threadIdx.x < 4) {
+        if (sL) sL[threadIdx.x] = 0.0f;
+        if (sR) sR[threadIdx.x] = 0.0f;
+    }
     float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
     for (int p = threadIdx.x; p < nparts; p += TPB) {
         float4 b = part[p];
@@ -1906,9 +1913,9 @@ static void pstate_free(PState &p) {
 }
 
 static void shard_free_slots(Shard *h) {
-    void *ptrs[] = {h->inv, h->owned, h->dst, h->keep, h->kdst, h->obsum, h->orho, h->opr};
+    void *ptrs[] = {h->keep, h->kdst, h->src, h->obsum, h->orho, h->opr};
     for (void *p : ptrs) if (p) (void)hipFree(p);
-    h->inv = h->owned = h->dst = h->keep = h->kdst = h->obsum = nullptr;
+    h->keep = h->kdst = h->src = h->obsum = nullptr;
     h->orho = h->opr = nullptr;
     h->cap_slots = 0;
 }
@@ -2156,13 +2163,12 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     if (h) {
         shard_free_slots(h);
         const size_t S1 = N + 1;
-        int32_t **iv[] = {&h->inv, &h->owned, &h->dst, &h->keep, &h->kdst};
+        int32_t **iv[] = {&h->keep, &h->kdst, &h->src};
         for (int32_t **q : iv) LPE_HIP(ctx, hipMalloc((void **)q, sizeof(int32_t) * S1));
         LPE_HIP(ctx, hipMalloc((void **)&h->obsum, sizeof(int32_t) * (S1 / SCAN_ELEMS + 2)));
         LPE_HIP(ctx, hipMalloc((void **)&h->orho, sizeof(float) * S1));
         LPE_HIP(ctx, hipMalloc((void **)&h->opr, sizeof(float) * S1));
         // the scans zero their count arrays after use; they start zeroed
-        LPE_HIP(ctx, hipMemsetAsync(h->owned, 0, sizeof(int32_t) * S1, ctx->stream));
         LPE_HIP(ctx, hipMemsetAsync(h->keep, 0, sizeof(int32_t) * S1, ctx->stream));
         h->cap_slots = (int)N;
     }
@@ -2382,7 +2388,7 @@ static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool pr
                        d.tmpId, d.tmpOld, (const int32_t *)nullptr);
     LPE_KERNEL(ctx, "k_rank_permute", k_rank_permute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.start,
                        d.tmpId, d.tmpOld, d.P, sph_kstate(d), d.S, d.nbA, (float2 *)d.nbB, probe ? 1 : 0,
-                       (const int32_t *)nullptr, 0, (int32_t *)nullptr, (int32_t *)nullptr, sph_ref_inv(d), d.W);
+                       (const int32_t *)nullptr, (int32_t *)nullptr, sph_ref_inv(d), d.W);
     LPE_CHECK_LAUNCH(ctx, "hash");
     return LPE_OK;
 }
@@ -2441,23 +2447,25 @@ static size_t mig_bytes(int cap) { return sizeof(float) * (HDR + (size_t)cap * M
 static int shard_slots(const Shard &h) { return 2 * h.cap; }   // ghost slots after the owned ones
 
 // the sharded grid hash: kick owned, global bbox, ghost exchange, sort owned + ghosts
-static int sph_hash_shard(lpe_ctx *ctx, float subDt, float halfDt, bool first) {
+// (kicked > 0: the previous forces pass kicked this sub-step and left that
+// many bbox partials)
+static int sph_hash_shard(lpe_ctx *ctx, float subDt, float halfDt, bool first, int kicked = 0) {
     SphDev &d = ctx->sph;
     Shard &h = *d.shard;
     Transport *tr = ctx->transport;
     hipStream_t s = ctx->stream;
     const int C = 4 * d.W * d.H;
-    const int kb = std::min(MAX_KICK_BLOCKS, std::max(1, nblk(d.n)));
+    const int kb = kicked ? kicked : std::min(MAX_KICK_BLOCKS, std::max(1, nblk(d.n)));
     const float eps = d.cfg.gridConfig.gridEpsilon;
-    LPE_KERNEL(ctx, "k_kick_drift", k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
-               first ? 1 : 0, 0, eps, d.cs, d.ox, d.oy, d.W, d.H, d.P, sph_kstate(d), d.key, d.count, d.bboxPart,
-               d.status);
-    LPE_KERNEL(ctx, "k_bbox_reduce", k_bbox_reduce, dim3(1), dim3(TPB), 0, s, d.bboxPart, kb, h.bb);
+    if (!kicked)
+        LPE_KERNEL(ctx, "k_kick_drift", k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
+                   first ? 1 : 0, 0, eps, d.cs, d.ox, d.oy, d.W, d.H, d.P, sph_kstate(d), d.key, d.count,
+                   d.bboxPart, d.status);
+    static_assert(HDR == 4, "k_bbox_reduce clears 4 header words");
+    LPE_KERNEL(ctx, "k_bbox_reduce", k_bbox_reduce, dim3(1), dim3(TPB), 0, s, d.bboxPart, kb, h.bb, h.gsL, h.gsR);
     LPE_CHECK_LAUNCH(ctx, "shard kick");
     int st = tr->allreduce(ctx, (float *)h.bb, 4, 1);
     if (st) return st;
-    LPE_HIP(ctx, hipMemsetAsync(h.gsL, 0, sizeof(float) * HDR, s));
-    LPE_HIP(ctx, hipMemsetAsync(h.gsR, 0, sizeof(float) * HDR, s));
     const float drift = h.D - 2.0f * d.cfg.gridConfig.smoothingLength;
     LPE_KERNEL(ctx, "k_ghost_pack", k_ghost_pack, dim3(nblk1(d.n)), dim3(TPB), 0, s, d.n, d.P, sph_kstate(d), h.x0,
                h.x1, h.D,
@@ -2478,20 +2486,10 @@ static int sph_hash_shard(lpe_ctx *ctx, float subDt, float halfDt, bool first) {
     LPE_KERNEL(ctx, "k_scatter", k_scatter, dim3(nblk1(ncap)), dim3(TPB), 0, s, ncap, d.key, d.P.id, d.cursor,
                d.tmpId, d.tmpOld, (const int32_t *)h.ntot);
     LPE_KERNEL(ctx, "k_rank_permute", k_rank_permute, dim3(nblk1(ncap)), dim3(TPB), 0, s, ncap, d.key, d.start,
-               d.tmpId, d.tmpOld, d.P, sph_kstate(d), d.S, d.nbA, (float2 *)d.nbB, 0, (const int32_t *)h.ntot, d.n,
-               h.inv, h.owned,
-               (int32_t *)nullptr, d.W);
+               d.tmpId, d.tmpOld, d.P, sph_kstate(d), d.S, d.nbA, (float2 *)d.nbB, 0, (const int32_t *)h.ntot,
+               h.src, (int32_t *)nullptr, d.W);
     LPE_CHECK_LAUNCH(ctx, "shard hash");
     return LPE_OK;
-}
-
-// after the density pass: the owned-slot compaction map (exclusive scan of
-// the owned flags of the sorted slots)
-static int sph_owned_map(lpe_ctx *ctx) {
-    SphDev &d = ctx->sph;
-    Shard &h = *d.shard;
-    const int ncap = d.n + shard_slots(h);
-    return sph_scan(ctx, ncap, h.owned, h.dst, (int32_t *)d.key, h.obsum, 0, false);
 }
 
 // once per tick: particles that left the slab go to the neighbour (one host
@@ -2645,7 +2643,8 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
     sp.diag = d.diag;
     sp.refInv = sph_ref_inv(d);
     sp.nptr = nullptr;
-    sp.dst = nullptr;
+    sp.oldSlot = nullptr;
+    sp.nown = 0;
     sp.orho = sp.opr = nullptr;
     sp.nstride = d.cap_n;
     Shard *sh = d.shard;
@@ -2660,25 +2659,25 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
     if (sh) {
         sp.n = d.n + shard_slots(*sh);
         sp.nptr = sh->ntot;
-        sp.dst = sh->dst;
+        sp.oldSlot = sh->src;
+        sp.nown = d.n;
         sp.orho = sh->orho;
         sp.opr = sh->opr;
     }
     CoupleParams cp;
     sph_couple_params(d, cp);
-    // single domain: each forces pass but the last also kicks the next
-    // sub-step (KickNext), so its hash starts at the scan (LPE_NO_KICK_FUSION=1: off)
+    // each forces pass but the last also kicks the next sub-step (KickNext),
+    // so its hash starts at the scan (slab ranks: at the bbox all-reduce);
+    // LPE_NO_KICK_FUSION=1: off
     static const bool nofuse = getenv("LPE_NO_KICK_FUSION") != nullptr;
-    const bool fuse = !sh && !nofuse;
+    const bool fuse = !nofuse;
     const int fblocks = nblk1(sp.n, HB);
     int kicked = 0;
     for (int step = 0; step < c.numSubSteps; step++) {
         if (sh) {
-            st = sph_hash_shard(ctx, subDt, halfDt, step == 0);
+            st = sph_hash_shard(ctx, subDt, halfDt, step == 0, kicked);
             if (st) return st;
             st = sph_density(ctx, sp.n, sh->ntot, d.rho, d.pr);
-            if (st) return st;
-            st = sph_owned_map(ctx);
         } else if (step == 0 && pre) {
             st = LPE_OK;                              // waited for above
         } else {
