@@ -319,7 +319,7 @@ k_scan_final(int C, int W, int ox, int oy, int32_t *__restrict__ cnt,
              const int32_t *__restrict__ bsum, int32_t *__restrict__ start,
              int32_t *__restrict__ cursor, GridParams *__restrict__ gp,
              int32_t *__restrict__ status, int do_stats, int fused, const float4 *__restrict__ bboxPart,
-             int nparts, float gcs) {
+             int nparts, float gcs, const float4 *__restrict__ bbG) {
     __shared__ int s_max, s_out, s_over;
     if (threadIdx.x == 0) { s_max = 0; s_out = 0; s_over = 0; }
     GridParams g{};
@@ -333,10 +333,17 @@ k_scan_final(int C, int W, int ox, int oy, int32_t *__restrict__ cnt,
             all += v;
         }
         float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
-        for (int p = threadIdx.x; p < nparts; p += TPB) {
-            const float4 b = bboxPart[p];
-            mnx = fminf(mnx, b.x); mxx = fmaxf(mxx, b.y);
-            mny = fminf(mny, b.z); mxy = fmaxf(mxy, b.w);
+        if (bbG) {
+            // slab decomposition: the all-reduced bbox of every rank's particles
+            // (stored as minX, minY, -maxX, -maxY for one MIN all-reduce)
+            const float4 b = *bbG;
+            mnx = b.x; mny = b.y; mxx = -b.z; mxy = -b.w;
+        } else {
+            for (int p = threadIdx.x; p < nparts; p += TPB) {
+                const float4 b = bboxPart[p];
+                mnx = fminf(mnx, b.x); mxx = fmaxf(mxx, b.y);
+                mny = fminf(mny, b.z); mxy = fmaxf(mxy, b.w);
+            }
         }
         for (int off = 32; off > 0; off >>= 1) {
             pre += __shfl_xor(pre, off);
@@ -2300,7 +2307,7 @@ static int sph_scan(lpe_ctx *ctx, int C, int32_t *cnt, int32_t *start, int32_t *
     // the fluid hash with few tiles: k_scan_blocks' work folded into every
     // k_scan_final block (LPE_NO_SCAN_FUSION=1: off)
     static const bool nofuse = getenv("LPE_NO_SCAN_FUSION") != nullptr;
-    const bool fused = fluid && !bbG && nb <= 1024 && !nofuse;
+    const bool fused = fluid && nb <= 1024 && !nofuse;
     LPE_KERNEL(ctx, "k_scan_reduce", k_scan_reduce, dim3(nb), dim3(TPB), 0, s, C, cnt, bsum,
                fused ? d.stat_cur : (int32_t *)nullptr);
     if (!fused)
@@ -2308,7 +2315,7 @@ static int sph_scan(lpe_ctx *ctx, int C, int32_t *cnt, int32_t *start, int32_t *
                    nparts, d.cs, fluid ? d.gp_cur : (GridParams *)nullptr, d.stat_cur, bbG);
     LPE_KERNEL(ctx, "k_scan_final", k_scan_final, dim3(nb), dim3(TPB), 0, s, C, d.W, d.ox, d.oy, cnt, bsum,
                start, cursor, d.gp_cur, d.stat_cur, fluid ? 1 : 0, fused ? 1 : 0, (const float4 *)d.bboxPart,
-               nparts, d.cs);
+               nparts, d.cs, bbG);
     LPE_CHECK_LAUNCH(ctx, "scan");
     return LPE_OK;
 }
