@@ -60,7 +60,10 @@ def kernel_bytes(name, n, cells):
     model = {
         "k_kick_drift": 44.0 * n,                    # x,y,vx,vy,ax,ay -> x,y,vh + key
         "k_density": 24.0 * n + 8.0 * cells,         # idx,x,y,m -> rho,p ; cell ranges
-        "k_forces_couple": (40.0 + 24.0 + 8.0) * n,  # forces + finish + coupling test
+        # forces + finish + coupling test, plus the next sub-step's kick fused
+        # into 9 of a tick's 10 launches (KickNext): x,y,vx,vy,ax,ay are already
+        # in registers, so +16 B kicked state + 4 B key per particle on those
+        "k_forces_couple": (40.0 + 24.0 + 8.0 + 0.9 * 20.0) * n,
         "k_scatter": 12.0 * n / 2.0,                 # counting sort (12 B) split over
         "k_rank_permute": 12.0 * n / 2.0,            #   scatter + rank
     }
