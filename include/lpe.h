@@ -507,6 +507,21 @@ int  lpe_bh_upload(lpe_ctx *ctx, int n, const double *x, const double *y, const 
  * be NULL.  Blocks until done. */
 int  lpe_bh_step(lpe_ctx *ctx, const lpe_bh_config *cfg, double dt, lpe_bh_stats *stats);
 int  lpe_bh_download(lpe_ctx *ctx, double *vx, double *vy);
+/* BarnesHutSystem inside lpe_world_tick (position 5 of sim.cpp:107-114, on
+ * the rigid context's bodies, after the collision system and before
+ * rotation).  Enabled by default with lpe_bh_config_default() and the rigid
+ * config's universe size (the reference registers the system in every
+ * scene, sim.cpp:111).  enable = 0 switches it off; cfg (may be NULL: the
+ * defaults) replaces the config; order (n body indices, may be NULL / 0)
+ * is the insertion order, i.e. the bodies of view<Position, Mass>
+ * (exclude<Boundary>) in that view's iteration order - by default every
+ * body with LPE_BODY_HAS_MASS and without LPE_BODY_BOUNDARY, last body
+ * first (EnTT views iterate newest first).  The small-mass early exit is
+ * decided once per upload / config change.  A world whose fluid particles
+ * would make the system act fails with LPE_ERR_STATE (strict mode handles
+ * it through lpe_bh_step).  Shares the buffers of lpe_bh_upload. */
+int  lpe_world_set_barnes_hut(lpe_ctx *ctx, int enable, const lpe_bh_config *cfg, int n,
+                              const int32_t *order);
 
 #ifdef __cplusplus
 }

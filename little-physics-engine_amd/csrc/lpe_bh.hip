@@ -27,6 +27,7 @@
 // fold of each node, which is the reference's own dependency chain.  fp64
 // throughout, no FMA contraction (Makefile), IEEE division and square root.
 #include "lpe_internal.h"
+#include "rigid_dev.h"
 
 #include <hipcub/hipcub.hpp>
 
@@ -64,6 +65,15 @@ struct BhDev {
     void *tmp = nullptr;
     size_t tmpBytes = 0;
     lpe_bh_stats last{};
+    // BarnesHutSystem inside lpe_world_tick (lpe_world_set_barnes_hut)
+    bool w_on = true;                           // the reference always runs the system (sim.cpp:111)
+    bool w_cfg_set = false;                     // else: defaults + the rigid config's universe
+    lpe_bh_config w_cfg{};
+    std::vector<int32_t> w_order_user;          // insertion order given by the host (empty: default)
+    int32_t *w_order = nullptr;                 // device: body index per inserted body
+    int w_n = 0, w_cap = 0;
+    bool w_valid = false, w_active = false, w_fluid_heavy = false;
+    unsigned w_rgen = ~0u, w_sgen = ~0u;
 };
 
 // ---- kernels ---------------------------------------------------------------
@@ -249,17 +259,47 @@ __global__ void k_bh_force(int n, const double *__restrict__ x, const double *__
     vy[p] = wy;
 }
 
+// the world's bodies in insertion order -> the Barnes-Hut arrays
+__global__ void k_bh_gather(int n, const int32_t *__restrict__ order, const lpe_body *__restrict__ bodies,
+                            double *__restrict__ x, double *__restrict__ y, double *__restrict__ vx,
+                            double *__restrict__ vy, double *__restrict__ m, uint8_t *__restrict__ hv) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const lpe_body &b = bodies[order[k]];
+    x[k] = b.x; y[k] = b.y; vx[k] = b.vx; vy[k] = b.vy; m[k] = b.mass;
+    hv[k] = (b.flags & LPE_BODY_HAS_VEL) ? 1 : 0;
+}
+__global__ void k_bh_scatter(int n, const int32_t *__restrict__ order, const double *__restrict__ vx,
+                             const double *__restrict__ vy, const uint8_t *__restrict__ hv,
+                             lpe_body *__restrict__ bodies) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n || !hv[k]) return;
+    lpe_body &b = bodies[order[k]];
+    b.vx = vx[k];
+    b.vy = vy[k];
+}
+
 // ---- host ------------------------------------------------------------------
 
 static inline int bblk(long n, int t = 256) { return (int)std::max<long>(1, (n + t - 1) / t); }
 
+// the body / tree buffers (the world-tick settings and order stay)
 static void bh_free(BhDev &d) {
     for (void *p : {(void *)d.x, (void *)d.y, (void *)d.vx, (void *)d.vy, (void *)d.m, (void *)d.hv,
                     (void *)d.key[0], (void *)d.key[1], (void *)d.val[0], (void *)d.val[1], (void *)d.route,
                     (void *)d.segB, (void *)d.segE, (void *)d.nodes, (void *)d.cnt, d.tmp})
         if (p) (void)hipFree(p);
     if (d.hcnt) (void)hipHostFree(d.hcnt);
-    d = BhDev{};
+    d.x = d.y = d.vx = d.vy = d.m = nullptr;
+    d.hv = d.route = nullptr;
+    d.key[0] = d.key[1] = d.val[0] = d.val[1] = nullptr;
+    d.segB = d.segE = nullptr;
+    d.nodes = nullptr;
+    d.cnt = d.hcnt = nullptr;
+    d.tmp = nullptr;
+    d.n = d.cap = d.segCap = 0;
+    d.ncap = 0;
+    d.tmpBytes = 0;
 }
 
 static BhDev &bh_dev(lpe_ctx *ctx) {
@@ -335,8 +375,10 @@ using namespace lpe;
 int lpe_bh_destroy_internal(lpe_ctx *ctx) {
     if (!ctx->bh) return LPE_OK;
     (void)hipStreamSynchronize(ctx->stream);
-    bh_free(*(BhDev *)ctx->bh);
-    delete (BhDev *)ctx->bh;
+    BhDev *d = (BhDev *)ctx->bh;
+    bh_free(*d);
+    if (d->w_order) (void)hipFree(d->w_order);
+    delete d;
     ctx->bh = nullptr;
     return LPE_OK;
 }
@@ -374,11 +416,10 @@ extern "C" int lpe_bh_upload(lpe_ctx *ctx, int n, const double *x, const double 
     return LPE_OK;
 }
 
-extern "C" int lpe_bh_step(lpe_ctx *ctx, const lpe_bh_config *cfg, double dt, lpe_bh_stats *stats) {
-    if (!ctx || !cfg) return LPE_ERR_ARG;
-    if (!ctx->bh) return LPE_ERR_STATE;
-    (void)hipSetDevice(ctx->device);
-    BhDev &d = *(BhDev *)ctx->bh;
+// One update on the bodies in the BhDev arrays (n = d.n); check_small: the
+// small-mass early exit on the device (the world path decides it itself)
+static int bh_run(lpe_ctx *ctx, BhDev &d, const lpe_bh_config *cfg, double dt, lpe_bh_stats *stats,
+                  bool check_small) {
     hipStream_t s = ctx->stream;
     d.last = lpe_bh_stats{};
     if (stats) *stats = d.last;
@@ -386,7 +427,7 @@ extern "C" int lpe_bh_step(lpe_ctx *ctx, const lpe_bh_config *cfg, double dt, lp
     if (n == 0) return LPE_OK;
     const double thr = cfg->small_mass_threshold;
     LPE_HIP(ctx, hipMemsetAsync(d.cnt, 0, sizeof(int32_t) * 4, s));
-    if (thr > 0.0) {                                        // early exit (:55-71)
+    if (thr > 0.0 && check_small) {                         // early exit (:55-71)
         LPE_KERNEL(ctx, "k_bh_masscheck", k_bh_masscheck, dim3(bblk(n)), dim3(256), 0, s, n, d.m, thr, d.cnt);
         LPE_CHECK_LAUNCH(ctx, "k_bh_masscheck");
         int st = bh_readback(ctx, d);
@@ -447,6 +488,13 @@ extern "C" int lpe_bh_step(lpe_ctx *ctx, const lpe_bh_config *cfg, double dt, lp
     return LPE_OK;
 }
 
+extern "C" int lpe_bh_step(lpe_ctx *ctx, const lpe_bh_config *cfg, double dt, lpe_bh_stats *stats) {
+    if (!ctx || !cfg) return LPE_ERR_ARG;
+    if (!ctx->bh) return LPE_ERR_STATE;
+    (void)hipSetDevice(ctx->device);
+    return bh_run(ctx, *(BhDev *)ctx->bh, cfg, dt, stats, true);
+}
+
 extern "C" int lpe_bh_download(lpe_ctx *ctx, double *vx, double *vy) {
     if (!ctx || !vx || !vy) return LPE_ERR_ARG;
     if (!ctx->bh) return LPE_ERR_STATE;
@@ -456,5 +504,104 @@ extern "C" int lpe_bh_download(lpe_ctx *ctx, double *vx, double *vy) {
     LPE_HIP(ctx, hipMemcpyAsync(vx, d.vx, sizeof(double) * (size_t)d.n, hipMemcpyDeviceToHost, ctx->stream));
     LPE_HIP(ctx, hipMemcpyAsync(vy, d.vy, sizeof(double) * (size_t)d.n, hipMemcpyDeviceToHost, ctx->stream));
     LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LPE_OK;
+}
+
+extern "C" int lpe_world_set_barnes_hut(lpe_ctx *ctx, int enable, const lpe_bh_config *cfg, int n,
+                                        const int32_t *order) {
+    if (!ctx || n < 0 || (n > 0 && !order)) return LPE_ERR_ARG;
+    BhDev &d = bh_dev(ctx);
+    d.w_on = enable != 0;
+    d.w_cfg_set = cfg != nullptr;
+    if (cfg) d.w_cfg = *cfg;
+    d.w_order_user.assign(order, order + n);
+    d.w_valid = false;
+    return LPE_OK;
+}
+
+// BarnesHutSystem::update inside the world tick.  The early exit and the
+// insertion order depend only on masses and component flags, which change
+// only by an upload or a config change: decided once (one read-back) and
+// cached.  Fluid particles are entities with Position + Mass too; a world
+// whose fluid would make the system act fails loudly (its velocities live
+// in fp32 on the device: strict mode runs it through lpe_bh_step).
+int bh_world_tick(lpe_ctx *ctx, double dt_state) {
+    BhDev &d = bh_dev(ctx);
+    if (!d.w_on) return LPE_OK;
+    RigidDev *rd = (RigidDev *)ctx->rigid;
+    SphDev &sd = ctx->sph;
+    const int nb = rd ? rd->nb : 0;
+    lpe_bh_config cfg;
+    if (d.w_cfg_set) cfg = d.w_cfg;
+    else {
+        lpe_bh_config_default(&cfg);
+        cfg.universe_size = rd ? rd->cfg.universeSize : 0.0;
+    }
+    const unsigned rgen = rd ? rd->gen : 0u;
+    if (!d.w_valid || d.w_rgen != rgen || d.w_sgen != sd.upload_gen) {
+        std::vector<lpe_body> hb(nb);
+        if (nb) {
+            LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+            LPE_HIP(ctx, hipMemcpy(hb.data(), rd->bodies, sizeof(lpe_body) * nb, hipMemcpyDeviceToHost));
+        }
+        const double thr = cfg.small_mass_threshold;
+        auto inserted = [](const lpe_body &b) {
+            return (b.flags & LPE_BODY_HAS_MASS) && !(b.flags & LPE_BODY_BOUNDARY);
+        };
+        std::vector<int32_t> ord;
+        if (!d.w_order_user.empty()) {
+            for (int32_t i : d.w_order_user) {
+                if (i < 0 || i >= nb || !inserted(hb[i])) {
+                    ctx->err = "lpe_world_set_barnes_hut: order names a body without Mass or with Boundary";
+                    return LPE_ERR_ARG;
+                }
+                ord.push_back(i);
+            }
+        } else {
+            for (int i = nb - 1; i >= 0; i--)          // EnTT views iterate newest first
+                if (inserted(hb[i])) ord.push_back(i);
+        }
+        bool heavy = thr <= 0.0;
+        for (int i : ord) heavy = heavy || hb[i].mass >= thr;
+        bool fheavy = false;
+        if (sd.n > 0 && !sd.shard && sd.P.m) {
+            std::vector<float> fm(sd.n);
+            LPE_HIP(ctx, hipMemcpy(fm.data(), sd.P.m, sizeof(float) * sd.n, hipMemcpyDeviceToHost));
+            for (float v : fm) fheavy = fheavy || thr <= 0.0 || (double)v >= thr;
+        }
+        int st = bh_alloc(ctx, d, std::max((int)ord.size(), 1));
+        if (st) return st;
+        if ((int)ord.size() > d.w_cap) {
+            if (d.w_order) (void)hipFree(d.w_order);
+            d.w_order = nullptr;
+            LPE_HIP(ctx, hipMalloc(&d.w_order, sizeof(int32_t) * std::max<size_t>(ord.size(), 1)));
+            d.w_cap = (int)ord.size();
+        }
+        if (!ord.empty())
+            LPE_HIP(ctx, hipMemcpy(d.w_order, ord.data(), sizeof(int32_t) * ord.size(), hipMemcpyHostToDevice));
+        d.w_n = (int)ord.size();
+        d.w_active = heavy || fheavy;
+        d.w_fluid_heavy = sd.n > 0 || sd.shard;
+        d.w_rgen = rgen;
+        d.w_sgen = sd.upload_gen;
+        d.w_valid = true;
+    }
+    if (!d.w_active) return LPE_OK;
+    if (d.w_fluid_heavy) {
+        ctx->err = "Barnes-Hut would act on a world with fluid particles: run it in strict mode (lpe_bh_step)";
+        return LPE_ERR_STATE;
+    }
+    if (d.w_n == 0) return LPE_OK;
+    int st = bh_alloc(ctx, d, d.w_n);
+    if (st) return st;
+    d.n = d.w_n;
+    hipStream_t s = ctx->stream;
+    LPE_KERNEL(ctx, "k_bh_gather", k_bh_gather, dim3(bblk(d.n)), dim3(256), 0, s, d.n, d.w_order, rd->bodies, d.x,
+               d.y, d.vx, d.vy, d.m, d.hv);
+    st = bh_run(ctx, d, &cfg, dt_state, nullptr, false);
+    if (st) return st;
+    LPE_KERNEL(ctx, "k_bh_scatter", k_bh_scatter, dim3(bblk(d.n)), dim3(256), 0, s, d.n, d.w_order, d.vx, d.vy,
+               d.hv, rd->bodies);
+    LPE_CHECK_LAUNCH(ctx, "world barnes-hut");
     return LPE_OK;
 }

@@ -96,6 +96,7 @@ struct SphDev {
     int mode = 0;                 // LPE_SPH_MODE_* (lpe_sph_set_mode)
     int32_t *refInv = nullptr;    // reference cell-capacity mode: sorted slot of each particle id
     void *plans = nullptr;        // pure density pass: per-tile staging plans (lpe_sph.hip Hood)
+    unsigned upload_gen = 0;      // bumped by every lpe_sph_upload (world Barnes-Hut cache)
     size_t cap_plans = 0;
     struct Shard *shard = nullptr;// x-slab decomposition state (lpe_sph_set_slab), else single domain
 };
@@ -220,3 +221,6 @@ int sph_alloc_rigids(lpe_ctx *ctx, int n);
 int lpe_sph_hash_current(lpe_ctx *ctx);
 int lpe_timer_destroy_internal(lpe_ctx *ctx);
 int lpe_bh_destroy_internal(lpe_ctx *ctx);
+// BarnesHutSystem inside lpe_world_tick (lpe_bh.hip): on the rigid context's
+// bodies, between the collision system and rotation (sim.cpp:107-114)
+int bh_world_tick(lpe_ctx *ctx, double dt_state);

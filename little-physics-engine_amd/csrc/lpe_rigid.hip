@@ -2025,9 +2025,14 @@ extern "C" int lpe_rigid_config_default(lpe_rigid_config *c) {
 }
 
 extern "C" int lpe_rigid_set_config(lpe_ctx *ctx, const lpe_rigid_config *cfg) {
-    if (ctx) rdev(ctx)->heavy_valid = false;
     if (!ctx || !cfg) return LPE_ERR_ARG;
     RigidDev *d = rdev(ctx);
+    // the cached mass checks stay valid across an unchanged config (the
+    // resident host path re-sets it every tick)
+    if (!d->cfg_set || std::memcmp(&d->cfg, cfg, sizeof(*cfg)) != 0) {
+        d->heavy_valid = false;
+        d->gen++;
+    }
     d->cfg = *cfg;
     d->cfg_set = true;
     return LPE_OK;
@@ -2121,7 +2126,7 @@ static int rscan(lpe_ctx *ctx, RigidDev *d, const int32_t *nptr, int ncap, const
 
 extern "C" int lpe_rigid_upload(lpe_ctx *ctx, int nb, const lpe_body *bodies, int nverts,
                                 const double *verts) {
-    if (ctx) rdev(ctx)->heavy_valid = false;
+    if (ctx) { rdev(ctx)->heavy_valid = false; rdev(ctx)->gen++; }
     if (!ctx || nb < 0 || nverts < 0 || (nb > 0 && !bodies) || (nverts > 0 && !verts))
         return LPE_ERR_ARG;
     (void)hipSetDevice(ctx->device);

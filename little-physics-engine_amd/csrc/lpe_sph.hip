@@ -2230,6 +2230,7 @@ extern "C" int lpe_sph_upload(lpe_ctx *ctx, int n, const float *x, const float *
         LPE_HIP(ctx, hipStreamSynchronize(s));
     }
     LPE_HIP(ctx, hipMemsetAsync(d.status, 0, sizeof(int32_t) * ST_COUNT, s));
+    d.upload_gen++;
     if (d.shard) shard_reset_wire(*d.shard);          // new particles: the first exchange sends the capacity
     return LPE_OK;
 }

@@ -240,7 +240,10 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
         // 4) RigidBodyCollisionSystem
         st = overlap ? rigid_tick_finish(ctx) : lpe_rigid_step(ctx, nullptr);
         if (st) return st;
-        // 5) BarnesHut (early out), 6) Rotation, 7) Movement, 8) Sleep
+        // 5) BarnesHut (its small-mass early exit cached until an upload), 6) Rotation,
+        // 7) Movement, 8) Sleep
+        st = bh_world_tick(ctx, dt_state);
+        if (st) return st;
         st = lpe_rigid_integrate(ctx, 4 | 8 | 16, dt_state, dt_move);
         if (st) return st;
         LPE_CHECK_LAUNCH(ctx, "world tick");

@@ -62,6 +62,7 @@ struct RigidDev {
     int32_t *counts = nullptr;                // [0]=np [1]=nc [4]=npos [5]=heavy [6]=pair overflow
     bool detect_launched = false;             // this tick's detection is on the side stream
     bool heavy_valid = false;                 // counts[5] holds the planetary-mass check of the bodies
+    unsigned gen = 0;                         // bumped by every upload / config change (world Barnes-Hut cache)
                                               // (masses and flags change only by upload / config)
                                               // [7]=solver fault [8]=colours [9]=colouring rounds
                                               // [10]=special broadphase bodies [11]=contact truncation

@@ -23,6 +23,8 @@ struct World {
     size_t positions = 0;                  // Position storage size at upload
     BodySet bodies;                        // non-Liquid entities (rigid path)
     std::vector<entt::entity> fluid;       // Liquid entities in gather order
+    bool bhSent = false;                   // Barnes-Hut config + order given to the device
+    lpe_bh_config bhCfg{};
 };
 
 struct State {
@@ -331,6 +333,24 @@ void residentTick(entt::registry &reg, const SharedSystemConfig &sh) {
         const auto &st = reg.get<Components::SimulatorState>(sv.front());
         wc.baseTimeAcceleration = st.baseTimeAcceleration;
         wc.timeScale = st.timeScale;
+    }
+    if (rc.haveBh && (!w.bhSent || std::memcmp(&w.bhCfg, &rc.bh, sizeof(rc.bh)) != 0)) {
+        // BarnesHutSystem's insertion order: view<Position, Mass>(exclude<Boundary>)
+        // in its own iteration order (barnes_hut.cpp:117-128), as world body
+        // indices (Liquid entities are not world bodies: a world whose fluid
+        // would make the system act fails in lpe_world_tick)
+        std::unordered_map<uint32_t, int32_t> idx;
+        for (size_t i = 0; i < w.bodies.ents.size(); i++) idx[(uint32_t)w.bodies.ents[i]] = (int32_t)i;
+        std::vector<int32_t> order;
+        for (auto e : reg.view<Components::Position, Components::Mass>(entt::exclude<Components::Boundary>)) {
+            auto it = idx.find((uint32_t)e);
+            if (it != idx.end()) order.push_back(it->second);
+        }
+        if (!check(lpe_world_set_barnes_hut(ctx, 1, &rc.bh, (int)order.size(), order.empty() ? nullptr : order.data()),
+                   "lpe_world_set_barnes_hut"))
+            return;
+        w.bhSent = true;
+        w.bhCfg = rc.bh;
     }
     if (!check(lpe_world_tick(ctx, &wc, 1), "lpe_world_tick")) return;
     w.ticks++;

@@ -60,6 +60,8 @@ struct ResidentConfigs {
     lpe_rigid_config rigid;
     lpe_fluid_config fluid;
     bool haveFluid = false;
+    lpe_bh_config bh;            // BarnesHutSystem's (recorded by its update())
+    bool haveBh = false;
 };
 ResidentConfigs &residentConfigs();
 // Runs one device tick (lpe_world_tick) for the registry; uploads the world

@@ -7,11 +7,11 @@
  * on the device (lpe_bh_step: same nodes, same centre-of-mass fold order, same
  * child order as the recursion) and scatters the velocities back.
  *
- * Resident mode keeps the world on the device and its tick (lpe_world_tick)
- * has no Barnes-Hut pass: every metric scene takes the early exit (all masses
- * below smallMassThreshold, :55-71).  A resident world that would NOT take it
- * fails loudly (LPE_ERR_STATE through lpe::host::check) instead of silently
- * skipping gravity; strict mode handles it.
+ * Resident mode records the config; the device tick (lpe_world_tick, run by
+ * the last system) applies Barnes-Hut at this system's place in the order,
+ * on the world bodies in this view's order.  A resident world whose fluid
+ * particles would make it act fails loudly there (LPE_ERR_STATE); strict
+ * mode handles it.
  */
 #include "systems/barnes_hut.hpp"
 
@@ -25,16 +25,24 @@ BarnesHutSystem::BarnesHutSystem() = default;
 
 void BarnesHutSystem::update(entt::registry &registry) {
     const double thr = specificConfig.smallMassThreshold;
+    if (lpe::host::mode() == lpe::host::Mode::Resident) {
+        // the device tick (SleepSystem, the last system) runs it - early exit
+        // included - after the collision system as here (lpe_world_set_barnes_hut)
+        lpe_bh_config &bc = lpe::host::residentConfigs().bh;
+        lpe_bh_config_default(&bc);
+        bc.theta = specificConfig.theta;
+        bc.small_mass_threshold = thr;
+        bc.universe_size = sysConfig.UniverseSizeMeters;
+        bc.softener = sysConfig.GravitationalSoftener;
+        lpe::host::residentConfigs().haveBh = true;
+        return;
+    }
     if (thr > 0.0) {                                                   // early exit (:55-71)
         bool skip = true;
         auto mv = registry.view<Components::Mass>(entt::exclude<Components::Boundary>);
         for (auto e : mv)
             if (mv.get<Components::Mass>(e).value >= thr) { skip = false; break; }
         if (skip) return;
-    }
-    if (lpe::host::mode() == lpe::host::Mode::Resident) {
-        lpe::host::check(LPE_ERR_STATE, "BarnesHutSystem: masses >= smallMassThreshold need strict mode");
-        return;
     }
     auto sv = registry.view<Components::SimulatorState>();
     if (sv.empty()) return;                                            // (:75-79)

@@ -232,6 +232,7 @@ SIGNATURES["lpe_bh_config_default"] = ([C.POINTER(BhConfig)], C.c_int)
 SIGNATURES["lpe_bh_upload"] = ([C.c_void_p, C.c_int] + [_DP] * 5 + [C.c_void_p], C.c_int)
 SIGNATURES["lpe_bh_step"] = ([C.c_void_p, C.POINTER(BhConfig), C.c_double, C.POINTER(BhStats)], C.c_int)
 SIGNATURES["lpe_bh_download"] = ([C.c_void_p, _DP, _DP], C.c_int)
+SIGNATURES["lpe_world_set_barnes_hut"] = ([C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p], C.c_int)
 
 
 def bh_config(universe: float, theta: float = 0.5, small_mass_threshold: float = 1e3,
@@ -565,3 +566,14 @@ class Context:
         self._chk(lib().lpe_bh_download(self._h, vx.ctypes.data_as(_DP), vy.ctypes.data_as(_DP)),
                   "lpe_bh_download")
         return vx, vy
+
+    def world_set_barnes_hut(self, enable=True, cfg: "BhConfig" = None, order=None):
+        """BarnesHutSystem inside lpe_world_tick (on by default; cfg None: the
+        defaults with the rigid config's universe; order None: every massive
+        non-boundary body, last first)."""
+        o = None if order is None else np.ascontiguousarray(order, np.int32)
+        self._bh_world_keep = o
+        self._chk(lib().lpe_world_set_barnes_hut(self._h, 1 if enable else 0,
+                                                  None if cfg is None else C.byref(cfg),
+                                                  0 if o is None else len(o), None if o is None else o.ctypes.data),
+                  "lpe_world_set_barnes_hut")

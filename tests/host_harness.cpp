@@ -7,9 +7,6 @@
  * oracle/Makefile.ref (it needs the reference's headers and its
  * vector_math.cpp, which defines the Position/Vector constructors) into
  * oracle/_ref/liblpe_host_harness.so.
- *
- * BarnesHutSystem (a reference CPU system outside the hot path) is left out:
- * it returns early for every mass < 1e3 (barnes_hut.cpp:54-70).
  */
 #include <entt/entt.hpp>
 
@@ -117,12 +114,13 @@ extern "C" int lpeh_world(int mode, int sync_every, const lpe_rigid_config *rc,
     sh.GridSize = 50;
     sh.CellSizePixels = 12.0;
 
-    /* ECSSimulator::createSystems (sim.cpp:103-150), minus BarnesHut */
+    /* ECSSimulator::createSystems (sim.cpp:103-150) */
     std::vector<std::unique_ptr<Systems::ISystem>> systems;
     systems.push_back(std::make_unique<Systems::FluidSystem>());
     systems.push_back(std::make_unique<Systems::BoundarySystem>());
     systems.push_back(std::make_unique<Systems::BasicGravitySystem>());
     systems.push_back(std::make_unique<Systems::RigidBodyCollisionSystem>());
+    systems.push_back(std::make_unique<Systems::BarnesHutSystem>());
     systems.push_back(std::make_unique<Systems::RotationSystem>());
     systems.push_back(std::make_unique<Systems::MovementSystem>());
     systems.push_back(std::make_unique<Systems::SleepSystem>());
@@ -145,6 +143,7 @@ extern "C" int lpeh_world(int mode, int sync_every, const lpe_rigid_config *rc,
         else if (auto *s = dynamic_cast<Systems::BoundarySystem *>(sys.get())) s->setSpecificConfig(bc);
         else if (auto *s = dynamic_cast<Systems::BasicGravitySystem *>(sys.get())) s->setSpecificConfig(gc);
         else if (auto *s = dynamic_cast<Systems::RigidBodyCollisionSystem *>(sys.get())) s->setSpecificConfig(rbc);
+        else if (auto *s = dynamic_cast<Systems::BarnesHutSystem *>(sys.get())) s->setSpecificConfig(Systems::BarnesHutConfig{});
         else if (auto *s = dynamic_cast<Systems::RotationSystem *>(sys.get())) s->setSpecificConfig(roc);
         else if (auto *s = dynamic_cast<Systems::SleepSystem *>(sys.get())) s->setSpecificConfig(sc);
     }

@@ -88,3 +88,93 @@ def test_device_empty_and_single(gpu_ctx):
     assert gpu_ctx.bh_step(lpe.bh_config(10.0), 1.0)["nodes"] == 0
     gx, gy, st = device(gpu_ctx, lpe.bh_config(10.0), [5.0], [5.0], [1.0], [2.0], [1e9], 1.0)
     assert st["nodes"] == 1 and gx[0] == 1.0 and gy[0] == 2.0
+
+
+def _planet_world(n=48, seed=4, U=2000.0):
+    """Massive circles far apart (no contacts): only Barnes-Hut couples them."""
+    rng = np.random.default_rng(seed)
+    b = scenes.Bodies()
+    scenes.add_walls(b, U)
+    g = int(np.ceil(np.sqrt(n)))
+    for i in range(n):
+        x = 200.0 + (i % g) * 150.0 + rng.uniform(-20, 20)
+        y = 200.0 + (i // g) * 150.0 + rng.uniform(-20, 20)
+        b.add(x=x, y=y, vx=rng.normal(0, 0.1), vy=rng.normal(0, 0.1), mass=10.0 ** rng.uniform(11, 14),
+              circle=True, radius=1.0, shape_size=1.0, has_angvel=True, has_inertia=True, inertia=1.0)
+    return scenes.to_bodies(b), U
+
+
+def test_world_tick_runs_barnes_hut(gpu_ctx, oracle_mod):
+    """lpe_world_tick's BarnesHutSystem (position 5 of sim.cpp:107-114) equals the
+    systems run one by one: boundary + gravity, collision, Barnes-Hut on the
+    bodies in EnTT view order (last body first, walls excluded) through the
+    restatement, rotation + movement + sleep."""
+    (bodies, verts), U = _planet_world()
+    cfg = lpe.rigid_config(universe=U)
+    dt = 1.0 / 120.0
+    w = lpe.Context(0)
+    try:
+        w.rigid_set_config(cfg)
+        w.rigid_upload(bodies, verts)
+        w.world_tick(dt, 1)
+        got = w.rigid_download()
+    finally:
+        w.close()
+    m = lpe.Context(0)
+    try:
+        m.rigid_set_config(cfg)
+        m.rigid_upload(bodies, verts)
+        m.rigid_integrate(lpe.SYS_BOUNDARY | lpe.SYS_GRAVITY, dt)
+        m.rigid_step(stats=False)
+        mid = m.rigid_download()
+        sel = [i for i in range(len(mid))[::-1]
+               if (mid[i]["flags"] & lpe.BODY_HAS_MASS) and not (mid[i]["flags"] & lpe.BODY_BOUNDARY)]
+        bc = lpe.bh_config(U)
+        vx, vy, st = oracle_mod.bh_step(bc, mid["x"][sel], mid["y"][sel], mid["vx"][sel], mid["vy"][sel],
+                                        mid["mass"][sel], dt)
+        assert st["skipped"] == 0 and st["nodes"] > len(sel)
+        mid["vx"][sel] = vx
+        mid["vy"][sel] = vy
+        m.rigid_upload(mid, verts)
+        m.rigid_integrate(lpe.SYS_ROTATION | lpe.SYS_MOVEMENT | lpe.SYS_SLEEP, dt)
+        ref = m.rigid_download()
+    finally:
+        m.close()
+    assert np.any(ref["vx"] != bodies["vx"])
+    for k in ("x", "y", "vx", "vy", "angle", "omega"):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+def test_world_tick_barnes_hut_off_and_fluid_guard(gpu_ctx):
+    (bodies, verts), U = _planet_world(n=16)
+    dt = 1.0 / 120.0
+    a, b = lpe.Context(0), lpe.Context(0)
+    try:
+        for c in (a, b):
+            c.rigid_set_config(lpe.rigid_config(universe=U))
+            c.rigid_upload(bodies, verts)
+        b.world_set_barnes_hut(False)
+        a.world_tick(dt, 1)
+        b.world_tick(dt, 1)
+        assert np.any(a.rigid_download()["vx"] != b.rigid_download()["vx"])
+    finally:
+        a.close()
+        b.close()
+    # a heavy world with fluid particles: strict mode only (fails loudly)
+    hb = scenes.Bodies()
+    scenes.add_walls(hb, 20.0)
+    for i in range(4):
+        hb.add(x=4.0 + 4.0 * i, y=6.0, mass=1e12, circle=True, radius=0.5, shape_size=0.5, has_angvel=True,
+               has_inertia=True)
+    hbod, hverts = scenes.to_bodies(hb)
+    fl = scenes.fluid_lattice(np.random.default_rng(1), 8, 8, 8.0, 14.0)
+    c = lpe.Context(0)
+    try:
+        c.rigid_set_config(lpe.rigid_config(universe=20.0))
+        c.rigid_upload(hbod, hverts)
+        c.sph_set_config(lpe.default_fluid_config())
+        c.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+        with pytest.raises(lpe.LpeError, match="STATE|strict"):
+            c.world_tick(dt, 1)
+    finally:
+        c.close()
