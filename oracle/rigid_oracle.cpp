@@ -648,13 +648,24 @@ extern "C" int lpeo_position_solver(const lpe_rigid_config *cfg, int nb, lpe_bod
  * the pairs that produced contacts are edge-coloured so that no two pairs of
  * one colour share a movable body (finite mass or rotatable), by rounds: every
  * uncoloured pair claims its movable bodies with the priority (hash(p), p),
- * the lowest wins a body, and a pair that won all its bodies takes the lowest
- * colour free on both.  Visiting order: colour-major, pairs ascending inside a colour, each
- * pair's contacts in narrowphase order.  The reference's PGS order is an
+ * the lowest wins a body, and a pair that won all its bodies takes a colour
+ * free on both: with more pairs than one solver slot (1024), the first free
+ * colour of the first K = ceil(pairs / 960) in the rotation r = hash(p ^
+ * 0x9e3779b9) * K >> 32 (colours r, r + 1, .. mod K), else the lowest free
+ * colour; balanced colours of <= 1024 pairs are one solver slot each.
+ * Visiting order: colour-major, pairs ascending inside a colour, each pair's contacts in narrowphase order.  The reference's PGS order is an
  * unordered_map's (contact_manager.cpp:169-245); pairs of one colour touch
  * disjoint movable bodies, so any order inside a colour is bit-identical.
  * contacts must be grouped by pair (narrowphase order).  Returns the number
  * of colours, or -1 if more than 64 would be needed. */
+uint32_t colour_hash(uint32_t x) {                /* lpe_rigid.hip colour_hash */
+    x ^= x >> 16; x *= 0x7feb352du;
+    x ^= x >> 15; x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+constexpr int COLOUR_SLOT = 1024;                    /* lpe_rigid.hip SOLVE_TPB */
+
 extern "C" int lpeo_colour_order(int nb, const lpe_body *bodies, int nc, const lpe_contact *cs,
                                  int32_t *order, int32_t *pair_colour, int npairs) {
     auto dep = [&](int i) {
@@ -678,12 +689,10 @@ extern "C" int lpeo_colour_order(int nb, const lpe_body *bodies, int nc, const l
     const unsigned long long NONE = ~0ull;
     std::vector<unsigned long long> claim(nb, NONE);
     auto prio = [&](int p) {
-        uint32_t x = (uint32_t)p;                 /* lpe_rigid.hip colour_hash */
-        x ^= x >> 16; x *= 0x7feb352du;
-        x ^= x >> 15; x *= 0x846ca68bu;
-        x ^= x >> 16;
-        return ((unsigned long long)x << 32) | (uint32_t)p;
+        return ((unsigned long long)colour_hash((uint32_t)p) << 32) | (uint32_t)p;
     };
+    const int FILL = COLOUR_SLOT - COLOUR_SLOT / 16;
+    const int K = m > COLOUR_SLOT ? std::min((m + FILL - 1) / FILL, 64) : 0;
     for (int left = m; left > 0;) {
         for (int q = 0; q < m; q++) {
             if (col[q] != -2) continue;
@@ -697,8 +706,19 @@ extern "C" int lpeo_colour_order(int nb, const lpe_body *bodies, int nc, const l
             if ((a < 0 || claim[a] == prio(pid[q])) && (b < 0 || claim[b] == prio(pid[q]))) {
                 unsigned long long forb = (a >= 0 ? used[a] : 0ull) | (b >= 0 ? used[b] : 0ull);
                 if (forb == ~0ull) return -1;
-                int c = 0;
-                while (forb & (1ull << c)) c++;
+                int c = -1;
+                if (K > 0) {                          /* the first free of the first K, rotated by r */
+                    const uint32_t r = (uint32_t)(((unsigned long long)colour_hash((uint32_t)pid[q] ^ 0x9e3779b9u) *
+                                                   (unsigned)K) >> 32);
+                    for (int i = 0; i < K && c < 0; i++) {
+                        const int k = (int)((r + (uint32_t)i) % (uint32_t)K);
+                        if (!((forb >> k) & 1ull)) c = k;
+                    }
+                }
+                if (c < 0) {
+                    c = 0;
+                    while (forb & (1ull << c)) c++;
+                }
                 col[q] = -3 - c;
                 won.push_back(q);
             }
