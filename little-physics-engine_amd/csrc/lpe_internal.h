@@ -7,6 +7,7 @@
 #include <string>
 #include <vector>
 #include <utility>
+#include <functional>
 #include "../../include/lpe.h"
 
 namespace lpe {
@@ -89,7 +90,7 @@ struct SphDev {
     // never P, so it can be voided at any time (sph_void_prelaunch) and may
     // outlive the lpe_world_tick call that launched it
     hipStream_t pside = nullptr;
-    hipEvent_t preReady = nullptr, preDone = nullptr;
+    hipEvent_t preReady = nullptr, preDone = nullptr, fbgDone = nullptr;
     bool pre = false;
     double pre_dt = 0.0;
     int diag = 0;                 // count the ST_NL_OVERFLOW / ST_RIGID_CAND / ST_NEIGH stats
@@ -206,13 +207,15 @@ static inline int lpe_grow(lpe_ctx *ctx, T **p, int *cap, long want, long elems_
 int lpe_rigid_destroy_internal(lpe_ctx *ctx);
 // world tick: rigid collision detection overlapped with the fluid step (lpe_rigid.hip)
 int rigid_tick_begin(lpe_ctx *ctx);
-int rigid_tick_boundary(lpe_ctx *ctx);
+int rigid_tick_boundary(lpe_ctx *ctx, bool gravity = false, double dt_state = 0.0);   // + BasicGravity fused
 int rigid_tick_detect(lpe_ctx *ctx);   // host half of the detection + colouring launch
 int rigid_tick_hook(lpe_ctx *ctx, int step);   // fluid-step hook (after each sub-step's forces)
 int rigid_tick_finish(lpe_ctx *ctx);
 // lpe_sph_step with a host callback after the forces of sub-step `after`
 int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int));
-int sph_prelaunch(lpe_ctx *ctx, double dt_tick);
+// first (optional): launched on the side stream ahead of the prelaunch (the
+// tick's own fluid boundary / gravity pass); fbgDone is recorded after it
+int sph_prelaunch(lpe_ctx *ctx, double dt_tick, const std::function<int(hipStream_t)> &first = {});
 int lpe_sph_cover_box(lpe_ctx *ctx, double x0, double y0, double x1, double y1);
 // coupling rigids' device arrays (rig, accum, acq) for n rigids (grow-only)
 int sph_alloc_rigids(lpe_ctx *ctx, int n);

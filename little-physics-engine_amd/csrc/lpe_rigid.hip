@@ -1906,13 +1906,7 @@ __global__ void k_boundary_pos(int nb, lpe_body *__restrict__ bodies, double m, 
     }
     bits[i] = f;
 }
-__global__ void k_boundary_vel(int nb, lpe_body *__restrict__ bodies, const int32_t *__restrict__ bits,
-                               double damp, double maxSpeed) {
-    int i = blockIdx.x * RTPB + threadIdx.x;
-    if (i >= nb) return;
-    const int f = bits[i];
-    if (!f) return;
-    lpe_body &b = bodies[i];
+__device__ __forceinline__ void boundary_vel_one(lpe_body &b, int f, double damp, double maxSpeed) {
     double vx = b.vx, vy = b.vy;
     if (f & 1) vx = fabs(vx) * damp;
     else if (f & 2) vx = -fabs(vx) * damp;
@@ -1921,6 +1915,14 @@ __global__ void k_boundary_vel(int nb, lpe_body *__restrict__ bodies, const int3
     double sp = sqrt(vx * vx + vy * vy);
     if (sp > maxSpeed) { vx = (vx / sp) * maxSpeed; vy = (vy / sp) * maxSpeed; }
     b.vx = vx; b.vy = vy;
+}
+__global__ void k_boundary_vel(int nb, lpe_body *__restrict__ bodies, const int32_t *__restrict__ bits,
+                               double damp, double maxSpeed) {
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb) return;
+    const int f = bits[i];
+    if (!f) return;
+    boundary_vel_one(bodies[i], f, damp, maxSpeed);
 }
 __device__ __forceinline__ bool gravity_view(const lpe_body &b) {
     return (b.flags & LPE_BODY_HAS_PHASE) && (b.flags & LPE_BODY_HAS_VEL) &&
@@ -1938,13 +1940,23 @@ __global__ void k_gravity(int nb, lpe_body *__restrict__ bodies, double g, doubl
     if (i >= nb || *heavy) return;
     if (gravity_view(bodies[i])) bodies[i].vy += g * dt;
 }
-__global__ void k_rotation(int nb, lpe_body *__restrict__ bodies, double dt, double damping,
-                           double maxw) {   // rotation.cpp:18-60
+// BoundarySystem's velocity half then BasicGravitySystem, per body (the world
+// tick: nothing between them touches the bodies)
+__global__ void k_boundary_vel_gravity(int nb, lpe_body *__restrict__ bodies, const int32_t *__restrict__ bits,
+                                       double damp, double maxSpeed, double g, double dt,
+                                       const int32_t *__restrict__ heavy) {
     int i = blockIdx.x * RTPB + threadIdx.x;
     if (i >= nb) return;
-    lpe_body b = bodies[i];
-    if (!(b.flags & LPE_BODY_HAS_ANGPOS) || !(b.flags & LPE_BODY_HAS_ANGVEL)) return;
-    if (b.flags & LPE_BODY_BOUNDARY) return;
+    const int f = bits[i];
+    lpe_body &b = bodies[i];
+    if (f) boundary_vel_one(b, f, damp, maxSpeed);
+    if (!*heavy && gravity_view(b)) b.vy += g * dt;
+}
+// RotationSystem, MovementSystem, SleepSystem on one body (each returns
+// whether it wrote the body; the kernels below store it back only then)
+__device__ __forceinline__ bool rotation_one(lpe_body &b, double dt, double damping, double maxw) {   // rotation.cpp:18-60
+    if (!(b.flags & LPE_BODY_HAS_ANGPOS) || !(b.flags & LPE_BODY_HAS_ANGVEL)) return false;
+    if (b.flags & LPE_BODY_BOUNDARY) return false;
     const double Pi = 3.141592654;
     b.angle += b.omega * dt;
     if (damping < 1.0) b.omega *= damping;
@@ -1954,25 +1966,18 @@ __global__ void k_rotation(int nb, lpe_body *__restrict__ bodies, double dt, dou
     }
     if (b.angle > 2.0 * Pi) b.angle -= 2.0 * Pi;
     else if (b.angle < 0) b.angle += 2.0 * Pi;
-    bodies[i] = b;
+    return true;
 }
-__global__ void k_movement(int nb, lpe_body *__restrict__ bodies, double dt) {  // movement.cpp:13-39
-    int i = blockIdx.x * RTPB + threadIdx.x;
-    if (i >= nb) return;
-    lpe_body b = bodies[i];
-    if (!(b.flags & LPE_BODY_HAS_VEL) || (b.flags & LPE_BODY_BOUNDARY)) return;
-    if ((b.flags & LPE_BODY_HAS_PHASE) && (b.flags & LPE_BODY_LIQUID)) return;
+__device__ __forceinline__ bool movement_one(lpe_body &b, double dt) {   // movement.cpp:13-39
+    if (!(b.flags & LPE_BODY_HAS_VEL) || (b.flags & LPE_BODY_BOUNDARY)) return false;
+    if ((b.flags & LPE_BODY_HAS_PHASE) && (b.flags & LPE_BODY_LIQUID)) return false;
     b.x += b.vx * dt;
     b.y += b.vy * dt;
-    bodies[i] = b;
+    return true;
 }
-__global__ void k_sleep(int nb, lpe_body *__restrict__ bodies, double lin, double ang,
-                        int frames) {   // sleep.cpp:19-67
-    int i = blockIdx.x * RTPB + threadIdx.x;
-    if (i >= nb) return;
-    lpe_body b = bodies[i];
+__device__ __forceinline__ bool sleep_one(lpe_body &b, double lin, double ang, int frames) {   // sleep.cpp:19-67
     const uint32_t need = LPE_BODY_HAS_VEL | LPE_BODY_HAS_PHASE | LPE_BODY_HAS_MASS | LPE_BODY_HAS_SLEEP;
-    if ((b.flags & need) != need || (b.flags & LPE_BODY_BOUNDARY)) return;
+    if ((b.flags & need) != need || (b.flags & LPE_BODY_BOUNDARY)) return false;
     double speed = sqrt(b.vx * b.vx + b.vy * b.vy);
     double as = (b.flags & LPE_BODY_HAS_ANGVEL) ? fabs(b.omega) : 0.0;
     bool asleep = (b.flags & LPE_BODY_ASLEEP) != 0;
@@ -1992,7 +1997,36 @@ __global__ void k_sleep(int nb, lpe_body *__restrict__ bodies, double lin, doubl
     } else {
         b.flags &= ~LPE_BODY_ASLEEP;
     }
-    bodies[i] = b;
+    return true;
+}
+__global__ void k_rotation(int nb, lpe_body *__restrict__ bodies, double dt, double damping, double maxw) {
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb) return;
+    lpe_body b = bodies[i];
+    if (rotation_one(b, dt, damping, maxw)) bodies[i] = b;
+}
+__global__ void k_movement(int nb, lpe_body *__restrict__ bodies, double dt) {
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb) return;
+    lpe_body b = bodies[i];
+    if (movement_one(b, dt)) bodies[i] = b;
+}
+__global__ void k_sleep(int nb, lpe_body *__restrict__ bodies, double lin, double ang, int frames) {
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb) return;
+    lpe_body b = bodies[i];
+    if (sleep_one(b, lin, ang, frames)) bodies[i] = b;
+}
+// the three in one launch (sim.cpp:112-114 order, per body)
+__global__ void k_rotation_movement_sleep(int nb, lpe_body *__restrict__ bodies, double dt_state, double damping,
+                                          double maxw, double dt_move, double lin, double ang, int frames) {
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb) return;
+    lpe_body b = bodies[i];
+    bool w = rotation_one(b, dt_state, damping, maxw);
+    w |= movement_one(b, dt_move);
+    w |= sleep_one(b, lin, ang, frames);
+    if (w) bodies[i] = b;
 }
 
 }  // namespace lpe
@@ -2632,10 +2666,16 @@ int rigid_tick_hook(lpe_ctx *ctx, int step) {
 }
 
 // the boundary system's velocity part, at its place in the tick
-int rigid_tick_boundary(lpe_ctx *ctx) {
+int rigid_tick_boundary(lpe_ctx *ctx, bool gravity, double dt_state) {
     RigidDev *d = rdev(ctx);
     if (d->nb <= 0) return LPE_OK;
     const lpe_rigid_config &c = d->cfg;
+    if (gravity) {   // the planetary-mass check (k_gravity_check) is queued before
+        LPE_KERNEL(ctx, "k_boundary_vel_gravity", k_boundary_vel_gravity, dim3(rblk(d->nb)), dim3(RTPB), 0,
+                   ctx->stream, d->nb, d->bodies, d->bbits, c.bounceDamping, c.maxSpeed, c.gravity, dt_state,
+                   d->counts + 5);
+        return LPE_OK;
+    }
     LPE_KERNEL(ctx, "k_boundary_vel", k_boundary_vel, dim3(rblk(d->nb)), dim3(RTPB), 0, ctx->stream, d->nb,
                d->bodies, d->bbits, c.bounceDamping, c.maxSpeed);
     return LPE_OK;
@@ -2738,6 +2778,12 @@ extern "C" int lpe_rigid_integrate(lpe_ctx *ctx, int systems, double dt_state, d
     }
     if (systems & 2) {
         LPE_KERNEL(ctx, "k_gravity", k_gravity, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, c.gravity, dt_state, d->counts + 5);
+    }
+    if ((systems & (4 | 8 | 16)) == (4 | 8 | 16)) {
+        LPE_KERNEL(ctx, "k_rotation_movement_sleep", k_rotation_movement_sleep, dim3(rblk(nb)), dim3(RTPB), 0, s, nb,
+                   d->bodies, dt_state, c.angularDamping, c.maxAngularSpeed, dt_move, c.linearSleepThreshold,
+                   c.angularSleepThreshold, c.sleepFramesThreshold);
+        systems &= ~(4 | 8 | 16);
     }
     if (systems & 4)
         LPE_KERNEL(ctx, "k_rotation", k_rotation, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, dt_state, c.angularDamping, c.maxAngularSpeed);

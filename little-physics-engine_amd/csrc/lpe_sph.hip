@@ -1947,7 +1947,7 @@ static void sph_free(SphDev &d) {
                     d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.raabb, d.accum, d.acq, d.rbinStart, d.rgrid, d.rmax,
                     d.rbinList, d.rbinCount, d.coupleBody, d.plans};
     for (void *p : ptrs) if (p) (void)hipFree(p);
-    hipEvent_t evs[] = {d.preReady, d.preDone};
+    hipEvent_t evs[] = {d.preReady, d.preDone, d.fbgDone};
     for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
     if (d.pside) (void)hipStreamDestroy(d.pside);
     d = SphDev();
@@ -2569,7 +2569,7 @@ static int sph_migrate(lpe_ctx *ctx) {
 // CU-masked queue (round 1 kept 16 CUs free for the solvers) cost a third of
 // the tick rate on MI355X (396 vs 554 ticks/s on the settled metric scene),
 // while the solvers start promptly without it.
-int sph_prelaunch(lpe_ctx *ctx, double dt_tick) {
+int sph_prelaunch(lpe_ctx *ctx, double dt_tick, const std::function<int(hipStream_t)> &first) {
     SphDev &d = ctx->sph;
     d.pre = false;
     if (d.shard || d.n <= 0 || !d.P.x) return LPE_OK;
@@ -2577,9 +2577,18 @@ int sph_prelaunch(lpe_ctx *ctx, double dt_tick) {
         LPE_HIP(ctx, hipStreamCreateWithFlags(&d.pside, hipStreamNonBlocking));
         LPE_HIP(ctx, hipEventCreateWithFlags(&d.preReady, hipEventDisableTiming));
         LPE_HIP(ctx, hipEventCreateWithFlags(&d.preDone, hipEventDisableTiming));
+        LPE_HIP(ctx, hipEventCreateWithFlags(&d.fbgDone, hipEventDisableTiming));
     }
     LPE_HIP(ctx, hipEventRecord(d.preReady, ctx->stream));
     LPE_HIP(ctx, hipStreamWaitEvent(d.pside, d.preReady, 0));
+    if (first) {
+        const int st0 = first(d.pside);
+        if (st0) {
+            (void)hipStreamSynchronize(d.pside);
+            return st0;
+        }
+        LPE_HIP(ctx, hipEventRecord(d.fbgDone, d.pside));
+    }
     const lpe_fluid_config &c = d.cfg;
     const float subDt = (float)dt_tick / (float)c.numSubSteps;
     const float halfDt = 0.5f * subDt;

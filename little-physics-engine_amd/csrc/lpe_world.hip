@@ -216,25 +216,38 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
         }
         // 2) BoundarySystem, 3) BasicGravitySystem: bodies and fluid
         // (the planetary-mass check spans bodies and fluid, gravity.cpp:43-51)
+        // the bodies' boundary (velocity half) and gravity as one pass when
+        // overlapped (the position half ran in rigid_tick_begin); the fluid's
+        // boundary + gravity pass leads the prelaunch on its side stream
+        // (it touches no body; the context stream joins it at the tick's end)
         int st;
         if (overlap) {
-            st = rigid_tick_boundary(ctx);
-            if (!st) st = lpe_rigid_integrate(ctx, 32, dt_state, dt_move);
+            st = lpe_rigid_integrate(ctx, 32, dt_state, dt_move);
+            if (!st) st = rigid_tick_boundary(ctx, true, dt_state);
         } else {
             st = lpe_rigid_integrate(ctx, 1 | 32, dt_state, dt_move);
         }
         if (st) return st;
-        if (d.n > 0) {
-            LPE_KERNEL(ctx, "k_fluid_boundary_gravity", k_fluid_boundary_gravity, dim3(wblk(d.n)), dim3(256), 0, s, d.n, d.P, rc.marginPixels * rc.metersPerPixel, rc.universeSize, rc.bounceDamping, rc.maxSpeed, rc.gravity, dt_state, rd->nb > 0 ? rd->counts + 5 : (const int32_t *)nullptr, d.fluid_heavy ? 1 : 0);
+        const bool prelaunch = !serial && fluid && !d.shard;
+        const bool fbg_side = prelaunch && d.n > 0 && d.P.x;
+        auto fbg = [&](hipStream_t fs) {
+            LPE_KERNEL(ctx, "k_fluid_boundary_gravity", k_fluid_boundary_gravity, dim3(wblk(d.n)), dim3(256), 0, fs, d.n, d.P, rc.marginPixels * rc.metersPerPixel, rc.universeSize, rc.bounceDamping, rc.maxSpeed, rc.gravity, dt_state, rd->nb > 0 ? rd->counts + 5 : (const int32_t *)nullptr, d.fluid_heavy ? 1 : 0);
+            return LPE_OK;
+        };
+        if (d.n > 0 && !fbg_side) {
+            st = fbg(s);
+            if (st) return st;
         }
-        st = lpe_rigid_integrate(ctx, 2, dt_state, dt_move);
-        if (st) return st;
+        if (!overlap) {
+            st = lpe_rigid_integrate(ctx, 2, dt_state, dt_move);
+            if (st) return st;
+        }
         // the fluid state is final for this tick: the next tick's first
         // sub-step (up to its forces) runs beside the rigid solvers -- also
         // after the last tick of this call, for the next call (it writes only
         // scratch, so downloads and state changes in between are safe)
-        if (!serial && fluid && !d.shard) {
-            st = sph_prelaunch(ctx, dt_fluid);
+        if (prelaunch) {
+            st = fbg_side ? sph_prelaunch(ctx, dt_fluid, fbg) : sph_prelaunch(ctx, dt_fluid);
             if (st) return st;
         }
         // 4) RigidBodyCollisionSystem
@@ -246,6 +259,7 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
         if (st) return st;
         st = lpe_rigid_integrate(ctx, 4 | 8 | 16, dt_state, dt_move);
         if (st) return st;
+        if (fbg_side) LPE_HIP(ctx, hipStreamWaitEvent(s, d.fbgDone, 0));
         LPE_CHECK_LAUNCH(ctx, "world tick");
     }
     return LPE_OK;
