@@ -91,6 +91,7 @@ struct SphDev {
     // outlive the lpe_world_tick call that launched it
     hipStream_t pside = nullptr;
     hipEvent_t preReady = nullptr, preDone = nullptr, fbgDone = nullptr;
+    lpe_body *wb_bodies = nullptr;   // world tick: k_rigid_writeback also scatters to these (coupleBody)
     bool pre = false;
     double pre_dt = 0.0;
     int diag = 0;                 // count the ST_NL_OVERFLOW / ST_RIGID_CAND / ST_NEIGH stats

@@ -1809,7 +1809,8 @@ k_rbin_sort(int B, int32_t *__restrict__ start, int32_t *__restrict__ list, int 
 // exact sums rounded to fp32 (kept in accum_out for download), then zeroed
 __global__ void k_rigid_writeback(int nr, lpe_gpu_rigid *__restrict__ rig,
                                   unsigned long long *__restrict__ acq, float *__restrict__ accum_out,
-                                  float damping) {
+                                  float damping, const int32_t *__restrict__ coupleBody,
+                                  lpe_body *__restrict__ bodies) {
     int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nr) return;
     lpe_gpu_rigid &rb = rig[r];
@@ -1826,6 +1827,11 @@ __global__ void k_rigid_writeback(int nr, lpe_gpu_rigid *__restrict__ rig,
     rb.omega += tq * invInertia;
     rb.omega *= damping;
     rb.accumFx = 0.f; rb.accumFy = 0.f; rb.accumTorque = 0.f;
+    if (bodies) {   // world tick: the velocities straight back to the coupled bodies (fluid.cpp:564-579)
+        lpe_body &b = bodies[coupleBody[r]];
+        if (b.flags & LPE_BODY_HAS_VEL) { b.vx = rb.vx; b.vy = rb.vy; }
+        if (b.flags & LPE_BODY_HAS_ANGVEL) b.omega = rb.omega;
+    }
 }
 
 // reference cell index (metal:224-236) of each particle, written at its id
@@ -2738,7 +2744,7 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
             if (st) return st;
         }
         LPE_KERNEL(ctx, "k_rigid_writeback", k_rigid_writeback, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig,
-                           d.acq, d.accum, c.dampingFactor);
+                           d.acq, d.accum, c.dampingFactor, (const int32_t *)d.coupleBody, d.wb_bodies);
         LPE_CHECK_LAUNCH(ctx, "k_rigid_writeback");
     }
     if (sh) return sph_migrate(ctx);

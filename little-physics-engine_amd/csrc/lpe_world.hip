@@ -66,16 +66,8 @@ __global__ void k_gather_rigids(int nr, const int32_t *__restrict__ coupleBody,
     rig[r] = rb;
 }
 
-// writeBackRigidBodies' ECS part (fluid.cpp:564-579): v and omega of every
-// gathered rigid, fp32 -> double
-__global__ void k_scatter_rigid_vel(int nr, const int32_t *__restrict__ coupleBody,
-                                    const lpe_gpu_rigid *__restrict__ rig, lpe_body *__restrict__ bodies) {
-    int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nr) return;
-    lpe_body &b = bodies[coupleBody[r]];
-    if (b.flags & LPE_BODY_HAS_VEL) { b.vx = rig[r].vx; b.vy = rig[r].vy; }
-    if (b.flags & LPE_BODY_HAS_ANGVEL) b.omega = rig[r].omega;
-}
+// writeBackRigidBodies' ECS part (fluid.cpp:564-579: v and omega of every
+// gathered rigid, fp32 -> double) is k_rigid_writeback's tail (lpe_sph.hip)
 
 // Boundary (boundary.cpp:23-69) then Gravity (gravity.cpp:53-57) on fluid
 // particles (no Sleep component, not Boundary): widen, update, narrow
@@ -209,10 +201,12 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
         if (fluid) {
             // the detection launches after the first sub-step, its host half
             // and the colouring after the third (rigid_tick_hook)
+            // (the write-back of the coupled rigids' velocities scatters them
+            // to their bodies in the same kernel: d.wb_bodies)
+            d.wb_bodies = nr > 0 ? rd->bodies : nullptr;
             int st = sph_step_hooked(ctx, dt_fluid, overlap ? rigid_tick_hook : nullptr);
+            d.wb_bodies = nullptr;
             if (st) return st;
-            if (nr > 0)
-                LPE_KERNEL(ctx, "k_scatter_rigid_vel", k_scatter_rigid_vel, dim3(wblk(nr, 128)), dim3(128), 0, s, nr, d.coupleBody, d.rig, rd->bodies);
         }
         // 2) BoundarySystem, 3) BasicGravitySystem: bodies and fluid
         // (the planetary-mass check spans bodies and fluid, gravity.cpp:43-51)
