@@ -71,6 +71,7 @@ struct SphDev {
     int32_t *rbinStart = nullptr; // rigid bins (absolute grid of bin size bcs)
     int32_t *rbinList = nullptr;
     int32_t *rbinCount = nullptr;
+    int rbin_zero = 0;            // rbinCount[0, rbin_zero) is zero (left so by k_rbin_sort)
     int cap_rbins = 0, cap_rlist = 0;
     float4 *raabb = nullptr;      // coupling rigids' AABBs (minX, maxX, minY, maxY), per tick
     int cap_raabb = 0;

@@ -1778,10 +1778,11 @@ __global__ void k_rbin_fill(int nr, const lpe_gpu_rigid *__restrict__ rig, float
 static constexpr int RBS_WAVES = 4;                        // bins per 256-thread block
 __global__ void __launch_bounds__(256)
 k_rbin_sort(int B, int32_t *__restrict__ start, int32_t *__restrict__ list, int cap,
-            const float4 *__restrict__ aabb, float4 *__restrict__ baabb) {
+            const float4 *__restrict__ aabb, float4 *__restrict__ baabb, int32_t *__restrict__ count) {
     const int b = blockIdx.x * RBS_WAVES + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (b >= B) return;                                     // (whole wave)
+    if (lane == 0) count[b] = 0;                            // the next build's histogram (consumed by the scan)
     const int s = min(start[b], cap), e = min(start[b + 1], cap), n = e - s;
     if (n <= 0) return;
     if (n > 64) {
@@ -1859,8 +1860,9 @@ __global__ void k_unpermute(int n, const int32_t *__restrict__ id, int nf, Field
 }
 
 // the prelaunched sub-step's stats (status[1]) into the step's (status[0])
-__global__ void k_merge_prestats(int32_t *__restrict__ st, int32_t *__restrict__ pre) {
+__global__ void k_merge_prestats(int32_t *__restrict__ st, int32_t *__restrict__ pre, int reset) {
     if (threadIdx.x != 0) return;
+    if (reset) { st[ST_MAX_OCC] = 0; st[ST_OVER_CAP] = 0; st[ST_REF_UB] = 0; }   // sph_reset_step_stats
     st[ST_CAP_OVERFLOW] |= pre[ST_CAP_OVERFLOW];
     st[ST_MAX_OCC] = max(st[ST_MAX_OCC], pre[ST_MAX_OCC]);
     st[ST_NOT_INSERTED] = pre[ST_NOT_INSERTED];
@@ -2344,6 +2346,7 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
         LPE_HIP(ctx, hipMalloc((void **)&d.rbinStart, sizeof(int32_t) * (B + 1)));
         LPE_HIP(ctx, hipMalloc((void **)&d.rbinCount, sizeof(int32_t) * ((size_t)B * 2 + nbs + 4)));
         d.cap_rbins = B;
+        d.rbin_zero = 0;
     }
     hipStream_t s = ctx->stream;
     if (d.nr > d.cap_raabb || !d.raabb) {
@@ -2353,7 +2356,9 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
     }
     LPE_KERNEL(ctx, "k_rig_couple", k_rig_couple, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig,
                d.cfg.impulseSolver.maxSafeVelocitySq, d.raabb);
-    LPE_HIP(ctx, hipMemsetAsync(d.rbinCount, 0, sizeof(int32_t) * B, s));
+    if (B > d.rbin_zero)   // else the previous build's k_rbin_sort left counts [0, B) zeroed
+        LPE_HIP(ctx, hipMemsetAsync(d.rbinCount, 0, sizeof(int32_t) * B, s));
+    d.rbin_zero = 0;
     LPE_KERNEL(ctx, "k_rbin_count", k_rbin_count, dim3(nblk(d.nr, 4)), dim3(256), 0, s, d.nr, d.rig, d.bcs,
                        d.bx0, d.by0, d.bW, d.bH, d.rbinCount);
     int32_t *cursor = d.rbinCount + B;
@@ -2375,8 +2380,9 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
     LPE_KERNEL(ctx, "k_rbin_fill", k_rbin_fill, dim3(nblk(d.nr, 4)), dim3(256), 0, s, d.nr, d.rig, d.bcs,
                        d.bx0, d.by0, d.bW, d.bH, cursor, d.rbinList, d.cap_rlist, d.status);
     LPE_KERNEL(ctx, "k_rbin_sort", k_rbin_sort, dim3((B + RBS_WAVES - 1) / RBS_WAVES), dim3(256), 0, s, B, d.rbinStart, d.rbinList, d.cap_rlist,
-               d.raabb, rbin_aabb(d));
+               d.raabb, rbin_aabb(d), d.rbinCount);
     LPE_CHECK_LAUNCH(ctx, "rbin");
+    d.rbin_zero = B;
     d.rig_dirty = false;
     return LPE_OK;
 }
@@ -2648,13 +2654,15 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
     d.pre = false;
     int st = sph_build_rigid_bins(ctx);
     if (st) return st;
-    st = sph_reset_step_stats(ctx, s, d.status);
-    if (st) return st;
     if (pre) {
         std::swap(d.rho, d.rhoN);                     // sub-step 0's density is the prelaunch's
         std::swap(d.pr, d.prN);
         LPE_HIP(ctx, hipStreamWaitEvent(s, d.preDone, 0));
-        LPE_KERNEL(ctx, "k_merge_prestats", k_merge_prestats, dim3(1), dim3(64), 0, s, d.status, d.status + ST_COUNT);
+        // (resets the step stats as sph_reset_step_stats, then merges)
+        LPE_KERNEL(ctx, "k_merge_prestats", k_merge_prestats, dim3(1), dim3(64), 0, s, d.status, d.status + ST_COUNT, 1);
+    } else {
+        st = sph_reset_step_stats(ctx, s, d.status);
+        if (st) return st;
     }
     SphStepParams sp;
     sp.n = d.n; sp.W = d.W; sp.H = d.H; sp.ox = d.ox; sp.oy = d.oy;
