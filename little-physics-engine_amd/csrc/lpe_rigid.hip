@@ -1091,11 +1091,22 @@ k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
              const int2 *__restrict__ seg, int segLds, const float4 *__restrict__ rowN,
              const float4 *__restrict__ rowR, const int2 *__restrict__ rowAB,
              const float4 *__restrict__ rowM, float *__restrict__ vel, int iters, float mu,
-             float *__restrict__ lamN, float *__restrict__ lamF) {
+             float *__restrict__ lamN, float *__restrict__ lamF, lpe_body *__restrict__ bodies,
+             const int32_t *__restrict__ inContact) {
     extern __shared__ float sv[];   // 3 floats per body
     __shared__ int scb[MAX_COLOURS + 1];
     const int ncol = counts[8];
-    for (int i = threadIdx.x; i < 3 * nb; i += SOLVE_TPB) sv[i] = vel[i];
+    if (bodies) {   // k_pgs_bodies (velocities) in the prologue
+        for (int i = threadIdx.x; i < nb; i += SOLVE_TPB) {
+            const lpe_body &b = bodies[i];
+            const bool cr = can_rotate(b);
+            sv[3 * i] = (float)b.vx;
+            sv[3 * i + 1] = (float)b.vy;
+            sv[3 * i + 2] = cr ? (float)b.omega : 0.f;
+        }
+    } else {
+        for (int i = threadIdx.x; i < 3 * nb; i += SOLVE_TPB) sv[i] = vel[i];
+    }
     for (int c = threadIdx.x; c <= ncol; c += SOLVE_TPB) scb[c] = cbase[c];
     __syncthreads();
     (void)segLds;
@@ -1252,7 +1263,20 @@ k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
         step(bufA, bufB, sgB, sgA);
         if (s + 1 < total) step(bufB, bufA, sgA, sgB);
     }
-    for (int i = threadIdx.x; i < 3 * nb; i += SOLVE_TPB) vel[i] = sv[i];
+    if (total == 0) __syncthreads();   // (no sweep: the prologue's LDS writes)
+    if (bodies) {   // k_pgs_writeback in the epilogue (only the velocity fields: the
+                    // position solver writes the poses of the same bodies concurrently)
+        for (int i = threadIdx.x; i < nb; i += SOLVE_TPB) {
+            if (!inContact[i]) continue;
+            lpe_body &b = bodies[i];
+            if (infinite_mass(b)) continue;
+            b.vx = sv[3 * i];
+            b.vy = sv[3 * i + 1];
+            if (can_rotate(b)) b.omega = sv[3 * i + 2];
+        }
+    } else {
+        for (int i = threadIdx.x; i < 3 * nb; i += SOLVE_TPB) vel[i] = sv[i];
+    }
 }
 
 // a wave that sees no progress for this many passes gives up and raises
@@ -2467,10 +2491,9 @@ static int colour_pos(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
 static int colour_pgs(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     const lpe_rigid_config &c = d->cfg;
     const int nb = d->nb;
-    LPE_KERNEL(ctx, "k_pgs_bodies", k_pgs_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->imii, 2);
+    // (k_pgs_bodies and k_pgs_writeback run as the kernel's prologue / epilogue)
     const size_t lds = sizeof(float) * 3 * (size_t)nb;
-    LPE_KERNEL(ctx, "k_pgs_colour", k_pgs_colour, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts, d->cbase, d->cseg, 0, d->rowN, d->rowR, d->rowAB, d->rowM, d->vel0, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF);
-    LPE_KERNEL(ctx, "k_pgs_writeback", k_pgs_writeback, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->inContact);
+    LPE_KERNEL(ctx, "k_pgs_colour", k_pgs_colour, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts, d->cbase, d->cseg, 0, d->rowN, d->rowR, d->rowAB, d->rowM, d->vel0, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF, d->bodies, (const int32_t *)d->inContact);
     LPE_CHECK_LAUNCH(ctx, "pgs");
     return LPE_OK;
 }
