@@ -68,7 +68,41 @@ host: $(HOSTLIB)
 ref: host
 	$(MAKE) -f oracle/Makefile.ref
 
+# AddressSanitizer + UndefinedBehaviorSanitizer builds of the CPU side
+# (SURVEY.md §5): the oracle (the checker every GPU test compares against),
+# the reference's own rigid sources + driver (oracle/_ref) and the C++ host
+# mirror with its EnTT harness.  Host code only (no device code is
+# instrumented).  tests/test_sanitizers.py runs the CPU checks against them.
+SANFLAGS := -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=undefined
+SAN      := build/asan
+SAN_ORC  := $(patsubst oracle/%.c,$(SAN)/oracle/%.o,$(ORC_SRC)) $(patsubst oracle/%.cpp,$(SAN)/oracle/%.opp,$(ORX_SRC))
+
+$(SAN)/oracle/%.o: oracle/%.c oracle/*.h include/lpe.h
+	@mkdir -p $(dir $@)
+	$(CC) -std=c11 $(OFLAGS) $(SANFLAGS) -c $< -o $@
+
+$(SAN)/oracle/%.opp: oracle/%.cpp oracle/*.h include/lpe.h
+	@mkdir -p $(dir $@)
+	$(CXX) -std=c++17 $(OFLAGS) $(SANFLAGS) -c $< -o $@
+
+$(SAN)/liblpe_oracle.so: $(SAN_ORC)
+	$(CXX) -shared -fPIC -fopenmp $(SANFLAGS) -o $@ $^ -lm
+
+SAN_HOST_OBJ := $(patsubst $(HOSTDIR)/%.cpp,$(SAN)/host/%.o,$(HOST_SRC))
+
+$(SAN)/host/%.o: $(HOSTDIR)/%.cpp $(HOST_HDR)
+	@mkdir -p $(dir $@)
+	$(CXX) $(HOSTFLAGS) $(SANFLAGS) -c $< -o $@
+
+$(SAN)/liblpe_systems.so: $(SAN_HOST_OBJ) $(LIB)
+	$(CXX) -shared -fPIC $(SANFLAGS) -o $@ $(SAN_HOST_OBJ) -L$(PKG) -llpe_hip \
+	    -Wl,-rpath,$(abspath $(PKG)) -Wl,-rpath,/opt/rocm/lib
+
+asan: $(SAN)/liblpe_oracle.so
+	@if [ -d "$(REF)/src" ]; then $(MAKE) $(SAN)/liblpe_systems.so && \
+	    $(MAKE) -f oracle/Makefile.ref sanitized; fi
+
 clean:
 	rm -rf build $(LIB) $(ORACLE) $(HOSTLIB) oracle/_ref
 
-.PHONY: all ref host clean
+.PHONY: all ref host clean asan

@@ -525,7 +525,7 @@ extern "C" int lpe_world_set_barnes_hut(lpe_ctx *ctx, int enable, const lpe_bh_c
 // cached.  Fluid particles are entities with Position + Mass too; a world
 // whose fluid would make the system act fails loudly (its velocities live
 // in fp32 on the device: strict mode runs it through lpe_bh_step).
-int bh_world_tick(lpe_ctx *ctx, double dt_state) {
+int bh_world_prepare(lpe_ctx *ctx) {
     BhDev &d = bh_dev(ctx);
     if (!d.w_on) return LPE_OK;
     RigidDev *rd = (RigidDev *)ctx->rigid;
@@ -539,11 +539,21 @@ int bh_world_tick(lpe_ctx *ctx, double dt_state) {
     }
     const unsigned rgen = rd ? rd->gen : 0u;
     if (!d.w_valid || d.w_rgen != rgen || d.w_sgen != sd.upload_gen) {
+        // the reads below see the bodies and the fluid masses after every
+        // kernel queued so far (k_forces_couple rewrites P.m in sorted order)
+        LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
         std::vector<lpe_body> hb(nb);
         if (nb) {
-            LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
-            LPE_HIP(ctx, hipMemcpy(hb.data(), rd->bodies, sizeof(lpe_body) * nb, hipMemcpyDeviceToHost));
+            LPE_HIP(ctx, hipMemcpyAsync(hb.data(), rd->bodies, sizeof(lpe_body) * nb, hipMemcpyDeviceToHost,
+                                        ctx->stream));
         }
+        const bool fluid_m = sd.n > 0 && !sd.shard && sd.P.m;
+        std::vector<float> fm(fluid_m ? sd.n : 0);
+        if (fluid_m) {
+            LPE_HIP(ctx, hipMemcpyAsync(fm.data(), sd.P.m, sizeof(float) * sd.n, hipMemcpyDeviceToHost,
+                                        ctx->stream));
+        }
+        LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
         const double thr = cfg.small_mass_threshold;
         auto inserted = [](const lpe_body &b) {
             return (b.flags & LPE_BODY_HAS_MASS) && !(b.flags & LPE_BODY_BOUNDARY);
@@ -564,11 +574,7 @@ int bh_world_tick(lpe_ctx *ctx, double dt_state) {
         bool heavy = thr <= 0.0;
         for (int i : ord) heavy = heavy || hb[i].mass >= thr;
         bool fheavy = false;
-        if (sd.n > 0 && !sd.shard && sd.P.m) {
-            std::vector<float> fm(sd.n);
-            LPE_HIP(ctx, hipMemcpy(fm.data(), sd.P.m, sizeof(float) * sd.n, hipMemcpyDeviceToHost));
-            for (float v : fm) fheavy = fheavy || thr <= 0.0 || (double)v >= thr;
-        }
+        for (float v : fm) fheavy = fheavy || thr <= 0.0 || (double)v >= thr;
         int st = bh_alloc(ctx, d, std::max((int)ord.size(), 1));
         if (st) return st;
         if ((int)ord.size() > d.w_cap) {
@@ -586,10 +592,25 @@ int bh_world_tick(lpe_ctx *ctx, double dt_state) {
         d.w_sgen = sd.upload_gen;
         d.w_valid = true;
     }
-    if (!d.w_active) return LPE_OK;
-    if (d.w_fluid_heavy) {
+    if (d.w_active && d.w_fluid_heavy) {
         ctx->err = "Barnes-Hut would act on a world with fluid particles: run it in strict mode (lpe_bh_step)";
         return LPE_ERR_STATE;
+    }
+    return LPE_OK;
+}
+
+int bh_world_tick(lpe_ctx *ctx, double dt_state) {
+    BhDev &d = bh_dev(ctx);
+    if (!d.w_on) return LPE_OK;
+    int st0 = bh_world_prepare(ctx);
+    if (st0) return st0;
+    if (!d.w_active) return LPE_OK;
+    RigidDev *rd = (RigidDev *)ctx->rigid;
+    lpe_bh_config cfg;
+    if (d.w_cfg_set) cfg = d.w_cfg;
+    else {
+        lpe_bh_config_default(&cfg);
+        cfg.universe_size = rd ? rd->cfg.universeSize : 0.0;
     }
     if (d.w_n == 0) return LPE_OK;
     int st = bh_alloc(ctx, d, d.w_n);

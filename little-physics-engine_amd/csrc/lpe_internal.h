@@ -229,3 +229,7 @@ int lpe_bh_destroy_internal(lpe_ctx *ctx);
 // BarnesHutSystem inside lpe_world_tick (lpe_bh.hip): on the rigid context's
 // bodies, between the collision system and rotation (sim.cpp:107-114)
 int bh_world_tick(lpe_ctx *ctx, double dt_state);
+// its early-exit decision and fluid guard (cached per upload / config change):
+// lpe_world_tick calls it before queuing any work, so a world the system
+// cannot run fails before the tick starts
+int bh_world_prepare(lpe_ctx *ctx);

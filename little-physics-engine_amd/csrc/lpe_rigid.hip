@@ -29,6 +29,7 @@
 // and std::unordered_map orders bit for bit.
 #include "lpe_internal.h"
 #include "rigid_dev.h"
+#include "lpe_trig.h"
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -154,7 +155,7 @@ __device__ D2 support1(const DShape &s, D2 d) {
         if (len > 1e-9) { dn.x /= len; dn.y /= len; }
         return d2(s.pos.x + dn.x * s.radius, s.pos.y + dn.y * s.radius);
     }
-    double c = cos(s.angle), sn = sin(s.angle);                   // polygon.hpp:55-76
+    double c = lpe_cos(s.angle), sn = lpe_sin(s.angle);                 // polygon.hpp:55-76
     double best = -1e9;
     D2 bp = d2(0.0, 0.0);
     for (int i = 0; i < s.nv; i++) {
@@ -259,8 +260,8 @@ __device__ bool epa(const DShape &A, const DShape &B, const D2 *simplex, D2 &n, 
 __device__ __forceinline__ void world_verts(const DShape &s, D2 *v) {  // narrowphase.cpp:56-81
     for (int i = 0; i < s.nv; i++) {
         double lx = s.lv[2 * i], ly = s.lv[2 * i + 1];
-        double rx = lx * cos(s.angle) - ly * sin(s.angle);
-        double ry = lx * sin(s.angle) + ly * cos(s.angle);
+        double rx = lx * lpe_cos(s.angle) - ly * lpe_sin(s.angle);
+        double ry = lx * lpe_sin(s.angle) + ly * lpe_cos(s.angle);
         v[i] = d2(s.pos.x + rx, s.pos.y + ry);
     }
 }
@@ -300,8 +301,8 @@ __global__ void k_rb_prep(int nb, const lpe_body *__restrict__ bodies, const dou
         const double *lv = verts + 2 * (size_t)b.vert_off;
         for (int k = 0; k < b.vert_cnt; k++) {
             double vx = lv[2 * k], vy = lv[2 * k + 1];
-            double rx = vx * cos(angle) - vy * sin(angle);
-            double ry = vx * sin(angle) + vy * cos(angle);
+            double rx = vx * lpe_cos(angle) - vy * lpe_sin(angle);
+            double ry = vx * lpe_sin(angle) + vy * lpe_cos(angle);
             double wx = b.x + rx, wy = b.y + ry;
             if (wx < mnx) mnx = wx;
             if (wx > mxx) mxx = wx;

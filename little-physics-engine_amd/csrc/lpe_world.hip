@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include "rigid_dev.h"
 #include "sph_coupling.h"
+#include "lpe_trig.h"
 #include <algorithm>
 #include <cmath>
 #include <vector>
@@ -47,7 +48,8 @@ __global__ void k_gather_rigids(int nr, const int32_t *__restrict__ coupleBody,
         rb.radius = 0.f;
         int cnt = min(b.vert_cnt, LPE_MAX_POLY_VERTS);
         rb.vertCount = cnt;
-        double c = cos((double)rb.angle), s = sin((double)rb.angle);
+        // std::cos(float) (fluid.cpp:399-400: rb.angle is a float)
+        double c = (double)lpe_cosf(rb.angle), s = (double)lpe_sinf(rb.angle);
         float mnx = 3.402823466e38f, mxx = -3.402823466e38f, mny = 3.402823466e38f, mxy = -3.402823466e38f;
         const double *lv = verts + 2 * (size_t)b.vert_off;
         for (int i = 0; i < cnt; i++) {
@@ -181,6 +183,12 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
         int st = lpe_sph_cover_box(ctx, -1.0, -1.0, U + 1.0, U + 1.0);
         if (st) return st;
     }
+    {
+        // BarnesHutSystem's guard (a fluid world it would act on) before any
+        // work of the tick is queued
+        int st = bh_world_prepare(ctx);
+        if (st) return st;
+    }
     // collision detection overlapped with the fluid step (LPE_SERIAL_TICK=1:
     // everything on the context stream, in the systems' order)
     const char *ser = std::getenv("LPE_SERIAL_TICK");
@@ -244,15 +252,21 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
             st = fbg_side ? sph_prelaunch(ctx, dt_fluid, fbg) : sph_prelaunch(ctx, dt_fluid);
             if (st) return st;
         }
+        // an error past this point still joins the side stream's fluid
+        // boundary / gravity pass (it writes P), so later calls cannot race it
+        auto fail = [&](int code) {
+            if (fbg_side) (void)hipStreamWaitEvent(s, d.fbgDone, 0);
+            return code;
+        };
         // 4) RigidBodyCollisionSystem
         st = overlap ? rigid_tick_finish(ctx) : lpe_rigid_step(ctx, nullptr);
-        if (st) return st;
+        if (st) return fail(st);
         // 5) BarnesHut (its small-mass early exit cached until an upload), 6) Rotation,
         // 7) Movement, 8) Sleep
         st = bh_world_tick(ctx, dt_state);
-        if (st) return st;
+        if (st) return fail(st);
         st = lpe_rigid_integrate(ctx, 4 | 8 | 16, dt_state, dt_move);
-        if (st) return st;
+        if (st) return fail(st);
         if (fbg_side) LPE_HIP(ctx, hipStreamWaitEvent(s, d.fbgDone, 0));
         LPE_CHECK_LAUNCH(ctx, "world tick");
     }

@@ -15,6 +15,7 @@
 #include "entities/entity_components.hpp"
 #include "lpe_backend.hpp"
 #include "math/polygon.hpp"
+#include "../csrc/lpe_trig.h"
 
 namespace Systems
 {
@@ -138,7 +139,9 @@ std::vector<GPURigidBody> FluidSystem::gatherRigidBodies(
             int cnt = (int)poly->vertices.size();
             if (cnt > GPU_POLYGON_MAX_VERTS) cnt = GPU_POLYGON_MAX_VERTS;
             rb.vertCount = cnt;
-            double c = std::cos(rb.angle), s = std::sin(rb.angle);
+            // std::cos(float) as the reference (rb.angle is a float), evaluated by
+            // the implementation the device and the oracle share (csrc/lpe_trig.h)
+            double c = lpe_cosf(rb.angle), s = lpe_sinf(rb.angle);
             float mnx = std::numeric_limits<float>::max(), mxx = -std::numeric_limits<float>::max();
             float mny = std::numeric_limits<float>::max(), mxy = -std::numeric_limits<float>::max();
             for (int i = 0; i < cnt; i++)

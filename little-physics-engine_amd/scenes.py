@@ -136,7 +136,9 @@ def fluid_lattice(rng, nx, ny, x0, y0, s=LATTICE_S, mass=FLUID_MASS):
 def gather_rigids(b: Bodies, order=None) -> np.ndarray:
     """FluidSystem::gatherRigidBodies (fluid.cpp:304-438) for the given body
     order: float pose, polygon world verts computed in double from
-    float(angle) and cast to float, AABB of the float verts; circles use
+    cos/sin of float(angle) in float precision (the reference calls
+    std::cos(float), fluid.cpp:399-400) and cast to float, AABB of the float
+    verts; circles use
     float radius.  Missing mass/inertia default to 1."""
     idx = list(range(len(b))) if order is None else list(order)
     out = np.zeros(len(idx), RIGID_DTYPE)
@@ -162,8 +164,8 @@ def gather_rigids(b: Bodies, order=None) -> np.ndarray:
             verts = r["verts"][:MAX_POLY_VERTS]
             rb["shapeType"] = 1
             rb["vertCount"] = len(verts)
-            c = math.cos(float(angle))
-            s = math.sin(float(angle))
+            c = float(np.float32(math.cos(float(angle))))
+            s = float(np.float32(math.sin(float(angle))))
             wx = np.array([r["x"] + (lx * c - ly * s) for lx, ly in verts], np.float64)
             wy = np.array([r["y"] + (lx * s + ly * c) for lx, ly in verts], np.float64)
             fx = wx.astype(np.float32)

@@ -13,7 +13,9 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(HERE, "liblpe_oracle.so")
+# LPE_ORACLE_LIB / LPE_REF_LIB: the ASan+UBSan builds (Makefile `asan`,
+# tests/test_sanitizers.py)
+LIB_PATH = os.environ.get("LPE_ORACLE_LIB") or os.path.join(HERE, "liblpe_oracle.so")
 
 import sys as _sys
 
@@ -173,6 +175,15 @@ def _rigid_lib():
     return L
 
 
+def set_libm_trig(on: bool):
+    """Rigid restatement's trigonometry: the platform libm as the reference
+    calls it (on: checking the reference fixtures bit for bit) or the portable
+    implementation the device shares (off, the default: device parity)."""
+    L = _rigid_lib()
+    L.lpeo_set_libm_trig.argtypes = [C.c_int]
+    L.lpeo_set_libm_trig(1 if on else 0)
+
+
 def _bodies(b):
     return np.ascontiguousarray(b, dtype=lpe.BODY_DTYPE).copy()
 
@@ -269,7 +280,7 @@ def integrate(cfg, bodies, which, dt=None):
 # ---------------------------------------------------------------------------
 # the reference itself (oracle/_ref/liblpe_ref.so, built by oracle/Makefile.ref
 # only where /root/reference exists)
-REF_PATH = os.path.join(HERE, "_ref", "liblpe_ref.so")
+REF_PATH = os.environ.get("LPE_REF_LIB") or os.path.join(HERE, "_ref", "liblpe_ref.so")
 
 
 def ref_available():

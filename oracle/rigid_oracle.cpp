@@ -31,6 +31,21 @@
 #include <cstring>
 #include <limits>
 #include <vector>
+#include "../little-physics-engine_amd/csrc/lpe_trig.h"
+
+/* Trigonometry of the restatement.  Portable (default): the implementation
+ * the device shares (csrc/lpe_trig.h), so device and oracle agree bit for
+ * bit.  libm (lpeo_set_libm_trig(1)): the platform's std::cos/std::sin, as
+ * the reference calls them -- the mode the reference fixtures are checked
+ * in (tests/test_oracle_rigid.py), bit for bit; the two modes differ only by
+ * the libm's last-bit rounding (<= 1 ulp). */
+static int g_libm_trig = 0;
+extern "C" void lpeo_set_libm_trig(int on) { g_libm_trig = on != 0; }
+static inline double ocos(double x) { return g_libm_trig ? std::cos(x) : lpe_cos(x); }
+static inline double osin(double x) { return g_libm_trig ? std::sin(x) : lpe_sin(x); }
+/* the fluid gather's std::cos(float) (fluid.cpp:399-400: rb.angle is a float) */
+static inline float ocosf(float x) { return g_libm_trig ? std::cos(x) : lpe_cosf(x); }
+static inline float osinf(float x) { return g_libm_trig ? std::sin(x) : lpe_sinf(x); }
 
 namespace {
 
@@ -75,7 +90,7 @@ Shape shape_of(const lpe_body &b, const double *verts) {
 
 /* supportPolygon (polygon.hpp:55-76) */
 V2 support_poly(const Shape &s, const V2 &d) {
-    double c = std::cos(s.angle), sn = std::sin(s.angle);
+    double c = ocos(s.angle), sn = osin(s.angle);
     double bestProj = -1e9;
     V2 best;
     for (int i = 0; i < s.nv; i++) {
@@ -210,14 +225,14 @@ std::vector<V2> world_verts(const Shape &s) {
         double step = (2.0 * M_PI) / samples;
         for (int i = 0; i < samples; i++) {
             double a = i * step + s.angle;
-            v.emplace_back(s.pos.x + s.radius * std::cos(a), s.pos.y + s.radius * std::sin(a));
+            v.emplace_back(s.pos.x + s.radius * ocos(a), s.pos.y + s.radius * osin(a));
         }
         return v;
     }
     for (int i = 0; i < s.nv; i++) {
         double lx = s.lv[2 * i], ly = s.lv[2 * i + 1];
-        double rx = lx * std::cos(s.angle) - ly * std::sin(s.angle);
-        double ry = lx * std::sin(s.angle) + ly * std::cos(s.angle);
+        double rx = lx * ocos(s.angle) - ly * osin(s.angle);
+        double ry = lx * osin(s.angle) + ly * ocos(s.angle);
         v.emplace_back(s.pos.x + rx, s.pos.y + ry);
     }
     return v;
@@ -303,8 +318,8 @@ void aabb(const lpe_body &b, const double *verts, double &mnx, double &mny, doub
     const double *lv = verts + 2 * (size_t)b.vert_off;
     for (int i = 0; i < b.vert_cnt; i++) {
         double vx = lv[2 * i], vy = lv[2 * i + 1];
-        double rx = vx * std::cos(angle) - vy * std::sin(angle);
-        double ry = vx * std::sin(angle) + vy * std::cos(angle);
+        double rx = vx * ocos(angle) - vy * osin(angle);
+        double ry = vx * osin(angle) + vy * ocos(angle);
         double wx = b.x + rx, wy = b.y + ry;
         if (wx < mnx) mnx = wx;
         if (wx > mxx) mxx = wx;
@@ -910,7 +925,8 @@ static lpe_gpu_rigid gather_rigid(const lpe_body &b, const double *verts) {
         rb.shapeType = 1;
         int cnt = std::min(b.vert_cnt, (int)LPE_MAX_POLY_VERTS);
         rb.vertCount = cnt;
-        double c = std::cos((double)rb.angle), s = std::sin((double)rb.angle);
+        /* std::cos(float) (fluid.cpp:399-400: rb.angle is a float) */
+        double c = (double)ocosf(rb.angle), s = (double)osinf(rb.angle);
         float mnx = FLT_MAX, mxx = -FLT_MAX, mny = FLT_MAX, mxy = -FLT_MAX;
         const double *lv = verts + 2 * (size_t)b.vert_off;
         for (int i = 0; i < cnt; i++) {

@@ -16,7 +16,7 @@ import pytest
 
 from conftest import ROOT, lpe, scenes
 
-HARNESS = os.path.join(ROOT, "oracle", "_ref", "liblpe_host_harness.so")
+HARNESS = os.environ.get("LPE_HARNESS_LIB") or os.path.join(ROOT, "oracle", "_ref", "liblpe_host_harness.so")
 SYSTEMS = os.path.join(ROOT, "little-physics-engine_amd", "host", "liblpe_systems.so")
 DT = 1.0 / 120.0
 
@@ -45,7 +45,7 @@ def test_host_mirror_exports():
         assert name in syms, name
 
 
-def run_world(name, mode, nticks, sync_every=1):
+def run_world(name, mode, nticks, sync_every=1, expect_status=0):
     s = scenes.scene(name) if isinstance(name, str) else name
     b, v = scenes.to_bodies(s["bodies"])
     fl = s["fluid"]
@@ -62,7 +62,7 @@ def run_world(name, mode, nticks, sync_every=1):
                     bodies.ctypes.data, v.ctypes.data, n,
                     *[arr[k].ctypes.data for k in ("x", "y", "vx", "vy", "mass", "density", "pressure")],
                     nticks, fg.ctypes.data, rg.ctypes.data, stats.ctypes.data)
-    assert st == 0, f"host mirror failed with status {st}"
+    assert st == expect_status, f"host mirror returned status {st}"
     return s, b, v, fl, arr, bodies, fg, rg, stats, rc, fc
 
 
@@ -78,23 +78,27 @@ def test_host_mirror_tick_matches_oracle(oracle_mod, mode):
     p, rb = oracle_mod.world_tick(fc, rc, p0, b, v, couple, DT, 1)
     for k, col in (("x", 0), ("y", 1), ("vx", 2), ("vy", 3), ("density", 11), ("pressure", 12)):
         np.testing.assert_array_equal(arr[k][fg], p[:, col], err_msg=k)
-    for k in ("x", "y", "angle"):
-        np.testing.assert_allclose(bodies[k], rb[k], rtol=1e-6, atol=1e-7, err_msg=k)
-    for k in ("vx", "vy", "omega"):
-        np.testing.assert_allclose(bodies[k], rb[k], rtol=1e-5, atol=1e-5, err_msg=k)
+    for k in ("x", "y", "angle", "vx", "vy", "omega"):
+        np.testing.assert_array_equal(bodies[k], rb[k], err_msg=k)
     assert 0 < stats[1] <= 64 or mode == 1
 
 
 @needs_build
 @pytest.mark.gpu
-def test_host_mirror_strict_equals_resident():
-    """Three ticks: per-system ECS round trips (strict) and the device-owned
-    world (resident, ECS synced every 2 ticks and at the end) agree."""
-    _, _, _, _, a0, b0, *_ = run_world("small64_8", 0, 3)
-    _, _, _, _, a1, b1, *_ = run_world("small64_8", 1, 3, sync_every=2)
-    for k in ("x", "y"):
-        np.testing.assert_allclose(a0[k], a1[k], rtol=1e-5, atol=1e-5, err_msg=k)
-        np.testing.assert_allclose(b0[k], b1[k], rtol=1e-5, atol=1e-4, err_msg=k)
+@pytest.mark.parametrize("nticks,sync_every", [(3, 2), (8, 3)])
+def test_host_mirror_strict_equals_resident(nticks, sync_every):
+    """Per-system ECS round trips (strict) and the device-owned world
+    (resident, ECS synced every `sync_every` ticks and at the end) agree bit
+    for bit, fluid and bodies.  (Until round 3 the device's fluid gather
+    evaluated cos/sin in double where the reference, and the strict gather,
+    call std::cos(float) (fluid.cpp:399-400): the modes drifted apart from
+    the third tick.)"""
+    _, _, _, _, a0, b0, *_ = run_world("small64_8", 0, nticks)
+    _, _, _, _, a1, b1, *_ = run_world("small64_8", 1, nticks, sync_every=sync_every)
+    for k in ("x", "y", "vx", "vy", "density", "pressure"):
+        np.testing.assert_array_equal(a0[k], a1[k], err_msg=k)
+    for k in ("x", "y", "angle", "vx", "vy", "omega", "sleep_counter", "flags"):
+        np.testing.assert_array_equal(b0[k], b1[k], err_msg=k)
 
 
 @needs_build

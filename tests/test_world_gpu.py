@@ -5,9 +5,10 @@ over oracle/sph_oracle.c).
 
 The fluid is bit-identical tick after tick (the fluid->rigid accumulators
 are exact sums rounded once on both sides, so nothing on the path depends on
-thread order).  The bodies carry fp64 geometry whose device sin/cos/sqrt may
-differ from glibc's by an ulp, so they are compared at
-1e-9 relative (poses) and 1e-5 (velocities after PGS, which runs in fp32)."""
+thread order).  So are the bodies: their fp64 geometry uses the sine and
+cosine device and oracle share (csrc/lpe_trig.h; the platform libms differ
+in the last bit), the rest is IEEE-exact arithmetic
+(correctly rounded division and square root, no FMA contraction)."""
 import numpy as np
 import pytest
 
@@ -15,6 +16,7 @@ from conftest import lpe, scenes
 
 pytestmark = pytest.mark.gpu
 DT = 1.0 / 120.0
+BODY_STATE = ("x", "y", "angle", "vx", "vy", "omega", "sleep_counter")
 
 
 def setup(ctx, name):
@@ -41,10 +43,8 @@ def test_world_one_tick(gpu_ctx, oracle_mod, name):
     p, rb = oracle_mod.world_tick(fcfg, rcfg, scenes.particles_aos(fl), b, v, couple, DT, 1)
     for k, col in (("x", 0), ("y", 1), ("vx", 2), ("vy", 3), ("density", 11), ("pressure", 12)):
         np.testing.assert_array_equal(out[k], p[:, col], err_msg=k)
-    for k in ("x", "y", "angle"):
-        np.testing.assert_allclose(bodies[k], rb[k], rtol=1e-9, atol=1e-12, err_msg=k)
-    for k in ("vx", "vy", "omega"):
-        np.testing.assert_allclose(bodies[k], rb[k], rtol=1e-5, atol=1e-6, err_msg=k)
+    for k in BODY_STATE:
+        np.testing.assert_array_equal(bodies[k], rb[k], err_msg=k)
 
 
 def test_world_multi_tick(gpu_ctx, oracle_mod):
@@ -57,10 +57,8 @@ def test_world_multi_tick(gpu_ctx, oracle_mod):
     p, rb = oracle_mod.world_tick(fcfg, rcfg, scenes.particles_aos(fl), b, v, couple, DT, 5)
     for k, col in (("x", 0), ("y", 1), ("vx", 2), ("vy", 3), ("density", 11), ("pressure", 12)):
         np.testing.assert_array_equal(out[k], p[:, col], err_msg=k)
-    for k in ("x", "y", "angle"):
-        np.testing.assert_allclose(bodies[k], rb[k], rtol=1e-9, atol=1e-12, err_msg=k)
-    for k in ("vx", "vy", "omega"):
-        np.testing.assert_allclose(bodies[k], rb[k], rtol=1e-5, atol=1e-6, err_msg=k)
+    for k in BODY_STATE:
+        np.testing.assert_array_equal(bodies[k], rb[k], err_msg=k)
 
 
 def _world_run(name, nticks, serial, fluid=True):
@@ -163,10 +161,8 @@ def test_world_one_tick_bounces(gpu_ctx, oracle_mod):
     p, rb = oracle_mod.world_tick(fcfg, rcfg, scenes.particles_aos(fl), b, v, couple, DT, 1)
     for k, col in (("x", 0), ("y", 1), ("vx", 2), ("vy", 3)):
         np.testing.assert_array_equal(out[k], p[:, col], err_msg=k)
-    for k in ("x", "y", "angle"):
-        np.testing.assert_allclose(bodies[k], rb[k], rtol=1e-9, atol=1e-12, err_msg=k)
-    for k in ("vx", "vy", "omega"):
-        np.testing.assert_allclose(bodies[k], rb[k], rtol=1e-5, atol=1e-6, err_msg=k)
+    for k in BODY_STATE:
+        np.testing.assert_array_equal(bodies[k], rb[k], err_msg=k)
 
 
 def test_world_one_tick_calls_equal_multi_tick(oracle_mod):
