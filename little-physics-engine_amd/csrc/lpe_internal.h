@@ -102,6 +102,11 @@ struct SphDev {
     unsigned upload_gen = 0;      // bumped by every lpe_sph_upload (world Barnes-Hut cache)
     size_t cap_plans = 0;
     struct Shard *shard = nullptr;// x-slab decomposition state (lpe_sph_set_slab), else single domain
+    // one-launch scan (lpe_sph.hip k_scan_rows): the kick's row totals by parity
+    int32_t *rowtot = nullptr;    // [2][cap_rows] particles per device row
+    int cap_rows = 0;
+    long fastIdx = 0;             // row scans launched (parity)
+    bool fast_armed = false;      // the pending kick recorded the row totals
 };
 
 // status slots

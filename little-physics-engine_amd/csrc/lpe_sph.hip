@@ -114,7 +114,7 @@ __device__ __forceinline__ void kick_one(float x, float y, float vx, float vy, f
     py = y + hy * dt;
 }
 __device__ __forceinline__ uint32_t bin_key(float px, float py, float eps, float cs, int ox, int oy, int W, int H,
-                                            int32_t *__restrict__ status) {
+                                            int32_t *__restrict__ status, int *okx = nullptr, int *oky = nullptr) {
     float tx = (px + eps) / cs, ty = (py + eps) / cs;
     int gx = (int)floorf(tx), gy = (int)floorf(ty);
     int qx = (int)floorf(2.0f * tx) - 2 * gx;
@@ -125,6 +125,7 @@ __device__ __forceinline__ uint32_t bin_key(float px, float py, float eps, float
         kx = min(max(kx, 0), W - 1);
         ky = min(max(ky, 0), H - 1);
     }
+    if (okx) { *okx = kx; *oky = ky; }
     return (((uint32_t)ky * (uint32_t)W + (uint32_t)kx) << 2) | (uint32_t)(qy * 2 + qx);
 }
 // the block's bbox partial (exact: min/max are order independent); every
@@ -149,6 +150,18 @@ __device__ __forceinline__ void bbox_partial(float mnx, float mxx, float mny, fl
     }
 }
 
+// Row totals for the next sub-step's scan (single domain): besides the bin
+// histogram the kick counts the particles of every device-grid row, so that
+// k_scan_rows scans a row per block with no tile-total pass.  Summed in LDS
+// over 8 rows from a base row near the block's particles (a block's
+// particles are a run of the sorted order: one or two rows), other rows
+// directly.  The totals alternate between two buffers by the scan's parity
+// (k_scan_rows clears the other one).
+struct FastKick {
+    int on;
+    int32_t *rowtot;          // [H] particles per device row
+};
+
 // The next sub-step's kick, fused into the forces pass of the current one
 // (sub-steps 1..numSubSteps-1 of a single-domain tick): the finished state
 // of a particle is exactly what k_kick_drift would read back from P.
@@ -160,6 +173,7 @@ struct KickNext {
     uint32_t *key;
     int32_t *count;
     float4 *bboxPart;                 // one partial per forces block
+    FastKick fk;                      // the next sub-step's one-pass sort (fk.on)
 };
 
 // k_kick_drift: velocityVerletHalf + bin key + histogram + bbox partials.
@@ -168,7 +182,8 @@ __global__ void __launch_bounds__(TPB)
 k_kick_drift(int n, float dt, float hdt, int first, int probe, float eps, float cs,
              int ox, int oy, int W, int H, PState P, KState K, uint32_t *__restrict__ key,
              int32_t *__restrict__ count, float4 *__restrict__ bboxPart,
-             int32_t *__restrict__ status) {
+             int32_t *__restrict__ status, FastKick fk) {
+    if (fk.on && blockIdx.x == 0 && threadIdx.x == 0) status[ST_NOT_INSERTED] = 0;   // (k_scan_rows adds)
     float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
     const int stride = gridDim.x * TPB;
     const int iters = (n + stride - 1) / stride;
@@ -195,6 +210,23 @@ k_kick_drift(int n, float dt, float hdt, int first, int probe, float eps, float 
         int len; bool st;
         (void)wave_runs(k, active, &len, &st);
         if (st) atomicAdd(&count[k], len);
+        if (fk.on) {                       // row totals: base row from the chunk's first particle
+            __shared__ int ltab[8], lbase;
+            const int row = active ? (int)((k >> 2) / (uint32_t)W) : -1;
+            if (threadIdx.x < 8) ltab[threadIdx.x] = 0;
+            if (threadIdx.x == 0) lbase = row - 3;
+            __syncthreads();
+            const int rowBase = lbase;
+            (void)wave_runs((uint32_t)row, active, &len, &st);
+            if (st) {
+                const int t = row - rowBase;
+                if (t >= 0 && t < 8) atomicAdd(&ltab[t], len);
+                else atomicAdd(&fk.rowtot[row], len);
+            }
+            __syncthreads();
+            if (threadIdx.x < 8 && ltab[threadIdx.x]) atomicAdd(&fk.rowtot[rowBase + threadIdx.x], ltab[threadIdx.x]);
+            __syncthreads();
+        }
     }
     bbox_partial(mnx, mxx, mny, mxy, bboxPart + blockIdx.x);
 }
@@ -427,6 +459,7 @@ k_scatter(int n, const uint32_t *__restrict__ key, const int32_t *__restrict__ i
     base = __shfl(base, first);
     if (active) {
         int slot = base + (lane_id() - first);
+        if ((unsigned)slot >= (unsigned)(nptr ? *nptr : n)) return;   // (never: the bins hold every particle)
         tmpId[slot] = id[i];
         tmpOld[slot] = i;
     }
@@ -441,7 +474,7 @@ k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restric
                const int32_t *__restrict__ tmpId, const int32_t *__restrict__ tmpOld,
                PState P, KState K, PState S, float4 *__restrict__ nbA, float2 *__restrict__ nbB,
                int probe, const int32_t *__restrict__ nptr, int32_t *__restrict__ src,
-               int32_t *__restrict__ refInv, int W) {
+               int32_t *__restrict__ refInv, int W, int32_t *__restrict__ clearCnt) {
     int s = blockIdx.x * TPB + threadIdx.x;
     if (s >= (nptr ? *nptr : n)) return;
     int o = tmpOld[s];
@@ -460,6 +493,116 @@ k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restric
     if (refInv) refInv[myid] = d;         // reference cell-capacity mode: id -> sorted slot
     if (!probe) { S.vhx[d] = K.vhx[o]; S.vhy[d] = K.vhy[o]; }
     if (src) src[d] = o;          // slab decomposition: sorted slot -> P slot (ghosts: >= the owned count)
+    if (clearCnt) clearCnt[k] = 0;  // (k_scan_rows leaves the counts for the next kick to find zeroed)
+}
+
+// ---------------------------------------------------------------------------
+// k_scan_rows (single domain, FastKick): one launch replaces k_scan_reduce +
+// k_scan_final.  One block per device-grid row.  Every block finishes the
+// bbox and the reference grid from the kick's partials (as the fused
+// k_scan_final) while its row's counts and the row totals below it are
+// already in flight; rows outside the particles' rows +-2 (the device grid
+// covers the universe in world mode and is mostly empty) only clear their
+// entry of the other parity's row totals.  An active row's prefix is the sum
+// of the kick's row totals of the active rows below it (no tile-total pass,
+// no inter-block wait); its 4W bins are then scanned cell by cell into start
+// and cursor with the reference-grid stats.  The counts are left for
+// k_rank_permute to clear.  Bins outside the active rows are never read (the
+// walks stay within a row of a particle's row; the last active row stores
+// the end of its last bin).
+static constexpr int SR_CELLS = 2 * TPB;   // cells a block loads before it knows its row is active
+__global__ void __launch_bounds__(TPB)
+k_scan_rows(int W, int H, int ox, int oy, float eps, const int32_t *__restrict__ cnt, int32_t *__restrict__ start,
+            int32_t *__restrict__ cursor, const int32_t *__restrict__ rowtot, int32_t *__restrict__ rowtotNext,
+            GridParams *__restrict__ gp, int32_t *__restrict__ status,
+            const float4 *__restrict__ bboxPart, int nparts, float gcs) {
+    const int r = (int)blockIdx.x;
+    if (threadIdx.x == 0) rowtotNext[r] = 0;
+    // everything the block needs is loaded up front (one round trip): the
+    // row's first SR_CELLS cells, the row totals below it, the bbox partials
+    int4 v[SR_CELLS / TPB];
+#pragma unroll
+    for (int u = 0; u < SR_CELLS / TPB; u++) {
+        const int c = u * TPB + (int)threadIdx.x;
+        v[u] = c < W ? *(const int4 *)(cnt + ((size_t)r * W + c) * 4) : make_int4(0, 0, 0, 0);
+    }
+    int pre = 0;
+    for (int q = (int)threadIdx.x; q < r; q += TPB) pre += rowtot[q];     // (rows below the active ones hold 0)
+    float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
+    for (int p = threadIdx.x; p < nparts; p += TPB) {
+        const float4 b = bboxPart[p];
+        mnx = fminf(mnx, b.x); mxx = fmaxf(mxx, b.y);
+        mny = fminf(mny, b.z); mxy = fmaxf(mxy, b.w);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        pre += __shfl_xor(pre, off);
+        mnx = fminf(mnx, __shfl_xor(mnx, off));
+        mxx = fmaxf(mxx, __shfl_xor(mxx, off));
+        mny = fminf(mny, __shfl_xor(mny, off));
+        mxy = fmaxf(mxy, __shfl_xor(mxy, off));
+    }
+    __shared__ float4 wb[TPB / 64];
+    __shared__ int wsum[TPB / 64];
+    __shared__ int s_max, s_out, s_over;
+    if (lane_id() == 0) {
+        wb[threadIdx.x >> 6] = make_float4(mnx, mxx, mny, mxy);
+        wsum[threadIdx.x >> 6] = pre;
+    }
+    if (threadIdx.x == 0) { s_max = 0; s_out = 0; s_over = 0; }
+    __syncthreads();
+    float4 b = wb[0];
+    pre = wsum[0];
+    for (int w = 1; w < TPB / 64; w++) {
+        b.x = fminf(b.x, wb[w].x); b.y = fmaxf(b.y, wb[w].y);
+        b.z = fminf(b.z, wb[w].z); b.w = fmaxf(b.w, wb[w].w);
+        pre += wsum[w];
+    }
+    const GridParams g = grid_from_bbox(b.x, b.y, b.z, b.w, gcs);
+    // every particle's row is in [row(minY), row(maxY)] (bin_key's row is
+    // monotone in y); the walks reach one row further, the reference
+    // cell-capacity walk stays inside the reference grid
+    const int ylo = min((int)floorf((b.z + eps) / gcs), g.gridMinY), yhi = max((int)floorf((b.w + eps) / gcs), g.gridMaxY);
+    const int ry0 = max(ylo - oy - 2, 0), ry1 = min(yhi - oy + 2, H - 1);
+    if (r < ry0 || r > ry1) return;
+    if (r == ry0 && threadIdx.x == 0) *gp = g;
+    const int gy = r + oy;
+    const bool rowIn = gy >= g.gridMinY && gy < g.gridMinY + g.gridDimY;
+    for (int c0 = 0; c0 < W; c0 += TPB) {
+        const int c = c0 + (int)threadIdx.x;
+        const size_t base = ((size_t)r * W + c) * 4;
+        int4 vv;
+        if (c0 < SR_CELLS) {
+            vv = v[0];
+#pragma unroll
+            for (int u = 1; u < SR_CELLS / TPB; u++) if (c0 == u * TPB) vv = v[u];
+        } else {
+            vv = c < W ? *(const int4 *)(cnt + base) : make_int4(0, 0, 0, 0);
+        }
+        const int sum = vv.x + vv.y + vv.z + vv.w;
+        if (sum > 0) {
+            // the reference grid excludes gx > gridMax (fluid.cpp:745-746 vs
+            // metal:224-226): those particles are "not inserted"
+            const int gx = c + ox;
+            const bool in = rowIn && gx >= g.gridMinX && gx < g.gridMinX + g.gridDimX;
+            if (in) atomicMax(&s_max, sum); else atomicAdd(&s_out, sum);
+            if (in && sum > LPE_REF_MAX_PER_CELL) atomicAdd(&s_over, 1);
+        }
+        int tot;
+        int ex = block_excl_scan(sum, &tot) + pre;
+        if (c < W) {
+            const int4 st4 = make_int4(ex, ex + vv.x, ex + vv.x + vv.y, ex + vv.x + vv.y + vv.z);
+            *(int4 *)(start + base) = st4;
+            *(int4 *)(cursor + base) = st4;
+        }
+        pre += tot;
+    }
+    if (r == ry1 && threadIdx.x == 0) start[(size_t)(r + 1) * W * 4] = pre;   // end of the last active bin
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (s_max) { atomicMax(&status[ST_MAX_OCC], s_max); atomicMax(&status[ST_MAX_OCC_TOTAL], s_max); }
+        if (s_out) atomicAdd(&status[ST_NOT_INSERTED], s_out);
+        if (s_over) { atomicAdd(&status[ST_OVER_CAP], s_over); atomicAdd(&status[ST_OVER_CAP_TOTAL], s_over); }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1453,12 +1596,23 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     if (kn.on) {            // the next sub-step's k_kick_drift for this particle (block-uniform)
         float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
         uint32_t k = 0xFFFFFFFFu;
+        int ky = 0;
+        // the next scan's row totals (FastKick), summed in LDS over the 8 rows
+        // around the row of the block's first slot in the current order
+        __shared__ int ltab[8];
+        int rowBase = 0;
+        if (kn.fk.on) {
+            if (threadIdx.x < 8) ltab[threadIdx.x] = 0;
+            if (lb == 0 && threadIdx.x == 0) status[ST_NOT_INSERTED] = 0;   // (k_scan_rows adds)
+            rowBase = (__float_as_int(nbA[s0].w) >> 17) - 3;
+        }
         if (live) {
             float px, py, hx, hy;
             kick_one(st.x, st.y, st.vx, st.vy, st.ax, st.ay, kn.dt, kn.hdt, px, py, hx, hy);
             kn.kvhx[out] = hx; kn.kvhy[out] = hy;
             kn.kx[out] = px; kn.ky[out] = py;
-            k = bin_key(px, py, kn.eps, kn.cs, kn.ox, kn.oy, kn.W, kn.H, status);
+            int kx;
+            k = bin_key(px, py, kn.eps, kn.cs, kn.ox, kn.oy, kn.W, kn.H, status, &kx, &ky);
             kn.key[out] = k;
             mnx = mxx = px;
             mny = mxy = py;
@@ -1466,7 +1620,20 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         int len; bool stt;
         (void)wave_runs(k, live, &len, &stt);
         if (stt) atomicAdd(&kn.count[k], len);
-        bbox_partial(mnx, mxx, mny, mxy, kn.bboxPart + lb);
+        if (kn.fk.on) {
+            __syncthreads();                               // (ltab zeroed)
+            (void)wave_runs(live ? (uint32_t)ky : 0xFFFFFFFFu, live, &len, &stt);
+            if (stt) {
+                const int t = ky - rowBase;
+                if (t >= 0 && t < 8) atomicAdd(&ltab[t], len);
+                else atomicAdd(&kn.fk.rowtot[ky], len);
+            }
+        }
+        bbox_partial(mnx, mxx, mny, mxy, kn.bboxPart + lb);   // (a block barrier)
+        if (kn.fk.on && threadIdx.x < 8) {
+            const int v = ltab[threadIdx.x];
+            if (v) atomicAdd(&kn.fk.rowtot[rowBase + threadIdx.x], v);
+        }
     }
 #ifdef LPE_FTRACE
     if (g_ftrace_on) atomicMax(&g_ftrace[lb * 8 + 3], wall_clock64());
@@ -1952,6 +2119,7 @@ static void sph_free(SphDev &d) {
     pstate_free(d.P);
     pstate_free(d.S);
     void *ptrs[] = {d.rho, d.pr, d.rhoN, d.prN, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.refInv, d.stage, d.count, d.start, d.cursor,
+                    d.rowtot,
                     d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.raabb, d.accum, d.acq, d.rbinStart, d.rgrid, d.rmax,
                     d.rbinList, d.rbinCount, d.coupleBody, d.plans};
     for (void *p : ptrs) if (p) (void)hipFree(p);
@@ -2067,10 +2235,8 @@ static int sph_set_grid(lpe_ctx *ctx, int gx0, int gy0, int gx1, int gy1) {
     long C = 4L * d.W * d.H;
     if (C > (1L << 29)) { ctx->err = "device grid too large"; return LPE_ERR_CAPACITY; }
     if (C > d.cap_cells) {
-        if (d.count) (void)hipFree(d.count);
-        if (d.start) (void)hipFree(d.start);
-        if (d.cursor) (void)hipFree(d.cursor);
-        if (d.blocksum) (void)hipFree(d.blocksum);
+        void *old[] = {d.count, d.start, d.cursor, d.blocksum};
+        for (void *p : old) if (p) (void)hipFree(p);
         d.count = d.start = d.cursor = d.blocksum = nullptr;
         LPE_HIP(ctx, hipMalloc((void **)&d.count, sizeof(int32_t) * C));
         LPE_HIP(ctx, hipMalloc((void **)&d.start, sizeof(int32_t) * (C + 1)));
@@ -2078,7 +2244,15 @@ static int sph_set_grid(lpe_ctx *ctx, int gx0, int gy0, int gx1, int gy1) {
         LPE_HIP(ctx, hipMalloc((void **)&d.blocksum, sizeof(int32_t) * (C / SCAN_ELEMS + 2)));
         d.cap_cells = (int)C;
     }
+    if (d.H > d.cap_rows || !d.rowtot) {
+        if (d.rowtot) (void)hipFree(d.rowtot);
+        d.rowtot = nullptr;
+        LPE_HIP(ctx, hipMalloc((void **)&d.rowtot, sizeof(int32_t) * 2 * (size_t)d.H));
+        d.cap_rows = d.H;
+    }
     LPE_HIP(ctx, hipMemsetAsync(d.count, 0, sizeof(int32_t) * C, ctx->stream));
+    LPE_HIP(ctx, hipMemsetAsync(d.rowtot, 0, sizeof(int32_t) * 2 * (size_t)d.cap_rows, ctx->stream));
+    d.fast_armed = false;
     d.rig_dirty = true;    // the coupling bins span the device grid
     return LPE_OK;
 }
@@ -2172,6 +2346,7 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpOld, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.refInv, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.stage, sizeof(float) * N));
+
     // bbox partials: the kick's blocks, or the forces pass's when it kicks the next sub-step
     LPE_HIP(ctx, hipMalloc((void **)&d.bboxPart, sizeof(float4) * std::max<size_t>(MAX_KICK_BLOCKS, (N + HB - 1) / HB)));
     d.cap_n = n;
@@ -2387,6 +2562,26 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
     return LPE_OK;
 }
 
+// The one-launch scan (k_scan_rows) on a single domain (LPE_NO_ROW_SCAN=1:
+// off): the kick that prepares it records the row totals (FastKick) into the
+// buffer of the scan's parity.
+static bool sph_rowscan_ok(const SphDev &d) {
+    static const bool off = getenv("LPE_NO_ROW_SCAN") != nullptr;
+    return !off && !d.shard && d.rowtot && d.n > 0;
+}
+static FastKick sph_fastkick(lpe_ctx *ctx, bool on) {
+    SphDev &d = ctx->sph;
+    FastKick fk{};
+    fk.on = on ? 1 : 0;
+    if (on) {
+        fk.rowtot = d.rowtot + (size_t)(d.fastIdx & 1) * d.cap_rows;
+        // a kick whose scan never ran (an error in between) left its totals
+        if (d.fast_armed) (void)hipMemsetAsync(fk.rowtot, 0, sizeof(int32_t) * (size_t)d.cap_rows, ctx->stream);
+    }
+    d.fast_armed = on;
+    return fk;
+}
+
 // one grid hash: kick (unless probe) + histogram + scan + scatter + rank/permute
 // kicked > 0: the previous forces pass already kicked this sub-step (KickNext)
 // and left `kicked` bbox partials
@@ -2397,18 +2592,33 @@ static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool pr
     int kb = kicked;
     if (!kicked) {
         kb = std::min(MAX_KICK_BLOCKS, std::max(1, nblk(d.n)));
+        const FastKick fk = sph_fastkick(ctx, !probe && sph_rowscan_ok(d));
         LPE_KERNEL(ctx, "k_kick_drift", k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
                    first ? 1 : 0, probe ? 1 : 0, d.cfg.gridConfig.gridEpsilon, d.cs, d.ox,
-                   d.oy, d.W, d.H, d.P, sph_kstate(d), d.key, d.count, d.bboxPart, d.stat_cur);
+                   d.oy, d.W, d.H, d.P, sph_kstate(d), d.key, d.count, d.bboxPart, d.stat_cur, fk);
         LPE_CHECK_LAUNCH(ctx, "k_kick_drift");
     }
-    int st = sph_scan(ctx, C, d.count, d.start, d.cursor, d.blocksum, kb, true);
-    if (st) return st;
+    int32_t *clear = nullptr;
+    if (d.fast_armed && !probe) {
+        // one launch for the scan (the counts are cleared by the permute)
+        const int par = (int)(d.fastIdx & 1);
+        LPE_KERNEL(ctx, "k_scan_rows", k_scan_rows, dim3(d.H), dim3(TPB), 0, s, d.W, d.H, d.ox, d.oy,
+                   d.cfg.gridConfig.gridEpsilon, d.count, d.start, d.cursor, d.rowtot + (size_t)par * d.cap_rows,
+                   d.rowtot + (size_t)(1 - par) * d.cap_rows, d.gp_cur, d.stat_cur, (const float4 *)d.bboxPart, kb,
+                   d.cs);
+        LPE_CHECK_LAUNCH(ctx, "k_scan_rows");
+        d.fastIdx++;
+        clear = d.count;
+    } else {
+        int st = sph_scan(ctx, C, d.count, d.start, d.cursor, d.blocksum, kb, true);
+        if (st) return st;
+    }
+    d.fast_armed = false;
     LPE_KERNEL(ctx, "k_scatter", k_scatter, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.P.id, d.cursor,
                        d.tmpId, d.tmpOld, (const int32_t *)nullptr);
     LPE_KERNEL(ctx, "k_rank_permute", k_rank_permute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.start,
                        d.tmpId, d.tmpOld, d.P, sph_kstate(d), d.S, d.nbA, (float2 *)d.nbB, probe ? 1 : 0,
-                       (const int32_t *)nullptr, (int32_t *)nullptr, sph_ref_inv(d), d.W);
+                       (const int32_t *)nullptr, (int32_t *)nullptr, sph_ref_inv(d), d.W, clear);
     LPE_CHECK_LAUNCH(ctx, "hash");
     return LPE_OK;
 }
@@ -2480,7 +2690,7 @@ static int sph_hash_shard(lpe_ctx *ctx, float subDt, float halfDt, bool first, i
     if (!kicked)
         LPE_KERNEL(ctx, "k_kick_drift", k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
                    first ? 1 : 0, 0, eps, d.cs, d.ox, d.oy, d.W, d.H, d.P, sph_kstate(d), d.key, d.count,
-                   d.bboxPart, d.status);
+                   d.bboxPart, d.status, FastKick{});
     static_assert(HDR == 4, "k_bbox_reduce clears 4 header words");
     LPE_KERNEL(ctx, "k_bbox_reduce", k_bbox_reduce, dim3(1), dim3(TPB), 0, s, d.bboxPart, kb, h.bb, h.gsL, h.gsR);
     LPE_CHECK_LAUNCH(ctx, "shard kick");
@@ -2507,7 +2717,7 @@ static int sph_hash_shard(lpe_ctx *ctx, float subDt, float halfDt, bool first, i
                d.tmpId, d.tmpOld, (const int32_t *)h.ntot);
     LPE_KERNEL(ctx, "k_rank_permute", k_rank_permute, dim3(nblk1(ncap)), dim3(TPB), 0, s, ncap, d.key, d.start,
                d.tmpId, d.tmpOld, d.P, sph_kstate(d), d.S, d.nbA, (float2 *)d.nbB, 0, (const int32_t *)h.ntot,
-               h.src, (int32_t *)nullptr, d.W);
+               h.src, (int32_t *)nullptr, d.W, (int32_t *)nullptr);
     LPE_CHECK_LAUNCH(ctx, "shard hash");
     return LPE_OK;
 }
@@ -2725,6 +2935,7 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
             const KState K = sph_kstate(d);
             kn.kx = K.x; kn.ky = K.y; kn.kvhx = K.vhx; kn.kvhy = K.vhy;
             kn.key = d.key; kn.count = d.count; kn.bboxPart = d.bboxPart;
+            kn.fk = sph_fastkick(ctx, sph_rowscan_ok(d));
         }
         kicked = kn.on ? fblocks : 0;
         LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(fblocks), dim3(HB), 0, s, sp, cp,

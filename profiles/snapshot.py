@@ -30,7 +30,7 @@ else:
     r = k / (time.perf_counter() - t0)
     ctx.timing(1); ctx.timing_reset(); ctx.world_tick(1 / 120, 10); t = ctx.timing_read(); ctx.timing(0)
     ks = {kk: round(vv[0] / max(vv[1], 1) * 1e3, 2) for kk, vv in t.items()}
-    top = dict(sorted(ks.items(), key=lambda kv: -kv[1])[:8])
+    top = dict(sorted(ks.items(), key=lambda kv: -kv[1])[:int(os.environ.get("TOPK", "8"))])
     print(os.environ.get("LPE_LIB", "default"), "ticks/s", round(r, 1), top)
     if os.environ.get("FIRST"):
         ctx.rigid_upload(z["bodies"], z["verts"])
