@@ -293,7 +293,48 @@ def rigid_microbench(lpe, device, reps=10):
     return dict(fixture="tests/golden/pile_M_t250.npz", pairs=st["pairs"], contacts=st["contacts"],
                 colours=st["pgsLevels"], colour_rounds=st["colourRounds"], reps=reps, step_kernels_us=round(step, 1),
                 kernels_us={k: us[k] for k in ("k_bg_key", "k_bg_pairs", "k_narrow", "k_pair_colour", "k_pgs_colour",
-                                               "k_pos_colour") if k in us})
+                                               "k_pos_colour", "k_stripe_pairs", "k_stripe_setup", "k_group_lists",
+                                               "k_group_colour", "k_stripe_layout", "k_stripe_fill", "k_pgs_stripes",
+                                               "k_pos_stripes") if k in us})
+
+
+def bh_bench(lpe, scenes, device, reps=5):
+    """BarnesHutSystem::update (barnes_hut.cpp:50-99) on the device (SURVEY.md
+    §8(f) rank 4): the 20k-body Keplerian disk and the 65k-body clustered
+    scene of tests/test_bh_gpu.py (parity-checked there, bit-exact fp64 against
+    the restatement), one step = tree build + force walk + velocity update of
+    every body.  bodies/s over the step's wall time (lpe_bh_step blocks until
+    done) and per-stage device time (HIP events on the library's stream)."""
+    out = {}
+    for kind, n in (("disk", 20000), ("clustered", 65536)):
+        s = scenes.bh_disk(n) if kind == "disk" else scenes.bh_clustered(n)
+        cfg = lpe.bh_config(s["U"], softener=s["softener"])
+        ctx = lpe.Context(device)
+        try:
+            ctx.bh_upload(s["x"], s["y"], s["vx"], s["vy"], s["m"])
+            st = ctx.bh_step(cfg, 0.75)                 # warm
+            ctx.sync()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                ctx.bh_upload(s["x"], s["y"], s["vx"], s["vy"], s["m"])
+                ctx.bh_step(cfg, 0.75)
+            wall = (time.perf_counter() - t0) / reps
+            ctx.timing(1)
+            ctx.timing_reset()
+            for _ in range(reps):
+                ctx.bh_upload(s["x"], s["y"], s["vx"], s["vy"], s["m"])
+                ctx.bh_step(cfg, 0.75)
+            t = ctx.timing_read()
+            ctx.timing(0)
+        finally:
+            ctx.close()
+        dev_us = sum(v[0] for v in t.values()) / reps * 1e3
+        out[f"{kind}{n}"] = dict(bodies=n, nodes=st["nodes"], depth=st["depth"],
+                                 bodies_per_s=round(n / wall, 1), step_ms_wall=round(wall * 1e3, 3),
+                                 step_us_device=round(dev_us, 1),
+                                 kernels_us={k: round(v[0] / reps * 1e3, 1) for k, v in sorted(t.items())},
+                                 note="wall includes the upload and the per-level host read-back of the build")
+    return out
 
 
 def timed_windows(ctx, dt_tick, rate_hint, nwin=5, min_s=2.0, min_ticks=50):
@@ -361,13 +402,29 @@ def config_lines(lpe, scenes, device, dt_tick, with_ref):
             ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
             ctx.world_set_coupling(None)
             ctx.world_tick(dt_tick, prep)
+            ctx.sph_diag(False)                       # restart the window totals
             w = timed_windows(ctx, dt_tick, 500.0, nwin=3, min_s=1.0)
             st = ctx.sph_stats()
+            over = st["overCapCellsTotal"]
+            wcap = None
+            if over > 0:
+                # outside the reference's 64-slot cells: time the reference's own
+                # capped-cell semantics too (LPE_SPH_MODE_REF_CELL_CAP)
+                ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP)
+                wcap = timed_windows(ctx, dt_tick, 500.0, nwin=3, min_s=1.0)
+                ctx.sph_set_mode(0)
         finally:
             ctx.close()
         out[name] = dict(desc=s["desc"], ticks_per_s=w["median"], windows=w, fluid_particles=len(fl["x"]),
                          bodies=len(b), max_cell_occupancy=st["maxCellOccupancy"],
-                         cells_over_64=st["overCapCells"])
+                         cells_over_64=st["overCapCells"],
+                         reference_envelope=dict(max_cell_occupancy_window=st["maxCellOccupancyTotal"],
+                                                 cells_over_64_window=over, inside=over == 0))
+        if wcap is not None:
+            out[name]["ref_cell_cap_mode"] = dict(ticks_per_s=wcap["median"], windows=wcap,
+                                                  note="the reference's 64-slot cell semantics (dropped inserts, "
+                                                       "cross-cell reads), bit-exact vs the oracle in "
+                                                       "tests/test_configs_gpu.py")
     anchors = {"C1": (555.0, 600), "C3": (12.1, 240)}
     for name in ("C1", "C3"):
         s = scenes.rigid_scene(name)
@@ -552,6 +609,14 @@ def main():
             roof["valu"] = dict(wave_insts=vi, achieved_ginst_s=round(vi / avg_s / 1e9, 1),
                                 peak_ginst_s=VALU_PEAK_GINST, frac=round(vi / avg_s / 1e9 / VALU_PEAK_GINST, 4),
                                 source=vsrc)
+    # the whole tick against HBM: the staged
+    # compulsory model B_tick = substeps x (152 B x N + 24 B x C) at the
+    # measured tick rate
+    btick = 10.0 * (152.0 * n + 24.0 * cells)
+    tick_rate = args.steps / elapsed
+    roof_tick = dict(model="10 x (152 B x N + 24 B x C) per tick (SURVEY.md §8(d))", bytes_per_tick=btick,
+                     achieved=round(btick * tick_rate / 1e9, 1), unit="GB/s",
+                     frac=round(btick * tick_rate / 1e9 / HBM_PEAK_GBS, 4), ticks_per_s=round(tick_rate, 2))
     dens = times.get("k_density")
     roof_d = None
     if dens:
@@ -591,6 +656,7 @@ def main():
                                   ("single GPU" if world == 1 else f"replica x{world}")},
         "roofline": roof,
         "roofline_density": roof_d,
+        "roofline_tick": roof_tick,
         "kernels_us": {k: round(v[0] / max(v[1], 1) * 1e3, 2) for k, v in times.items()},
         "dominant_kernel": overall,
         "max_cell_occupancy": stats["maxCellOccupancy"],
@@ -616,6 +682,7 @@ def main():
     if world == 1 and not args.no_density_microbench:
         line["density_microbench"] = density_microbench(lpe, scenes, local)
         line["rigid_microbench"] = rigid_microbench(lpe, local)
+        line["barnes_hut"] = bh_bench(lpe, scenes, local)
         line["render_density"] = render
     if world == 1 and not args.no_cpu_baseline and args.scene == "M":
         line["cpu_baseline"] = cpu_baseline(args.scene, settled)

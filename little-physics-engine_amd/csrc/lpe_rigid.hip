@@ -967,10 +967,10 @@ typedef float pk2 __attribute__((ext_vector_type(2)));
 // The x/y halves of the row are computed as packed fp32 pairs (v_pk_mul_f32 /
 // v_pk_add_f32: each lane of a packed op is the IEEE scalar op, unfused), so
 // the results are the scalar code's bit for bit with fewer VALU issues.
-__device__ __forceinline__ void pgs_row_regs(float4 rn, float4 rr, float imA, float iiA, float imB,
-                                             float iiB, bool hasA, bool hasB, float mu, float &ln,
-                                             float &lf, float &vxA, float &vyA, float &wA, float &vxB,
-                                             float &vyB, float &wB) {
+template <bool BL>
+__device__ __forceinline__ void pgs_row_t(float4 rn, float4 rr, float imA, float iiA, float imB, float iiB,
+                                          bool hasA, bool hasB, float mu, float &ln, float &lf, float &vxA,
+                                          float &vyA, float &wA, float &vxB, float &vyB, float &wB) {
     pk2 vA = {vxA, vyA}, vB = {vxB, vyB};
     const pk2 lA = {-rr.y, rr.x}, lB = {-rr.w, rr.z};
 #pragma unroll
@@ -995,7 +995,7 @@ __device__ __forceinline__ void pgs_row_regs(float4 rn, float4 rr, float imA, fl
         if (nl > hi) nl = hi;
         dl = nl - old;
         if (row == 0) ln = nl; else lf = nl;
-#if PGS_BRANCHLESS
+        if constexpr (BL) {
         // the skipped / absent-body cases as selects of the unchanged values
         // (bit-identical to the branches; keeps exec-mask updates and their
         // VALU -> SALU hazards out of the row chain)
@@ -1006,7 +1006,7 @@ __device__ __forceinline__ void pgs_row_regs(float4 rn, float4 rr, float imA, fl
         const bool uA = apply && hasA, uB = apply && hasB;
         vA.x = uA ? nvA.x : vA.x; vA.y = uA ? nvA.y : vA.y; wA = uA ? nwA : wA;
         vB.x = uB ? nvB.x : vB.x; vB.y = uB ? nvB.y : vB.y; wB = uB ? nwB : wB;
-#else
+        } else {
         if (fabsf(dl) < 1e-15F) continue;
         if (hasA) {
             vA -= d * (dl * imA);
@@ -1018,9 +1018,15 @@ __device__ __forceinline__ void pgs_row_regs(float4 rn, float4 rr, float imA, fl
             float crossB = rr.z * d.y - rr.w * d.x;
             wB += crossB * dl * iiB;
         }
-#endif
+        }
     }
     vxA = vA.x; vyA = vA.y; vxB = vB.x; vyB = vB.y;
+}
+__device__ __forceinline__ void pgs_row_regs(float4 rn, float4 rr, float imA, float iiA, float imB,
+                                             float iiB, bool hasA, bool hasB, float mu, float &ln,
+                                             float &lf, float &vxA, float &vyA, float &wA, float &vxB,
+                                             float &vyB, float &wB) {
+    pgs_row_t<PGS_BRANCHLESS != 0>(rn, rr, imA, iiA, imB, iiB, hasA, hasB, mu, ln, lf, vxA, vyA, wA, vxB, vyB, wB);
 }
 
 // A colour step is latency-bound (one workgroup; a pair's rows are a chain),
@@ -1579,6 +1585,28 @@ __device__ __forceinline__ void pos_item_regs(double nx, double ny, double corr,
     }
 }
 
+// the same, the skip and the static-body cases as selects of the unchanged
+// values (bit-identical: every value that is kept is computed by the same
+// operations; a skipped item's arithmetic is discarded)
+__device__ __forceinline__ void pos_item_sel(double nx, double ny, double corr, double px, double py,
+                                             int flags, double invMA, double invMB, double invIA,
+                                             double invIB, double &xA, double &yA, double &tA,
+                                             double &xB, double &yB, double &tB) {
+    D2 rA = d2(px - xA, py - yA);
+    D2 rB = d2(px - xB, py - yB);
+    D2 n = d2(nx, ny);
+    double rAn = crs(rA, n), rBn = crs(rB, n);
+    double denom = invMA + invMB + (rAn * rAn) * invIA + (rBn * rBn) * invIB;
+    const bool apply = !(flags & 1) && !(denom < 1e-12);
+    double sc = corr / denom;
+    double dx = n.x * sc, dy = n.y * sc;
+    const bool uA = apply && (invMA != 0.0 || (flags & 2)), uB = apply && (invMB != 0.0 || (flags & 4));
+    const double nxA = xA - dx * invMA, nyA = yA - dy * invMA, ntA = tA - rAn * sc * invIA;
+    const double nxB = xB + dx * invMB, nyB = yB + dy * invMB, ntB = tB + rBn * sc * invIB;
+    xA = uA ? nxA : xA; yA = uA ? nyA : yA; tA = (uA && (flags & 2)) ? ntA : tA;
+    xB = uB ? nxB : xB; yB = uB ? nyB : yB; tB = (uB && (flags & 4)) ? ntB : tB;
+}
+
 __device__ __forceinline__ void pos_item(const PosRec &q, double *sp) {
     if (q.flags & 1) return;
     const int a = q.a, b = q.b;
@@ -1890,6 +1918,745 @@ k_pos_flow(int nb, const int32_t *__restrict__ kptr, const PosRec *__restrict__ 
 
 // ---------------------------------------------------------------------------
 // integrator systems (per body, fp64)
+// ===========================================================================
+// Striped Gauss-Seidel: the canonical solver order since round 3 (restated by
+// oracle/rigid_oracle.cpp lpeo_stripe_order; see there for the definition).
+// The movable bodies of the contact pairs are cut into S x-stripes no
+// narrower than the longest pair; band j = stripes 2j and 2j+1, seam j =
+// the stripe pair 2j+1 | 2j+2.  A pair lies inside one band or across one
+// seam; each band's and each seam's pairs are coloured greedily.  A sweep is
+// phase A (every band) then phase B (every seam); the bands touch disjoint
+// bodies and so do the seams, so workgroup j runs band j, then seam j,
+// concurrently with the others: only stripes 2j and 2j+2 are shared with a
+// neighbour, handed over through global memory with one flag per phase
+// (write-through stores and loads, MI355X_MICROARCH.md hand-off table, first
+// row).  W = S/2 workgroups (one per CU) instead of one: a sweep's critical
+// path is one band's colours plus one seam's (about 10 steps at scene M)
+// instead of every colour of the scene, each step 1/W of the pairs.
+static constexpr int STRIPES_MAX = 64;
+static constexpr int SGROUPS = 2 * STRIPES_MAX;          // (S groups are used: S/2 bands, S/2 - 1 seams)
+static constexpr int SCOLS = 64;                 // colours per group (a greedy colouring needs degree + 1)
+static constexpr int STEPS_MAX = SGROUPS * SCOLS;
+static constexpr int STPB = 256;                 // threads of a stripe workgroup
+
+struct StripeBufs {
+    int32_t *bstripe;      // [nb] stripe of a movable body in a contact pair, else -1
+    int32_t *bpos;         // [nb] slot of a contact-pair body in sbList, else -1
+    double *bred;          // [3 blocks of k_stripe_pairs] x min, x max, longest pair
+    int32_t *pflag;        // [cap_pairs] 1 has contacts, 2 A movable, 4 B movable
+    double2 *px;           // [cap_pairs] x of A and B
+    int32_t *pgroup;       // [cap_pairs] group of a pair with contacts, else -1
+    int32_t *pcolg;        // [cap_pairs] colour inside its group
+    int32_t *prank;        // [cap_pairs] rank inside (group, colour)
+    int32_t *prowoff;      // [cap_pairs] first row inside (group, colour)
+    int32_t *glist;        // [cap_pairs] pairs by group, ascending inside a group
+    int32_t *gstart;       // [SGROUPS + 1]
+    int32_t *gcnt;         // [SGROUPS][SCOLS][2] pairs, rows per (group, colour); [SGROUPS*SCOLS*2 + g]: colours of g
+    int32_t *stepIdx;      // [SGROUPS * SCOLS] canonical step of (group, colour)
+    int32_t *stepPair;     // [STEPS_MAX + 1] first coloured-pair slot of a step
+    int32_t *stepRow;      // [STEPS_MAX + 1] first row of a step
+    int32_t *wgStep;       // [STRIPES_MAX / 2][4] phase A [first, end), phase B [first, end)
+    int32_t *sbStart;      // [STRIPES_MAX + 2] bodies of each stripe; [STRIPES_MAX + 1]: end of the static ones
+    int32_t *sbList;       // [nb] movable contact-pair bodies by stripe, then the static ones
+    uint32_t *sflag;       // [2][STRIPES_MAX / 2] hand-over flags (phase A, phase B) per solver
+    float *gvel;           // [3 nb] velocities handed over (PGS), by sbList slot
+    double *gpos;          // [3 nb] poses handed over (position solver), by sbList slot
+};
+
+__device__ __forceinline__ int stripe_of(double x, double x0, double w, int S) {
+    if (S == 1) return 0;
+    const double f = floor((x - x0) / w);
+    return (int)fmin((double)(S - 1), fmax(0.0, f));
+}
+
+// per pair with contacts: which bodies move and their x; per block the range
+// of the movable bodies' x and the longest pair (sb.bred, 3 doubles a block)
+__global__ void __launch_bounds__(RTPB)
+k_stripe_pairs(const int32_t *__restrict__ npptr, const int2 *__restrict__ pairs,
+               const int32_t *__restrict__ ccount, const lpe_body *__restrict__ bodies, StripeBufs sb) {
+    __shared__ double wr[3][RTPB / 64];
+    const int p = blockIdx.x * RTPB + threadIdx.x;
+    const int np = *npptr;
+    if ((int)(blockIdx.x * RTPB) >= np) return;
+    double mn = 1.7976931348623157e308, mx = -1.7976931348623157e308, sp = 0.0;
+    if (p < np) {
+        int f = 0;
+        double2 x = make_double2(0.0, 0.0);
+        if (ccount[p] > 0) {
+            const int2 pr = pairs[p];
+            const lpe_body &A = bodies[pr.x], &B = bodies[pr.y];
+            const bool da = colour_dep(A), db = colour_dep(B);
+            x = make_double2(A.x, B.x);
+            f = 1 | (da ? 2 : 0) | (db ? 4 : 0);
+            if (da) { mn = fmin(mn, x.x); mx = fmax(mx, x.x); }
+            if (db) { mn = fmin(mn, x.y); mx = fmax(mx, x.y); }
+            if (da && db) sp = fabs(x.x - x.y);
+        }
+        sb.pflag[p] = f;
+        sb.px[p] = x;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        mn = fmin(mn, __shfl_xor(mn, off));
+        mx = fmax(mx, __shfl_xor(mx, off));
+        sp = fmax(sp, __shfl_xor(sp, off));
+    }
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) { wr[0][w] = mn; wr[1][w] = mx; wr[2][w] = sp; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < RTPB / 64; k++) {
+            mn = fmin(mn, wr[0][k]); mx = fmax(mx, wr[1][k]); sp = fmax(sp, wr[2][k]);
+        }
+        sb.bred[3 * blockIdx.x] = mn;
+        sb.bred[3 * blockIdx.x + 1] = mx;
+        sb.bred[3 * blockIdx.x + 2] = sp;
+    }
+}
+
+// One workgroup: the stripe count and width, the stripes' body lists (then
+// the static bodies of contact pairs), the pairs' groups and the groups'
+// sizes (counts[12] = S, counts[13] = workgroups).
+__global__ void __launch_bounds__(SOLVE_TPB)
+k_stripe_setup(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict__ pairs,
+               const lpe_body *__restrict__ bodies, StripeBufs sb, int32_t *__restrict__ counts) {
+    extern __shared__ unsigned int bmark[];                 // [2][words]: movable / static contact-pair bodies
+    __shared__ double wr[3][SOLVE_TPB / 64];
+    __shared__ double sx0, sw;
+    __shared__ int sS, sViol, nstat, statcur;
+    __shared__ int scnt[STRIPES_MAX], scur[STRIPES_MAX], gcount[SGROUPS];
+    const int np = *npptr;
+    const int words = (nb + 31) >> 5;
+    for (int i = threadIdx.x; i < 2 * words; i += SOLVE_TPB) bmark[i] = 0u;
+    for (int i = threadIdx.x; i < STRIPES_MAX; i += SOLVE_TPB) scnt[i] = 0;
+    for (int i = threadIdx.x; i < SGROUPS; i += SOLVE_TPB) gcount[i] = 0;
+    if (threadIdx.x == 0) { sViol = 0; nstat = 0; }
+    double mn = 1.7976931348623157e308, mx = -1.7976931348623157e308, sp = 0.0;
+    const int nblk = (np + RTPB - 1) / RTPB;
+    for (int k = threadIdx.x; k < nblk; k += SOLVE_TPB) {
+        mn = fmin(mn, sb.bred[3 * k]); mx = fmax(mx, sb.bred[3 * k + 1]); sp = fmax(sp, sb.bred[3 * k + 2]);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        mn = fmin(mn, __shfl_xor(mn, off));
+        mx = fmax(mx, __shfl_xor(mx, off));
+        sp = fmax(sp, __shfl_xor(sp, off));
+    }
+    if ((threadIdx.x & 63) == 0) { wr[0][threadIdx.x >> 6] = mn; wr[1][threadIdx.x >> 6] = mx; wr[2][threadIdx.x >> 6] = sp; }
+    __syncthreads();
+    for (int p = threadIdx.x; p < np; p += SOLVE_TPB) {
+        const int f = sb.pflag[p];
+        if (!(f & 1)) continue;
+        const int2 pr = pairs[p];
+        atomicOr(&bmark[((f & 2) ? 0 : words) + (pr.x >> 5)], 1u << (pr.x & 31));
+        atomicOr(&bmark[((f & 4) ? 0 : words) + (pr.y >> 5)], 1u << (pr.y & 31));
+    }
+    if (threadIdx.x == 0) {
+        for (int k = 1; k < SOLVE_TPB / 64; k++) {
+            mn = fmin(mn, wr[0][k]); mx = fmax(mx, wr[1][k]); sp = fmax(sp, wr[2][k]);
+        }
+        int S = 1;
+        if (mx > mn) {
+            const double q = (mx - mn) / sp;          // (span 0: +inf)
+            if (q >= 2.0) S = min(STRIPES_MAX, (int)floor(fmin(q, 1e9))) & ~1;
+        }
+        sS = S;
+        sx0 = mn;
+        sw = (mx - mn) / S;
+    }
+    __syncthreads();
+    int S = sS;
+    const double x0 = sx0, w = sw;
+    // a pair more than one stripe apart (a rounding edge): one stripe
+    for (int p = threadIdx.x; p < np && S > 1; p += SOLVE_TPB) {
+        if ((sb.pflag[p] & 6) != 6) continue;
+        const double2 x = sb.px[p];
+        if (abs(stripe_of(x.x, x0, w, S) - stripe_of(x.y, x0, w, S)) > 1) sViol = 1;
+    }
+    __syncthreads();
+    if (sViol) S = 1;
+    for (int b = threadIdx.x; b < nb; b += SOLVE_TPB) {
+        int s = -1;
+        if ((bmark[b >> 5] >> (b & 31)) & 1u) {
+            s = stripe_of(bodies[b].x, x0, w, S);
+            atomicAdd(&scnt[s], 1);
+        } else if ((bmark[words + (b >> 5)] >> (b & 31)) & 1u) {
+            atomicAdd(&nstat, 1);
+        }
+        sb.bstripe[b] = s;
+    }
+    for (int p = threadIdx.x; p < np; p += SOLVE_TPB) {
+        const int f = sb.pflag[p];
+        int g = -1;
+        if (f & 1) {
+            const double2 x = sb.px[p];
+            int sa = (f & 2) ? stripe_of(x.x, x0, w, S) : -1;
+            int sb2 = (f & 4) ? stripe_of(x.y, x0, w, S) : -1;
+            if (sa < 0) sa = sb2;
+            if (sb2 < 0) sb2 = sa;
+            if (sa < 0) sa = sb2 = 0;
+            g = (sa >> 1) == (sb2 >> 1) ? 2 * (sa >> 1) : 2 * (min(sa, sb2) >> 1) + 1;
+            atomicAdd(&gcount[g], 1);
+        }
+        sb.pgroup[p] = g;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int acc = 0;
+        for (int s = 0; s < STRIPES_MAX; s++) { sb.sbStart[s] = acc; scur[s] = acc; acc += scnt[s]; }
+        sb.sbStart[STRIPES_MAX] = acc;
+        statcur = acc;
+        sb.sbStart[STRIPES_MAX + 1] = acc + nstat;
+        acc = 0;
+        for (int g = 0; g < SGROUPS; g++) { sb.gstart[g] = acc; acc += gcount[g]; }
+        sb.gstart[SGROUPS] = acc;
+        counts[12] = S;
+        counts[13] = (S + 1) / 2;
+    }
+    __syncthreads();
+    for (int b = threadIdx.x; b < nb; b += SOLVE_TPB) {
+        const int s = sb.bstripe[b];
+        int i = -1;
+        if (s >= 0) i = atomicAdd(&scur[s], 1);
+        else if ((bmark[words + (b >> 5)] >> (b & 31)) & 1u) i = atomicAdd(&statcur, 1);
+        if (i >= 0) sb.sbList[i] = b;
+        sb.bpos[b] = i;
+    }
+}
+
+// one workgroup per group: its pairs in ascending order (stable compaction)
+__global__ void __launch_bounds__(RTPB)
+k_group_lists(const int32_t *__restrict__ npptr, const int32_t *__restrict__ counts, StripeBufs sb) {
+    const int g = (int)blockIdx.x;
+    if (g >= counts[12]) return;                       // groups: bands 0, 2, .. and seams 1, 3, .. < S
+    const int np = *npptr;
+    int base = sb.gstart[g];
+    for (int p0 = 0; p0 < np; p0 += 4 * RTPB) {
+        int f[4], c = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const int p = p0 + 4 * (int)threadIdx.x + k;
+            f[k] = (p < np && sb.pgroup[p] == g) ? 1 : 0;
+            c += f[k];
+        }
+        int tot;
+        int off = r_block_excl(c, &tot) + base;
+#pragma unroll
+        for (int k = 0; k < 4; k++)
+            if (f[k]) sb.glist[off++] = p0 + 4 * (int)threadIdx.x + k;
+        base += tot;
+    }
+}
+
+// one wave per group: greedy colouring of its pairs in ascending order (the
+// lowest colour free on the pair's movable bodies), the pair's rank and row
+// offset inside its (group, colour), the group's colour sizes.  The bodies'
+// colour masks live in LDS by stripe-list slot (the group's bodies lie in
+// its one or two stripes).
+__global__ void __launch_bounds__(64)
+k_group_colour(const int32_t *__restrict__ counts, const int2 *__restrict__ pairs,
+               const int32_t *__restrict__ ccount, StripeBufs sb) {
+    extern __shared__ unsigned long long used[];             // per stripe-list slot of the group's stripes
+    __shared__ int qa[64], qb[64], qn[64], qc[64];
+    __shared__ int cpairs[SCOLS], crows[SCOLS];
+    __shared__ int sfault;
+    const int g = (int)blockIdx.x;
+    const int S = counts[12];
+    if (g >= S) return;
+    const int lane = (int)threadIdx.x;
+    const int s = (g >> 1) * 2 + (g & 1);               // band j: stripes 2j, 2j+1; seam j: 2j+1, 2j+2
+    const int u0 = sb.sbStart[s], u1 = sb.sbStart[min(s + 2, S)];
+    for (int i = lane; i < u1 - u0; i += 64) used[i] = 0ull;
+    cpairs[lane] = 0; crows[lane] = 0;
+    if (lane == 0) sfault = 0;
+    __syncthreads();
+    const int g0 = sb.gstart[g], g1 = sb.gstart[g + 1];
+    int ncol = 0;
+    for (int c0 = g0; c0 < g1; c0 += 64) {
+        const int t = c0 + lane;
+        int p = -1;
+        if (t < g1) {
+            p = sb.glist[t];
+            const int2 pr = pairs[p];
+            const int f = sb.pflag[p];
+            qa[lane] = (f & 2) ? sb.bpos[pr.x] - u0 : -1;
+            qb[lane] = (f & 4) ? sb.bpos[pr.y] - u0 : -1;
+            qn[lane] = ccount[p];
+        }
+        __syncthreads();
+        if (lane == 0) {
+            const int m = min(64, g1 - c0);
+            for (int i = 0; i < m; i++) {
+                const int a = qa[i], b = qb[i];
+                const unsigned long long forb = (a >= 0 ? used[a] : 0ull) | (b >= 0 ? used[b] : 0ull);
+                const int c = forb == ~0ull ? 0 : __ffsll((long long)~forb) - 1;
+                if (forb == ~0ull) sfault = 1;
+                if (a >= 0) used[a] |= 1ull << c;
+                if (b >= 0) used[b] |= 1ull << c;
+                qc[i] = c;
+                ncol = max(ncol, c + 1);
+                // ranks and row offsets in ascending order (qa / qb reused)
+                qa[i] = cpairs[c]++;
+                qb[i] = crows[c];
+                crows[c] += qn[i];
+            }
+        }
+        __syncthreads();
+        if (t < g1) {
+            sb.pcolg[p] = qc[lane];
+            sb.prank[p] = qa[lane];
+            sb.prowoff[p] = qb[lane];
+        }
+        __syncthreads();
+    }
+    ncol = __shfl(ncol, 0);
+    int32_t *gc = sb.gcnt + (size_t)g * SCOLS * 2;
+    gc[2 * lane] = cpairs[lane];
+    gc[2 * lane + 1] = crows[lane];
+    if (lane == 0) {
+        sb.gcnt[SGROUPS * SCOLS * 2 + g] = ncol;
+        if (sfault) atomicOr((int *)&counts[7], 1);
+    }
+}
+
+// the canonical step sequence: phase A (the bands, groups 0, 2, 4, ..), then
+// phase B (the seams, groups 1, 3, ..), colours ascending.  Thread t is the
+// t-th group of that sequence (phase t >> 6, band / seam j = t & 63); one
+// block scan gives every group's first step, pair slot and row.
+__global__ void __launch_bounds__(RTPB)
+k_stripe_layout(StripeBufs sb, int32_t *__restrict__ counts) {
+    const int S = counts[12];
+    const int t = (int)threadIdx.x;
+    const int ph = t >> 6, j = t & 63, g = 2 * j + ph;
+    const bool valid = t < SGROUPS && 2 * j + ph < S;
+    const int nc = valid ? sb.gcnt[SGROUPS * SCOLS * 2 + g] : 0;
+    int gp = 0, gr = 0;
+    const int32_t *gc = sb.gcnt + (size_t)(valid ? g : 0) * SCOLS * 2;
+    for (int c = 0; c < nc; c++) { gp += gc[2 * c]; gr += gc[2 * c + 1]; }
+    int ts, tp, trw;
+    const int s0 = r_block_excl(nc, &ts), p0 = r_block_excl(gp, &tp), q0 = r_block_excl(gr, &trw);
+    int pa = p0, ra = q0;
+    for (int c = 0; c < nc; c++) {
+        sb.stepIdx[g * SCOLS + c] = s0 + c;
+        sb.stepPair[s0 + c] = pa;
+        sb.stepRow[s0 + c] = ra;
+        pa += gc[2 * c];
+        ra += gc[2 * c + 1];
+    }
+    if (t < SGROUPS && j < STRIPES_MAX / 2) {       // workgroup j runs band j and seam j
+        sb.wgStep[4 * j + 2 * ph] = s0;
+        sb.wgStep[4 * j + 2 * ph + 1] = s0 + nc;
+    }
+    if (t == 0) {
+        sb.stepPair[ts] = tp;
+        sb.stepRow[ts] = trw;
+        counts[8] = ts;
+    }
+}
+
+// each pair's slot in the step sequence (seg: its rows, contiguous) and its
+// rows' contact indices (order); pcol = the pair's step (-1: no contact)
+__global__ void k_stripe_fill(const int32_t *__restrict__ npptr, const int32_t *__restrict__ ccount,
+                              const int32_t *__restrict__ cstart, StripeBufs sb, int32_t *__restrict__ pcol,
+                              int2 *__restrict__ seg, int32_t *__restrict__ order) {
+    const int p = blockIdx.x * RTPB + threadIdx.x;
+    if (p >= *npptr) return;
+    const int g = sb.pgroup[p];
+    if (g < 0) { pcol[p] = -1; return; }
+    const int st = sb.stepIdx[g * SCOLS + sb.pcolg[p]];
+    const int q = sb.stepPair[st] + sb.prank[p];
+    const int rs = sb.stepRow[st] + sb.prowoff[p];
+    const int n = ccount[p], c0 = cstart[p];
+    seg[q] = make_int2(rs, n | (1 << 8));
+    for (int j = 0; j < n; j++) order[rs + j] = c0 + j;
+    pcol[p] = st;
+}
+
+// ---- hand-over of a stripe's bodies between neighbouring workgroups --------
+// (MI355X_MICROARCH.md, inter-workgroup hand-off table, first row: every
+// store and load of the handed-over values write-through / L1-bypassing
+// (relaxed agent-scope atomics: global_store / global_load ... sc1), each
+// storing wave drained before the workgroup barrier, one lane's sc1 flag
+// store; the consumer's lane 0 polls the flag with sc1 loads, the others load
+// after the barrier it joins.  One workgroup per CU, hipMalloc memory.)
+// Values travel by stripe-list slot; lv holds them by slot - s0.
+template <typename T>
+__device__ __forceinline__ void stripe_publish(const StripeBufs &sb, int s, int s0, const T *lv, T *g) {
+    const int b0 = 3 * sb.sbStart[s], b1 = 3 * sb.sbStart[s + 1];
+    for (int i = b0 + (int)threadIdx.x; i < b1; i += STPB)
+        __hip_atomic_store(&g[i], lv[i - 3 * s0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ void stripe_reload(const StripeBufs &sb, int s, int s0, T *lv, const T *g) {
+    const int b0 = 3 * sb.sbStart[s], b1 = 3 * sb.sbStart[s + 1];
+    for (int i = b0 + (int)threadIdx.x; i < b1; i += STPB)
+        lv[i - 3 * s0] = __hip_atomic_load(&g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stripe_signal(uint32_t *flag, uint32_t v) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // this wave's hand-over stores are done
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// a wait that sees no progress for ~0.2 s gives up and raises counts[7] bit 2
+// (never expected: the schedule is deadlock free and every workgroup is
+// resident); the solve's result is then wrong and the next detection fails
+__device__ __forceinline__ void stripe_wait(const uint32_t *flag, uint32_t v, int32_t *fault) {
+    if (threadIdx.x == 0) {
+        unsigned spins = 0;
+        while ((int)(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - v) < 0) {
+            __builtin_amdgcn_s_sleep(2);
+            if (++spins > (1u << 22)) { atomicOr(fault, 2); break; }
+        }
+    }
+    __syncthreads();
+}
+
+// What workgroup j works on: bodies of stripes 2j .. 2j+2 (sbList slots
+// [s0, s1)), phase A steps [a0, a1) (stripe 2j's two groups) and phase B
+// steps [b0, b1) (stripe 2j+1's), and their pairs and rows, each a contiguous
+// range of the step sequence with A before B.  The LDS copies number pairs
+// and rows A first, then B (lpair / lrow); local step k = lstep(st).
+struct StripeView {
+    int S, j, s0, s1, nDyn, nAll;
+    int a0, a1, b0, b1;
+    int pA0, nA, pB0, nB;
+    int rA0, nRA, rB0, nRB;
+    __device__ int lpair(int q) const { return q < pA0 + nA ? q - pA0 : nA + q - pB0; }
+    __device__ int lrow(int r) const { return r < rA0 + nRA ? r - rA0 : nRA + r - rB0; }
+    __device__ int lstep(int st) const { return st < a1 ? st - a0 : (a1 - a0) + st - b0; }
+    __device__ int nsteps() const { return (a1 - a0) + (b1 - b0); }
+    __device__ int npairs() const { return nA + nB; }
+    __device__ int nrows() const { return nRA + nRB; }
+    __device__ int nloc() const { return s1 - s0; }
+};
+__device__ __forceinline__ StripeView stripe_view(const StripeBufs &sb, const int32_t *counts, int j) {
+    StripeView v;
+    v.S = counts[12]; v.j = j;
+    v.s0 = sb.sbStart[2 * j];
+    v.s1 = sb.sbStart[min(2 * j + 3, v.S)];
+    v.nDyn = sb.sbStart[STRIPES_MAX];
+    v.nAll = sb.sbStart[STRIPES_MAX + 1];
+    v.a0 = sb.wgStep[4 * j]; v.a1 = sb.wgStep[4 * j + 1];
+    v.b0 = sb.wgStep[4 * j + 2]; v.b1 = sb.wgStep[4 * j + 3];
+    v.pA0 = sb.stepPair[v.a0]; v.nA = sb.stepPair[v.a1] - v.pA0;
+    v.pB0 = sb.stepPair[v.b0]; v.nB = sb.stepPair[v.b1] - v.pB0;
+    v.rA0 = sb.stepRow[v.a0]; v.nRA = sb.stepRow[v.a1] - v.rA0;
+    v.rB0 = sb.stepRow[v.b0]; v.nRB = sb.stepRow[v.b1] - v.rB0;
+    return v;
+}
+// the local steps' first local pairs (and the end), into LDS
+__device__ __forceinline__ void stripe_steps_lds(const StripeBufs &sb, const StripeView &v, int *stepL) {
+    const int ns = v.nsteps();
+    for (int k = threadIdx.x; k <= ns; k += STPB) {
+        const int st = k < v.a1 - v.a0 ? v.a0 + k : v.b0 + (k - (v.a1 - v.a0));
+        stepL[k] = k == ns ? v.npairs() : v.lpair(sb.stepPair[st]);
+    }
+}
+
+#ifdef LPE_PTRACE
+__device__ unsigned long long g_strace[2][32][64];
+extern "C" int lpe_strace(unsigned long long *host) {
+    if (host) (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_strace), sizeof(unsigned long long) * 2 * 32 * 64);
+    return 0;
+}
+#define STR(w, j, k) do { if (threadIdx.x == 0 && (k) < 64 && (j) < 32) g_strace[w][j][k] = wall_clock64(); } while (0)
+#else
+#define STR(w, j, k) do { } while (0)
+#endif
+
+// The sweeps of one stripe pair per workgroup (the loop shared by both
+// solvers): phase A = stripe 2j's steps, phase B = stripe 2j+1's; before a
+// phase the shared stripe a neighbour changed last is reloaded, after it the
+// one the neighbour needs next is published.  solve(st, it) runs one step.
+template <typename T, typename Solve>
+__device__ __forceinline__ void stripe_sweeps(const StripeBufs &sb, const StripeView &v, int iters, uint32_t base,
+                                              uint32_t *flagA, uint32_t *flagB, T *lv, T *g, int32_t *fault,
+                                              Solve solve, int tw = 0) {
+    const int j = v.j;
+    const bool right = 2 * j + 2 < v.S;             // seam j (phase B) exists
+    (void)tw;
+    STR(tw, j, 1);
+    for (int it = 0; it < iters; it++) {
+        if (it > 0 && j > 0) {                    // stripe 2j, after the left neighbour's phase B of it - 1
+            stripe_wait(&flagB[j - 1], base + it, fault);
+            stripe_reload(sb, 2 * j, v.s0, lv, g);
+            __syncthreads();
+        }
+        STR(tw, j, 2 + 6 * it);
+        for (int st = v.a0; st < v.a1; st++) { solve(st, it); __syncthreads(); }
+        STR(tw, j, 3 + 6 * it);
+        if (j > 0) {
+            stripe_publish(sb, 2 * j, v.s0, lv, g);
+            stripe_signal(&flagA[j], base + it + 1);
+        }
+        STR(tw, j, 4 + 6 * it);
+        if (!right) continue;
+        {                                         // stripe 2j+2, after the right neighbour's phase A of it
+            stripe_wait(&flagA[j + 1], base + it + 1, fault);
+            stripe_reload(sb, 2 * j + 2, v.s0, lv, g);
+            __syncthreads();
+        }
+        STR(tw, j, 5 + 6 * it);
+        for (int st = v.b0; st < v.b1; st++) { solve(st, it); __syncthreads(); }
+        STR(tw, j, 6 + 6 * it);
+        stripe_publish(sb, 2 * j + 2, v.s0, lv, g);
+        stripe_signal(&flagB[j], base + it + 1);
+        STR(tw, j, 7 + 6 * it);
+    }
+}
+// the stripes whose final values this workgroup holds: 2j+1, 2j+2, and 0
+__device__ __forceinline__ bool stripe_owned(int s, int j, int S) {
+    return s >= 0 && s < S && (s == 2 * j + 1 || s == 2 * j + 2 || (j == 0 && s == 0));
+}
+
+// bytes of LDS a stripe workgroup may use (one workgroup per CU)
+static constexpr int STRIPE_LDS = 150 * 1024;
+__host__ __device__ constexpr int lds_align(int b) { return (b + 15) & ~15; }
+
+// PGS (solveLcpPgs, contact_solver.cpp:381-440) over the striped order.  The
+// workgroup's rows, pairs, multipliers and its bodies' velocities live in LDS
+// for the whole solve (staged once: rows are 40 bytes, pairs 32); a
+// workgroup whose rows do not fit reads them from global memory instead.
+__global__ void __launch_bounds__(STPB)
+k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__restrict__ seg,
+              const float4 *__restrict__ rowN, const float4 *__restrict__ rowR, const int2 *__restrict__ rowAB,
+              const float4 *__restrict__ rowM, int iters, float mu, float *__restrict__ lamN,
+              float *__restrict__ lamF, lpe_body *__restrict__ bodies, const int32_t *__restrict__ inContact,
+              uint32_t base, int32_t *__restrict__ fault) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int j = (int)blockIdx.x;
+    if (j >= counts[13]) return;
+    STR(0, j, 0);
+    const StripeView v = stripe_view(sb, counts, j);
+    const int NR = v.nrows(), NP = v.npairs(), NL = v.nloc(), NS = v.nsteps();
+    // layout: rn, rr [NR] float4 | pr [NP] int4 | pm [NP] float4 | ln, lf [NR] | lv [3 NL] | stepL [NS + 1]
+    const int oRR = 16 * NR, oPR = oRR + 16 * NR, oPM = oPR + 16 * NP, oLN = oPM + 16 * NP, oLF = oLN + 4 * NR,
+              oLV = oLF + 4 * NR, oST = oLV + 12 * NL, total = oST + 4 * (NS + 1);
+    const bool inL = total <= STRIPE_LDS;
+    float *lv = inL ? (float *)(smem + oLV) : (float *)smem;
+    for (int i = v.s0 + (int)threadIdx.x; i < v.s1; i += STPB) {
+        const lpe_body &b = bodies[sb.sbList[i]];
+        float *o = lv + 3 * (i - v.s0);
+        o[0] = (float)b.vx; o[1] = (float)b.vy; o[2] = can_rotate(b) ? (float)b.omega : 0.f;
+    }
+    const int *bpos = sb.bpos;
+    auto lbody = [&](int b) { return b >= 0 ? bpos[b] - v.s0 : -1; };
+    if (inL) {
+        float4 *rn = (float4 *)smem, *rr = (float4 *)(smem + oRR), *pm = (float4 *)(smem + oPM);
+        int4 *pr = (int4 *)(smem + oPR);
+        float *ln = (float *)(smem + oLN), *lf = (float *)(smem + oLF);
+        int *stepL = (int *)(smem + oST);
+        for (int r = threadIdx.x; r < NR; r += STPB) {
+            const int g = r < v.nRA ? v.rA0 + r : v.rB0 + (r - v.nRA);
+            rn[r] = rowN[g]; rr[r] = rowR[g];
+            ln[r] = 0.f; lf[r] = 0.f;
+        }
+        for (int q = threadIdx.x; q < NP; q += STPB) {
+            const int gq = q < v.nA ? v.pA0 + q : v.pB0 + (q - v.nA);
+            const int2 sg = seg[gq];
+            const int2 ab = rowAB[sg.x];
+            pr[q] = make_int4(v.lrow(sg.x), sg.y & 0xff, lbody(ab.x), lbody(ab.y));
+            pm[q] = rowM[sg.x];
+        }
+        stripe_steps_lds(sb, v, stepL);
+        __syncthreads();
+        auto solve = [&](int st, int) {
+            const int k = v.lstep(st);
+            const int q1 = stepL[k + 1];
+            for (int q = stepL[k] + (int)threadIdx.x; q < q1; q += STPB) {
+                const int4 p = pr[q];
+                const float4 m = pm[q];
+                const bool hasA = p.z >= 0, hasB = p.w >= 0;
+                float vxA = 0.f, vyA = 0.f, wA = 0.f, vxB = 0.f, vyB = 0.f, wB = 0.f;
+                if (hasA) { vxA = lv[3 * p.z]; vyA = lv[3 * p.z + 1]; wA = lv[3 * p.z + 2]; }
+                if (hasB) { vxB = lv[3 * p.w]; vyB = lv[3 * p.w + 1]; wB = lv[3 * p.w + 2]; }
+                constexpr int U = 4;                    // rows loaded together
+                for (int j0 = 0; j0 < p.y; j0 += U) {
+                    float4 a[U], c[U];
+                    float n[U], f[U];
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        const int t = p.x + min(j0 + u, p.y - 1);
+                        a[u] = rn[t]; c[u] = rr[t]; n[u] = ln[t]; f[u] = lf[t];
+                    }
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        if (j0 + u >= p.y) break;
+                        pgs_row_t<true>(a[u], c[u], m.x, m.y, m.z, m.w, hasA, hasB, mu, n[u], f[u], vxA, vyA, wA,
+                                     vxB, vyB, wB);
+                        ln[p.x + j0 + u] = n[u];
+                        lf[p.x + j0 + u] = f[u];
+                    }
+                }
+                if (hasA) { lv[3 * p.z] = vxA; lv[3 * p.z + 1] = vyA; lv[3 * p.z + 2] = wA; }
+                if (hasB) { lv[3 * p.w] = vxB; lv[3 * p.w + 1] = vyB; lv[3 * p.w + 2] = wB; }
+            }
+        };
+        stripe_sweeps(sb, v, iters, base, sb.sflag, sb.sflag + STRIPES_MAX / 2, lv, sb.gvel, fault, solve, 0);
+    } else {
+        __syncthreads();
+        auto solve = [&](int st, int it) {
+            const int q1 = sb.stepPair[st + 1];
+            for (int q = sb.stepPair[st] + (int)threadIdx.x; q < q1; q += STPB) {
+                const int2 sg = seg[q];
+                const int rs = sg.x, nrow = sg.y & 0xff;
+                const int2 ab = rowAB[rs];
+                const float4 m = rowM[rs];
+                const int la = lbody(ab.x), lb = lbody(ab.y);
+                const bool hasA = la >= 0, hasB = lb >= 0;
+                float vxA = 0.f, vyA = 0.f, wA = 0.f, vxB = 0.f, vyB = 0.f, wB = 0.f;
+                if (hasA) { vxA = lv[3 * la]; vyA = lv[3 * la + 1]; wA = lv[3 * la + 2]; }
+                if (hasB) { vxB = lv[3 * lb]; vyB = lv[3 * lb + 1]; wB = lv[3 * lb + 2]; }
+                for (int t = rs; t < rs + nrow; t++) {
+                    float n = it ? lamN[t] : 0.f, f = it ? lamF[t] : 0.f;
+                    pgs_row_t<true>(rowN[t], rowR[t], m.x, m.y, m.z, m.w, hasA, hasB, mu, n, f, vxA, vyA, wA, vxB,
+                                 vyB, wB);
+                    lamN[t] = n;
+                    lamF[t] = f;
+                }
+                if (hasA) { lv[3 * la] = vxA; lv[3 * la + 1] = vyA; lv[3 * la + 2] = wA; }
+                if (hasB) { lv[3 * lb] = vxB; lv[3 * lb + 1] = vyB; lv[3 * lb + 2] = wB; }
+            }
+        };
+        stripe_sweeps(sb, v, iters, base, sb.sflag, sb.sflag + STRIPES_MAX / 2, lv, sb.gvel, fault, solve, 0);
+    }
+    __syncthreads();
+    // k_pgs_writeback for the stripes this workgroup finished last (only the
+    // velocity fields: the position solver writes the poses concurrently)
+    for (int s = 2 * j; s <= 2 * j + 2; s++) {
+        if (!stripe_owned(s, j, v.S)) continue;
+        for (int i = sb.sbStart[s] + (int)threadIdx.x; i < sb.sbStart[s + 1]; i += STPB) {
+            const int b = sb.sbList[i];
+            if (!inContact[b]) continue;
+            lpe_body &bd = bodies[b];
+            if (infinite_mass(bd)) continue;
+            const float *o = lv + 3 * (i - v.s0);
+            bd.vx = o[0];
+            bd.vy = o[1];
+            if (can_rotate(bd)) bd.omega = o[2];
+        }
+    }
+}
+
+// Position solver (solvePositionContactsOnce, position_solver.cpp:215-290)
+// over the striped order.  The poses (fp64) of the workgroup's stripes and of
+// the static bodies its pairs touch, its rows (44 bytes) and pairs (48) live
+// in LDS; a workgroup whose rows do not fit reads them from global memory.
+__global__ void __launch_bounds__(STPB)
+k_pos_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__restrict__ seg, PosRows rows,
+              lpe_body *__restrict__ bodies, const double *__restrict__ st, const int32_t *__restrict__ inPos,
+              int iters, uint32_t base, int32_t *__restrict__ fault) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int j = (int)blockIdx.x;
+    if (j >= counts[13]) return;
+    STR(1, j, 0);
+    const StripeView v = stripe_view(sb, counts, j);
+    const int NR = v.nrows(), NP = v.npairs(), NS = v.nsteps();
+    const int NL = v.nloc() + (v.nAll - v.nDyn);      // the stripes' bodies, then the static ones
+    // layout: n, c [NR] double2 | pm, pi [NP] double2 | pr [NP] int4 | py [NR] | lp [3 NL] | fl [NR] | stepL
+    const int oC = 16 * NR, oPM = oC + 16 * NR, oPI = oPM + 16 * NP, oPR = oPI + 16 * NP, oPY = oPR + 16 * NP,
+              oLP = oPY + 8 * NR, oFL = oLP + 24 * NL, oST = oFL + 4 * NR, total = oST + 4 * (NS + 1);
+    const bool inL = total <= STRIPE_LDS;
+    double *lp = inL ? (double *)(smem + oLP) : (double *)smem;
+    for (int i = threadIdx.x; i < NL; i += STPB) {
+        const int slot = i < v.nloc() ? v.s0 + i : v.nDyn + (i - v.nloc());
+        const lpe_body &b = bodies[sb.sbList[slot]];
+        lp[3 * i] = b.x; lp[3 * i + 1] = b.y;
+        lp[3 * i + 2] = (b.flags & LPE_BODY_HAS_ANGPOS) ? b.angle : 0.0;
+    }
+    const int *bpos = sb.bpos;
+    auto lbody = [&](int b) {
+        const int p = bpos[b];
+        return p >= v.nDyn ? v.nloc() + (p - v.nDyn) : p - v.s0;
+    };
+    // one pair's rows against the poses in lp (a static body, invM = 0 and no
+    // rotation, is never written: pairs of one step may share it)
+    auto pair_rows = [&](int a, int b, double2 mm, double2 ii, int nrow, auto row) {
+        double xA = lp[3 * a], yA = lp[3 * a + 1], tA = lp[3 * a + 2];
+        double xB = lp[3 * b], yB = lp[3 * b + 1], tB = lp[3 * b + 2];
+        const int fl0 = row(0, mm, ii, xA, yA, tA, xB, yB, tB);
+        for (int k = 1; k < nrow; k++) row(k, mm, ii, xA, yA, tA, xB, yB, tB);
+        if (mm.x != 0.0 || (fl0 & 2)) { lp[3 * a] = xA; lp[3 * a + 1] = yA; lp[3 * a + 2] = tA; }
+        if (mm.y != 0.0 || (fl0 & 4)) { lp[3 * b] = xB; lp[3 * b + 1] = yB; lp[3 * b + 2] = tB; }
+    };
+    if (inL) {
+        double2 *ln = (double2 *)smem, *lc = (double2 *)(smem + oC), *pm = (double2 *)(smem + oPM),
+                *pi = (double2 *)(smem + oPI);
+        int4 *pr = (int4 *)(smem + oPR);
+        double *py = (double *)(smem + oPY);
+        int *fl = (int *)(smem + oFL), *stepL = (int *)(smem + oST);
+        for (int r = threadIdx.x; r < NR; r += STPB) {
+            const int g = r < v.nRA ? v.rA0 + r : v.rB0 + (r - v.nRA);
+            ln[r] = rows.n[g]; lc[r] = rows.c[g]; py[r] = rows.py[g]; fl[r] = rows.fl[g];
+        }
+        for (int q = threadIdx.x; q < NP; q += STPB) {
+            const int gq = q < v.nA ? v.pA0 + q : v.pB0 + (q - v.nA);
+            const int2 sg = seg[gq];
+            const int2 ab = rows.ab[sg.x];
+            pr[q] = make_int4(v.lrow(sg.x), sg.y & 0xff, lbody(ab.x), lbody(ab.y));
+            pm[q] = rows.m[sg.x];
+            pi[q] = rows.i[sg.x];
+        }
+        stripe_steps_lds(sb, v, stepL);
+        __syncthreads();
+        auto solve = [&](int stp, int) {
+            const int k = v.lstep(stp);
+            const int q1 = stepL[k + 1];
+            for (int q = stepL[k] + (int)threadIdx.x; q < q1; q += STPB) {
+                const int4 p = pr[q];
+                const int r0 = p.x;
+                pair_rows(p.z, p.w, pm[q], pi[q], p.y,
+                          [&](int k2, double2 mm, double2 ii, double &xA, double &yA, double &tA, double &xB,
+                              double &yB, double &tB) {
+                              const int t = r0 + k2;
+                              const double2 n = ln[t], c = lc[t];
+                              const int f = fl[t];
+                              pos_item_sel(n.x, n.y, c.x, c.y, py[t], f, mm.x, mm.y, ii.x, ii.y, xA, yA, tA, xB,
+                                            yB, tB);
+                              return f;
+                          });
+            }
+        };
+        stripe_sweeps(sb, v, iters, base, sb.sflag + STRIPES_MAX, sb.sflag + STRIPES_MAX + STRIPES_MAX / 2, lp,
+                      sb.gpos, fault, solve, 1);
+    } else {
+        __syncthreads();
+        auto solve = [&](int stp, int) {
+            const int q1 = sb.stepPair[stp + 1];
+            for (int q = sb.stepPair[stp] + (int)threadIdx.x; q < q1; q += STPB) {
+                const int2 sg = seg[q];
+                const int rs = sg.x;
+                const int2 ab = rows.ab[rs];
+                pair_rows(lbody(ab.x), lbody(ab.y), rows.m[rs], rows.i[rs], sg.y & 0xff,
+                          [&](int k2, double2 mm, double2 ii, double &xA, double &yA, double &tA, double &xB,
+                              double &yB, double &tB) {
+                              const int t = rs + k2;
+                              const double2 n = rows.n[t], c = rows.c[t];
+                              const int f = rows.fl[t];
+                              pos_item_sel(n.x, n.y, c.x, c.y, rows.py[t], f, mm.x, mm.y, ii.x, ii.y, xA, yA, tA,
+                                            xB, yB, tB);
+                              return f;
+                          });
+            }
+        };
+        stripe_sweeps(sb, v, iters, base, sb.sflag + STRIPES_MAX, sb.sflag + STRIPES_MAX + STRIPES_MAX / 2, lp,
+                      sb.gpos, fault, solve, 1);
+    }
+    __syncthreads();
+    // storeBodyData (:176-197) for the stripes this workgroup finished last
+    for (int s = 2 * j; s <= 2 * j + 2; s++) {
+        if (!stripe_owned(s, j, v.S)) continue;
+        for (int i = sb.sbStart[s] + (int)threadIdx.x; i < sb.sbStart[s + 1]; i += STPB) {
+            const int b = sb.sbList[i];
+            if (!inPos[b]) continue;
+            const int f = (int)st[3 * b + 2];
+            if (!(f & 2)) continue;
+            lpe_body &bd = bodies[b];
+            const double *o = lp + 3 * (i - v.s0);
+            bd.x = o[0]; bd.y = o[1];
+            if ((f & 1) && (bd.flags & LPE_BODY_HAS_ANGPOS)) bd.angle = o[2];
+        }
+    }
+}
+
 __global__ void k_boundary(int nb, lpe_body *__restrict__ bodies, double m, double U, double damp,
                            double maxSpeed) {   // boundary.cpp:13-70
     int i = blockIdx.x * RTPB + threadIdx.x;
@@ -2084,6 +2851,13 @@ int lpe_rigid_destroy_internal(lpe_ctx *ctx) {
                     d->counts, d->pcol, d->cseg, d->cbase, d->bgCount, d->bgStart, d->bgCursor,
                     d->bgList, d->bgKey, d->bgSpecial, d->bbits};
     for (void *p : ptrs) if (p) (void)hipFree(p);
+    if (StripeBufs *sb = (StripeBufs *)d->stripes) {
+        void *sp[] = {sb->bstripe, sb->pgroup, sb->pcolg, sb->prank, sb->prowoff, sb->glist, sb->gstart, sb->gcnt,
+                      sb->stepIdx, sb->stepPair, sb->stepRow, sb->wgStep, sb->sbStart, sb->sbList, sb->sflag,
+                      sb->gvel, sb->gpos, sb->bpos, sb->pflag, sb->px, sb->bred};
+        for (void *p : sp) if (p) (void)hipFree(p);
+        delete sb;
+    }
     if (d->hc) (void)hipHostFree(d->hc);
     hipEvent_t evs[] = {d->evStart, d->evDetect, d->evColour, d->evFork, d->evJoin};
     for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
@@ -2222,6 +2996,8 @@ extern "C" int lpe_rigid_upload(lpe_ctx *ctx, int nb, const lpe_body *bodies, in
         (void)hipFuncSetAttribute((const void *)k_pos_colour, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         // k_pair_colour also holds ~1 KB of static LDS
         (void)hipFuncSetAttribute((const void *)k_pair_colour, hipFuncAttributeMaxDynamicSharedMemorySize, 156 * 1024);
+        (void)hipFuncSetAttribute((const void *)k_pgs_stripes, hipFuncAttributeMaxDynamicSharedMemorySize, STRIPE_LDS);
+        (void)hipFuncSetAttribute((const void *)k_pos_stripes, hipFuncAttributeMaxDynamicSharedMemorySize, STRIPE_LDS);
         (void)hipGetLastError();   // a refused attribute must not surface at a later launch check
         lds_attr = true;
     }
@@ -2418,7 +3194,73 @@ static int rigid_detect(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pai
 // k_pair_colour); otherwise pgs_order (NULL = narrowphase order) for the PGS
 // and narrowphase order for the position solver (reference-order replay)
 // the canonical colouring of the pairs (k_pair_colour) on stream s
+// The striped solver (canonical since round 3) or, with LPE_COLOUR_SOLVER=1,
+// round 2's single-workgroup colour sweeps (a different sequential order:
+// for measurements only, the oracle restates the striped one).
+static bool striped() {
+    static const bool old = getenv("LPE_COLOUR_SOLVER") != nullptr;
+    return !old;
+}
+static StripeBufs *stripe_bufs(lpe_ctx *ctx, RigidDev *d) {
+    StripeBufs *sb = (StripeBufs *)d->stripes;
+    if (!sb) {
+        sb = new StripeBufs();
+        std::memset(sb, 0, sizeof(*sb));
+        d->stripes = sb;
+    }
+    auto grow = [&](auto **p, size_t n) { return rgrow(ctx, p, n); };
+    if (d->nb > d->cap_stripe_nb || !sb->bstripe) {
+        const size_t N = (size_t)std::max(d->nb, 1);
+        if (grow(&sb->bstripe, N) || grow(&sb->bpos, N) || grow(&sb->sbList, N) || grow(&sb->gvel, 3 * N) ||
+            grow(&sb->gpos, 3 * N))
+            return nullptr;
+        d->cap_stripe_nb = d->nb;
+    }
+    if (d->cap_pairs > d->cap_stripe_pairs || !sb->pgroup) {
+        const size_t P = (size_t)std::max(d->cap_pairs, 1);
+        if (grow(&sb->pgroup, P) || grow(&sb->pcolg, P) || grow(&sb->prank, P) || grow(&sb->prowoff, P) ||
+            grow(&sb->glist, P) || grow(&sb->pflag, P) || grow(&sb->px, P) || grow(&sb->bred, 3 * (P / RTPB + 1)))
+            return nullptr;
+        d->cap_stripe_pairs = d->cap_pairs;
+    }
+    if (!sb->gstart) {
+        if (grow(&sb->gstart, SGROUPS + 1) || grow(&sb->gcnt, (size_t)SGROUPS * SCOLS * 2 + SGROUPS) ||
+            grow(&sb->stepIdx, (size_t)SGROUPS * SCOLS) || grow(&sb->stepPair, STEPS_MAX + 1) ||
+            grow(&sb->stepRow, STEPS_MAX + 1) || grow(&sb->wgStep, 2 * STRIPES_MAX) ||
+            grow(&sb->sbStart, STRIPES_MAX + 2) || grow(&sb->sflag, 2 * STRIPES_MAX))
+            return nullptr;
+        if (hipMemset(sb->sflag, 0, sizeof(uint32_t) * 2 * STRIPES_MAX) != hipSuccess) return nullptr;
+    }
+    return sb;
+}
+
+// stripes, groups, greedy colourings and the step layout on stream s
+static int stripe_launch(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
+    const int nb = d->nb;
+    if (d->cap_pcol < d->cap_pairs || !d->pcol) {
+        int st0 = rgrow(ctx, &d->pcol, (size_t)d->cap_pairs);
+        if (!st0) st0 = rgrow(ctx, &d->cseg, (size_t)d->cap_pairs);
+        if (st0) return st0;
+        d->cap_pcol = d->cap_pairs;
+    }
+    StripeBufs *sb = stripe_bufs(ctx, d);
+    if (!sb) return LPE_ERR_HIP;
+    LPE_KERNEL(ctx, "k_stripe_pairs", k_stripe_pairs, dim3(rblk(d->cap_pairs)), dim3(RTPB), 0, s, d->counts,
+               d->pairs, d->ccount, d->bodies, *sb);
+    LPE_KERNEL(ctx, "k_stripe_setup", k_stripe_setup, dim3(1), dim3(SOLVE_TPB), sizeof(uint32_t) * 2 * ((nb + 31) / 32 + 1),
+               s, nb, d->counts, d->pairs, d->bodies, *sb, d->counts);
+    LPE_KERNEL(ctx, "k_group_lists", k_group_lists, dim3(SGROUPS), dim3(RTPB), 0, s, d->counts, d->counts, *sb);
+    LPE_KERNEL(ctx, "k_group_colour", k_group_colour, dim3(SGROUPS), dim3(64), sizeof(unsigned long long) * (size_t)nb,
+               s, d->counts, d->pairs, d->ccount, *sb);
+    LPE_KERNEL(ctx, "k_stripe_layout", k_stripe_layout, dim3(1), dim3(RTPB), 0, s, *sb, d->counts);
+    LPE_KERNEL(ctx, "k_stripe_fill", k_stripe_fill, dim3(rblk(d->cap_pairs)), dim3(RTPB), 0, s, d->counts, d->ccount,
+               d->cstart, *sb, d->pcol, d->cseg, d->order);
+    LPE_CHECK_LAUNCH(ctx, "stripes");
+    return LPE_OK;
+}
+
 static int colour_launch(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
+    if (striped()) return stripe_launch(ctx, d, s);
     int nb = d->nb;
     if (d->cap_pcol < d->cap_pairs || !d->pcol) {
         int st0 = rgrow(ctx, &d->pcol, (size_t)d->cap_pairs);
@@ -2483,6 +3325,17 @@ static int colour_prep(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
 static int colour_pos(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     const lpe_rigid_config &c = d->cfg;
     const int nb = d->nb;
+    if (striped()) {
+        StripeBufs *sb = stripe_bufs(ctx, d);
+        if (!sb) return LPE_ERR_HIP;
+        const uint32_t base = d->sbase_pos;
+        d->sbase_pos += (uint32_t)c.posIterations + 2;
+        LPE_KERNEL(ctx, "k_pos_stripes", k_pos_stripes, dim3(STRIPES_MAX / 2), dim3(STPB), STRIPE_LDS, s, d->counts, *sb,
+                   d->cseg, pos_rows(d), d->bodies, d->posState, d->inContact + nb, c.posIterations, base,
+                   d->counts + 7);
+        LPE_CHECK_LAUNCH(ctx, "position solver");
+        return LPE_OK;
+    }
     const size_t lds2 = sizeof(double) * 3 * (size_t)nb;
     LPE_KERNEL(ctx, "k_pos_colour", k_pos_colour, dim3(1), dim3(SOLVE_TPB), lds2, s, nb, d->counts, d->cbase, d->cseg, pos_rows(d), d->bodies, d->posState, d->inContact + nb, c.posIterations);
     LPE_CHECK_LAUNCH(ctx, "position solver");
@@ -2492,6 +3345,17 @@ static int colour_pos(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
 static int colour_pgs(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     const lpe_rigid_config &c = d->cfg;
     const int nb = d->nb;
+    if (striped()) {
+        StripeBufs *sb = stripe_bufs(ctx, d);
+        if (!sb) return LPE_ERR_HIP;
+        const uint32_t base = d->sbase_pgs;
+        d->sbase_pgs += (uint32_t)c.pgsIterations + 2;
+        LPE_KERNEL(ctx, "k_pgs_stripes", k_pgs_stripes, dim3(STRIPES_MAX / 2), dim3(STPB), STRIPE_LDS, s, d->counts, *sb,
+                   d->cseg, d->rowN, d->rowR, d->rowAB, d->rowM, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF,
+                   d->bodies, (const int32_t *)d->inContact, base, d->counts + 7);
+        LPE_CHECK_LAUNCH(ctx, "pgs");
+        return LPE_OK;
+    }
     // (k_pgs_bodies and k_pgs_writeback run as the kernel's prologue / epilogue)
     const size_t lds = sizeof(float) * 3 * (size_t)nb;
     LPE_KERNEL(ctx, "k_pgs_colour", k_pgs_colour, dim3(1), dim3(SOLVE_TPB), lds, s, nb, d->counts, d->cbase, d->cseg, 0, d->rowN, d->rowR, d->rowAB, d->rowM, d->vel0, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF, d->bodies, (const int32_t *)d->inContact);

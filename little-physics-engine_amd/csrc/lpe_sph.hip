@@ -1586,10 +1586,16 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         }
     }
     if (live) {
-        P.x[out] = st.x; P.y[out] = st.y;
+        // a sub-step that kicks the next one (kn.on) leaves only what the next
+        // hash reads from P (velocity, mass, id: the kicked position and
+        // half-step velocity go to the K scratch below); x, y, vh and a are
+        // written by the tick's last sub-step
+        if (!kn.on) {
+            P.x[out] = st.x; P.y[out] = st.y;
+            P.vhx[out] = st.vhx; P.vhy[out] = st.vhy;
+            P.ax[out] = st.ax; P.ay[out] = st.ay;
+        }
         P.vx[out] = st.vx; P.vy[out] = st.vy;
-        P.vhx[out] = st.vhx; P.vhy[out] = st.vhy;
-        P.ax[out] = st.ax; P.ay[out] = st.ay;
         P.m[out] = st.mass; P.id[out] = S.id[s];
         if (sp.orho) { sp.orho[out] = rhoi; sp.opr[out] = pi; }
     }

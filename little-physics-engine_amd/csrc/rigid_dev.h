@@ -89,6 +89,10 @@ struct RigidDev {
     hipEvent_t evStart = nullptr, evDetect = nullptr, evColour = nullptr;
     bool overlap_pending = false;             // detection queued on the side stream
     bool colour_pending = false;              // ... finished by the host, colouring queued
+    // striped solver buffers (lpe_rigid.hip StripeBufs, allocated on first use)
+    void *stripes = nullptr;
+    int cap_stripe_nb = 0, cap_stripe_pairs = 0;
+    uint32_t sbase_pgs = 16, sbase_pos = 16;  // hand-over flag epochs of the two solvers
     // the position solver runs beside the PGS on its own stream (rigid_solve)
     hipStream_t psolve = nullptr;
     hipEvent_t evFork = nullptr, evJoin = nullptr;

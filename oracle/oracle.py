@@ -247,6 +247,22 @@ def colour_order(bodies, contacts, npairs):
     return order[:len(c)], col[:npairs], n
 
 
+def stripe_order(bodies, contacts, npairs):
+    """lpeo_stripe_order: (order, pair_step, nsteps, nstripes) of the canonical
+    striped Gauss-Seidel order the device solvers run (round 3)."""
+    L = _rigid_lib()
+    f = L.lpeo_stripe_order
+    f.argtypes = [C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int,
+                  C.POINTER(C.c_int32)]
+    b = _bodies(bodies)
+    c = np.ascontiguousarray(contacts, lpe.CONTACT_DTYPE)
+    order = np.zeros(max(len(c), 1), np.int32)
+    col = np.zeros(max(npairs, 1), np.int32)
+    ns = C.c_int32(0)
+    n = f(len(b), b.ctypes.data, len(c), c.ctypes.data, order.ctypes.data, col.ctypes.data, npairs, C.byref(ns))
+    return order[:len(c)], col[:npairs], n, ns.value
+
+
 def rigid_update(cfg, bodies, verts):
     b = _bodies(bodies)
     v = np.ascontiguousarray(verts, np.float64)

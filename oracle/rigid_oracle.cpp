@@ -766,6 +766,122 @@ extern "C" int lpeo_colour_order(int nb, const lpe_body *bodies, int nc, const l
     return ncol;
 }
 
+/* The canonical solver order of the device path since round 3 (lpe_rigid.hip
+ * k_stripe_setup / k_group_colour / k_pgs_stripes / k_pos_stripes): striped
+ * Gauss-Seidel.
+ *  - movable body: finite mass or rotatable (colour_dep); the movable bodies
+ *    of the pairs with contacts take part;
+ *  - stripes: x0, x1 = min, max of their x; span = max |x_a - x_b| over the
+ *    pairs whose two bodies are movable; q = (x1 - x0) / span; S = 1 unless
+ *    q >= 2, else min(64, floor(q)) rounded down to even; w = (x1 - x0) / S;
+ *    stripe(b) = clamp(floor((x_b - x0) / w), 0, S - 1).  A pair whose two
+ *    movable bodies lie more than one stripe apart (a rounding edge) makes it
+ *    one stripe (S = 1);
+ *  - groups: band j = stripes 2j and 2j + 1, seam j = the stripe pair
+ *    2j + 1 | 2j + 2.  A pair whose movable bodies (none: stripe 0) lie in
+ *    one band is in the band's group 2j, one across bands j | j + 1 in the
+ *    seam's group 2j + 1;
+ *  - each group coloured greedily: its pairs ascending, each takes the
+ *    lowest colour free on its movable bodies (64 at most);
+ *  - order: phase A (the bands, groups 0, 2, 4, ..) then phase B (the seams,
+ *    groups 1, 3, ..); per group its colours ascending, pairs ascending
+ *    inside a colour, contacts in narrowphase order.
+ * The bands touch disjoint bodies, and so do the seams: the device runs each
+ * phase's groups concurrently (workgroup j: band j, then seam j, handing the
+ * shared stripes 2j and 2j + 2 over with its neighbours), bit-identical to
+ * this sequential order.  pair_step (optional, npairs)
+ * receives the canonical step (group colour) of each pair, -1 without
+ * contacts.  Returns the number of steps, or -1 (a group needs > 64 colours). */
+constexpr int STRIPES_MAX = 64;                       /* lpe_rigid.hip STRIPES_MAX */
+extern "C" int lpeo_stripe_order(int nb, const lpe_body *bodies, int nc, const lpe_contact *cs,
+                                 int32_t *order, int32_t *pair_step, int npairs, int32_t *nstripes) {
+    auto dep = [&](int i) {
+        const lpe_body &b = bodies[i];
+        bool inf = (b.flags & LPE_BODY_HAS_MASS) && b.mass > 1e29;
+        bool rot = (b.flags & LPE_BODY_HAS_INERTIA) && b.inertia > 1e-12 && b.inertia < 1e29;
+        return !inf || rot;
+    };
+    std::vector<int> pid, pa, pb, ps, pn;             /* pairs with contacts, ascending */
+    for (int k = 0; k < nc; k++) {
+        if (k == 0 || cs[k].pair != cs[k - 1].pair) {
+            pid.push_back(cs[k].pair); pa.push_back(cs[k].a); pb.push_back(cs[k].b);
+            ps.push_back(k); pn.push_back(0);
+        }
+        pn.back()++;
+    }
+    const int m = (int)pid.size();
+    double x0 = 0.0, x1 = 0.0, span = 0.0;
+    bool any = false;
+    for (int q = 0; q < m; q++) {
+        for (int e : {pa[q], pb[q]}) {
+            if (!dep(e)) continue;
+            const double x = bodies[e].x;
+            if (!any) { x0 = x1 = x; any = true; }
+            x0 = std::min(x0, x); x1 = std::max(x1, x);
+        }
+        if (dep(pa[q]) && dep(pb[q])) span = std::max(span, std::fabs(bodies[pa[q]].x - bodies[pb[q]].x));
+    }
+    int S = 1;
+    const double qn = (x1 - x0) / span;               /* (span 0: +inf; x1 == x0: 0 or NaN) */
+    if (any && x1 > x0 && qn >= 2.0) S = std::min(STRIPES_MAX, (int)std::floor(std::min(qn, 1e9))) & ~1;
+    const double w = (x1 - x0) / S;
+    auto stripe = [&](int e) {
+        if (S == 1) return 0;
+        double f = std::floor((bodies[e].x - x0) / w);
+        return (int)std::min((double)(S - 1), std::max(0.0, f));
+    };
+    for (int q = 0; q < m && S > 1; q++)
+        if (dep(pa[q]) && dep(pb[q]) && std::abs(stripe(pa[q]) - stripe(pb[q])) > 1) S = 1;
+    std::vector<int> grp(m);
+    for (int q = 0; q < m; q++) {
+        const bool da = dep(pa[q]), db = dep(pb[q]);
+        int sa = da ? stripe(pa[q]) : -1, sb = db ? stripe(pb[q]) : -1;
+        if (sa < 0) sa = sb;
+        if (sb < 0) sb = sa;
+        if (sa < 0) sa = sb = 0;
+        grp[q] = (sa >> 1) == (sb >> 1) ? 2 * (sa >> 1) : 2 * (std::min(sa, sb) >> 1) + 1;
+    }
+    /* greedy colouring per group, pairs ascending */
+    const int G = S;                                  /* bands 0, 2, .., seams 1, 3, .. */
+    std::vector<int> col(m, -1), ncol(G, 0);
+    std::vector<unsigned long long> used(nb, 0ull);
+    for (int g = 0; g < G; g++) {
+        std::vector<int> touched;
+        for (int q = 0; q < m; q++) {
+            if (grp[q] != g) continue;
+            const int a = dep(pa[q]) ? pa[q] : -1, b = dep(pb[q]) ? pb[q] : -1;
+            const unsigned long long forb = (a >= 0 ? used[a] : 0ull) | (b >= 0 ? used[b] : 0ull);
+            if (forb == ~0ull) return -1;
+            int c = 0;
+            while (forb & (1ull << c)) c++;
+            col[q] = c;
+            ncol[g] = std::max(ncol[g], c + 1);
+            if (a >= 0) { used[a] |= 1ull << c; touched.push_back(a); }
+            if (b >= 0) { used[b] |= 1ull << c; touched.push_back(b); }
+        }
+        for (int e : touched) used[e] = 0ull;
+    }
+    /* canonical step sequence */
+    std::vector<int> stepOf(G * 64, -1);
+    int steps = 0;
+    for (int ph = 0; ph < 2; ph++)
+        for (int g = ph; g < G; g += 2)
+            for (int c = 0; c < ncol[g]; c++) stepOf[g * 64 + c] = steps++;
+    std::vector<std::vector<int>> bystep(steps);
+    for (int q = 0; q < m; q++) bystep[stepOf[grp[q] * 64 + col[q]]].push_back(q);
+    int t = 0;
+    for (int k = 0; k < steps; k++)
+        for (int q : bystep[k])
+            for (int j = 0; j < pn[q]; j++) order[t++] = ps[q] + j;
+    if (pair_step) {
+        for (int p = 0; p < npairs; p++) pair_step[p] = -1;
+        for (int q = 0; q < m; q++)
+            if (pid[q] >= 0 && pid[q] < npairs) pair_step[pid[q]] = stepOf[grp[q] * 64 + col[q]];
+    }
+    if (nstripes) *nstripes = S;
+    return steps;
+}
+
 extern "C" int lpeo_rigid_update(const lpe_rigid_config *cfg, int nb, lpe_body *bodies,
                                  const double *verts, lpeo_rigid_stats *st) {
     std::vector<int32_t> pairs(2 * 1024);
@@ -783,7 +899,7 @@ extern "C" int lpeo_rigid_update(const lpe_rigid_config *cfg, int nb, lpe_body *
     if (st) { st->pairs = np; st->contacts = nc; st->manifolds = 0; st->dynamicBodies = 0; }
     if (nc == 0) return 0;   /* rigid_body_collision.cpp:35-37 */
     std::vector<int32_t> order(nc);
-    if (lpeo_colour_order(nb, bodies, nc, cs.data(), order.data(), nullptr, 0) < 0)
+    if (lpeo_stripe_order(nb, bodies, nc, cs.data(), order.data(), nullptr, 0, nullptr) < 0)
         return -1;
     int nd = lpeo_pgs(cfg, nb, bodies, nc, cs.data(), order.data());
     lpeo_position_solver(cfg, nb, bodies, nc, cs.data(), order.data());

@@ -36,7 +36,7 @@ int lpeo_pgs(const lpe_rigid_config *cfg, int nb, lpe_body *bodies, int nc,
 int lpeo_position_solver(const lpe_rigid_config *cfg, int nb, lpe_body *bodies, int nc,
                          const lpe_contact *contacts, const int32_t *order);
 
-/* Canonical solver order (the device's k_pair_colour): colour-major over the
+/* Round-2 canonical order (k_pair_colour, kept for comparison): colour-major over the
  * edge-coloured contact pairs, pairs ascending inside a colour, contacts of a
  * pair in narrowphase order.  order receives nc contact indices; pair_colour
  * (optional, npairs entries) the colour of each pair (-1: no contact).
@@ -44,9 +44,18 @@ int lpeo_position_solver(const lpe_rigid_config *cfg, int nb, lpe_body *bodies, 
 int lpeo_colour_order(int nb, const lpe_body *bodies, int nc, const lpe_contact *cs,
                       int32_t *order, int32_t *pair_colour, int npairs);
 
+/* Canonical solver order since round 3: striped Gauss-Seidel (see
+ * rigid_oracle.cpp): x-stripes of the movable bodies, per stripe an interior
+ * and a boundary group, each coloured greedily; phase A (even stripes) then
+ * phase B (odd stripes).  pair_step (optional) receives each pair's step,
+ * nstripes (optional) the stripe count.  Returns the steps (-1: > 64 colours
+ * in a group). */
+int lpeo_stripe_order(int nb, const lpe_body *bodies, int nc, const lpe_contact *cs,
+                      int32_t *order, int32_t *pair_step, int npairs, int32_t *nstripes);
+
 /* RigidBodyCollisionSystem::update (rigid_body_collision.cpp:24-50) with the
  * canonical orders: pairs by (eid_a, eid_b); PGS and position solver in the
- * colour-major order of lpeo_colour_order. */
+ * striped order of lpeo_stripe_order. */
 int lpeo_rigid_update(const lpe_rigid_config *cfg, int nb, lpe_body *bodies,
                       const double *verts, lpeo_rigid_stats *stats);
 

@@ -1,0 +1,38 @@
+"""Per-workgroup phase times of k_pgs_stripes / k_pos_stripes on the rigid
+microbench fixture (tests/golden/pile_M_t250.npz).
+
+    profiles/trace_build.sh rigid pt -DLPE_PTRACE
+    LPE_LIB=profiles/_var/liblpe_pt.so python3 profiles/stripe_trace.py
+
+Stamps (wall_clock64, 100 MHz) per workgroup: 0 kernel entry, 1 staged, then
+per iteration: A start (after the wait + reload), A end, A published, B start,
+B end, B published."""
+import ctypes as C, os, sys
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from conftest import lpe
+z = np.load(os.path.join(ROOT, "tests", "golden", "pile_M_t250.npz"))
+ctx = lpe.Context(0)
+ctx.rigid_set_config(lpe.rigid_config(universe=32.0))
+for _ in range(3):
+    ctx.rigid_upload(z["bodies"], z["verts"]); st = ctx.rigid_step()
+L = lpe.lib(); L.lpe_strace.argtypes = [C.c_void_p]
+buf = np.zeros(2 * 32 * 64, np.uint64); L.lpe_strace(buf.ctypes.data)
+buf = buf.reshape(2, 32, 64).astype(np.int64)
+it = 10
+for w, name in ((0, "pgs"), (1, "pos")):
+    t = buf[w]
+    t0 = t[:, 0].min()
+    rel = (t - t0) / 100.0
+    print(f"{name}: entry spread {rel[:, 0].max():.2f} us, staged by {rel[:, 1].max():.2f} us, "
+          f"end {rel[:, 7 + 6 * (it - 1)].max():.2f} us")
+    ph = rel[:, 2:2 + 6 * it].reshape(32, it, 6)
+    A = ph[:, :, 1] - ph[:, :, 0]; B = ph[:, :, 4] - ph[:, :, 3]
+    pubA = ph[:, :, 2] - ph[:, :, 1]; waitB = ph[:, :, 3] - ph[:, :, 2]; pubB = ph[:, :, 5] - ph[:, :, 4]
+    waitA = ph[:, 1:, 0] - ph[:, :-1, 5]
+    for nm, a in (("A", A), ("B", B), ("pubA", pubA), ("waitB", waitB), ("pubB", pubB), ("waitA", waitA)):
+        print(f"  {nm:6s} mean {a.mean():6.2f}  max {a.max():6.2f}  per-WG mean over it: "
+              f"{np.round(a.mean(1)[:8], 2).tolist()}")
+    print("  WG0 timeline it0-2:", np.round(ph[0, :3].ravel(), 2).tolist())
+    print("  WG1 timeline it0-2:", np.round(ph[1, :3].ravel(), 2).tolist())

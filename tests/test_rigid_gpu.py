@@ -47,10 +47,17 @@ def same(a, b, keys, rtol=0.0, atol=0.0):
 
 
 def close_state(out, ref):
+    """Device vs the restatement in the canonical order: bit for bit (the
+    trigonometry is the implementation both share, csrc/lpe_trig.h)."""
+    same(out, ref, POSE)
+    same(out, ref, VEL)
+
+
+def ref_state(out, ref):
+    """Device vs the reference's own fixture (its platform libm rounds sin/cos
+    in the last bit differently): poses 1e-7, velocities 1e-5 relative."""
     same(out, ref, POSE, rtol=1e-7, atol=1e-9)
     same(out, ref, VEL, rtol=1e-5, atol=1e-6)
-    d = max(float(np.max(np.abs(out[k] - ref[k]))) for k in POSE + VEL)
-    print(f"max |device - reference| over pose/velocity: {d:.3e}")
 
 
 @pytest.mark.parametrize("path", FIXTURES, ids=[os.path.basename(p) for p in FIXTURES])
@@ -66,7 +73,7 @@ def test_reference_orders_replay(gpu_ctx, path):
     same(cs, ref, GEOM, rtol=1e-12, atol=1e-14)
     out = gpu_ctx.rigid_download()
     if len(ref):
-        close_state(out, z["after_pos"])
+        ref_state(out, z["after_pos"])
 
 
 @pytest.mark.parametrize("path", FIXTURES, ids=[os.path.basename(p) for p in FIXTURES])
@@ -81,7 +88,7 @@ def test_canonical_step_matches_restatement(gpu_ctx, oracle_mod, path):
     np.testing.assert_array_equal(pairs, ref_pairs)          # bit-exact pair list, canonical order
     ref_cs = oracle_mod.narrowphase(pre, z["verts"], ref_pairs)
     same(cs, ref_cs, ("a", "b", "pair"))
-    same(cs, ref_cs, GEOM, rtol=1e-12, atol=1e-14)
+    same(cs, ref_cs, GEOM)                                    # (shared trigonometry: exact)
     out = gpu_ctx.rigid_download()
     ref, rst = oracle_mod.rigid_update(cfg, pre, z["verts"])
     close_state(out, ref)
@@ -103,9 +110,9 @@ def test_integrators_match_reference(gpu_ctx, path):
 
 @pytest.mark.parametrize("path", FIXTURES, ids=[os.path.basename(p) for p in FIXTURES])
 def test_colour_order_matches_restatement(gpu_ctx, oracle_mod, path):
-    """The canonical solver order: the device's pair colouring equals the
-    restated one (integer work, bit-exact) and is proper: no movable body
-    appears twice in one colour."""
+    """The canonical solver order (striped Gauss-Seidel, round 3): every
+    pair's step on the device equals the restated one (integer work,
+    bit-exact) and every step is proper: no movable body appears twice."""
     z, cfg = load(path)
     pre = z["before_rigid"]
     gpu_ctx.rigid_set_config(cfg)
@@ -113,7 +120,7 @@ def test_colour_order_matches_restatement(gpu_ctx, oracle_mod, path):
     st = gpu_ctx.rigid_step()
     pairs, cs = gpu_ctx.rigid_contacts()
     col, ncol = gpu_ctx.rigid_colours()
-    _, ref_col, ref_ncol = oracle_mod.colour_order(pre, cs, len(pairs))
+    _, ref_col, ref_ncol, _ = oracle_mod.stripe_order(pre, cs, len(pairs))
     np.testing.assert_array_equal(col, ref_col)
     assert ncol == ref_ncol == st["pgsLevels"]
     inf = ((pre["flags"] & lpe.BODY_HAS_MASS) != 0) & (pre["mass"] > 1e29)
@@ -162,9 +169,9 @@ def test_metric_pile_canonical(gpu_ctx, oracle_mod):
     assert st["pairs"] == rst.pairs and st["contacts"] == rst.contacts and rst.contacts > 20000
     pairs, cs = gpu_ctx.rigid_contacts()
     col, ncol = gpu_ctx.rigid_colours()
-    _, ref_col, ref_ncol = oracle_mod.colour_order(b, cs, len(pairs))
+    _, ref_col, ref_ncol, ns = oracle_mod.stripe_order(b, cs, len(pairs))
     np.testing.assert_array_equal(col, ref_col)
-    assert ncol == ref_ncol
+    assert ncol == ref_ncol and ns >= 16, (ncol, ns)
     close_state(gpu_ctx.rigid_download(), ref)
 
 
