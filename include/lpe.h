@@ -145,9 +145,8 @@ typedef struct lpe_sph_stats {
     int32_t overCapCellsTotal;
     int32_t maxCellOccupancyTotal;
     /* slab decomposition: ghost records this rank sends to its left / right
-     * neighbour per sub-step (the neighbour's request: 1.5x its largest
-     * receive of the previous tick + 512, at most the capacity; 0 without a
-     * neighbour or off a slab) */
+     * neighbour per sub-step (every exchange moves the capacity, ghost_cap of
+     * lpe_sph_set_slab; 0 without a neighbour or off a slab) */
     int32_t haloWire[2];
 } lpe_sph_stats;
 

@@ -1680,12 +1680,11 @@ struct Shard {
     float x0 = 0.f, x1 = 0.f, D = 0.f;
     int hasL = 0, hasR = 0;
     int cap = 0;                       // ghosts / migrants per side
-    // records on the wire per direction (ghosts: wg*, migrants: wm*; s = this
-    // rank sends, r = receives; L/R = neighbour): the receiver's request from
-    // the previous tick, carried in the migration headers (sph_migrate); the
-    // first tick sends the capacity
-    int wgsL = 0, wgsR = 0, wgrL = 0, wgrR = 0;
-    int wmsL = 0, wmsR = 0, wmrL = 0, wmrR = 0;
+    // Every exchange moves the whole capacity-sized buffer (HDR + cap records):
+    // both ends know its size without a host round trip, so a spike of
+    // ghosts or migrants within the capacity costs nothing.  (Round 2 sized
+    // the wire by the receiver's request from the previous tick; a spike
+    // above the request was fatal and lost migrants.)
     int32_t *ntot = nullptr;           // device: owned + ghosts of the sub-step
     float *gsL = nullptr, *gsR = nullptr, *grL = nullptr, *grR = nullptr;
     float *msL = nullptr, *msR = nullptr, *mrL = nullptr, *mrR = nullptr;
@@ -1696,11 +1695,6 @@ struct Shard {
     int32_t *obsum = nullptr;
     float *orho = nullptr, *opr = nullptr;   // rho / p of the owned particles, P order
 };
-
-static inline void shard_reset_wire(Shard &h) {
-    h.wgsL = h.wgsR = h.wgrL = h.wgrR = h.cap;
-    h.wmsL = h.wmsR = h.wmrL = h.wmrR = h.cap;
-}
 
 // (also clears the ghost send headers for the pack that follows: two
 // memset launches fewer per sub-step)
@@ -1761,22 +1755,18 @@ __global__ void k_ghost_pack(int n, PState P, KState K, float x0, float x1, floa
     }
 }
 
-// ghosts -> P[nown ...] (left ones first), bin key + histogram
-// (wL / wR: records the neighbour put on the wire; its header holds how many
-// it packed, which may exceed that - a ghost lost on the wire: overflow)
+// ghosts -> P[nown ...] (left ones first), bin key + histogram (a header
+// count above the capacity: the sender flagged ST_HALO_OVERFLOW)
 __global__ void k_ghost_unpack(const float *__restrict__ rL, const float *__restrict__ rR, int cap,
-                               int wL, int wR,
                                int nown, PState P, KState K, uint32_t *__restrict__ key,
                                int32_t *__restrict__ count, float eps, float cs, int ox, int oy,
                                int W, int H, int32_t *__restrict__ ntot, int32_t *__restrict__ status) {
     const int t = blockIdx.x * TPB + threadIdx.x;
-    const int gL = rcount(rL, wL), gR = rcount(rR, wR);
+    const int gL = rcount(rL, cap), gR = rcount(rR, cap);
     if (t == 0) {
         *ntot = nown + gL + gR;
-        const int cL = rL ? *(const int *)rL : 0, cR = rR ? *(const int *)rR : 0;
-        if (cL > wL || cR > wR) atomicOr(&status[ST_HALO_OVERFLOW], 1);
-        atomicMax(&status[ST_RX_GHOST_L], cL);
-        atomicMax(&status[ST_RX_GHOST_R], cR);
+        atomicMax(&status[ST_RX_GHOST_L], rL ? *(const int *)rL : 0);
+        atomicMax(&status[ST_RX_GHOST_R], rR ? *(const int *)rR : 0);
     }
     const float *src;
     int slot;
@@ -1809,11 +1799,13 @@ __global__ void k_ghost_unpack(const float *__restrict__ rL, const float *__rest
     atomicAdd(&count[k], 1);
 }
 
-// particles that left the slab -> migrant buffers; keep flags for the rest
+// particles that left the slab -> migrant buffers; keep flags for the rest.
+// Migrants beyond the capacity stay owned here this tick and leave with a
+// later one (the owner of a particle never changes its result: ghosts carry
+// the global id; the drift check bounds how far outside it may stay)
 __global__ void k_mig_pack(int n, PState P, const float *__restrict__ rho, const float *__restrict__ pr,
                            float x0, float x1, int hasL, int hasR, float *__restrict__ mL,
-                           float *__restrict__ mR, int32_t *__restrict__ keep, int cap,
-                           int32_t *__restrict__ status) {
+                           float *__restrict__ mR, int32_t *__restrict__ keep, int cap) {
     int i = blockIdx.x * TPB + threadIdx.x;
     if (i >= n) return;
     const float x = P.x[i];
@@ -1823,35 +1815,18 @@ __global__ void k_mig_pack(int n, PState P, const float *__restrict__ rho, const
     keep[i] = buf ? 0 : 1;
     if (!buf) return;
     int k = atomicAdd(hdr(buf), 1);
-    if (k >= cap) { atomicOr(&status[ST_HALO_OVERFLOW], 1); keep[i] = 1; return; }
+    if (k >= cap) { keep[i] = 1; return; }
     float *r = buf + HDR + (size_t)k * MREC;
     r[0] = x; r[1] = P.y[i]; r[2] = P.vx[i]; r[3] = P.vy[i];
     r[4] = P.m[i]; r[5] = __int_as_float(P.id[i]); r[6] = rho[i]; r[7] = pr[i];
 }
 
-// The sizes this rank asks its neighbours to send next tick, into header
-// words 1 (ghost records) and 2 (migrant records) of the outgoing migration
-// messages: 1.5x the most ghosts received in a sub-step of this tick + 512
-// (ghost counts change by well under 1% a tick), 2x the most migrants ever
-// received + 512, both capped at the buffers' capacity.  A sub-step that
-// still exceeds it raises ST_HALO_OVERFLOW (k_ghost_unpack), never silently.
-__global__ void k_wire_request(float *__restrict__ mL, float *__restrict__ mR, int cap,
-                               int32_t *__restrict__ status) {
-    if (threadIdx.x != 0) return;
-    auto g = [cap](int c) { return min(cap, c + c / 2 + 512); };
-    auto m = [cap](int c) { return min(cap, 2 * c + 512); };
-    if (mL) { hdr(mL)[1] = g(status[ST_RX_GHOST_L]); hdr(mL)[2] = m(status[ST_RX_MIG_L]); }
-    if (mR) { hdr(mR)[1] = g(status[ST_RX_GHOST_R]); hdr(mR)[2] = m(status[ST_RX_MIG_R]); }
-    status[ST_RX_GHOST_L] = status[ST_RX_GHOST_R] = 0;
-}
-
-// the migrants received this tick: their true counts (header word 0) against
-// what came over the wire, and the running maxima that size the next requests
-__global__ void k_mig_received(const float *__restrict__ mrL, const float *__restrict__ mrR, int wL, int wR,
+// the migrants received this tick (header word 0; beyond the capacity the
+// sender kept them): the most so far, a statistic
+__global__ void k_mig_received(const float *__restrict__ mrL, const float *__restrict__ mrR,
                                int32_t *__restrict__ status) {
     if (threadIdx.x != 0) return;
     const int cL = mrL ? *(const int *)mrL : 0, cR = mrR ? *(const int *)mrR : 0;
-    if (cL > wL || cR > wR) atomicOr(&status[ST_HALO_OVERFLOW], 1);
     status[ST_RX_MIG_L] = max(status[ST_RX_MIG_L], cL);
     status[ST_RX_MIG_R] = max(status[ST_RX_MIG_R], cR);
 }
@@ -2420,7 +2395,6 @@ extern "C" int lpe_sph_upload(lpe_ctx *ctx, int n, const float *x, const float *
     }
     LPE_HIP(ctx, hipMemsetAsync(d.status, 0, sizeof(int32_t) * ST_COUNT, s));
     d.upload_gen++;
-    if (d.shard) shard_reset_wire(*d.shard);          // new particles: the first exchange sends the capacity
     return LPE_OK;
 }
 
@@ -2707,13 +2681,12 @@ static int sph_hash_shard(lpe_ctx *ctx, float subDt, float halfDt, bool first, i
                h.x1, h.D,
                drift, h.hasL, h.hasR, h.gsL, h.gsR, h.cap, d.status);
     LPE_CHECK_LAUNCH(ctx, "k_ghost_pack");
+    const size_t gb = ghost_bytes(h.cap);
     st = tr->halo(ctx, h.hasL ? h.gsL : nullptr, h.hasR ? h.gsR : nullptr, h.hasL ? h.grL : nullptr,
-                  h.hasR ? h.grR : nullptr, ghost_bytes(h.wgsL), ghost_bytes(h.wgsR), ghost_bytes(h.wgrL),
-                  ghost_bytes(h.wgrR));
+                  h.hasR ? h.grR : nullptr, gb, gb, gb, gb);
     if (st) return st;
     LPE_KERNEL(ctx, "k_ghost_unpack", k_ghost_unpack, dim3(nblk1(2 * h.cap)), dim3(TPB), 0, s,
-               h.hasL ? h.grL : (const float *)nullptr, h.hasR ? h.grR : (const float *)nullptr, h.cap, h.wgrL,
-               h.wgrR, d.n,
+               h.hasL ? h.grL : (const float *)nullptr, h.hasR ? h.grR : (const float *)nullptr, h.cap, d.n,
                d.P, sph_kstate(d), d.key, d.count, eps, d.cs, d.ox, d.oy, d.W, d.H, h.ntot, d.status);
     LPE_CHECK_LAUNCH(ctx, "k_ghost_unpack");
     st = sph_scan(ctx, C, d.count, d.start, d.cursor, d.blocksum, kb, true, h.bb);
@@ -2737,30 +2710,23 @@ static int sph_migrate(lpe_ctx *ctx) {
     LPE_HIP(ctx, hipMemsetAsync(h.msL, 0, sizeof(float) * HDR, s));
     LPE_HIP(ctx, hipMemsetAsync(h.msR, 0, sizeof(float) * HDR, s));
     LPE_KERNEL(ctx, "k_mig_pack", k_mig_pack, dim3(nblk1(d.n)), dim3(TPB), 0, s, d.n, d.P, h.orho, h.opr, h.x0,
-               h.x1, h.hasL, h.hasR, h.msL, h.msR, h.keep, h.cap, d.status);
-    LPE_KERNEL(ctx, "k_wire_request", k_wire_request, dim3(1), dim3(64), 0, s, h.hasL ? h.msL : (float *)nullptr,
-               h.hasR ? h.msR : (float *)nullptr, h.cap, d.status);
+               h.x1, h.hasL, h.hasR, h.msL, h.msR, h.keep, h.cap);
     LPE_CHECK_LAUNCH(ctx, "k_mig_pack");
+    const size_t mb = mig_bytes(h.cap);
     int st = ctx->transport->halo(ctx, h.hasL ? h.msL : nullptr, h.hasR ? h.msR : nullptr,
-                                  h.hasL ? h.mrL : nullptr, h.hasR ? h.mrR : nullptr, mig_bytes(h.wmsL),
-                                  mig_bytes(h.wmsR), mig_bytes(h.wmrL), mig_bytes(h.wmrR));
+                                  h.hasL ? h.mrL : nullptr, h.hasR ? h.mrR : nullptr, mb, mb, mb, mb);
     if (st) return st;
     LPE_KERNEL(ctx, "k_mig_received", k_mig_received, dim3(1), dim3(64), 0, s, h.hasL ? h.mrL : (const float *)nullptr,
-               h.hasR ? h.mrR : (const float *)nullptr, h.wmrL, h.wmrR, d.status);
-    // the four headers: [0] migrant count, [1] / [2] the ghost / migrant
-    // records requested for the next tick (k_wire_request)
+               h.hasR ? h.mrR : (const float *)nullptr, d.status);
+    // the four headers: [0] migrants packed (beyond the capacity: kept)
     int32_t hd4[4][HDR] = {};
     float *hb[4] = {h.hasL ? h.msL : nullptr, h.hasR ? h.msR : nullptr, h.hasL ? h.mrL : nullptr,
                     h.hasR ? h.mrR : nullptr};
     for (int k = 0; k < 4; k++)
         if (hb[k]) LPE_HIP(ctx, hipMemcpyAsync(hd4[k], hb[k], sizeof(int32_t) * HDR, hipMemcpyDeviceToHost, s));
     LPE_HIP(ctx, hipStreamSynchronize(s));
-    int32_t cnt[4] = {std::min(hd4[0][0], h.cap), std::min(hd4[1][0], h.cap), std::min(hd4[2][0], h.wmrL),
-                      std::min(hd4[3][0], h.wmrR)};
-    // next tick's wire: what I asked for (my outgoing headers) I receive,
-    // what the neighbours asked for (their headers) I send
-    if (h.hasL) { h.wgrL = hd4[0][1]; h.wmrL = hd4[0][2]; h.wgsL = hd4[2][1]; h.wmsL = hd4[2][2]; }
-    if (h.hasR) { h.wgrR = hd4[1][1]; h.wmrR = hd4[1][2]; h.wgsR = hd4[3][1]; h.wmsR = hd4[3][2]; }
+    int32_t cnt[4];
+    for (int k = 0; k < 4; k++) cnt[k] = std::min(hd4[k][0], h.cap);
     const int kept = d.n - cnt[0] - cnt[1];
     const int nn = kept + cnt[2] + cnt[3];
     if (nn + shard_slots(h) > d.cap_n) {
@@ -3022,7 +2988,8 @@ static int check_status(lpe_ctx *ctx) {
         return LPE_ERR_OVERFLOW;
     }
     if (status[ST_HALO_OVERFLOW]) {
-        ctx->err = "a slab exchange buffer overflowed (raise ghost_cap of lpe_sph_set_slab)";
+        ctx->err = "slab decomposition: more ghosts than ghost_cap within the halo of a slab edge (raise "
+                   "ghost_cap of lpe_sph_set_slab)";
         return LPE_ERR_OVERFLOW;
     }
     return LPE_OK;
@@ -3096,8 +3063,8 @@ extern "C" int lpe_sph_get_stats(lpe_ctx *ctx, lpe_sph_stats *out) {
     out->refUndefined = status[ST_REF_UB];
     out->overCapCellsTotal = status[ST_OVER_CAP_TOTAL];
     out->maxCellOccupancyTotal = status[ST_MAX_OCC_TOTAL];
-    out->haloWire[0] = (d.shard && d.shard->hasL) ? d.shard->wgsL : 0;
-    out->haloWire[1] = (d.shard && d.shard->hasR) ? d.shard->wgsR : 0;
+    out->haloWire[0] = (d.shard && d.shard->hasL) ? d.shard->cap : 0;
+    out->haloWire[1] = (d.shard && d.shard->hasR) ? d.shard->cap : 0;
     return LPE_OK;
 }
 
@@ -3198,7 +3165,6 @@ extern "C" int lpe_sph_set_slab(lpe_ctx *ctx, float x0, float x1, float halo, in
     h->x0 = x0; h->x1 = x1; h->D = halo;
     h->hasL = has_left ? 1 : 0; h->hasR = has_right ? 1 : 0;
     h->cap = ghost_cap;
-    shard_reset_wire(*h);
     d.shard = h;
     LPE_HIP(ctx, hipMalloc((void **)&h->ntot, sizeof(int32_t)));
     LPE_HIP(ctx, hipMalloc((void **)&h->bb, sizeof(float4)));

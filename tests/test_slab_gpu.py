@@ -111,35 +111,50 @@ def test_slab_coupled_first_tick():
             np.testing.assert_array_equal(r_out[k], rref[k], err_msg=k)
 
 
-def test_slab_wire_sized_by_fill():
-    """After the first tick each direction's exchange carries the receiver's
-    request (1.5x its largest ghost receive + 512), not the capacity; the
-    merged state stays bit-identical to the single domain over 5 ticks with
-    particles migrating across the edges."""
+def test_slab_spike_within_capacity():
+    """Every exchange moves the whole capacity (a spike above the
+    previous tick's request used to be fatal and lost migrants): a velocity
+    jump after 2 ticks pushes many more ghosts and migrants over the edges,
+    and 3 more ticks stay bit-identical to the single domain; the reported
+    wire is the capacity."""
     s = scenes.scene("small96_0")
     fl = dict(s["fluid"])
     fl["vx"] = np.full(len(fl["x"]), 0.8)
     rig = np.zeros(0, lpe.RIGID_DTYPE)
-    ref, _, _ = _single(fl, rig, 5)
+    ref2, _, _ = _single(fl, rig, 2)
     edges = slab.slab_edges(fl["x"], 3)
     cfg = lpe.default_fluid_config()
-    ctxs = [lpe.Context(0) for _ in range(3)]
-    try:
-        caps = [slab.ghost_capacity(np.asarray(fl["x"], np.float32), edges, slab.default_halo(cfg))] * 3
-        for r, c in enumerate(ctxs):
-            slab.setup_rank(c, r, 3, fl, edges, cfg, rig)
-        lpe.mg_loopback_run(ctxs, 5, DT)
-        wires = [c.sph_stats()["haloWire"] for c in ctxs]
-        parts = [c.sph_download_owned(cap=len(fl["x"])) for c in ctxs]
-    finally:
-        for c in ctxs:
-            c.close()
-    got = slab.merge_owned(parts, len(fl["x"]))
+    cap = slab.ghost_capacity(np.asarray(fl["x"], np.float32), edges, slab.default_halo(cfg))
+
+    def loop(flin, nticks):
+        ctxs = [lpe.Context(0) for _ in range(3)]
+        try:
+            for r, c in enumerate(ctxs):
+                slab.setup_rank(c, r, 3, flin, edges, cfg, rig, ghost_cap=cap)
+            lpe.mg_loopback_run(ctxs, nticks, DT)
+            wires = [c.sph_stats()["haloWire"] for c in ctxs]
+            parts = [c.sph_download_owned(cap=len(flin["x"])) for c in ctxs]
+        finally:
+            for c in ctxs:
+                c.close()
+        return slab.merge_owned(parts, len(flin["x"])), wires
+
+    got2, _ = loop(fl, 2)
     for k in slab.FIELDS:
-        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+        np.testing.assert_array_equal(got2[k], ref2[k], err_msg=k)
+
+    def jumped(state):
+        out = dict(x=state["x"], y=state["y"], vx=np.asarray(state["vx"], np.float32) + np.float32(3.0),
+                   vy=state["vy"], mass=fl["mass"], density=state["density"], pressure=state["pressure"])
+        return out
+
+    ref5, _, _ = _single(jumped(ref2), rig, 3)
+    got5, wires = loop(jumped(got2), 3)
+    for k in slab.FIELDS:
+        np.testing.assert_array_equal(got5[k], ref5[k], err_msg=k)
     assert wires[0][0] == 0 and wires[2][1] == 0            # no neighbour there
     for w in (wires[0][1], wires[1][0], wires[1][1], wires[2][0]):
-        assert 512 < w < caps[0], (wires, caps)
+        assert w == cap, (wires, cap)
 
 
 def test_slab_halo_overflow_reported():
