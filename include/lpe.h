@@ -25,6 +25,7 @@
 #ifndef LPE_H
 #define LPE_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -440,6 +441,24 @@ int  lpe_sph_set_domain(lpe_ctx *ctx, double x0, double y0, double x1, double y1
  * rank 0 creates the 128-byte id, every rank passes it to lpe_mg_init_rccl. */
 int  lpe_mg_unique_id(char id[128]);
 int  lpe_mg_init_rccl(lpe_ctx *ctx, int nranks, int rank, const char *id);
+/* Host-staged transport: the caller moves host copies of the exchange
+ * buffers between the ranks' processes (e.g. torch.distributed over gloo).
+ * halo: send sbL bytes of sendL to rank-1 and sbR of sendR to rank+1,
+ * receive rbL bytes from rank-1 into recvL and rbR from rank+1 into recvR
+ * (NULL / 0 where there is no neighbour); the sizes must equal the
+ * neighbour's (the callback checks them and returns non-zero on a mismatch).
+ * allreduce_f32 (op 0 sum, 1 min) and allreduce_i64 (sum, two's-complement
+ * wrap) reduce n host values in place.  Every callback returns 0 on success;
+ * a non-zero return fails the step with LPE_ERR_STATE.  Every call drains
+ * the context's stream (validation transport, not the production path). */
+typedef struct lpe_host_transport {
+    void *user;
+    int (*halo)(void *user, const void *sendL, size_t sbL, const void *sendR, size_t sbR, void *recvL,
+                size_t rbL, void *recvR, size_t rbR);
+    int (*allreduce_f32)(void *user, float *buf, int n, int op);
+    int (*allreduce_i64)(void *user, long long *buf, int n);
+} lpe_host_transport;
+int  lpe_mg_init_host(lpe_ctx *ctx, int nranks, int rank, const lpe_host_transport *t);
 /* In-process transport for tests: n contexts (ranks 0..n-1, any devices)
  * each advanced nticks by its own host thread — lpe_world_tick(cfg, 1) per
  * tick when cfg is non-NULL, else lpe_sph_step(dt_tick). */

@@ -195,9 +195,97 @@ struct LoopTransport : Transport {
     }
 };
 
+// ---------------------------------------------------------------------------
+// Host-staged: the caller's callbacks (lpe_host_transport) move host copies of
+// the buffers between processes -- e.g. torch.distributed over gloo.  Each
+// operation drains the context's stream, stages device -> pinned host, calls
+// the callback, and copies the result back.  Slow by construction; it exists
+// so the cross-process protocol (both ends' sizes, the order of the calls)
+// runs on hardware that has one GPU (RCCL refuses two ranks on one device).
+struct HostTransport : Transport {
+    lpe_host_transport cb{};
+    std::vector<char *> pinned;            // [sendL, sendR, recvL, recvR, reduce]
+    std::vector<size_t> pcap;
+    ~HostTransport() override {
+        for (char *p : pinned)
+            if (p) (void)hipHostFree(p);
+    }
+    char *stage(lpe_ctx *ctx, int k, size_t bytes) {
+        if (pcap[k] < bytes) {
+            if (pinned[k]) (void)hipHostFree(pinned[k]);
+            pinned[k] = nullptr;
+            pcap[k] = 0;
+            if (hipHostMalloc((void **)&pinned[k], std::max<size_t>(bytes, 64), 0) != hipSuccess) {
+                ctx->err = "host transport: hipHostMalloc failed";
+                return nullptr;
+            }
+            pcap[k] = std::max<size_t>(bytes, 64);
+        }
+        return pinned[k];
+    }
+    int callback_failed(lpe_ctx *ctx, const char *what, int rc) {
+        ctx->err = std::string("host transport: ") + what + " callback returned " + std::to_string(rc) +
+                   " (a size that differs from the neighbour's, or a failed peer)";
+        return LPE_ERR_STATE;
+    }
+    int halo(lpe_ctx *ctx, const void *sendL, const void *sendR, void *recvL, void *recvR,
+             size_t sbL, size_t sbR, size_t rbL, size_t rbR) override {
+        const bool L = sendL && recvL && rank > 0, R = sendR && recvR && rank < nranks - 1;
+        char *hs[2] = {L ? stage(ctx, 0, sbL) : nullptr, R ? stage(ctx, 1, sbR) : nullptr};
+        char *hr[2] = {L ? stage(ctx, 2, rbL) : nullptr, R ? stage(ctx, 3, rbR) : nullptr};
+        if ((L && (!hs[0] || !hr[0])) || (R && (!hs[1] || !hr[1]))) return LPE_ERR_HIP;
+        if (L && hipMemcpyAsync(hs[0], sendL, sbL, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) return LPE_ERR_HIP;
+        if (R && hipMemcpyAsync(hs[1], sendR, sbR, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess) return LPE_ERR_HIP;
+        if (hipStreamSynchronize(ctx->stream) != hipSuccess) return LPE_ERR_HIP;
+        const int rc = cb.halo(cb.user, hs[0], L ? sbL : 0, hs[1], R ? sbR : 0, hr[0], L ? rbL : 0, hr[1],
+                               R ? rbR : 0);
+        if (rc) return callback_failed(ctx, "halo", rc);
+        if (L && hipMemcpyAsync(recvL, hr[0], rbL, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) return LPE_ERR_HIP;
+        if (R && hipMemcpyAsync(recvR, hr[1], rbR, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) return LPE_ERR_HIP;
+        // the pinned staging buffers are reused by the next call
+        return hipStreamSynchronize(ctx->stream) == hipSuccess ? LPE_OK : LPE_ERR_HIP;
+    }
+    template <class T, class F>
+    int reduce(lpe_ctx *ctx, T *buf, int n, const char *what, F call) {
+        if (nranks == 1 || n <= 0) return LPE_OK;
+        T *h = (T *)stage(ctx, 4, sizeof(T) * (size_t)n);
+        if (!h) return LPE_ERR_HIP;
+        if (hipMemcpyAsync(h, buf, sizeof(T) * n, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess)
+            return LPE_ERR_HIP;
+        const int rc = call(h);
+        if (rc) return callback_failed(ctx, what, rc);
+        if (hipMemcpyAsync(buf, h, sizeof(T) * n, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+            hipStreamSynchronize(ctx->stream) != hipSuccess)
+            return LPE_ERR_HIP;
+        return LPE_OK;
+    }
+    int allreduce(lpe_ctx *ctx, float *buf, int n, int op) override {
+        return reduce(ctx, buf, n, "allreduce_f32", [&](float *h) { return cb.allreduce_f32(cb.user, h, n, op); });
+    }
+    int allreduce_i64(lpe_ctx *ctx, long long *buf, int n) override {
+        return reduce(ctx, buf, n, "allreduce_i64", [&](long long *h) { return cb.allreduce_i64(cb.user, h, n); });
+    }
+};
+
 }  // namespace lpe
 
 using namespace lpe;
+
+extern "C" int lpe_mg_init_host(lpe_ctx *ctx, int nranks, int rank, const lpe_host_transport *t) {
+    if (!ctx || !t || !t->halo || !t->allreduce_f32 || !t->allreduce_i64 || nranks < 1 || rank < 0 ||
+        rank >= nranks)
+        return LPE_ERR_ARG;
+    if (ctx->transport) { delete ctx->transport; ctx->transport = nullptr; }
+    auto *h = new HostTransport();
+    h->cb = *t;
+    h->rank = rank;
+    h->nranks = nranks;
+    h->pinned.assign(5, nullptr);
+    h->pcap.assign(5, 0);
+    ctx->transport = h;
+    return LPE_OK;
+}
 
 extern "C" int lpe_mg_unique_id(char *id) {
     if (!id) return LPE_ERR_ARG;

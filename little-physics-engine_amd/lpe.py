@@ -204,6 +204,18 @@ SIGNATURES["lpe_sph_download_owned"] = ([C.c_void_p, C.c_int] + [_FP] * 6 + [_IP
 SIGNATURES["lpe_sph_set_domain"] = ([C.c_void_p] + [C.c_double] * 4, C.c_int)
 SIGNATURES["lpe_mg_unique_id"] = ([C.c_char_p], C.c_int)
 SIGNATURES["lpe_mg_init_rccl"] = ([C.c_void_p, C.c_int, C.c_int, C.c_char_p], C.c_int)
+HALO_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p,
+                      C.c_size_t, C.c_void_p, C.c_size_t)
+REDF_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_float), C.c_int, C.c_int)
+REDI_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_longlong), C.c_int)
+
+
+class HostTransport(C.Structure):
+    """lpe_host_transport: the callbacks of the host-staged slab transport."""
+    _fields_ = [("user", C.c_void_p), ("halo", HALO_FN), ("allreduce_f32", REDF_FN), ("allreduce_i64", REDI_FN)]
+
+
+SIGNATURES["lpe_mg_init_host"] = ([C.c_void_p, C.c_int, C.c_int, C.POINTER(HostTransport)], C.c_int)
 SIGNATURES["lpe_mg_loopback_run"] = ([C.c_int, C.POINTER(C.c_void_p), C.POINTER(WorldConfig), C.c_double,
                                       C.c_int], C.c_int)
 
@@ -446,6 +458,44 @@ class Context:
     def mg_init_rccl(self, nranks: int, rank: int, uid: bytes):
         assert len(uid) == 128
         self._chk(lib().lpe_mg_init_rccl(self._h, int(nranks), int(rank), uid), "lpe_mg_init_rccl")
+
+    def mg_init_host(self, nranks: int, rank: int, transport):
+        """Host-staged transport: `transport` has halo(sendL, sendR, recvL,
+        recvR) over numpy uint8 views (None where there is no neighbour),
+        allreduce_f32(arr, op) and allreduce_i64(arr), each reducing in place
+        and raising on failure (slab.GlooTransport is the torch.distributed
+        one).  The callbacks stay referenced by this context."""
+        def view(ptr, n, ct):
+            return None if not ptr or n == 0 else np.ctypeslib.as_array((ct * n).from_address(ptr))
+
+        def halo(_u, sL, nsL, sR, nsR, rL, nrL, rR, nrR):
+            try:
+                transport.halo(view(sL, nsL, C.c_uint8), view(sR, nsR, C.c_uint8),
+                               view(rL, nrL, C.c_uint8), view(rR, nrR, C.c_uint8))
+                return 0
+            except Exception as e:       # noqa: BLE001  (no exception may cross the C boundary)
+                transport.last_error = repr(e)
+                return 1
+
+        def redf(_u, buf, n, op):
+            try:
+                transport.allreduce_f32(np.ctypeslib.as_array(buf, shape=(n,)), int(op))
+                return 0
+            except Exception as e:       # noqa: BLE001
+                transport.last_error = repr(e)
+                return 1
+
+        def redi(_u, buf, n):
+            try:
+                transport.allreduce_i64(np.ctypeslib.as_array(buf, shape=(n,)))
+                return 0
+            except Exception as e:       # noqa: BLE001
+                transport.last_error = repr(e)
+                return 1
+
+        t = HostTransport(None, HALO_FN(halo), REDF_FN(redf), REDI_FN(redi))
+        self._host_transport = (t, transport)
+        self._chk(lib().lpe_mg_init_host(self._h, int(nranks), int(rank), C.byref(t)), "lpe_mg_init_host")
 
     def sph_probe_cells(self):
         cells = np.empty(self.n, np.int32)

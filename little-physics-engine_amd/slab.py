@@ -147,3 +147,61 @@ def gather_owned(owned: dict, n_global: int, rank: int, world: int):
     parts = [None] * world if rank == 0 else None
     dist.gather_object({k: np.asarray(v) for k, v in owned.items()}, parts, dst=0)
     return merge_owned(parts, n_global) if rank == 0 else None
+
+
+class GlooTransport:
+    """The host-staged slab transport (lpe_mg_init_host) over the default
+    torch.distributed process group (gloo): the cross-process counterpart of
+    the in-process loopback, for validating the exchange protocol where RCCL
+    cannot run (two ranks on one GPU).  Every halo first swaps a 2-word header
+    per link, [bytes I send you, bytes I expect from you], so both ends see
+    the same four sizes and a mismatch fails on both ends instead of hanging
+    or truncating; then the payloads move with isend / irecv."""
+
+    def __init__(self, rank: int, world: int):
+        self.rank, self.world = rank, world
+        self.last_error = None
+        self.calls = {"halo": 0, "allreduce_f32": 0, "allreduce_i64": 0}
+
+    def halo(self, sendL, sendR, recvL, recvR):
+        import torch
+        import torch.distributed as dist
+        self.calls["halo"] += 1
+        links = []
+        if self.rank > 0 and sendL is not None:
+            links.append((self.rank - 1, sendL, recvL))
+        if self.rank < self.world - 1 and sendR is not None:
+            links.append((self.rank + 1, sendR, recvR))
+        hdr_out, hdr_in, reqs = [], [], []
+        for peer, s, r in links:
+            mine = torch.tensor([s.nbytes, 0 if r is None else r.nbytes], dtype=torch.int64)
+            theirs = torch.zeros(2, dtype=torch.int64)
+            hdr_out.append(mine)
+            hdr_in.append(theirs)
+            reqs += [dist.isend(mine, peer), dist.irecv(theirs, peer)]
+        for q in reqs:
+            q.wait()
+        bad = [peer for (peer, _, _), m, t in zip(links, hdr_out, hdr_in)
+               if int(t[0]) != int(m[1]) or int(t[1]) != int(m[0])]
+        if bad:
+            raise RuntimeError(f"slab halo: rank {self.rank}: send/receive sizes differ from rank(s) {bad}'s "
+                               f"({[(m.tolist(), t.tolist()) for m, t in zip(hdr_out, hdr_in)]})")
+        reqs = []
+        for peer, s, r in links:
+            reqs.append(dist.isend(torch.from_numpy(s), peer))
+            if r is not None:
+                reqs.append(dist.irecv(torch.from_numpy(r), peer))
+        for q in reqs:
+            q.wait()
+
+    def allreduce_f32(self, arr, op):
+        import torch
+        import torch.distributed as dist
+        self.calls["allreduce_f32"] += 1
+        dist.all_reduce(torch.from_numpy(arr), op=dist.ReduceOp.MIN if op else dist.ReduceOp.SUM)
+
+    def allreduce_i64(self, arr):
+        import torch
+        import torch.distributed as dist
+        self.calls["allreduce_i64"] += 1
+        dist.all_reduce(torch.from_numpy(arr), op=dist.ReduceOp.SUM)
