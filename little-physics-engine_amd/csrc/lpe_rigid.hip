@@ -576,11 +576,19 @@ k_narrow(const int32_t *__restrict__ npptr, int cap, const int2 *__restrict__ pa
     ccount[k] = cnt;
 }
 
+// (also the contact count: counts[1] = the contacts kept, at most cap;
+// counts[14] = the contacts found -- more than cap is an overflow)
 __global__ void k_compact(const int32_t *__restrict__ npptr, int cap_pairs, const lpe_contact *__restrict__ slots,
                           const int32_t *__restrict__ ccount, const int32_t *__restrict__ cstart,
-                          lpe_contact *__restrict__ out, int cap) {
+                          lpe_contact *__restrict__ out, int cap, int32_t *__restrict__ counts) {
     int k = blockIdx.x * RTPB + threadIdx.x;
-    if (k >= min(*npptr, cap_pairs)) return;
+    const int np = min(*npptr, cap_pairs);
+    if (k == 0) {
+        const int tot = cstart[np];
+        counts[1] = min(tot, cap);
+        counts[14] = tot;
+    }
+    if (k >= np) return;
     int s = cstart[k];
     for (int j = 0; j < ccount[k]; j++)
         if (s + j < cap) out[s + j] = slots[(size_t)k * MAXC + j];
@@ -2838,9 +2846,13 @@ static int rgrow(lpe_ctx *ctx, T **p, size_t n) {
     return LPE_OK;
 }
 
+static int rigid_lag_drain(lpe_ctx *ctx, RigidDev *d);
+static void rigid_lag_off(lpe_ctx *ctx, RigidDev *d);
+
 int lpe_rigid_destroy_internal(lpe_ctx *ctx) {
     RigidDev *d = (RigidDev *)ctx->rigid;
     if (!d) return LPE_OK;
+    rigid_lag_off(ctx, d);
     if (d->side) (void)hipStreamSynchronize(d->side);      // nothing may still use the buffers
     if (d->psolve) (void)hipStreamSynchronize(d->psolve);
     void *ptrs[] = {d->bodies, d->verts, d->rank, d->byRank, d->aabb, d->cand, d->pcount, d->pstart,
@@ -2859,7 +2871,8 @@ int lpe_rigid_destroy_internal(lpe_ctx *ctx) {
         delete sb;
     }
     if (d->hc) (void)hipHostFree(d->hc);
-    hipEvent_t evs[] = {d->evStart, d->evDetect, d->evColour, d->evFork, d->evJoin};
+    if (d->hcr) (void)hipHostFree(d->hcr);
+    hipEvent_t evs[] = {d->evStart, d->evDetect, d->evColour, d->evFork, d->evJoin, d->evHc[0], d->evHc[1]};
     for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
     if (d->side) (void)hipStreamDestroy(d->side);
     if (d->psolve) (void)hipStreamDestroy(d->psolve);
@@ -2888,6 +2901,7 @@ extern "C" int lpe_rigid_set_config(lpe_ctx *ctx, const lpe_rigid_config *cfg) {
     if (!d->cfg_set || std::memcmp(&d->cfg, cfg, sizeof(*cfg)) != 0) {
         d->heavy_valid = false;
         d->gen++;
+        rigid_lag_off(ctx, d);
     }
     d->cfg = *cfg;
     d->cfg_set = true;
@@ -2987,6 +3001,7 @@ extern "C" int lpe_rigid_upload(lpe_ctx *ctx, int nb, const lpe_body *bodies, in
         return LPE_ERR_ARG;
     (void)hipSetDevice(ctx->device);
     RigidDev *d = rdev(ctx);
+    rigid_lag_off(ctx, d);
     if (!d->cfg_set) { lpe_rigid_config_default(&d->cfg); d->cfg_set = true; }
     static bool lds_attr = false;
     if (!lds_attr) {
@@ -3079,7 +3094,7 @@ static int rigid_versions(lpe_ctx *ctx, RigidDev *d, const int32_t *kptr, int kc
 // narrowphase on stream s, ending with the counts copied to hc (host) —
 // nothing here waits for the host.
 static int detect_launch(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pairs_in, hipStream_t s,
-                         int32_t *hc) {
+                         int32_t *hc, bool lagged = false) {
     const lpe_rigid_config &c = d->cfg;
     int nb = d->nb;
     // [0..3], [6] (counts[4], [5] belong to the solvers / gravity; [7]: solver fault, sticky)
@@ -3136,7 +3151,10 @@ static int detect_launch(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pa
     LPE_KERNEL(ctx, "k_narrow", k_narrow, dim3(rblk(d->cap_pairs, 128)), dim3(128), 0, s, d->counts, d->cap_pairs, d->pairs, d->bodies, d->verts, d->cslots, d->ccount, d->counts);
     int st = rscan(ctx, d, d->counts, d->cap_pairs, d->ccount, d->cstart, nullptr, s);
     if (st) return st;
-    LPE_HIP(ctx, hipMemcpyAsync(hc, d->counts, sizeof(int32_t) * 12, hipMemcpyDeviceToHost, s));
+    if (lagged)     // the compaction right away (capacity-bounded; the counts are checked later)
+        LPE_KERNEL(ctx, "k_compact", k_compact, dim3(rblk(d->cap_pairs)), dim3(RTPB), 0, s, d->counts, d->cap_pairs,
+                   d->cslots, d->ccount, d->cstart, d->contacts, d->cap_contacts, d->counts);
+    LPE_HIP(ctx, hipMemcpyAsync(hc, d->counts, sizeof(int32_t) * 16, hipMemcpyDeviceToHost, s));
     return LPE_OK;
 }
 
@@ -3166,8 +3184,8 @@ static int detect_finish(lpe_ctx *ctx, RigidDev *d, hipStream_t s, const int32_t
         int st = rigid_alloc_contacts(ctx, d, ncv + 4096);
         if (st) return st;
     }
-    LPE_HIP(ctx, hipMemcpyAsync(d->counts + 1, &ncv, sizeof(int32_t), hipMemcpyHostToDevice, s));
-    LPE_KERNEL(ctx, "k_compact", k_compact, dim3(rblk(d->cap_pairs)), dim3(RTPB), 0, s, d->counts, d->cap_pairs, d->cslots, d->ccount, d->cstart, d->contacts, d->cap_contacts);
+    LPE_KERNEL(ctx, "k_compact", k_compact, dim3(rblk(d->cap_pairs)), dim3(RTPB), 0, s, d->counts, d->cap_pairs,
+               d->cslots, d->ccount, d->cstart, d->contacts, d->cap_contacts, d->counts);
     LPE_CHECK_LAUNCH(ctx, "detect");
     d->last_np = np;
     d->last_nc = ncv;
@@ -3178,7 +3196,7 @@ static int rigid_detect(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pai
                         hipStream_t s = nullptr) {
     if (!s) s = ctx->stream;
     for (int attempt = 0; attempt < 4; attempt++) {
-        int32_t hc[12];
+        int32_t hc[16];
         int st = detect_launch(ctx, d, np_in, pairs_in, s, hc);
         if (st) return st;
         LPE_HIP(ctx, hipStreamSynchronize(s));
@@ -3310,7 +3328,8 @@ static PosRows pos_rows(RigidDev *d) {
 
 static int colour_prep(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     const lpe_rigid_config &c = d->cfg;
-    const int nb = d->nb, nc = d->last_nc;
+    // (lagged detection: the count is on the device only, the grids cover the capacity)
+    const int nb = d->nb, nc = d->lag ? d->cap_contacts : d->last_nc;
     int32_t *inPos = d->inContact + nb;
     LPE_HIP(ctx, hipMemsetAsync(d->inContact, 0, sizeof(int32_t) * 2 * nb, s));
     LPE_KERNEL(ctx, "k_mark_contacts", k_mark_contacts, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->contacts, d->inContact);
@@ -3462,7 +3481,9 @@ static int rigid_step_impl(lpe_ctx *ctx, int np, const int32_t *pairs, int nc_or
     if (stats) std::memset(stats, 0, sizeof(*stats));
     if (d->nb <= 0) return LPE_OK;
     (void)hipSetDevice(ctx->device);
-    int st = rigid_detect(ctx, d, np, pairs);
+    int st = d->lag ? rigid_lag_drain(ctx, d) : LPE_OK;       // (a world tick's pending checks)
+    if (st) return st;
+    st = rigid_detect(ctx, d, np, pairs);
     if (st) return st;
     if (pgs_order && nc_order != d->last_nc) {
         ctx->err = "lpe_rigid_step_ordered: pgs_order length differs from the contact count";
@@ -3476,6 +3497,7 @@ extern "C" int lpe_rigid_reserve(lpe_ctx *ctx, int pairs, int contacts) {
     if (!ctx || pairs < 1 || contacts < 1) return LPE_ERR_ARG;
     (void)hipSetDevice(ctx->device);
     RigidDev *d = rdev(ctx);
+    rigid_lag_off(ctx, d);
     if (d->side) LPE_HIP(ctx, hipStreamSynchronize(d->side));
     LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
     d->cap_pairs = 0;                     // re-allocated at exactly the requested sizes
@@ -3504,6 +3526,57 @@ extern "C" int lpe_rigid_step(lpe_ctx *ctx, lpe_rigid_stats *stats) {
 // position clamp is applied (k_boundary_pos, at the start of the tick: the
 // fluid step and gravity write only velocities); the solvers, which need the
 // velocities, wait for the colouring on the context stream.
+// ---- lagged detection checks (RigidDev::lag) ---------------------------
+// The counts of one lagged detection (slot), once its copy has landed: an
+// overflow of that tick fails loudly; counts past half a capacity schedule a
+// growth for the next tick start.  wait = false: only if already complete.
+static int rigid_lag_check(lpe_ctx *ctx, RigidDev *d, int slot, bool wait) {
+    if (!d->hpend[slot]) return LPE_OK;
+    if (wait) {
+        LPE_HIP(ctx, hipEventSynchronize(d->evHc[slot]));
+    } else {
+        const hipError_t q = hipEventQuery(d->evHc[slot]);
+        if (q == hipErrorNotReady) return LPE_OK;
+        if (q != hipSuccess) { ctx->err = "hipEventQuery (lagged detection)"; return LPE_ERR_HIP; }
+    }
+    d->hpend[slot] = false;
+    const int32_t *hc = d->hcr + 16 * slot;
+    if (hc[7]) {
+        ctx->err = "rigid solver watchdog fired (a dataflow solve made no progress)";
+        return LPE_ERR_OVERFLOW;
+    }
+    if (hc[11]) {
+        ctx->err = "narrowphase: a pair produced more contacts than a pair slot holds (MAXC)";
+        return LPE_ERR_OVERFLOW;
+    }
+    if (hc[6] || hc[0] > d->cap_pairs || hc[14] > d->cap_contacts) {
+        d->lag = false;
+        ctx->err = "rigid pair / contact buffers overflowed in a tick checked after the fact (the counts grew "
+                   "more than 4x within two ticks); reserve more with lpe_rigid_reserve";
+        return LPE_ERR_OVERFLOW;
+    }
+    d->last_np = hc[0];
+    d->last_nc = hc[14];
+    if (2 * hc[0] > d->cap_pairs) d->grow_pairs = std::max(d->grow_pairs, 4 * hc[0] + 1024);
+    if (2 * hc[14] > d->cap_contacts) d->grow_contacts = std::max(d->grow_contacts, 4 * hc[14] + 4096);
+    return LPE_OK;
+}
+
+// every pending check, oldest first (last_np / last_nc end as the newest tick's)
+static int rigid_lag_drain(lpe_ctx *ctx, RigidDev *d) {
+    int st = rigid_lag_check(ctx, d, (int)(d->htick & 1u), true);
+    const int st2 = rigid_lag_check(ctx, d, (int)((d->htick + 1u) & 1u), true);
+    return st ? st : st2;
+}
+
+// leave lagged mode (upload, reserve, config): the next detection is synchronous
+static void rigid_lag_off(lpe_ctx *ctx, RigidDev *d) {
+    if (d->hcr) (void)rigid_lag_drain(ctx, d);
+    d->hpend[0] = d->hpend[1] = false;
+    d->lag = d->lag_next = false;
+    d->grow_pairs = d->grow_contacts = 0;
+}
+
 int rigid_tick_begin(lpe_ctx *ctx) {
     RigidDev *d = rdev(ctx);
     d->overlap_pending = false;
@@ -3516,6 +3589,32 @@ int rigid_tick_begin(lpe_ctx *ctx) {
         LPE_HIP(ctx, hipEventCreateWithFlags(&d->evDetect, hipEventDisableTiming));
         LPE_HIP(ctx, hipEventCreateWithFlags(&d->evColour, hipEventDisableTiming));
         LPE_HIP(ctx, hipHostMalloc((void **)&d->hc, sizeof(int32_t) * 16, 0));
+        LPE_HIP(ctx, hipHostMalloc((void **)&d->hcr, sizeof(int32_t) * 32, 0));
+        LPE_HIP(ctx, hipEventCreateWithFlags(&d->evHc[0], hipEventDisableTiming));
+        LPE_HIP(ctx, hipEventCreateWithFlags(&d->evHc[1], hipEventDisableTiming));
+    }
+    if (d->lag) {
+        // the previous tick's counts if they are in (a growth they ask for
+        // then happens before this tick's detection)
+        int st = rigid_lag_check(ctx, d, (int)((d->htick + 1u) & 1u), false);
+        if (st) return st;
+    }
+    if (d->grow_pairs > d->cap_pairs || d->grow_contacts > d->cap_contacts) {
+        // (asked for by a check: nothing in flight may use the old buffers)
+        int st = d->lag ? rigid_lag_drain(ctx, d) : LPE_OK;
+        if (st) return st;
+        LPE_HIP(ctx, hipStreamSynchronize(d->side));
+        if (d->psolve) LPE_HIP(ctx, hipStreamSynchronize(d->psolve));
+        LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (d->grow_pairs > d->cap_pairs && (st = rigid_alloc_pairs(ctx, d, d->grow_pairs))) return st;
+        if (d->grow_contacts > d->cap_contacts && (st = rigid_alloc_contacts(ctx, d, d->grow_contacts)))
+            return st;
+        d->regrows++;
+    }
+    d->grow_pairs = d->grow_contacts = 0;
+    if (d->lag_next) {                        // a synchronous tick left 4x headroom
+        d->lag = true;
+        d->lag_next = false;
     }
     hipStream_t s = ctx->stream;
     LPE_KERNEL(ctx, "k_boundary_pos", k_boundary_pos, dim3(rblk(d->nb)), dim3(RTPB), 0, s, d->nb, d->bodies,
@@ -3533,8 +3632,21 @@ int rigid_tick_begin(lpe_ctx *ctx) {
 static int rigid_tick_launch(lpe_ctx *ctx, RigidDev *d) {
     if (d->detect_launched) return LPE_OK;
     LPE_HIP(ctx, hipStreamWaitEvent(d->side, d->evStart, 0));
-    int st = detect_launch(ctx, d, 0, nullptr, d->side, d->hc);
-    if (st) return st;
+    if (d->lag) {
+        // lagged: the compaction follows at once and the counts go to a ring
+        // slot, checked when the slot comes round again (two ticks later)
+        const int slot = (int)(d->htick & 1u);
+        int st = rigid_lag_check(ctx, d, slot, true);
+        if (st) return st;
+        st = detect_launch(ctx, d, 0, nullptr, d->side, d->hcr + 16 * slot, true);
+        if (st) return st;
+        LPE_HIP(ctx, hipEventRecord(d->evHc[slot], d->side));
+        d->hpend[slot] = true;
+        d->htick++;
+    } else {
+        int st = detect_launch(ctx, d, 0, nullptr, d->side, d->hc);
+        if (st) return st;
+    }
     LPE_HIP(ctx, hipEventRecord(d->evDetect, d->side));
     d->detect_launched = true;
     return LPE_OK;
@@ -3584,13 +3696,36 @@ int rigid_tick_detect(lpe_ctx *ctx) {
     int st0 = rigid_tick_launch(ctx, d);
     if (st0) return st0;
     d->overlap_pending = false;
+    int st;
+    if (d->lag) {
+        // no host wait: the colouring and the preparation take the counts
+        // from the device (an empty tick colours nothing and solves nothing)
+        st = solver_streams(ctx, d);
+        if (!st) st = solver_lds_check(ctx, d);
+        if (!st) st = colour_launch(ctx, d, d->side);
+        if (!st) st = colour_prep(ctx, d, d->side);
+        if (st) return st;
+        LPE_HIP(ctx, hipEventRecord(d->evColour, d->side));
+        d->colour_pending = true;
+        return LPE_OK;
+    }
     LPE_HIP(ctx, hipEventSynchronize(d->evDetect));
     int retry = 0;
-    int st = detect_finish(ctx, d, d->side, d->hc, &retry);
+    st = detect_finish(ctx, d, d->side, d->hc, &retry);
     if (st) return st;
     if (retry) {                     // the pair buffer grew: detect again (rare)
         st = rigid_detect(ctx, d, 0, nullptr, d->side);
         if (st) return st;
+    }
+    // the next ticks check their counts after the fact once the buffers have
+    // 4x headroom (striped solver only); else grow them at the next tick start
+    if (striped()) {
+        if (4 * d->last_np <= d->cap_pairs && 4 * d->last_nc <= d->cap_contacts) {
+            d->lag_next = true;
+        } else {
+            d->grow_pairs = std::max(d->cap_pairs, 4 * d->last_np + 1024);
+            d->grow_contacts = std::max(d->cap_contacts, 4 * d->last_nc + 4096);
+        }
     }
     st = solver_streams(ctx, d);
     if (st) return st;
@@ -3614,7 +3749,7 @@ int rigid_tick_finish(lpe_ctx *ctx) {
     if (st) return st;
     d->colour_pending = false;
     hipStream_t s = ctx->stream;
-    if (d->last_nc == 0) {                    // early out (rigid_body_collision.cpp:35-37)
+    if (!d->lag && d->last_nc == 0) {         // early out (rigid_body_collision.cpp:35-37)
         LPE_HIP(ctx, hipStreamWaitEvent(s, d->evColour, 0));
         if (d->pcol && d->last_np > 0)
             LPE_HIP(ctx, hipMemsetAsync(d->pcol, 0xff, sizeof(int32_t) * d->last_np, s));
@@ -3696,7 +3831,7 @@ extern "C" int lpe_rigid_download(lpe_ctx *ctx, lpe_body *bodies) {
         ctx->err = "rigid solver watchdog fired (a dataflow solve made no progress)";
         return LPE_ERR_OVERFLOW;
     }
-    return LPE_OK;
+    return d->lag ? rigid_lag_drain(ctx, d) : LPE_OK;       // (the ticks checked after the fact)
 }
 
 extern "C" int lpe_rigid_download_contacts(lpe_ctx *ctx, int pair_cap, int32_t *pairs,
@@ -3705,6 +3840,11 @@ extern "C" int lpe_rigid_download_contacts(lpe_ctx *ctx, int pair_cap, int32_t *
     if (!ctx) return LPE_ERR_ARG;
     RigidDev *d = rdev(ctx);
     hipStream_t s = ctx->stream;
+    if (d->lag) {                             // the last tick's counts (lagged checks)
+        LPE_HIP(ctx, hipStreamSynchronize(s));
+        int st = rigid_lag_drain(ctx, d);
+        if (st) return st;
+    }
     if (np) *np = d->last_np;
     if (nc) *nc = d->last_nc;
     if (pairs && d->last_np > 0)
@@ -3719,6 +3859,11 @@ extern "C" int lpe_rigid_download_colours(lpe_ctx *ctx, int cap, int32_t *pair_c
     if (!ctx || cap < 0) return LPE_ERR_ARG;
     RigidDev *d = rdev(ctx);
     hipStream_t s = ctx->stream;
+    if (d->lag) {
+        LPE_HIP(ctx, hipStreamSynchronize(s));
+        int st = rigid_lag_drain(ctx, d);
+        if (st) return st;
+    }
     int32_t nc = 0;
     if (d->counts) LPE_HIP(ctx, hipMemcpyAsync(&nc, d->counts + 8, sizeof(int32_t), hipMemcpyDeviceToHost, s));
     if (pair_colour && d->pcol && d->last_np > 0 && cap > 0)

@@ -1477,22 +1477,38 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     } else if (cnt <= NLIST_CAP) {
         // the density pass's list: the r^2 < h^2 neighbours in canonical
         // order as slot offsets, so the heavy pair math runs only on real
-        // neighbours
-        constexpr int U = 8;                      // one group of eight entries
-        for (int j = 0; j < cnt; j += U) {
-            const uint4 g8 = nlist[(size_t)(j >> 3) * sp.nstride + s];
-            const uint32_t w[4] = {g8.x, g8.y, g8.z, g8.w};
-            int kk[U];
+        // neighbours.  Software-pipelined in quads: the records of the next
+        // quad (and the list word after the next) are in flight while a quad
+        // is computed, so a wave pays about one memory latency per quad
+        // instead of two (list word, then records) plus the math.
+        const size_t ns = (size_t)sp.nstride;
+        struct Quad { FRec r[4]; };
+        // records of list entries j .. j+3 held by words (wa, wb) of a list group
+        auto quad = [&](uint32_t wa, uint32_t wb, int j) {
+            const uint32_t w2[4] = {wa & 0xffffu, wa >> 16, wb & 0xffffu, wb >> 16};
+            Quad q;
 #pragma unroll
-            for (int u = 0; u < U; u++) kk[u] = (int)(int16_t)((w[u >> 1] >> (16 * (u & 1))) & 0xffffu);
+            for (int u = 0; u < 4; u++) {
+                const int k = s + (j + u < cnt ? (int)(int16_t)w2[u] : 0);   // (past the end: itself, unused)
+                q.r[u] = FRec{nbA[k], nbB[k]};
+            }
+            return q;
+        };
+        uint4 gA = make_uint4(0u, 0u, 0u, 0u), gB = gA;
+        if (cnt > 0) gA = nlist[s];                   // entries 0-7
+        if (cnt > 8) gB = nlist[ns + s];              // entries 8-15 (in flight)
+        Quad cur = quad(gA.x, gA.y, 0);
+        for (int j = 0; j < cnt; j += 8) {
+            const Quad nxt = quad(gA.z, gA.w, j + 4);   // entries j+4 .. j+7
 #pragma unroll
-            for (int u = 0; u < U; u++) kk[u] = s + (j + u < cnt ? kk[u] : 0);
-            FRec r[U];
+            for (int u = 0; u < 4; u++)
+                if (j + u < cnt) pair(cur.r[u].a, cur.r[u].b);
+            cur = quad(gB.x, gB.y, j + 8);            // entries j+8 .. j+11
 #pragma unroll
-            for (int u = 0; u < U; u++) r[u] = FRec{nbA[kk[u]], nbB[kk[u]]};
-#pragma unroll
-            for (int u = 0; u < U; u++)
-                if (j + u < cnt) pair(r[u].a, r[u].b);
+            for (int u = 0; u < 4; u++)
+                if (j + 4 + u < cnt) pair(nxt.r[u].a, nxt.r[u].b);
+            gA = gB;
+            if (j + 16 < cnt) gB = nlist[(size_t)((j >> 3) + 2) * ns + s];   // entries j+16 .. j+23
         }
     } else {
         walk_neighbours<4>(xi, yi, sp.eps, cs, walk_reach(hi, cs), g, sp.W, sp.H, sp.ox, sp.oy, start,

@@ -59,7 +59,7 @@ struct RigidDev {
     int32_t *sItemA = nullptr, *sItemB = nullptr;    // dependency bodies per item (-1 none)
     int4 *sVer = nullptr;                            // rank/cnt on A, rank/cnt on B
     int32_t *sBCount = nullptr, *sBStart = nullptr, *sBCursor = nullptr, *sEnt = nullptr;
-    int32_t *counts = nullptr;                // [0]=np [1]=nc [4]=npos [5]=heavy [6]=pair overflow
+    int32_t *counts = nullptr;                // [0]=np [1]=nc [4]=npos [5]=heavy [6]=pair overflow [14]=contacts found
     bool detect_launched = false;             // this tick's detection is on the side stream
     bool heavy_valid = false;                 // counts[5] holds the planetary-mass check of the bodies
     unsigned gen = 0;                         // bumped by every upload / config change (world Barnes-Hut cache)
@@ -89,6 +89,20 @@ struct RigidDev {
     hipEvent_t evStart = nullptr, evDetect = nullptr, evColour = nullptr;
     bool overlap_pending = false;             // detection queued on the side stream
     bool colour_pending = false;              // ... finished by the host, colouring queued
+    // world tick, lagged detection check (rigid_tick_launch): once a
+    // synchronous detection left 4x headroom in the pair and contact buffers,
+    // the detections run without a host wait -- the stages take their sizes
+    // from the device counts and capacity-sized grids, and the host checks
+    // each tick's counts (copied to hcr[slot]) when it reuses the slot two
+    // ticks later, or at a download.  Counts past half the capacity grow the
+    // buffers at the next tick start; an overflow (more than 4x growth within
+    // two ticks) fails loudly (LPE_ERR_OVERFLOW).  counts[14] = contacts found.
+    bool lag = false, lag_next = false;
+    int32_t *hcr = nullptr;                   // pinned [2][16]
+    hipEvent_t evHc[2] = {nullptr, nullptr};
+    bool hpend[2] = {false, false};
+    unsigned htick = 0;                       // detections issued in lagged mode
+    int grow_pairs = 0, grow_contacts = 0;    // capacities wanted at the next tick start
     // striped solver buffers (lpe_rigid.hip StripeBufs, allocated on first use)
     void *stripes = nullptr;
     int cap_stripe_nb = 0, cap_stripe_pairs = 0;
