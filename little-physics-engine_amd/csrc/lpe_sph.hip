@@ -711,6 +711,19 @@ __device__ __forceinline__ int xcd_block(int nb) {
     return lb < nb ? lb : -1;
 }
 
+// Chunked XCD order: runs of C consecutive blocks go to one XCD, the runs
+// round robin over the XCDs (launch xcd_chunk_grid(nb, C) blocks).  A run's
+// blocks share their halo rows in one L2, while a spatial cluster of heavy
+// blocks longer than a run still spreads over several XCDs.
+__host__ __device__ __forceinline__ int xcd_chunk_grid(int nb, int C) {
+    return ((nb + NXCD * C - 1) / (NXCD * C)) * NXCD * C;
+}
+__device__ __forceinline__ int xcd_chunk_block(int nb, int C) {
+    const int x = (int)(blockIdx.x % NXCD), k = (int)(blockIdx.x / NXCD);
+    const int lb = (k / C) * (NXCD * C) + x * C + (k % C);
+    return lb < nb ? lb : -1;
+}
+
 __device__ __forceinline__ float walk_reach(float h, float cs) {
     return (2.0f * h / cs) * 1.002f + 2e-3f;
 }
@@ -1369,6 +1382,7 @@ struct SphStepParams {
     float viscosity, minDist, minDens;
     int diag;                 // count diagnostics into status (lpe_sph_diag)
     const int32_t *refInv;    // reference cell-capacity mode: id -> slot (else null)
+    int nblk, chunk;          // forces pass: logical blocks, blocks per XCD run (0: plain order)
 };
 
 // computeForces + velocityVerletFinish + impulse + push-out; reads the sorted
@@ -1402,7 +1416,8 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     // plain block order (blocks go round robin over the XCDs): the costly
     // blocks, the particles in and around the rigid pile, are one spatial
     // run that an XCD-contiguous mapping (xcd_block) would put on one XCD
-    const int lb = (int)blockIdx.x;
+    const int lb = sp.chunk > 0 ? xcd_chunk_block(sp.nblk, sp.chunk) : (int)blockIdx.x;
+    if (lb < 0) return;                       // (padding of the chunked grid)
     const int nn = sp.nptr ? *sp.nptr : sp.n;
     const int s0 = lb * HB, s1 = min(s0 + HB, nn);
     if (s0 >= s1) {
@@ -1444,26 +1459,128 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         float r2 = dx * dx + dy * dy;
         if (r2 < sp.minDist) return;
         if (r2 >= h_ij2) return;
+#ifdef LPE_DIAG_FASTDIV      // profiling variants only: approximate division / sqrt (not bit-exact)
+        float r = __builtin_amdgcn_sqrtf(r2);
+#else
         float r = sqrtf(r2);
+#endif
         float rhoj = ob.z;
         if (rhoj < sp.minDens || !rhoi_ok) return;
         float mj = oa.z;
         float term = pti + ob.w;
         float diff = (h_ij - r);
         float wSpiky = spF * (diff * diff);
+#ifdef LPE_DIAG_FASTDIV
+        const float ir = __builtin_amdgcn_rcpf(r);
+        float rx = dx * ir, ry = dy * ir;
+#else
         float rx = dx / r, ry = dy / r;
+#endif
         float fxPress = -mj * term * wSpiky;
         float fx = fxPress * rx;
         float fy = fxPress * ry;
         float vx_ij = vxi - ob.x, vy_ij = vyi - ob.y;
         float wVisc = lapC * diff;
+#ifdef LPE_DIAG_FASTDIV
+        float fVisc = sp.viscosity * mj * (wVisc * __builtin_amdgcn_rcpf(rhoj));
+#else
         float fVisc = sp.viscosity * mj * (wVisc / rhoj);
+#endif
         fx -= fVisc * vx_ij;
         fy -= fVisc * vy_ij;
         sumFx += fx;
         sumFy += fy;
     };
+#ifdef LPE_DIAG_NONBR        // profiling variants only: no fluid pair forces
+    const int cnt = 0;
+#else
     const int cnt = live ? ncount[s] : 0;
+#endif
+    // the neighbour list's first two words, in flight during phase 0
+    const size_t ns = (size_t)sp.nstride;
+    uint4 gA = make_uint4(0u, 0u, 0u, 0u), gB = gA;
+    if (cnt > 0 && cnt <= NLIST_CAP) gA = nlist[s];   // entries 0-7
+    if (cnt > 8 && cnt <= NLIST_CAP) gB = nlist[ns + s];   // entries 8-15
+    // ---- coupling, phase 0: the rigid candidates (positions only) --------
+    // (impulse solver only if R > 0, fluid.cpp:910; push-out always).  The
+    // (particle, rigid) pairs whose AABB test passes are few and clustered
+    // (particles in and around the rigid pile), so they are spread over the
+    // block: each wave appends its particles' pairs to the block's list (one
+    // LDS atomic per wave; a particle's pairs stay consecutive, in candidate
+    // = ascending rigid order); the waves that finish their fluid forces
+    // first compute the pairs' geometry (couple_geom) while the others are
+    // still summing theirs; after a barrier the impulse halves (couple_imp,
+    // which need the finished velocities) go round robin, and each particle
+    // folds its own pairs in order.  A block with more than PAIR_CAP pairs
+    // couples per thread instead (couple_both, the same arithmetic).
+    __shared__ int pRig[PAIR_CAP];
+    __shared__ unsigned char pOwn[PAIR_CAP], pFlag[PAIR_CAP];
+    __shared__ PairGeo pGeo[PAIR_CAP];
+    __shared__ CoupleIn lIn[HB];
+    __shared__ int pCount, pNext, pWaves;
+    if (threadIdx.x == 0) { pCount = 0; pNext = 0; pWaves = 0; }
+    __syncthreads();
+    const int lane = (int)threadIdx.x & 63;
+    int nh = 0, off = 0;
+    {
+        int k0 = 0, k1 = 0;
+#ifdef LPE_DIAG_NOCOUPLE     // profiling variants only: no rigid coupling
+        if (false) {
+#else
+        if (cp.nr > 0 && live) {
+#endif
+            float fbx = fminf(fmaxf(floorf(xi / cp.bcs) - (float)cp.bx0, 0.f), (float)(cp.bW - 1));
+            float fby = fminf(fmaxf(floorf(yi / cp.bcs) - (float)cp.by0, 0.f), (float)(cp.bH - 1));
+            int bin = (int)fby * cp.bW + (int)fbx;
+            k0 = rbinStart[bin]; k1 = rbinStart[bin + 1];
+            if (sp.diag && k1 > k0) atomicAdd(&status[ST_RIGID_CAND], k1 - k0);
+#ifdef LPE_FTRACE
+            if (g_ftrace_on) atomicMax(&g_ftrace[lb * 8 + 7], (unsigned long long)(k1 - k0));
+#endif
+        }
+        // AABB hits among the bin's candidates (bin-ordered AABBs, 8 loads in
+        // flight); the first 64 candidates' hits kept as a mask
+        unsigned long long hitm = 0ull;
+        for (int k = k0; k < k1; k += 8) {
+            float4 bb[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) bb[u] = rbinAabb[min(k + u, k1 - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+                if (k + u < k1 && aabb_holds(bb[u], xi, yi)) {
+                    nh++;
+                    if (k + u - k0 < 64) hitm |= 1ull << (k + u - k0);
+                }
+        }
+        // the wave's run of the block list
+        int incl = nh;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int v = __shfl_up(incl, d);
+            if (lane >= d) incl += v;
+        }
+        const int wtot = __shfl(incl, 63);
+        int wbase = 0;
+        if (lane == 0 && wtot > 0) wbase = atomicAdd(&pCount, wtot);
+        off = __shfl(wbase, 0) + incl - nh;
+        if (nh > 0 && off + nh <= PAIR_CAP) {
+            int q = off;
+            for (unsigned long long m = hitm; m; m &= m - 1ull, q++) {
+                pRig[q] = rbinList[k0 + __ffsll((long long)m) - 1];
+                pOwn[q] = (unsigned char)threadIdx.x;
+            }
+            for (int k = k0 + 64; k < k1; k++)             // (a bin of more than 64 candidates)
+                if (aabb_holds(rbinAabb[k], xi, yi)) { pRig[q] = rbinList[k]; pOwn[q] = (unsigned char)threadIdx.x; q++; }
+        }
+        // the particle's coupling inputs but the velocity (set after the
+        // fluid forces); pow only for a particle with candidates
+        CoupleState st0;
+        st0.x = xi; st0.y = yi; st0.vx = st0.vy = 0.f; st0.mass = meA.z; st0.rho = rhoi; st0.p = pi;
+        st0.vhx = st0.vhy = st0.ax = st0.ay = 0.f;
+        lIn[threadIdx.x] = couple_in(st0, cp, cp.nr > 0 && nh > 0);
+        __threadfence_block();                                 // (the LDS writes before the count)
+        if (lane == 0) atomicAdd(&pWaves, 1);
+    }
     if (sp.diag && live) {
         atomicAdd(&status[ST_NEIGH], cnt);
         if (cnt > NLIST_CAP) atomicAdd(&status[ST_NL_OVERFLOW], 1);
@@ -1481,7 +1598,6 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         // quad (and the list word after the next) are in flight while a quad
         // is computed, so a wave pays about one memory latency per quad
         // instead of two (list word, then records) plus the math.
-        const size_t ns = (size_t)sp.nstride;
         struct Quad { FRec r[4]; };
         // records of list entries j .. j+3 held by words (wa, wb) of a list group
         auto quad = [&](uint32_t wa, uint32_t wb, int j) {
@@ -1494,9 +1610,6 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
             }
             return q;
         };
-        uint4 gA = make_uint4(0u, 0u, 0u, 0u), gB = gA;
-        if (cnt > 0) gA = nlist[s];                   // entries 0-7
-        if (cnt > 8) gB = nlist[ns + s];              // entries 8-15 (in flight)
         Quad cur = quad(gA.x, gA.y, 0);
         for (int j = 0; j < cnt; j += 8) {
             const Quad nxt = quad(gA.z, gA.w, j + 4);   // entries j+4 .. j+7
@@ -1529,75 +1642,65 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     st.vx = st.vhx + sp.hdt * st.ax;
     st.vy = st.vhy + sp.hdt * st.ay;
     st.mass = meA.z; st.rho = rhoi; st.p = pi;
-    int k0 = 0, k1 = 0;
-    if (cp.nr > 0 && live) {
-        float fbx = fminf(fmaxf(floorf(st.x / cp.bcs) - (float)cp.bx0, 0.f), (float)(cp.bW - 1));
-        float fby = fminf(fmaxf(floorf(st.y / cp.bcs) - (float)cp.by0, 0.f), (float)(cp.bH - 1));
-        int bin = (int)fby * cp.bW + (int)fbx;
-        k0 = rbinStart[bin]; k1 = rbinStart[bin + 1];
-        if (sp.diag && k1 > k0) atomicAdd(&status[ST_RIGID_CAND], k1 - k0);
-#ifdef LPE_FTRACE
-        if (g_ftrace_on) atomicMax(&g_ftrace[lb * 8 + 7], (unsigned long long)(k1 - k0));
-#endif
-    }
-    // Coupling (impulse solver only if R > 0, fluid.cpp:910; push-out
-    // always).  The (particle, rigid) pairs whose AABB test passes are few
-    // and clustered (particles in and around the rigid pile), so they are
-    // spread over the whole block: each particle's pairs get consecutive
-    // slots (block scan of the hit counts), every thread computes pairs round
-    // robin into LDS, then each particle folds its own pairs in candidate
-    // (ascending rigid) order.  A block with more than PAIR_CAP pairs couples
-    // per thread instead (same arithmetic).
-    // AABB hits among the bin's candidates (bin-ordered AABBs, 8 loads in
-    // flight); the first 64 candidates' hits kept as a mask
-    int nh = 0;
-    unsigned long long hitm = 0ull;
-    for (int k = k0; k < k1; k += 8) {
-        float4 bb[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) bb[u] = rbinAabb[min(k + u, k1 - 1)];
-#pragma unroll
-        for (int u = 0; u < 8; u++)
-            if (k + u < k1 && aabb_holds(bb[u], st.x, st.y)) {
-                nh++;
-                if (k + u - k0 < 64) hitm |= 1ull << (k + u - k0);
-            }
-    }
-    const CoupleIn cin = couple_in(st, cp, cp.nr > 0 && nh > 0);
+    lIn[threadIdx.x].vx = st.vx;
+    lIn[threadIdx.x].vy = st.vy;
     const float4 *rc = raabb + cp.nr;                 // the compact records (k_rig_couple)
-    int total;
-    const int off = block_excl_scan(nh, &total);       // (HB == TPB)
+    // ---- coupling, phase 2: the pairs' geometry, by whichever waves are here
+    if (cp.nr > 0) {
+        if (lane == 0)                                // every wave of the block has appended its pairs
+            while (__hip_atomic_load(&pWaves, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < HB / 64)
+                __builtin_amdgcn_s_sleep(1);
+        const int tot = __shfl(lane == 0 ? __hip_atomic_load(&pCount, __ATOMIC_RELAXED,
+                                                             __HIP_MEMORY_SCOPE_WORKGROUP) : 0, 0);
+        if (tot <= PAIR_CAP) {
+            for (;;) {
+                int q0 = 0;
+                if (lane == 0) q0 = atomicAdd(&pNext, 64);
+                q0 = __shfl(q0, 0);
+                if (q0 >= tot) break;
+                const int q = q0 + lane;
+                if (q < tot) {
+                    const int o = pOwn[q];
+                    PairGeo ge;
+                    pFlag[q] = (unsigned char)couple_geom(lIn[o].x, lIn[o].y, cp, true, rc, pRig[q], ge);
+                    pGeo[q] = ge;
+                }
+            }
+        }
+    }
+    __syncthreads();                                  // (fluid forces, geometry and lIn complete)
     FTR(1);
+    const int total = pCount;
 #ifdef LPE_FTRACE
     if (g_ftrace_on && threadIdx.x == 0) g_ftrace[lb * 8 + 4] = total;
 #endif
     if (total > PAIR_CAP) {
-        if (live) couple_both(st, cp, sp.dt, cp.nr > 0, rc, rbinAabb, rbinList, k0, k1, acq, status);
+        if (live) {
+            const float fbx = fminf(fmaxf(floorf(st.x / cp.bcs) - (float)cp.bx0, 0.f), (float)(cp.bW - 1));
+            const float fby = fminf(fmaxf(floorf(st.y / cp.bcs) - (float)cp.by0, 0.f), (float)(cp.bH - 1));
+            const int bin = (int)fby * cp.bW + (int)fbx;
+            couple_both(st, cp, sp.dt, cp.nr > 0, rc, rbinAabb, rbinList, rbinStart[bin], rbinStart[bin + 1], acq,
+                        status);
+        }
     } else {
-        __shared__ int pRig[PAIR_CAP];
-        __shared__ unsigned char pOwn[PAIR_CAP], pFlag[PAIR_CAP];
-        __shared__ PairTerm pTerm[PAIR_CAP];
-        __shared__ CoupleIn lIn[HB];
-        lIn[threadIdx.x] = cin;
-        int q = off;
-        for (unsigned long long m = hitm; m; m &= m - 1ull, q++) {
-            pRig[q] = rbinList[k0 + __ffsll((long long)m) - 1];
-            pOwn[q] = (unsigned char)threadIdx.x;
-        }
-        for (int k = k0 + 64; k < k1; k++)                 // (a bin of more than 64 candidates)
-            if (aabb_holds(rbinAabb[k], cin.x, cin.y)) { pRig[q] = rbinList[k]; pOwn[q] = (unsigned char)threadIdx.x; q++; }
-        __syncthreads();
-        for (int q = threadIdx.x; q < total; q += HB) {
-            const int r = pRig[q];
-            PairTerm t;
-            pFlag[q] = (unsigned char)couple_pair(lIn[pOwn[q]], cp, sp.dt, cp.nr > 0, rc, r, acq, status, t);
-            pTerm[q] = t;
-        }
-        __syncthreads();
+        // ---- phase 3: the impulse halves (finished velocities), round robin
+        for (int q = threadIdx.x; q < total; q += HB)
+            if (pFlag[q] & PT_WANT) {
+                float fx, fy;
+                couple_imp(lIn[pOwn[q]], cp, sp.dt, rc, pRig[q], pGeo[q].pen, pGeo[q].nx, pGeo[q].ny, acq,
+                           status, fx, fy);
+                pGeo[q].nx = fx;                      // (the fold's fluid-force term)
+                pGeo[q].ny = fy;
+                pFlag[q] = (unsigned char)(pFlag[q] | PT_IMP);
+            }
+        if (total > 0) __syncthreads();
         FTR(2);
         if (live) {
             CoupleAcc a;
-            for (int q = off; q < off + nh; q++) a.fold(pTerm[q], pFlag[q]);
+            for (int q = off; q < off + nh; q++) {
+                const PairGeo ge = pGeo[q];
+                a.fold(PairTerm{ge.ax, ge.ay, ge.nx, ge.ny}, pFlag[q]);
+            }
             couple_finish(st, cp, a);
         }
     }
@@ -2901,6 +3004,14 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
     static const bool nofuse = getenv("LPE_NO_KICK_FUSION") != nullptr;
     const bool fuse = !nofuse;
     const int fblocks = nblk1(sp.n, HB);
+    // forces blocks in XCD runs of LPE_FORCES_CHUNK blocks (0: plain order)
+    static const int fchunk = [] {
+        const char *e = getenv("LPE_FORCES_CHUNK");
+        return e ? std::max(0, atoi(e)) : 0;
+    }();
+    sp.nblk = fblocks;
+    sp.chunk = fchunk;
+    const int fgrid = fchunk > 0 ? xcd_chunk_grid(fblocks, fchunk) : fblocks;
     int kicked = 0;
     for (int step = 0; step < c.numSubSteps; step++) {
         if (sh) {
@@ -2926,7 +3037,7 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
             kn.fk = sph_fastkick(ctx, sph_rowscan_ok(d));
         }
         kicked = kn.on ? fblocks : 0;
-        LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(fblocks), dim3(HB), 0, s, sp, cp,
+        LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(fgrid), dim3(HB), 0, s, sp, cp,
                            (step == 0 && pre) ? d.gp + 1 : d.gp,
                            d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart, d.rbinList,
                            rbin_aabb(d),

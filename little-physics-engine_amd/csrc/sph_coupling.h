@@ -394,6 +394,91 @@ __device__ __forceinline__ int couple_pair(const CoupleIn &in, const CoupleParam
     return flags | PT_COLL;
 }
 
+// couple_pair in two halves, so the forces pass can compute the geometry
+// (containment, closest point, penetration, normal, the position solver's
+// term) while the particle's fluid forces are still being summed, and the
+// impulse solver's term (which needs the finished velocity) afterwards.  The
+// same operations in the same order as couple_pair: bit-identical terms.
+// PT_WANT: the impulse solver runs for the pair (pen, nx, ny hold its input).
+static constexpr int PT_WANT = 4;
+struct PairGeo { float ax, ay, pen, nx, ny; };
+
+__device__ __forceinline__ int couple_geom(float px, float py, const CoupleParams &cp, bool impulse,
+                                           const float4 *__restrict__ rc, int r, PairGeo &g) {
+    RigC rb;
+    const float4 *vt = rigc_load(rc, r, rb);
+    const bool doImp = impulse && !rb.fast;
+    int flags = 0;
+    g.pen = g.nx = g.ny = 0.f;
+    if (rb.shape == 0) {
+        const float rx = px - rb.px, ry = py - rb.py;
+        const float dist2 = rx * rx + ry * ry;
+        const float radius = rb.radius;
+        if (!(dist2 < radius * radius)) return 0;
+        const float dist0 = sqrtf(dist2);
+        if (doImp) {
+            float dist = dist0;
+            if (dist < cp.minPenetration) dist = cp.minPenetration;
+            float pen = radius - dist;
+            if (pen < 0.0f) pen = 0.0f;
+            if (!(pen < cp.minPenetration)) {
+                g.pen = pen; g.nx = rx / dist; g.ny = ry / dist;
+                flags |= PT_WANT;
+            }
+        }
+        float dist = dist0, dx = rx, dy = ry;
+        if (dist < cp.minSafeDistance) { dist = cp.minSafeDistance; dx = 1.0f; dy = 0.0f; }
+        const float pen = (radius - dist) + cp.safetyMargin;
+        const float dirx = dx / dist, diry = dy / dist;
+        g.ax = -(dirx * pen * cp.relaxFactor);                 // acx -= ...
+        g.ay = -(diry * pen * cp.relaxFactor);
+    } else if (rb.shape == 1) {
+        if (rb.nv < 3 || !pip_rec(px, py, rb.nv, vt)) return 0;
+        float cx, cy;
+        closest_rec(px, py, rb.nv, vt, cx, cy);
+        const float dx = px - cx, dy = py - cy;
+        const float d0 = sqrtf(dx * dx + dy * dy);
+        if (doImp) {
+            float d = d0;
+            if (d < cp.minPenetration) d = cp.minPenetration;
+            float pen = d;
+            if (pen < 0.0f) pen = 0.0f;
+            if (!(pen < cp.minPenetration)) {
+                g.pen = pen; g.nx = dx / d; g.ny = dy / d;
+                flags |= PT_WANT;
+            }
+        }
+        float d = d0, cdx = dx, cdy = dy;
+        if (d < cp.minSafeDistance) { d = cp.minSafeDistance; cdx = 1.0f; cdy = 0.0f; }
+        const float pen = d + cp.safetyMargin;
+        const float dirx = cdx / d, diry = cdy / d;
+        g.ax = dirx * pen * cp.relaxFactor;                    // acx += ...
+        g.ay = diry * pen * cp.relaxFactor;
+    } else {
+        return 0;
+    }
+    return flags | PT_COLL;
+}
+
+// the impulse solver's half of a pair whose geometry asked for it (PT_WANT):
+// the rigid accumulators take the force, the particle the returned term
+__device__ __forceinline__ void couple_imp(const CoupleIn &in, const CoupleParams &cp, float dt,
+                                           const float4 *__restrict__ rc, int r, float pen, float nx, float ny,
+                                           unsigned long long *__restrict__ acq, int32_t *__restrict__ status,
+                                           float &fx, float &fy) {
+    RigC rb;
+    (void)rigc_load(rc, r, rb);
+    CoupleState st;                    // the fields impulse_term reads
+    st.x = in.x; st.y = in.y; st.vx = in.vx; st.vy = in.vy; st.mass = in.mass;
+    st.vhx = st.vhy = st.ax = st.ay = st.rho = st.p = 0.f;
+    float tfx, tfy;
+    // lever arm: px - rb.px (circle: rx; polygon: px - rb.px, metal:856-857)
+    impulse_term(st, cp, dt, rb, in.effArea, r, pen, in.x - rb.px, in.y - rb.py, nx, ny, in.densityF,
+                 in.pressureF, acq, status, tfx, tfy);
+    fx = -(tfx * cp.fluidForceScale);                          // tffx -= tfx * fluidForceScale
+    fy = -(tfy * cp.fluidForceScale);
+}
+
 // the per-particle accumulators of the two solvers
 struct CoupleAcc {
     float tffx = 0.f, tffy = 0.f, acx = 0.f, acy = 0.f;
