@@ -1,0 +1,13 @@
+# round 3 (i): two lanes per particle in the forces pass: parity, A/B sweep, phase trace
+mkdir -p gpurun_out
+ok() { local rc=$1; if [ $rc -eq 124 ] || [ $rc -eq 134 ] || [ $rc -eq 137 ] || [ $rc -eq 139 ]; then echo "stop: rc=$rc"; exit $rc; fi; return 0; }
+timeout -k 10 400 python -u -m pytest tests/test_sph_gpu.py tests/test_world_gpu.py tests/test_configs_gpu.py tests/test_slab_gpu.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r03i_pytest.log 2>&1; rc=$?; echo "pytest rc=$rc"; ok $rc
+timeout -k 10 120 python -u profiles/snapshot.py --save 3000 > gpurun_out/r03i_snap.log 2>&1 || exit 1
+for rep in 1 2; do
+for cfg in "1 0" "2 0" "2 1"; do
+  set -- $cfg
+  echo "lpp=$1 rev=$2" >> gpurun_out/r03i_rates.txt
+  LPE_FORCES_LPP=$1 LPE_FORCES_REV=$2 TOPK=8 timeout -k 10 60 python -u profiles/snapshot.py --load 600 >> gpurun_out/r03i_rates.txt 2>&1 || exit 1
+done
+done
+LPE_LIB=profiles/_var/liblpe_ft.so timeout -k 10 60 python -u profiles/forces_phase_trace.py > gpurun_out/r03i_ftrace.txt 2>&1
