@@ -85,6 +85,7 @@ struct SphDev {
     lpe_fluid_config cfg{};
     bool cfg_set = false;
     bool rig_dirty = true;
+    bool rig_coupled = false;     // the coupling records were written by the world gather (skip k_rig_couple)
     // world tick: sub-step 0's kick/hash/density of the next tick, launched on
     // a side stream while the rigid solvers run (sph_prelaunch).  It writes
     // only scratch (kicked state, bins, sorted records, gp[1], status[1]),
@@ -220,6 +221,7 @@ int rigid_tick_hook(lpe_ctx *ctx, int step);   // fluid-step hook (after each su
 int rigid_tick_finish(lpe_ctx *ctx);
 // lpe_sph_step with a host callback after the forces of sub-step `after`
 int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int));
+float4 *sph_rig_records(lpe_ctx *ctx, int nr);   // the coupling records buffer (nr rigids)
 // first (optional): launched on the side stream ahead of the prelaunch (the
 // tick's own fluid boundary / gravity pass); fbgDone is recorded after it
 int sph_prelaunch(lpe_ctx *ctx, double dt_tick, const std::function<int(hipStream_t)> &first = {});

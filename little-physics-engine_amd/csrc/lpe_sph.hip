@@ -1995,17 +1995,7 @@ __global__ void k_rig_couple(int nr, const lpe_gpu_rigid *__restrict__ rig, floa
                              float4 *__restrict__ aabb) {
     int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nr) return;
-    const lpe_gpu_rigid &b = rig[r];
-    aabb[r] = make_float4(b.minX, b.maxX, b.minY, b.maxY);
-    float4 *q = aabb + nr + (size_t)r * RIGC_F4;
-    const bool fast = (b.vx * b.vx + b.vy * b.vy + b.omega * b.omega) > maxSafeVelocitySq;
-    const int nv = min(max(b.vertCount, 0), LPE_MAX_POLY_VERTS);
-    const int fl = (b.shapeType & 0xff) | ((b.shapeType == 1 ? nv : 0) << 8) | ((fast ? 1 : 0) << 16);
-    q[0] = make_float4(b.posX, b.posY, b.radius, __int_as_float(b.shapeType == 0 || b.shapeType == 1 ? fl : 0xff));
-    q[1] = make_float4(b.vx, b.vy, b.omega, b.mass);
-    q[2] = make_float4(b.inertia, 0.f, 0.f, 0.f);
-    for (int k = 0; k < LPE_MAX_POLY_VERTS / 2; k++)
-        q[3 + k] = make_float4(b.vertsX[2 * k], b.vertsY[2 * k], b.vertsX[2 * k + 1], b.vertsY[2 * k + 1]);
+    rig_couple_one(rig[r], r, nr, maxSafeVelocitySq, aabb);
 }
 
 // one wave per rigid, lanes stride over the bins its AABB covers (a wall
@@ -2603,6 +2593,23 @@ static int sph_scan(lpe_ctx *ctx, int C, int32_t *cnt, int32_t *start, int32_t *
     return LPE_OK;
 }
 
+// the compact coupling records of nr rigids (k_rig_couple's output; the world
+// tick's gather writes them itself, rig_coupled)
+float4 *sph_rig_records(lpe_ctx *ctx, int nr) {
+    SphDev &d = ctx->sph;
+    if (nr > d.cap_raabb || !d.raabb) {
+        if (d.raabb) (void)hipFree(d.raabb);
+        d.raabb = nullptr;
+        d.cap_raabb = 0;
+        if (hipMalloc((void **)&d.raabb, sizeof(float4) * (size_t)std::max(nr, 1) * (1 + RIGC_F4)) != hipSuccess) {
+            ctx->err = "hipMalloc (rigid coupling records)";
+            return nullptr;
+        }
+        d.cap_raabb = std::max(nr, 1);
+    }
+    return d.raabb;
+}
+
 static int sph_build_rigid_bins(lpe_ctx *ctx) {
     SphDev &d = ctx->sph;
     if (d.nr <= 0 || !d.rig_dirty) return LPE_OK;
@@ -2623,13 +2630,11 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
         d.rbin_zero = 0;
     }
     hipStream_t s = ctx->stream;
-    if (d.nr > d.cap_raabb || !d.raabb) {
-        if (d.raabb) (void)hipFree(d.raabb);
-        LPE_HIP(ctx, hipMalloc((void **)&d.raabb, sizeof(float4) * (size_t)d.nr * (1 + RIGC_F4)));
-        d.cap_raabb = d.nr;
-    }
-    LPE_KERNEL(ctx, "k_rig_couple", k_rig_couple, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig,
-               d.cfg.impulseSolver.maxSafeVelocitySq, d.raabb);
+    if (!sph_rig_records(ctx, d.nr)) return LPE_ERR_HIP;
+    if (!d.rig_coupled)
+        LPE_KERNEL(ctx, "k_rig_couple", k_rig_couple, dim3(nblk(d.nr, 128)), dim3(128), 0, s, d.nr, d.rig,
+                   d.cfg.impulseSolver.maxSafeVelocitySq, d.raabb);
+    d.rig_coupled = false;
     if (B > d.rbin_zero)   // else the previous build's k_rbin_sort left counts [0, B) zeroed
         LPE_HIP(ctx, hipMemsetAsync(d.rbinCount, 0, sizeof(int32_t) * B, s));
     d.rbin_zero = 0;
@@ -2953,14 +2958,17 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
     }
     const bool pre = d.pre;
     d.pre = false;
-    int st = sph_build_rigid_bins(ctx);
-    if (st) return st;
     if (pre) {
         std::swap(d.rho, d.rhoN);                     // sub-step 0's density is the prelaunch's
         std::swap(d.pr, d.prN);
         LPE_HIP(ctx, hipStreamWaitEvent(s, d.preDone, 0));
+    }
+    int st = sph_build_rigid_bins(ctx);
+    if (st) return st;
+    if (pre) {
         // (resets the step stats as sph_reset_step_stats, then merges)
-        LPE_KERNEL(ctx, "k_merge_prestats", k_merge_prestats, dim3(1), dim3(64), 0, s, d.status, d.status + ST_COUNT, 1);
+        LPE_KERNEL(ctx, "k_merge_prestats", k_merge_prestats, dim3(1), dim3(64), 0, s, d.status,
+                   d.status + ST_COUNT, 1);
     } else {
         st = sph_reset_step_stats(ctx, s, d.status);
         if (st) return st;

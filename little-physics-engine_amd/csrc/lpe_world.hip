@@ -19,9 +19,10 @@
 namespace lpe {
 
 // gatherRigidBodies (fluid.cpp:304-438) for one coupling rigid
+// (recs: also the fluid coupling's compact AABBs and records, k_rig_couple's work)
 __global__ void k_gather_rigids(int nr, const int32_t *__restrict__ coupleBody,
                                 const lpe_body *__restrict__ bodies, const double *__restrict__ verts,
-                                lpe_gpu_rigid *__restrict__ rig) {
+                                lpe_gpu_rigid *__restrict__ rig, float maxSafeVelocitySq, float4 *__restrict__ recs) {
     int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nr) return;
     const lpe_body b = bodies[coupleBody[r]];
@@ -66,6 +67,7 @@ __global__ void k_gather_rigids(int nr, const int32_t *__restrict__ coupleBody,
         rb.minX = mnx; rb.maxX = mxx; rb.minY = mny; rb.maxY = mxy;
     }
     rig[r] = rb;
+    if (recs) rig_couple_one(rb, r, nr, maxSafeVelocitySq, recs);
 }
 
 // writeBackRigidBodies' ECS part (fluid.cpp:564-579: v and omega of every
@@ -198,9 +200,13 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
         // 1) FluidSystem::update (fluid.cpp:958-1021)
         int nr = fluid ? d.couple_n : 0;
         if (nr > 0) {
-            LPE_KERNEL(ctx, "k_gather_rigids", k_gather_rigids, dim3(wblk(nr, 128)), dim3(128), 0, s, nr, d.coupleBody, rd->bodies, rd->verts, d.rig);
+            float4 *recs = sph_rig_records(ctx, nr);
+            if (!recs) return LPE_ERR_HIP;
+            LPE_KERNEL(ctx, "k_gather_rigids", k_gather_rigids, dim3(wblk(nr, 128)), dim3(128), 0, s, nr,
+                       d.coupleBody, rd->bodies, rd->verts, d.rig, d.cfg.impulseSolver.maxSafeVelocitySq, recs);
             d.nr = nr;
             d.rig_dirty = true;
+            d.rig_coupled = true;
         }
         if (overlap) {          // after the gather: the fluid sees the unclamped poses
             int st = rigid_tick_begin(ctx);

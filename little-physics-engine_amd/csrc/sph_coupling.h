@@ -81,6 +81,22 @@ __device__ __forceinline__ float2 rigc_vert(const float4 *__restrict__ vt, int i
     return (i & 1) ? make_float2(p.z, p.w) : make_float2(p.x, p.y);
 }
 
+// the compact AABB (minX, maxX, minY, maxY) of coupling rigid r and its
+// compact coupling record (sph_coupling.h RigC), nr AABBs first
+__device__ __forceinline__ void rig_couple_one(const lpe_gpu_rigid &b, int r, int nr, float maxSafeVelocitySq,
+                                               float4 *__restrict__ aabb) {
+    aabb[r] = make_float4(b.minX, b.maxX, b.minY, b.maxY);
+    float4 *q = aabb + nr + (size_t)r * RIGC_F4;
+    const bool fast = (b.vx * b.vx + b.vy * b.vy + b.omega * b.omega) > maxSafeVelocitySq;
+    const int nv = min(max(b.vertCount, 0), LPE_MAX_POLY_VERTS);
+    const int fl = (b.shapeType & 0xff) | ((b.shapeType == 1 ? nv : 0) << 8) | ((fast ? 1 : 0) << 16);
+    q[0] = make_float4(b.posX, b.posY, b.radius, __int_as_float(b.shapeType == 0 || b.shapeType == 1 ? fl : 0xff));
+    q[1] = make_float4(b.vx, b.vy, b.omega, b.mass);
+    q[2] = make_float4(b.inertia, 0.f, 0.f, 0.f);
+    for (int k = 0; k < LPE_MAX_POLY_VERTS / 2; k++)
+        q[3 + k] = make_float4(b.vertsX[2 * k], b.vertsY[2 * k], b.vertsX[2 * k + 1], b.vertsY[2 * k + 1]);
+}
+
 // pointInPolygon / closestPointOnPolygon (above) on the compact record's
 // vertices (n <= LPE_MAX_POLY_VERTS), each edge's vertices loaded once.  The
 // parity test's toggles commute; the closest-point scan keeps the original
