@@ -70,20 +70,38 @@ def kernel_bytes(name, n, cells):
     return model.get(name)
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC
-    measurement (profiles/r*/pmc_traffic.json, written by
-    profiles/pmc_traffic.py from separate rocprofv3 FETCH_SIZE / WRITE_SIZE
-    passes of this bench on the same scene), or (None, None)."""
+def lib_sha256():
+    """sha256 of the library this run loads (the PMC summaries record the one they profiled)."""
+    import hashlib
+    lpe = _load("lpe", os.path.join(PKG, "lpe.py"))
+    try:
+        return hashlib.sha256(open(lpe.LIB_PATH, "rb").read()).hexdigest()
+    except OSError:
+        return None
+
+
+def _pmc_lookup(fname, kernel, field):
+    """(value, source, same_build) from the newest committed profiles/r*/fname
+    holding `kernel`; same_build: its recorded library hash equals this run's."""
     import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")), reverse=True):
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", fname)), reverse=True):
         try:
             d = json.load(open(path))
         except (OSError, ValueError):
             continue
         if kernel in d:
-            return d[kernel]["hbm_bytes"], os.path.relpath(path, ROOT)
-    return None, None
+            built = d.get("_build", {}).get("lib_sha256")
+            return d[kernel][field], os.path.relpath(path, ROOT), (built is not None and built == lib_sha256())
+    return None, None, False
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC
+    measurement (profiles/r*/pmc_traffic.json, written by
+    profiles/pmc_traffic.py from separate rocprofv3 FETCH_SIZE / WRITE_SIZE
+    passes of the settled metric scene), its file, and whether it profiled
+    the library this run loads."""
+    return _pmc_lookup("pmc_traffic.json", kernel, "hbm_bytes")
 
 
 # VALU issue peak: 256 CUs x 4 SIMDs x 2.4 GHz, one wave64 instruction per 2
@@ -94,16 +112,8 @@ VALU_PEAK_GINST = 256 * 4 * 2.4 / 2.0
 
 def pmc_valu(kernel):
     """VALU wave-instructions per launch of `kernel` from the newest committed
-    PMC pass (profiles/r*/pmc_valu.json: SQ_INSTS_VALU), or (None, None)."""
-    import glob
-    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_valu.json")), reverse=True):
-        try:
-            d = json.load(open(path))
-        except (OSError, ValueError):
-            continue
-        if kernel in d:
-            return d[kernel]["valu_wave_insts"], os.path.relpath(path, ROOT)
-    return None, None
+    PMC pass (profiles/r*/pmc_valu.json: SQ_INSTS_VALU), its file, same build."""
+    return _pmc_lookup("pmc_valu.json", kernel, "valu_wave_insts")
 
 
 def cpu_model():
@@ -596,19 +606,22 @@ def main():
     roof = None
     if b is not None:
         ach = b / avg_s / 1e9
-        traffic, tsrc = pmc_traffic(dname) if world == 1 and args.scene == "M" else (None, None)
+        traffic, tsrc, tsame = pmc_traffic(dname) if world == 1 and args.scene == "M" else (None, None, False)
         roof = dict(kernel=dname, bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS,
                     unit="GB/s", frac=round(ach / HBM_PEAK_GBS, 4), traffic=traffic,
                     avg_us=round(avg_s * 1e6, 2), algorithmic_bytes=b)
         if tsrc:
-            roof["traffic_source"] = tsrc + " (HBM bytes per launch, rocprofv3 PMC, last 5 ticks)"
-        vi, vsrc = pmc_valu(dname) if world == 1 and args.scene == "M" else (None, None)
+            roof["traffic_source"] = tsrc + " (HBM bytes per launch, rocprofv3 PMC FETCH_SIZE x2 + WRITE_SIZE, " \
+                                            "settled metric scene)"
+            roof["traffic_same_build"] = tsame
+            roof["traffic_frac_of_algorithmic"] = round(traffic / b, 3)
+        vi, vsrc, vsame = pmc_valu(dname) if world == 1 and args.scene == "M" else (None, None, False)
         if vi:
             # the compute side of the same launch: VALU instructions (PMC) over
             # the live duration, against the chip's VALU issue rate
             roof["valu"] = dict(wave_insts=vi, achieved_ginst_s=round(vi / avg_s / 1e9, 1),
                                 peak_ginst_s=VALU_PEAK_GINST, frac=round(vi / avg_s / 1e9 / VALU_PEAK_GINST, 4),
-                                source=vsrc)
+                                source=vsrc, same_build=vsame)
     # the whole tick against HBM: the staged
     # compulsory model B_tick = substeps x (152 B x N + 24 B x C) at the
     # measured tick rate

@@ -1945,7 +1945,10 @@ static constexpr int STRIPES_MAX = 64;
 static constexpr int SGROUPS = 2 * STRIPES_MAX;          // (S groups are used: S/2 bands, S/2 - 1 seams)
 static constexpr int SCOLS = 64;                 // colours per group (a greedy colouring needs degree + 1)
 static constexpr int STEPS_MAX = SGROUPS * SCOLS;
-static constexpr int STPB = 256;                 // threads of a stripe workgroup
+#ifndef LPE_STPB
+#define LPE_STPB 256
+#endif
+static constexpr int STPB = LPE_STPB;             // threads of a stripe workgroup
 
 struct StripeBufs {
     int32_t *bstripe;      // [nb] stripe of a movable body in a contact pair, else -1
@@ -2435,6 +2438,11 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
     STR(0, j, 0);
     const StripeView v = stripe_view(sb, counts, j);
     const int NR = v.nrows(), NP = v.npairs(), NL = v.nloc(), NS = v.nsteps();
+#ifdef LPE_PTRACE
+    if (threadIdx.x == 0 && j < 32) {   // (trace slots 61-63: phase A / B steps, pairs)
+        g_strace[0][j][61] = v.a1 - v.a0; g_strace[0][j][62] = v.b1 - v.b0; g_strace[0][j][63] = NP;
+    }
+#endif
     // layout: rn, rr [NR] float4 | pr [NP] int4 | pm [NP] float4 | ln, lf [NR] | lv [3 NL] | stepL [NS + 1]
     const int oRR = 16 * NR, oPR = oRR + 16 * NR, oPM = oPR + 16 * NP, oLN = oPM + 16 * NP, oLF = oLN + 4 * NR,
               oLV = oLF + 4 * NR, oST = oLV + 12 * NL, total = oST + 4 * (NS + 1);

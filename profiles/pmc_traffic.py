@@ -13,6 +13,7 @@ written; bench.py reports it as the roofline `traffic`.
 import csv
 import json
 import re
+import hashlib
 import sys
 from collections import defaultdict
 
@@ -45,6 +46,9 @@ def main():
                   "dispatches": min(f[k][1], w[k][1]),
                   "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes; "
                             "FETCH_SIZE x2 (gfx950 wide-read correction); KiB -> bytes"}
+    if "--lib" in sys.argv:     # the library the passes profiled (bench.py compares it with its own)
+        lib = sys.argv[sys.argv.index("--lib") + 1]
+        res["_build"] = {"lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(), "lib": lib}
     json.dump(res, open(dst, "w"), indent=1)
     print(json.dumps(res, indent=1))
 

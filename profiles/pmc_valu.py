@@ -12,6 +12,7 @@ compute side.
 import csv
 import json
 import re
+import hashlib
 import sys
 from collections import defaultdict
 
@@ -42,6 +43,9 @@ def main():
         out[k]["dispatches"] = n
         out[k]["method"] = ("rocprofv3 --pmc " + " ".join(FIELDS) + " (one pass), last dispatches of "
                             "bench.py's timed window")
+    if "--lib" in sys.argv:     # the library the passes profiled (bench.py compares it with its own)
+        lib = sys.argv[sys.argv.index("--lib") + 1]
+        out["_build"] = {"lib_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest(), "lib": lib}
     json.dump(out, open(dst, "w"), indent=1)
     print(json.dumps(out, indent=1))
 

@@ -36,3 +36,13 @@ for w, name in ((0, "pgs"), (1, "pos")):
               f"{np.round(a.mean(1)[:8], 2).tolist()}")
     print("  WG0 timeline it0-2:", np.round(ph[0, :3].ravel(), 2).tolist())
     print("  WG1 timeline it0-2:", np.round(ph[1, :3].ravel(), 2).tolist())
+st = buf[0]
+na, nbs, npr = st[:, 61], st[:, 62], st[:, 63]
+used = npr > 0
+print("pgs steps per WG: A", na[used].tolist(), "B", nbs[used].tolist(), "pairs", npr[used].tolist())
+t = buf[0]; t0 = t[:, 0].min(); rel = (t - t0) / 100.0
+ph = rel[:, 2:2 + 6 * it].reshape(32, it, 6)
+A = (ph[:, :, 1] - ph[:, :, 0]).mean(1); B = (ph[:, :, 4] - ph[:, :, 3]).mean(1)
+print("pgs us per step: A", np.round(A[used] / np.maximum(na[used], 1), 2).tolist())
+print("pgs us per step: B", np.round(B[used] / np.maximum(nbs[used], 1), 2).tolist())
+
