@@ -108,6 +108,13 @@ struct SphDev {
     int cap_rows = 0;
     long fastIdx = 0;             // row scans launched (parity)
     bool fast_armed = false;      // the pending kick recorded the row totals
+    // in-bin order without a scatter pass (lpe_sph.hip k_bucket_permute): the
+    // kick files each particle id under its bin (BKT_CAP per bin, the rest in
+    // an overflow list by parity)
+    int32_t *bucket = nullptr;    // [cap_bucket][BKT_CAP] ids by bin, arrival order
+    long cap_bucket = 0;          // bins the bucket covers (0: off, the scatter path)
+    int32_t *bovf = nullptr;      // [2][OVF_WORDS]: count, then (bin, id) pairs
+    bool fast_bucket = false;     // the pending kick filed the ids
 };
 
 // status slots
@@ -127,6 +134,7 @@ enum StatusSlot {
     ST_REF_UB = 12,         // reference cell-capacity mode read past the last cell (undefined in the reference)
     ST_OVER_CAP_TOTAL = 13, // ST_OVER_CAP summed since the last lpe_sph_diag call (bench windows)
     ST_MAX_OCC_TOTAL = 14,  // ST_MAX_OCC maximum since the last lpe_sph_diag call
+    ST_BUCKET_OVERFLOW = 15,// the in-bin sort's overflow list overflowed (a tick's sort is wrong: fails loudly)
     ST_RX_GHOST_L = 16,     // slab decomposition: most ghosts the left / right neighbour packed for this
     ST_RX_GHOST_R = 17,     //   rank in a sub-step of the current tick (sizes the next tick's exchange)
     ST_RX_MIG_L = 18,       // most migrants received from the left / right neighbour so far

@@ -160,7 +160,29 @@ __device__ __forceinline__ void bbox_partial(float mnx, float mxx, float mny, fl
 struct FastKick {
     int on;
     int32_t *rowtot;          // [H] particles per device row
+    int32_t *bucket;          // [bins][BKT_CAP] particle ids by bin (k_bucket_permute), or null
+    int32_t *ovf;             // the parity's overflow list: count, -, -, -, then (bin, id, arrival, -)
+    int ovfcap;               // its entries (the particle capacity: it cannot overflow)
 };
+
+// The in-bin order without a scatter pass: the kick's atomic on its bin's
+// count returns the particle's arrival index there, and the id is filed
+// under the bin at that index (the first BKT_CAP of a bin).  Later arrivals
+// go to an overflow list (bin, id, arrival) that k_scan_rows places at
+// tmpId[start[bin] + arrival] once it has the bin's start; k_bucket_permute
+// then ranks a particle among its bin's ids directly.  The list is
+// double-buffered by the scan's parity (k_scan_rows clears the other one).
+static constexpr int BKT_CAP = 32;
+__device__ __forceinline__ void bucket_file(const FastKick &fk, uint32_t k, int a, int id,
+                                            int32_t *__restrict__ status) {
+    if (a < BKT_CAP) {
+        fk.bucket[(size_t)k * BKT_CAP + a] = id;
+    } else {
+        const int e = atomicAdd(&fk.ovf[0], 1);
+        if (e < fk.ovfcap) ((int4 *)(fk.ovf + 4))[e] = make_int4((int)k, id, a, 0);
+        else atomicOr(&status[ST_BUCKET_OVERFLOW], 1);
+    }
+}
 
 // The next sub-step's kick, fused into the forces pass of the current one
 // (sub-steps 1..numSubSteps-1 of a single-domain tick): the finished state
@@ -208,8 +230,15 @@ k_kick_drift(int n, float dt, float hdt, int first, int probe, float eps, float 
             mny = fminf(mny, py); mxy = fmaxf(mxy, py);
         }
         int len; bool st;
-        (void)wave_runs(k, active, &len, &st);
-        if (st) atomicAdd(&count[k], len);
+        const int first = wave_runs(k, active, &len, &st);
+        if (fk.on && fk.bucket) {
+            int base = 0;
+            if (st) base = atomicAdd(&count[k], len);
+            base = __shfl(base, first);
+            if (active) bucket_file(fk, k, base + lane_id() - first, P.id[i], status);
+        } else if (st) {
+            atomicAdd(&count[k], len);
+        }
         if (fk.on) {                       // row totals: base row from the chunk's first particle
             __shared__ int ltab[8], lbase;
             const int row = active ? (int)((k >> 2) / (uint32_t)W) : -1;
@@ -496,6 +525,43 @@ k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restric
     if (clearCnt) clearCnt[k] = 0;  // (k_scan_rows leaves the counts for the next kick to find zeroed)
 }
 
+// k_scatter + k_rank_permute in one pass (single domain, the kick filed the
+// ids by bin): thread o takes P slot o, ranks its id among its bin's ids
+// (the bin's first BKT_CAP arrivals in the bucket, the rest in the overflow
+// list) and writes the same records as k_rank_permute to slot start[bin] +
+// rank.  Reads of P are coalesced; the writes land near o (a sub-step moves
+// few particles to another bin).
+__global__ void __launch_bounds__(TPB)
+k_bucket_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restrict__ start,
+                 const int32_t *__restrict__ bucket, const int32_t *__restrict__ tmpId, PState P, KState K, PState S,
+                 float4 *__restrict__ nbA, float2 *__restrict__ nbB, int32_t *__restrict__ refInv, int W,
+                 int32_t *__restrict__ clearCnt, int32_t *__restrict__ status) {
+    const int o = blockIdx.x * TPB + threadIdx.x;
+    if (o >= n) return;
+    const uint32_t k = key[o];
+    const int myid = P.id[o];
+    const int b = start[k], nk = start[k + 1] - b;
+    const int4 *bk = (const int4 *)(bucket + (size_t)k * BKT_CAP);
+    int rank = 0;
+    for (int j = 0; j < min(nk, BKT_CAP); j += 4) {
+        const int4 q = bk[j >> 2];
+        rank += (q.x < myid) + (j + 1 < nk && q.y < myid) + (j + 2 < nk && q.z < myid) + (j + 3 < nk && q.w < myid);
+    }
+    for (int j = b + BKT_CAP; j < b + nk; j++) rank += tmpId[j] < myid ? 1 : 0;   // (a full bin's later arrivals)
+    if (rank >= nk) {              // (never: the bin's filed ids are its particles) fail loudly, write nothing
+        atomicOr(&status[ST_BUCKET_OVERFLOW], 2);
+        return;
+    }
+    const int d = b + rank;
+    const uint32_t cl = k >> 2, cyr = cl / (uint32_t)W, cxr = cl - cyr * (uint32_t)W;
+    nbA[d] = make_float4(K.x[o], K.y[o], P.m[o], __int_as_float((int)((cyr << 17) | (cxr << 2) | (k & 3))));
+    nbB[2 * d] = make_float2(P.vx[o], P.vy[o]);
+    S.id[d] = myid;
+    if (refInv) refInv[myid] = d;
+    S.vhx[d] = K.vhx[o]; S.vhy[d] = K.vhy[o];
+    clearCnt[k] = 0;
+}
+
 // ---------------------------------------------------------------------------
 // k_scan_rows (single domain, FastKick): one launch replaces k_scan_reduce +
 // k_scan_final.  One block per device-grid row.  Every block finishes the
@@ -515,9 +581,11 @@ __global__ void __launch_bounds__(TPB)
 k_scan_rows(int W, int H, int ox, int oy, float eps, const int32_t *__restrict__ cnt, int32_t *__restrict__ start,
             int32_t *__restrict__ cursor, const int32_t *__restrict__ rowtot, int32_t *__restrict__ rowtotNext,
             GridParams *__restrict__ gp, int32_t *__restrict__ status,
-            const float4 *__restrict__ bboxPart, int nparts, float gcs) {
+            const float4 *__restrict__ bboxPart, int nparts, float gcs, const int32_t *__restrict__ ovf,
+            int ovfcap, int32_t *__restrict__ ovfNext, int32_t *__restrict__ tmpId) {
     const int r = (int)blockIdx.x;
     if (threadIdx.x == 0) rowtotNext[r] = 0;
+    if (ovfNext && r == 0 && threadIdx.x == 0) ovfNext[0] = 0;
     // everything the block needs is loaded up front (one round trip): the
     // row's first SR_CELLS cells, the row totals below it, the bbox partials
     int4 v[SR_CELLS / TPB];
@@ -598,6 +666,16 @@ k_scan_rows(int W, int H, int ox, int oy, float eps, const int32_t *__restrict__
     }
     if (r == ry1 && threadIdx.x == 0) start[(size_t)(r + 1) * W * 4] = pre;   // end of the last active bin
     __syncthreads();
+    if (ovf) {
+        // the bucket's overflow entries of this row's bins to tmpId[start + arrival]
+        // (k_bucket_permute reads a full bin's later arrivals there)
+        const int L = min(ovf[0], ovfcap);
+        const int4 *e = (const int4 *)(ovf + 4);
+        for (int t = (int)threadIdx.x; t < L; t += TPB) {
+            const int4 v = e[t];
+            if ((int)(((uint32_t)v.x >> 2) / (uint32_t)W) == r) tmpId[start[v.x] + v.z] = v.y;
+        }
+    }
     if (threadIdx.x == 0) {
         if (s_max) { atomicMax(&status[ST_MAX_OCC], s_max); atomicMax(&status[ST_MAX_OCC_TOTAL], s_max); }
         if (s_out) atomicAdd(&status[ST_NOT_INSERTED], s_out);
@@ -1743,8 +1821,15 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
             mny = mxy = py;
         }
         int len; bool stt;
-        (void)wave_runs(k, live, &len, &stt);
-        if (stt) atomicAdd(&kn.count[k], len);
+        const int first = wave_runs(k, live, &len, &stt);
+        if (kn.fk.on && kn.fk.bucket) {
+            int base = 0;
+            if (stt) base = atomicAdd(&kn.count[k], len);
+            base = __shfl(base, first);
+            if (live) bucket_file(kn.fk, k, base + lane_id() - first, S.id[s], status);
+        } else if (stt) {
+            atomicAdd(&kn.count[k], len);
+        }
         if (kn.fk.on) {
             __syncthreads();                               // (ltab zeroed)
             (void)wave_runs(live ? (uint32_t)ky : 0xFFFFFFFFu, live, &len, &stt);
@@ -2121,6 +2206,7 @@ __global__ void k_merge_prestats(int32_t *__restrict__ st, int32_t *__restrict__
     if (threadIdx.x != 0) return;
     if (reset) { st[ST_MAX_OCC] = 0; st[ST_OVER_CAP] = 0; st[ST_REF_UB] = 0; }   // sph_reset_step_stats
     st[ST_CAP_OVERFLOW] |= pre[ST_CAP_OVERFLOW];
+    st[ST_BUCKET_OVERFLOW] |= pre[ST_BUCKET_OVERFLOW];
     st[ST_MAX_OCC] = max(st[ST_MAX_OCC], pre[ST_MAX_OCC]);
     st[ST_NOT_INSERTED] = pre[ST_NOT_INSERTED];
     st[ST_STAGE_FALLBACK] += pre[ST_STAGE_FALLBACK];
@@ -2145,6 +2231,8 @@ static inline float4 *rbin_aabb(const SphDev &d) {
     return d.rbinList ? (float4 *)((char *)d.rbinList + rbin_list_pad(d.cap_rlist)) : nullptr;
 }
 static inline int nblk1(long n, int t = TPB) { return std::max(1, nblk(n, t)); }   // never an empty grid
+// ints per parity of the grid hash's overflow list (header + one int4 per particle slot)
+static inline size_t ovf_words(const SphDev &d) { return 4 + 4 * (size_t)std::max(d.cap_n, 1); }
 
 // the id -> slot map of the reference cell-capacity mode, or null (mode off)
 static inline int32_t *sph_ref_inv(const SphDev &d) {
@@ -2209,7 +2297,7 @@ static void sph_free(SphDev &d) {
     pstate_free(d.P);
     pstate_free(d.S);
     void *ptrs[] = {d.rho, d.pr, d.rhoN, d.prN, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.refInv, d.stage, d.count, d.start, d.cursor,
-                    d.rowtot,
+                    d.rowtot, d.bucket, d.bovf,
                     d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.raabb, d.accum, d.acq, d.rbinStart, d.rgrid, d.rmax,
                     d.rbinList, d.rbinCount, d.coupleBody, d.plans};
     for (void *p : ptrs) if (p) (void)hipFree(p);
@@ -2340,9 +2428,21 @@ static int sph_set_grid(lpe_ctx *ctx, int gx0, int gy0, int gx1, int gy1) {
         LPE_HIP(ctx, hipMalloc((void **)&d.rowtot, sizeof(int32_t) * 2 * (size_t)d.H));
         d.cap_rows = d.H;
     }
+    // the in-bin id bucket (k_bucket_permute) for grids up to 2^25 bins (4 GiB;
+    // LPE_NO_BUCKET=1: off, the scatter + rank pass)
+    static const bool noBucket = getenv("LPE_NO_BUCKET") != nullptr;
+    if (!noBucket && C <= (1L << 25) && C > d.cap_bucket) {
+        if (d.bucket) (void)hipFree(d.bucket);
+        d.bucket = nullptr;
+        d.cap_bucket = 0;
+        LPE_HIP(ctx, hipMalloc((void **)&d.bucket, sizeof(int32_t) * BKT_CAP * (size_t)C));
+        d.cap_bucket = C;
+    }
+    if (d.bovf) LPE_HIP(ctx, hipMemsetAsync(d.bovf, 0, sizeof(int32_t) * 2 * ovf_words(d), ctx->stream));
     LPE_HIP(ctx, hipMemsetAsync(d.count, 0, sizeof(int32_t) * C, ctx->stream));
     LPE_HIP(ctx, hipMemsetAsync(d.rowtot, 0, sizeof(int32_t) * 2 * (size_t)d.cap_rows, ctx->stream));
     d.fast_armed = false;
+    d.fast_bucket = false;
     d.rig_dirty = true;    // the coupling bins span the device grid
     return LPE_OK;
 }
@@ -2436,6 +2536,11 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpOld, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.refInv, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.stage, sizeof(float) * N));
+    // the grid hash's overflow lists (one entry per particle at most; both counts start at 0)
+    if (d.bovf) (void)hipFree(d.bovf);
+    d.bovf = nullptr;
+    LPE_HIP(ctx, hipMalloc((void **)&d.bovf, sizeof(int32_t) * 2 * (4 + 4 * N)));
+    LPE_HIP(ctx, hipMemsetAsync(d.bovf, 0, sizeof(int32_t) * 2 * (4 + 4 * N), ctx->stream));
 
     // bbox partials: the kick's blocks, or the forces pass's when it kicks the next sub-step
     LPE_HIP(ctx, hipMalloc((void **)&d.bboxPart, sizeof(float4) * std::max<size_t>(MAX_KICK_BLOCKS, (N + HB - 1) / HB)));
@@ -2677,12 +2782,23 @@ static FastKick sph_fastkick(lpe_ctx *ctx, bool on) {
     SphDev &d = ctx->sph;
     FastKick fk{};
     fk.on = on ? 1 : 0;
+    const bool bucket = on && d.bucket && d.bovf && d.cap_bucket >= 4L * d.W * d.H;
     if (on) {
         fk.rowtot = d.rowtot + (size_t)(d.fastIdx & 1) * d.cap_rows;
+        if (bucket) {
+            fk.bucket = d.bucket;
+            fk.ovf = d.bovf + (size_t)(d.fastIdx & 1) * ovf_words(d);
+            fk.ovfcap = d.cap_n;
+        }
         // a kick whose scan never ran (an error in between) left its totals
-        if (d.fast_armed) (void)hipMemsetAsync(fk.rowtot, 0, sizeof(int32_t) * (size_t)d.cap_rows, ctx->stream);
+        if (d.fast_armed) {
+            (void)hipMemsetAsync(fk.rowtot, 0, sizeof(int32_t) * (size_t)d.cap_rows, ctx->stream);
+            if (d.bovf)
+                (void)hipMemsetAsync(d.bovf + (size_t)(d.fastIdx & 1) * ovf_words(d), 0, sizeof(int32_t), ctx->stream);
+        }
     }
     d.fast_armed = on;
+    d.fast_bucket = bucket;
     return fk;
 }
 
@@ -2703,13 +2819,15 @@ static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool pr
         LPE_CHECK_LAUNCH(ctx, "k_kick_drift");
     }
     int32_t *clear = nullptr;
+    const int par = (int)(d.fastIdx & 1);
+    const bool bucket = d.fast_armed && d.fast_bucket && !probe;
     if (d.fast_armed && !probe) {
         // one launch for the scan (the counts are cleared by the permute)
-        const int par = (int)(d.fastIdx & 1);
         LPE_KERNEL(ctx, "k_scan_rows", k_scan_rows, dim3(d.H), dim3(TPB), 0, s, d.W, d.H, d.ox, d.oy,
                    d.cfg.gridConfig.gridEpsilon, d.count, d.start, d.cursor, d.rowtot + (size_t)par * d.cap_rows,
                    d.rowtot + (size_t)(1 - par) * d.cap_rows, d.gp_cur, d.stat_cur, (const float4 *)d.bboxPart, kb,
-                   d.cs);
+                   d.cs, bucket ? d.bovf + (size_t)par * ovf_words(d) : (const int32_t *)nullptr, d.cap_n,
+                   d.bovf ? d.bovf + (size_t)(1 - par) * ovf_words(d) : (int32_t *)nullptr, d.tmpId);
         LPE_CHECK_LAUNCH(ctx, "k_scan_rows");
         d.fastIdx++;
         clear = d.count;
@@ -2718,6 +2836,14 @@ static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool pr
         if (st) return st;
     }
     d.fast_armed = false;
+    d.fast_bucket = false;
+    if (bucket) {
+        LPE_KERNEL(ctx, "k_bucket_permute", k_bucket_permute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key,
+                   d.start, d.bucket, d.tmpId, d.P, sph_kstate(d), d.S, d.nbA,
+                   (float2 *)d.nbB, sph_ref_inv(d), d.W, clear, d.stat_cur);
+        LPE_CHECK_LAUNCH(ctx, "hash");
+        return LPE_OK;
+    }
     LPE_KERNEL(ctx, "k_scatter", k_scatter, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.P.id, d.cursor,
                        d.tmpId, d.tmpOld, (const int32_t *)nullptr);
     LPE_KERNEL(ctx, "k_rank_permute", k_rank_permute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.start,
@@ -3111,6 +3237,10 @@ static int check_status(lpe_ctx *ctx) {
     }
     if (status[ST_LIST_OVERFLOW]) {
         ctx->err = "the rigid coupling bin list overflowed its capacity bound";
+        return LPE_ERR_OVERFLOW;
+    }
+    if (status[ST_BUCKET_OVERFLOW]) {
+        ctx->err = "the grid hash's in-bin sort lost a particle (bucket overflow list or rank check)";
         return LPE_ERR_OVERFLOW;
     }
     if (status[ST_HALO_DRIFT]) {

@@ -241,6 +241,27 @@ def test_ref_cell_cap_tick_bit_exact(gpu_ctx, oracle_mod, extra):
     np.testing.assert_array_equal(acc, racc)
 
 
+@pytest.mark.parametrize("extra", [90, 300])
+def test_tick_over_full_bins_bit_exact(gpu_ctx, oracle_mod, extra):
+    """Default mode, one coupled tick with 90 / 300 extra particles in one
+    cell: the grid hash files at most 32 ids per (cell, quadrant) bin and the
+    rest in its overflow list (k_bucket_permute); the in-bin order, and so
+    every sum, stays the oracle's (ascending id)."""
+    fl = compressed_scene(extra=extra)
+    rig = _crowd_rigids()
+    _upload(gpu_ctx, fl, rig)
+    gpu_ctx.sph_step(DT)
+    out = gpu_ctx.sph_download()
+    r_out, acc = gpu_ctx.sph_download_rigids()
+    st = gpu_ctx.sph_stats()
+    ref, rref, racc, ost = oracle_mod.fluid_tick(scenes.particles_aos(fl), rig, DT)
+    assert st["maxCellOccupancy"] == ost.maxOcc > 64     # (its quadrants hold 34 / 82 particles)
+    for k, col in (("x", 0), ("y", 1), ("vx", 2), ("vy", 3), ("vxHalf", 4), ("vyHalf", 5),
+                   ("ax", 6), ("ay", 7), ("density", 11), ("pressure", 12)):
+        np.testing.assert_array_equal(out[k], ref[:, col], err_msg=k)
+    np.testing.assert_array_equal(acc, racc)
+
+
 def test_ref_cell_cap_equals_default_below_64(gpu_ctx, oracle_mod):
     s = scenes.scene("small64_8")
     rig = scenes.gather_rigids(s["bodies"])
