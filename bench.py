@@ -469,6 +469,20 @@ def config_lines(lpe, scenes, device, dt_tick, with_ref):
                     t0 = time.perf_counter()
                 line["reference_this_host"] = dict(ticks_per_s=round(nt / el, 2), ticks=nt, cores=1,
                                                    kind="reference", cpu_model=cpu_model())
+            # the restatement's rigid tick on the same state (oracle/rigid_oracle.cpp, 1 thread): the
+            # calibration of cpu_baseline's "port" against the reference
+            bb, nt, t0 = warm, 0, time.perf_counter()
+            while True:
+                bb, _ = oracle.rigid_tick(cfg, bb, v, dt_tick)
+                nt += 1
+                el = time.perf_counter() - t0
+                if el > 1.0 or nt >= 512:
+                    break
+            line["restatement_this_host"] = dict(ticks_per_s=round(nt / el, 2), ticks=nt, cores=1, kind="port",
+                                                 cpu_model=cpu_model())
+            if "reference_this_host" in line:
+                line["restatement_over_reference"] = round(line["restatement_this_host"]["ticks_per_s"]
+                                                           / line["reference_this_host"]["ticks_per_s"], 3)
         out[name] = line
     return out
 
