@@ -399,7 +399,7 @@ k_scan_final(int C, int W, int ox, int oy, int32_t *__restrict__ cnt,
             // (stored as minX, minY, -maxX, -maxY for one MIN all-reduce)
             const float4 b = *bbG;
             mnx = b.x; mny = b.y; mxx = -b.z; mxy = -b.w;
-        } else {
+        } else if (fused == 1) {                  // (fused == 2: a plain prefix, no grid)
             for (int p = threadIdx.x; p < nparts; p += TPB) {
                 const float4 b = bboxPart[p];
                 mnx = fminf(mnx, b.x); mxx = fmaxf(mxx, b.y);
@@ -432,7 +432,7 @@ k_scan_final(int C, int W, int ox, int oy, int32_t *__restrict__ cnt,
         g = grid_from_bbox(b.x, b.y, b.z, b.w, gcs);
         prefix = pre;
         if (blockIdx.x == 0 && threadIdx.x == 0) {
-            *gp = g;
+            if (fused == 1) *gp = g;
             start[C] = all;
         }
     } else {
@@ -1461,6 +1461,7 @@ struct SphStepParams {
     int diag;                 // count diagnostics into status (lpe_sph_diag)
     const int32_t *refInv;    // reference cell-capacity mode: id -> slot (else null)
     int nblk, chunk;          // forces pass: logical blocks, blocks per XCD run (0: plain order)
+    int32_t *mergePre;        // sub-step 0 after a prelaunch: its stats to merge into status (else null)
 };
 
 // computeForces + velocityVerletFinish + impulse + push-out; reads the sorted
@@ -1473,6 +1474,21 @@ struct SphStepParams {
 #endif
 struct FRec { float4 a, b; };        // nbA (x, y, m, -), nbB (vx, vy, rho, p / rho^2)
 static constexpr int PAIR_CAP = 1024;
+// the prelaunched sub-step's stats (pre) into the step's (st), resetting the
+// step stats first (what k_merge_prestats did as its own launch): one thread
+// of the first forces pass, atomics where the pass itself adds to a slot
+__device__ __forceinline__ void merge_prestats_dev(int32_t *__restrict__ st, int32_t *__restrict__ pre) {
+    st[ST_MAX_OCC] = pre[ST_MAX_OCC];
+    st[ST_OVER_CAP] = pre[ST_OVER_CAP];
+    st[ST_REF_UB] = pre[ST_REF_UB];
+    st[ST_NOT_INSERTED] = pre[ST_NOT_INSERTED];
+    atomicOr(&st[ST_CAP_OVERFLOW], pre[ST_CAP_OVERFLOW]);
+    atomicOr(&st[ST_BUCKET_OVERFLOW], pre[ST_BUCKET_OVERFLOW]);
+    atomicAdd(&st[ST_STAGE_FALLBACK], pre[ST_STAGE_FALLBACK]);
+    atomicAdd(&st[ST_OVER_CAP_TOTAL], pre[ST_OVER_CAP_TOTAL]);
+    atomicMax(&st[ST_MAX_OCC_TOTAL], pre[ST_MAX_OCC_TOTAL]);
+    for (int k = 0; k < ST_COUNT; k++) pre[k] = 0;
+}
 #ifdef LPE_FTRACE
 __device__ unsigned long long g_ftrace[4096 * 8];
 __device__ int g_ftrace_on;
@@ -1496,6 +1512,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     // run that an XCD-contiguous mapping (xcd_block) would put on one XCD
     const int lb = sp.chunk > 0 ? xcd_chunk_block(sp.nblk, sp.chunk) : (int)blockIdx.x;
     if (lb < 0) return;                       // (padding of the chunked grid)
+    if (sp.mergePre && lb == 0 && threadIdx.x == 0) merge_prestats_dev(status, sp.mergePre);   // (before the kick's reset)
     const int nn = sp.nptr ? *sp.nptr : sp.n;
     const int s0 = lb * HB, s1 = min(s0 + HB, nn);
     if (s0 >= s1) {
@@ -2201,21 +2218,6 @@ __global__ void k_unpermute(int n, const int32_t *__restrict__ id, int nf, Field
     for (int k = 0; k < nf; k++) f.dst[k][d] = f.src[k][i];
 }
 
-// the prelaunched sub-step's stats (status[1]) into the step's (status[0])
-__global__ void k_merge_prestats(int32_t *__restrict__ st, int32_t *__restrict__ pre, int reset) {
-    if (threadIdx.x != 0) return;
-    if (reset) { st[ST_MAX_OCC] = 0; st[ST_OVER_CAP] = 0; st[ST_REF_UB] = 0; }   // sph_reset_step_stats
-    st[ST_CAP_OVERFLOW] |= pre[ST_CAP_OVERFLOW];
-    st[ST_BUCKET_OVERFLOW] |= pre[ST_BUCKET_OVERFLOW];
-    st[ST_MAX_OCC] = max(st[ST_MAX_OCC], pre[ST_MAX_OCC]);
-    st[ST_NOT_INSERTED] = pre[ST_NOT_INSERTED];
-    st[ST_STAGE_FALLBACK] += pre[ST_STAGE_FALLBACK];
-    st[ST_OVER_CAP] += pre[ST_OVER_CAP];
-    st[ST_REF_UB] |= pre[ST_REF_UB];
-    st[ST_OVER_CAP_TOTAL] += pre[ST_OVER_CAP_TOTAL];
-    st[ST_MAX_OCC_TOTAL] = max(st[ST_MAX_OCC_TOTAL], pre[ST_MAX_OCC_TOTAL]);
-    for (int k = 0; k < ST_COUNT; k++) pre[k] = 0;
-}
 
 }  // namespace lpe
 
@@ -2684,15 +2686,16 @@ static int sph_scan(lpe_ctx *ctx, int C, int32_t *cnt, int32_t *start, int32_t *
     hipStream_t s = ctx->stream;
     // the fluid hash with few tiles: k_scan_blocks' work folded into every
     // k_scan_final block (LPE_NO_SCAN_FUSION=1: off)
+    // (the rigid bins too, as a plain prefix: no grid, no stats)
     static const bool nofuse = getenv("LPE_NO_SCAN_FUSION") != nullptr;
-    const bool fused = fluid && nb <= 1024 && !nofuse;
+    const bool fused = nb <= 1024 && !nofuse;
     LPE_KERNEL(ctx, "k_scan_reduce", k_scan_reduce, dim3(nb), dim3(TPB), 0, s, C, cnt, bsum,
-               fused ? d.stat_cur : (int32_t *)nullptr);
+               fused && fluid ? d.stat_cur : (int32_t *)nullptr);
     if (!fused)
         LPE_KERNEL(ctx, "k_scan_blocks", k_scan_blocks, dim3(1), dim3(TPB), 0, s, nb, bsum, start + C, d.bboxPart,
                    nparts, d.cs, fluid ? d.gp_cur : (GridParams *)nullptr, d.stat_cur, bbG);
     LPE_KERNEL(ctx, "k_scan_final", k_scan_final, dim3(nb), dim3(TPB), 0, s, C, d.W, d.ox, d.oy, cnt, bsum,
-               start, cursor, d.gp_cur, d.stat_cur, fluid ? 1 : 0, fused ? 1 : 0, (const float4 *)d.bboxPart,
+               start, cursor, d.gp_cur, d.stat_cur, fluid ? 1 : 0, fused ? (fluid ? 1 : 2) : 0, (const float4 *)d.bboxPart,
                nparts, d.cs, bbG);
     LPE_CHECK_LAUNCH(ctx, "scan");
     return LPE_OK;
@@ -3092,9 +3095,7 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
     int st = sph_build_rigid_bins(ctx);
     if (st) return st;
     if (pre) {
-        // (resets the step stats as sph_reset_step_stats, then merges)
-        LPE_KERNEL(ctx, "k_merge_prestats", k_merge_prestats, dim3(1), dim3(64), 0, s, d.status,
-                   d.status + ST_COUNT, 1);
+        // (the first forces pass resets the step stats and merges the prelaunch's: sp.mergePre)
     } else {
         st = sph_reset_step_stats(ctx, s, d.status);
         if (st) return st;
@@ -3171,6 +3172,7 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
             kn.fk = sph_fastkick(ctx, sph_rowscan_ok(d));
         }
         kicked = kn.on ? fblocks : 0;
+        sp.mergePre = (step == 0 && pre) ? d.status + ST_COUNT : nullptr;
         LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(fgrid), dim3(HB), 0, s, sp, cp,
                            (step == 0 && pre) ? d.gp + 1 : d.gp,
                            d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart, d.rbinList,
