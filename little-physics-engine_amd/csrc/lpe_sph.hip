@@ -635,6 +635,7 @@ k_scan_rows(int W, int H, int ox, int oy, float eps, const int32_t *__restrict__
     if (r == ry0 && threadIdx.x == 0) *gp = g;
     const int gy = r + oy;
     const bool rowIn = gy >= g.gridMinY && gy < g.gridMinY + g.gridDimY;
+    int tmax = 0, tout = 0, tover = 0;                 // this thread's cells' stats (reduced once at the end)
     for (int c0 = 0; c0 < W; c0 += TPB) {
         const int c = c0 + (int)threadIdx.x;
         const size_t base = ((size_t)r * W + c) * 4;
@@ -652,8 +653,8 @@ k_scan_rows(int W, int H, int ox, int oy, float eps, const int32_t *__restrict__
             // metal:224-226): those particles are "not inserted"
             const int gx = c + ox;
             const bool in = rowIn && gx >= g.gridMinX && gx < g.gridMinX + g.gridDimX;
-            if (in) atomicMax(&s_max, sum); else atomicAdd(&s_out, sum);
-            if (in && sum > LPE_REF_MAX_PER_CELL) atomicAdd(&s_over, 1);
+            if (in) tmax = max(tmax, sum); else tout += sum;
+            if (in && sum > LPE_REF_MAX_PER_CELL) tover++;
         }
         int tot;
         int ex = block_excl_scan(sum, &tot) + pre;
@@ -665,6 +666,16 @@ k_scan_rows(int W, int H, int ox, int oy, float eps, const int32_t *__restrict__
         pre += tot;
     }
     if (r == ry1 && threadIdx.x == 0) start[(size_t)(r + 1) * W * 4] = pre;   // end of the last active bin
+    for (int off = 32; off > 0; off >>= 1) {
+        tmax = max(tmax, __shfl_xor(tmax, off));
+        tout += __shfl_xor(tout, off);
+        tover += __shfl_xor(tover, off);
+    }
+    if (lane_id() == 0) {
+        if (tmax) atomicMax(&s_max, tmax);
+        if (tout) atomicAdd(&s_out, tout);
+        if (tover) atomicAdd(&s_over, tover);
+    }
     __syncthreads();
     if (ovf) {
         // the bucket's overflow entries of this row's bins to tmpId[start + arrival]
