@@ -586,6 +586,7 @@ k_scan_rows(int W, int H, int ox, int oy, float eps, const int32_t *__restrict__
     const int r = (int)blockIdx.x;
     if (threadIdx.x == 0) rowtotNext[r] = 0;
     if (ovfNext && r == 0 && threadIdx.x == 0) ovfNext[0] = 0;
+    const int novf = ovf ? min(ovf[0], ovfcap) : 0;      // (in flight with the loads below)
     // everything the block needs is loaded up front (one round trip): the
     // row's first SR_CELLS cells, the row totals below it, the bbox partials
     int4 v[SR_CELLS / TPB];
@@ -677,12 +678,11 @@ k_scan_rows(int W, int H, int ox, int oy, float eps, const int32_t *__restrict__
         if (tover) atomicAdd(&s_over, tover);
     }
     __syncthreads();
-    if (ovf) {
+    if (novf > 0) {
         // the bucket's overflow entries of this row's bins to tmpId[start + arrival]
         // (k_bucket_permute reads a full bin's later arrivals there)
-        const int L = min(ovf[0], ovfcap);
         const int4 *e = (const int4 *)(ovf + 4);
-        for (int t = (int)threadIdx.x; t < L; t += TPB) {
+        for (int t = (int)threadIdx.x; t < novf; t += TPB) {
             const int4 v = e[t];
             if ((int)(((uint32_t)v.x >> 2) / (uint32_t)W) == r) tmpId[start[v.x] + v.z] = v.y;
         }
