@@ -1093,7 +1093,11 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     __shared__ float4 lrec[HCAP + 4];                     // + 4: the span walk reads up to 3 past a span
     __shared__ int lbnd[HBND];
     __shared__ uint4 lnl[NL ? HB : 1];                    // per thread: the current group of 8 offsets
+#ifdef LPE_DENSITY_PLAIN      // (A/B variant: plain block order, as the forces pass)
+    const int lb = (int)blockIdx.x < (n + HB - 1) / HB ? (int)blockIdx.x : -1;
+#else
     const int lb = xcd_block((n + HB - 1) / HB);
+#endif
     if (lb < 0) return;                                   // whole block idle
     const int nn = nptr ? *nptr : n;
     const int s0 = lb * HB, s1 = min(s0 + HB, nn);
