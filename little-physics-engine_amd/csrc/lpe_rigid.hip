@@ -96,17 +96,37 @@ __global__ void __launch_bounds__(RTPB) k_rscan_blocks(const int32_t *nptr, int 
     }
     if (threadIdx.x == 0) start[n] = carry;
 }
+// fused (<= 1,024 tiles): bsum holds the raw tile totals and each block sums
+// the ones before it (k_rscan_blocks' work, one launch fewer); block 0 stores
+// the total at start[n]
 __global__ void __launch_bounds__(RTPB) k_rscan_final(const int32_t *nptr, int ncap,
                                                       const int32_t *__restrict__ cnt,
                                                       const int32_t *__restrict__ bsum,
                                                       int32_t *__restrict__ start,
-                                                      int32_t *__restrict__ cursor) {
+                                                      int32_t *__restrict__ cursor, int fused) {
     int n = nptr ? min(*nptr, ncap) : ncap;   // a count past the capacity (overflow, redone) is clipped
     int base = blockIdx.x * 1024 + threadIdx.x * 4;
+    int pfx = 0;
+    if (fused) {
+        const int nt = (n + 1023) / 1024;
+        int pre = 0, all = 0;
+        for (int t = threadIdx.x; t < nt; t += RTPB) {
+            const int v = bsum[t];
+            pre += t < (int)blockIdx.x ? v : 0;
+            all += v;
+        }
+        int tp, ta;
+        (void)r_block_excl(pre, &tp);
+        (void)r_block_excl(all, &ta);
+        pfx = tp;
+        if (blockIdx.x == 0 && threadIdx.x == 0) start[n] = ta;
+    } else if (base < n || threadIdx.x == 0) {
+        pfx = bsum[blockIdx.x];
+    }
     int v[4], s = 0;
     for (int k = 0; k < 4; k++) { int c = base + k; v[k] = (c < n) ? cnt[c] : 0; s += v[k]; }
     int tot;
-    int ex = r_block_excl(s, &tot) + ((base < n || threadIdx.x == 0) ? bsum[blockIdx.x] : 0);
+    int ex = r_block_excl(s, &tot) + pfx;
     for (int k = 0; k < 4; k++) {
         int c = base + k;
         if (c < n) { start[c] = ex; if (cursor) cursor[c] = ex; }
@@ -286,9 +306,24 @@ __device__ __forceinline__ bool body_candidate(const lpe_body &b) {
     return (b.flags & LPE_BODY_HAS_MASS) && (b.flags & LPE_BODY_HAS_PHASE) && (b.flags & LPE_BODY_SOLID);
 }
 
+// (also zeroes what the detection after it counts into: counts [0..3], [6],
+// [10], [11], the per-body pair counts and the broadphase cell counts -- six
+// memset launches fewer at the head of the detection)
 __global__ void k_rb_prep(int nb, const lpe_body *__restrict__ bodies, const double *__restrict__ verts,
-                          double lo, double hi, double4 *__restrict__ aabb, int32_t *__restrict__ cand) {
+                          double lo, double hi, double4 *__restrict__ aabb, int32_t *__restrict__ cand,
+                          int32_t *__restrict__ counts, int32_t *__restrict__ pcount, int32_t *__restrict__ bgCount,
+                          int cells, int32_t *__restrict__ inContact) {
     int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i == 0) {
+        counts[0] = counts[1] = counts[2] = counts[3] = 0;
+        counts[6] = counts[10] = counts[11] = 0;
+    }
+    for (int c = i; c < cells; c += (int)gridDim.x * RTPB) bgCount[c] = 0;
+    if (i < nb) {
+        pcount[i] = 0;
+        inContact[i] = 0;                // (and the solvers' contact marks, for colour_prep)
+        inContact[nb + i] = 0;
+    }
     if (i >= nb) return;
     const lpe_body b = bodies[i];
     double mnx, mny, mxx, mxy;
@@ -3002,9 +3037,14 @@ static int rscan(lpe_ctx *ctx, RigidDev *d, const int32_t *nptr, int ncap, const
     if (st) return st;
     int nb = ncap / 1024 + 1;
     if (!s) s = ctx->stream;
+    // <= 1,024 tiles: the tile prefix inside k_rscan_final (LPE_NO_RSCAN_FUSION=1: off)
+    static const bool nofuse = getenv("LPE_NO_RSCAN_FUSION") != nullptr;
+    const int fused = (nb <= 1024 && !nofuse) ? 1 : 0;
     LPE_KERNEL(ctx, "k_rscan_reduce", k_rscan_reduce, dim3(nb), dim3(RTPB), 0, s, nptr, ncap, cnt, d->bsum);
-    LPE_KERNEL(ctx, "k_rscan_blocks", k_rscan_blocks, dim3(1), dim3(RTPB), 0, s, nptr, ncap, d->bsum, start);
-    LPE_KERNEL(ctx, "k_rscan_final", k_rscan_final, dim3(nb), dim3(RTPB), 0, s, nptr, ncap, cnt, d->bsum, start, cursor);
+    if (!fused)
+        LPE_KERNEL(ctx, "k_rscan_blocks", k_rscan_blocks, dim3(1), dim3(RTPB), 0, s, nptr, ncap, d->bsum, start);
+    LPE_KERNEL(ctx, "k_rscan_final", k_rscan_final, dim3(nb), dim3(RTPB), 0, s, nptr, ncap, cnt, d->bsum, start, cursor,
+               fused);
     LPE_CHECK_LAUNCH(ctx, "rscan");
     return LPE_OK;
 }
@@ -3113,10 +3153,11 @@ static int detect_launch(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pa
     const lpe_rigid_config &c = d->cfg;
     int nb = d->nb;
     // [0..3], [6] (counts[4], [5] belong to the solvers / gravity; [7]: solver fault, sticky)
-    LPE_HIP(ctx, hipMemsetAsync(d->counts, 0, sizeof(int32_t) * 4, s));
-    LPE_HIP(ctx, hipMemsetAsync(d->counts + 6, 0, sizeof(int32_t), s));
-    LPE_HIP(ctx, hipMemsetAsync(d->counts + 11, 0, sizeof(int32_t), s));
+    d->contacts_zeroed = false;
     if (pairs_in) {
+        LPE_HIP(ctx, hipMemsetAsync(d->counts, 0, sizeof(int32_t) * 4, s));
+        LPE_HIP(ctx, hipMemsetAsync(d->counts + 6, 0, sizeof(int32_t), s));
+        LPE_HIP(ctx, hipMemsetAsync(d->counts + 11, 0, sizeof(int32_t), s));
         if (np_in > d->cap_pairs) {
             int st = rigid_alloc_pairs(ctx, d, np_in + 1024);
             if (st) return st;
@@ -3126,8 +3167,6 @@ static int detect_launch(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pa
         LPE_HIP(ctx, hipMemcpyAsync(d->counts, &np_in, sizeof(int32_t), hipMemcpyHostToDevice, s));
     } else {
         double lo = -c.boundaryBuffer, hi = -c.boundaryBuffer + (c.universeSize + 2 * c.boundaryBuffer);
-        LPE_KERNEL(ctx, "k_rb_prep", k_rb_prep, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->verts, lo, hi, d->aabb, d->cand);
-        LPE_HIP(ctx, hipMemsetAsync(d->pcount, 0, sizeof(int32_t) * nb, s));
         // grid over the universe plus 1 m (bodies the boundary system lets
         // stray further, or larger than a cell, are "special")
         const double org = -1.0, g = d->bp_cell > 0.0 ? d->bp_cell : 1.0;
@@ -3144,8 +3183,9 @@ static int detect_launch(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pa
             if (st0) return st0;
             d->cap_bgcells = cells;
         }
-        LPE_HIP(ctx, hipMemsetAsync(d->bgCount, 0, sizeof(int32_t) * cells, s));
-        LPE_HIP(ctx, hipMemsetAsync(d->counts + 10, 0, sizeof(int32_t), s));
+        LPE_KERNEL(ctx, "k_rb_prep", k_rb_prep, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->verts, lo, hi, d->aabb,
+                   d->cand, d->counts, d->pcount, d->bgCount, cells, d->inContact);
+        d->contacts_zeroed = true;
         LPE_KERNEL(ctx, "k_bg_key", k_bg_key, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->byRank, d->aabb, d->cand, org, g,
                    (int)G, d->bgKey, d->bgCount, d->bgSpecial, d->counts + 10);
         int st = rscan(ctx, d, nullptr, cells, d->bgCount, d->bgStart, d->bgCursor, s);
@@ -3346,7 +3386,9 @@ static int colour_prep(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     // (lagged detection: the count is on the device only, the grids cover the capacity)
     const int nb = d->nb, nc = d->lag ? d->cap_contacts : d->last_nc;
     int32_t *inPos = d->inContact + nb;
-    LPE_HIP(ctx, hipMemsetAsync(d->inContact, 0, sizeof(int32_t) * 2 * nb, s));
+    if (!d->contacts_zeroed || s != d->side)      // (k_rb_prep zeroed them on the detection stream)
+        LPE_HIP(ctx, hipMemsetAsync(d->inContact, 0, sizeof(int32_t) * 2 * nb, s));
+    d->contacts_zeroed = false;
     LPE_KERNEL(ctx, "k_mark_contacts", k_mark_contacts, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->contacts, d->inContact);
     LPE_KERNEL(ctx, "k_pgs_bodies", k_pgs_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->imii, 1);
     LPE_KERNEL(ctx, "k_pgs_rows", k_pgs_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->order, d->contacts, d->bodies, d->imii, d->rowN, d->rowR, d->rowAB, d->rowM, d->sItemA, d->sItemB);

@@ -98,6 +98,7 @@ struct RigidDev {
     // buffers at the next tick start; an overflow (more than 4x growth within
     // two ticks) fails loudly (LPE_ERR_OVERFLOW).  counts[14] = contacts found.
     bool lag = false, lag_next = false;
+    bool contacts_zeroed = false;       // k_rb_prep of this detection zeroed inContact (colour_prep skips its memset)
     int32_t *hcr = nullptr;                   // pinned [2][16]
     hipEvent_t evHc[2] = {nullptr, nullptr};
     bool hpend[2] = {false, false};
