@@ -125,41 +125,77 @@ __device__ __forceinline__ void bh_fold(BhNode &nd, double x, double y, double m
     if (m >= thr) nd.flags &= ~BH_SMALL;
 }
 
-// one thread per node of the level: the node's insertion sequence through
+// lane i's double (i wave-uniform): two v_readlane, no LDS round trip
+__device__ __forceinline__ double bh_lane(double v, int i) {
+    const long long u = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)u, i);
+    const int hi = __builtin_amdgcn_readlane((int)(u >> 32), i);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+// one wave per node of the level: the node's insertion sequence through
 // insertParticle's state machine (:143-196); route[k] = 1 where member k is
-// passed on to a child (the child itself is found by k_bh_route)
-__global__ void k_bh_fold(int base, int nlev, const int32_t *__restrict__ segB, const int32_t *__restrict__ segE,
-                          const int32_t *__restrict__ val, const double *__restrict__ x,
-                          const double *__restrict__ y, const double *__restrict__ m, double thr,
-                          BhNode *__restrict__ nodes, uint8_t *__restrict__ route, int32_t *cnt) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+// passed on to a child (the child itself is found by k_bh_route).  The
+// sequence is one dependent chain in fp64, so the lanes only fetch: each
+// round gathers 64 members' (id, x, y, m) at once and every lane replays
+// them in order from its registers (wave-uniform state), so the chain pays
+// one gather latency per 64 members instead of one per member.
+__global__ __launch_bounds__(64) void k_bh_fold(int base, int nlev, const int32_t *__restrict__ segB,
+                                                const int32_t *__restrict__ segE, const int32_t *__restrict__ val,
+                                                const double *__restrict__ x, const double *__restrict__ y,
+                                                const double *__restrict__ m, double thr,
+                                                BhNode *__restrict__ nodes, uint8_t *__restrict__ route,
+                                                int32_t *cnt) {
+    const int j = blockIdx.x;
     if (j >= nlev) return;
+    const int lane = threadIdx.x;
     const int id = base + j;
     BhNode nd = nodes[id];
     const int b = segB[j], e = segE[j];
     int occK = -1;                                          // position of the occupant in the segment
-    for (int k = b; k < e; k++) {
-        const int p = val[k];
-        const double px = x[p], py = y[p], pm = m[p];
-        route[k] = 0;
-        if (nd.mass == 0.0) {                               // empty: store (:144-154)
-            nd.mass = pm;
-            nd.cx = px;
-            nd.cy = py;
-            nd.single = p;
-            occK = k;
-            if (pm >= thr) nd.flags &= ~BH_SMALL;
-            continue;
+    int lateOcc = -1;                                       // occupant routed after its round was written
+    for (int k0 = b; k0 < e; k0 += 64) {
+        const int nk = min(64, e - k0);
+        int p = 0;
+        double px = 0.0, py = 0.0, pm = 0.0;
+        if (lane < nk) {
+            p = val[k0 + lane];
+            px = x[p];
+            py = y[p];
+            pm = m[p];
         }
-        if (nd.flags & BH_LEAF) {                           // split (:157-169)
-            nd.flags &= ~BH_LEAF;
-            const int o = nd.single;
-            bh_fold(nd, x[o], y[o], m[o], thr);             // the occupant again, via the internal branch
-            route[occK] = 1;
+        uint64_t rmask = 0;                                 // route bits of this round (uniform)
+        for (int i = 0; i < nk; i++) {
+            const int qp = __builtin_amdgcn_readlane(p, i);
+            const double qx = bh_lane(px, i), qy = bh_lane(py, i), qm = bh_lane(pm, i);
+            const int k = k0 + i;
+            if (nd.mass == 0.0) {                           // empty: store (:144-154)
+                nd.mass = qm;
+                nd.cx = qx;
+                nd.cy = qy;
+                nd.single = qp;
+                occK = k;
+                if (qm >= thr) nd.flags &= ~BH_SMALL;
+                rmask &= ~(1ull << i);
+                continue;
+            }
+            if (nd.flags & BH_LEAF) {                       // split (:157-169)
+                nd.flags &= ~BH_LEAF;
+                const int o = nd.single;
+                bh_fold(nd, x[o], y[o], m[o], thr);         // the occupant again, via the internal branch
+                if (occK >= k0) rmask |= 1ull << (occK - k0);
+                else lateOcc = occK;
+            }
+            bh_fold(nd, qx, qy, qm, thr);
+            rmask |= 1ull << i;
         }
-        bh_fold(nd, px, py, pm, thr);
-        route[k] = 1;
+        if (lane < nk) route[k0 + lane] = (uint8_t)((rmask >> lane) & 1);
     }
+    if (lateOcc >= 0) {                                     // after this wave's earlier store of 0 landed
+        __threadfence();
+        if (lane == 0) route[lateOcc] = 1;
+    }
+    if (lane != 0) return;
     if (!(nd.flags & BH_LEAF)) {                            // subdivide (:199-238)
         const int c = atomicAdd(&cnt[0], 4);
         nd.child = c;
@@ -467,7 +503,7 @@ static int bh_run(lpe_ctx *ctx, BhDev &d, const lpe_bh_config *cfg, double dt, l
         LPE_HIP(ctx, hipMemsetAsync(d.segE, 0, sizeof(int32_t) * (size_t)nlev, s));
         LPE_KERNEL(ctx, "k_bh_segs", k_bh_segs, dim3(bblk(A)), dim3(256), 0, s, A, (int)base, d.key[cur], d.segB,
                    d.segE);
-        LPE_KERNEL(ctx, "k_bh_fold", k_bh_fold, dim3(bblk(nlev, 64)), dim3(64), 0, s, (int)base, nlev, d.segB,
+        LPE_KERNEL(ctx, "k_bh_fold", k_bh_fold, dim3(std::max(1, nlev)), dim3(64), 0, s, (int)base, nlev, d.segB,
                    d.segE, d.val[cur], d.x, d.y, d.m, thr, d.nodes, d.route, d.cnt);
         LPE_HIP(ctx, hipMemsetAsync(d.cnt + 1, 0, sizeof(int32_t), s));
         LPE_KERNEL(ctx, "k_bh_route", k_bh_route, dim3(bblk(A)), dim3(256), 0, s, A, d.key[cur], d.val[cur],
