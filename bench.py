@@ -239,41 +239,70 @@ def render_bench(ctx, U, reps=3):
 
 
 def loopback_check(args, lpe, scenes, slab, device):
-    """K slab ranks of MW{K} (or of C5 with --scene C5) on one GPU through the in-process transport:
-    exercises the sharded bench path (scene, slab set-up, world ticks with
-    halo exchange and migration) where only one GPU is available.  Prints one
-    JSON check line (not the metric: K ranks share one GPU)."""
+    """K slab ranks of MW{K} (or of C5 with --scene C5) on one GPU through the
+    in-process transport (stream-ordered like RCCL: the host never waits for
+    the device), beside the same scene as ONE domain on the same GPU: the
+    ratio of the two walls is the decomposition's overhead (ghost work,
+    exchanges, the extra launches), since both do the same physics on the
+    same GPU.  Prints one JSON check line (not the metric)."""
     K = args.loopback
     name = "C5" if args.scene == "C5" else f"MW{K}"
     s = scenes.scene(name)
     fl = s["fluid"]
     bodies, verts = scenes.to_bodies(s["bodies"])
-    edges = slab.slab_edges(fl["x"], K)
+    cfg = lpe.default_fluid_config()
+    wc = lpe.WorldConfig(1.0 / 120.0, 1.0, 1.0, 1.0)
+    nt = args.warmup + args.steps
+
+    one = lpe.Context(device)
+    try:
+        one.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+        one.rigid_upload(bodies, verts)
+        one.sph_set_config(cfg)
+        one.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+        one.world_set_coupling(None)
+        one.world_tick(1.0 / 120.0, args.prep + args.warmup)
+        one.sync()
+        t0 = time.perf_counter()
+        one.world_tick(1.0 / 120.0, args.steps)
+        one.sync()
+        single = args.steps / (time.perf_counter() - t0)
+    finally:
+        one.close()
+
+    edges = slab.slab_edges(fl["x"], K, cfg)
     ctxs = [lpe.Context(device) for _ in range(K)]
     try:
         for r, c in enumerate(ctxs):
             c.rigid_set_config(lpe.rigid_config(universe=s["U"]))
             c.rigid_upload(bodies, verts)
-            slab.setup_rank(c, r, K, fl, edges, lpe.default_fluid_config())
+            slab.setup_rank(c, r, K, fl, edges, cfg, rebalance=args.rebalance)
             c.world_set_coupling(None)
-        wc = lpe.WorldConfig(1.0 / 120.0, 1.0, 1.0, 1.0)
+        lpe.mg_loopback_run(ctxs, args.prep + args.warmup, world=wc)
         t0 = time.perf_counter()
-        lpe.mg_loopback_run(ctxs, args.prep + args.warmup + args.steps, world=wc)
+        lpe.mg_loopback_run(ctxs, args.steps, world=wc)
         el = time.perf_counter() - t0
+        st = [c.sph_stats() for c in ctxs]
+        info = [c.sph_slab_info() for c in ctxs]
         parts = [c.sph_download_owned() for c in ctxs]
         merged = slab.merge_owned(parts, len(fl["x"]))
         rb = [c.rigid_download() for c in ctxs]
         same = all(np.array_equal(rb[0][k], r[k]) for r in rb[1:] for k in ("x", "y", "angle"))
-        st = ctxs[0].sph_stats()
     finally:
         for c in ctxs:
             c.close()
-    print(json.dumps({"check": "loopback", "ranks": K, "scene": name, "ticks": args.prep + args.warmup + args.steps,
-                      "seconds": round(el, 3), "ticks_per_s_all_ranks_on_one_gpu":
-                          round((args.prep + args.warmup + args.steps) / el, 2),
-                      "owned": [len(p["x"]) for p in parts],
+    loop = args.steps / el
+    print(json.dumps({"check": "loopback", "ranks": K, "scene": name, "particles": len(fl["x"]),
+                      "prep_ticks": args.prep, "ticks_timed": args.steps,
+                      "single_domain_ticks_per_s": round(single, 2),
+                      "loopback_ticks_per_s_all_ranks_on_one_gpu": round(loop, 2),
+                      "wall_ratio_loopback_over_single": round(single / loop, 3),
+                      "owned": [x["slabOwned"] for x in st], "slots": [x["slabSlots"] for x in st],
+                      "ghosts_in_max": [x["ghostsIn"] for x in st], "wire_records": st[0]["haloWire"][1],
+                      "edges_columns": [int(e) for e in info[0]["edges"][1:-1]],
                       "finite": bool(np.isfinite(merged["x"]).all() and np.isfinite(merged["vy"]).all()),
-                      "rigid_replicas_identical": bool(same), "max_cell_occupancy_rank0": st["maxCellOccupancy"]}))
+                      "rigid_replicas_identical": bool(same), "max_cell_occupancy_rank0": st[0]["maxCellOccupancy"],
+                      "note": "K ranks share one GPU: the ratio is the decomposition's overhead, not scaling"}))
 
 
 def rigid_microbench(lpe, device, reps=10):
@@ -487,6 +516,28 @@ def config_lines(lpe, scenes, device, dt_tick, with_ref):
     return out
 
 
+def launch_ranks(n, cmd=None):
+    """`python bench.py --gpus N` without a launcher: start N rank processes
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torch.distributed.run sets
+    them, rendezvous on 127.0.0.1) from this parent, which never touches the
+    GPU, and return the first non-zero status of the children (0 if none).
+    cmd: the rank command (default: this script with the same arguments)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd, env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -505,11 +556,22 @@ def main():
     ap.add_argument("--loopback", type=int, default=0,
                     help="validation only: K slab ranks of MW{K} in this process on one GPU "
                          "(in-process transport); prints a check line, not the metric")
+    ap.add_argument("--rebalance", type=int, default=10,
+                    help="N > 1: move the slab edges towards equal counts every this many ticks (0: fixed)")
+    ap.add_argument("--cells", choices=("ref", "unbounded"), default="ref",
+                    help="ref (default): the timed window runs the reference's 64-particle cells "
+                         "(LPE_SPH_MODE_REF_CELL_CAP, fluid.hpp:56); unbounded: no per-cell cap")
     args = ap.parse_args()
     if args.prep is None:
         args.prep = 240 if args.scene == "C5" else 3000
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1 and not args.loopback:
+        sys.exit(launch_ranks(args.gpus))       # (the parent makes no HIP call)
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and not args.loopback:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: refusing to report a {world}-rank run "
+              f"as {args.gpus} GPU(s)", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -534,8 +596,9 @@ def main():
     ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
     ctx.rigid_upload(bodies, verts)
     if sharded:
-        edges = slab.slab_edges(fl["x"], world)
-        slab.setup_rank(ctx, rank, world, fl, edges, lpe.default_fluid_config())
+        cfg = lpe.default_fluid_config()
+        edges = slab.slab_edges(fl["x"], world, cfg)
+        slab.setup_rank(ctx, rank, world, fl, edges, cfg, rebalance=args.rebalance)
         uid = slab.broadcast_uid(lpe.mg_unique_id() if rank == 0 else None, rank)
         ctx.mg_init_rccl(world, rank, uid)
     else:
@@ -547,6 +610,13 @@ def main():
     # pile (the steady state: ~10k pairs, ~35k contacts); BASELINE.md times
     # the reference's pile the same way, after 240 warm-up ticks
     ctx.world_tick(dt_tick, args.prep)
+    # the timed window in the reference's own cell semantics (its 64-slot
+    # cells: dropped inserts, cross-cell reads; fluid.hpp:56, metal:237-240,
+    # :281-283) -- the mode tests/test_configs_gpu.py pins at this state;
+    # slab ranks run unbounded cells (the capped walk is single-domain)
+    capped = args.cells == "ref" and not sharded
+    if capped:
+        ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP)
     ctx.world_tick(dt_tick, args.warmup)
     ctx.sync()
 
@@ -564,11 +634,25 @@ def main():
     barrier()
     elapsed = t1 - t0
     wstats = ctx.sph_stats()
+    ranks_info = None
     if dist is not None:
         import torch
+        mine = dict(rank=rank, ms_per_tick=elapsed / args.steps * 1e3, owned=wstats["slabOwned"],
+                    slots=wstats["slabSlots"], ghosts_in=wstats["ghostsIn"], wire=wstats["haloWire"],
+                    comm_ranks=ctx.mg_info()["comm_ranks"] if sharded else None,
+                    edges=[int(e) for e in ctx.sph_slab_info()["edges"][1:-1]] if sharded else None)
+        every = [None] * world
+        dist.all_gather_object(every, mine)
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+        slow = max(every, key=lambda e: e["ms_per_tick"])
+        ranks_info = dict(ranks_seen=every[0]["comm_ranks"], world_size=world,
+                          ms_per_tick=[round(e["ms_per_tick"], 4) for e in every],
+                          slowest_rank=slow["rank"], slowest_ms_per_tick=round(slow["ms_per_tick"], 4),
+                          owned=[e["owned"] for e in every], slots=[e["slots"] for e in every],
+                          ghosts_in_max=[e["ghosts_in"] for e in every], wire_records=every[0]["wire"],
+                          edges_columns=every[0]["edges"])
     extras = {}
     if world == 1 and not args.no_extras:
         rate = args.steps / elapsed
@@ -678,6 +762,8 @@ def main():
                                "RigidBodyCollision (broadphase, GJK/EPA, PGS 10 it, position 10 it)",
                                "Rotation", "Movement", "Sleep"],
                    "mode": "resident (ECS sync skipped inside the timed region)",
+                   "cells": ("the reference's 64-particle cells (LPE_SPH_MODE_REF_CELL_CAP)" if capped
+                             else "unbounded cells"),
                    "parallelism": (f"SPH x-slabs x{world} (RCCL halo + bbox/accumulator all-reduce), "
                                    f"rigid pass replicated") if sharded else
                                   ("single GPU" if world == 1 else f"replica x{world}")},
@@ -693,18 +779,20 @@ def main():
             "inside": wstats["overCapCellsTotal"] == 0,
             "note": "reference cells (2h) holding more than GPU_MAX_PER_CELL = 64 particles, summed over the "
                     "sub-steps of the timed window: where non-zero the reference drops inserts and reads "
-                    "across cells (fluid.hpp:56, fluid_kernels.metal:237-240, :281-283); the headline runs "
-                    "the unbounded lists, and LPE_SPH_MODE_REF_CELL_CAP reproduces the reference's behaviour "
-                    "exactly (tests/test_configs_gpu.py checks both at this scene)"},
+                    "across cells (fluid.hpp:56, fluid_kernels.metal:237-240, :281-283); the window runs "
+                    "LPE_SPH_MODE_REF_CELL_CAP (config.cells), which reproduces that behaviour exactly "
+                    "(tests/test_configs_gpu.py checks both modes at this scene)"},
         "rigid": {"pairs": int(len(pairs)), "contacts": int(len(contacts)), "colours": int(ncolours)},
     }
+    if ranks_info is not None:
+        line["ranks"] = ranks_info
     line.update(extras)
     if world == 1 and not args.no_extras:
-        # the same scene in the reference's own 64-slot cell mode
-        ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP)
+        # the same scene in the other cell mode
+        ctx.sph_set_mode(0 if capped else lpe.SPH_MODE_REF_CELL_CAP)
         w = timed_windows(ctx, dt_tick, args.steps / elapsed, nwin=3, min_s=1.0)
-        ctx.sph_set_mode(0)
-        line["ref_cell_cap_mode"] = dict(ticks_per_s=w["median"], windows=w)
+        ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP if capped else 0)
+        line["unbounded_cells_mode" if capped else "ref_cell_cap_mode"] = dict(ticks_per_s=w["median"], windows=w)
         line["configs"] = config_lines(lpe, scenes, local, dt_tick, not args.no_cpu_baseline)
     if world == 1 and not args.no_density_microbench:
         line["density_microbench"] = density_microbench(lpe, scenes, local)

@@ -145,10 +145,16 @@ typedef struct lpe_sph_stats {
      * since the last lpe_sph_diag call (a bench window) */
     int32_t overCapCellsTotal;
     int32_t maxCellOccupancyTotal;
-    /* slab decomposition: ghost records this rank sends to its left / right
-     * neighbour per sub-step (every exchange moves the capacity, ghost_cap of
+    /* slab decomposition: ghost records each exchange moves to the left /
+     * right neighbour per sub-step (the wire capacity, wire_cap of
      * lpe_sph_set_slab; 0 without a neighbour or off a slab) */
     int32_t haloWire[2];
+    /* slab decomposition: the particles this rank owns now, its slots in use
+     * (owned + ghosts of the last sub-step), and the most ghost records the
+     * left / right neighbour filed for it in a sub-step since the last
+     * lpe_sph_diag; all 0 off a slab */
+    int32_t slabOwned, slabSlots;
+    int32_t ghostsIn[2];
 } lpe_sph_stats;
 
 /* ------------------------------------------------------------------------ */
@@ -408,39 +414,54 @@ int  lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *cfg, int nticks);
 
 /* ---- x-slab decomposition of the SPH step -----------
  * The reference has one FluidSystem per process (fluid.cpp:958-1021); these
- * entry points split its particle set over ranks by x slab.  Each rank owns
- * the particles with x in [x0, x1) (the first slab has no left edge, the last
- * no right edge) and runs lpe_sph_step on them; per sub-step it receives the
- * neighbours' particles within `halo` of its edges (ghosts, with their global
- * ids, so every density/force sum is the single-domain one bit for bit); the
- * halo is deep enough that every ghost the forces pass reads has all its
- * neighbours present, so its locally computed density is its owner's.  The reference
- * grid is derived from the all-reduced bbox of all ranks.  Once per tick the
- * rigid accumulators are all-reduced (rank order) before the write-back and
- * particles that left the slab move to the neighbour.  halo must cover twice
- * the smoothing length plus one tick's drift (a particle further outside its
- * slab raises LPE_ERR_OVERFLOW); ghost_cap bounds the ghosts and migrants per
- * side (overflow: LPE_ERR_OVERFLOW from the next download).  A slab with two
- * neighbours must be at least 2 * halo - 2h wide (ghosts come from the two
- * neighbours only); the host mirror (slab.py:default_halo) picks 2h + 1.5 m. */
-/* Call before lpe_sph_upload (the particle arrays get owned + ghost slots). */
-int  lpe_sph_set_slab(lpe_ctx *ctx, float x0, float x1, float halo, int has_left,
-                      int has_right, int ghost_cap);
+ * entry points split its particle set over ranks by x slab.  Rank r owns the
+ * particles whose reference-cell column floor((x + eps) / 2h) lies in
+ * [edges[r], edges[r+1]) / 2h (the first slab has no left edge, the last no
+ * right edge), judged from the kicked position at every sub-step, and runs
+ * lpe_sph_step / lpe_world_tick on them.  Per sub-step it exchanges with its
+ * two neighbours the particles within two cell columns of (or past) an edge
+ * -- ghosts, with their global ids and full state, so every density / force
+ * sum is the single-domain one bit for bit and a particle that crossed an
+ * edge is adopted by the rank it entered -- plus every rank's bbox record
+ * (the reference grid is the global one).  Once per tick the rigid
+ * accumulators are all-reduced (exact int64 limbs) before the write-back.
+ * No host synchronisation: the exchanges are stream-ordered.
+ * edges: nranks + 1 values in metres; the inner ones must be multiples of
+ * the reference cell size 2h (0.1 m at the default h; the outer two are
+ * ignored) and at least 8 cells apart.  wire_cap: ghost records per
+ * direction and sub-step (both ends the same; more raise LPE_ERR_OVERFLOW at
+ * the next download).  rebalance > 0: every that many fluid steps the inner
+ * edges move one cell column towards equal owned counts (an all-reduced
+ * histogram; identical on every rank), at most a quarter of the narrowest
+ * slab from where they started.  Call after lpe_sph_set_config and before
+ * lpe_sph_upload (the particle arrays get slots for the ghosts and growth).
+ * A slab rank must not skip a tick or a step its neighbours take. */
+int  lpe_sph_set_slab(lpe_ctx *ctx, int nranks, int rank, const float *edges, int wire_cap,
+                      int rebalance);
+/* A slab rank's current edges as reference-cell columns (nranks + 1 into
+ * edges when cap allows; the outer two are -/+ 2^29), its rank count and
+ * how many columns an edge may move from where it started (0: fixed). */
+int  lpe_sph_slab_info(lpe_ctx *ctx, int cap, int32_t *edges, int *nranks, int *move);
 /* Global particle ids of the n uploaded (owned) particles (default 0..n-1). */
 int  lpe_sph_set_ids(lpe_ctx *ctx, int n, const int32_t *ids);
-/* The particles this context owns, in device order, with their global ids
- * (*n_out = count; LPE_ERR_CAPACITY if it exceeds cap).  Also valid without
- * a slab (ids 0..n-1 permuted). */
+/* The particles this context owns with their global ids (*n_out = count;
+ * LPE_ERR_CAPACITY if it exceeds cap); in device order without a slab (ids
+ * 0..n-1 permuted), in no particular order on a slab rank. */
 int  lpe_sph_download_owned(lpe_ctx *ctx, int cap, float *x, float *y, float *vx, float *vy,
                             float *density, float *pressure, int32_t *ids, int *n_out);
 /* Grow the device grid (fixed absolute cell grid, sized at upload from the
- * particles) to cover [x0, x1] x [y0, y1]: a slab rank sees particles of the
- * whole domain only as ghosts and migrants.  Call after lpe_sph_upload. */
+ * particles) to cover [x0, x1] x [y0, y1] (a slab rank: within its slab's
+ * reach).  Call after lpe_sph_upload. */
 int  lpe_sph_set_domain(lpe_ctx *ctx, double x0, double y0, double x1, double y1);
 /* RCCL transport (one process per GPU, rank r of n, neighbours r-1 / r+1):
  * rank 0 creates the 128-byte id, every rank passes it to lpe_mg_init_rccl. */
 int  lpe_mg_unique_id(char id[128]);
 int  lpe_mg_init_rccl(lpe_ctx *ctx, int nranks, int rank, const char *id);
+/* The context's transport: its rank count and rank, and the ranks its
+ * communicator reports (ncclCommCount for RCCL -- the bench's check that the
+ * N-GPU run really joined N ranks; the group size for the host-staged and
+ * in-process transports; all 0 without a transport). */
+int  lpe_mg_info(lpe_ctx *ctx, int *nranks, int *rank, int *comm_ranks);
 /* Host-staged transport: the caller moves host copies of the exchange
  * buffers between the ranks' processes (e.g. torch.distributed over gloo).
  * halo: send sbL bytes of sendL to rank-1 and sbR of sendR to rank+1,

@@ -115,6 +115,12 @@ struct SphDev {
     long cap_bucket = 0;          // bins the bucket covers (0: off, the scatter path)
     int32_t *bovf = nullptr;      // [2][OVF_WORDS]: count, then (bin, id) pairs
     bool fast_bucket = false;     // the pending kick filed the ids
+    // over-full reference cells of a sub-step (lpe_sph.hip ovl_append), two
+    // lists alternating by scan: the capped-cell mode's per-particle test
+    int32_t *ovl = nullptr;       // [2][OVL_WORDS]
+    long ovlIdx = 0;              // scans that wrote a list (parity)
+    const int32_t *ovl_cur = nullptr;   // the last hash's list
+    const int32_t *ovl_pre = nullptr;   // the prelaunched sub-step's
 };
 
 // status slots
@@ -137,8 +143,8 @@ enum StatusSlot {
     ST_BUCKET_OVERFLOW = 15,// the in-bin sort's overflow list overflowed (a tick's sort is wrong: fails loudly)
     ST_RX_GHOST_L = 16,     // slab decomposition: most ghosts the left / right neighbour packed for this
     ST_RX_GHOST_R = 17,     //   rank in a sub-step of the current tick (sizes the next tick's exchange)
-    ST_RX_MIG_L = 18,       // most migrants received from the left / right neighbour so far
-    ST_RX_MIG_R = 19,
+    ST_SLAB_CAPACITY = 18,  // slab decomposition: the received ghosts did not fit the rank's slots
+    ST_SPARE_19 = 19,
     ST_COUNT = 20
 };
 
@@ -234,6 +240,8 @@ float4 *sph_rig_records(lpe_ctx *ctx, int nr);   // the coupling records buffer 
 // tick's own fluid boundary / gravity pass); fbgDone is recorded after it
 int sph_prelaunch(lpe_ctx *ctx, double dt_tick, const std::function<int(hipStream_t)> &first = {});
 int lpe_sph_cover_box(lpe_ctx *ctx, double x0, double y0, double x1, double y1);
+// a slab rank's P slots in use (device count; ids -1 mark dropped slots), else null
+const int32_t *sph_slab_slots(lpe_ctx *ctx);
 // coupling rigids' device arrays (rig, accum, acq) for n rigids (grow-only)
 int sph_alloc_rigids(lpe_ctx *ctx, int n);
 // sort the CURRENT particle positions into the bins (no integration): the

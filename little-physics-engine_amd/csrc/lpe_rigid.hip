@@ -612,16 +612,26 @@ k_narrow(const int32_t *__restrict__ npptr, int cap, const int2 *__restrict__ pa
 }
 
 // (also the contact count: counts[1] = the contacts kept, at most cap;
-// counts[14] = the contacts found -- more than cap is an overflow)
-__global__ void k_compact(const int32_t *__restrict__ npptr, int cap_pairs, const lpe_contact *__restrict__ slots,
+// counts[14] = the contacts found -- more than cap is an overflow;
+// counts[15] = the pairs found.)  An overflowing detection (pairs past
+// cap_pairs or the pair-overflow flag, contacts past cap) zeroes the pair and
+// contact counts, so every kernel after it -- the striped order, the rows,
+// the solvers -- sees an empty tick and stays inside its buffers; only a
+// lagged detection gets here with an overflow (the synchronous one grows and
+// redoes first), and its check reports it from counts[15] / [14] / [6].
+__global__ void k_compact(int32_t *__restrict__ npptr, int cap_pairs, const lpe_contact *__restrict__ slots,
                           const int32_t *__restrict__ ccount, const int32_t *__restrict__ cstart,
                           lpe_contact *__restrict__ out, int cap, int32_t *__restrict__ counts) {
     int k = blockIdx.x * RTPB + threadIdx.x;
-    const int np = min(*npptr, cap_pairs);
+    const int raw = *npptr;
+    const int np = min(raw, cap_pairs);
     if (k == 0) {
         const int tot = cstart[np];
-        counts[1] = min(tot, cap);
+        const bool over = counts[6] != 0 || raw > cap_pairs || tot > cap;
+        counts[1] = over ? 0 : tot;
         counts[14] = tot;
+        counts[15] = raw;
+        if (over) *npptr = 0;          // (blocks that read it first compact within the capacities)
     }
     if (k >= np) return;
     int s = cstart[k];
@@ -2064,7 +2074,7 @@ k_stripe_pairs(const int32_t *__restrict__ npptr, const int2 *__restrict__ pairs
 // sizes (counts[12] = S, counts[13] = workgroups).
 __global__ void __launch_bounds__(SOLVE_TPB)
 k_stripe_setup(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict__ pairs,
-               const lpe_body *__restrict__ bodies, StripeBufs sb, int32_t *__restrict__ counts) {
+               const lpe_body *__restrict__ bodies, StripeBufs sb, int32_t *__restrict__ counts, int smax) {
     extern __shared__ unsigned int bmark[];                 // [2][words]: movable / static contact-pair bodies
     __shared__ double wr[3][SOLVE_TPB / 64];
     __shared__ double sx0, sw;
@@ -2102,7 +2112,9 @@ k_stripe_setup(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict
         int S = 1;
         if (mx > mn) {
             const double q = (mx - mn) / sp;          // (span 0: +inf)
-            if (q >= 2.0) S = min(STRIPES_MAX, (int)floor(fmin(q, 1e9))) & ~1;
+            // (smax: the two solvers' S / 2 workgroups each must be co-resident,
+            // one per CU -- stripe_cap)
+            if (q >= 2.0 && smax >= 2) S = min(smax, (int)floor(fmin(q, 1e9))) & ~1;
         }
         sS = S;
         sx0 = mn;
@@ -3213,13 +3225,22 @@ static int detect_launch(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pa
     return LPE_OK;
 }
 
+// counts[7]: bit 1 a dataflow (replay) solve made no progress, bit 2 a
+// striped solver's workgroup waited ~0.2 s for a neighbour's hand-over
+static const char *watchdog_msg(int bits) {
+    if (bits & 2)
+        return "striped rigid solver: a workgroup waited too long for its neighbour's hand-over (fewer "
+               "co-resident workgroups than stripes, or CUs held by other work); that solve is wrong";
+    return "rigid solver watchdog fired (a dataflow solve made no progress)";
+}
+
 // Part 2, once hc has arrived: capacity checks (1: the pair buffer
 // overflowed and was grown, run part 1 again) and the contact compaction.
 static int detect_finish(lpe_ctx *ctx, RigidDev *d, hipStream_t s, const int32_t *hc, int *retry) {
     *retry = 0;
     int np = hc[0];
     if (hc[7]) {
-        ctx->err = "rigid solver watchdog fired (a dataflow solve made no progress)";
+        ctx->err = watchdog_msg(hc[7]);
         return LPE_ERR_OVERFLOW;
     }
     if (hc[6] || np > d->cap_pairs) {   // pair buffer overflow: grow and redo
@@ -3307,6 +3328,22 @@ static StripeBufs *stripe_bufs(lpe_ctx *ctx, RigidDev *d) {
     return sb;
 }
 
+// The stripe count bound: k_pgs_stripes and k_pos_stripes run at the same
+// time with S / 2 workgroups each, one per CU (their LDS), and hand data
+// between workgroups with spin waits, so all S must be resident at once:
+// S <= the device's CU count (256 on an MI355X: STRIPES_MAX binds; a smaller
+// compute partition gets fewer, wider stripes).
+static int stripe_cap(lpe_ctx *ctx) {
+    static int cap = 0;
+    if (!cap) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
+            cus = 2;
+        cap = std::min(STRIPES_MAX, cus) & ~1;
+    }
+    return cap;
+}
+
 // stripes, groups, greedy colourings and the step layout on stream s
 static int stripe_launch(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     const int nb = d->nb;
@@ -3321,7 +3358,7 @@ static int stripe_launch(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     LPE_KERNEL(ctx, "k_stripe_pairs", k_stripe_pairs, dim3(rblk(d->cap_pairs)), dim3(RTPB), 0, s, d->counts,
                d->pairs, d->ccount, d->bodies, *sb);
     LPE_KERNEL(ctx, "k_stripe_setup", k_stripe_setup, dim3(1), dim3(SOLVE_TPB), sizeof(uint32_t) * 2 * ((nb + 31) / 32 + 1),
-               s, nb, d->counts, d->pairs, d->bodies, *sb, d->counts);
+               s, nb, d->counts, d->pairs, d->bodies, *sb, d->counts, stripe_cap(ctx));
     LPE_KERNEL(ctx, "k_group_lists", k_group_lists, dim3(SGROUPS), dim3(RTPB), 0, s, d->counts, d->counts, *sb);
     LPE_KERNEL(ctx, "k_group_colour", k_group_colour, dim3(SGROUPS), dim3(64), sizeof(unsigned long long) * (size_t)nb,
                s, d->counts, d->pairs, d->ccount, *sb);
@@ -3599,20 +3636,23 @@ static int rigid_lag_check(lpe_ctx *ctx, RigidDev *d, int slot, bool wait) {
     d->hpend[slot] = false;
     const int32_t *hc = d->hcr + 16 * slot;
     if (hc[7]) {
-        ctx->err = "rigid solver watchdog fired (a dataflow solve made no progress)";
+        ctx->err = watchdog_msg(hc[7]);
         return LPE_ERR_OVERFLOW;
     }
     if (hc[11]) {
         ctx->err = "narrowphase: a pair produced more contacts than a pair slot holds (MAXC)";
         return LPE_ERR_OVERFLOW;
     }
-    if (hc[6] || hc[0] > d->cap_pairs || hc[14] > d->cap_contacts) {
+    // (hc[15]: the pairs the detection found; k_compact zeroed hc[0] of an
+    // overflowing tick, which therefore solved nothing)
+    if (hc[6] || hc[15] > d->cap_pairs || hc[14] > d->cap_contacts) {
         d->lag = false;
         ctx->err = "rigid pair / contact buffers overflowed in a tick checked after the fact (the counts grew "
-                   "more than 4x within two ticks); reserve more with lpe_rigid_reserve";
+                   "more than 4x within two ticks; that tick's contacts were dropped); reserve more with "
+                   "lpe_rigid_reserve";
         return LPE_ERR_OVERFLOW;
     }
-    d->last_np = hc[0];
+    d->last_np = hc[15];
     d->last_nc = hc[14];
     if (2 * hc[0] > d->cap_pairs) d->grow_pairs = std::max(d->grow_pairs, 4 * hc[0] + 1024);
     if (2 * hc[14] > d->cap_contacts) d->grow_contacts = std::max(d->grow_contacts, 4 * hc[14] + 4096);
@@ -3885,7 +3925,7 @@ extern "C" int lpe_rigid_download(lpe_ctx *ctx, lpe_body *bodies) {
         LPE_HIP(ctx, hipMemcpyAsync(&fault, d->counts + 7, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
     LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
     if (fault) {
-        ctx->err = "rigid solver watchdog fired (a dataflow solve made no progress)";
+        ctx->err = watchdog_msg(fault);
         return LPE_ERR_OVERFLOW;
     }
     return d->lag ? rigid_lag_drain(ctx, d) : LPE_OK;       // (the ticks checked after the fact)

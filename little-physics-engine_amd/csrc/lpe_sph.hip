@@ -184,6 +184,52 @@ __device__ __forceinline__ void bucket_file(const FastKick &fk, uint32_t k, int 
     }
 }
 
+// x-slab decomposition (the slab section below): a slab rank's kick files
+// the particles bound for a neighbour -- kicked into, or past, the
+// SLAB_BAND cell columns along an edge -- as ghost records in that
+// neighbour's send buffer.
+static constexpr int SLAB_BAND = 2;                  // ghost cell columns each side of an edge
+static constexpr uint32_t KEY_DEAD = 0xFFFFFFFFu;    // a slot the sub-step drops (no bin)
+struct SlabKick {
+    int on;
+    const int32_t *edges;     // device [nranks + 1] edge cell columns
+    int rank, hasL, hasR;
+    float *sL, *sR;           // send buffers: HDR header floats, then wcap records of GREC floats
+    int wcap;
+    const int32_t *nslot;     // k_kick_drift: the P slots in use
+};
+// wave-aggregated append of this lane's particle to the send buffers of the
+// sides it is bound for (gx: its kicked bin's column); every lane of the
+// wave calls it
+__device__ __forceinline__ void slab_file(const SlabKick &sk, int cx0, int cx1, bool active, int gx, float px,
+                                          float py, float vx, float vy, float hx, float hy, float ms, int id,
+                                          int32_t *__restrict__ status) {
+    const int lane = lane_id();
+    for (int side = 0; side < 2; side++) {
+        const bool go = active && (side == 0 ? (sk.hasL && gx < cx0 + SLAB_BAND) : (sk.hasR && gx >= cx1 - SLAB_BAND));
+        const unsigned long long bal = __ballot(go);
+        if (!bal) continue;
+        float *buf = side == 0 ? sk.sL : sk.sR;
+        const int leader = __ffsll((long long)bal) - 1;
+        int b = 0;
+        if (lane == leader) b = atomicAdd((int *)buf, __popcll(bal));
+        b = __shfl(b, leader);
+        if (!go) continue;
+        const int k = b + __popcll(bal & ((1ull << lane) - 1ull));
+        if (k < sk.wcap) {
+            float4 *r = (float4 *)(buf + 4 + (size_t)k * 8);        // (HDR, GREC)
+            r[0] = make_float4(px, py, vx, vy);
+            r[1] = make_float4(hx, hy, ms, __int_as_float(id));
+        } else {
+            atomicOr(&status[ST_HALO_OVERFLOW], 1);
+        }
+    }
+}
+__device__ __forceinline__ void slab_cols(const SlabKick &sk, int &cx0, int &cx1) {
+    cx0 = sk.hasL ? sk.edges[sk.rank] : -(1 << 29);
+    cx1 = sk.hasR ? sk.edges[sk.rank + 1] : (1 << 29);
+}
+
 // The next sub-step's kick, fused into the forces pass of the current one
 // (sub-steps 1..numSubSteps-1 of a single-domain tick): the finished state
 // of a particle is exactly what k_kick_drift would read back from P.
@@ -196,6 +242,7 @@ struct KickNext {
     int32_t *count;
     float4 *bboxPart;                 // one partial per forces block
     FastKick fk;                      // the next sub-step's one-pass sort (fk.on)
+    SlabKick sk;                      // slab rank: the ghost records of the next sub-step
 };
 
 // k_kick_drift: velocityVerletHalf + bin key + histogram + bbox partials.
@@ -204,31 +251,46 @@ __global__ void __launch_bounds__(TPB)
 k_kick_drift(int n, float dt, float hdt, int first, int probe, float eps, float cs,
              int ox, int oy, int W, int H, PState P, KState K, uint32_t *__restrict__ key,
              int32_t *__restrict__ count, float4 *__restrict__ bboxPart,
-             int32_t *__restrict__ status, FastKick fk) {
+             int32_t *__restrict__ status, FastKick fk, SlabKick sk) {
     if (fk.on && blockIdx.x == 0 && threadIdx.x == 0) status[ST_NOT_INSERTED] = 0;   // (k_scan_rows adds)
     float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
     const int stride = gridDim.x * TPB;
     const int iters = (n + stride - 1) / stride;
+    // a slab rank: its P slots in use (sk.nslot), the dead ones (id -1) skipped
+    const int nn = sk.on ? min(*sk.nslot, n) : n;
+    int cx0 = 0, cx1 = 0;
+    if (sk.on) slab_cols(sk, cx0, cx1);
     for (int it = 0; it < iters; it++) {
         int i = it * stride + blockIdx.x * TPB + threadIdx.x;
-        bool active = i < n;
+        bool active = i < nn;
         uint32_t k = 0xFFFFFFFFu;
+        float px = 0.f, py = 0.f, hx = 0.f, hy = 0.f, vx = 0.f, vy = 0.f, ms = 0.f;
+        int id = -1, kx = 0;
+        if (active && sk.on) {
+            id = P.id[i];
+            if (id < 0) {
+                key[i] = KEY_DEAD;
+                active = false;
+            }
+        }
         if (active) {
-            float px, py;
             if (probe) {
                 px = P.x[i]; py = P.y[i];
             } else {
-                float hx, hy;
-                kick_one(P.x[i], P.y[i], P.vx[i], P.vy[i], first ? 0.f : P.ax[i], first ? 0.f : P.ay[i], dt, hdt,
+                vx = P.vx[i]; vy = P.vy[i];
+                kick_one(P.x[i], P.y[i], vx, vy, first ? 0.f : P.ax[i], first ? 0.f : P.ay[i], dt, hdt,
                          px, py, hx, hy);
                 K.vhx[i] = hx; K.vhy[i] = hy;
             }
             K.x[i] = px; K.y[i] = py;
-            k = bin_key(px, py, eps, cs, ox, oy, W, H, status);
+            int ky;
+            k = bin_key(px, py, eps, cs, ox, oy, W, H, status, &kx, &ky);
             key[i] = k;
             mnx = fminf(mnx, px); mxx = fmaxf(mxx, px);
             mny = fminf(mny, py); mxy = fmaxf(mxy, py);
+            if (sk.on) ms = P.m[i];
         }
+        if (sk.on) slab_file(sk, cx0, cx1, active, kx + ox, px, py, vx, vy, hx, hy, ms, id, status);
         int len; bool st;
         const int first = wave_runs(k, active, &len, &st);
         if (fk.on && fk.bucket) {
@@ -280,6 +342,20 @@ __device__ __forceinline__ GridParams grid_from_bbox(float minX, float maxX, flo
     return g;
 }
 
+// The sub-step's over-full reference cells (more than GPU_MAX_PER_CELL = 64,
+// fluid.hpp:56), listed by the scan as absolute (cell x, cell y): in the
+// reference cell-capacity mode a particle takes the literal capped walk only
+// if one of its 3x3 cells is listed (ref_cap_near), so a sub-step with none
+// costs the mode one uniform load per particle.  [0] = count (beyond
+// OVL_CAP: every particle checks its cells' counts, ref_cap_slow), then
+// pairs.  Two lists alternate by scan (the scan clears the next one).
+static constexpr int OVL_CAP = 1024;
+static constexpr int OVL_WORDS = 2 + 2 * OVL_CAP;
+__device__ __forceinline__ void ovl_append(int32_t *__restrict__ ovl, int gx, int gy) {
+    const int e = atomicAdd(&ovl[0], 1);
+    if (e < OVL_CAP) { ovl[2 + 2 * e] = gx; ovl[3 + 2 * e] = gy; }
+}
+
 // ---------------------------------------------------------------------------
 // scan
 __device__ __forceinline__ int wave_incl_scan(int v) {
@@ -306,8 +382,10 @@ __device__ __forceinline__ int block_excl_scan(int v, int *total) {
 }
 
 __global__ void __launch_bounds__(TPB)
-k_scan_reduce(int C, const int32_t *__restrict__ cnt, int32_t *__restrict__ bsum, int32_t *__restrict__ status) {
+k_scan_reduce(int C, const int32_t *__restrict__ cnt, int32_t *__restrict__ bsum, int32_t *__restrict__ status,
+              int32_t *__restrict__ ovl, int32_t *__restrict__ ovlNext) {
     if (status && blockIdx.x == 0 && threadIdx.x == 0) status[ST_NOT_INSERTED] = 0;   // (fused scan)
+    if (ovl && blockIdx.x == 0 && threadIdx.x == 0) { ovl[0] = 0; ovlNext[0] = 0; }  // (k_scan_final appends)
     int base = blockIdx.x * SCAN_ELEMS;
     int s = 0;
     for (int k = 0; k < 4; k++) {
@@ -380,7 +458,7 @@ k_scan_final(int C, int W, int ox, int oy, int32_t *__restrict__ cnt,
              const int32_t *__restrict__ bsum, int32_t *__restrict__ start,
              int32_t *__restrict__ cursor, GridParams *__restrict__ gp,
              int32_t *__restrict__ status, int do_stats, int fused, const float4 *__restrict__ bboxPart,
-             int nparts, float gcs, const float4 *__restrict__ bbG) {
+             int nparts, float gcs, const float4 *__restrict__ bbG, int32_t *__restrict__ ovl) {
     __shared__ int s_max, s_out, s_over;
     if (threadIdx.x == 0) { s_max = 0; s_out = 0; s_over = 0; }
     GridParams g{};
@@ -456,7 +534,10 @@ k_scan_final(int C, int W, int ox, int oy, int32_t *__restrict__ cnt,
         bool in = gx >= g.gridMinX && gx < g.gridMinX + g.gridDimX &&
                   gy >= g.gridMinY && gy < g.gridMinY + g.gridDimY;
         if (in) atomicMax(&s_max, s); else atomicAdd(&s_out, s);
-        if (in && s > LPE_REF_MAX_PER_CELL) atomicAdd(&s_over, 1);
+        if (in && s > LPE_REF_MAX_PER_CELL) {
+            atomicAdd(&s_over, 1);
+            if (ovl) ovl_append(ovl, gx, gy);
+        }
     }
     int tot;
     int ex = block_excl_scan(s, &tot) + prefix;
@@ -480,7 +561,8 @@ k_scatter(int n, const uint32_t *__restrict__ key, const int32_t *__restrict__ i
           int32_t *__restrict__ tmpOld, const int32_t *__restrict__ nptr) {
     int i = blockIdx.x * TPB + threadIdx.x;
     bool active = i < (nptr ? *nptr : n);
-    uint32_t k = active ? key[i] : 0xFFFFFFFFu;
+    uint32_t k = active ? key[i] : KEY_DEAD;
+    active = active && k != KEY_DEAD;          // (slab rank: a dropped slot)
     int len; bool st;
     int first = wave_runs(k, active, &len, &st);
     int base = 0;
@@ -502,8 +584,8 @@ __global__ void __launch_bounds__(TPB)
 k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restrict__ start,
                const int32_t *__restrict__ tmpId, const int32_t *__restrict__ tmpOld,
                PState P, KState K, PState S, float4 *__restrict__ nbA, float2 *__restrict__ nbB,
-               int probe, const int32_t *__restrict__ nptr, int32_t *__restrict__ src,
-               int32_t *__restrict__ refInv, int W, int32_t *__restrict__ clearCnt) {
+               int probe, const int32_t *__restrict__ nptr, int32_t *__restrict__ refInv, int W,
+               int32_t *__restrict__ clearCnt) {
     int s = blockIdx.x * TPB + threadIdx.x;
     if (s >= (nptr ? *nptr : n)) return;
     int o = tmpOld[s];
@@ -521,7 +603,6 @@ k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restric
     S.id[d] = myid;
     if (refInv) refInv[myid] = d;         // reference cell-capacity mode: id -> sorted slot
     if (!probe) { S.vhx[d] = K.vhx[o]; S.vhy[d] = K.vhy[o]; }
-    if (src) src[d] = o;          // slab decomposition: sorted slot -> P slot (ghosts: >= the owned count)
     if (clearCnt) clearCnt[k] = 0;  // (k_scan_rows leaves the counts for the next kick to find zeroed)
 }
 
@@ -532,13 +613,15 @@ k_rank_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restric
 // rank.  Reads of P are coalesced; the writes land near o (a sub-step moves
 // few particles to another bin).
 __global__ void __launch_bounds__(TPB)
-k_bucket_permute(int n, const uint32_t *__restrict__ key, const int32_t *__restrict__ start,
-                 const int32_t *__restrict__ bucket, const int32_t *__restrict__ tmpId, PState P, KState K, PState S,
-                 float4 *__restrict__ nbA, float2 *__restrict__ nbB, int32_t *__restrict__ refInv, int W,
-                 int32_t *__restrict__ clearCnt, int32_t *__restrict__ status) {
+k_bucket_permute(int n, const int32_t *__restrict__ nptr, const uint32_t *__restrict__ key,
+                 const int32_t *__restrict__ start, const int32_t *__restrict__ bucket,
+                 const int32_t *__restrict__ tmpId, PState P, KState K, PState S, float4 *__restrict__ nbA,
+                 float2 *__restrict__ nbB, int32_t *__restrict__ refInv, int W, int32_t *__restrict__ clearCnt,
+                 int32_t *__restrict__ status) {
     const int o = blockIdx.x * TPB + threadIdx.x;
-    if (o >= n) return;
+    if (o >= (nptr ? *nptr : n)) return;      // (slab rank: its own slots and the received ghosts)
     const uint32_t k = key[o];
+    if (k == KEY_DEAD) return;                 // (slab rank: a slot the previous sub-step dropped)
     const int myid = P.id[o];
     const int b = start[k], nk = start[k + 1] - b;
     const int4 *bk = (const int4 *)(bucket + (size_t)k * BKT_CAP);
@@ -582,10 +665,12 @@ k_scan_rows(int W, int H, int ox, int oy, float eps, const int32_t *__restrict__
             int32_t *__restrict__ cursor, const int32_t *__restrict__ rowtot, int32_t *__restrict__ rowtotNext,
             GridParams *__restrict__ gp, int32_t *__restrict__ status,
             const float4 *__restrict__ bboxPart, int nparts, float gcs, const int32_t *__restrict__ ovf,
-            int ovfcap, int32_t *__restrict__ ovfNext, int32_t *__restrict__ tmpId) {
+            int ovfcap, int32_t *__restrict__ ovfNext, int32_t *__restrict__ tmpId, int32_t *__restrict__ ovl,
+            int32_t *__restrict__ ovlNext, const float4 *__restrict__ bbG, int32_t *__restrict__ ntot, SlabKick sk) {
     const int r = (int)blockIdx.x;
     if (threadIdx.x == 0) rowtotNext[r] = 0;
     if (ovfNext && r == 0 && threadIdx.x == 0) ovfNext[0] = 0;
+    if (ovlNext && r == 0 && threadIdx.x == 0) ovlNext[0] = 0;    // (the next scan's over-cap list)
     const int novf = ovf ? min(ovf[0], ovfcap) : 0;      // (in flight with the loads below)
     // everything the block needs is loaded up front (one round trip): the
     // row's first SR_CELLS cells, the row totals below it, the bbox partials
@@ -598,10 +683,14 @@ k_scan_rows(int W, int H, int ox, int oy, float eps, const int32_t *__restrict__
     int pre = 0;
     for (int q = (int)threadIdx.x; q < r; q += TPB) pre += rowtot[q];     // (rows below the active ones hold 0)
     float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
-    for (int p = threadIdx.x; p < nparts; p += TPB) {
-        const float4 b = bboxPart[p];
-        mnx = fminf(mnx, b.x); mxx = fmaxf(mxx, b.y);
-        mny = fminf(mny, b.z); mxy = fmaxf(mxy, b.w);
+    if (bbG) {                              // slab rank: every rank's particles (k_ghost_unpack)
+        if (threadIdx.x == 0) { const float4 b = *bbG; mnx = b.x; mxx = b.y; mny = b.z; mxy = b.w; }
+    } else {
+        for (int p = threadIdx.x; p < nparts; p += TPB) {
+            const float4 b = bboxPart[p];
+            mnx = fminf(mnx, b.x); mxx = fmaxf(mxx, b.y);
+            mny = fminf(mny, b.z); mxy = fmaxf(mxy, b.w);
+        }
     }
     for (int off = 32; off > 0; off >>= 1) {
         pre += __shfl_xor(pre, off);
@@ -636,6 +725,9 @@ k_scan_rows(int W, int H, int ox, int oy, float eps, const int32_t *__restrict__
     if (r == ry0 && threadIdx.x == 0) *gp = g;
     const int gy = r + oy;
     const bool rowIn = gy >= g.gridMinY && gy < g.gridMinY + g.gridDimY;
+    // a slab rank's stats cover its own columns (the ghosts' are its neighbours')
+    int ocx0 = -(1 << 29), ocx1 = 1 << 29;
+    if (sk.on) slab_cols(sk, ocx0, ocx1);
     int tmax = 0, tout = 0, tover = 0;                 // this thread's cells' stats (reduced once at the end)
     for (int c0 = 0; c0 < W; c0 += TPB) {
         const int c = c0 + (int)threadIdx.x;
@@ -654,8 +746,13 @@ k_scan_rows(int W, int H, int ox, int oy, float eps, const int32_t *__restrict__
             // metal:224-226): those particles are "not inserted"
             const int gx = c + ox;
             const bool in = rowIn && gx >= g.gridMinX && gx < g.gridMinX + g.gridDimX;
-            if (in) tmax = max(tmax, sum); else tout += sum;
-            if (in && sum > LPE_REF_MAX_PER_CELL) tover++;
+            const bool mine = gx >= ocx0 && gx < ocx1;
+            if (!mine) {
+            } else if (in) tmax = max(tmax, sum); else tout += sum;
+            if (in && mine && sum > LPE_REF_MAX_PER_CELL) {
+                tover++;
+                if (ovl) ovl_append(ovl, gx, gy);
+            }
         }
         int tot;
         int ex = block_excl_scan(sum, &tot) + pre;
@@ -666,7 +763,10 @@ k_scan_rows(int W, int H, int ox, int oy, float eps, const int32_t *__restrict__
         }
         pre += tot;
     }
-    if (r == ry1 && threadIdx.x == 0) start[(size_t)(r + 1) * W * 4] = pre;   // end of the last active bin
+    if (r == ry1 && threadIdx.x == 0) {
+        start[(size_t)(r + 1) * W * 4] = pre;   // end of the last active bin
+        if (ntot) *ntot = pre;                  // (slab rank: the sorted slots of the sub-step)
+    }
     for (int off = 32; off > 0; off >>= 1) {
         tmax = max(tmax, __shfl_xor(tmax, off));
         tout += __shfl_xor(tout, off);
@@ -795,6 +895,7 @@ __device__ __forceinline__ void walk_neighbours(float xi, float yi, float eps, f
 static constexpr int NXCD = 8;
 __host__ __device__ __forceinline__ int xcd_grid(int nb) { return ((nb + NXCD - 1) / NXCD) * NXCD; }
 __device__ __forceinline__ int xcd_block(int nb) {
+    if ((int)blockIdx.x >= xcd_grid(nb)) return -1;   // (a grid sized for more blocks than are live)
     int per = (nb + NXCD - 1) / NXCD;
     int lb = (int)(blockIdx.x % NXCD) * per + (int)(blockIdx.x / NXCD);
     return lb < nb ? lb : -1;
@@ -851,41 +952,80 @@ __device__ __forceinline__ bool ref_cap_slow(float xi, float yi, float eps, cons
     return over;
 }
 
-// the reference's neighbour loop over its grid buffer: f(slot, id) for every
-// value read that is < n, in the reference's order (metal:272-291)
-template <class F>
+// ref_cap_slow through the scan's over-cap list (ovl_append): gx, gy = the
+// particle's absolute cell (its bin's, k_rank_permute's nbA.w)
+__device__ __forceinline__ bool ref_cap_near(const int32_t *__restrict__ ovl, int gx, int gy, float xi, float yi,
+                                             float eps, const GridParams &g, int W, int ox, int oy,
+                                             const int32_t *__restrict__ start) {
+    const int n = __builtin_amdgcn_readfirstlane(ovl[0]);
+    if (n == 0) return false;
+    if (n > OVL_CAP) return ref_cap_slow(xi, yi, eps, g, W, ox, oy, start);
+    bool near = false;
+    for (int k = 0; k < n; k++) {
+        const int cx = ovl[2 + 2 * k], cy = ovl[3 + 2 * k];
+        near |= abs(gx - cx) <= 1 && abs(gy - cy) <= 1;
+    }
+    return near;
+}
+
+// The reference's neighbour loop over its grid buffer (metal:272-291), in
+// its order: for each of the 3x3 cells c (row-major, inside the reference
+// grid) the words k < count(c) at flat position 65 c + 1 + k.  Words k < 64
+// are the cell's first min(count, 64) members -- in canonical insertion
+// order that is the contiguous slot range start(c) .. start(c) + min - 1,
+// walked U records at a time; past 64 (an over-full cell) the loop reads on
+// into the following cells' words: a count (read as an id), the next cell's
+// first members, zeros of the memset buffer.  ld(slot) loads a record,
+// f(slot, rec) consumes it, for every value read that is < n.
+template <int U, class L, class F>
 __device__ void ref_cap_walk(float xi, float yi, float eps, const GridParams &g, int W, int ox, int oy,
                              const int32_t *__restrict__ start, const int32_t *__restrict__ sid,
-                             const int32_t *__restrict__ refInv, int n, int32_t *__restrict__ status, F f) {
+                             const int32_t *__restrict__ refInv, int n, int32_t *__restrict__ status, L ld, F f) {
     constexpr int CI = LPE_REF_MAX_PER_CELL + 1;
     const int cellX = (int)floorf((xi + eps) / g.cellSize) - g.gridMinX;
     const int cellY = (int)floorf((yi + eps) / g.cellSize) - g.gridMinY;
     const long C = (long)g.gridDimX * g.gridDimY;
+    // the bin base of reference cell (cx, cy) of the flat index
+    auto base = [&](int cx, int cy) { return (((cy + g.gridMinY - oy) * W) + (cx + g.gridMinX - ox)) << 2; };
     for (int ny = -1; ny <= 1; ny++)
         for (int nx = -1; nx <= 1; nx++) {
             const int cx = cellX + nx, cy = cellY + ny;
             if (cx < 0 || cx >= g.gridDimX || cy < 0 || cy >= g.gridDimY) continue;
-            const int c = cy * g.gridDimX + cx;
-            const int b0 = ref_cell_base(c, g, W, ox, oy);
-            const int count = start[b0 + 4] - start[b0];
-            for (int k = 0; k < count; k++) {
-                const long pos = (long)CI * c + 1 + k;
-                const long cc = pos / CI;
-                const int j = (int)(pos - cc * CI);
-                int slot = -1, id;
-                if (cc >= C) {                            // past the buffer: undefined
+            const int b0 = base(cx, cy);
+            const int s0 = start[b0], count = start[b0 + 4] - s0;
+            const int m = min(count, LPE_REF_MAX_PER_CELL);
+            for (int k = 0; k < m; k += U) {
+                decltype(ld(0)) r[U];
+#pragma unroll
+                for (int j = 0; j < U; j++) r[j] = ld(s0 + min(k + j, m - 1));
+#pragma unroll
+                for (int j = 0; j < U; j++)
+                    if (k + j < m) f(s0 + k + j, r[j]);
+            }
+            if (count <= LPE_REF_MAX_PER_CELL) continue;
+            // past the cell's 64 slots: words 65 (c + 1) + j of the cells after it
+            long cc = (long)cy * g.gridDimX + cx + 1;
+            int j = 0, ccx = cx + 1, ccy = cy, bb = 0, bcnt = 0;
+            bool have = false;
+            for (int k = CI - 1; k < count; k++) {
+                int slot = -1, id = 0;
+                if (cc >= C) {                                 // past the buffer: undefined
                     atomicOr(&status[ST_REF_UB], 1);
-                    id = 0;
                 } else {
-                    const int bb = ref_cell_base((int)cc, g, W, ox, oy);
-                    const int cnt = start[bb + 4] - start[bb];
-                    if (j == 0) id = cnt;                              // the next cell's count
-                    else if (j - 1 < min(cnt, LPE_REF_MAX_PER_CELL)) { slot = start[bb] + (j - 1); id = sid[slot]; }
-                    else id = 0;                                        // memset slot
+                    if (!have) {
+                        if (ccx >= g.gridDimX) { ccx = 0; ccy++; }
+                        bb = base(ccx, ccy);
+                        bcnt = start[bb + 4] - start[bb];
+                        have = true;
+                    }
+                    if (j == 0) id = bcnt;                                   // the next cell's count
+                    else if (j - 1 < min(bcnt, LPE_REF_MAX_PER_CELL)) { slot = start[bb] + (j - 1); id = sid[slot]; }
+                    // else 0: the memset buffer
                 }
+                if (++j == CI) { j = 0; cc++; ccx++; have = false; }
                 if (id >= n) continue;
                 if (slot < 0) slot = refInv[id];
-                f(slot, id);
+                f(slot, ld(slot));
             }
         }
 }
@@ -1089,14 +1229,16 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
           const int32_t *__restrict__ start, const float4 *__restrict__ nbA, float2 *__restrict__ nbB,
           float *__restrict__ rho, float *__restrict__ pr, uint4 *__restrict__ nlist,
           int32_t *__restrict__ ncount, int32_t *__restrict__ status, const int32_t *__restrict__ sid,
-          const int32_t *__restrict__ refInv) {
+          const int32_t *__restrict__ refInv, const int32_t *__restrict__ ovl) {
     __shared__ float4 lrec[HCAP + 4];                     // + 4: the span walk reads up to 3 past a span
     __shared__ int lbnd[HBND];
     __shared__ uint4 lnl[NL ? HB : 1];                    // per thread: the current group of 8 offsets
 #ifdef LPE_DENSITY_PLAIN      // (A/B variant: plain block order, as the forces pass)
     const int lb = (int)blockIdx.x < (n + HB - 1) / HB ? (int)blockIdx.x : -1;
 #else
-    const int lb = xcd_block((n + HB - 1) / HB);
+    // (a slab rank's grid is sized by its slot capacity: the XCD runs are laid
+    // out over the slots in use, so every XCD gets its share)
+    const int lb = xcd_block(((nptr ? min(*nptr, n) : n) + HB - 1) / HB);
 #endif
     if (lb < 0) return;                                   // whole block idle
     const int nn = nptr ? *nptr : n;
@@ -1159,9 +1301,11 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
         cnt++;
     };
     // reference cell-capacity mode, an over-full cell in reach: the
-    // reference's literal loop (no neighbour list; the forces pass walks the
-    // same way)
-    const bool slow = live && refInv && ref_cap_slow(xi, yi, eps, g, W, ox, oy, start);
+    // reference's literal loop (the list in its order; past the list's
+    // capacity the forces pass walks the same way)
+    const bool slow = live && refInv &&
+                      ref_cap_near(ovl, ox + (int)((__float_as_int(me.w) >> 2) & 0x7fff), cyp, xi, yi, eps, g, W, ox,
+                                   oy, start);
     if (hd.ok) {
         // one span per cell row (hood_spans), the non-empty ones first; four
         // candidates per trip, trip counts wave-uniform: unmasked trips up to
@@ -1216,9 +1360,13 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
                            });
     }
     if (slow) {
-        ref_cap_walk(xi, yi, eps, g, W, ox, oy, start, sid, refInv, nn, status,
-                     [&](int k, int) { (void)term(nbA[k], true); });
-        cnt = NLIST_CAP + 1;
+        // (the neighbour list in the literal order, repeats included: the
+        // forces pass then sums exactly what the reference's loop visits)
+        ref_cap_walk<4>(xi, yi, eps, g, W, ox, oy, start, sid, refInv, nn, status,
+                        [&](int k) { return nbA[k]; },
+                        [&](int k, const float4 &o) {
+                            if (term(o, true) && NL && k != s) emit(k - s, k - s >= -32768 && k - s <= 32767);
+                        });
     }
     if (!live) return;
     if (NL) {
@@ -1465,16 +1613,14 @@ k_density_plan(int n, const int32_t *__restrict__ nptr, float eps, int W, int H,
 
 struct SphStepParams {
     const int32_t *nptr;      // slab decomposition: device slot count (owned + ghosts), else null
-    const int32_t *oldSlot;   // slab decomposition: the P slot of each sorted slot (tmpOld), else null;
-    int nown;                 //   P slots >= nown are ghosts (neighbours only).  Owned particles are
-                              //   written back to their own P slot: P keeps its order on a rank
-    float *orho, *opr;        // slab decomposition: rho / p of the owned particles in P order
+    SlabKick own;             // slab decomposition (own.on): the edges that decide which slots are owned
     int nstride;              // neighbour-list stride (allocated slots)
     int n, W, H, ox, oy;
     float h, eps, dt, hdt;
     float viscosity, minDist, minDens;
     int diag;                 // count diagnostics into status (lpe_sph_diag)
     const int32_t *refInv;    // reference cell-capacity mode: id -> slot (else null)
+    const int32_t *ovl;       //   and the sub-step's over-cap cells (ovl_append)
     int nblk, chunk;          // forces pass: logical blocks, blocks per XCD run (0: plain order)
     int32_t *mergePre;        // sub-step 0 after a prelaunch: its stats to merge into status (else null)
 };
@@ -1541,13 +1687,22 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     // block); lanes past the last slot and ghost slots only join the barriers
     const int s = s0 + threadIdx.x;
     bool live = s < s1;
-    int out = s;                              // P slot written
-    if (live && sp.oldSlot) {                 // ghosts are neighbours only
-        out = sp.oldSlot[s];
-        if (out >= sp.nown) live = false;
-    }
+    const int out = s;                        // P slot written (P is kept in the sorted order)
     const int sl = live ? s : s0;
     const float4 meA = nbA[sl], meB = nbB[sl];
+    int ocx0 = 0, ocx1 = 0;
+    if (sp.own.on) {
+        // a slab rank owns the slots whose bin column lies in its slab; the
+        // others are neighbours only, and their slots end here (dead: no
+        // bin in the next hash, id -1 for the next tick's kick)
+        slab_cols(sp.own, ocx0, ocx1);
+        const int gx = sp.ox + ((__float_as_int(meA.w) >> 2) & 0x7fff);
+        if (live && !(gx >= ocx0 && gx < ocx1)) {
+            live = false;
+            P.id[s] = -1;
+            if (kn.on) kn.key[s] = KEY_DEAD;
+        }
+    }
     const float xi = meA.x, yi = meA.y;
     const float vxi = meB.x, vyi = meB.y;
     const float rhoi = meB.z;
@@ -1696,11 +1851,16 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         if (cnt > NLIST_CAP) atomicAdd(&status[ST_NL_OVERFLOW], 1);
     }
     if (!live) {
-    } else if (sp.refInv && ref_cap_slow(xi, yi, sp.eps, g, sp.W, sp.ox, sp.oy, start)) {
-        // reference cell-capacity mode: the reference's literal loop
-        // (metal:345-351; nbrID == globalID is skipped)
-        ref_cap_walk(xi, yi, sp.eps, g, sp.W, sp.ox, sp.oy, start, S.id, sp.refInv, sp.n, status,
-                     [&](int k, int) { if (k != s) pair(nbA[k], nbB[k]); });
+    } else if (cnt > NLIST_CAP && sp.refInv &&
+               ref_cap_near(sp.ovl, sp.ox + (int)((__float_as_int(meA.w) >> 2) & 0x7fff),
+                            sp.oy + (int)((unsigned)__float_as_int(meA.w) >> 17), xi, yi, sp.eps, g, sp.W, sp.ox,
+                            sp.oy, start)) {
+        // reference cell-capacity mode, the literal loop's neighbours past the
+        // list's capacity: the loop itself (metal:345-351; nbrID == globalID
+        // is skipped)
+        ref_cap_walk<4>(xi, yi, sp.eps, g, sp.W, sp.ox, sp.oy, start, S.id, sp.refInv, sp.n, status,
+                        [&](int k) { return FRec{nbA[k], nbB[k]}; },
+                        [&](int k, const FRec &o) { if (k != s) pair(o.a, o.b); });
     } else if (cnt <= NLIST_CAP) {
         // the density pass's list: the r^2 < h^2 neighbours in canonical
         // order as slot offsets, so the heavy pair math runs only on real
@@ -1826,7 +1986,6 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         }
         P.vx[out] = st.vx; P.vy[out] = st.vy;
         P.m[out] = st.mass; P.id[out] = S.id[s];
-        if (sp.orho) { sp.orho[out] = rhoi; sp.opr[out] = pi; }
     }
     if (kn.on) {            // the next sub-step's k_kick_drift for this particle (block-uniform)
         float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
@@ -1841,17 +2000,19 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
             if (lb == 0 && threadIdx.x == 0) status[ST_NOT_INSERTED] = 0;   // (k_scan_rows adds)
             rowBase = (__float_as_int(nbA[s0].w) >> 17) - 3;
         }
+        float px = 0.f, py = 0.f, hx = 0.f, hy = 0.f;
+        int kx = 0;
         if (live) {
-            float px, py, hx, hy;
             kick_one(st.x, st.y, st.vx, st.vy, st.ax, st.ay, kn.dt, kn.hdt, px, py, hx, hy);
             kn.kvhx[out] = hx; kn.kvhy[out] = hy;
             kn.kx[out] = px; kn.ky[out] = py;
-            int kx;
             k = bin_key(px, py, kn.eps, kn.cs, kn.ox, kn.oy, kn.W, kn.H, status, &kx, &ky);
             kn.key[out] = k;
             mnx = mxx = px;
             mny = mxy = py;
         }
+        if (kn.sk.on)                                  // (the whole wave: ballots)
+            slab_file(kn.sk, ocx0, ocx1, live, kx + kn.ox, px, py, st.vx, st.vy, hx, hy, st.mass, S.id[sl], status);
         int len; bool stt;
         const int first = wave_runs(k, live, &len, &stt);
         if (kn.fk.on && kn.fk.bucket) {
@@ -1891,56 +2052,67 @@ extern "C" int lpe_ftrace(int on, unsigned long long *host, int n) {
 #endif
 
 // ---------------------------------------------------------------------------
-// x-slab decomposition.  A rank owns the particles of the
-// slab [x0, x1) (the first/last slab extend to -inf/+inf).  Per sub-step:
-//   kick owned -> all-reduce the bbox (MIN of minX, minY, -maxX, -maxY: the
-//   reference grid is the global one) -> ghosts: owned particles within D of
-//   a slab edge go to that neighbour with their global id (so the canonical
-//   in-bin order, and every sum, is the single-domain one) -> sort owned +
-//   ghosts -> density -> forces/finish/coupling on owned slots only,
-//   compacted back to P.
-// Deep halo: an owned particle is at most `drift` = D - 2h outside its slab
-// (checked, ST_HALO_DRIFT), so its neighbours lie within h + drift of the
-// edge and theirs within 2h + drift = D: every ghost the forces pass reads
-// has all its own neighbours present, and its density, computed locally in
-// the canonical order, is bit-identical to its owner's.  One neighbour
-// exchange per sub-step, no second exchange of ghost densities.
-// Once per tick: the rigid accumulators are all-reduced (SUM) before the
-// write-back, then particles that left the slab migrate to the neighbour.
-// ST_HALO_OVERFLOW flags exchange buffers that overflowed.
-static constexpr int GREC = 6;    // floats per ghost record: x, y, vx, vy, m, id
-static constexpr int MREC = 8;    // floats per migrant: x, y, vx, vy, m, id, rho, p
-static constexpr int HDR = 4;     // header floats of an exchange buffer ([0]: count, int)
+// x-slab decomposition.  Rank r owns the particles whose
+// reference-cell column gx = floor((x + eps) / cs) -- the column of their
+// grid bin -- lies in [cx0, cx1) = [edges[r], edges[r + 1]) (cell columns;
+// the first and last slab are open-ended), judged anew from the kicked
+// position at every sub-step.  Per sub-step:
+//   kick (k_kick_drift, or the previous forces pass): every particle the rank
+//     owned is kicked and hashed; those within SLAB_BAND columns of an edge,
+//     or past it, are also filed as ghost records for that neighbour
+//     (kicked position, velocity, half-step velocity, mass, global id:
+//     everything a particle carries between sub-steps);
+//   k_bbox_reduce: the rank's bbox record; transport exchange: the ghost
+//     records with both neighbours, and every rank's bbox record (the
+//     reference grid is the global one: the "not inserted" rule, the stats);
+//   k_ghost_unpack: the received ghosts after the rank's own slots (keys,
+//     histogram, bucket: the single-domain one-pass hash), the global bbox;
+//   k_scan_rows + k_bucket_permute: every local particle in canonical order
+//     (ascending global id inside a bin: every sum is the single domain's,
+//     bit for bit);
+//   density over all local slots; forces, finish, coupling and the next kick
+//     on the owned slots only.  A slot is owned iff its bin's column lies in
+//     [cx0, cx1): a ghost that crossed an edge is adopted by the rank it
+//     crossed into, and the sender marks the particle's slot dead (id = -1,
+//     key KEY_DEAD) -- ownership moves inside the sub-step, with no
+//     migration pass and no host synchronisation.
+// Why SLAB_BAND = 2 columns: an owned particle's neighbours lie in its 3 x 3
+// cells (columns cx0 - 1 .. cx1), theirs in columns cx0 - 2 .. cx1 + 1, all
+// present locally, so every ghost density the forces pass reads is computed
+// from its owner's neighbours in its owner's order.  A particle kicked more
+// than a slab away would be owned by no rank: the receiver's check
+// (ST_HALO_DRIFT) fails the step loudly.  Once per tick the rigid
+// accumulators are all-reduced (exact int64 limbs); every `rebalance` ticks
+// the inner edges move a column towards equal counts (k_slab_hist ->
+// all-reduce -> k_slab_rebalance, identically on every rank).
+static constexpr int GREC = 8;    // floats per ghost record: x, y, vx, vy, vhx, vhy, m, id
+static constexpr int HDR = 4;     // header floats of a wire buffer ([0]: record count, int)
+static constexpr int SLAB_OPEN = 1 << 29;   // the open ends' edge columns (-/+)
+static constexpr int SLAB_MINW = 8;         // narrowest slab (columns) the rebalancing leaves
 
 struct Shard {
-    float x0 = 0.f, x1 = 0.f, D = 0.f;
-    int hasL = 0, hasR = 0;
-    int cap = 0;                       // ghosts / migrants per side
-    // Every exchange moves the whole capacity-sized buffer (HDR + cap records):
-    // both ends know its size without a host round trip, so a spike of
-    // ghosts or migrants within the capacity costs nothing.  (Round 2 sized
-    // the wire by the receiver's request from the previous tick; a spike
-    // above the request was fatal and lost migrants.)
-    int32_t *ntot = nullptr;           // device: owned + ghosts of the sub-step
-    float *gsL = nullptr, *gsR = nullptr, *grL = nullptr, *grR = nullptr;
-    float *msL = nullptr, *msR = nullptr, *mrL = nullptr, *mrR = nullptr;
-    float4 *bb = nullptr;              // global bbox
-    int cap_slots = 0;                 // per-slot arrays below
-    int32_t *keep = nullptr, *kdst = nullptr;
-    int32_t *src = nullptr;            // the P slot of each sorted slot (k_rank_permute), for the forces pass
-    int32_t *obsum = nullptr;
-    float *orho = nullptr, *opr = nullptr;   // rho / p of the owned particles, P order
+    int nranks = 1, rank = 0, hasL = 0, hasR = 0;
+    int wcap = 0;                  // ghost records per direction (the wire: HDR + wcap records)
+    int rebalance = 0;             // ticks between edge moves (0: fixed edges)
+    long ticks = 0;
+    int n0 = 0;                    // particles uploaded
+    int mv = 0;                    // columns an inner edge may move from its initial one
+    std::vector<int> e0;           // initial edges (columns), host
+    int32_t *edges = nullptr;      // device [nranks + 1]: the current edges
+    int32_t *edges0 = nullptr;     // device [nranks + 1]: the initial ones (the rebalancing's range)
+    int32_t *cnt = nullptr;        // device: [0], [1] slots in use (sorted counts, by parity), [2] the
+                                   //   hash's input slots (own + received)
+    int cur = 0;                   // host: the parity of the committed slot count (P's layout)
+    float *sL = nullptr, *sR = nullptr, *rL = nullptr, *rR = nullptr;   // wire buffers
+    float4 *bbAll = nullptr;       // [nranks] every rank's bbox record (minX, minY, -maxX, -maxY)
+    float4 *bbG = nullptr;         // the global bbox (minX, maxX, minY, maxY)
+    float *hist = nullptr;         // rebalancing: owned particles per universe column
+    int hcol0 = 0, hcols = 0;
 };
 
-// (also clears the ghost send headers for the pack that follows: two
-// memset launches fewer per sub-step)
+// the rank's bbox record from the kick's block partials
 __global__ void __launch_bounds__(TPB)
-k_bbox_reduce(const float4 *__restrict__ part, int nparts, float4 *__restrict__ bb, float *__restrict__ sL,
-              float *__restrict__ sR) {
-    if (threadIdx.x < 4) {
-        if (sL) sL[threadIdx.x] = 0.0f;
-        if (sR) sR[threadIdx.x] = 0.0f;
-    }
+k_bbox_reduce(const float4 *__restrict__ part, int nparts, float4 *__restrict__ out) {
     float mnx = 1e30f, mxx = -1e30f, mny = 1e30f, mxy = -1e30f;
     for (int p = threadIdx.x; p < nparts; p += TPB) {
         float4 b = part[p];
@@ -1962,142 +2134,129 @@ k_bbox_reduce(const float4 *__restrict__ part, int nparts, float4 *__restrict__ 
             b.x = fminf(b.x, wb[w].x); b.y = fmaxf(b.y, wb[w].y);
             b.z = fminf(b.z, wb[w].z); b.w = fmaxf(b.w, wb[w].w);
         }
-        *bb = make_float4(b.x, b.z, -b.y, -b.w);
+        *out = make_float4(b.x, b.z, -b.y, -b.w);     // every component reduces by MIN
     }
 }
 
-__device__ __forceinline__ int *hdr(float *buf) { return (int *)buf; }
-__device__ __forceinline__ int rcount(const float *buf, int cap) {
-    return buf ? min(*(const int *)buf, cap) : 0;
-}
-
-__global__ void k_ghost_pack(int n, PState P, KState K, float x0, float x1, float D, float drift, int hasL,
-                             int hasR, float *__restrict__ sL, float *__restrict__ sR, int cap,
-                             int32_t *__restrict__ status) {
-    int i = blockIdx.x * TPB + threadIdx.x;
-    if (i >= n) return;
-    const float x = K.x[i];                      // the kicked position of this sub-step
-    if ((hasL && x < x0 - drift) || (hasR && x >= x1 + drift))
-        atomicOr(&status[ST_HALO_DRIFT], 1);       // beyond what the halo covers
-    for (int side = 0; side < 2; side++) {
-        const bool go = side == 0 ? (hasL && x < x0 + D) : (hasR && x >= x1 - D);
-        if (!go) continue;
-        float *buf = side == 0 ? sL : sR;
-        int k = atomicAdd(hdr(buf), 1);
-        if (k >= cap) { atomicOr(&status[ST_HALO_OVERFLOW], 1); continue; }
-        float *r = buf + HDR + (size_t)k * GREC;
-        r[0] = x; r[1] = K.y[i]; r[2] = P.vx[i]; r[3] = P.vy[i];
-        r[4] = P.m[i]; r[5] = __int_as_float(P.id[i]);
-    }
-}
-
-// ghosts -> P[nown ...] (left ones first), bin key + histogram (a header
-// count above the capacity: the sender flagged ST_HALO_OVERFLOW)
-__global__ void k_ghost_unpack(const float *__restrict__ rL, const float *__restrict__ rR, int cap,
-                               int nown, PState P, KState K, uint32_t *__restrict__ key,
-                               int32_t *__restrict__ count, float eps, float cs, int ox, int oy,
-                               int W, int H, int32_t *__restrict__ ntot, int32_t *__restrict__ status) {
+// The received ghosts -> slots [nslot, nslot + gL + gR) after the rank's own
+// (left ones first), with the kick's bin key, histogram, bucket filing and
+// row totals; the global bbox from every rank's record; the send headers
+// cleared for the next sub-step (the transport is done with them).
+__global__ void __launch_bounds__(TPB)
+k_ghost_unpack(const float *__restrict__ rL, const float *__restrict__ rR, int wcap, float *__restrict__ sL,
+               float *__restrict__ sR, const float4 *__restrict__ bbAll, int nranks, float4 *__restrict__ bbG,
+               const int32_t *__restrict__ nslot, int32_t *__restrict__ nin, int cap_slots, SlabKick sk, PState P,
+               KState K, uint32_t *__restrict__ key, int32_t *__restrict__ count, FastKick fk, float eps, float cs,
+               int ox, int oy, int W, int H, int32_t *__restrict__ status) {
     const int t = blockIdx.x * TPB + threadIdx.x;
-    const int gL = rcount(rL, cap), gR = rcount(rR, cap);
+    const int gL = rL ? min(*(const int *)rL, wcap) : 0, gR = rR ? min(*(const int *)rR, wcap) : 0;
+    const int base = *nslot;
+    const int room = max(cap_slots - base, 0);
     if (t == 0) {
-        *ntot = nown + gL + gR;
+        float4 b = bbAll[0];
+        for (int r = 1; r < nranks; r++) {
+            const float4 q = bbAll[r];
+            b.x = fminf(b.x, q.x); b.y = fminf(b.y, q.y); b.z = fminf(b.z, q.z); b.w = fminf(b.w, q.w);
+        }
+        *bbG = make_float4(b.x, -b.z, b.y, -b.w);
+        *nin = base + min(gL + gR, room);
+        if (gL + gR > room) atomicOr(&status[ST_SLAB_CAPACITY], 1);
         atomicMax(&status[ST_RX_GHOST_L], rL ? *(const int *)rL : 0);
         atomicMax(&status[ST_RX_GHOST_R], rR ? *(const int *)rR : 0);
+        if (sL) *(int *)sL = 0;
+        if (sR) *(int *)sR = 0;
     }
-    const float *src;
-    int slot;
-    if (t < cap) {
-        if (t >= gL) return;
-        src = rL + HDR + (size_t)t * GREC;
-        slot = nown + t;
-    } else {
-        const int k = t - cap;
-        if (k >= gR) return;
-        src = rR + HDR + (size_t)k * GREC;
-        slot = nown + gL + k;
+    const bool active = t < gL + gR && t < room;
+    uint32_t k = KEY_DEAD;
+    int id = 0, ky = 0;
+    if (active) {
+        const float4 *src = (const float4 *)(t < gL ? rL + HDR + (size_t)t * GREC : rR + HDR + (size_t)(t - gL) * GREC);
+        const float4 a = src[0], b = src[1];
+        const int slot = base + t;
+        id = __float_as_int(b.w);
+        K.x[slot] = a.x; K.y[slot] = a.y; P.vx[slot] = a.z; P.vy[slot] = a.w;
+        K.vhx[slot] = b.x; K.vhy[slot] = b.y; P.m[slot] = b.z; P.id[slot] = id;
+        int kx;
+        k = bin_key(a.x, a.y, eps, cs, ox, oy, W, H, status, &kx, &ky);
+        key[slot] = k;
+        // a ghost beyond this slab's far edge would be owned by no rank
+        int cx0, cx1;
+        slab_cols(sk, cx0, cx1);
+        const int gx = kx + ox;
+        if ((t < gL && gx >= cx1) || (t >= gL && gx < cx0)) atomicOr(&status[ST_HALO_DRIFT], 1);
     }
-    const float px = src[0], py = src[1];
-    K.x[slot] = px; K.y[slot] = py; P.vx[slot] = src[2]; P.vy[slot] = src[3];
-    K.vhx[slot] = src[2]; K.vhy[slot] = src[3];
-    P.m[slot] = src[4]; P.id[slot] = __float_as_int(src[5]);
-    float tx = (px + eps) / cs, ty = (py + eps) / cs;      // the key of k_kick_drift
-    int gx = (int)floorf(tx), gy = (int)floorf(ty);
-    int qx = (int)floorf(2.0f * tx) - 2 * gx;
-    int qy = (int)floorf(2.0f * ty) - 2 * gy;
-    int kx = gx - ox, ky = gy - oy;
-    if (kx < 0 || kx >= W || ky < 0 || ky >= H) {
-        atomicOr(&status[ST_CAP_OVERFLOW], 1);
-        kx = min(max(kx, 0), W - 1);
-        ky = min(max(ky, 0), H - 1);
+    int len; bool st;
+    const int first = wave_runs(k, active, &len, &st);
+    if (fk.on && fk.bucket) {
+        int b0 = 0;
+        if (st) b0 = atomicAdd(&count[k], len);
+        b0 = __shfl(b0, first);
+        if (active) bucket_file(fk, k, b0 + lane_id() - first, id, status);
+    } else if (st) {
+        atomicAdd(&count[k], len);
     }
-    uint32_t k = (((uint32_t)ky * (uint32_t)W + (uint32_t)kx) << 2) | (uint32_t)(qy * 2 + qx);
-    key[slot] = k;
-    atomicAdd(&count[k], 1);
+    if (fk.on && active) atomicAdd(&fk.rowtot[ky], 1);
 }
 
-// particles that left the slab -> migrant buffers; keep flags for the rest.
-// Migrants beyond the capacity stay owned here this tick and leave with a
-// later one (the owner of a particle never changes its result: ghosts carry
-// the global id; the drift check bounds how far outside it may stay)
-__global__ void k_mig_pack(int n, PState P, const float *__restrict__ rho, const float *__restrict__ pr,
-                           float x0, float x1, int hasL, int hasR, float *__restrict__ mL,
-                           float *__restrict__ mR, int32_t *__restrict__ keep, int cap) {
-    int i = blockIdx.x * TPB + threadIdx.x;
-    if (i >= n) return;
-    const float x = P.x[i];
-    float *buf = nullptr;
-    if (hasL && x < x0) buf = mL;
-    else if (hasR && x >= x1) buf = mR;
-    keep[i] = buf ? 0 : 1;
-    if (!buf) return;
-    int k = atomicAdd(hdr(buf), 1);
-    if (k >= cap) { keep[i] = 1; return; }
-    float *r = buf + HDR + (size_t)k * MREC;
-    r[0] = x; r[1] = P.y[i]; r[2] = P.vx[i]; r[3] = P.vy[i];
-    r[4] = P.m[i]; r[5] = __int_as_float(P.id[i]); r[6] = rho[i]; r[7] = pr[i];
+// Rebalancing: the owned particles per universe column (sorted order:
+// consecutive slots share columns, so one atomic per run of a wave)
+__global__ void __launch_bounds__(TPB)
+k_slab_hist(int n, const int32_t *__restrict__ nslot, const float *__restrict__ x, const int32_t *__restrict__ id,
+            float eps, float cs, int col0, int ncols, float *__restrict__ hist) {
+    const int i = blockIdx.x * TPB + threadIdx.x;
+    const bool active = i < *nslot && i < n && id[i] >= 0;
+    int c = 0;
+    if (active) c = min(max((int)floorf((x[i] + eps) / cs) - col0, 0), ncols - 1);
+    int len; bool st;
+    (void)wave_runs(active ? (uint32_t)c : KEY_DEAD, active, &len, &st);
+    if (st) atomicAdd(&hist[c], (float)len);
 }
 
-// the migrants received this tick (header word 0; beyond the capacity the
-// sender kept them): the most so far, a statistic
-__global__ void k_mig_received(const float *__restrict__ mrL, const float *__restrict__ mrR,
-                               int32_t *__restrict__ status) {
-    if (threadIdx.x != 0) return;
-    const int cL = mrL ? *(const int *)mrL : 0, cR = mrR ? *(const int *)mrR : 0;
-    status[ST_RX_MIG_L] = max(status[ST_RX_MIG_L], cL);
-    status[ST_RX_MIG_R] = max(status[ST_RX_MIG_R], cR);
-}
-
-// kept particles -> S[kdst[i]] (rho, p in S.vhx, S.vhy), then received
-// migrants after them; kdst is the exclusive scan of the keep flags (n + 1
-// entries), so particle i is kept iff kdst[i + 1] != kdst[i]
-__global__ void k_mig_compact(int n, const int32_t *__restrict__ kdst, PState P,
-                              const float *__restrict__ rho, const float *__restrict__ pr, PState S) {
-    int i = blockIdx.x * TPB + threadIdx.x;
-    if (i >= n) return;
-    const int d = kdst[i];
-    if (kdst[i + 1] == d) return;
-    S.x[d] = P.x[i]; S.y[d] = P.y[i]; S.vx[d] = P.vx[i]; S.vy[d] = P.vy[i];
-    S.m[d] = P.m[i]; S.id[d] = P.id[i]; S.vhx[d] = rho[i]; S.vhy[d] = pr[i];
-}
-__global__ void k_mig_append(const float *__restrict__ mrL, const float *__restrict__ mrR, int cap, int wL,
-                             int wR, int base, PState S) {
-    const int t = blockIdx.x * TPB + threadIdx.x;
-    const int nL = rcount(mrL, wL), nR = rcount(mrR, wR);
-    const float *src;
-    int d;
-    if (t < cap) {
-        if (t >= nL) return;
-        src = mrL + HDR + (size_t)t * MREC;
-        d = base + t;
-    } else {
-        const int k = t - cap;
-        if (k >= nR) return;
-        src = mrR + HDR + (size_t)k * MREC;
-        d = base + nL + k;
+// One block: the inner edges move one column towards equal counts (the
+// all-reduced histogram is the same on every rank, so are the edges), inside
+// [edges0 - mv, edges0 + mv] and at least SLAB_MINW columns apart; a
+// neighbourhood within 1 % of the mean count (or half the edge column's
+// count) stays put.  Clears the histogram for the next time.
+__global__ void __launch_bounds__(TPB)
+k_slab_rebalance(float *__restrict__ hist, int ncols, int col0, int32_t *__restrict__ edges,
+                 const int32_t *__restrict__ edges0, int nranks, int mv) {
+    __shared__ float wsum[TPB / 64];
+    __shared__ float s_tot;
+    auto block_sum = [&](float v) {
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+        __syncthreads();
+        if (lane_id() == 0) wsum[threadIdx.x >> 6] = v;
+        __syncthreads();
+        float tot = 0.f;
+        for (int w = 0; w < TPB / 64; w++) tot += wsum[w];
+        return tot;
+    };
+    float part = 0.f;
+    for (int c = threadIdx.x; c < ncols; c += TPB) part += hist[c];
+    const float total = block_sum(part);
+    if (threadIdx.x == 0) s_tot = total;
+    for (int j = 1; j < nranks; j++) {
+        const int e = edges[j];
+        float lp = 0.f;
+        for (int c = threadIdx.x; c < min(e - col0, ncols); c += TPB) lp += hist[c];
+        const float left = block_sum(lp);
+        if (threadIdx.x == 0) {
+            const float target = s_tot * (float)j / (float)nranks;
+            const float colc = (e - col0 >= 0 && e - col0 < ncols) ? hist[e - col0] : 0.f;
+            const float tol = fmaxf(0.01f * s_tot / (float)nranks, 0.5f * colc);
+            int ne = e;
+            if (left < target - tol) ne = e + 1;
+            else if (left > target + tol) ne = e - 1;
+            ne = min(max(ne, edges0[j] - mv), edges0[j] + mv);
+            if (j > 1) ne = max(ne, edges[j - 1] + SLAB_MINW);
+            if (j + 1 < nranks) ne = min(ne, edges[j + 1] - SLAB_MINW);
+            edges[j] = ne;
+        }
+        __syncthreads();
     }
-    S.x[d] = src[0]; S.y[d] = src[1]; S.vx[d] = src[2]; S.vy[d] = src[3];
-    S.m[d] = src[4]; S.id[d] = __float_as_int(src[5]); S.vhx[d] = src[6]; S.vhy[d] = src[7];
+    for (int c = threadIdx.x; c < ncols; c += TPB) hist[c] = 0.f;
 }
+
 
 // ---------------------------------------------------------------------------
 // rigid binning (once per tick)
@@ -2233,6 +2392,28 @@ __global__ void k_unpermute(int n, const int32_t *__restrict__ id, int nf, Field
     for (int k = 0; k < nf; k++) f.dst[k][d] = f.src[k][i];
 }
 
+// download of a slab rank's owned particles (P slots with an id), in no
+// particular order: x, y, vx, vy, rho, p and the id to staging arrays (ids
+// null: only their count)
+__global__ void k_slab_gather_owned(int n, const int32_t *__restrict__ nslot, PState P,
+                                    const float *__restrict__ rho, const float *__restrict__ pr, Fields6 f,
+                                    int32_t *__restrict__ ids, int32_t *__restrict__ cnt) {
+    const int i = blockIdx.x * TPB + threadIdx.x;
+    const bool live = i < n && i < *nslot && P.id[i] >= 0;
+    const unsigned long long m = __ballot(live);
+    if (!m) return;
+    const int lane = lane_id(), leader = __ffsll((long long)m) - 1;
+    int b = 0;
+    if (lane == leader) b = atomicAdd(cnt, __popcll(m));
+    if (!ids) return;
+    b = __shfl(b, leader);
+    if (!live) return;
+    const int d = b + __popcll(m & ((1ull << lane) - 1ull));
+    f.dst[0][d] = P.x[i]; f.dst[1][d] = P.y[i]; f.dst[2][d] = P.vx[i]; f.dst[3][d] = P.vy[i];
+    f.dst[4][d] = rho[i]; f.dst[5][d] = pr[i];
+    ids[d] = P.id[i];
+}
+
 
 }  // namespace lpe
 
@@ -2289,19 +2470,9 @@ static void pstate_free(PState &p) {
     p = PState();
 }
 
-static void shard_free_slots(Shard *h) {
-    void *ptrs[] = {h->keep, h->kdst, h->src, h->obsum, h->orho, h->opr};
-    for (void *p : ptrs) if (p) (void)hipFree(p);
-    h->keep = h->kdst = h->src = h->obsum = nullptr;
-    h->orho = h->opr = nullptr;
-    h->cap_slots = 0;
-}
-
 static void shard_free(Shard *h) {
     if (!h) return;
-    shard_free_slots(h);
-    void *ptrs[] = {h->ntot, h->gsL, h->gsR, h->grL, h->grR,
-                    h->msL, h->msR, h->mrL, h->mrR, h->bb};
+    void *ptrs[] = {h->edges, h->edges0, h->cnt, h->sL, h->sR, h->rL, h->rR, h->bbAll, h->bbG, h->hist};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     delete h;
 }
@@ -2313,7 +2484,7 @@ static void sph_free(SphDev &d) {
     d.shard = nullptr;
     pstate_free(d.P);
     pstate_free(d.S);
-    void *ptrs[] = {d.rho, d.pr, d.rhoN, d.prN, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.refInv, d.stage, d.count, d.start, d.cursor,
+    void *ptrs[] = {d.ovl, d.rho, d.pr, d.rhoN, d.prN, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.refInv, d.stage, d.count, d.start, d.cursor,
                     d.rowtot, d.bucket, d.bovf,
                     d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.raabb, d.accum, d.acq, d.rbinStart, d.rgrid, d.rmax,
                     d.rbinList, d.rbinCount, d.coupleBody, d.plans};
@@ -2488,12 +2659,13 @@ int lpe_sph_cover_box(lpe_ctx *ctx, double x0, double y0, double x1, double y1) 
     SphDev &d = ctx->sph;
     if (d.cs <= 0.f || (d.n <= 0 && !d.shard)) return LPE_OK;
     if (d.shard) {
-        // a slab rank only ever holds particles near its slab: owned ones at
-        // most a tick's drift outside it, ghosts within D of its edges
+        // a slab rank only ever holds particles near its slab: its edges move
+        // at most mv columns (rebalancing), its ghosts lie SLAB_BAND columns
+        // beyond them, a kicked particle a fraction of a column further
         const Shard &h = *d.shard;
-        const double m = 2.0 * h.D + 1.0;
-        if (h.hasL) x0 = std::max(x0, (double)h.x0 - m);
-        if (h.hasR) x1 = std::min(x1, (double)h.x1 + m);
+        const double m = (h.mv + SLAB_BAND + 4) * (double)d.cs;
+        if (h.hasL) x0 = std::max(x0, h.e0[h.rank] * (double)d.cs - m);
+        if (h.hasR) x1 = std::min(x1, h.e0[h.rank + 1] * (double)d.cs + m);
         if (x1 < x0) x1 = x0;
     }
     const double cs = d.cs;
@@ -2516,17 +2688,15 @@ static int pstate_alloc(lpe_ctx *ctx, PState &p, size_t N, bool with_a) {
     return LPE_OK;
 }
 
-static int shard_slots(const Shard &h);
-
-// slots per particle array: n (single domain); owned + ghost slots with room
-// for the owned count to grow through migration (slab decomposition)
+// slots per particle array: n (single domain); a slab rank's owned particles
+// and received ghosts, with room for its owned count to grow (slab_cap)
+static long slab_cap(const Shard &h, int n) { return 2L * n + 4L * h.wcap + 4096; }
 static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     SphDev &d = ctx->sph;
     Shard *h = d.shard;
     if (h) {
-        const long want = 2L * n + 4096 + shard_slots(*h);
+        const long want = slab_cap(*h, n);
         if (want > (1L << 30)) { ctx->err = "slab capacity too large"; return LPE_ERR_CAPACITY; }
-        if (n + shard_slots(*h) <= d.cap_n && d.P.x && h->cap_slots >= d.cap_n) return LPE_OK;
         n = (int)want;
     }
     if (n <= d.cap_n && d.P.x) return LPE_OK;
@@ -2562,17 +2732,10 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     // bbox partials: the kick's blocks, or the forces pass's when it kicks the next sub-step
     LPE_HIP(ctx, hipMalloc((void **)&d.bboxPart, sizeof(float4) * std::max<size_t>(MAX_KICK_BLOCKS, (N + HB - 1) / HB)));
     d.cap_n = n;
-    if (h) {
-        shard_free_slots(h);
-        const size_t S1 = N + 1;
-        int32_t **iv[] = {&h->keep, &h->kdst, &h->src};
-        for (int32_t **q : iv) LPE_HIP(ctx, hipMalloc((void **)q, sizeof(int32_t) * S1));
-        LPE_HIP(ctx, hipMalloc((void **)&h->obsum, sizeof(int32_t) * (S1 / SCAN_ELEMS + 2)));
-        LPE_HIP(ctx, hipMalloc((void **)&h->orho, sizeof(float) * S1));
-        LPE_HIP(ctx, hipMalloc((void **)&h->opr, sizeof(float) * S1));
-        // the scans zero their count arrays after use; they start zeroed
-        LPE_HIP(ctx, hipMemsetAsync(h->keep, 0, sizeof(int32_t) * S1, ctx->stream));
-        h->cap_slots = (int)N;
+    if (!d.ovl) {
+        LPE_HIP(ctx, hipMalloc((void **)&d.ovl, sizeof(int32_t) * 2 * OVL_WORDS));
+        LPE_HIP(ctx, hipMemsetAsync(d.ovl, 0, sizeof(int32_t) * 2 * OVL_WORDS, ctx->stream));
+        d.ovl_cur = d.ovl_pre = d.ovl;
     }
     if (!d.gp) {
         LPE_HIP(ctx, hipMalloc((void **)&d.gp, 2 * sizeof(GridParams)));
@@ -2597,6 +2760,15 @@ extern "C" int lpe_sph_upload(lpe_ctx *ctx, int n, const float *x, const float *
     int st = sph_alloc_particles(ctx, n);
     if (st) return st;
     d.n = n;
+    if (d.shard) {
+        // a slab rank's kernels run over its slot capacity, bounded by the
+        // device counts (Shard::cnt): n owned slots to start with
+        d.n = d.cap_n;
+        d.shard->n0 = n;
+        d.shard->cur = 0;
+        const int32_t c3[3] = {n, 0, 0};
+        LPE_HIP(ctx, hipMemcpy(d.shard->cnt, c3, sizeof(c3), hipMemcpyHostToDevice));
+    }
     d.rig_dirty = true;
     st = sph_plan_grid(ctx, x, y, n);
     if (st) return st;
@@ -2704,15 +2876,21 @@ static int sph_scan(lpe_ctx *ctx, int C, int32_t *cnt, int32_t *start, int32_t *
     // (the rigid bins too, as a plain prefix: no grid, no stats)
     static const bool nofuse = getenv("LPE_NO_SCAN_FUSION") != nullptr;
     const bool fused = nb <= 1024 && !nofuse;
+    int32_t *ovl = fluid ? d.ovl + (size_t)(d.ovlIdx & 1) * OVL_WORDS : nullptr;
+    int32_t *ovlNext = fluid ? d.ovl + (size_t)((d.ovlIdx + 1) & 1) * OVL_WORDS : nullptr;
     LPE_KERNEL(ctx, "k_scan_reduce", k_scan_reduce, dim3(nb), dim3(TPB), 0, s, C, cnt, bsum,
-               fused && fluid ? d.stat_cur : (int32_t *)nullptr);
+               fused && fluid ? d.stat_cur : (int32_t *)nullptr, ovl, ovlNext);
     if (!fused)
         LPE_KERNEL(ctx, "k_scan_blocks", k_scan_blocks, dim3(1), dim3(TPB), 0, s, nb, bsum, start + C, d.bboxPart,
                    nparts, d.cs, fluid ? d.gp_cur : (GridParams *)nullptr, d.stat_cur, bbG);
     LPE_KERNEL(ctx, "k_scan_final", k_scan_final, dim3(nb), dim3(TPB), 0, s, C, d.W, d.ox, d.oy, cnt, bsum,
                start, cursor, d.gp_cur, d.stat_cur, fluid ? 1 : 0, fused ? (fluid ? 1 : 2) : 0, (const float4 *)d.bboxPart,
-               nparts, d.cs, bbG);
+               nparts, d.cs, bbG, ovl);
     LPE_CHECK_LAUNCH(ctx, "scan");
+    if (fluid) {
+        d.ovl_cur = ovl;
+        d.ovlIdx++;
+    }
     return LPE_OK;
 }
 
@@ -2789,12 +2967,26 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
     return LPE_OK;
 }
 
-// The one-launch scan (k_scan_rows) on a single domain (LPE_NO_ROW_SCAN=1:
-// off): the kick that prepares it records the row totals (FastKick) into the
-// buffer of the scan's parity.
+// The one-launch scan (k_scan_rows; LPE_NO_ROW_SCAN=1: off on a single
+// domain, a slab rank always uses it): the kick that prepares it records the
+// row totals (FastKick) into the buffer of the scan's parity.
 static bool sph_rowscan_ok(const SphDev &d) {
     static const bool off = getenv("LPE_NO_ROW_SCAN") != nullptr;
-    return !off && !d.shard && d.rowtot && d.n > 0;
+    return (d.shard || !off) && d.rowtot && d.n > 0;
+}
+// the armed kick's FastKick again (the slab's ghost unpack files into the
+// same histogram, bucket and row totals), without re-arming
+static FastKick sph_fastkick_current(const SphDev &d) {
+    FastKick fk{};
+    if (!d.fast_armed) return fk;
+    fk.on = 1;
+    fk.rowtot = d.rowtot + (size_t)(d.fastIdx & 1) * d.cap_rows;
+    if (d.fast_bucket) {
+        fk.bucket = d.bucket;
+        fk.ovf = d.bovf + (size_t)(d.fastIdx & 1) * ovf_words(d);
+        fk.ovfcap = d.cap_n;
+    }
+    return fk;
 }
 static FastKick sph_fastkick(lpe_ctx *ctx, bool on) {
     SphDev &d = ctx->sph;
@@ -2820,22 +3012,14 @@ static FastKick sph_fastkick(lpe_ctx *ctx, bool on) {
     return fk;
 }
 
-// one grid hash: kick (unless probe) + histogram + scan + scatter + rank/permute
-// kicked > 0: the previous forces pass already kicked this sub-step (KickNext)
-// and left `kicked` bbox partials
-static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool probe, int kicked = 0) {
+// the sort after a kick: the scan (the reference grid and its stats), then
+// the permutation into the new sorted order.  Slab rank: bbG the global
+// bbox, ntot where the sorted count goes, nin the input slots (own +
+// received), sk its edges (the stats cover its own columns).
+static int sph_hash_sort(lpe_ctx *ctx, int kb, bool probe, const float4 *bbG, int32_t *ntot, const int32_t *nin,
+                         SlabKick sk) {
     SphDev &d = ctx->sph;
     hipStream_t s = ctx->stream;
-    int C = 4 * d.W * d.H;
-    int kb = kicked;
-    if (!kicked) {
-        kb = std::min(MAX_KICK_BLOCKS, std::max(1, nblk(d.n)));
-        const FastKick fk = sph_fastkick(ctx, !probe && sph_rowscan_ok(d));
-        LPE_KERNEL(ctx, "k_kick_drift", k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
-                   first ? 1 : 0, probe ? 1 : 0, d.cfg.gridConfig.gridEpsilon, d.cs, d.ox,
-                   d.oy, d.W, d.H, d.P, sph_kstate(d), d.key, d.count, d.bboxPart, d.stat_cur, fk);
-        LPE_CHECK_LAUNCH(ctx, "k_kick_drift");
-    }
     int32_t *clear = nullptr;
     const int par = (int)(d.fastIdx & 1);
     const bool bucket = d.fast_armed && d.fast_bucket && !probe;
@@ -2845,30 +3029,58 @@ static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool pr
                    d.cfg.gridConfig.gridEpsilon, d.count, d.start, d.cursor, d.rowtot + (size_t)par * d.cap_rows,
                    d.rowtot + (size_t)(1 - par) * d.cap_rows, d.gp_cur, d.stat_cur, (const float4 *)d.bboxPart, kb,
                    d.cs, bucket ? d.bovf + (size_t)par * ovf_words(d) : (const int32_t *)nullptr, d.cap_n,
-                   d.bovf ? d.bovf + (size_t)(1 - par) * ovf_words(d) : (int32_t *)nullptr, d.tmpId);
+                   d.bovf ? d.bovf + (size_t)(1 - par) * ovf_words(d) : (int32_t *)nullptr, d.tmpId,
+                   d.ovl + (size_t)(d.ovlIdx & 1) * OVL_WORDS, d.ovl + (size_t)((d.ovlIdx + 1) & 1) * OVL_WORDS,
+                   bbG, ntot, sk);
         LPE_CHECK_LAUNCH(ctx, "k_scan_rows");
+        d.ovl_cur = d.ovl + (size_t)(d.ovlIdx & 1) * OVL_WORDS;
+        d.ovlIdx++;
         d.fastIdx++;
         clear = d.count;
     } else {
-        int st = sph_scan(ctx, C, d.count, d.start, d.cursor, d.blocksum, kb, true);
+        if (sk.on) { ctx->err = "slab rank: the grid hash needs the row scan"; return LPE_ERR_STATE; }
+        int st = sph_scan(ctx, 4 * d.W * d.H, d.count, d.start, d.cursor, d.blocksum, kb, true);
         if (st) return st;
     }
     d.fast_armed = false;
     d.fast_bucket = false;
     if (bucket) {
-        LPE_KERNEL(ctx, "k_bucket_permute", k_bucket_permute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key,
+        LPE_KERNEL(ctx, "k_bucket_permute", k_bucket_permute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, nin, d.key,
                    d.start, d.bucket, d.tmpId, d.P, sph_kstate(d), d.S, d.nbA,
                    (float2 *)d.nbB, sph_ref_inv(d), d.W, clear, d.stat_cur);
         LPE_CHECK_LAUNCH(ctx, "hash");
         return LPE_OK;
     }
     LPE_KERNEL(ctx, "k_scatter", k_scatter, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.P.id, d.cursor,
-                       d.tmpId, d.tmpOld, (const int32_t *)nullptr);
+                       d.tmpId, d.tmpOld, nin);
     LPE_KERNEL(ctx, "k_rank_permute", k_rank_permute, dim3(nblk(d.n)), dim3(TPB), 0, s, d.n, d.key, d.start,
                        d.tmpId, d.tmpOld, d.P, sph_kstate(d), d.S, d.nbA, (float2 *)d.nbB, probe ? 1 : 0,
-                       (const int32_t *)nullptr, (int32_t *)nullptr, sph_ref_inv(d), d.W, clear);
+                       (const int32_t *)ntot, sph_ref_inv(d), d.W, clear);
     LPE_CHECK_LAUNCH(ctx, "hash");
     return LPE_OK;
+}
+
+
+static int sph_hash_slab(lpe_ctx *ctx, float subDt, float halfDt, bool first, int kicked);
+
+// one grid hash: kick (unless probe) + histogram + scan + scatter + rank/permute
+// kicked > 0: the previous forces pass already kicked this sub-step (KickNext)
+// and left `kicked` bbox partials.  A slab rank's hash (sph_hash_slab) adds
+// the exchange between the kick and the scan.
+static int sph_hash(lpe_ctx *ctx, float subDt, float halfDt, bool first, bool probe, int kicked = 0) {
+    SphDev &d = ctx->sph;
+    if (d.shard && !probe) return sph_hash_slab(ctx, subDt, halfDt, first, kicked);
+    hipStream_t s = ctx->stream;
+    int kb = kicked;
+    if (!kicked) {
+        kb = std::min(MAX_KICK_BLOCKS, std::max(1, nblk(d.n)));
+        const FastKick fk = sph_fastkick(ctx, !probe && sph_rowscan_ok(d));
+        LPE_KERNEL(ctx, "k_kick_drift", k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
+                   first ? 1 : 0, probe ? 1 : 0, d.cfg.gridConfig.gridEpsilon, d.cs, d.ox,
+                   d.oy, d.W, d.H, d.P, sph_kstate(d), d.key, d.count, d.bboxPart, d.stat_cur, fk, SlabKick{});
+        LPE_CHECK_LAUNCH(ctx, "k_kick_drift");
+    }
+    return sph_hash_sort(ctx, kb, probe, nullptr, nullptr, nullptr, SlabKick{});
 }
 
 // density over n slots (nptr: device count of the sharded sub-step); nl:
@@ -2909,116 +3121,100 @@ static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr, float *rho, flo
         LPE_KERNEL(ctx, "k_density", k_density<true>, dim3(xcd_grid(nblk(n, HB))), dim3(HB), 0, ctx->stream, n,
                    nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
                    c.restDensity, d.W, d.H, d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)d.nbB,
-                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d));
+                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d), d.ovl_cur);
     else
         LPE_KERNEL(ctx, "k_density", k_density<false>, dim3(xcd_grid(nblk(n, HB))), dim3(HB), 0, ctx->stream, n,
                    nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
                    c.restDensity, d.W, d.H, d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)d.nbB,
-                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d));
+                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d), d.ovl_cur);
     LPE_CHECK_LAUNCH(ctx, "k_density");
     return LPE_OK;
 }
 
 // ---- x-slab decomposition (host side of the kernels above) -------------
-static size_t ghost_bytes(int cap) { return sizeof(float) * (HDR + (size_t)cap * GREC); }
-static size_t mig_bytes(int cap) { return sizeof(float) * (HDR + (size_t)cap * MREC); }
-static int shard_slots(const Shard &h) { return 2 * h.cap; }   // ghost slots after the owned ones
-
-// the sharded grid hash: kick owned, global bbox, ghost exchange, sort owned + ghosts
-// (kicked > 0: the previous forces pass kicked this sub-step and left that
-// many bbox partials)
-static int sph_hash_shard(lpe_ctx *ctx, float subDt, float halfDt, bool first, int kicked = 0) {
-    SphDev &d = ctx->sph;
-    Shard &h = *d.shard;
-    Transport *tr = ctx->transport;
-    hipStream_t s = ctx->stream;
-    const int C = 4 * d.W * d.H;
-    const int kb = kicked ? kicked : std::min(MAX_KICK_BLOCKS, std::max(1, nblk(d.n)));
-    const float eps = d.cfg.gridConfig.gridEpsilon;
-    if (!kicked)
-        LPE_KERNEL(ctx, "k_kick_drift", k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
-                   first ? 1 : 0, 0, eps, d.cs, d.ox, d.oy, d.W, d.H, d.P, sph_kstate(d), d.key, d.count,
-                   d.bboxPart, d.status, FastKick{});
-    static_assert(HDR == 4, "k_bbox_reduce clears 4 header words");
-    LPE_KERNEL(ctx, "k_bbox_reduce", k_bbox_reduce, dim3(1), dim3(TPB), 0, s, d.bboxPart, kb, h.bb, h.gsL, h.gsR);
-    LPE_CHECK_LAUNCH(ctx, "shard kick");
-    int st = tr->allreduce(ctx, (float *)h.bb, 4, 1);
-    if (st) return st;
-    const float drift = h.D - 2.0f * d.cfg.gridConfig.smoothingLength;
-    LPE_KERNEL(ctx, "k_ghost_pack", k_ghost_pack, dim3(nblk1(d.n)), dim3(TPB), 0, s, d.n, d.P, sph_kstate(d), h.x0,
-               h.x1, h.D,
-               drift, h.hasL, h.hasR, h.gsL, h.gsR, h.cap, d.status);
-    LPE_CHECK_LAUNCH(ctx, "k_ghost_pack");
-    const size_t gb = ghost_bytes(h.cap);
-    st = tr->halo(ctx, h.hasL ? h.gsL : nullptr, h.hasR ? h.gsR : nullptr, h.hasL ? h.grL : nullptr,
-                  h.hasR ? h.grR : nullptr, gb, gb, gb, gb);
-    if (st) return st;
-    LPE_KERNEL(ctx, "k_ghost_unpack", k_ghost_unpack, dim3(nblk1(2 * h.cap)), dim3(TPB), 0, s,
-               h.hasL ? h.grL : (const float *)nullptr, h.hasR ? h.grR : (const float *)nullptr, h.cap, d.n,
-               d.P, sph_kstate(d), d.key, d.count, eps, d.cs, d.ox, d.oy, d.W, d.H, h.ntot, d.status);
-    LPE_CHECK_LAUNCH(ctx, "k_ghost_unpack");
-    st = sph_scan(ctx, C, d.count, d.start, d.cursor, d.blocksum, kb, true, h.bb);
-    if (st) return st;
-    const int ncap = d.n + shard_slots(h);
-    LPE_KERNEL(ctx, "k_scatter", k_scatter, dim3(nblk1(ncap)), dim3(TPB), 0, s, ncap, d.key, d.P.id, d.cursor,
-               d.tmpId, d.tmpOld, (const int32_t *)h.ntot);
-    LPE_KERNEL(ctx, "k_rank_permute", k_rank_permute, dim3(nblk1(ncap)), dim3(TPB), 0, s, ncap, d.key, d.start,
-               d.tmpId, d.tmpOld, d.P, sph_kstate(d), d.S, d.nbA, (float2 *)d.nbB, 0, (const int32_t *)h.ntot,
-               h.src, (int32_t *)nullptr, d.W, (int32_t *)nullptr);
-    LPE_CHECK_LAUNCH(ctx, "shard hash");
-    return LPE_OK;
+const int32_t *sph_slab_slots(lpe_ctx *ctx) {
+    const Shard *h = ctx->sph.shard;
+    return h ? h->cnt + h->cur : nullptr;
 }
 
-// once per tick: particles that left the slab go to the neighbour (one host
-// sync, for the new owned count)
-static int sph_migrate(lpe_ctx *ctx) {
+static size_t wire_bytes(int wcap) { return sizeof(float) * (HDR + (size_t)wcap * GREC); }
+
+// the slab rank's edges and send buffers for the kernels (nslot: the
+// committed slot count, P's layout)
+static SlabKick slab_kick(const SphDev &d) {
+    SlabKick sk{};
+    const Shard *h = d.shard;
+    if (!h) return sk;
+    sk.on = 1;
+    sk.edges = h->edges;
+    sk.rank = h->rank; sk.hasL = h->hasL; sk.hasR = h->hasR;
+    sk.sL = h->sL; sk.sR = h->sR; sk.wcap = h->wcap;
+    sk.nslot = h->cnt + h->cur;
+    return sk;
+}
+// where the hash in flight puts its sorted count (the density and forces
+// passes' slot count), or null on a single domain
+static const int32_t *slab_sorted(const SphDev &d) {
+    return d.shard ? d.shard->cnt + (1 - d.shard->cur) : nullptr;
+}
+
+// A slab rank's grid hash: the kick (unless the previous forces pass did it;
+// either files the ghost records), its bbox record, the exchange, the
+// received ghosts, then the sort of every local slot.  The sorted count goes
+// to cnt[1 - cur], committed (cur flipped) when the forces pass that reads
+// it is launched, so a voided prelaunch leaves P's count as it was.
+static int sph_hash_slab(lpe_ctx *ctx, float subDt, float halfDt, bool first, int kicked) {
     SphDev &d = ctx->sph;
     Shard &h = *d.shard;
     hipStream_t s = ctx->stream;
-    LPE_HIP(ctx, hipMemsetAsync(h.msL, 0, sizeof(float) * HDR, s));
-    LPE_HIP(ctx, hipMemsetAsync(h.msR, 0, sizeof(float) * HDR, s));
-    LPE_KERNEL(ctx, "k_mig_pack", k_mig_pack, dim3(nblk1(d.n)), dim3(TPB), 0, s, d.n, d.P, h.orho, h.opr, h.x0,
-               h.x1, h.hasL, h.hasR, h.msL, h.msR, h.keep, h.cap);
-    LPE_CHECK_LAUNCH(ctx, "k_mig_pack");
-    const size_t mb = mig_bytes(h.cap);
-    int st = ctx->transport->halo(ctx, h.hasL ? h.msL : nullptr, h.hasR ? h.msR : nullptr,
-                                  h.hasL ? h.mrL : nullptr, h.hasR ? h.mrR : nullptr, mb, mb, mb, mb);
+    if (!ctx->transport) {
+        ctx->err = "slab decomposition without a transport (lpe_mg_init_rccl / lpe_mg_loopback_run)";
+        return LPE_ERR_STATE;
+    }
+    if (!sph_rowscan_ok(d)) { ctx->err = "slab rank without particle arrays"; return LPE_ERR_STATE; }
+    const float eps = d.cfg.gridConfig.gridEpsilon;
+    int kb = kicked;
+    if (!kicked) {
+        kb = std::min(MAX_KICK_BLOCKS, std::max(1, nblk(d.n)));
+        const FastKick fk = sph_fastkick(ctx, true);
+        LPE_KERNEL(ctx, "k_kick_drift", k_kick_drift, dim3(kb), dim3(TPB), 0, s, d.n, subDt, halfDt,
+                   first ? 1 : 0, 0, eps, d.cs, d.ox, d.oy, d.W, d.H, d.P, sph_kstate(d), d.key, d.count,
+                   d.bboxPart, d.stat_cur, fk, slab_kick(d));
+        LPE_CHECK_LAUNCH(ctx, "k_kick_drift");
+    }
+    LPE_KERNEL(ctx, "k_bbox_reduce", k_bbox_reduce, dim3(1), dim3(TPB), 0, s, d.bboxPart, kb, h.bbAll + h.rank);
+    LPE_CHECK_LAUNCH(ctx, "k_bbox_reduce");
+    int st = ctx->transport->exchange(ctx, h.hasL ? h.sL : nullptr, h.hasR ? h.sR : nullptr,
+                                      h.hasL ? h.rL : nullptr, h.hasR ? h.rR : nullptr, wire_bytes(h.wcap), HDR, GREC,
+                                      h.bbAll);
     if (st) return st;
-    LPE_KERNEL(ctx, "k_mig_received", k_mig_received, dim3(1), dim3(64), 0, s, h.hasL ? h.mrL : (const float *)nullptr,
-               h.hasR ? h.mrR : (const float *)nullptr, d.status);
-    // the four headers: [0] migrants packed (beyond the capacity: kept)
-    int32_t hd4[4][HDR] = {};
-    float *hb[4] = {h.hasL ? h.msL : nullptr, h.hasR ? h.msR : nullptr, h.hasL ? h.mrL : nullptr,
-                    h.hasR ? h.mrR : nullptr};
-    for (int k = 0; k < 4; k++)
-        if (hb[k]) LPE_HIP(ctx, hipMemcpyAsync(hd4[k], hb[k], sizeof(int32_t) * HDR, hipMemcpyDeviceToHost, s));
-    LPE_HIP(ctx, hipStreamSynchronize(s));
-    int32_t cnt[4];
-    for (int k = 0; k < 4; k++) cnt[k] = std::min(hd4[k][0], h.cap);
-    const int kept = d.n - cnt[0] - cnt[1];
-    const int nn = kept + cnt[2] + cnt[3];
-    if (nn + shard_slots(h) > d.cap_n) {
-        ctx->err = "slab decomposition: owned particles exceed the rank's capacity";
-        return LPE_ERR_CAPACITY;
-    }
-    // (the scan leaves the keep flags zeroed; k_mig_pack writes all of them)
-    if (d.n > 0) {
-        st = sph_scan(ctx, d.n, h.keep, h.kdst, (int32_t *)d.key, h.obsum, 0, false);
-        if (st) return st;
-    }
-    LPE_KERNEL(ctx, "k_mig_compact", k_mig_compact, dim3(nblk1(d.n)), dim3(TPB), 0, s, d.n, h.kdst, d.P,
-               h.orho, h.opr, d.S);
-    LPE_KERNEL(ctx, "k_mig_append", k_mig_append, dim3(nblk1(2 * h.cap)), dim3(TPB), 0, s,
-               h.hasL ? h.mrL : (const float *)nullptr, h.hasR ? h.mrR : (const float *)nullptr, h.cap, cnt[2],
-               cnt[3], kept, d.S);
-    LPE_CHECK_LAUNCH(ctx, "migration");
-    const size_t B = sizeof(float) * (size_t)nn;
-    float *dstp[6] = {d.P.x, d.P.y, d.P.vx, d.P.vy, d.P.m, d.rho};
-    float *srcp[6] = {d.S.x, d.S.y, d.S.vx, d.S.vy, d.S.m, d.S.vhx};
-    for (int k = 0; k < 6; k++) LPE_HIP(ctx, hipMemcpyAsync(dstp[k], srcp[k], B, hipMemcpyDeviceToDevice, s));
-    LPE_HIP(ctx, hipMemcpyAsync(d.pr, d.S.vhy, B, hipMemcpyDeviceToDevice, s));
-    LPE_HIP(ctx, hipMemcpyAsync(d.P.id, d.S.id, sizeof(int32_t) * (size_t)nn, hipMemcpyDeviceToDevice, s));
-    d.n = nn;
+    LPE_KERNEL(ctx, "k_ghost_unpack", k_ghost_unpack, dim3(nblk1(2L * h.wcap)), dim3(TPB), 0, s,
+               h.hasL ? h.rL : (const float *)nullptr, h.hasR ? h.rR : (const float *)nullptr, h.wcap,
+               h.hasL ? h.sL : (float *)nullptr, h.hasR ? h.sR : (float *)nullptr, (const float4 *)h.bbAll, h.nranks,
+               h.bbG, (const int32_t *)(h.cnt + h.cur), h.cnt + 2, d.cap_n, slab_kick(d), d.P, sph_kstate(d), d.key,
+               d.count, sph_fastkick_current(d), eps, d.cs, d.ox, d.oy, d.W, d.H, d.stat_cur);
+    LPE_CHECK_LAUNCH(ctx, "k_ghost_unpack");
+    return sph_hash_sort(ctx, kb, false, h.bbG, h.cnt + (1 - h.cur), h.cnt + 2, slab_kick(d));
+}
+
+// Every `rebalance` ticks (after a fluid step): the owned particles per
+// column, all-reduced, and the inner edges moved a column towards equal
+// counts -- the same arithmetic on the same histogram on every rank.
+static int slab_rebalance(lpe_ctx *ctx) {
+    SphDev &d = ctx->sph;
+    Shard &h = *d.shard;
+    h.ticks++;
+    if (h.rebalance <= 0 || h.nranks < 2 || h.ticks % h.rebalance) return LPE_OK;
+    hipStream_t s = ctx->stream;
+    LPE_KERNEL(ctx, "k_slab_hist", k_slab_hist, dim3(nblk1(d.n)), dim3(TPB), 0, s, d.n,
+               (const int32_t *)(h.cnt + h.cur), (const float *)d.P.x, (const int32_t *)d.P.id,
+               d.cfg.gridConfig.gridEpsilon, d.cs, h.hcol0, h.hcols, h.hist);
+    LPE_CHECK_LAUNCH(ctx, "k_slab_hist");
+    int st = ctx->transport->allreduce(ctx, h.hist, h.hcols, 0);
+    if (st) return st;
+    LPE_KERNEL(ctx, "k_slab_rebalance", k_slab_rebalance, dim3(1), dim3(TPB), 0, s, h.hist, h.hcols, h.hcol0,
+               h.edges, (const int32_t *)h.edges0, h.nranks, h.mv);
+    LPE_CHECK_LAUNCH(ctx, "k_slab_rebalance");
     return LPE_OK;
 }
 
@@ -3026,15 +3222,16 @@ static int sph_migrate(lpe_ctx *ctx) {
 // of the NEXT tick read only the fluid state, which is final once this tick's
 // fluid boundary/gravity kernel has run; they are launched on a side stream
 // then, so they run while the rigid solvers (one CU each) run, and that
-// tick's lpe_sph_step starts at the forces (single domain; the slab path's
-// exchanges stay on the context stream).  The side stream is a plain one: a
+// tick's lpe_sph_step starts at the forces (a slab rank's sub-step 0
+// exchange runs on the side stream too, ordered after every exchange and
+// reduction of the tick on the context stream).  The side stream is a plain one: a
 // CU-masked queue (round 1 kept 16 CUs free for the solvers) cost a third of
 // the tick rate on MI355X (396 vs 554 ticks/s on the settled metric scene),
 // while the solvers start promptly without it.
 int sph_prelaunch(lpe_ctx *ctx, double dt_tick, const std::function<int(hipStream_t)> &first) {
     SphDev &d = ctx->sph;
     d.pre = false;
-    if (d.shard || d.n <= 0 || !d.P.x) return LPE_OK;
+    if (d.n <= 0 || !d.P.x) return LPE_OK;
     if (!d.pside) {
         LPE_HIP(ctx, hipStreamCreateWithFlags(&d.pside, hipStreamNonBlocking));
         LPE_HIP(ctx, hipEventCreateWithFlags(&d.preReady, hipEventDisableTiming));
@@ -3062,7 +3259,8 @@ int sph_prelaunch(lpe_ctx *ctx, double dt_tick, const std::function<int(hipStrea
     d.stat_cur = d.status + ST_COUNT;
     int st = hipMemsetAsync(d.stat_cur, 0, sizeof(int32_t) * ST_COUNT, d.pside) == hipSuccess ? LPE_OK : LPE_ERR_HIP;
     if (!st) st = sph_hash(ctx, subDt, halfDt, true, false);
-    if (!st) st = sph_density(ctx, d.n, nullptr, d.rhoN, d.prN);   // P-order rho / p stay the tick's
+    if (!st) st = sph_density(ctx, d.n, slab_sorted(d), d.rhoN, d.prN);   // P-order rho / p stay the tick's
+    d.ovl_pre = d.ovl_cur;
     ctx->stream = main;
     d.gp_cur = d.gp;
     d.stat_cur = d.status;
@@ -3095,8 +3293,9 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
     float halfDt = 0.5f * subDt;
     hipStream_t s = ctx->stream;
     // sub-step 0 up to the forces already launched (sph_prelaunch)?  One for
-    // another time step is discarded (it never touched P)
-    if (d.pre && (d.shard || d.pre_dt != dt_tick)) {
+    // another time step is discarded (it never touched P; on a slab rank every
+    // rank must discard it alike: it joined an exchange)
+    if (d.pre && d.pre_dt != dt_tick) {
         int st0 = sph_void_prelaunch(ctx);
         if (st0) return st0;
     }
@@ -3125,26 +3324,12 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
     sp.diag = d.diag;
     sp.refInv = sph_ref_inv(d);
     sp.nptr = nullptr;
-    sp.oldSlot = nullptr;
-    sp.nown = 0;
-    sp.orho = sp.opr = nullptr;
+    sp.own = slab_kick(d);            // (on a slab rank: the slots it owns)
     sp.nstride = d.cap_n;
     Shard *sh = d.shard;
     if (sh && !ctx->transport) {
         ctx->err = "slab decomposition without a transport (lpe_mg_init_rccl / lpe_mg_loopback_run)";
         return LPE_ERR_STATE;
-    }
-    if (sh && !(sh->D > 2.0f * c.gridConfig.smoothingLength)) {
-        ctx->err = "slab decomposition: the halo must exceed twice the smoothing length";
-        return LPE_ERR_ARG;
-    }
-    if (sh) {
-        sp.n = d.n + shard_slots(*sh);
-        sp.nptr = sh->ntot;
-        sp.oldSlot = sh->src;
-        sp.nown = d.n;
-        sp.orho = sh->orho;
-        sp.opr = sh->opr;
     }
     CoupleParams cp;
     sph_couple_params(d, cp);
@@ -3164,18 +3349,15 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
     const int fgrid = fchunk > 0 ? xcd_chunk_grid(fblocks, fchunk) : fblocks;
     int kicked = 0;
     for (int step = 0; step < c.numSubSteps; step++) {
-        if (sh) {
-            st = sph_hash_shard(ctx, subDt, halfDt, step == 0, kicked);
-            if (st) return st;
-            st = sph_density(ctx, sp.n, sh->ntot, d.rho, d.pr);
-        } else if (step == 0 && pre) {
+        if (step == 0 && pre) {
             st = LPE_OK;                              // waited for above
         } else {
             st = sph_hash(ctx, subDt, halfDt, step == 0, false, kicked);
             if (st) return st;
-            st = sph_density(ctx, d.n, nullptr, d.rho, d.pr);
+            st = sph_density(ctx, d.n, slab_sorted(d), d.rho, d.pr);
         }
         if (st) return st;
+        sp.nptr = slab_sorted(d);                     // (slab rank: the hash's sorted count)
         KickNext kn{};
         kn.on = fuse && step + 1 < c.numSubSteps;
         if (kn.on) {
@@ -3185,15 +3367,18 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
             kn.kx = K.x; kn.ky = K.y; kn.kvhx = K.vhx; kn.kvhy = K.vhy;
             kn.key = d.key; kn.count = d.count; kn.bboxPart = d.bboxPart;
             kn.fk = sph_fastkick(ctx, sph_rowscan_ok(d));
+            kn.sk = slab_kick(d);
         }
         kicked = kn.on ? fblocks : 0;
         sp.mergePre = (step == 0 && pre) ? d.status + ST_COUNT : nullptr;
+        sp.ovl = (step == 0 && pre) ? d.ovl_pre : d.ovl_cur;
         LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(fgrid), dim3(HB), 0, s, sp, cp,
                            (step == 0 && pre) ? d.gp + 1 : d.gp,
                            d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart, d.rbinList,
                            rbin_aabb(d),
                            d.acq, d.status, kn);
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
+        if (sh) sh->cur = 1 - sh->cur;               // P's slots are now the ones this pass wrote
         if (hook) {                                  // (lpe_world_tick: the rigid detection)
             st = hook(ctx, step);
             if (st) return st;
@@ -3216,7 +3401,7 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
                            d.acq, d.accum, c.dampingFactor, (const int32_t *)d.coupleBody, d.wb_bodies);
         LPE_CHECK_LAUNCH(ctx, "k_rigid_writeback");
     }
-    if (sh) return sph_migrate(ctx);
+    if (sh) return slab_rebalance(ctx);
     return LPE_OK;
 }
 
@@ -3261,17 +3446,21 @@ static int check_status(lpe_ctx *ctx) {
         return LPE_ERR_OVERFLOW;
     }
     if (status[ST_HALO_DRIFT]) {
-        ctx->err = "slab decomposition: a particle moved further outside its slab than halo - 2h allows "
-                   "(raise the halo of lpe_sph_set_slab)";
+        ctx->err = "slab decomposition: a particle was kicked past its neighbour's slab (it would belong to no "
+                   "rank; slabs must be wider than a sub-step's drift)";
         return LPE_ERR_OVERFLOW;
+    }
+    if (status[ST_SLAB_CAPACITY]) {
+        ctx->err = "slab decomposition: the rank's own and received particles outgrew its slots";
+        return LPE_ERR_CAPACITY;
     }
     if (status[ST_XACC_RANGE]) {
         ctx->err = "a rigid coupling force left the exact accumulator's range (|f| >= 2^64 or not finite)";
         return LPE_ERR_OVERFLOW;
     }
     if (status[ST_HALO_OVERFLOW]) {
-        ctx->err = "slab decomposition: more ghosts than ghost_cap within the halo of a slab edge (raise "
-                   "ghost_cap of lpe_sph_set_slab)";
+        ctx->err = "slab decomposition: more ghost records than wire_cap along a slab edge in a sub-step (raise "
+                   "wire_cap of lpe_sph_set_slab)";
         return LPE_ERR_OVERFLOW;
     }
     return LPE_OK;
@@ -3298,6 +3487,7 @@ extern "C" int lpe_sph_download_aux(lpe_ctx *ctx, float *vxHalf, float *vyHalf, 
                                     float *ay) {
     if (!ctx) return LPE_ERR_ARG;
     SphDev &d = ctx->sph;
+    if (d.shard) { ctx->err = "slab decomposition: use lpe_sph_download_owned"; return LPE_ERR_STATE; }
     if (d.n <= 0) return LPE_OK;
     const float *src[4] = {d.P.vhx, d.P.vhy, d.P.ax, d.P.ay};
     float *dst[4] = {vxHalf, vyHalf, ax, ay};
@@ -3345,8 +3535,23 @@ extern "C" int lpe_sph_get_stats(lpe_ctx *ctx, lpe_sph_stats *out) {
     out->refUndefined = status[ST_REF_UB];
     out->overCapCellsTotal = status[ST_OVER_CAP_TOTAL];
     out->maxCellOccupancyTotal = status[ST_MAX_OCC_TOTAL];
-    out->haloWire[0] = (d.shard && d.shard->hasL) ? d.shard->cap : 0;
-    out->haloWire[1] = (d.shard && d.shard->hasR) ? d.shard->cap : 0;
+    out->haloWire[0] = (d.shard && d.shard->hasL) ? d.shard->wcap : 0;
+    out->haloWire[1] = (d.shard && d.shard->hasR) ? d.shard->wcap : 0;
+    if (d.shard) {
+        Shard &h = *d.shard;
+        int32_t c2[2] = {0, 0};
+        LPE_HIP(ctx, hipMemsetAsync(h.cnt + 3, 0, sizeof(int32_t), ctx->stream));
+        LPE_KERNEL(ctx, "k_slab_gather_owned", k_slab_gather_owned, dim3(nblk1(d.n)), dim3(TPB), 0, ctx->stream,
+                   d.n, (const int32_t *)(h.cnt + h.cur), d.P, (const float *)d.rho, (const float *)d.pr, Fields6{},
+                   (int32_t *)nullptr, h.cnt + 3);
+        LPE_HIP(ctx, hipMemcpyAsync(&c2[0], h.cnt + 3, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+        LPE_HIP(ctx, hipMemcpyAsync(&c2[1], h.cnt + h.cur, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+        LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        out->slabOwned = c2[0];
+        out->slabSlots = c2[1];
+        out->ghostsIn[0] = status[ST_RX_GHOST_L];
+        out->ghostsIn[1] = status[ST_RX_GHOST_R];
+    }
     return LPE_OK;
 }
 
@@ -3370,12 +3575,14 @@ extern "C" int lpe_sph_diag(lpe_ctx *ctx, int on) {
     if (d.status) {
         LPE_HIP(ctx, hipMemsetAsync(d.status + ST_NL_OVERFLOW, 0, sizeof(int32_t) * 4, ctx->stream));
         LPE_HIP(ctx, hipMemsetAsync(d.status + ST_OVER_CAP_TOTAL, 0, sizeof(int32_t) * 2, ctx->stream));
+        LPE_HIP(ctx, hipMemsetAsync(d.status + ST_RX_GHOST_L, 0, sizeof(int32_t) * 2, ctx->stream));
     }
     return LPE_OK;
 }
 
 int lpe_sph_hash_current(lpe_ctx *ctx) {
     SphDev &d = ctx->sph;
+    if (d.shard) { ctx->err = "not on a slab rank (its slots hold ghosts)"; return LPE_ERR_STATE; }
     if (d.n <= 0) return LPE_OK;
     int st = sph_void_prelaunch(ctx);           // the probe's hash reuses the prelaunch's buffers
     if (st) return st;
@@ -3387,6 +3594,7 @@ int lpe_sph_hash_current(lpe_ctx *ctx) {
 extern "C" int lpe_sph_probe_cells(lpe_ctx *ctx, int32_t *cell_index, lpe_sph_stats *stats) {
     if (!ctx || !cell_index) return LPE_ERR_ARG;
     SphDev &d = ctx->sph;
+    if (d.shard) { ctx->err = "not on a slab rank (its slots hold ghosts)"; return LPE_ERR_STATE; }
     if (d.n <= 0) return LPE_OK;
     (void)hipSetDevice(ctx->device);
     int st = sph_void_prelaunch(ctx);           // the probe's hash reuses the prelaunch's buffers
@@ -3408,6 +3616,7 @@ extern "C" int lpe_sph_probe_cells(lpe_ctx *ctx, int32_t *cell_index, lpe_sph_st
 extern "C" int lpe_sph_probe_density(lpe_ctx *ctx, float *density, float *pressure) {
     if (!ctx) return LPE_ERR_ARG;
     SphDev &d = ctx->sph;
+    if (d.shard) { ctx->err = "not on a slab rank (its slots hold ghosts)"; return LPE_ERR_STATE; }
     if (d.n <= 0) return LPE_OK;
     (void)hipSetDevice(ctx->device);
     int st = sph_void_prelaunch(ctx);           // the probe's hash reuses the prelaunch's buffers
@@ -3428,42 +3637,97 @@ extern "C" int lpe_sph_probe_density(lpe_ctx *ctx, float *density, float *pressu
 }
 
 // ---- slab decomposition: configuration and owned-particle I/O -----------
-extern "C" int lpe_sph_set_slab(lpe_ctx *ctx, float x0, float x1, float halo, int has_left, int has_right,
-                                int ghost_cap) {
-    if (!ctx || ghost_cap < 1 || !(halo > 0.f) || (has_left && has_right && !(x1 > x0))) return LPE_ERR_ARG;
+extern "C" int lpe_sph_set_slab(lpe_ctx *ctx, int nranks, int rank, const float *edges, int wire_cap,
+                                int rebalance) {
+    if (!ctx || nranks < 1 || rank < 0 || rank >= nranks || !edges || wire_cap < 1 || rebalance < 0)
+        return LPE_ERR_ARG;
     (void)hipSetDevice(ctx->device);
     SphDev &d = ctx->sph;
     if (d.mode & LPE_SPH_MODE_REF_CELL_CAP) {
         ctx->err = "the reference cell-capacity mode is single-domain only (not on a slab rank)";
         return LPE_ERR_STATE;
     }
+    if (!d.cfg_set) {
+        ctx->err = "lpe_sph_set_slab: set the fluid config first (the edges are reference-cell columns)";
+        return LPE_ERR_STATE;
+    }
+    const float cs = ref_cell_size(d.cfg);
+    std::vector<int> e(nranks + 1);
+    e[0] = -SLAB_OPEN;
+    e[nranks] = SLAB_OPEN;
+    int minw = 1 << 20;
+    for (int j = 1; j < nranks; j++) {
+        const double q = (double)edges[j] / cs;
+        const double c = std::nearbyint(q);
+        if (!(std::fabs(q - c) < 1e-3) || std::fabs(c) > 1e8) {
+            ctx->err = "lpe_sph_set_slab: inner edges must lie on reference-cell boundaries (multiples of 2h)";
+            return LPE_ERR_ARG;
+        }
+        e[j] = (int)c;
+        if (j > 1) {
+            if (e[j] - e[j - 1] < SLAB_MINW) {
+                ctx->err = "lpe_sph_set_slab: inner slabs must be at least 8 reference cells wide";
+                return LPE_ERR_ARG;
+            }
+            minw = std::min(minw, e[j] - e[j - 1]);
+        }
+    }
     if (d.pside) LPE_HIP(ctx, hipStreamSynchronize(d.pside));
     d.pre = false;
     LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
     shard_free(d.shard);
     d.shard = nullptr;
-    d.cap_n = 0;                // the particle arrays are re-sized (owned + ghost slots) by the upload
+    d.cap_n = 0;                // the particle arrays are re-sized (slots for ghosts and growth) by the upload
     Shard *h = new Shard();
-    h->x0 = x0; h->x1 = x1; h->D = halo;
-    h->hasL = has_left ? 1 : 0; h->hasR = has_right ? 1 : 0;
-    h->cap = ghost_cap;
     d.shard = h;
-    LPE_HIP(ctx, hipMalloc((void **)&h->ntot, sizeof(int32_t)));
-    LPE_HIP(ctx, hipMalloc((void **)&h->bb, sizeof(float4)));
-    float **gb[] = {&h->gsL, &h->gsR, &h->grL, &h->grR};
-    for (float **q : gb) LPE_HIP(ctx, hipMalloc((void **)q, ghost_bytes(ghost_cap)));
-    float **mb[] = {&h->msL, &h->msR, &h->mrL, &h->mrR};
-    for (float **q : mb) LPE_HIP(ctx, hipMalloc((void **)q, mig_bytes(ghost_cap)));
-    float *all[] = {h->gsL, h->gsR, h->grL, h->grR, h->msL, h->msR, h->mrL, h->mrR};
-    for (float *q : all) LPE_HIP(ctx, hipMemsetAsync(q, 0, sizeof(float) * HDR, ctx->stream));
-    LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    h->nranks = nranks; h->rank = rank;
+    h->hasL = rank > 0 ? 1 : 0;
+    h->hasR = rank < nranks - 1 ? 1 : 0;
+    h->wcap = wire_cap;
+    h->rebalance = nranks > 1 ? rebalance : 0;
+    h->e0 = e;
+    h->mv = h->rebalance ? std::max(SLAB_MINW, std::min(minw / 4, 1024)) : 0;
+    const size_t E = sizeof(int32_t) * (size_t)(nranks + 1);
+    LPE_HIP(ctx, hipMalloc((void **)&h->edges, E));
+    LPE_HIP(ctx, hipMalloc((void **)&h->edges0, E));
+    LPE_HIP(ctx, hipMemcpy(h->edges, e.data(), E, hipMemcpyHostToDevice));
+    LPE_HIP(ctx, hipMemcpy(h->edges0, e.data(), E, hipMemcpyHostToDevice));
+    LPE_HIP(ctx, hipMalloc((void **)&h->cnt, sizeof(int32_t) * 4));
+    LPE_HIP(ctx, hipMemset(h->cnt, 0, sizeof(int32_t) * 4));
+    float **wb[] = {&h->sL, &h->sR, &h->rL, &h->rR};
+    for (float **q : wb) {
+        LPE_HIP(ctx, hipMalloc((void **)q, wire_bytes(wire_cap)));
+        LPE_HIP(ctx, hipMemset(*q, 0, sizeof(float) * HDR));
+    }
+    LPE_HIP(ctx, hipMalloc((void **)&h->bbAll, sizeof(float4) * (size_t)nranks));
+    LPE_HIP(ctx, hipMalloc((void **)&h->bbG, sizeof(float4)));
+    if (h->rebalance) {
+        h->hcol0 = e[1] - h->mv - 2;
+        h->hcols = e[nranks - 1] + h->mv + 2 - h->hcol0 + 1;
+        LPE_HIP(ctx, hipMalloc((void **)&h->hist, sizeof(float) * (size_t)h->hcols));
+        LPE_HIP(ctx, hipMemset(h->hist, 0, sizeof(float) * (size_t)h->hcols));
+    }
+    return LPE_OK;
+}
+
+extern "C" int lpe_sph_slab_info(lpe_ctx *ctx, int cap, int32_t *edges, int *nranks, int *move) {
+    if (!ctx || cap < 0) return LPE_ERR_ARG;
+    const Shard *h = ctx->sph.shard;
+    if (nranks) *nranks = h ? h->nranks : 0;
+    if (move) *move = h ? h->mv : 0;
+    if (!h) return LPE_OK;
+    if (edges && cap >= h->nranks + 1) {
+        LPE_HIP(ctx, hipMemcpyAsync(edges, h->edges, sizeof(int32_t) * (size_t)(h->nranks + 1),
+                                    hipMemcpyDeviceToHost, ctx->stream));
+        LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    }
     return LPE_OK;
 }
 
 extern "C" int lpe_sph_set_ids(lpe_ctx *ctx, int n, const int32_t *ids) {
     if (!ctx || n < 0 || (n > 0 && !ids)) return LPE_ERR_ARG;
     SphDev &d = ctx->sph;
-    if (n != d.n) return LPE_ERR_ARG;
+    if (n != (d.shard ? d.shard->n0 : d.n)) return LPE_ERR_ARG;
     if (n == 0) return LPE_OK;
     int st = sph_void_prelaunch(ctx);          // it sorted by the old ids
     if (st) return st;
@@ -3476,9 +3740,37 @@ extern "C" int lpe_sph_download_owned(lpe_ctx *ctx, int cap, float *x, float *y,
                                       float *density, float *pressure, int32_t *ids, int *n_out) {
     if (!ctx || !n_out || cap < 0) return LPE_ERR_ARG;
     SphDev &d = ctx->sph;
+    hipStream_t s = ctx->stream;
+    if (d.shard) {
+        // the owned slots (id >= 0) gathered into the staging arrays a pending
+        // prelaunch no longer needs (as sph_unpermute_download), ids to tmpOld
+        Shard &h = *d.shard;
+        *n_out = 0;
+        if (!d.P.x) return LPE_OK;
+        int st0 = sph_join_prelaunch(ctx);
+        if (st0) return st0;
+        LPE_HIP(ctx, hipMemsetAsync(h.cnt + 3, 0, sizeof(int32_t), s));
+        Fields6 f{};
+        float *stage[6] = {d.S.x, d.S.y, d.S.vx, d.S.vy, d.S.m, d.stage};
+        for (int k = 0; k < 6; k++) f.dst[k] = stage[k];
+        LPE_KERNEL(ctx, "k_slab_gather_owned", k_slab_gather_owned, dim3(nblk1(d.n)), dim3(TPB), 0, s, d.n,
+                   (const int32_t *)(h.cnt + h.cur), d.P, (const float *)d.rho, (const float *)d.pr, f, d.tmpOld,
+                   h.cnt + 3);
+        LPE_CHECK_LAUNCH(ctx, "k_slab_gather_owned");
+        int32_t m = 0;
+        LPE_HIP(ctx, hipMemcpyAsync(&m, h.cnt + 3, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        LPE_HIP(ctx, hipStreamSynchronize(s));
+        *n_out = m;
+        if (m > cap) return LPE_ERR_CAPACITY;
+        float *dst[6] = {x, y, vx, vy, density, pressure};
+        for (int k = 0; k < 6; k++)
+            if (dst[k] && m) LPE_HIP(ctx, hipMemcpyAsync(dst[k], stage[k], sizeof(float) * m, hipMemcpyDeviceToHost, s));
+        if (ids && m) LPE_HIP(ctx, hipMemcpyAsync(ids, d.tmpOld, sizeof(int32_t) * m, hipMemcpyDeviceToHost, s));
+        LPE_HIP(ctx, hipStreamSynchronize(s));
+        return check_status(ctx);
+    }
     *n_out = d.n;
     if (d.n > cap) return LPE_ERR_CAPACITY;
-    hipStream_t s = ctx->stream;
     int st0 = sph_join_prelaunch(ctx);
     if (st0) return st0;
     const size_t B = sizeof(float) * (size_t)d.n;

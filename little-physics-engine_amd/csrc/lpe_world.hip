@@ -77,9 +77,11 @@ __global__ void k_gather_rigids(int nr, const int32_t *__restrict__ coupleBody,
 // particles (no Sleep component, not Boundary): widen, update, narrow
 __global__ void k_fluid_boundary_gravity(int n, PState P, double m, double U, double damp,
                                          double maxSpeed, double g, double dt,
-                                         const int32_t *__restrict__ heavy_bodies, int heavy_fluid) {
+                                         const int32_t *__restrict__ heavy_bodies, int heavy_fluid,
+                                         const int32_t *__restrict__ nslot) {
     int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
+    if (nslot && (i >= *nslot || P.id[i] < 0)) return;     // (slab rank: slots in use, dropped ones skipped)
     double x = P.x[i], y = P.y[i], vx = P.vx[i], vy = P.vy[i];
     bool bounced = false;
     if (x < m) { x = m; vx = fabs(vx) * damp; bounced = true; }
@@ -236,10 +238,10 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
             st = lpe_rigid_integrate(ctx, 1 | 32, dt_state, dt_move);
         }
         if (st) return st;
-        const bool prelaunch = !serial && fluid && !d.shard;
+        const bool prelaunch = !serial && fluid;
         const bool fbg_side = prelaunch && d.n > 0 && d.P.x;
         auto fbg = [&](hipStream_t fs) {
-            LPE_KERNEL(ctx, "k_fluid_boundary_gravity", k_fluid_boundary_gravity, dim3(wblk(d.n)), dim3(256), 0, fs, d.n, d.P, rc.marginPixels * rc.metersPerPixel, rc.universeSize, rc.bounceDamping, rc.maxSpeed, rc.gravity, dt_state, rd->nb > 0 ? rd->counts + 5 : (const int32_t *)nullptr, d.fluid_heavy ? 1 : 0);
+            LPE_KERNEL(ctx, "k_fluid_boundary_gravity", k_fluid_boundary_gravity, dim3(wblk(d.n)), dim3(256), 0, fs, d.n, d.P, rc.marginPixels * rc.metersPerPixel, rc.universeSize, rc.bounceDamping, rc.maxSpeed, rc.gravity, dt_state, rd->nb > 0 ? rd->counts + 5 : (const int32_t *)nullptr, d.fluid_heavy ? 1 : 0, sph_slab_slots(ctx));
             return LPE_OK;
         };
         if (d.n > 0 && !fbg_side) {

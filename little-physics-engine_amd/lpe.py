@@ -75,10 +75,12 @@ class SphStats(C.Structure):
                 ("nlistOverflow", C.c_int32), ("rigidCandidates", C.c_int32), ("neighbours", C.c_int32),
                 ("stageFallback", C.c_int32), ("overCapCells", C.c_int32), ("refUndefined", C.c_int32),
                 ("overCapCellsTotal", C.c_int32), ("maxCellOccupancyTotal", C.c_int32),
-                ("haloWire", C.c_int32 * 2)]
+                ("haloWire", C.c_int32 * 2), ("slabOwned", C.c_int32), ("slabSlots", C.c_int32),
+                ("ghostsIn", C.c_int32 * 2)]
 
     def as_dict(self):
-        return {k: (list(getattr(self, k)) if k == "haloWire" else getattr(self, k)) for k, _ in self._fields_}
+        return {k: (list(getattr(self, k)) if k in ("haloWire", "ghostsIn") else getattr(self, k))
+                for k, _ in self._fields_}
 
 
 # numpy mirror of lpe_gpu_rigid / Systems::GPURigidBody (fluid.hpp:94-125), 200 B
@@ -197,13 +199,14 @@ class WorldConfig(C.Structure):
 SIGNATURES["lpe_world_set_coupling"] = ([C.c_void_p, C.c_int, C.c_void_p], C.c_int)
 SIGNATURES["lpe_world_tick"] = ([C.c_void_p, C.POINTER(WorldConfig), C.c_int], C.c_int)
 
-SIGNATURES["lpe_sph_set_slab"] = ([C.c_void_p, C.c_float, C.c_float, C.c_float, C.c_int, C.c_int, C.c_int],
-                                  C.c_int)
+SIGNATURES["lpe_sph_set_slab"] = ([C.c_void_p, C.c_int, C.c_int, _FP, C.c_int, C.c_int], C.c_int)
 SIGNATURES["lpe_sph_set_ids"] = ([C.c_void_p, C.c_int, _IP], C.c_int)
+SIGNATURES["lpe_sph_slab_info"] = ([C.c_void_p, C.c_int, _IP, _IP, _IP], C.c_int)
 SIGNATURES["lpe_sph_download_owned"] = ([C.c_void_p, C.c_int] + [_FP] * 6 + [_IP, _IP], C.c_int)
 SIGNATURES["lpe_sph_set_domain"] = ([C.c_void_p] + [C.c_double] * 4, C.c_int)
 SIGNATURES["lpe_mg_unique_id"] = ([C.c_char_p], C.c_int)
 SIGNATURES["lpe_mg_init_rccl"] = ([C.c_void_p, C.c_int, C.c_int, C.c_char_p], C.c_int)
+SIGNATURES["lpe_mg_info"] = ([C.c_void_p, _IP, _IP, _IP], C.c_int)
 HALO_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p,
                       C.c_size_t, C.c_void_p, C.c_size_t)
 REDF_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.POINTER(C.c_float), C.c_int, C.c_int)
@@ -412,9 +415,25 @@ class Context:
         self._chk(lib().lpe_sph_diag(self._h, int(on)), "lpe_sph_diag")
 
     # ---- x-slab decomposition --------------------------------------------
-    def sph_set_slab(self, x0, x1, halo, has_left, has_right, ghost_cap):
-        self._chk(lib().lpe_sph_set_slab(self._h, float(x0), float(x1), float(halo), int(has_left),
-                                         int(has_right), int(ghost_cap)), "lpe_sph_set_slab")
+    def sph_set_slab(self, nranks, rank, edges, wire_cap, rebalance=0):
+        """Slab `rank` of `nranks`: edges (nranks + 1 metres, inner ones on
+        reference-cell boundaries), wire_cap ghost records per direction and
+        sub-step, rebalance > 0: move the edges every that many fluid steps."""
+        e = np.ascontiguousarray(edges, np.float32)
+        assert len(e) == nranks + 1
+        self._slab_edges = e
+        self._chk(lib().lpe_sph_set_slab(self._h, int(nranks), int(rank), _fp(e), int(wire_cap), int(rebalance)),
+                  "lpe_sph_set_slab")
+
+    def sph_slab_info(self) -> dict:
+        """{nranks, mv, edges}: the slab rank's current edges in reference-cell
+        columns (re-balancing moves them) and how far they may move."""
+        nr, mv = C.c_int(0), C.c_int(0)
+        self._chk(lib().lpe_sph_slab_info(self._h, 0, None, C.byref(nr), C.byref(mv)), "lpe_sph_slab_info")
+        e = np.zeros(max(nr.value + 1, 1), np.int32)
+        self._chk(lib().lpe_sph_slab_info(self._h, len(e), e.ctypes.data_as(_IP), C.byref(nr), C.byref(mv)),
+                  "lpe_sph_slab_info")
+        return dict(nranks=nr.value, mv=mv.value, edges=e[:nr.value + 1])
 
     def sph_set_ids(self, ids):
         a = np.ascontiguousarray(ids, dtype=np.int32)
@@ -458,6 +477,13 @@ class Context:
     def mg_init_rccl(self, nranks: int, rank: int, uid: bytes):
         assert len(uid) == 128
         self._chk(lib().lpe_mg_init_rccl(self._h, int(nranks), int(rank), uid), "lpe_mg_init_rccl")
+
+    def mg_info(self) -> dict:
+        """{nranks, rank, comm_ranks}: the transport's group; comm_ranks is what
+        the communicator itself reports (ncclCommCount for RCCL)."""
+        a, b, c = C.c_int32(0), C.c_int32(0), C.c_int32(0)
+        self._chk(lib().lpe_mg_info(self._h, C.byref(a), C.byref(b), C.byref(c)), "lpe_mg_info")
+        return dict(nranks=a.value, rank=b.value, comm_ranks=c.value)
 
     def mg_init_host(self, nranks: int, rank: int, transport):
         """Host-staged transport: `transport` has halo(sendL, sendR, recvL,

@@ -2,13 +2,17 @@
 
 The reference runs one FluidSystem on one device (fluid.cpp:958-1021); here
 the particle set is split by x into one slab per rank and every rank runs
-the same lpe_sph_step on its owned particles, exchanging ghosts with its two
-neighbours each sub-step (include/lpe.h, "x-slab decomposition").  This
-module holds the host side of that split:
+the same lpe_sph_step / lpe_world_tick on the particles it owns, exchanging
+the particles within two reference-cell columns of its edges with its two
+neighbours every sub-step (include/lpe.h, "x-slab decomposition").  A rank
+owns the particles whose reference-cell column floor((x + eps) / 2h) lies in
+its slab, decided anew from every sub-step's kicked position, so a particle
+that crosses an edge changes owner inside that sub-step.  This module holds
+the host side of that split:
 
-  slab_edges      equal-count slab edges (x-quantiles)
-  owners          owning rank of each particle ([x0, x1) per slab)
-  ghost_capacity  exchange-buffer size per side from the initial layout
+  slab_edges      equal-count slab edges on reference-cell boundaries
+  owners          owning rank of each particle (the device's cell-column rule)
+  wire_capacity   ghost records per direction and sub-step
   setup_rank      configure + upload one rank's context
   merge_owned     reassemble the global state from the ranks' owned sets
   broadcast_uid / gather_owned   the torch.distributed plumbing (RCCL id
@@ -21,86 +25,75 @@ from __future__ import annotations
 import numpy as np
 
 FIELDS = ("x", "y", "vx", "vy", "density", "pressure")
+BAND = 2                  # ghost cell columns each side of an edge (lpe_sph.hip SLAB_BAND)
 
 
-def slab_edges(x, nranks: int) -> np.ndarray:
-    """nranks + 1 float32 edges [-inf, e1, ..., e_{n-1}, +inf]: inner edges at
-    the x-quantiles of the particles, so every slab starts with ~N/nranks
-    particles.  Deterministic in x, so every rank computes the same edges."""
-    xs = np.sort(np.asarray(x, np.float32))
-    n = len(xs)
-    edges = [np.float32(-np.inf)]
+def cell_size(cfg=None) -> float:
+    """The reference cell size 2 max(0.05, h) (fluid.cpp:724-737), fp32."""
+    h = 0.05 if cfg is None else float(cfg.gridConfig.smoothingLength)
+    return float(np.float32(2.0) * np.float32(max(0.05, h)))
+
+
+def _columns(x, cfg=None):
+    """Reference-cell column of each x: floor((x + eps) / cs) in fp32, the
+    device's bin column (lpe_sph.hip bin_key)."""
+    eps = np.float32(1e-6 if cfg is None else cfg.gridConfig.gridEpsilon)
+    cs = np.float32(cell_size(cfg))
+    return np.floor((np.asarray(x, np.float32) + eps) / cs).astype(np.int64)
+
+
+def slab_edges(x, nranks: int, cfg=None) -> np.ndarray:
+    """nranks + 1 float32 edges [-inf, e1, ..., e_{n-1}, +inf]: inner edges on
+    reference-cell boundaries at the column-count quantiles of the particles
+    (every slab starts with ~N/nranks particles), at least 8 columns apart.
+    Deterministic in x, so every rank computes the same edges."""
+    cs = cell_size(cfg)
+    col = np.sort(_columns(x, cfg))
+    n = len(col)
+    cuts = []
     for r in range(1, nranks):
-        e = xs[min(n - 1, (n * r) // nranks)] if n else np.float32(r)
-        if e <= edges[-1]:
-            e = np.nextafter(edges[-1], np.float32(np.inf), dtype=np.float32)
-        edges.append(np.float32(e))
-    edges.append(np.float32(np.inf))
+        c = int(col[min(n - 1, (n * r) // nranks)]) if n else 8 * r
+        if cuts and c < cuts[-1] + 8:
+            c = cuts[-1] + 8
+        cuts.append(c)
+    edges = [np.float32(-np.inf)] + [np.float32(c * cs) for c in cuts] + [np.float32(np.inf)]
     return np.array(edges, np.float32)
 
 
-def owners(x, edges) -> np.ndarray:
-    """Owning rank of each particle: slab r holds edges[r] <= x < edges[r+1]
-    (the device-side test of k_mig_pack, in float32)."""
-    xf = np.asarray(x, np.float32)
-    return np.searchsorted(np.asarray(edges, np.float32)[1:-1], xf, side="right").astype(np.int32)
+def owners(x, edges, cfg=None) -> np.ndarray:
+    """Owning rank of each particle: slab r holds the particles whose cell
+    column lies in [edges[r] / cs, edges[r+1] / cs) (the device's rule)."""
+    cs = cell_size(cfg)
+    cuts = np.rint(np.asarray(edges, np.float64)[1:-1] / cs).astype(np.int64)
+    return np.searchsorted(cuts, _columns(x, cfg), side="right").astype(np.int32)
 
 
-def ghost_capacity(x, edges, halo: float, factor: float = 3.0, floor: int = 4096) -> int:
-    """Ghost / migrant slots per side: `factor` times the most particles
-    within `halo` of any inner edge at the start (room for compression), plus
+def wire_capacity(x, edges, cfg=None, factor: float = 2.0, floor: int = 2048) -> int:
+    """Ghost records per direction and sub-step: `factor` times the most
+    particles in the BAND + 1 columns along any inner edge at the start (the
+    band, a column the re-balancing may move, room for compression), plus
     `floor`."""
-    xf = np.asarray(x, np.float32)
+    col = _columns(x, cfg)
+    cs = cell_size(cfg)
     worst = 0
-    for e in np.asarray(edges, np.float32)[1:-1]:
-        worst = max(worst, int(((xf >= e - halo) & (xf < e)).sum()), int(((xf >= e) & (xf < e + halo)).sum()))
+    for e in np.asarray(edges, np.float64)[1:-1]:
+        c = int(round(e / cs))
+        worst = max(worst, int(((col >= c - BAND - 1) & (col < c)).sum()),
+                    int(((col >= c) & (col < c + BAND + 1)).sum()))
     return int(factor * worst) + floor
 
 
-DRIFT_ALLOWANCE = 1.5     # metres an owned particle may travel outside its slab in one tick
-
-
-def default_halo(cfg, edges=None) -> float:
-    """Ghost width D = 2h + DRIFT_ALLOWANCE (1.6 m at the default h = 0.05).
-    2h so that every ghost the forces pass reads has all its own neighbours
-    (no second exchange of ghost densities); the allowance is how far an
-    owned particle may move outside its slab before the once-per-tick
-    migration: 1.5 m, 180 m/s at dt = 1/120 s.  Measured on the metric scenes
-    over 350 ticks (profiles/r01/slab_drift.json): at most 0.69 m per tick
-    (MW2) and 0.62 m (M), speeds up to ~94 m/s (fluid struck by the
-    pentagons).  Beyond the allowance the step fails loudly (ST_HALO_DRIFT).
-
-    A slab between two neighbours must be at least 2D - 2h wide (the ghosts a
-    rank needs come from its neighbours only); with `edges` the halo shrinks
-    to fit the narrowest such slab (the small test scenes)."""
-    h = float(cfg.gridConfig.smoothingLength)
-    D = 2.0 * h + DRIFT_ALLOWANCE
-    if edges is not None:
-        w = np.diff(np.asarray(edges, np.float64))[1:-1]
-        if len(w):
-            D = min(D, (float(w.min()) + 2.0 * h) / 2.0)
-    if not D > 2.0 * h:
-        raise ValueError("slab decomposition: a slab is narrower than the 2h the halo needs")
-    return D
-
-
-def setup_rank(ctx, rank: int, nranks: int, fluid: dict, edges, cfg, rigids=None, halo=None,
-               ghost_cap=None, domain=None):
+def setup_rank(ctx, rank: int, nranks: int, fluid: dict, edges, cfg, rigids=None, wire_cap=None,
+               domain=None, rebalance: int = 0):
     """Configure ctx as slab `rank` and upload the particles it owns (global
     ids = indices into `fluid`).  Returns the owned global ids."""
     import lpe  # the in-tree binding (little-physics-engine_amd/lpe.py)
-    halo = default_halo(cfg, edges) if halo is None else halo
-    w = np.diff(np.asarray(edges, np.float64))[1:-1]
-    if len(w) and 2.0 * halo - 2.0 * float(cfg.gridConfig.smoothingLength) > float(w.min()):
-        raise ValueError("slab decomposition: an inner slab is narrower than 2 * halo - 2h")
     x = np.asarray(fluid["x"], np.float32)
-    if ghost_cap is None:
-        ghost_cap = ghost_capacity(x, edges, halo)
-    own = np.nonzero(owners(x, edges) == rank)[0].astype(np.int32)
-    x0, x1 = float(edges[rank]), float(edges[rank + 1])
+    if wire_cap is None:
+        wire_cap = wire_capacity(x, edges, cfg)
+    own = np.nonzero(owners(x, edges, cfg) == rank)[0].astype(np.int32)
     ctx.sph_set_config(cfg)
-    ctx.sph_set_slab(x0 if np.isfinite(x0) else 0.0, x1 if np.isfinite(x1) else 0.0, halo,
-                     rank > 0, rank < nranks - 1, ghost_cap)
+    ctx.sph_set_slab(nranks, rank, edges, wire_cap, rebalance)
     sub = {k: np.asarray(fluid[k])[own] for k in ("x", "y", "vx", "vy", "mass", "density", "pressure")}
     ctx.sph_upload(sub["x"], sub["y"], sub["vx"], sub["vy"], sub["mass"], sub["density"], sub["pressure"])
     ctx.sph_set_ids(own)
@@ -111,6 +104,36 @@ def setup_rank(ctx, rank: int, nranks: int, fluid: dict, edges, cfg, rigids=None
     ctx.sph_set_domain(*domain)
     ctx.sph_upload_rigids(rigids if rigids is not None else np.zeros(0, lpe.RIGID_DTYPE))
     return own
+
+
+def rebalance_edges(hist, col0: int, edges, edges0, nranks: int, mv: int, minw: int = 8):
+    """One re-balancing move, as k_slab_rebalance (lpe_sph.hip) does it on the
+    device from the all-reduced column histogram: each inner edge j moves one
+    column towards the j / nranks count quantile unless the particles left
+    of it are within max(1 % of a slab's mean, half its column) of the
+    target, stays within edges0[j] -/+ mv and minw columns of its
+    neighbours.  fp32 sums as the device's (counts are exact integers)."""
+    hist = np.asarray(hist, np.float32)
+    e = np.array(edges, np.int64)
+    total = np.float32(hist.sum(dtype=np.float64))
+    for j in range(1, nranks):
+        c = int(e[j]) - col0
+        left = np.float32(hist[:max(0, min(c, len(hist)))].sum(dtype=np.float64))
+        target = np.float32(total * np.float32(j) / np.float32(nranks))
+        colc = np.float32(hist[c]) if 0 <= c < len(hist) else np.float32(0.0)
+        tol = max(np.float32(0.01) * total / np.float32(nranks), np.float32(0.5) * colc)
+        ne = int(e[j])
+        if left < target - tol:
+            ne += 1
+        elif left > target + tol:
+            ne -= 1
+        ne = min(max(ne, int(edges0[j]) - mv), int(edges0[j]) + mv)
+        if j > 1:
+            ne = max(ne, int(e[j - 1]) + minw)
+        if j + 1 < nranks:
+            ne = min(ne, int(e[j + 1]) - minw)
+        e[j] = ne
+    return e
 
 
 def merge_owned(parts, n_global: int) -> dict:

@@ -7,9 +7,9 @@ fluid on cuda:0 with the rigid pass replicated, installs the host-staged
 transport (lpe_mg_init_host over slab.GlooTransport), runs NTICKS resident
 world ticks (lpe_world_tick, one call per tick as the drop-in does) and
 writes its owned particles, its bodies and the transport's call counts to
-OUT.npz.  With SCENE ending in ":mismatch" rank 1 declares a ghost capacity
-different from rank 0's, so the first halo's sizes disagree: both ranks must
-fail with an error, not hang."""
+OUT.npz.  With SCENE ending in ":mismatch" rank 1 declares a wire capacity
+different from rank 0's, so the first exchange's sizes disagree: both ranks
+must fail with an error, not hang."""
 import importlib.util
 import os
 import sys
@@ -44,7 +44,7 @@ def main():
     b, v = scenes.to_bodies(s["bodies"])
     cfg = lpe.default_fluid_config()
     edges = slab.slab_edges(fl["x"], world)
-    cap = slab.ghost_capacity(np.asarray(fl["x"], np.float32), edges, slab.default_halo(cfg, edges))
+    cap = slab.wire_capacity(np.asarray(fl["x"], np.float32), edges, cfg)
     if mode == "mismatch" and rank == 1:
         cap += 64
     tr = slab.GlooTransport(rank, world)
@@ -53,7 +53,7 @@ def main():
     try:
         ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
         ctx.rigid_upload(b, v)
-        slab.setup_rank(ctx, rank, world, fl, edges, cfg, ghost_cap=cap)
+        slab.setup_rank(ctx, rank, world, fl, edges, cfg, wire_cap=cap)
         ctx.world_set_coupling(np.arange(len(b) - 1, -1, -1, dtype=np.int32))
         ctx.mg_init_host(world, rank, tr)
         try:

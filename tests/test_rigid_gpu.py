@@ -240,3 +240,38 @@ def test_pair_buffer_grow_in_world_tick():
     assert outs[0][1]["regrows"] >= 1
     for k in ("x", "y", "angle", "vx", "vy", "omega", "flags"):
         np.testing.assert_array_equal(outs[0][0][k], outs[1][0][k], err_msg=k)
+
+
+def test_lagged_overflow_reported_and_contained():
+    """a pair/contact overflow in a tick whose counts are checked
+    after the fact (lagged detection) must stay inside the buffers and fail
+    loudly.  256 pentagons 0.3 m apart (no contact) in columns that close on
+    each other at 14 m/s: the first, synchronous tick finds no pair and arms
+    the lagged mode on buffers reserved for 64 pairs / 256 contacts; the next
+    tick's detection finds ~4x more pairs than that.  The overflowing tick
+    solves nothing (k_compact zeroes its counts), the check raises
+    LPE_ERR_OVERFLOW, and the bodies stay finite."""
+    U = 12.0
+    b = scenes.Bodies()
+    scenes.add_walls(b, U)
+    for row in range(16):
+        for col in range(16):
+            verts = scenes.regular_polygon(5, 0.1)
+            b.add(x=3.0 + col * 0.3, y=3.0 + row * 0.3, vx=(7.0 if col % 2 == 0 else -7.0), vy=0.0, mass=5.0,
+                  verts=verts, shape_size=0.1, has_angvel=True, has_inertia=True,
+                  inertia=scenes.polygon_inertia(verts, 5.0))
+    bodies, verts = scenes.to_bodies(b)
+    ctx = lpe.Context(0)
+    try:
+        ctx.rigid_set_config(lpe.rigid_config(universe=U))
+        ctx.rigid_upload(bodies, verts)
+        ctx.rigid_reserve(64, 256)
+        with pytest.raises(lpe.LpeError, match="OVERFLOW"):
+            ctx.world_tick(DT, 4)
+            ctx.rigid_download()
+        out = ctx.rigid_download()
+    finally:
+        ctx.close()
+    for k in ("x", "y", "angle", "vx", "vy", "omega"):
+        assert np.isfinite(out[k]).all(), k
+    assert (out["x"][4:] > 0).all() and (out["x"][4:] < U).all()

@@ -2,14 +2,15 @@
 single-domain HIP step, which tests/test_sph_gpu.py pins to the oracle.
 
 Several ranks run on the one GPU of the box through the in-process loopback
-transport (lpe_mg_loopback_run: one host thread per rank, device-to-device
-copies for the halo, host reductions in rank order); the RCCL transport
-differs only in how the same buffers move.  Ghosts carry global ids and the
-reference grid comes from the all-reduced bbox, so without rigid contact the
-merged state is bit-identical to the single-domain run, tick after tick.
-With rigid coupling too: the rigid accumulators are exact fixed-point sums
-whose limbs are all-reduced as int64, so the split over ranks cannot change a
-bit, and full world ticks stay bit-identical to the single domain.""" 
+transport (lpe_mg_loopback_run: one host thread per rank, every exchange and
+reduction a kernel on the rank's stream ordered by events, reductions in
+rank order); the RCCL transport differs only in how the same buffers move.
+Ownership is decided per sub-step by cell column, ghosts carry global ids
+and the reference grid comes from every rank's bbox record, so the merged
+state is bit-identical to the single-domain run, tick after tick.  With
+rigid coupling too: the rigid accumulators are exact fixed-point sums whose
+limbs are all-reduced as int64, so the split over ranks cannot change a bit,
+and full world ticks stay bit-identical to the single domain."""
 import numpy as np
 import pytest
 
@@ -43,13 +44,13 @@ def _single(fl, rig, nticks):
         ctx.close()
 
 
-def _sharded(fl, rig, nticks, edges, ghost_cap=None):
+def _sharded(fl, rig, nticks, edges, wire_cap=None, rebalance=0):
     n = len(edges) - 1
     cfg = lpe.default_fluid_config()
     ctxs = [lpe.Context(0) for _ in range(n)]
     try:
         for r, c in enumerate(ctxs):
-            slab.setup_rank(c, r, n, fl, edges, cfg, rig, ghost_cap=ghost_cap)
+            slab.setup_rank(c, r, n, fl, edges, cfg, rig, wire_cap=wire_cap, rebalance=rebalance)
         counts0 = [c.n for c in ctxs]
         lpe.mg_loopback_run(ctxs, nticks, DT)
         parts = [c.sph_download_owned(cap=len(fl["x"])) for c in ctxs]
@@ -75,17 +76,20 @@ def test_slab_fluid_bit_exact(nranks):
 
 
 def test_slab_migration_and_empty_rank():
-    """Edges through the moving fluid (particles cross slab edges and
-    migrate) and a rank that starts empty and receives particles."""
+    """Edges through the moving fluid (particles cross slab edges and change
+    owner inside a sub-step) and a rank that starts empty and receives
+    particles."""
     s = scenes.scene("small64_0")
     fl = dict(s["fluid"])
     n = len(fl["x"])
-    fl["vx"] = np.full(n, 2.0)      # the whole block drifts right 2 m/s
+    fl["vx"] = np.full(n, 4.0)      # the whole block drifts right 4 m/s (0.13 m in 4 ticks)
     rig = np.zeros(0, lpe.RIGID_DTYPE)
     ref, _, _ = _single(fl, rig, 4)
-    xmax = np.float32(np.max(fl["x"]))
-    edges = np.array([-np.inf, np.median(np.float32(fl["x"])), xmax + np.float32(0.02), np.inf],
-                     np.float32)
+    cs = slab.cell_size()
+    col = slab._columns(fl["x"])
+    c_lo, c_hi = int(col.min()), int(col.max())
+    edges = np.array([-np.inf, (c_hi - 8) * cs, (c_hi + 1) * cs, np.inf], np.float32)
+    assert c_hi - 8 > c_lo
     got, _, c0, c1 = _sharded(fl, rig, 4, edges)
     assert c0[2] == 0 and c1[2] > 0, (c0, c1)
     for k in slab.FIELDS:
@@ -112,11 +116,10 @@ def test_slab_coupled_first_tick():
 
 
 def test_slab_spike_within_capacity():
-    """Every exchange moves the whole capacity (a spike above the
-    previous tick's request used to be fatal and lost migrants): a velocity
-    jump after 2 ticks pushes many more ghosts and migrants over the edges,
-    and 3 more ticks stay bit-identical to the single domain; the reported
-    wire is the capacity."""
+    """Every exchange moves a fixed wire both ends know (no host round trip
+    sizes it): a velocity jump after 2 ticks pushes many more particles over
+    the edges within the capacity, and 3 more ticks stay bit-identical to the
+    single domain; the reported wire is the capacity."""
     s = scenes.scene("small96_0")
     fl = dict(s["fluid"])
     fl["vx"] = np.full(len(fl["x"]), 0.8)
@@ -124,13 +127,13 @@ def test_slab_spike_within_capacity():
     ref2, _, _ = _single(fl, rig, 2)
     edges = slab.slab_edges(fl["x"], 3)
     cfg = lpe.default_fluid_config()
-    cap = slab.ghost_capacity(np.asarray(fl["x"], np.float32), edges, slab.default_halo(cfg))
+    cap = slab.wire_capacity(np.asarray(fl["x"], np.float32), edges, cfg)
 
     def loop(flin, nticks):
         ctxs = [lpe.Context(0) for _ in range(3)]
         try:
             for r, c in enumerate(ctxs):
-                slab.setup_rank(c, r, 3, flin, edges, cfg, rig, ghost_cap=cap)
+                slab.setup_rank(c, r, 3, flin, edges, cfg, rig, wire_cap=cap)
             lpe.mg_loopback_run(ctxs, nticks, DT)
             wires = [c.sph_stats()["haloWire"] for c in ctxs]
             parts = [c.sph_download_owned(cap=len(flin["x"])) for c in ctxs]
@@ -158,12 +161,12 @@ def test_slab_spike_within_capacity():
 
 
 def test_slab_halo_overflow_reported():
-    """A ghost buffer too small for the edge strip fails loudly."""
+    """A wire too small for the edge band fails loudly."""
     s = scenes.scene("small64_0")
     fl = s["fluid"]
     edges = slab.slab_edges(fl["x"], 2)
     with pytest.raises(lpe.LpeError, match="OVERFLOW|overflow"):
-        _sharded(fl, np.zeros(0, lpe.RIGID_DTYPE), 1, edges, ghost_cap=8)
+        _sharded(fl, np.zeros(0, lpe.RIGID_DTYPE), 1, edges, wire_cap=8)
 
 
 def _world_rank(ctx, r, n, s, edges):
@@ -231,3 +234,71 @@ def test_rccl_transport_single_rank():
         ctx.close()
     for k in slab.FIELDS:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+def test_slab_rebalance_bit_exact_and_model_edges():
+    """Re-balancing every step on a left-heavy split: the edge moves a column
+    per step towards equal counts -- exactly as slab.rebalance_edges
+    restates it from the owned particles' columns -- while the merged state
+    stays bit-identical to the single domain."""
+    s = scenes.scene("small96_0")
+    fl = s["fluid"]
+    rig = np.zeros(0, lpe.RIGID_DTYPE)
+    n = len(fl["x"])
+    cfg = lpe.default_fluid_config()
+    cs = slab.cell_size(cfg)
+    col = slab._columns(fl["x"])
+    edges = np.array([-np.inf, (int(col.min()) + 16) * cs, np.inf], np.float32)   # 16 of 24 columns left
+    e_model = np.array([-(1 << 29), int(col.min()) + 16, 1 << 29])
+    e0 = e_model.copy()
+    ctxs = [lpe.Context(0) for _ in range(2)]
+    try:
+        for r, c in enumerate(ctxs):
+            slab.setup_rank(c, r, 2, fl, edges, cfg, rig, rebalance=1)
+        mv = ctxs[0].sph_slab_info()["mv"]
+        col0 = int(e0[1]) - mv - 2
+        ncols = int(e0[1]) + mv + 2 - col0 + 1
+        for t in range(4):
+            lpe.mg_loopback_run(ctxs, 1, DT)
+            parts = [c.sph_download_owned(cap=n) for c in ctxs]
+            allx = np.concatenate([p["x"] for p in parts])
+            hist = np.bincount(np.clip(slab._columns(allx, cfg) - col0, 0, ncols - 1), minlength=ncols)
+            e_model = slab.rebalance_edges(hist.astype(np.float32), col0, e_model, e0, 2, mv)
+            for c in ctxs:
+                got = c.sph_slab_info()["edges"]
+                assert got[1] == e_model[1], (t, got, e_model)
+        got = slab.merge_owned(parts, n)
+    finally:
+        for c in ctxs:
+            c.close()
+    assert e_model[1] < e0[1]
+    ref, _, _ = _single(fl, rig, 4)
+    for k in slab.FIELDS:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+def test_slab_stats_and_prelaunch_one_tick_calls():
+    """The slab path with the prelaunched sub-step 0 (world ticks one call at
+    a time, as the drop-in does) equals multi-tick calls, and the stats
+    report the owned counts and the ghosts received."""
+    s = scenes.scene("small96_12")
+    n_glob = len(s["fluid"]["x"])
+    outs = []
+    for per_call in (1, 3):
+        edges = slab.slab_edges(s["fluid"]["x"], 3)
+        ctxs = [lpe.Context(0) for _ in range(3)]
+        try:
+            for r, c in enumerate(ctxs):
+                _world_rank(c, r, 3, s, edges)
+            for _ in range(3 // per_call):
+                lpe.mg_loopback_run(ctxs, per_call, world=lpe.WorldConfig(DT, 1.0, 1.0, 1.0))
+            st = [c.sph_stats() for c in ctxs]
+            outs.append(slab.merge_owned([c.sph_download_owned(cap=n_glob) for c in ctxs], n_glob))
+        finally:
+            for c in ctxs:
+                c.close()
+        assert sum(x["slabOwned"] for x in st) == n_glob
+        assert st[0]["ghostsIn"][1] > 0 and st[1]["ghostsIn"][0] > 0 and st[1]["ghostsIn"][1] > 0
+        assert all(x["slabSlots"] >= x["slabOwned"] for x in st)
+    for k in slab.FIELDS:
+        np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)

@@ -17,35 +17,104 @@ sys.modules["slab"] = slab
 _spec.loader.exec_module(slab)
 
 
-def test_edges_equal_count_and_ownership():
+def test_edges_on_cells_equal_count_and_ownership():
+    """Inner edges on reference-cell boundaries (multiples of 2h), equal
+    counts up to one cell column, ownership by the device's cell-column rule."""
     fl = scenes.scene("small96_0")["fluid"]
     x = np.float32(fl["x"])
-    for n in (1, 2, 3, 8):
+    cs = slab.cell_size()
+    col = slab._columns(x)
+    colmax = np.bincount(col - col.min()).max()
+    for n in (1, 2, 3):                  # (24 columns: 8 per slab at most 3 slabs)
         e = slab.slab_edges(x, n)
         assert len(e) == n + 1 and np.isneginf(e[0]) and np.isposinf(e[-1])
         assert (np.diff(e) > 0).all()
+        q = np.asarray(e[1:-1], np.float64) / cs
+        assert np.allclose(q, np.rint(q), atol=1e-3)                 # on cell boundaries
         own = slab.owners(x, e)
         cnt = np.bincount(own, minlength=n)
         assert cnt.sum() == len(x)
-        assert cnt.max() - cnt.min() <= max(2, len(x) // (10 * n))   # equal count, lattice ties aside
-        for r in range(n):                                           # [x0, x1) per slab
-            xs = x[own == r]
-            assert (xs >= e[r]).all() and (xs < e[r + 1]).all()
+        assert cnt.max() - cnt.min() <= colmax
+        cuts = np.rint(q).astype(np.int64)
+        for r in range(n):                                           # [cx0, cx1) per slab, in columns
+            c = col[own == r]
+            if r > 0:
+                assert (c >= cuts[r - 1]).all()
+            if r < n - 1:
+                assert (c < cuts[r]).all()
 
 
-def test_edge_value_goes_right():
+def test_owner_rule_uses_the_grid_epsilon():
+    """floor((x + eps) / cs): a particle within eps below an edge is in the
+    cell above it (the device's bin), so it belongs to the right slab."""
     e = np.array([-np.inf, 1.0, np.inf], np.float32)
-    assert list(slab.owners(np.float32([0.99999994, 1.0, 1.0000001]), e)) == [0, 1, 1]
+    x = np.float32([1.0 - 2e-6, 1.0 - 4e-7, 1.0, 1.05])
+    assert list(slab.owners(x, e)) == [0, 1, 1, 1]
 
 
-def test_ghost_capacity_covers_strip():
+def test_wire_capacity_covers_band():
     fl = scenes.scene("small96_0")["fluid"]
     x = np.float32(fl["x"])
     e = slab.slab_edges(x, 2)
-    halo = 0.2
-    strip = int(((x >= e[1] - halo) & (x < e[1] + halo)).sum())
-    assert slab.ghost_capacity(x, e, halo, factor=1.0, floor=0) >= strip // 2
-    assert slab.ghost_capacity(x, e, halo) >= 4 * (strip // 2)
+    col = slab._columns(x)
+    c = int(round(float(e[1]) / slab.cell_size()))
+    band = int(((col >= c - slab.BAND - 1) & (col < c)).sum())
+    assert slab.wire_capacity(x, e, factor=1.0, floor=0) >= band
+    assert slab.wire_capacity(x, e) >= 2 * band
+
+
+def test_ownership_protocol_model():
+    """The per-sub-step protocol of lpe_sph.hip on random walks (a numpy
+    model): each rank kicks the particles it owns, files those within BAND
+    columns of (or past) an edge for that neighbour, owns afterwards what lies
+    in its columns among its own and the received; every particle stays owned
+    by exactly one rank, and every rank holds every particle within BAND
+    columns of its slab (the neighbours its owned particles' ghosts need)."""
+    rng = np.random.default_rng(3)
+    n, nr = 4000, 4
+    col = rng.integers(0, 200, n)
+    cuts = np.array([50, 100, 150])
+    lo = np.r_[-10**9, cuts]
+    hi = np.r_[cuts, 10**9]
+    owner = np.searchsorted(cuts, col, side="right")
+    for step in range(60):
+        col = col + rng.integers(-1, 2, n)              # a sub-step moves a particle at most a column
+        held = [set() for _ in range(nr)]
+        for r in range(nr):
+            mine = np.nonzero(owner == r)[0]
+            held[r].update(mine.tolist())
+            if r > 0:
+                held[r - 1].update(mine[col[mine] < lo[r] + slab.BAND].tolist())
+            if r < nr - 1:
+                held[r + 1].update(mine[col[mine] >= hi[r] - slab.BAND].tolist())
+        new_owner = np.full(n, -1)
+        for r in range(nr):
+            ids = np.array(sorted(held[r]), np.int64)
+            own = ids[(col[ids] >= lo[r]) & (col[ids] < hi[r])]
+            assert (new_owner[own] == -1).all()            # no particle owned twice
+            new_owner[own] = r
+            need = np.nonzero((col >= lo[r] - slab.BAND) & (col < hi[r] + slab.BAND))[0]
+            assert set(need.tolist()) <= held[r]           # the ghosts the owned ones need
+        assert (new_owner >= 0).all()                      # none lost
+        owner = new_owner
+
+
+def test_rebalance_model_moves_towards_equal_counts():
+    """slab.rebalance_edges (the restatement of k_slab_rebalance): one column
+    per call towards equal counts, within its range, a dead band of 1 %."""
+    hist = np.zeros(100, np.float32)
+    hist[:] = 10.0
+    hist[:30] = 30.0                                      # left-heavy
+    edges = np.array([-(1 << 29), 50, 1 << 29])
+    e0 = edges.copy()
+    for _ in range(40):
+        edges = slab.rebalance_edges(hist, 0, edges, e0, 2, mv=30)
+    left = hist[:edges[1]].sum()
+    assert abs(left - hist.sum() / 2) <= hist[edges[1]]
+    assert edges[1] < 50
+    even = np.full(100, 10.0, np.float32)
+    same = slab.rebalance_edges(even, 0, np.array([-(1 << 29), 50, 1 << 29]), e0, 2, mv=30)
+    assert same[1] == 50
 
 
 def _parts(n, nr, rng):

@@ -3,9 +3,9 @@
 
 RCCL refuses two ranks on one GPU, so the 8-GPU bench is the only place the
 RCCL transport meets a second rank.  These tests run the same protocol --
-per sub-step the bbox all-reduce and the ghost halo, per tick the rigid
-accumulator all-reduce and the migration halo, with the sizes both ends
-declare -- between separate processes through the host-staged transport
+per sub-step one exchange (the ghost halo with the sizes both ends declare,
+and the bbox records), per tick the rigid accumulator all-reduce -- between
+separate processes through the host-staged transport
 (lpe_mg_init_host, slab.GlooTransport over torch.distributed gloo):
 
 - CPU: the transport's size handshake on a world_size-2 gloo group (matching
@@ -13,7 +13,7 @@ declare -- between separate processes through the host-staged transport
 - GPU: two worker processes (tests/mp_slab_worker.py), each a slab rank on
   cuda:0, run resident world ticks; the merged state is bit-identical to the
   single domain run in this process, and a rank that declares a different
-  ghost capacity makes both ranks fail loudly."""
+  wire capacity makes both ranks fail loudly."""
 import os
 import socket
 import subprocess
@@ -140,9 +140,11 @@ def test_two_process_slab_world_ticks_bit_exact(tmp_path):
     res = _run_workers("small96_12", nt, tmp_path)
     for r in res:
         assert str(r["err"]) == "", str(r["err"])
-        # per sub-step: a bbox all-reduce and a ghost halo; per tick: the
-        # accumulator all-reduce and the migration halo
-        assert list(r["calls"]) == [nt * 11, nt * 10, nt], r["calls"]
+        # per sub-step one exchange (the ghost halo and the bbox all-reduce);
+        # per tick the accumulator all-reduce.  From the second tick on,
+        # sub-step 0 is prelaunched at the end of the tick before, so the
+        # last tick leaves one exchange done for the next: 10 nt + 1
+        assert list(r["calls"]) == [nt * 10 + 1, nt * 10 + 1, nt], r["calls"]
     parts = [{k[4:]: r[k] for k in r if k.startswith("own_")} for r in res]
     got = slab.merge_owned(parts, len(fl["x"]))
     for k in slab.FIELDS:
@@ -154,7 +156,7 @@ def test_two_process_slab_world_ticks_bit_exact(tmp_path):
 
 @pytest.mark.gpu
 def test_two_process_size_mismatch_fails_on_both_ranks(tmp_path):
-    """Rank 1 declares a larger ghost capacity: the first halo's sizes
+    """Rank 1 declares a larger wire capacity: the first exchange's sizes
     disagree, and both processes return an error (RCCL would hang or
     truncate)."""
     res = _run_workers("small96_12:mismatch", 1, tmp_path)
