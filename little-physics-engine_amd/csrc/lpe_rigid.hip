@@ -3066,6 +3066,14 @@ extern "C" int lpe_rigid_upload(lpe_ctx *ctx, int nb, const lpe_body *bodies, in
     if (ctx) { rdev(ctx)->heavy_valid = false; rdev(ctx)->gen++; }
     if (!ctx || nb < 0 || nverts < 0 || (nb > 0 && !bodies) || (nverts > 0 && !verts))
         return LPE_ERR_ARG;
+    // the portable sin / cos (lpe_trig.h) reduce exactly for |angle| below
+    // LPE_TRIG_MAX_ARG (2^20 pi/2); the rotation system wraps every angle each
+    // tick, so only an uploaded one can be larger: refuse it
+    for (int i = 0; i < nb; i++)
+        if (!(std::fabs(bodies[i].angle) < LPE_TRIG_MAX_ARG)) {
+            ctx->err = "lpe_rigid_upload: a body angle is not finite or exceeds 2^20 * pi/2 rad (wrap it first)";
+            return LPE_ERR_ARG;
+        }
     (void)hipSetDevice(ctx->device);
     RigidDev *d = rdev(ctx);
     rigid_lag_off(ctx, d);

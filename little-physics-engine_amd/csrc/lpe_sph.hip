@@ -1650,6 +1650,12 @@ __device__ __forceinline__ void merge_prestats_dev(int32_t *__restrict__ st, int
     atomicMax(&st[ST_MAX_OCC_TOTAL], pre[ST_MAX_OCC_TOTAL]);
     for (int k = 0; k < ST_COUNT; k++) pre[k] = 0;
 }
+// the same as its own launch (the capped-cell mode: there the forces pass
+// itself may raise ST_REF_UB, which the in-pass merge's plain store of
+// that slot could erase)
+__global__ void k_merge_prestats(int32_t *__restrict__ st, int32_t *__restrict__ pre) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) merge_prestats_dev(st, pre);
+}
 #ifdef LPE_FTRACE
 __device__ unsigned long long g_ftrace[4096 * 8];
 __device__ int g_ftrace_on;
@@ -3184,10 +3190,15 @@ static int sph_hash_slab(lpe_ctx *ctx, float subDt, float halfDt, bool first, in
     }
     LPE_KERNEL(ctx, "k_bbox_reduce", k_bbox_reduce, dim3(1), dim3(TPB), 0, s, d.bboxPart, kb, h.bbAll + h.rank);
     LPE_CHECK_LAUNCH(ctx, "k_bbox_reduce");
-    int st = ctx->transport->exchange(ctx, h.hasL ? h.sL : nullptr, h.hasR ? h.sR : nullptr,
-                                      h.hasL ? h.rL : nullptr, h.hasR ? h.rR : nullptr, wire_bytes(h.wcap), HDR, GREC,
-                                      h.bbAll);
-    if (st) return st;
+    // (one rank has no peer to exchange with; LPE_SLAB_FORCE_XCHG=1 calls the
+    // transport anyway -- a probe of its per-call cost)
+    static const bool force = getenv("LPE_SLAB_FORCE_XCHG") != nullptr;
+    if (h.nranks > 1 || force) {
+        int st = ctx->transport->exchange(ctx, h.hasL ? h.sL : nullptr, h.hasR ? h.sR : nullptr,
+                                          h.hasL ? h.rL : nullptr, h.hasR ? h.rR : nullptr, wire_bytes(h.wcap), HDR,
+                                          GREC, h.bbAll);
+        if (st) return st;
+    }
     LPE_KERNEL(ctx, "k_ghost_unpack", k_ghost_unpack, dim3(nblk1(2L * h.wcap)), dim3(TPB), 0, s,
                h.hasL ? h.rL : (const float *)nullptr, h.hasR ? h.rR : (const float *)nullptr, h.wcap,
                h.hasL ? h.sL : (float *)nullptr, h.hasR ? h.sR : (float *)nullptr, (const float4 *)h.bbAll, h.nranks,
@@ -3371,6 +3382,10 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
         }
         kicked = kn.on ? fblocks : 0;
         sp.mergePre = (step == 0 && pre) ? d.status + ST_COUNT : nullptr;
+        if (sp.mergePre && sp.refInv) {
+            LPE_KERNEL(ctx, "k_merge_prestats", k_merge_prestats, dim3(1), dim3(64), 0, s, d.status, sp.mergePre);
+            sp.mergePre = nullptr;
+        }
         sp.ovl = (step == 0 && pre) ? d.ovl_pre : d.ovl_cur;
         LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(fgrid), dim3(HB), 0, s, sp, cp,
                            (step == 0 && pre) ? d.gp + 1 : d.gp,

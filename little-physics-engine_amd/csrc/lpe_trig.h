@@ -16,8 +16,10 @@
  * the platform from the result.
  *
  * Algorithm: the classic fdlibm/FreeBSD scheme — Cody–Waite reduction by
- * pi/2 in up to three 33-bit steps (exact for |x| < 2^20 * pi/2; angles here
- * stay within a few multiples of 2 pi: rotation.cpp wraps them every tick),
+ * pi/2 in up to three 33-bit steps (exact for |x| < LPE_TRIG_MAX_ARG =
+ * 2^20 * pi/2; angles here stay within a few multiples of 2 pi: rotation.cpp
+ * wraps them every tick, and lpe_rigid_upload refuses larger ones; beyond
+ * the range the functions return NaN instead of a silently wrong value),
  * then degree-13/14 minimax kernels on [-pi/4, pi/4].  Error < 1 ulp
  * (measured against glibc over 2^24 arguments: tests/test_oracle_rigid.py).
  * lpe_cosf / lpe_sinf, the reference's std::cos(float), are the double
@@ -35,6 +37,8 @@
 #else
 #define LPE_TRIG_FN static inline
 #endif
+
+#define LPE_TRIG_MAX_ARG 1647099.0   /* just below 2^20 * pi / 2 (the high word 0x413921fb) */
 
 LPE_TRIG_FN uint32_t lpe_trig_hi(double x) {
     uint64_t u;
@@ -107,6 +111,7 @@ LPE_TRIG_FN double lpe_sin(double x) {
         return lpe_ksin(x, 0.0, 0);
     }
     if (ix >= 0x7ff00000u) return x - x;        /* inf, nan */
+    if (ix >= 0x413921fbu) return (x - x) / (x - x);   /* |x| >= 2^20 pi/2: outside the exact reduction */
     double y0, y1;
     int n = lpe_rem_pio2(x, &y0, &y1);
     switch (n & 3) {
@@ -124,6 +129,7 @@ LPE_TRIG_FN double lpe_cos(double x) {
         return lpe_kcos(x, 0.0);
     }
     if (ix >= 0x7ff00000u) return x - x;
+    if (ix >= 0x413921fbu) return (x - x) / (x - x);
     double y0, y1;
     int n = lpe_rem_pio2(x, &y0, &y1);
     switch (n & 3) {

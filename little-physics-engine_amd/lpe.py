@@ -12,6 +12,15 @@ import os
 
 import numpy as np
 
+# One hardware queue per stream.  A context runs up to four streams (the
+# fluid step, the prelaunch, the collision detection, the position solver)
+# and RCCL adds its own; HIP maps streams round robin onto
+# GPU_MAX_HW_QUEUES queues (4 by default), and two streams on one queue
+# execute in submission order: the overlaps the tick is built on (detection
+# beside the fluid step, the prelaunch beside the solvers) collapse.  Set
+# before the library initialises HIP; a value the caller set wins.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LPE_LIB") or os.path.join(HERE, "liblpe_hip.so")   # LPE_LIB: an alternative build (A/B runs)
 
