@@ -176,46 +176,62 @@ def cpu_baseline(scene_name, state=None, budget_s=20.0):
 
 def density_microbench(lpe, scenes, device, side=4096, reps=5):
     """SURVEY.md §8(d) density microbench: a side x side lattice (16.7M
-    particles at side 4096) in a U = 104 m universe, one pure density pass
-    (computeDensity, no neighbour list) from a pre-built grid
-    (lpe_sph_probe_density: hash of the current positions, then
-    k_density_plan + k_density_pair, two particles per lane; avg_us is the SUM
-    of both launches), timed with HIP events on the library's stream;
-    algorithmic bytes 24 B/particle + 8 B/cell (§8(d))."""
+    particles at side 4096) in a U = 104 m universe, one density pass from a
+    pre-built grid (lpe_sph_probe_density: hash of the current positions,
+    then the pass), timed with HIP events on the library's stream;
+    algorithmic bytes 24 B/particle + 8 B/cell (§8(d)).  Two passes:
+    the pure one (computeDensity's outputs: k_density_plan + k_density_pair,
+    two particles per lane, avg_us the SUM of both launches) and, as
+    `tick_pass`, the tick's own k_density<true> (which also writes the forces
+    pass's neighbour lists, 256 B of list per particle at this size)."""
     rng = np.random.default_rng(7)
     U = 104.0
     x0 = 0.5 * (U - side * scenes.LATTICE_S)
     fl = scenes.fluid_lattice(rng, side, side, x0, x0)
     ctx = lpe.Context(device)
+    res = {}
     try:
         ctx.sph_set_config(lpe.default_fluid_config())
         ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
         del fl
-        rho, _ = ctx.sph_probe_density()          # warm (code objects, caches)
-        ctx.sph_diag(True)                        # resets the stage-fallback counter
-        ctx.timing(2)
-        ctx.timing_reset()
-        for _ in range(reps):
-            rho, _ = ctx.sph_probe_density()
-        tr = ctx.timing_read()
-        ctx.timing(0)
-        st = ctx.sph_stats()
+        for tag, mode in (("pure", 0), ("tick", lpe.SPH_MODE_PROBE_TICK_PASS)):
+            ctx.sph_set_mode(mode)
+            rho, _ = ctx.sph_probe_density()          # warm (code objects, caches)
+            ctx.sph_diag(True)                        # resets the stage-fallback counter
+            ctx.timing(2)
+            ctx.timing_reset()
+            for _ in range(reps):
+                rho, _ = ctx.sph_probe_density()
+            tr = ctx.timing_read()
+            ctx.timing(0)
+            st = ctx.sph_stats()
+            res[tag] = (tr, st, float(np.mean(rho)))
+        ctx.sph_set_mode(0)
     finally:
         ctx.close()
-    t = tr.get("k_density")
-    tp = tr.get("k_density_plan", (0.0, 0))       # the pass's per-tile staging plans (its own launch)
     n = side * side
-    cells = st["gridDimX"] * st["gridDimY"]
-    avg_s = (t[0] + tp[0]) / max(t[1], 1) / 1e3
-    b = 24.0 * n + 8.0 * cells
-    ach = b / avg_s / 1e9
-    return dict(kernel="k_density", particles=n, cells=cells, avg_us=round(avg_s * 1e6, 1),
-                kernels_us={"k_density_plan": round(tp[0] / max(tp[1], 1) * 1e3, 1),
-                            "k_density": round(t[0] / max(t[1], 1) * 1e3, 1)},
-                algorithmic_bytes=b, achieved=round(ach, 1), unit="GB/s", peak=HBM_PEAK_GBS,
-                frac=round(ach / HBM_PEAK_GBS, 4), launches=t[1],
-                stage_fallback_blocks=st["stageFallback"] // max(reps, 1),
-                mean_density=float(np.mean(rho)), max_cell_occupancy=st["maxCellOccupancy"])
+    out = None
+    for tag in ("pure", "tick"):
+        tr, st, mean_rho = res[tag]
+        t = tr.get("k_density")
+        tp = tr.get("k_density_plan", (0.0, 0))       # the pure pass's per-tile staging plans (its own launch)
+        cells = st["gridDimX"] * st["gridDimY"]
+        avg_s = (t[0] + tp[0]) / max(t[1], 1) / 1e3
+        b = 24.0 * n + 8.0 * cells
+        ach = b / avg_s / 1e9
+        d = dict(kernel="k_density_pair" if tag == "pure" else "k_density<true>", particles=n, cells=cells,
+                 avg_us=round(avg_s * 1e6, 1),
+                 kernels_us={"k_density_plan": round(tp[0] / max(tp[1], 1) * 1e3, 1),
+                             "k_density": round(t[0] / max(t[1], 1) * 1e3, 1)},
+                 algorithmic_bytes=b, achieved=round(ach, 1), unit="GB/s", peak=HBM_PEAK_GBS,
+                 frac=round(ach / HBM_PEAK_GBS, 4), launches=t[1],
+                 stage_fallback_blocks=st["stageFallback"] // max(reps, 1),
+                 mean_density=mean_rho, max_cell_occupancy=st["maxCellOccupancy"])
+        if tag == "pure":
+            out = d
+        else:
+            out["tick_pass"] = d
+    return out
 
 
 def render_bench(ctx, U, reps=3):

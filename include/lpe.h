@@ -316,6 +316,11 @@ int  lpe_sph_diag(lpe_ctx *ctx, int on);
  *   counting sort has no capacity), i.e. the reference's intent.  Not
  *   available on a slab rank (LPE_ERR_STATE). */
 #define LPE_SPH_MODE_REF_CELL_CAP 1
+/* LPE_SPH_MODE_PROBE_TICK_PASS: lpe_sph_probe_density runs the tick's density
+ * pass (which also writes the forces pass's neighbour lists) instead of the
+ * pure computeDensity pass; the same sums, bit for bit (the density
+ * microbench times both). */
+#define LPE_SPH_MODE_PROBE_TICK_PASS 2
 int  lpe_sph_set_mode(lpe_ctx *ctx, int flags);
 
 /* Parity probe: the reference's assignCells cell index for each particle

@@ -1522,7 +1522,7 @@ __device__ __forceinline__ void density_out(int s, float a, float stiffness, flo
     if (pres < 0.f) pres = 0.f;
     rho[s] = a;
     pr[s] = pres;
-    nbB[2 * s + 1] = make_float2(a, pres / (a * a));   // the p_j / rho_j^2 of metal:370
+    if (nbB) nbB[2 * s + 1] = make_float2(a, pres / (a * a));   // the p_j / rho_j^2 of metal:370
 }
 
 // A plan (sizeof(Hood) bytes) copied global -> LDS by wave 0, asynchronously
@@ -1584,6 +1584,16 @@ k_density_pair(int n, const int32_t *__restrict__ nptr, float h, float eps, floa
     const int pair = perm[threadIdx.x];
     const f2v acc = pair_tile(hd, lrec, lbnd, s0, s1, pair, h, eps, g, W, H, ox, oy, start, nbA, status);
     const int sa = s0 + 2 * pair;
+    if (sa + 1 < s1 && !nbB) {
+        // the pure pass (nbB null: computeDensity's outputs only, 8 B per
+        // particle): the pair's two densities and pressures as one 8-B store each
+        float p0 = stiffness * (acc.x - restDensity), p1 = stiffness * (acc.y - restDensity);
+        if (p0 < 0.f) p0 = 0.f;
+        if (p1 < 0.f) p1 = 0.f;
+        *(float2 *)(rho + sa) = make_float2(acc.x, acc.y);
+        *(float2 *)(pr + sa) = make_float2(p0, p1);
+        return;
+    }
     if (sa < s1) density_out(sa, acc.x, stiffness, restDensity, rho, pr, nbB);
     if (sa + 1 < s1) density_out(sa + 1, acc.y, stiffness, restDensity, rho, pr, nbB);
 }
@@ -3120,7 +3130,7 @@ static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr, float *rho, flo
                    c.gridConfig.gridEpsilon, d.W, d.H, d.ox, d.oy, d.gp_cur, d.start, d.nbA, (Hood *)d.plans);
         LPE_KERNEL(ctx, "k_density", k_density_pair, dim3(xcd_grid(ntiles)), dim3(DT_NT), 0, ctx->stream, n, nptr,
                    c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness, c.restDensity, d.W, d.H,
-                   d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)d.nbB, rho, pr, d.stat_cur,
+                   d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)nullptr, rho, pr, d.stat_cur,
                    (const Hood *)d.plans);
     }
     else if (nl)
@@ -3571,7 +3581,7 @@ extern "C" int lpe_sph_get_stats(lpe_ctx *ctx, lpe_sph_stats *out) {
 }
 
 extern "C" int lpe_sph_set_mode(lpe_ctx *ctx, int flags) {
-    if (!ctx || (flags & ~LPE_SPH_MODE_REF_CELL_CAP)) return LPE_ERR_ARG;
+    if (!ctx || (flags & ~(LPE_SPH_MODE_REF_CELL_CAP | LPE_SPH_MODE_PROBE_TICK_PASS))) return LPE_ERR_ARG;
     SphDev &d = ctx->sph;
     if ((flags & LPE_SPH_MODE_REF_CELL_CAP) && d.shard) {
         ctx->err = "the reference cell-capacity mode is single-domain only (not on a slab rank)";
@@ -3640,7 +3650,9 @@ extern "C" int lpe_sph_probe_density(lpe_ctx *ctx, float *density, float *pressu
     if (st) return st;
     st = sph_hash(ctx, 0.f, 0.f, false, true);
     if (st) return st;
-    st = sph_density(ctx, d.n, nullptr, d.rho, d.pr, false);   // the tick's density kernel, no neighbour lists
+    // the pure pass (computeDensity's outputs), or with LPE_SPH_MODE_PROBE_TICK_PASS the tick's
+    // pass (which also writes the forces pass's neighbour lists)
+    st = sph_density(ctx, d.n, nullptr, d.rho, d.pr, (d.mode & LPE_SPH_MODE_PROBE_TICK_PASS) != 0);
     if (st) return st;
     // rho/p are in S slot order here; S.x.. are the unpermute staging buffers,
     // so keep S.id aside in tmpOld first

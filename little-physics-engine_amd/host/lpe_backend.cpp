@@ -80,7 +80,13 @@ bool check(int st, const char *what) {
 
 int lastStatus() { return state().status; }
 
+PhaseTimes &fluidTimes() {
+    static PhaseTimes t;
+    return t;
+}
+
 void reset() {
+    fluidTimes() = PhaseTimes();
     State &s = state();
     s.disabled = false;
     s.status = LPE_OK;

@@ -35,6 +35,15 @@ void reset();            // drops the disabled flag and the resident world
 void setMode(Mode m, int syncEvery = 1);
 Mode mode();
 
+// Wall time of the fluid system's phases (strict mode), accumulated since the
+// last reset(): the ECS gather, the uploads, the device step, the downloads,
+// the ECS write-back -- what the drop-in costs beyond the device's own work.
+struct PhaseTimes {
+    double gather = 0, upload = 0, device = 0, download = 0, scatter = 0;
+    long calls = 0;
+};
+PhaseTimes &fluidTimes();
+
 // ---- ECS gathers shared by the rigid and integrator systems ---------------
 // Every entity with a Position (optionally skipping Liquid), in storage order,
 // as lpe_body rows (components flattened into flags) plus the local polygon

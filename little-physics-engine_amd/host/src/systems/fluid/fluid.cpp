@@ -5,6 +5,7 @@
  * (little-physics-engine_amd/csrc/lpe_sph.hip); the gathers and write-backs
  * keep the reference's ECS contract.
  */
+#include <chrono>
 #include "systems/fluid/fluid.hpp"
 
 #include <cstddef>
@@ -186,6 +187,10 @@ void FluidSystem::update(entt::registry &registry)
     {
         return;   // fluid.cpp:961-964
     }
+    using clock = std::chrono::steady_clock;
+    lpe::host::PhaseTimes &pt = lpe::host::fluidTimes();
+    auto since = [](clock::time_point t0) { return std::chrono::duration<double>(clock::now() - t0).count(); };
+    clock::time_point t0 = clock::now();
     std::vector<entt::entity> fluidEntities;
     std::vector<GPUFluidParticle> parts = gatherFluidParticles(registry, fluidEntities);
     if (parts.empty())
@@ -204,6 +209,8 @@ void FluidSystem::update(entt::registry &registry)
         m[i] = parts[i].mass;
         rho[i] = parts[i].density; p[i] = parts[i].pressure;
     }
+    pt.gather += since(t0);
+    t0 = clock::now();
     const lpe_fluid_config cfg = toC(getSpecificConfig());
     if (!lpe::host::check(lpe_sph_set_config(ctx, &cfg), "lpe_sph_set_config")) return;
     if (!lpe::host::check(lpe_sph_upload(ctx, n, x.data(), y.data(), vx.data(), vy.data(), m.data(),
@@ -215,10 +222,17 @@ void FluidSystem::update(entt::registry &registry)
         return;
     // dt = float(SecondsPerTick * TimeAcceleration) (fluid.cpp:592)
     const double dt = getSharedSystemConfig().SecondsPerTick * getSharedSystemConfig().TimeAcceleration;
+    pt.upload += since(t0);
+    t0 = clock::now();
     if (!lpe::host::check(lpe_sph_step(ctx, dt), "lpe_sph_step")) return;
+    if (!lpe::host::check(lpe_sync(ctx), "lpe_sync")) return;
+    pt.device += since(t0);
+    t0 = clock::now();
     if (!lpe::host::check(lpe_sph_download(ctx, x.data(), y.data(), vx.data(), vy.data(), rho.data(),
                                            p.data()), "lpe_sph_download"))
         return;
+    pt.download += since(t0);
+    t0 = clock::now();
     // writeBackToECS (fluid.cpp:496-524)
     for (int i = 0; i < n; i++)
     {
@@ -247,6 +261,8 @@ void FluidSystem::update(entt::registry &registry)
     }
     lpe_sph_stats st;
     if (lpe_sph_get_stats(ctx, &st) == LPE_OK) lastMaxOcc_ = st.maxCellOccupancy;
+    pt.scatter += since(t0);
+    pt.calls++;
 }
 
 } // namespace Systems

@@ -272,6 +272,7 @@ def bh_config(universe: float, theta: float = 0.5, small_mass_threshold: float =
 
 SYS_BOUNDARY, SYS_GRAVITY, SYS_ROTATION, SYS_MOVEMENT, SYS_SLEEP = 1, 2, 4, 8, 16
 SPH_MODE_REF_CELL_CAP = 1       # LPE_SPH_MODE_REF_CELL_CAP (include/lpe.h)
+SPH_MODE_PROBE_TICK_PASS = 2    # LPE_SPH_MODE_PROBE_TICK_PASS
 
 
 def lib():

@@ -10,6 +10,7 @@
  */
 #include <entt/entt.hpp>
 
+#include <chrono>
 #include <cstring>
 #include <memory>
 #include <unordered_map>
@@ -30,12 +31,15 @@
 
 #include "lpe_backend.hpp"
 
-extern "C" int lpeh_world(int mode, int sync_every, const lpe_rigid_config *rc,
-                          const lpe_fluid_config *fc, double spt, double time_accel, double bta,
-                          double ts, int nb, lpe_body *bodies, const double *verts, int nf,
-                          float *x, float *y, float *vx, float *vy, const float *m, float *rho,
-                          float *p, int nticks, int32_t *fluid_gather, int32_t *rigid_gather,
-                          int32_t *stats) {
+/* nticks ticks, then ntimed more with their wall time (timing, when given:
+ * [0] seconds of the ntimed ticks, [1] FluidSystem::update, [2]
+ * RigidBodyCollisionSystem::update, [3] the other systems (in resident mode
+ * SleepSystem runs the whole device tick and the ECS syncs), [4..8] the
+ * fluid system's gather / upload / device / download / write-back) */
+static int run_world(int mode, int sync_every, const lpe_rigid_config *rc, const lpe_fluid_config *fc, double spt,
+                     double time_accel, double bta, double ts, int nb, lpe_body *bodies, const double *verts, int nf,
+                     float *x, float *y, float *vx, float *vy, const float *m, float *rho, float *p, int nticks,
+                     int32_t *fluid_gather, int32_t *rigid_gather, int32_t *stats, int ntimed, double *timing) {
     entt::registry reg;
     auto se = reg.create();                        /* reset(): SimulatorState first (sim.cpp:93-94) */
     reg.emplace<Components::SimulatorState>(se, bta, ts);
@@ -151,6 +155,25 @@ extern "C" int lpeh_world(int mode, int sync_every, const lpe_rigid_config *rc,
     lpe::host::setMode(mode ? lpe::host::Mode::Resident : lpe::host::Mode::Strict, sync_every);
     for (int t = 0; t < nticks; t++)               /* ECSSimulator::tick (sim.cpp:156-163) */
         for (auto &sys : systems) sys->update(reg);
+    if (ntimed > 0 && timing) {
+        using clock = std::chrono::steady_clock;
+        if (lpe_ctx *c = lpe::host::context()) lpe_sync(c);
+        lpe::host::fluidTimes() = lpe::host::PhaseTimes();
+        double per[3] = {0, 0, 0};
+        const auto t0 = clock::now();
+        for (int t = 0; t < ntimed; t++)
+            for (size_t k = 0; k < systems.size(); k++) {
+                const auto a = clock::now();
+                systems[k]->update(reg);
+                per[k == 0 ? 0 : (k == 3 ? 1 : 2)] += std::chrono::duration<double>(clock::now() - a).count();
+            }
+        if (lpe_ctx *c = lpe::host::context()) lpe_sync(c);
+        timing[0] = std::chrono::duration<double>(clock::now() - t0).count();
+        timing[1] = per[0]; timing[2] = per[1]; timing[3] = per[2];
+        const lpe::host::PhaseTimes &ft = lpe::host::fluidTimes();
+        timing[4] = ft.gather; timing[5] = ft.upload; timing[6] = ft.device; timing[7] = ft.download;
+        timing[8] = ft.scatter;
+    }
     if (mode) lpe::host::residentSync(reg);
 
     for (int i = 0; i < nb; i++) {
@@ -183,6 +206,28 @@ extern "C" int lpeh_world(int mode, int sync_every, const lpe_rigid_config *rc,
     stats[3] = rs->lastContacts();
     lpe::host::setMode(lpe::host::Mode::Strict, 1);
     return stats[0];
+}
+
+extern "C" int lpeh_world(int mode, int sync_every, const lpe_rigid_config *rc,
+                          const lpe_fluid_config *fc, double spt, double time_accel, double bta,
+                          double ts, int nb, lpe_body *bodies, const double *verts, int nf,
+                          float *x, float *y, float *vx, float *vy, const float *m, float *rho,
+                          float *p, int nticks, int32_t *fluid_gather, int32_t *rigid_gather,
+                          int32_t *stats) {
+    return run_world(mode, sync_every, rc, fc, spt, time_accel, bta, ts, nb, bodies, verts, nf, x, y, vx, vy, m,
+                     rho, p, nticks, fluid_gather, rigid_gather, stats, 0, nullptr);
+}
+
+/* lpeh_world with `ntimed` timed ticks after `nticks` untimed ones (the
+ * drop-in's own cost, profiles/dropin_timing.py) */
+extern "C" int lpeh_world_timed(int mode, int sync_every, const lpe_rigid_config *rc,
+                                const lpe_fluid_config *fc, double spt, int nb, lpe_body *bodies,
+                                const double *verts, int nf, float *x, float *y, float *vx, float *vy,
+                                const float *m, float *rho, float *p, int nticks, int ntimed, int32_t *stats,
+                                double *timing) {
+    std::vector<int32_t> fg((size_t)std::max(nf, 1)), rg((size_t)std::max(nb, 1));
+    return run_world(mode, sync_every, rc, fc, spt, 1.0, 1.0, 1.0, nb, bodies, verts, nf, x, y, vx, vy, m, rho, p,
+                     nticks, fg.data(), rg.data(), stats, ntimed, timing);
 }
 
 /* The drop-in Systems::BarnesHutSystem (host/src/systems/barnes_hut.cpp) on

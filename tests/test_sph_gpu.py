@@ -69,12 +69,14 @@ def test_density_bit_exact(gpu_ctx, oracle_mod, name):
     np.testing.assert_array_equal(p, rp)
 
 
-@pytest.mark.parametrize("kind", ["C2", "jitter", "jitter_wide"])
-def test_density_pair_kernel_staged_bit_exact(gpu_ctx, oracle_mod, kind):
-    """The two-particles-per-lane pure density pass (k_density_pair) on wide
-    fluids, where its 512-slot tiles stage their neighbourhoods (no fallback):
-    the C2 dam break, and a jittered lattice with uneven cells (pairs that
-    straddle quadrants, cells and the tiles' two row runs)."""
+@pytest.mark.parametrize("kind,mode", [("C2", 0), ("jitter", 0), ("jitter_wide", 0), ("C2", 2), ("jitter", 2)])
+def test_density_pair_kernel_staged_bit_exact(gpu_ctx, oracle_mod, kind, mode):
+    """The two-particles-per-lane pure density pass (k_density_pair, 8-byte
+    pair stores) on wide fluids, where its 512-slot tiles stage their
+    neighbourhoods (no fallback): the C2 dam break, and a jittered lattice
+    with uneven cells (pairs that straddle quadrants, cells and the tiles'
+    two row runs).  mode 2 (LPE_SPH_MODE_PROBE_TICK_PASS): the same probe
+    through the tick's k_density<true>, the microbench's second pass."""
     if kind == "C2":
         fl = scenes.scene("C2")["fluid"]
     else:
@@ -84,9 +86,11 @@ def test_density_pair_kernel_staged_bit_exact(gpu_ctx, oracle_mod, kind):
         fl["x"] = (fl["x"] + rng.uniform(-0.006, 0.006, len(fl["x"])))
         fl["y"] = (fl["y"] + rng.uniform(-0.006, 0.006, len(fl["y"])))
     _upload(gpu_ctx, fl)
+    gpu_ctx.sph_set_mode(mode)
     gpu_ctx.sph_diag(True)
     rho, p = gpu_ctx.sph_probe_density()
     st = gpu_ctx.sph_stats()
+    gpu_ctx.sph_set_mode(0)
     rrho, rp, g, _ = oracle_mod.density(scenes.particles_aos(fl))
     np.testing.assert_array_equal(rho, rrho)
     np.testing.assert_array_equal(p, rp)
