@@ -2420,17 +2420,61 @@ extern "C" int lpe_strace(unsigned long long *host) {
 #define STR(w, j, k) do { } while (0)
 #endif
 
+// Does every colour step of this workgroup hold at most one wave of pairs?
+// Then wave 0 runs the steps alone (stripe_sweeps, `single`): a step's
+// pairs touch disjoint bodies, and one wave's LDS stores are visible to its
+// own later loads once they have completed (s_waitcnt), so consecutive steps
+// need no workgroup barrier -- the barrier, and the three idle waves'
+// re-issue, were a third of a step's latency (profiles/r03/pgs_step_cost.txt).
+// stepL: the LDS step table (or null: the global one).  Every thread calls it.
+__device__ __forceinline__ bool stripe_single_wave(const StripeBufs &sb, const StripeView &v, const int *stepL) {
+    __shared__ int s_big;
+    if (threadIdx.x == 0) s_big = 0;
+    __syncthreads();
+    const int ns = v.nsteps();
+    for (int k = threadIdx.x; k < ns; k += STPB) {
+        int len;
+        if (stepL) {
+            len = stepL[k + 1] - stepL[k];
+        } else {
+            const int st = k < v.a1 - v.a0 ? v.a0 + k : v.b0 + (k - (v.a1 - v.a0));
+            len = sb.stepPair[st + 1] - sb.stepPair[st];
+        }
+        if (len > 64) s_big = 1;
+    }
+    __syncthreads();
+    return s_big == 0;
+}
+
 // The sweeps of one stripe pair per workgroup (the loop shared by both
 // solvers): phase A = stripe 2j's steps, phase B = stripe 2j+1's; before a
 // phase the shared stripe a neighbour changed last is reloaded, after it the
 // one the neighbour needs next is published.  solve(st, it) runs one step.
+// single: wave 0 runs the steps without workgroup barriers between them
+// (stripe_single_wave); the workgroup joins at the phase's end.
 template <typename T, typename Solve>
 __device__ __forceinline__ void stripe_sweeps(const StripeBufs &sb, const StripeView &v, int iters, uint32_t base,
                                               uint32_t *flagA, uint32_t *flagB, T *lv, T *g, int32_t *fault,
-                                              Solve solve, int tw = 0) {
+                                              Solve solve, int tw = 0, bool single = false) {
     const int j = v.j;
     const bool right = 2 * j + 2 < v.S;             // seam j (phase B) exists
     (void)tw;
+    auto steps = [&](int s0, int s1, int it) {
+        if (single) {
+            if (threadIdx.x < 64) {
+                for (int st = s0; st < s1; st++) {
+                    solve(st, it);
+                    // this wave's LDS stores complete before its next step's loads
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    __builtin_amdgcn_s_waitcnt(0xc07f);        // lgkmcnt(0)
+                    __builtin_amdgcn_wave_barrier();
+                }
+            }
+            __syncthreads();
+        } else {
+            for (int st = s0; st < s1; st++) { solve(st, it); __syncthreads(); }
+        }
+    };
     STR(tw, j, 1);
     for (int it = 0; it < iters; it++) {
         if (it > 0 && j > 0) {                    // stripe 2j, after the left neighbour's phase B of it - 1
@@ -2439,7 +2483,7 @@ __device__ __forceinline__ void stripe_sweeps(const StripeBufs &sb, const Stripe
             __syncthreads();
         }
         STR(tw, j, 2 + 6 * it);
-        for (int st = v.a0; st < v.a1; st++) { solve(st, it); __syncthreads(); }
+        steps(v.a0, v.a1, it);
         STR(tw, j, 3 + 6 * it);
         if (j > 0) {
             stripe_publish(sb, 2 * j, v.s0, lv, g);
@@ -2453,7 +2497,7 @@ __device__ __forceinline__ void stripe_sweeps(const StripeBufs &sb, const Stripe
             __syncthreads();
         }
         STR(tw, j, 5 + 6 * it);
-        for (int st = v.b0; st < v.b1; st++) { solve(st, it); __syncthreads(); }
+        steps(v.b0, v.b1, it);
         STR(tw, j, 6 + 6 * it);
         stripe_publish(sb, 2 * j + 2, v.s0, lv, g);
         stripe_signal(&flagB[j], base + it + 1);
@@ -2521,6 +2565,7 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
         }
         stripe_steps_lds(sb, v, stepL);
         __syncthreads();
+        const bool single = stripe_single_wave(sb, v, stepL);
         auto solve = [&](int st, int) {
             const int k = v.lstep(st);
             const int q1 = stepL[k + 1];
@@ -2560,9 +2605,11 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
                 if (hasB) { lv[3 * p.w] = vxB; lv[3 * p.w + 1] = vyB; lv[3 * p.w + 2] = wB; }
             }
         };
-        stripe_sweeps(sb, v, iters, base, sb.sflag, sb.sflag + STRIPES_MAX / 2, lv, sb.gvel, fault, solve, 0);
+        stripe_sweeps(sb, v, iters, base, sb.sflag, sb.sflag + STRIPES_MAX / 2, lv, sb.gvel, fault, solve, 0,
+                      single);
     } else {
         __syncthreads();
+        const bool single = stripe_single_wave(sb, v, nullptr);
         auto solve = [&](int st, int it) {
             const int q1 = sb.stepPair[st + 1];
             for (int q = sb.stepPair[st] + (int)threadIdx.x; q < q1; q += STPB) {
@@ -2586,7 +2633,8 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
                 if (hasB) { lv[3 * lb] = vxB; lv[3 * lb + 1] = vyB; lv[3 * lb + 2] = wB; }
             }
         };
-        stripe_sweeps(sb, v, iters, base, sb.sflag, sb.sflag + STRIPES_MAX / 2, lv, sb.gvel, fault, solve, 0);
+        stripe_sweeps(sb, v, iters, base, sb.sflag, sb.sflag + STRIPES_MAX / 2, lv, sb.gvel, fault, solve, 0,
+                      single);
     }
     __syncthreads();
     // k_pgs_writeback for the stripes this workgroup finished last (only the
@@ -2667,6 +2715,7 @@ k_pos_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
         }
         stripe_steps_lds(sb, v, stepL);
         __syncthreads();
+        const bool single = stripe_single_wave(sb, v, stepL);
         auto solve = [&](int stp, int) {
             const int k = v.lstep(stp);
             const int q1 = stepL[k + 1];
@@ -2686,9 +2735,10 @@ k_pos_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
             }
         };
         stripe_sweeps(sb, v, iters, base, sb.sflag + STRIPES_MAX, sb.sflag + STRIPES_MAX + STRIPES_MAX / 2, lp,
-                      sb.gpos, fault, solve, 1);
+                      sb.gpos, fault, solve, 1, single);
     } else {
         __syncthreads();
+        const bool single = stripe_single_wave(sb, v, nullptr);
         auto solve = [&](int stp, int) {
             const int q1 = sb.stepPair[stp + 1];
             for (int q = sb.stepPair[stp] + (int)threadIdx.x; q < q1; q += STPB) {
@@ -2708,7 +2758,7 @@ k_pos_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
             }
         };
         stripe_sweeps(sb, v, iters, base, sb.sflag + STRIPES_MAX, sb.sflag + STRIPES_MAX + STRIPES_MAX / 2, lp,
-                      sb.gpos, fault, solve, 1);
+                      sb.gpos, fault, solve, 1, single);
     }
     __syncthreads();
     // storeBodyData (:176-197) for the stripes this workgroup finished last
