@@ -116,6 +116,27 @@ def pmc_valu(kernel):
     return _pmc_lookup("pmc_valu.json", kernel, "valu_wave_insts")
 
 
+def dropin_record():
+    """The drop-in timed through the reference's own tick loop (the EnTT host
+    harness, profiles/dropin_timing.py), from the newest committed
+    profiles/r*/dropin.json: ticks/s of strict mode and of resident mode
+    synced every 1 / 10 ticks, and whether it timed the library this run
+    loads.  It is measured beside the bench (its 3,000-tick settle and three
+    host-driven runs take minutes), not inside it."""
+    import glob
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "dropin.json")), reverse=True):
+        try:
+            d = json.loads(open(path).read().strip().splitlines()[-1])
+        except (OSError, ValueError, IndexError):
+            continue
+        built = d.get("_build", {}).get("lib_sha256")
+        runs = {k: dict(ticks_per_s=r["ticks_per_s"], ms_per_tick=r["ms_per_tick"]) for k, r in d.get("runs", {}).items()}
+        strict = d.get("runs", {}).get("strict", {})
+        return dict(source=os.path.relpath(path, ROOT), same_build=built is not None and built == lib_sha256(),
+                    driver=d.get("driver"), runs=runs, strict_fluid_phases_ms_per_tick=strict.get("fluid_phases_ms_per_tick"))
+    return None
+
+
 def cpu_model():
     try:
         for line in open("/proc/cpuinfo"):
@@ -817,6 +838,8 @@ def main():
         line["render_density"] = render
     if world == 1 and not args.no_cpu_baseline and args.scene == "M":
         line["cpu_baseline"] = cpu_baseline(args.scene, settled)
+    if world == 1 and args.scene == "M":
+        line["dropin"] = dropin_record()
     print(json.dumps(line))
     if dist is not None:
         dist.barrier()

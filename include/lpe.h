@@ -155,6 +155,9 @@ typedef struct lpe_sph_stats {
      * lpe_sph_diag; all 0 off a slab */
     int32_t slabOwned, slabSlots;
     int32_t ghostsIn[2];
+    int32_t forcesGlobal;       /* forces-pass blocks whose neighbourhood exceeded the LDS image, summed
+                                   since the upload (their neighbours are gathered from global memory:
+                                   the same sums, slower) */
 } lpe_sph_stats;
 
 /* ------------------------------------------------------------------------ */

@@ -40,7 +40,9 @@ struct SphDev {
     float *rhoN = nullptr, *prN = nullptr;// the prelaunched sub-step's (swapped in when it is consumed)
     float4 *nbA = nullptr;        // sorted neighbour records (x, y, m, -)
     float4 *nbB = nullptr;        // (vx, vy, rho, p / rho^2)
-    uint4 *nlist = nullptr;       // per-slot neighbour list k - s (int16, 8 per uint4), [cap/8][cap_n]
+    uint4 *nlist = nullptr;       // per-slot neighbour list (int16, 8 per uint4), [cap/8][cap_n]: LDS indices of
+                                  // the forces pass's image, or slot offsets k - s (ncount's NL_OFFS bit)
+    void *fplans = nullptr;       // the density pass's block plans (Hood), for the forces pass's image
     float *rgrid = nullptr;       // renderer density grid, two W*H buffers (lpe_render_density)
     size_t cap_rgrid = 0;
     uint32_t *rmax = nullptr;     // renderer: max of the blurred grid (float bits)
@@ -144,7 +146,7 @@ enum StatusSlot {
     ST_RX_GHOST_L = 16,     // slab decomposition: most ghosts the left / right neighbour packed for this
     ST_RX_GHOST_R = 17,     //   rank in a sub-step of the current tick (sizes the next tick's exchange)
     ST_SLAB_CAPACITY = 18,  // slab decomposition: the received ghosts did not fit the rank's slots
-    ST_SPARE_19 = 19,
+    ST_FORCES_GLOBAL = 19,  // forces blocks whose neighbourhood did not fit the LDS image (global gathers)
     ST_COUNT = 20
 };
 

@@ -2569,9 +2569,6 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
         auto solve = [&](int st, int) {
             const int k = v.lstep(st);
             const int q1 = stepL[k + 1];
-#ifdef LPE_PGS_EMPTY          // profiling variants only: the step loop without its pairs
-            if (q1 >= 0) return;
-#endif
             for (int q = stepL[k] + (int)threadIdx.x; q < q1; q += STPB) {
                 const int4 p = pr[q];
                 const float4 m = pm[q];
@@ -2591,12 +2588,8 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
 #pragma unroll
                     for (int u = 0; u < U; u++) {
                         if (j0 + u >= p.y) break;
-#ifdef LPE_PGS_NOMATH         // profiling variants only: loads and stores without the row math
-                        n[u] += a[u].x; f[u] += c[u].y; vxA += a[u].z; vyB += c[u].w;
-#else
                         pgs_row_t<true>(a[u], c[u], m.x, m.y, m.z, m.w, hasA, hasB, mu, n[u], f[u], vxA, vyA, wA,
                                      vxB, vyB, wB);
-#endif
                         ln[p.x + j0 + u] = n[u];
                         lf[p.x + j0 + u] = f[u];
                     }

@@ -57,6 +57,8 @@ static constexpr int TPB = 256;
 static constexpr int SCAN_ELEMS = 1024;   // elements per scan block (256 thr x 4)
 static constexpr int MAX_KICK_BLOCKS = 2048;
 static constexpr int NLIST_CAP = 128;     // neighbours kept per particle (column-major list)
+static constexpr int NL_OFFS = 1 << 30;   // ncount flag: the list holds slot offsets k - s (else LDS indices)
+static constexpr int FCAP = 1024;         // records of the forces pass's LDS image (k_forces_couple)
 
 // kernel coefficients (metal:19-38), fp32
 __device__ __forceinline__ float poly6Coeff2D(float h) {
@@ -1222,6 +1224,10 @@ __device__ __forceinline__ void hood_spans(const Hood &hd, const int *lbnd, floa
 // [NLIST_CAP / 8][nstride]: each thread collects eight offsets in its 16-byte
 // LDS slot and writes them with one 16-byte store.  More than NLIST_CAP
 // neighbours: ncount > NLIST_CAP and the forces pass walks the bins.
+// fplans (NL only): the block's plan, for the forces pass to stage the same
+// image; when that image fits the forces pass's LDS (L <= FCAP) the list
+// holds LDS indices of the image instead of slot offsets, except for the
+// particles whose list came from a global walk (ncount's NL_OFFS bit).
 template <bool NL>
 __global__ void __launch_bounds__(HB)
 k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float eps, float stiffness,
@@ -1229,17 +1235,13 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
           const int32_t *__restrict__ start, const float4 *__restrict__ nbA, float2 *__restrict__ nbB,
           float *__restrict__ rho, float *__restrict__ pr, uint4 *__restrict__ nlist,
           int32_t *__restrict__ ncount, int32_t *__restrict__ status, const int32_t *__restrict__ sid,
-          const int32_t *__restrict__ refInv, const int32_t *__restrict__ ovl) {
+          const int32_t *__restrict__ refInv, const int32_t *__restrict__ ovl, Hood *__restrict__ fplans) {
     __shared__ float4 lrec[HCAP + 4];                     // + 4: the span walk reads up to 3 past a span
     __shared__ int lbnd[HBND];
-    __shared__ uint4 lnl[NL ? HB : 1];                    // per thread: the current group of 8 offsets
-#ifdef LPE_DENSITY_PLAIN      // (A/B variant: plain block order, as the forces pass)
-    const int lb = (int)blockIdx.x < (n + HB - 1) / HB ? (int)blockIdx.x : -1;
-#else
+    __shared__ uint4 lnl[NL ? 2 * HB : 1];                // per thread: a ring of two groups of 8 entries
     // (a slab rank's grid is sized by its slot capacity: the XCD runs are laid
     // out over the slots in use, so every XCD gets its share)
     const int lb = xcd_block(((nptr ? min(*nptr, n) : n) + HB - 1) / HB);
-#endif
     if (lb < 0) return;                                   // whole block idle
     const int nn = nptr ? *nptr : n;
     const int s0 = lb * HB, s1 = min(s0 + HB, nn);
@@ -1251,9 +1253,14 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
         Hood p;
         hood_plan(p, s0, s1, nbA, eps, cs, W, H, ox, oy, start);
         if (p.ok) hood_stage(p, lrec, lbnd, nbA, start, s0);
-        if (threadIdx.x == 0) hd = p;
+        if (threadIdx.x == 0) {
+            hd = p;
+            if (NL && fplans) fplans[lb] = p;
+        }
     }
     __syncthreads();
+    // the list as LDS indices of the forces pass's image (block-uniform)
+    const bool lidx = NL && fplans && hd.ok && hd.L <= FCAP;
     // every lane stays to the end (the span walk's trip counts are wave
     // reductions); lanes past the block's last slot walk nothing
     const int s = s0 + threadIdx.x;
@@ -1268,7 +1275,9 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     const float reach = walk_reach(h, cs);
     float acc = 0.0f;
     int cnt = 0;
-    int16_t *grp = reinterpret_cast<int16_t *>(&lnl[NL ? threadIdx.x : 0]);
+    int16_t *ring = reinterpret_cast<int16_t *>(&lnl[NL ? 2 * threadIdx.x : 0]);
+    // the ring's group g, as one 16-byte word
+    auto group = [&](int g) { return lnl[NL ? 2 * threadIdx.x + (g & 1) : 0]; };
     // one candidate: r^2 < h^2 adds m * poly6 (h^2 - r^2)^3; otherwise +0,
     // which leaves the non-negative sum unchanged bit for bit
     auto term = [&](const float4 &o, bool valid) {
@@ -1290,11 +1299,11 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
         const float t = o.z * (poly6 * diff * diff * diff);
         acc += valid ? t : 0.0f;
     };
-    // a neighbour for the forces pass: its slot offset k - s
+    // a neighbour for the forces pass (its image index or slot offset k - s)
     auto emit = [&](int code, bool ok) {
         if (cnt < NLIST_CAP && ok) {
-            grp[cnt & 7] = (int16_t)code;
-            if ((cnt & 7) == 7) nlist[(size_t)(cnt >> 3) * nstride + s] = lnl[threadIdx.x];
+            ring[cnt & 15] = (int16_t)code;
+            if ((cnt & 7) == 7) nlist[(size_t)(cnt >> 3) * nstride + s] = group(cnt >> 3);
         } else {
             cnt = NLIST_CAP;                              // overflow: forces walks the bins
         }
@@ -1324,28 +1333,44 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
                     sb[r] = sb[r + 1]; se[r] = se[r + 1]; sh[r] = sh[r + 1];
                     sb[r + 1] = se[r + 1] = 0;
                 }
+        int selfL[3];                                     // the particle's own LDS index, per span
+#pragma unroll
+        for (int r = 0; r < 3; r++) selfL[r] = s - sh[r];
 #pragma unroll
         for (int r = 0; r < 3; r++) {
             const int b = sb[r], len = se[r] - b;
             int lmin, lmax;
             wave_minmax(len, lmin, lmax);
             if (lmax == 0) break;                         // (later spans are empty too)
+            // (the list without branches per candidate: every candidate's code
+            // is written to the ring at cnt, which advances only for a
+            // neighbour -- a trip adds at most 4 < 8, so the group it
+            // completes is flushed after the trip, before the ring comes
+            // round to it again)
             auto trip = [&](int t, bool masked) {
                 const int a = min(b + t, HCAP);           // past every span: reads the pad, masked
                 float4 o[4];
 #pragma unroll
                 for (int j = 0; j < 4; j++) o[j] = lrec[a + j];
+                const int c0 = cnt;
+                // the trip's first code (image index or slot offset); a slot
+                // offset outside int16 overflows the list, for the whole trip
+                const int cb = lidx ? b + t : b + t + sh[r] - s;
+                const int lim = (lidx || (cb >= -32768 && cb + 3 <= 32767)) ? NLIST_CAP : 0;
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
                     const bool valid = !masked || t + j < len;
                     if (NL) {
                         const bool in = term(o[j], valid);
-                        const int oc = b + t + j + sh[r] - s;
-                        if (in && oc != 0) emit(oc, oc >= -32768 && oc <= 32767);   // (not itself: metal:360-366)
+                        ring[cnt & 15] = (int16_t)(cb + j);
+                        if (in && b + t + j != selfL[r])                          // (not itself: metal:360-366)
+                            cnt = cnt < lim ? cnt + 1 : NLIST_CAP + 1;           // (past: forces walks the bins)
                     } else {
                         term0(o[j], valid);
                     }
                 }
+                if (NL && (cnt >> 3) != (c0 >> 3) && cnt <= NLIST_CAP)
+                    nlist[(size_t)(c0 >> 3) * nstride + s] = group(c0 >> 3);
             };
             int t = 0;
             for (; t + 4 <= lmin; t += 4) trip(t, false);
@@ -1370,8 +1395,8 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     }
     if (!live) return;
     if (NL) {
-        if (cnt <= NLIST_CAP && (cnt & 7)) nlist[(size_t)(cnt >> 3) * nstride + s] = lnl[threadIdx.x];
-        ncount[s] = cnt;
+        if (cnt <= NLIST_CAP && (cnt & 7)) nlist[(size_t)(cnt >> 3) * nstride + s] = group(cnt >> 3);
+        ncount[s] = cnt | ((!lidx || slow) ? NL_OFFS : 0);
     }
     float pres = stiffness * (acc - restDensity);
     if (pres < 0.f) pres = 0.f;
@@ -1636,10 +1661,14 @@ struct SphStepParams {
 };
 
 // computeForces + velocityVerletFinish + impulse + push-out; reads the sorted
-// records, writes P.  The block stages the same neighbourhood as the density
-// pass (same HB-slot blocks, same plan), now with both records of every
-// slot, so the neighbour list's LDS indices address the staged image and the
-// gathers never leave the CU.
+// records, writes P.  The block is the density pass's block (same HB slots,
+// same plan, fplans): it stages the records of that neighbourhood -- both
+// of every slot, 32 B -- as an LDS image of at most FCAP records, and the
+// neighbour list (LDS indices, k_density) gathers from it without leaving the
+// CU.  A block whose neighbourhood is larger, and a particle whose list came
+// from a global walk (NL_OFFS), gather from global memory by slot offsets.
+// After the fluid loop the image's LDS is reused for the coupling's
+// per-block pair list (CouplePool).
 #ifndef LPE_FORCES_MINW
 #define LPE_FORCES_MINW 4
 #endif
@@ -1656,6 +1685,7 @@ __device__ __forceinline__ void merge_prestats_dev(int32_t *__restrict__ st, int
     atomicOr(&st[ST_CAP_OVERFLOW], pre[ST_CAP_OVERFLOW]);
     atomicOr(&st[ST_BUCKET_OVERFLOW], pre[ST_BUCKET_OVERFLOW]);
     atomicAdd(&st[ST_STAGE_FALLBACK], pre[ST_STAGE_FALLBACK]);
+    atomicAdd(&st[ST_FORCES_GLOBAL], pre[ST_FORCES_GLOBAL]);
     atomicAdd(&st[ST_OVER_CAP_TOTAL], pre[ST_OVER_CAP_TOTAL]);
     atomicMax(&st[ST_MAX_OCC_TOTAL], pre[ST_MAX_OCC_TOTAL]);
     for (int k = 0; k < ST_COUNT; k++) pre[k] = 0;
@@ -1672,7 +1702,15 @@ __device__ int g_ftrace_on;
 #define FTR(k) do { if (g_ftrace_on && threadIdx.x == 0) g_ftrace[lb * 8 + (k)] = wall_clock64(); } while (0)
 #else
 #define FTR(k) do {} while (0)
-#endif   // coupling pairs shared by a block (k_forces_couple)
+#endif
+
+// the coupling's per-block arrays, laid over the image once the fluid loop is done
+struct CouplePool {
+    PairGeo geo[PAIR_CAP];
+    CoupleIn in[HB];
+    unsigned char flag[PAIR_CAP];
+};
+static_assert(sizeof(CouplePool) <= sizeof(float4) * 2 * FCAP, "the coupling pool fits the forces image");
 
 __global__ void __launch_bounds__(HB, LPE_FORCES_MINW)
 k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict__ gp,
@@ -1683,7 +1721,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                 const int32_t *__restrict__ rbinStart, const int32_t *__restrict__ rbinList,
                 const float4 *__restrict__ rbinAabb,
                 unsigned long long *__restrict__ acq,
-                int32_t *__restrict__ status, KickNext kn) {
+                int32_t *__restrict__ status, KickNext kn, const Hood *__restrict__ fplans) {
     // plain block order (blocks go round robin over the XCDs): the costly
     // blocks, the particles in and around the rigid pile, are one spatial
     // run that an XCD-contiguous mapping (xcd_block) would put on one XCD
@@ -1697,6 +1735,15 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         return;
     }
     FTR(0);
+    // the image: records [0, FCAP) nbA, [FCAP, 2 FCAP) nbB; then the CouplePool
+    __shared__ float4 fimg[2 * FCAP];
+    __shared__ int hraw[64];
+    __shared__ int pRig[PAIR_CAP];
+    __shared__ unsigned char pOwn[PAIR_CAP];
+    __shared__ int pCount;
+    CouplePool &pool = *reinterpret_cast<CouplePool *>(fimg);
+    if (threadIdx.x == 0) pCount = 0;
+    if (fplans) hood_fetch(fplans, lb, hraw);
     const GridParams g = *gp;
     const float cs = g.cellSize;
     // every lane stays to the end (the coupling pairs are shared by the
@@ -1740,84 +1787,78 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         float r2 = dx * dx + dy * dy;
         if (r2 < sp.minDist) return;
         if (r2 >= h_ij2) return;
-#ifdef LPE_DIAG_FASTDIV      // profiling variants only: approximate division / sqrt (not bit-exact)
-        float r = __builtin_amdgcn_sqrtf(r2);
-#else
         float r = sqrtf(r2);
-#endif
         float rhoj = ob.z;
         if (rhoj < sp.minDens || !rhoi_ok) return;
         float mj = oa.z;
         float term = pti + ob.w;
         float diff = (h_ij - r);
         float wSpiky = spF * (diff * diff);
-#ifdef LPE_DIAG_FASTDIV
-        const float ir = __builtin_amdgcn_rcpf(r);
-        float rx = dx * ir, ry = dy * ir;
-#else
         float rx = dx / r, ry = dy / r;
-#endif
         float fxPress = -mj * term * wSpiky;
         float fx = fxPress * rx;
         float fy = fxPress * ry;
         float vx_ij = vxi - ob.x, vy_ij = vyi - ob.y;
         float wVisc = lapC * diff;
-#ifdef LPE_DIAG_FASTDIV
-        float fVisc = sp.viscosity * mj * (wVisc * __builtin_amdgcn_rcpf(rhoj));
-#else
         float fVisc = sp.viscosity * mj * (wVisc / rhoj);
-#endif
         fx -= fVisc * vx_ij;
         fy -= fVisc * vy_ij;
         sumFx += fx;
         sumFy += fy;
     };
-#ifdef LPE_DIAG_NONBR        // profiling variants only: no fluid pair forces
-    const int cnt = 0;
-#else
-    const int cnt = live ? ncount[s] : 0;
-#endif
-    // the neighbour list's first two words, in flight during phase 0
+    const int craw = live ? ncount[s] : 0;
+    const int cnt = craw & ~NL_OFFS;
+    const bool offs = (craw & NL_OFFS) != 0;      // the list holds slot offsets (else image indices)
+    // the neighbour list's first two words, in flight during the staging
     const size_t ns = (size_t)sp.nstride;
     uint4 gA = make_uint4(0u, 0u, 0u, 0u), gB = gA;
     if (cnt > 0 && cnt <= NLIST_CAP) gA = nlist[s];   // entries 0-7
     if (cnt > 8 && cnt <= NLIST_CAP) gB = nlist[ns + s];   // entries 8-15
+    __syncthreads();                                  // (the plan, pCount)
+    const Hood &hd = *reinterpret_cast<const Hood *>(hraw);
+    const bool img = fplans && hd.ok && hd.L <= FCAP;   // (block-uniform; k_density's lidx)
+    if (img) {
+        // the image, one pass of asynchronous global -> LDS copies (retired
+        // by the barrier after phase 0)
+        const int wbase = threadIdx.x & ~63;
+#pragma unroll
+        for (int u = 0; u < FCAP / HB; u++) {
+            const int f0 = u * HB;
+            if (f0 >= hd.L) break;
+            const int f = f0 + threadIdx.x;
+            int d = hd.ss[0] - hd.l[0];
+#pragma unroll
+            for (int i = 1; i < 6; i++)
+                if (f >= hd.l[i]) d = hd.ss[i] - hd.l[i];
+            const int src = f < hd.L ? f + d : s0;        // lanes past the end copy a valid record
+            __builtin_amdgcn_global_load_lds((glb_void_t *)(nbA + src), (lds_void_t *)(fimg + f0 + wbase), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((glb_void_t *)(nbB + src), (lds_void_t *)(fimg + FCAP + f0 + wbase), 16,
+                                             0, 0);
+        }
+    } else if (fplans && threadIdx.x == 0) {
+        atomicAdd(&status[ST_FORCES_GLOBAL], 1);
+    }
     // ---- coupling, phase 0: the rigid candidates (positions only) --------
     // (impulse solver only if R > 0, fluid.cpp:910; push-out always).  The
     // (particle, rigid) pairs whose AABB test passes are few and clustered
     // (particles in and around the rigid pile), so they are spread over the
     // block: each wave appends its particles' pairs to the block's list (one
     // LDS atomic per wave; a particle's pairs stay consecutive, in candidate
-    // = ascending rigid order); the waves that finish their fluid forces
-    // first compute the pairs' geometry (couple_geom) while the others are
-    // still summing theirs; after a barrier the impulse halves (couple_imp,
-    // which need the finished velocities) go round robin, and each particle
+    // = ascending rigid order); after the fluid loop every thread computes
+    // pairs' geometry (couple_geom), then their impulse halves (couple_imp,
+    // which need the finished velocities), round robin, and each particle
     // folds its own pairs in order.  A block with more than PAIR_CAP pairs
     // couples per thread instead (couple_both, the same arithmetic).
-    __shared__ int pRig[PAIR_CAP];
-    __shared__ unsigned char pOwn[PAIR_CAP], pFlag[PAIR_CAP];
-    __shared__ PairGeo pGeo[PAIR_CAP];
-    __shared__ CoupleIn lIn[HB];
-    __shared__ int pCount, pNext, pWaves;
-    if (threadIdx.x == 0) { pCount = 0; pNext = 0; pWaves = 0; }
-    __syncthreads();
     const int lane = (int)threadIdx.x & 63;
     int nh = 0, off = 0;
     {
         int k0 = 0, k1 = 0;
-#ifdef LPE_DIAG_NOCOUPLE     // profiling variants only: no rigid coupling
-        if (false) {
-#else
         if (cp.nr > 0 && live) {
-#endif
             float fbx = fminf(fmaxf(floorf(xi / cp.bcs) - (float)cp.bx0, 0.f), (float)(cp.bW - 1));
             float fby = fminf(fmaxf(floorf(yi / cp.bcs) - (float)cp.by0, 0.f), (float)(cp.bH - 1));
             int bin = (int)fby * cp.bW + (int)fbx;
             k0 = rbinStart[bin]; k1 = rbinStart[bin + 1];
             if (sp.diag && k1 > k0) atomicAdd(&status[ST_RIGID_CAND], k1 - k0);
-#ifdef LPE_FTRACE
-            if (g_ftrace_on) atomicMax(&g_ftrace[lb * 8 + 7], (unsigned long long)(k1 - k0));
-#endif
         }
         // AABB hits among the bin's candidates (bin-ordered AABBs, 8 loads in
         // flight); the first 64 candidates' hits kept as a mask
@@ -1853,19 +1894,13 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
             for (int k = k0 + 64; k < k1; k++)             // (a bin of more than 64 candidates)
                 if (aabb_holds(rbinAabb[k], xi, yi)) { pRig[q] = rbinList[k]; pOwn[q] = (unsigned char)threadIdx.x; q++; }
         }
-        // the particle's coupling inputs but the velocity (set after the
-        // fluid forces); pow only for a particle with candidates
-        CoupleState st0;
-        st0.x = xi; st0.y = yi; st0.vx = st0.vy = 0.f; st0.mass = meA.z; st0.rho = rhoi; st0.p = pi;
-        st0.vhx = st0.vhy = st0.ax = st0.ay = 0.f;
-        lIn[threadIdx.x] = couple_in(st0, cp, cp.nr > 0 && nh > 0);
-        __threadfence_block();                                 // (the LDS writes before the count)
-        if (lane == 0) atomicAdd(&pWaves, 1);
     }
     if (sp.diag && live) {
         atomicAdd(&status[ST_NEIGH], cnt);
         if (cnt > NLIST_CAP) atomicAdd(&status[ST_NL_OVERFLOW], 1);
     }
+    __syncthreads();                                  // (the image, the block's pair list)
+    FTR(1);
     if (!live) {
     } else if (cnt > NLIST_CAP && sp.refInv &&
                ref_cap_near(sp.ovl, sp.ox + (int)((__float_as_int(meA.w) >> 2) & 0x7fff),
@@ -1879,20 +1914,26 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                         [&](int k, const FRec &o) { if (k != s) pair(o.a, o.b); });
     } else if (cnt <= NLIST_CAP) {
         // the density pass's list: the r^2 < h^2 neighbours in canonical
-        // order as slot offsets, so the heavy pair math runs only on real
-        // neighbours.  Software-pipelined in quads: the records of the next
-        // quad (and the list word after the next) are in flight while a quad
-        // is computed, so a wave pays about one memory latency per quad
-        // instead of two (list word, then records) plus the math.
+        // order, so the heavy pair math runs only on real neighbours.
+        // Software-pipelined in quads: the records of the next quad (and the
+        // list word after the next) are in flight while a quad is computed.
         struct Quad { FRec r[4]; };
         // records of list entries j .. j+3 held by words (wa, wb) of a list group
         auto quad = [&](uint32_t wa, uint32_t wb, int j) {
             const uint32_t w2[4] = {wa & 0xffffu, wa >> 16, wb & 0xffffu, wb >> 16};
             Quad q;
+            if (!offs) {                              // image indices
 #pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const int k = s + (j + u < cnt ? (int)(int16_t)w2[u] : 0);   // (past the end: itself, unused)
-                q.r[u] = FRec{nbA[k], nbB[k]};
+                for (int u = 0; u < 4; u++) {
+                    const int k = j + u < cnt ? (int)w2[u] : 0;
+                    q.r[u] = FRec{fimg[k], fimg[FCAP + k]};
+                }
+            } else {                                  // slot offsets (past the end: itself, unused)
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const int k = s + (j + u < cnt ? (int)(int16_t)w2[u] : 0);
+                    q.r[u] = FRec{nbA[k], nbB[k]};
+                }
             }
             return q;
         };
@@ -1914,12 +1955,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                            [&](int k, int) { return FRec{nbA[k], nbB[k]}; },
                            [&](int k, const FRec &o) { if (k != s) pair(o.a, o.b); });
     }
-#ifdef LPE_FTRACE
-    if (g_ftrace_on) {
-        atomicMax(&g_ftrace[lb * 8 + 5], wall_clock64());
-        atomicMax(&g_ftrace[lb * 8 + 6], (unsigned long long)cnt);
-    }
-#endif
+    FTR(5);
     CoupleState st;
     st.x = xi; st.y = yi;
     st.vhx = S.vhx[sl]; st.vhy = S.vhy[sl];
@@ -1928,38 +1964,8 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     st.vx = st.vhx + sp.hdt * st.ax;
     st.vy = st.vhy + sp.hdt * st.ay;
     st.mass = meA.z; st.rho = rhoi; st.p = pi;
-    lIn[threadIdx.x].vx = st.vx;
-    lIn[threadIdx.x].vy = st.vy;
     const float4 *rc = raabb + cp.nr;                 // the compact records (k_rig_couple)
-    // ---- coupling, phase 2: the pairs' geometry, by whichever waves are here
-    if (cp.nr > 0) {
-        if (lane == 0)                                // every wave of the block has appended its pairs
-            while (__hip_atomic_load(&pWaves, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < HB / 64)
-                __builtin_amdgcn_s_sleep(1);
-        const int tot = __shfl(lane == 0 ? __hip_atomic_load(&pCount, __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_WORKGROUP) : 0, 0);
-        if (tot <= PAIR_CAP) {
-            for (;;) {
-                int q0 = 0;
-                if (lane == 0) q0 = atomicAdd(&pNext, 64);
-                q0 = __shfl(q0, 0);
-                if (q0 >= tot) break;
-                const int q = q0 + lane;
-                if (q < tot) {
-                    const int o = pOwn[q];
-                    PairGeo ge;
-                    pFlag[q] = (unsigned char)couple_geom(lIn[o].x, lIn[o].y, cp, true, rc, pRig[q], ge);
-                    pGeo[q] = ge;
-                }
-            }
-        }
-    }
-    __syncthreads();                                  // (fluid forces, geometry and lIn complete)
-    FTR(1);
-    const int total = pCount;
-#ifdef LPE_FTRACE
-    if (g_ftrace_on && threadIdx.x == 0) g_ftrace[lb * 8 + 4] = total;
-#endif
+    const int total = pCount;                         // (block-uniform: final since the barrier)
     if (total > PAIR_CAP) {
         if (live) {
             const float fbx = fminf(fmaxf(floorf(st.x / cp.bcs) - (float)cp.bx0, 0.f), (float)(cp.bW - 1));
@@ -1969,27 +1975,41 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                         status);
         }
     } else {
-        // ---- phase 3: the impulse halves (finished velocities), round robin
-        for (int q = threadIdx.x; q < total; q += HB)
-            if (pFlag[q] & PT_WANT) {
-                float fx, fy;
-                couple_imp(lIn[pOwn[q]], cp, sp.dt, rc, pRig[q], pGeo[q].pen, pGeo[q].nx, pGeo[q].ny, acq,
-                           status, fx, fy);
-                pGeo[q].nx = fx;                      // (the fold's fluid-force term)
-                pGeo[q].ny = fy;
-                pFlag[q] = (unsigned char)(pFlag[q] | PT_IMP);
+        CoupleAcc a;
+        if (total > 0) {
+            __syncthreads();                          // (every read of the image done: the pool replaces it)
+            // the particle's coupling inputs (pow only for a particle with hits)
+            pool.in[threadIdx.x] = couple_in(st, cp, cp.nr > 0 && nh > 0);
+            __syncthreads();
+            // ---- the pairs' geometry, round robin
+            for (int q = threadIdx.x; q < total; q += HB) {
+                const int o = pOwn[q];
+                PairGeo ge;
+                pool.flag[q] = (unsigned char)couple_geom(pool.in[o].x, pool.in[o].y, cp, true, rc, pRig[q], ge);
+                pool.geo[q] = ge;
             }
-        if (total > 0) __syncthreads();
-        FTR(2);
-        if (live) {
-            CoupleAcc a;
-            for (int q = off; q < off + nh; q++) {
-                const PairGeo ge = pGeo[q];
-                a.fold(PairTerm{ge.ax, ge.ay, ge.nx, ge.ny}, pFlag[q]);
-            }
-            couple_finish(st, cp, a);
+            __syncthreads();
+            FTR(2);
+            // ---- the impulse halves (finished velocities), round robin
+            for (int q = threadIdx.x; q < total; q += HB)
+                if (pool.flag[q] & PT_WANT) {
+                    float fx, fy;
+                    couple_imp(pool.in[pOwn[q]], cp, sp.dt, rc, pRig[q], pool.geo[q].pen, pool.geo[q].nx,
+                               pool.geo[q].ny, acq, status, fx, fy);
+                    pool.geo[q].nx = fx;                  // (the fold's fluid-force term)
+                    pool.geo[q].ny = fy;
+                    pool.flag[q] = (unsigned char)(pool.flag[q] | PT_IMP);
+                }
+            __syncthreads();
+            if (live)
+                for (int q = off; q < off + nh; q++) {
+                    const PairGeo ge = pool.geo[q];
+                    a.fold(PairTerm{ge.ax, ge.ay, ge.nx, ge.ny}, pool.flag[q]);
+                }
         }
+        if (live) couple_finish(st, cp, a);
     }
+    FTR(4);
     if (live) {
         // a sub-step that kicks the next one (kn.on) leaves only what the next
         // hash reads from P (velocity, mass, id: the kicked position and
@@ -2054,9 +2074,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
             if (v) atomicAdd(&kn.fk.rowtot[rowBase + threadIdx.x], v);
         }
     }
-#ifdef LPE_FTRACE
-    if (g_ftrace_on) atomicMax(&g_ftrace[lb * 8 + 3], wall_clock64());
-#endif
+    FTR(3);
 }
 #ifdef LPE_FTRACE
 extern "C" int lpe_ftrace(int on, unsigned long long *host, int n) {
@@ -2503,7 +2521,7 @@ static void sph_free(SphDev &d) {
     void *ptrs[] = {d.ovl, d.rho, d.pr, d.rhoN, d.prN, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.refInv, d.stage, d.count, d.start, d.cursor,
                     d.rowtot, d.bucket, d.bovf,
                     d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.raabb, d.accum, d.acq, d.rbinStart, d.rgrid, d.rmax,
-                    d.rbinList, d.rbinCount, d.coupleBody, d.plans};
+                    d.rbinList, d.rbinCount, d.coupleBody, d.plans, d.fplans};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     hipEvent_t evs[] = {d.preReady, d.preDone, d.fbgDone};
     for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
@@ -2719,7 +2737,7 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     pstate_free(d.P);
     pstate_free(d.S);
     void *ptrs[] = {d.rho, d.pr, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.bboxPart, d.refInv,
-                    d.stage, d.rhoN, d.prN};
+                    d.stage, d.rhoN, d.prN, d.fplans};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     size_t N = (size_t)std::max(n, 1);
     int st = pstate_alloc(ctx, d.P, N, true);
@@ -2734,6 +2752,7 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     LPE_HIP(ctx, hipMalloc((void **)&d.nbB, sizeof(float4) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.nlist, sizeof(uint4) * N * (NLIST_CAP / 8)));
     LPE_HIP(ctx, hipMalloc((void **)&d.ncount, sizeof(int32_t) * N));
+    LPE_HIP(ctx, hipMalloc(&d.fplans, sizeof(Hood) * ((N + HB - 1) / HB)));
     LPE_HIP(ctx, hipMalloc((void **)&d.key, sizeof(uint32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpId, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpOld, sizeof(int32_t) * N));
@@ -3137,12 +3156,12 @@ static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr, float *rho, flo
         LPE_KERNEL(ctx, "k_density", k_density<true>, dim3(xcd_grid(nblk(n, HB))), dim3(HB), 0, ctx->stream, n,
                    nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
                    c.restDensity, d.W, d.H, d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)d.nbB,
-                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d), d.ovl_cur);
+                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d), d.ovl_cur, (Hood *)d.fplans);
     else
         LPE_KERNEL(ctx, "k_density", k_density<false>, dim3(xcd_grid(nblk(n, HB))), dim3(HB), 0, ctx->stream, n,
                    nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
                    c.restDensity, d.W, d.H, d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)d.nbB,
-                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d), d.ovl_cur);
+                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d), d.ovl_cur, (Hood *)nullptr);
     LPE_CHECK_LAUNCH(ctx, "k_density");
     return LPE_OK;
 }
@@ -3401,7 +3420,7 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
                            (step == 0 && pre) ? d.gp + 1 : d.gp,
                            d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart, d.rbinList,
                            rbin_aabb(d),
-                           d.acq, d.status, kn);
+                           d.acq, d.status, kn, (const Hood *)d.fplans);
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
         if (sh) sh->cur = 1 - sh->cur;               // P's slots are now the ones this pass wrote
         if (hook) {                                  // (lpe_world_tick: the rigid detection)
@@ -3556,6 +3575,7 @@ extern "C" int lpe_sph_get_stats(lpe_ctx *ctx, lpe_sph_stats *out) {
     out->rigidCandidates = status[ST_RIGID_CAND];
     out->neighbours = status[ST_NEIGH];
     out->stageFallback = status[ST_STAGE_FALLBACK];
+    out->forcesGlobal = status[ST_FORCES_GLOBAL];
     out->overCapCells = status[ST_OVER_CAP];
     out->refUndefined = status[ST_REF_UB];
     out->overCapCellsTotal = status[ST_OVER_CAP_TOTAL];

@@ -85,7 +85,7 @@ class SphStats(C.Structure):
                 ("stageFallback", C.c_int32), ("overCapCells", C.c_int32), ("refUndefined", C.c_int32),
                 ("overCapCellsTotal", C.c_int32), ("maxCellOccupancyTotal", C.c_int32),
                 ("haloWire", C.c_int32 * 2), ("slabOwned", C.c_int32), ("slabSlots", C.c_int32),
-                ("ghostsIn", C.c_int32 * 2)]
+                ("ghostsIn", C.c_int32 * 2), ("forcesGlobal", C.c_int32)]
 
     def as_dict(self):
         return {k: (list(getattr(self, k)) if k in ("haloWire", "ghostsIn") else getattr(self, k))

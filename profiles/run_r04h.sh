@@ -10,3 +10,6 @@ GPU_MAX_HW_QUEUES=4 timeout -k 10 300 python -u profiles/slab_probe.py --loop > 
 GPU_MAX_HW_QUEUES=4 timeout -k 10 500 python -u bench.py --no-extras --no-density-microbench --no-cpu-baseline > gpurun_out/r04h_bench_q4.json 2> gpurun_out/r04h_bench_q4.err || exit 1
 timeout -k 10 300 python -u bench.py --loopback 8 --scene C5 --prep 60 --warmup 5 --steps 20 > gpurun_out/r04h_loop_c5.json 2> gpurun_out/r04h_loop_c5.err || exit 1
 timeout -k 10 600 python -u profiles/dropin_timing.py > gpurun_out/r04h_dropin.json 2> gpurun_out/r04h_dropin.err || exit 1
+timeout -k 10 200 python -u profiles/small_probe.py --scene C1 > gpurun_out/r04h_small_c1.json 2> gpurun_out/r04h_small_c1.err || exit 1
+timeout -k 10 200 python -u profiles/small_probe.py --scene C2 > gpurun_out/r04h_small_c2.json 2> gpurun_out/r04h_small_c2.err || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/r04h_prof_c1 -o c1 -- python3 profiles/small_probe.py --scene C1 --rounds 1 > gpurun_out/r04h_prof_c1.log 2>&1 || exit 1
