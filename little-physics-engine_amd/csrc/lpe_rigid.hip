@@ -2208,14 +2208,17 @@ k_group_lists(const int32_t *__restrict__ npptr, const int32_t *__restrict__ cou
 // lowest colour free on the pair's movable bodies), the pair's rank and row
 // offset inside its (group, colour), the group's colour sizes.  The bodies'
 // colour masks live in LDS by stripe-list slot (the group's bodies lie in
-// its one or two stripes).
+// its one or two stripes).  The colouring is one sequential chain, run by
+// the whole wave on wave-uniform values: the chunk's pair bodies and row
+// counts are read across lanes (readlane), colour c's pair / row counters
+// live in lane c, and the next pair's masks are loaded before the current
+// pair's are stored (a body the two pairs share takes the stored value:
+// forwarding), so a pair costs its compare / select chain, not LDS round
+// trips.
 __global__ void __launch_bounds__(64)
 k_group_colour(const int32_t *__restrict__ counts, const int2 *__restrict__ pairs,
                const int32_t *__restrict__ ccount, StripeBufs sb) {
     extern __shared__ unsigned long long used[];             // per stripe-list slot of the group's stripes
-    __shared__ int qa[64], qb[64], qn[64], qc[64];
-    __shared__ int cpairs[SCOLS], crows[SCOLS];
-    __shared__ int sfault;
     const int g = (int)blockIdx.x;
     const int S = counts[12];
     if (g >= S) return;
@@ -2223,55 +2226,68 @@ k_group_colour(const int32_t *__restrict__ counts, const int2 *__restrict__ pair
     const int s = (g >> 1) * 2 + (g & 1);               // band j: stripes 2j, 2j+1; seam j: 2j+1, 2j+2
     const int u0 = sb.sbStart[s], u1 = sb.sbStart[min(s + 2, S)];
     for (int i = lane; i < u1 - u0; i += 64) used[i] = 0ull;
-    cpairs[lane] = 0; crows[lane] = 0;
-    if (lane == 0) sfault = 0;
     __syncthreads();
     const int g0 = sb.gstart[g], g1 = sb.gstart[g + 1];
-    int ncol = 0;
+    int ncol = 0, fault = 0;
+    int cp = 0, cr = 0;                                   // lane c: colour c's pairs and rows so far
     for (int c0 = g0; c0 < g1; c0 += 64) {
         const int t = c0 + lane;
-        int p = -1;
+        int p = -1, ma = -1, mb = -1, mn = 0;
         if (t < g1) {
             p = sb.glist[t];
             const int2 pr = pairs[p];
             const int f = sb.pflag[p];
-            qa[lane] = (f & 2) ? sb.bpos[pr.x] - u0 : -1;
-            qb[lane] = (f & 4) ? sb.bpos[pr.y] - u0 : -1;
-            qn[lane] = ccount[p];
+            ma = (f & 2) ? sb.bpos[pr.x] - u0 : -1;
+            mb = (f & 4) ? sb.bpos[pr.y] - u0 : -1;
+            mn = ccount[p];
         }
-        __syncthreads();
-        if (lane == 0) {
-            const int m = min(64, g1 - c0);
-            for (int i = 0; i < m; i++) {
-                const int a = qa[i], b = qb[i];
-                const unsigned long long forb = (a >= 0 ? used[a] : 0ull) | (b >= 0 ? used[b] : 0ull);
-                const int c = forb == ~0ull ? 0 : __ffsll((long long)~forb) - 1;
-                if (forb == ~0ull) sfault = 1;
-                if (a >= 0) used[a] |= 1ull << c;
-                if (b >= 0) used[b] |= 1ull << c;
-                qc[i] = c;
-                ncol = max(ncol, c + 1);
-                // ranks and row offsets in ascending order (qa / qb reused)
-                qa[i] = cpairs[c]++;
-                qb[i] = crows[c];
-                crows[c] += qn[i];
-            }
+        const int m = min(64, g1 - c0);
+        int myc = 0, myrank = 0, myrow = 0;
+        int a = __builtin_amdgcn_readlane(ma, 0), b = __builtin_amdgcn_readlane(mb, 0);
+        unsigned long long ua = a >= 0 ? used[a] : 0ull, ub = b >= 0 ? used[b] : 0ull;
+        for (int i = 0; i < m; i++) {
+            // the next pair's bodies and masks (loads issued before this pair's stores)
+            const int a2 = i + 1 < m ? __builtin_amdgcn_readlane(ma, i + 1) : -1;
+            const int b2 = i + 1 < m ? __builtin_amdgcn_readlane(mb, i + 1) : -1;
+            // (lane 0 loads a2's mask, lane 1 b2's: a per-lane load whose wait
+            // falls after this pair's chain, where the lanes are read)
+            const int la = lane == 0 ? a2 : (lane == 1 ? b2 : -1);
+            const unsigned long long lu = la >= 0 ? used[la] : 0ull;
+            const unsigned long long forb = ua | ub;
+            const int c = forb == ~0ull ? 0 : __ffsll((long long)~forb) - 1;
+            fault |= forb == ~0ull;
+            const unsigned long long bit = 1ull << c;
+            const unsigned long long na = ua | bit, nb2 = ub | bit;
+            if (a >= 0) used[a] = na;
+            if (b >= 0) used[b] = nb2;
+            unsigned long long ua2 = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(lu >> 32), 0) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readlane((int)lu, 0);
+            unsigned long long ub2 = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(lu >> 32), 1) << 32) |
+                                     (uint32_t)__builtin_amdgcn_readlane((int)lu, 1);
+            if (a2 >= 0 && a2 == a) ua2 = na;
+            if (a2 >= 0 && a2 == b) ua2 = nb2;
+            if (b2 >= 0 && b2 == a) ub2 = na;
+            if (b2 >= 0 && b2 == b) ub2 = nb2;
+            ncol = max(ncol, c + 1);
+            // rank and row offset in ascending order
+            const int rank = __builtin_amdgcn_readlane(cp, c), row = __builtin_amdgcn_readlane(cr, c);
+            const int n = __builtin_amdgcn_readlane(mn, i);
+            if (lane == c) { cp += 1; cr += n; }
+            if (lane == i) { myc = c; myrank = rank; myrow = row; }
+            a = a2; b = b2; ua = ua2; ub = ub2;
         }
-        __syncthreads();
         if (t < g1) {
-            sb.pcolg[p] = qc[lane];
-            sb.prank[p] = qa[lane];
-            sb.prowoff[p] = qb[lane];
+            sb.pcolg[p] = myc;
+            sb.prank[p] = myrank;
+            sb.prowoff[p] = myrow;
         }
-        __syncthreads();
     }
-    ncol = __shfl(ncol, 0);
     int32_t *gc = sb.gcnt + (size_t)g * SCOLS * 2;
-    gc[2 * lane] = cpairs[lane];
-    gc[2 * lane + 1] = crows[lane];
+    gc[2 * lane] = cp;
+    gc[2 * lane + 1] = cr;
     if (lane == 0) {
         sb.gcnt[SGROUPS * SCOLS * 2 + g] = ncol;
-        if (sfault) atomicOr((int *)&counts[7], 1);
+        if (fault) atomicOr((int *)&counts[7], 1);
     }
 }
 
@@ -2452,24 +2468,31 @@ __device__ __forceinline__ bool stripe_single_wave(const StripeBufs &sb, const S
 // one the neighbour needs next is published.  solve(st, it) runs one step.
 // single: wave 0 runs the steps without workgroup barriers between them
 // (stripe_single_wave); the workgroup joins at the phase's end.
-template <typename T, typename Solve>
+// wave 0's steps [s0, s1) one after the other (the `single` schedule)
+template <typename Solve>
+__device__ __forceinline__ void wave_steps(int s0, int s1, int it, Solve &solve) {
+    if (threadIdx.x < 64) {
+        for (int st = s0; st < s1; st++) {
+            solve(st, it);
+            // this wave's LDS stores complete before its next step's loads
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            __builtin_amdgcn_s_waitcnt(0xc07f);        // lgkmcnt(0)
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+// single: `phase(s0, s1, it)` runs wave 0's steps (wave_steps, or a solver's
+// own pipelined loop); the workgroup joins at the phase's end.
+template <typename T, typename Solve, typename Phase>
 __device__ __forceinline__ void stripe_sweeps(const StripeBufs &sb, const StripeView &v, int iters, uint32_t base,
                                               uint32_t *flagA, uint32_t *flagB, T *lv, T *g, int32_t *fault,
-                                              Solve solve, int tw = 0, bool single = false) {
+                                              Solve solve, int tw, bool single, Phase phase) {
     const int j = v.j;
     const bool right = 2 * j + 2 < v.S;             // seam j (phase B) exists
     (void)tw;
     auto steps = [&](int s0, int s1, int it) {
         if (single) {
-            if (threadIdx.x < 64) {
-                for (int st = s0; st < s1; st++) {
-                    solve(st, it);
-                    // this wave's LDS stores complete before its next step's loads
-                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-                    __builtin_amdgcn_s_waitcnt(0xc07f);        // lgkmcnt(0)
-                    __builtin_amdgcn_wave_barrier();
-                }
-            }
+            phase(s0, s1, it);
             __syncthreads();
         } else {
             for (int st = s0; st < s1; st++) { solve(st, it); __syncthreads(); }
@@ -2598,8 +2621,63 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
                 if (hasB) { lv[3 * p.w] = vxB; lv[3 * p.w + 1] = vyB; lv[3 * p.w + 2] = wB; }
             }
         };
+        // the single-wave schedule, software-pipelined: a step's pair record,
+        // masses and first U rows (with their multipliers) do not depend on
+        // the velocities, so the next step's are loaded before this step's
+        // row math; only the bodies' velocities are read after the previous
+        // step's stores (one wave: its LDS operations complete in order).
+        // Same rows, same order, same arithmetic as `solve`.
+        auto phase = [&](int s0, int s1, int) {
+            if (threadIdx.x >= 64 || s0 >= s1) return;
+            constexpr int U = 4;
+            struct Nx { int4 p; float4 m; float4 a[U], c[U]; float n[U], f[U]; };
+            auto fetch = [&](int st, Nx &x) {
+                const int k = v.lstep(st);
+                const int q = stepL[k] + (int)threadIdx.x;
+                const bool ok = q < stepL[k + 1];
+                x.p = ok ? pr[q] : make_int4(0, 0, -1, -1);
+                x.m = pm[ok ? q : 0];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int t = x.p.x + max(min(u, x.p.y - 1), 0);
+                    x.a[u] = rn[t]; x.c[u] = rr[t]; x.n[u] = ln[t]; x.f[u] = lf[t];
+                }
+            };
+            Nx cur, nxt;
+            fetch(s0, cur);
+            for (int st = s0; st < s1; st++) {
+                if (st + 1 < s1) fetch(st + 1, nxt);
+                const int4 p = cur.p;
+                const float4 m = cur.m;
+                const bool hasA = p.z >= 0, hasB = p.w >= 0;
+                float vxA = 0.f, vyA = 0.f, wA = 0.f, vxB = 0.f, vyB = 0.f, wB = 0.f;
+                if (hasA) { vxA = lv[3 * p.z]; vyA = lv[3 * p.z + 1]; wA = lv[3 * p.z + 2]; }
+                if (hasB) { vxB = lv[3 * p.w]; vyB = lv[3 * p.w + 1]; wB = lv[3 * p.w + 2]; }
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    if (u >= p.y) break;
+                    float n = cur.n[u], f = cur.f[u];
+                    pgs_row_t<true>(cur.a[u], cur.c[u], m.x, m.y, m.z, m.w, hasA, hasB, mu, n, f, vxA, vyA, wA, vxB,
+                                    vyB, wB);
+                    ln[p.x + u] = n;
+                    lf[p.x + u] = f;
+                }
+                for (int jr = U; jr < p.y; jr++) {       // (pairs of more than U rows: the rest on demand)
+                    const int t = p.x + jr;
+                    float n = ln[t], f = lf[t];
+                    pgs_row_t<true>(rn[t], rr[t], m.x, m.y, m.z, m.w, hasA, hasB, mu, n, f, vxA, vyA, wA, vxB, vyB,
+                                    wB);
+                    ln[t] = n;
+                    lf[t] = f;
+                }
+                if (hasA) { lv[3 * p.z] = vxA; lv[3 * p.z + 1] = vyA; lv[3 * p.z + 2] = wA; }
+                if (hasB) { lv[3 * p.w] = vxB; lv[3 * p.w + 1] = vyB; lv[3 * p.w + 2] = wB; }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // (program order of the LDS accesses)
+                cur = nxt;
+            }
+        };
         stripe_sweeps(sb, v, iters, base, sb.sflag, sb.sflag + STRIPES_MAX / 2, lv, sb.gvel, fault, solve, 0,
-                      single);
+                      single, phase);
     } else {
         __syncthreads();
         const bool single = stripe_single_wave(sb, v, nullptr);
@@ -2627,7 +2705,8 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
             }
         };
         stripe_sweeps(sb, v, iters, base, sb.sflag, sb.sflag + STRIPES_MAX / 2, lv, sb.gvel, fault, solve, 0,
-                      single);
+                      single,
+                      [&](int a0, int a1, int itv) { wave_steps(a0, a1, itv, solve); });
     }
     __syncthreads();
     // k_pgs_writeback for the stripes this workgroup finished last (only the
@@ -2727,8 +2806,57 @@ k_pos_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
                           });
             }
         };
+        // the single-wave schedule, software-pipelined as the PGS's: the next
+        // step's pair record and first U rows are loaded before this step's
+        // rows run; only the poses are read after the previous step's stores
+        auto phase = [&](int s0, int s1, int) {
+            if (threadIdx.x >= 64 || s0 >= s1) return;
+            constexpr int U = 4;
+            struct Nx { int4 p; double2 mm, ii; double2 n[U], c[U]; double y[U]; int f[U]; };
+            auto fetch = [&](int stp, Nx &x) {
+                const int k = v.lstep(stp);
+                const int q = stepL[k] + (int)threadIdx.x;
+                const bool ok = q < stepL[k + 1];
+                x.p = ok ? pr[q] : make_int4(0, 0, 0, 0);
+                x.mm = pm[ok ? q : 0];
+                x.ii = pi[ok ? q : 0];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const int t = x.p.x + max(min(u, x.p.y - 1), 0);
+                    x.n[u] = ln[t]; x.c[u] = lc[t]; x.y[u] = py[t]; x.f[u] = fl[t];
+                }
+            };
+            Nx cur, nxt;
+            fetch(s0, cur);
+            for (int stp = s0; stp < s1; stp++) {
+                if (stp + 1 < s1) fetch(stp + 1, nxt);
+                const int4 p = cur.p;
+                if (p.y > 0) {
+                    const int a = p.z, b = p.w;
+                    const double2 mm = cur.mm, ii = cur.ii;
+                    double xA = lp[3 * a], yA = lp[3 * a + 1], tA = lp[3 * a + 2];
+                    double xB = lp[3 * b], yB = lp[3 * b + 1], tB = lp[3 * b + 2];
+#pragma unroll
+                    for (int u = 0; u < U; u++) {
+                        if (u >= p.y) break;
+                        pos_item_sel(cur.n[u].x, cur.n[u].y, cur.c[u].x, cur.c[u].y, cur.y[u], cur.f[u], mm.x, mm.y,
+                                     ii.x, ii.y, xA, yA, tA, xB, yB, tB);
+                    }
+                    for (int k2 = U; k2 < p.y; k2++) {       // (pairs of more than U rows: the rest on demand)
+                        const int t = p.x + k2;
+                        const double2 n = ln[t], c = lc[t];
+                        pos_item_sel(n.x, n.y, c.x, c.y, py[t], fl[t], mm.x, mm.y, ii.x, ii.y, xA, yA, tA, xB, yB, tB);
+                    }
+                    const int fl0 = cur.f[0];
+                    if (mm.x != 0.0 || (fl0 & 2)) { lp[3 * a] = xA; lp[3 * a + 1] = yA; lp[3 * a + 2] = tA; }
+                    if (mm.y != 0.0 || (fl0 & 4)) { lp[3 * b] = xB; lp[3 * b + 1] = yB; lp[3 * b + 2] = tB; }
+                }
+                __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // (program order of the LDS accesses)
+                cur = nxt;
+            }
+        };
         stripe_sweeps(sb, v, iters, base, sb.sflag + STRIPES_MAX, sb.sflag + STRIPES_MAX + STRIPES_MAX / 2, lp,
-                      sb.gpos, fault, solve, 1, single);
+                      sb.gpos, fault, solve, 1, single, phase);
     } else {
         __syncthreads();
         const bool single = stripe_single_wave(sb, v, nullptr);
@@ -2751,7 +2879,8 @@ k_pos_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
             }
         };
         stripe_sweeps(sb, v, iters, base, sb.sflag + STRIPES_MAX, sb.sflag + STRIPES_MAX + STRIPES_MAX / 2, lp,
-                      sb.gpos, fault, solve, 1, single);
+                      sb.gpos, fault, solve, 1, single,
+                      [&](int a0, int a1, int itv) { wave_steps(a0, a1, itv, solve); });
     }
     __syncthreads();
     // storeBodyData (:176-197) for the stripes this workgroup finished last

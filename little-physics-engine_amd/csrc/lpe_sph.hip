@@ -1700,8 +1700,10 @@ __global__ void k_merge_prestats(int32_t *__restrict__ st, int32_t *__restrict__
 __device__ unsigned long long g_ftrace[4096 * 8];
 __device__ int g_ftrace_on;
 #define FTR(k) do { if (g_ftrace_on && threadIdx.x == 0) g_ftrace[lb * 8 + (k)] = wall_clock64(); } while (0)
+#define FTRMAX(k, v) do { if (g_ftrace_on && (threadIdx.x & 63) == 0) atomicMax(&g_ftrace[lb * 8 + (k)], (unsigned long long)(v)); } while (0)
 #else
 #define FTR(k) do {} while (0)
+#define FTRMAX(k, v) do {} while (0)
 #endif
 
 // the coupling's per-block arrays, laid over the image once the fluid loop is done
@@ -1901,6 +1903,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     }
     __syncthreads();                                  // (the image, the block's pair list)
     FTR(1);
+    FTRMAX(7, img ? hd.L : 100000 + (fplans ? hd.L : 0));
     if (!live) {
     } else if (cnt > NLIST_CAP && sp.refInv &&
                ref_cap_near(sp.ovl, sp.ox + (int)((__float_as_int(meA.w) >> 2) & 0x7fff),
@@ -1955,7 +1958,8 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                            [&](int k, int) { return FRec{nbA[k], nbB[k]}; },
                            [&](int k, const FRec &o) { if (k != s) pair(o.a, o.b); });
     }
-    FTR(5);
+    FTRMAX(5, wall_clock64());
+    FTRMAX(6, cnt);
     CoupleState st;
     st.x = xi; st.y = yi;
     st.vhx = S.vhx[sl]; st.vhy = S.vhy[sl];
@@ -3273,7 +3277,16 @@ int sph_prelaunch(lpe_ctx *ctx, double dt_tick, const std::function<int(hipStrea
     d.pre = false;
     if (d.n <= 0 || !d.P.x) return LPE_OK;
     if (!d.pside) {
-        LPE_HIP(ctx, hipStreamCreateWithFlags(&d.pside, hipStreamNonBlocking));
+        // the lowest priority: when the tick's solvers and this stream's
+        // kernels become ready together, the solvers' workgroups (a whole
+        // CU's LDS each) are dispatched first (LPE_PSIDE_PRIO=0: default
+        // priority, for A/B measurements)
+        static const char *pp = getenv("LPE_PSIDE_PRIO");
+        int least = 0, greatest = 0;
+        if ((!pp || std::atoi(pp) != 0) && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+            LPE_HIP(ctx, hipStreamCreateWithPriority(&d.pside, hipStreamNonBlocking, least));
+        else
+            LPE_HIP(ctx, hipStreamCreateWithFlags(&d.pside, hipStreamNonBlocking));
         LPE_HIP(ctx, hipEventCreateWithFlags(&d.preReady, hipEventDisableTiming));
         LPE_HIP(ctx, hipEventCreateWithFlags(&d.preDone, hipEventDisableTiming));
         LPE_HIP(ctx, hipEventCreateWithFlags(&d.fbgDone, hipEventDisableTiming));

@@ -238,7 +238,10 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
             st = lpe_rigid_integrate(ctx, 1 | 32, dt_state, dt_move);
         }
         if (st) return st;
-        const bool prelaunch = !serial && fluid;
+        // (LPE_NO_PRELAUNCH=1: the next tick's sub-step 0 runs in its own
+        // tick, for A/B measurements of the overlap)
+        static const bool nopre = std::getenv("LPE_NO_PRELAUNCH") != nullptr;
+        const bool prelaunch = !serial && fluid && !nopre;
         const bool fbg_side = prelaunch && d.n > 0 && d.P.x;
         auto fbg = [&](hipStream_t fs) {
             LPE_KERNEL(ctx, "k_fluid_boundary_gravity", k_fluid_boundary_gravity, dim3(wblk(d.n)), dim3(256), 0, fs, d.n, d.P, rc.marginPixels * rc.metersPerPixel, rc.universeSize, rc.bounceDamping, rc.maxSpeed, rc.gravity, dt_state, rd->nb > 0 ? rd->counts + 5 : (const int32_t *)nullptr, d.fluid_heavy ? 1 : 0, sph_slab_slots(ctx));

@@ -35,6 +35,8 @@ ap.add_argument("--ticks", type=int, default=100)
 ap.add_argument("--rounds", type=int, default=3)
 ap.add_argument("--timing", action="store_true", help="per-kernel HIP-event times of one window each")
 ap.add_argument("--loop", action="store_true", help="also a 1-rank slab through the in-process transport")
+ap.add_argument("--only", choices=("single", "slab1", "slab1_loopback"), default=None,
+                help="build and time only this configuration (for a profiler run)")
 a = ap.parse_args()
 s = scenes.scene(a.scene)
 fl = s["fluid"]
@@ -63,9 +65,12 @@ def make(slabbed, rccl=True):
     return c
 
 
-ctxs = {"single": make(False), "slab1": make(True)}
-if a.loop:
-    ctxs["slab1_loopback"] = make(True, rccl=False)
+if a.only:
+    ctxs = {a.only: make(a.only != "single", rccl=a.only == "slab1")}
+else:
+    ctxs = {"single": make(False), "slab1": make(True)}
+    if a.loop:
+        ctxs["slab1_loopback"] = make(True, rccl=False)
 rates = {k: [] for k in ctxs}
 for _ in range(a.rounds):
     for k, c in ctxs.items():
@@ -91,8 +96,8 @@ if a.timing:
         c.timing(0)
         out[f"kernels_us_{k}"] = {n: round(ms / max(cl, 1) * 1e3, 2) for n, (ms, cl) in sorted(t.items())}
         out[f"tick_kernel_ms_{k}"] = round(sum(ms for ms, _ in t.values()) / 20, 3)
-st = ctxs["slab1"].sph_stats()
-out["slab1_owned"] = st["slabOwned"]
+if "slab1" in ctxs:
+    out["slab1_owned"] = ctxs["slab1"].sph_stats()["slabOwned"]
 for c in ctxs.values():
     c.close()
 print(json.dumps(out))
