@@ -304,6 +304,7 @@ def loopback_check(args, lpe, scenes, slab, device):
         one.world_tick(1.0 / 120.0, args.steps)
         one.sync()
         single = args.steps / (time.perf_counter() - t0)
+        gpu_single = kernel_ms_per_tick([one], lambda n: one.world_tick(1.0 / 120.0, n))
     finally:
         one.close()
 
@@ -317,8 +318,11 @@ def loopback_check(args, lpe, scenes, slab, device):
             c.world_set_coupling(None)
         lpe.mg_loopback_run(ctxs, args.prep + args.warmup, world=wc)
         t0 = time.perf_counter()
+        cpu0 = time.process_time()
         lpe.mg_loopback_run(ctxs, args.steps, world=wc)
         el = time.perf_counter() - t0
+        host_cpu = time.process_time() - cpu0
+        gpu_loop = kernel_ms_per_tick(ctxs, lambda n: lpe.mg_loopback_run(ctxs, n, world=wc))
         st = [c.sph_stats() for c in ctxs]
         info = [c.sph_slab_info() for c in ctxs]
         parts = [c.sph_download_owned() for c in ctxs]
@@ -339,7 +343,28 @@ def loopback_check(args, lpe, scenes, slab, device):
                       "edges_columns": [int(e) for e in info[0]["edges"][1:-1]],
                       "finite": bool(np.isfinite(merged["x"]).all() and np.isfinite(merged["vy"]).all()),
                       "rigid_replicas_identical": bool(same), "max_cell_occupancy_rank0": st[0]["maxCellOccupancy"],
-                      "note": "K ranks share one GPU: the ratio is the decomposition's overhead, not scaling"}))
+                      "gpu_kernel_ms_per_tick": {"single": gpu_single, "loopback_all_ranks": gpu_loop,
+                                                 "ratio": round(gpu_loop / gpu_single, 3) if gpu_single else None},
+                      "host_cpu_s_per_tick_loopback": round(host_cpu / args.steps, 5),
+                      "note": "K ranks share one GPU: the ratio is the decomposition's overhead, not scaling; "
+                              "gpu_kernel_ms_per_tick sums every launch's HIP-event time (all ranks) over "
+                              "5 further ticks: the GPU work of the decomposition against the single domain's, "
+                              "apart from the host's launch and rendezvous costs of K ranks in one process"}))
+
+
+def kernel_ms_per_tick(ctxs, run, n=5):
+    """Sum of the kernels' HIP-event times per tick over n ticks (every context)."""
+    for c in ctxs:
+        c.timing(True)
+        c.timing_reset()
+    run(n)
+    for c in ctxs:
+        c.sync()
+    tot = 0.0
+    for c in ctxs:
+        tot += sum(ms for ms, _ in c.timing_read().values())
+        c.timing(False)
+    return round(tot / n, 3)
 
 
 def rigid_microbench(lpe, device, reps=10):
@@ -369,7 +394,7 @@ def rigid_microbench(lpe, device, reps=10):
     return dict(fixture="tests/golden/pile_M_t250.npz", pairs=st["pairs"], contacts=st["contacts"],
                 colours=st["pgsLevels"], colour_rounds=st["colourRounds"], reps=reps, step_kernels_us=round(step, 1),
                 kernels_us={k: us[k] for k in ("k_bg_key", "k_bg_pairs", "k_narrow", "k_pair_colour", "k_pgs_colour",
-                                               "k_pos_colour", "k_stripe_pairs", "k_stripe_setup", "k_group_lists",
+                                               "k_pos_colour", "k_stripe_pairs", "k_stripe_setup",
                                                "k_group_colour", "k_stripe_layout", "k_stripe_fill", "k_pgs_stripes",
                                                "k_pos_stripes") if k in us})
 

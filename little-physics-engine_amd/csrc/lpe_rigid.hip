@@ -134,6 +134,36 @@ __global__ void __launch_bounds__(RTPB) k_rscan_final(const int32_t *nptr, int n
     }
 }
 
+// the whole scan in one block (capacities of a few tiles: one launch instead
+// of two), tile by tile with a running carry; also copies the total to
+// *total_out when given (the pair count the narrowphase reads)
+__global__ void __launch_bounds__(RTPB) k_rscan_single(const int32_t *nptr, int ncap,
+                                                       const int32_t *__restrict__ cnt,
+                                                       int32_t *__restrict__ start,
+                                                       int32_t *__restrict__ cursor,
+                                                       int32_t *__restrict__ total_out) {
+    const int n = nptr ? min(*nptr, ncap) : ncap;   // a count past the capacity (overflow, redone) is clipped
+    int carry = 0;
+    for (int t0 = 0; t0 < n; t0 += 1024) {
+        const int base = t0 + threadIdx.x * 4;
+        int v[4], s = 0;
+        for (int k = 0; k < 4; k++) { const int c = base + k; v[k] = (c < n) ? cnt[c] : 0; s += v[k]; }
+        int tot;
+        int ex = r_block_excl(s, &tot) + carry;
+        for (int k = 0; k < 4; k++) {
+            const int c = base + k;
+            if (c < n) { start[c] = ex; if (cursor) cursor[c] = ex; }
+            ex += v[k];
+        }
+        carry += tot;
+    }
+    if (threadIdx.x == 0) {
+        start[n] = carry;
+        if (total_out) *total_out = carry;
+    }
+}
+static constexpr int RSCAN_SINGLE_MAX = 4096;   // capacities scanned by k_rscan_single
+
 // ---------------------------------------------------------------------------
 // geometry (fp64), restating vector_math.cpp / polygon.hpp
 struct D2 { double x, y; };
@@ -351,70 +381,68 @@ __global__ void k_rb_prep(int nb, const lpe_body *__restrict__ bodies, const dou
 }
 
 // each body's pair list sorted by partner rank (the ranks in a list are
-// distinct): lists of up to BP_SHORT entries by one wave each, in registers
-// (an entry's place is the number of smaller keys), longer ones by
-// k_bp_sort_long
+// distinct), four bodies per block: a list of up to BP_SHORT entries by its
+// wave, in registers (an entry's place is the number of smaller keys); a
+// longer one (the walls' lists, filled by many threads in arrival order) by
+// the whole block afterwards, bitonic-sorted in LDS
 static constexpr int BP_SHORT = 64;
 static constexpr int BP_LONG = 4096;       // longest list sorted in LDS (longer: one thread)
 __global__ void __launch_bounds__(RTPB)
 k_bp_sort(int nb, const int32_t *__restrict__ pstart, int2 *__restrict__ pairs,
           int32_t *__restrict__ rk, int cap_pairs) {
-    const int r = blockIdx.x * (RTPB / 64) + (threadIdx.x >> 6);
+    const int r0 = blockIdx.x * (RTPB / 64);
+    const int r = r0 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    if (r >= nb) return;                                     // (whole wave)
-    const int s = pstart[r], e = min(pstart[r + 1], cap_pairs), n = e - s;
-    if (n <= 1 || (n > BP_SHORT && n <= BP_LONG)) return;
-    if (n > BP_LONG) {                                       // (never expected) one lane, in place
-        if (lane == 0)
-            for (int k = s + 1; k < e; k++) {
-                int v = rk[k];
-                int2 p = pairs[k];
-                int j = k - 1;
-                while (j >= s && rk[j] > v) { rk[j + 1] = rk[j]; pairs[j + 1] = pairs[j]; j--; }
-                rk[j + 1] = v; pairs[j + 1] = p;
-            }
-        return;
+    if (r < nb) {
+        const int s = pstart[r], e = min(pstart[r + 1], cap_pairs), n = e - s;
+        if (n > BP_LONG) {                                   // (never expected) one lane, in place
+            if (lane == 0)
+                for (int k = s + 1; k < e; k++) {
+                    int v = rk[k];
+                    int2 p = pairs[k];
+                    int j = k - 1;
+                    while (j >= s && rk[j] > v) { rk[j + 1] = rk[j]; pairs[j + 1] = pairs[j]; j--; }
+                    rk[j + 1] = v; pairs[j + 1] = p;
+                }
+        } else if (n > 1 && n <= BP_SHORT) {
+            const int key = lane < n ? rk[s + lane] : 0x7fffffff;
+            const int2 val = lane < n ? pairs[s + lane] : make_int2(0, 0);
+            int rank = 0;
+            for (int j = 0; j < n; j++) rank += __shfl(key, j) < key ? 1 : 0;
+            if (lane < n) { rk[s + rank] = key; pairs[s + rank] = val; }
+        }
     }
-    const int key = lane < n ? rk[s + lane] : 0x7fffffff;
-    const int2 val = lane < n ? pairs[s + lane] : make_int2(0, 0);
-    int rank = 0;
-    for (int j = 0; j < n; j++) rank += __shfl(key, j) < key ? 1 : 0;
-    if (lane < n) { rk[s + rank] = key; pairs[s + rank] = val; }
-}
-
-// one block per body; a list of BP_SHORT < n <= BP_LONG entries (the walls'
-// lists, filled by many threads in arrival order) is bitonic-sorted in LDS
-__global__ void __launch_bounds__(RTPB)
-k_bp_sort_long(int nb, const int32_t *__restrict__ pstart, int2 *__restrict__ pairs,
-               int32_t *__restrict__ rk, int cap_pairs) {
-    const int r = blockIdx.x;
-    if (r >= nb) return;
-    const int s = pstart[r], e = min(pstart[r + 1], cap_pairs), n = e - s;
-    if (n <= BP_SHORT || n > BP_LONG) return;
     __shared__ int key[BP_LONG];
     __shared__ int2 val[BP_LONG];
-    int m = 1;
-    while (m < n) m <<= 1;
-    for (int i = threadIdx.x; i < m; i += RTPB) {
-        key[i] = i < n ? rk[s + i] : 0x7fffffff;
-        val[i] = i < n ? pairs[s + i] : make_int2(0, 0);
-    }
-    __syncthreads();
-    for (int size = 2; size <= m; size <<= 1)
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = threadIdx.x; i < m; i += RTPB) {
-                const int j = i ^ stride;
-                if (j > i) {
-                    const bool up = (i & size) == 0;
-                    if ((key[i] > key[j]) == up) {
-                        const int tk = key[i]; key[i] = key[j]; key[j] = tk;
-                        const int2 tv = val[i]; val[i] = val[j]; val[j] = tv;
+    for (int w = 0; w < RTPB / 64; w++) {                    // (block-uniform)
+        const int rb = r0 + w;
+        if (rb >= nb) break;
+        const int s = pstart[rb], e = min(pstart[rb + 1], cap_pairs), n = e - s;
+        if (n <= BP_SHORT || n > BP_LONG) continue;
+        int m = 1;
+        while (m < n) m <<= 1;
+        for (int i = threadIdx.x; i < m; i += RTPB) {
+            key[i] = i < n ? rk[s + i] : 0x7fffffff;
+            val[i] = i < n ? pairs[s + i] : make_int2(0, 0);
+        }
+        __syncthreads();
+        for (int size = 2; size <= m; size <<= 1)
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                for (int i = threadIdx.x; i < m; i += RTPB) {
+                    const int j = i ^ stride;
+                    if (j > i) {
+                        const bool up = (i & size) == 0;
+                        if ((key[i] > key[j]) == up) {
+                            const int tk = key[i]; key[i] = key[j]; key[j] = tk;
+                            const int2 tv = val[i]; val[i] = val[j]; val[j] = tv;
+                        }
                     }
                 }
+                __syncthreads();
             }
-            __syncthreads();
-        }
-    for (int i = threadIdx.x; i < n; i += RTPB) { rk[s + i] = key[i]; pairs[s + i] = val[i]; }
+        for (int i = threadIdx.x; i < n; i += RTPB) { rk[s + i] = key[i]; pairs[s + i] = val[i]; }
+        __syncthreads();                                     // (LDS reused by the next long list)
+    }
 }
 
 // ---- uniform-grid broadphase --------------------------------------------
@@ -1611,6 +1639,110 @@ __global__ void k_pos_fill_rows(const int32_t *__restrict__ ncptr, const int32_t
     out.ab[u] = make_int2(c.a, c.b);
 }
 
+// The solver preparation in two launches (colour_prep; the same arithmetic as
+// the five kernels above, which the replay path keeps): per body the PGS's
+// inverse masses (k_pgs_bodies, what = 1), the position solver's body data
+// (k_pos_bodies) and the contact marks cleared; then per solver-order item
+// the body marks (k_mark_contacts: the same set of bodies, marked from the
+// same contacts), the PGS row (k_pgs_rows) and the position row
+// (k_pos_fill_rows).
+__global__ void k_prep_bodies(int nb, const lpe_body *__restrict__ bodies, float *__restrict__ imii,
+                              double *__restrict__ st, int32_t *__restrict__ inContact) {
+    const int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i >= nb) return;
+    const lpe_body b = bodies[i];
+    {
+        const bool cr = can_rotate(b);
+        const double m = b.mass;
+        const float im = (m > 1e29) ? 0.f : (float)(1.0 / m);
+        float iv = 0.f;
+        if (cr) {
+            const double I = b.inertia;
+            if (I > 1e-12 && I < 1e29) iv = (float)(1.0 / I);
+        }
+        imii[2 * i] = im; imii[2 * i + 1] = iv;
+    }
+    {
+        const double invM = (b.mass > 1e29) ? 0.0 : (1.0 / b.mass);
+        double invI = 0.0;
+        int fl = 0;
+        if (b.flags & LPE_BODY_HAS_INERTIA) {
+            const double I = b.inertia;
+            if (I < 1e29 && I > 1e-12) { fl |= 1; invI = 1.0 / I; }
+        }
+        if (b.flags & LPE_BODY_HAS_MASS) fl |= 2;
+        if (solid_body(b)) fl |= 4;
+        st[3 * i] = invM;
+        st[3 * i + 1] = invI;
+        st[3 * i + 2] = (double)fl;
+    }
+    inContact[i] = 0;
+    inContact[nb + i] = 0;
+}
+__global__ void k_prep_items(const int32_t *__restrict__ ncptr, const int32_t *__restrict__ order,
+                             const lpe_contact *__restrict__ cs, const lpe_body *__restrict__ bodies,
+                             const float *__restrict__ imii, const double *__restrict__ st, float4 *__restrict__ rowN,
+                             float4 *__restrict__ rowR, int2 *__restrict__ rowAB, float4 *__restrict__ rowM,
+                             int32_t *__restrict__ sItemA, int32_t *__restrict__ sItemB, PosRows out,
+                             int32_t *__restrict__ inContact, int32_t *__restrict__ inPos, double baumgarte,
+                             double slop) {
+    const int t = blockIdx.x * RTPB + threadIdx.x;
+    if (t >= *ncptr) return;
+    const lpe_contact c = cs[order[t]];
+    const lpe_body A = bodies[c.a], B = bodies[c.b];
+    inContact[c.a] = 1;
+    inContact[c.b] = 1;
+    {   // k_pgs_rows
+        const int a = infinite_mass(A) ? -1 : c.a;
+        const int b = infinite_mass(B) ? -1 : c.b;
+        const D2 u = nrm(d2(c.nx, c.ny));
+        const float dirX = (float)u.x, dirY = (float)u.y;
+        const float rxA = (float)(c.px - A.x), ryA = (float)(c.py - A.y);
+        const float rxB = (float)(c.px - B.x), ryB = (float)(c.py - B.y);
+        float imA = 0.f, imB = 0.f, iiA = 0.f, iiB = 0.f;
+        if (a >= 0) { imA = imii[2 * a]; iiA = imii[2 * a + 1]; }
+        if (b >= 0) { imB = imii[2 * b]; iiB = imii[2 * b + 1]; }
+        float effN, effF;
+        {
+            const float rAxn = cross2f(rxA, ryA, dirX, dirY), rBxn = cross2f(rxB, ryB, dirX, dirY);
+            const float sum = imA + imB + (rAxn * rAxn) * iiA + (rBxn * rBxn) * iiB;
+            effN = (sum < 1e-12F) ? 0.F : 1.F / sum;
+        }
+        {
+            const float fx = -dirY, fy = dirX;
+            const float rAxn = cross2f(rxA, ryA, fx, fy), rBxn = cross2f(rxB, ryB, fx, fy);
+            const float sum = imA + imB + (rAxn * rAxn) * iiA + (rBxn * rBxn) * iiB;
+            effF = (sum < 1e-12F) ? 0.F : 1.F / sum;
+        }
+        rowN[t] = make_float4(dirX, dirY, effN, effF);
+        rowR[t] = make_float4(rxA, ryA, rxB, ryB);
+        rowAB[t] = make_int2(a, b);
+        rowM[t] = make_float4(imA, iiA, imB, iiB);
+        sItemA[t] = a;
+        sItemB[t] = b;
+    }
+    {   // k_pos_fill_rows
+        const bool kept = solid_body(A) || solid_body(B);
+        const int fa = (int)st[3 * c.a + 2], fb = (int)st[3 * c.b + 2];
+        int fl = kept ? 0 : 1;
+        if (kept) { inPos[c.a] = 1; inPos[c.b] = 1; }
+        if (!(fa & 2) || !(fb & 2)) fl |= 1;
+        if (!(fa & 4) && !(fb & 4)) fl |= 1;
+        const double pen = c.pen - slop;
+        if (pen <= 0.0) fl |= 1;
+        if (fa & 1) fl |= 2;
+        if (fb & 1) fl |= 4;
+        const D2 n = nrm(d2(c.nx, c.ny));
+        out.n[t] = make_double2(n.x, n.y);
+        out.c[t] = make_double2(baumgarte * pen, c.px);
+        out.py[t] = c.py;
+        out.fl[t] = fl;
+        out.m[t] = make_double2(st[3 * c.a], st[3 * c.b]);
+        out.i[t] = make_double2(st[3 * c.a + 1], st[3 * c.b + 1]);
+        out.ab[t] = make_int2(c.a, c.b);
+    }
+}
+
 // one item on the pair's poses in registers (the colour solver): the items of
 // a pair share its bodies, their inverse masses and rotation flags
 __device__ __forceinline__ void pos_item_regs(double nx, double ny, double corr, double px, double py,
@@ -1994,6 +2126,11 @@ static constexpr int STEPS_MAX = SGROUPS * SCOLS;
 #define LPE_STPB 256
 #endif
 static constexpr int STPB = LPE_STPB;             // threads of a stripe workgroup
+// At most this many pairs with contacts: one stripe (one workgroup, no
+// hand-overs).  A small scene's colours are few (a box stack's are two), so
+// its sweeps are a handful of steps, while the stripes' per-phase hand-overs
+// (~1-3 us each) were most of its solve (C1: 153 us with 40 stripes).
+static constexpr int STRIPE_MIN_PAIRS = 1024;
 
 struct StripeBufs {
     int32_t *bstripe;      // [nb] stripe of a movable body in a contact pair, else -1
@@ -2078,14 +2215,14 @@ k_stripe_setup(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict
     extern __shared__ unsigned int bmark[];                 // [2][words]: movable / static contact-pair bodies
     __shared__ double wr[3][SOLVE_TPB / 64];
     __shared__ double sx0, sw;
-    __shared__ int sS, sViol, nstat, statcur;
+    __shared__ int sS, sViol, nstat, statcur, sPairs;
     __shared__ int scnt[STRIPES_MAX], scur[STRIPES_MAX], gcount[SGROUPS];
     const int np = *npptr;
     const int words = (nb + 31) >> 5;
     for (int i = threadIdx.x; i < 2 * words; i += SOLVE_TPB) bmark[i] = 0u;
     for (int i = threadIdx.x; i < STRIPES_MAX; i += SOLVE_TPB) scnt[i] = 0;
     for (int i = threadIdx.x; i < SGROUPS; i += SOLVE_TPB) gcount[i] = 0;
-    if (threadIdx.x == 0) { sViol = 0; nstat = 0; }
+    if (threadIdx.x == 0) { sViol = 0; nstat = 0; sPairs = 0; }
     double mn = 1.7976931348623157e308, mx = -1.7976931348623157e308, sp = 0.0;
     const int nblk = (np + RTPB - 1) / RTPB;
     for (int k = threadIdx.x; k < nblk; k += SOLVE_TPB) {
@@ -2098,19 +2235,22 @@ k_stripe_setup(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict
     }
     if ((threadIdx.x & 63) == 0) { wr[0][threadIdx.x >> 6] = mn; wr[1][threadIdx.x >> 6] = mx; wr[2][threadIdx.x >> 6] = sp; }
     __syncthreads();
+    int mine = 0;                                          // pairs with contacts
     for (int p = threadIdx.x; p < np; p += SOLVE_TPB) {
         const int f = sb.pflag[p];
         if (!(f & 1)) continue;
+        mine++;
         const int2 pr = pairs[p];
         atomicOr(&bmark[((f & 2) ? 0 : words) + (pr.x >> 5)], 1u << (pr.x & 31));
         atomicOr(&bmark[((f & 4) ? 0 : words) + (pr.y >> 5)], 1u << (pr.y & 31));
     }
+    if (mine) atomicAdd(&sPairs, mine);
     if (threadIdx.x == 0) {
         for (int k = 1; k < SOLVE_TPB / 64; k++) {
             mn = fmin(mn, wr[0][k]); mx = fmax(mx, wr[1][k]); sp = fmax(sp, wr[2][k]);
         }
         int S = 1;
-        if (mx > mn) {
+        if (mx > mn && sPairs > STRIPE_MIN_PAIRS) {
             const double q = (mx - mn) / sp;          // (span 0: +inf)
             // (smax: the two solvers' S / 2 workgroups each must be co-resident,
             // one per CU -- stripe_cap)
@@ -2180,30 +2320,6 @@ k_stripe_setup(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict
     }
 }
 
-// one workgroup per group: its pairs in ascending order (stable compaction)
-__global__ void __launch_bounds__(RTPB)
-k_group_lists(const int32_t *__restrict__ npptr, const int32_t *__restrict__ counts, StripeBufs sb) {
-    const int g = (int)blockIdx.x;
-    if (g >= counts[12]) return;                       // groups: bands 0, 2, .. and seams 1, 3, .. < S
-    const int np = *npptr;
-    int base = sb.gstart[g];
-    for (int p0 = 0; p0 < np; p0 += 4 * RTPB) {
-        int f[4], c = 0;
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const int p = p0 + 4 * (int)threadIdx.x + k;
-            f[k] = (p < np && sb.pgroup[p] == g) ? 1 : 0;
-            c += f[k];
-        }
-        int tot;
-        int off = r_block_excl(c, &tot) + base;
-#pragma unroll
-        for (int k = 0; k < 4; k++)
-            if (f[k]) sb.glist[off++] = p0 + 4 * (int)threadIdx.x + k;
-        base += tot;
-    }
-}
-
 // one wave per group: greedy colouring of its pairs in ascending order (the
 // lowest colour free on the pair's movable bodies), the pair's rank and row
 // offset inside its (group, colour), the group's colour sizes.  The bodies'
@@ -2215,18 +2331,40 @@ k_group_lists(const int32_t *__restrict__ npptr, const int32_t *__restrict__ cou
 // pair's are stored (a body the two pairs share takes the stored value:
 // forwarding), so a pair costs its compare / select chain, not LDS round
 // trips.
-__global__ void __launch_bounds__(64)
-k_group_colour(const int32_t *__restrict__ counts, const int2 *__restrict__ pairs,
+// The block first lists its group's pairs in ascending order (a stable
+// compaction by all RTPB threads), then wave 0 colours them.
+__global__ void __launch_bounds__(RTPB)
+k_group_colour(const int32_t *__restrict__ npptr, const int32_t *__restrict__ counts, const int2 *__restrict__ pairs,
                const int32_t *__restrict__ ccount, StripeBufs sb) {
     extern __shared__ unsigned long long used[];             // per stripe-list slot of the group's stripes
     const int g = (int)blockIdx.x;
     const int S = counts[12];
-    if (g >= S) return;
-    const int lane = (int)threadIdx.x;
+    if (g >= S) return;                                // groups: bands 0, 2, .. and seams 1, 3, .. < S
+    {
+        const int np = *npptr;
+        int base = sb.gstart[g];
+        for (int p0 = 0; p0 < np; p0 += 4 * RTPB) {
+            int f[4], c = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int p = p0 + 4 * (int)threadIdx.x + k;
+                f[k] = (p < np && sb.pgroup[p] == g) ? 1 : 0;
+                c += f[k];
+            }
+            int tot;
+            int off = r_block_excl(c, &tot) + base;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (f[k]) sb.glist[off++] = p0 + 4 * (int)threadIdx.x + k;
+            base += tot;
+        }
+    }
     const int s = (g >> 1) * 2 + (g & 1);               // band j: stripes 2j, 2j+1; seam j: 2j+1, 2j+2
     const int u0 = sb.sbStart[s], u1 = sb.sbStart[min(s + 2, S)];
-    for (int i = lane; i < u1 - u0; i += 64) used[i] = 0ull;
-    __syncthreads();
+    for (int i = (int)threadIdx.x; i < u1 - u0; i += RTPB) used[i] = 0ull;
+    __syncthreads();                                   // (the list, in global memory, and the masks)
+    if (threadIdx.x >= 64) return;
+    const int lane = (int)threadIdx.x;
     const int g0 = sb.gstart[g], g1 = sb.gstart[g + 1];
     int ncol = 0, fault = 0;
     int cp = 0, cr = 0;                                   // lane c: colour c's pairs and rows so far
@@ -3216,11 +3354,17 @@ static int rigid_alloc_bsum(lpe_ctx *ctx, RigidDev *d, long n) {
 
 // exclusive scan of n (device count nptr or host ncap) ints; start[n] = total
 static int rscan(lpe_ctx *ctx, RigidDev *d, const int32_t *nptr, int ncap, const int32_t *cnt,
-                 int32_t *start, int32_t *cursor, hipStream_t s = nullptr) {
+                 int32_t *start, int32_t *cursor, hipStream_t s = nullptr, int32_t *total_out = nullptr) {
+    if (!s) s = ctx->stream;
+    if (ncap <= RSCAN_SINGLE_MAX) {
+        LPE_KERNEL(ctx, "k_rscan_single", k_rscan_single, dim3(1), dim3(RTPB), 0, s, nptr, ncap, cnt, start, cursor,
+                   total_out);
+        LPE_CHECK_LAUNCH(ctx, "rscan");
+        return LPE_OK;
+    }
     int st = rigid_alloc_bsum(ctx, d, ncap);
     if (st) return st;
     int nb = ncap / 1024 + 1;
-    if (!s) s = ctx->stream;
     // <= 1,024 tiles: the tile prefix inside k_rscan_final (LPE_NO_RSCAN_FUSION=1: off)
     static const bool nofuse = getenv("LPE_NO_RSCAN_FUSION") != nullptr;
     const int fused = (nb <= 1024 && !nofuse) ? 1 : 0;
@@ -3229,6 +3373,10 @@ static int rscan(lpe_ctx *ctx, RigidDev *d, const int32_t *nptr, int ncap, const
         LPE_KERNEL(ctx, "k_rscan_blocks", k_rscan_blocks, dim3(1), dim3(RTPB), 0, s, nptr, ncap, d->bsum, start);
     LPE_KERNEL(ctx, "k_rscan_final", k_rscan_final, dim3(nb), dim3(RTPB), 0, s, nptr, ncap, cnt, d->bsum, start, cursor,
                fused);
+    if (total_out) {               // (a host-sized scan: the total is start[ncap])
+        if (nptr) { ctx->err = "rscan: total_out needs a host-sized count"; return LPE_ERR_ARG; }
+        LPE_HIP(ctx, hipMemcpyAsync(total_out, start + ncap, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
+    }
     LPE_CHECK_LAUNCH(ctx, "rscan");
     return LPE_OK;
 }
@@ -3386,14 +3534,13 @@ static int detect_launch(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pa
         LPE_KERNEL(ctx, "k_bg_pairs", k_bg_pairs, dim3((nb + BG_WAVES - 1) / BG_WAVES), dim3(RTPB), 0, s, nb, 0, d->byRank, d->bodies, d->aabb,
                    c.smallParticleThreshold, (int)G, d->bgKey, d->bgStart, d->bgList, d->bgSpecial, d->counts + 10,
                    d->pcount, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6);
-        st = rscan(ctx, d, nullptr, nb, d->pcount, d->pstart, d->pcursor, s);
+        // (the scan also leaves the pair count in counts[0])
+        st = rscan(ctx, d, nullptr, nb, d->pcount, d->pstart, d->pcursor, s, d->counts);
         if (st) return st;
         LPE_KERNEL(ctx, "k_bg_pairs", k_bg_pairs, dim3((nb + BG_WAVES - 1) / BG_WAVES), dim3(RTPB), 0, s, nb, 1, d->byRank, d->bodies, d->aabb,
                    c.smallParticleThreshold, (int)G, d->bgKey, d->bgStart, d->bgList, d->bgSpecial, d->counts + 10,
                    d->pcount, d->pcursor, d->pairs, d->pairRankB, d->cap_pairs, d->counts + 6);
         LPE_KERNEL(ctx, "k_bp_sort", k_bp_sort, dim3((nb + RTPB / 64 - 1) / (RTPB / 64)), dim3(RTPB), 0, s, nb, d->pstart, d->pairs, d->pairRankB, d->cap_pairs);
-        LPE_KERNEL(ctx, "k_bp_sort_long", k_bp_sort_long, dim3(nb), dim3(RTPB), 0, s, nb, d->pstart, d->pairs, d->pairRankB, d->cap_pairs);
-        LPE_HIP(ctx, hipMemcpyAsync(d->counts, d->pstart + nb, sizeof(int32_t), hipMemcpyDeviceToDevice, s));
     }
     LPE_KERNEL(ctx, "k_narrow", k_narrow, dim3(rblk(d->cap_pairs, 128)), dim3(128), 0, s, d->counts, d->cap_pairs, d->pairs, d->bodies, d->verts, d->cslots, d->ccount, d->counts);
     int st = rscan(ctx, d, d->counts, d->cap_pairs, d->ccount, d->cstart, nullptr, s);
@@ -3539,9 +3686,8 @@ static int stripe_launch(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
                d->pairs, d->ccount, d->bodies, *sb);
     LPE_KERNEL(ctx, "k_stripe_setup", k_stripe_setup, dim3(1), dim3(SOLVE_TPB), sizeof(uint32_t) * 2 * ((nb + 31) / 32 + 1),
                s, nb, d->counts, d->pairs, d->bodies, *sb, d->counts, stripe_cap(ctx));
-    LPE_KERNEL(ctx, "k_group_lists", k_group_lists, dim3(SGROUPS), dim3(RTPB), 0, s, d->counts, d->counts, *sb);
-    LPE_KERNEL(ctx, "k_group_colour", k_group_colour, dim3(SGROUPS), dim3(64), sizeof(unsigned long long) * (size_t)nb,
-               s, d->counts, d->pairs, d->ccount, *sb);
+    LPE_KERNEL(ctx, "k_group_colour", k_group_colour, dim3(SGROUPS), dim3(RTPB), sizeof(unsigned long long) * (size_t)nb,
+               s, d->counts, d->counts, d->pairs, d->ccount, *sb);
     LPE_KERNEL(ctx, "k_stripe_layout", k_stripe_layout, dim3(1), dim3(RTPB), 0, s, *sb, d->counts);
     LPE_KERNEL(ctx, "k_stripe_fill", k_stripe_fill, dim3(rblk(d->cap_pairs)), dim3(RTPB), 0, s, d->counts, d->ccount,
                d->cstart, *sb, d->pcol, d->cseg, d->order);
@@ -3603,14 +3749,12 @@ static int colour_prep(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     // (lagged detection: the count is on the device only, the grids cover the capacity)
     const int nb = d->nb, nc = d->lag ? d->cap_contacts : d->last_nc;
     int32_t *inPos = d->inContact + nb;
-    if (!d->contacts_zeroed || s != d->side)      // (k_rb_prep zeroed them on the detection stream)
-        LPE_HIP(ctx, hipMemsetAsync(d->inContact, 0, sizeof(int32_t) * 2 * nb, s));
-    d->contacts_zeroed = false;
-    LPE_KERNEL(ctx, "k_mark_contacts", k_mark_contacts, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->contacts, d->inContact);
-    LPE_KERNEL(ctx, "k_pgs_bodies", k_pgs_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->vel0, d->imii, 1);
-    LPE_KERNEL(ctx, "k_pgs_rows", k_pgs_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->order, d->contacts, d->bodies, d->imii, d->rowN, d->rowR, d->rowAB, d->rowM, d->sItemA, d->sItemB);
-    LPE_KERNEL(ctx, "k_pos_bodies", k_pos_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->posState);
-    LPE_KERNEL(ctx, "k_pos_fill_rows", k_pos_fill_rows, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->order, d->contacts, d->bodies, d->posState, pos_rows(d), inPos, c.baumgarte, c.slop);
+    d->contacts_zeroed = false;                   // (k_prep_bodies clears the marks)
+    LPE_KERNEL(ctx, "k_prep_bodies", k_prep_bodies, dim3(rblk(nb)), dim3(RTPB), 0, s, nb, d->bodies, d->imii,
+               d->posState, d->inContact);
+    LPE_KERNEL(ctx, "k_prep_items", k_prep_items, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->order,
+               d->contacts, d->bodies, d->imii, d->posState, d->rowN, d->rowR, d->rowAB, d->rowM, d->sItemA, d->sItemB,
+               pos_rows(d), d->inContact, inPos, c.baumgarte, c.slop);
     LPE_CHECK_LAUNCH(ctx, "solver preparation");
     return LPE_OK;
 }

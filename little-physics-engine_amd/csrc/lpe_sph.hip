@@ -1708,7 +1708,7 @@ __device__ int g_ftrace_on;
 
 // the coupling's per-block arrays, laid over the image once the fluid loop is done
 struct CouplePool {
-    PairGeo geo[PAIR_CAP];
+    PairTerm term[PAIR_CAP];
     CoupleIn in[HB];
     unsigned char flag[PAIR_CAP];
 };
@@ -1985,31 +1985,18 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
             // the particle's coupling inputs (pow only for a particle with hits)
             pool.in[threadIdx.x] = couple_in(st, cp, cp.nr > 0 && nh > 0);
             __syncthreads();
-            // ---- the pairs' geometry, round robin
+            // ---- the pairs (geometry and impulse in one pass: the
+            // velocities are final), round robin
             for (int q = threadIdx.x; q < total; q += HB) {
-                const int o = pOwn[q];
-                PairGeo ge;
-                pool.flag[q] = (unsigned char)couple_geom(pool.in[o].x, pool.in[o].y, cp, true, rc, pRig[q], ge);
-                pool.geo[q] = ge;
+                PairTerm t;
+                pool.flag[q] = (unsigned char)couple_pair(pool.in[pOwn[q]], cp, sp.dt, true, rc, pRig[q], acq,
+                                                          status, t);
+                pool.term[q] = t;
             }
             __syncthreads();
             FTR(2);
-            // ---- the impulse halves (finished velocities), round robin
-            for (int q = threadIdx.x; q < total; q += HB)
-                if (pool.flag[q] & PT_WANT) {
-                    float fx, fy;
-                    couple_imp(pool.in[pOwn[q]], cp, sp.dt, rc, pRig[q], pool.geo[q].pen, pool.geo[q].nx,
-                               pool.geo[q].ny, acq, status, fx, fy);
-                    pool.geo[q].nx = fx;                  // (the fold's fluid-force term)
-                    pool.geo[q].ny = fy;
-                    pool.flag[q] = (unsigned char)(pool.flag[q] | PT_IMP);
-                }
-            __syncthreads();
             if (live)
-                for (int q = off; q < off + nh; q++) {
-                    const PairGeo ge = pool.geo[q];
-                    a.fold(PairTerm{ge.ax, ge.ay, ge.nx, ge.ny}, pool.flag[q]);
-                }
+                for (int q = off; q < off + nh; q++) a.fold(pool.term[q], pool.flag[q]);
         }
         if (live) couple_finish(st, cp, a);
     }
@@ -3136,6 +3123,14 @@ static int sph_cu_count(lpe_ctx *ctx) {
     return cus;
 }
 
+// the density pass's block plans for the forces pass's LDS image
+// (LPE_FORCES_NOIMG=1: none -- both passes fall back to slot-offset lists and
+// global gathers, for A/B measurements)
+static Hood *sph_fplans(SphDev &d) {
+    static const bool off = getenv("LPE_FORCES_NOIMG") != nullptr;
+    return off ? nullptr : (Hood *)d.fplans;
+}
+
 static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr, float *rho, float *pr, bool nl = true) {
     SphDev &d = ctx->sph;
     const lpe_fluid_config &c = d.cfg;
@@ -3160,7 +3155,7 @@ static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr, float *rho, flo
         LPE_KERNEL(ctx, "k_density", k_density<true>, dim3(xcd_grid(nblk(n, HB))), dim3(HB), 0, ctx->stream, n,
                    nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
                    c.restDensity, d.W, d.H, d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)d.nbB,
-                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d), d.ovl_cur, (Hood *)d.fplans);
+                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d), d.ovl_cur, sph_fplans(d));
     else
         LPE_KERNEL(ctx, "k_density", k_density<false>, dim3(xcd_grid(nblk(n, HB))), dim3(HB), 0, ctx->stream, n,
                    nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
@@ -3277,13 +3272,13 @@ int sph_prelaunch(lpe_ctx *ctx, double dt_tick, const std::function<int(hipStrea
     d.pre = false;
     if (d.n <= 0 || !d.P.x) return LPE_OK;
     if (!d.pside) {
-        // the lowest priority: when the tick's solvers and this stream's
-        // kernels become ready together, the solvers' workgroups (a whole
-        // CU's LDS each) are dispatched first (LPE_PSIDE_PRIO=0: default
-        // priority, for A/B measurements)
+        // default priority.  (LPE_PSIDE_PRIO=1: the lowest, so that the
+        // solvers' workgroups would be dispatched first -- measured: the
+        // tick rate halves, 344 against 740 ticks/s on the settled metric
+        // scene, profiles/r04/prelaunch_priority_ab.txt)
         static const char *pp = getenv("LPE_PSIDE_PRIO");
         int least = 0, greatest = 0;
-        if ((!pp || std::atoi(pp) != 0) && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
+        if (pp && std::atoi(pp) != 0 && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess)
             LPE_HIP(ctx, hipStreamCreateWithPriority(&d.pside, hipStreamNonBlocking, least));
         else
             LPE_HIP(ctx, hipStreamCreateWithFlags(&d.pside, hipStreamNonBlocking));
@@ -3433,7 +3428,7 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
                            (step == 0 && pre) ? d.gp + 1 : d.gp,
                            d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart, d.rbinList,
                            rbin_aabb(d),
-                           d.acq, d.status, kn, (const Hood *)d.fplans);
+                           d.acq, d.status, kn, (const Hood *)sph_fplans(d));
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
         if (sh) sh->cur = 1 - sh->cur;               // P's slots are now the ones this pass wrote
         if (hook) {                                  // (lpe_world_tick: the rigid detection)

@@ -773,7 +773,8 @@ extern "C" int lpeo_colour_order(int nb, const lpe_body *bodies, int nc, const l
  *    of the pairs with contacts take part;
  *  - stripes: x0, x1 = min, max of their x; span = max |x_a - x_b| over the
  *    pairs whose two bodies are movable; q = (x1 - x0) / span; S = 1 unless
- *    q >= 2, else min(64, floor(q)) rounded down to even; w = (x1 - x0) / S;
+ *    there are more than 1024 pairs with contacts and q >= 2, else
+ *    min(64, floor(q)) rounded down to even; w = (x1 - x0) / S;
  *    stripe(b) = clamp(floor((x_b - x0) / w), 0, S - 1).  A pair whose two
  *    movable bodies lie more than one stripe apart (a rounding edge) makes it
  *    one stripe (S = 1);
@@ -793,6 +794,7 @@ extern "C" int lpeo_colour_order(int nb, const lpe_body *bodies, int nc, const l
  * receives the canonical step (group colour) of each pair, -1 without
  * contacts.  Returns the number of steps, or -1 (a group needs > 64 colours). */
 constexpr int STRIPES_MAX = 64;                       /* lpe_rigid.hip STRIPES_MAX */
+constexpr int STRIPE_MIN_PAIRS = 1024;                /* lpe_rigid.hip STRIPE_MIN_PAIRS */
 extern "C" int lpeo_stripe_order(int nb, const lpe_body *bodies, int nc, const lpe_contact *cs,
                                  int32_t *order, int32_t *pair_step, int npairs, int32_t *nstripes) {
     auto dep = [&](int i) {
@@ -823,7 +825,8 @@ extern "C" int lpeo_stripe_order(int nb, const lpe_body *bodies, int nc, const l
     }
     int S = 1;
     const double qn = (x1 - x0) / span;               /* (span 0: +inf; x1 == x0: 0 or NaN) */
-    if (any && x1 > x0 && qn >= 2.0) S = std::min(STRIPES_MAX, (int)std::floor(std::min(qn, 1e9))) & ~1;
+    if (any && x1 > x0 && m > STRIPE_MIN_PAIRS && qn >= 2.0)
+        S = std::min(STRIPES_MAX, (int)std::floor(std::min(qn, 1e9))) & ~1;
     const double w = (x1 - x0) / S;
     auto stripe = [&](int e) {
         if (S == 1) return 0;
