@@ -2143,6 +2143,8 @@ struct StripeBufs {
     int32_t *prank;        // [cap_pairs] rank inside (group, colour)
     int32_t *prowoff;      // [cap_pairs] first row inside (group, colour)
     int32_t *glist;        // [cap_pairs] pairs by group, ascending inside a group
+    int32_t *gla, *glb, *gln;  // [cap_pairs] by glist position: the pair's two movable bodies' slots in its
+                               // group's stripes (-1: static) and its contact count (k_group_colour)
     int32_t *gstart;       // [SGROUPS + 1]
     int32_t *gcnt;         // [SGROUPS][SCOLS][2] pairs, rows per (group, colour); [SGROUPS*SCOLS*2 + g]: colours of g
     int32_t *stepIdx;      // [SGROUPS * SCOLS] canonical step of (group, colour)
@@ -2340,7 +2342,11 @@ k_group_colour(const int32_t *__restrict__ npptr, const int32_t *__restrict__ co
     const int g = (int)blockIdx.x;
     const int S = counts[12];
     if (g >= S) return;                                // groups: bands 0, 2, .. and seams 1, 3, .. < S
+    const int s = (g >> 1) * 2 + (g & 1);               // band j: stripes 2j, 2j+1; seam j: 2j+1, 2j+2
+    const int u0 = sb.sbStart[s], u1 = sb.sbStart[min(s + 2, S)];
     {
+        // the list, and each listed pair's body slots and contact count
+        // (the colouring chain below then reads three plain arrays)
         const int np = *npptr;
         int base = sb.gstart[g];
         for (int p0 = 0; p0 < np; p0 += 4 * RTPB) {
@@ -2355,12 +2361,19 @@ k_group_colour(const int32_t *__restrict__ npptr, const int32_t *__restrict__ co
             int off = r_block_excl(c, &tot) + base;
 #pragma unroll
             for (int k = 0; k < 4; k++)
-                if (f[k]) sb.glist[off++] = p0 + 4 * (int)threadIdx.x + k;
+                if (f[k]) {
+                    const int p = p0 + 4 * (int)threadIdx.x + k;
+                    const int2 pr = pairs[p];
+                    const int fl = sb.pflag[p];
+                    sb.glist[off] = p;
+                    sb.gla[off] = (fl & 2) ? sb.bpos[pr.x] - u0 : -1;
+                    sb.glb[off] = (fl & 4) ? sb.bpos[pr.y] - u0 : -1;
+                    sb.gln[off] = ccount[p];
+                    off++;
+                }
             base += tot;
         }
     }
-    const int s = (g >> 1) * 2 + (g & 1);               // band j: stripes 2j, 2j+1; seam j: 2j+1, 2j+2
-    const int u0 = sb.sbStart[s], u1 = sb.sbStart[min(s + 2, S)];
     for (int i = (int)threadIdx.x; i < u1 - u0; i += RTPB) used[i] = 0ull;
     __syncthreads();                                   // (the list, in global memory, and the masks)
     if (threadIdx.x >= 64) return;
@@ -2368,19 +2381,59 @@ k_group_colour(const int32_t *__restrict__ npptr, const int32_t *__restrict__ co
     const int g0 = sb.gstart[g], g1 = sb.gstart[g + 1];
     int ncol = 0, fault = 0;
     int cp = 0, cr = 0;                                   // lane c: colour c's pairs and rows so far
+    const bool regs = u1 - u0 <= 256;                     // (block-uniform) the masks fit four registers
+    unsigned long long mk0 = 0ull, mk1 = 0ull, mk2 = 0ull, mk3 = 0ull;
+    // chunk loads one chunk ahead (independent of the chain)
+    int np_ = -1, nma = -1, nmb = -1, nmn = 0;
+    if (g0 + lane < g1) { np_ = sb.glist[g0 + lane]; nma = sb.gla[g0 + lane]; nmb = sb.glb[g0 + lane]; nmn = sb.gln[g0 + lane]; }
     for (int c0 = g0; c0 < g1; c0 += 64) {
         const int t = c0 + lane;
-        int p = -1, ma = -1, mb = -1, mn = 0;
-        if (t < g1) {
-            p = sb.glist[t];
-            const int2 pr = pairs[p];
-            const int f = sb.pflag[p];
-            ma = (f & 2) ? sb.bpos[pr.x] - u0 : -1;
-            mb = (f & 4) ? sb.bpos[pr.y] - u0 : -1;
-            mn = ccount[p];
+        const int p = np_, ma = nma, mb = nmb, mn = nmn;
+        np_ = -1; nma = -1; nmb = -1; nmn = 0;
+        if (t + 64 < g1) {
+            np_ = sb.glist[t + 64]; nma = sb.gla[t + 64]; nmb = sb.glb[t + 64]; nmn = sb.gln[t + 64];
         }
         const int m = min(64, g1 - c0);
         int myc = 0, myrank = 0, myrow = 0;
+        if (regs) {
+            // the masks in registers: slot u in lane u & 63 of mk[u >> 6]
+            // (no memory round trip in the chain)
+            for (int i = 0; i < m; i++) {
+                const int a = __builtin_amdgcn_readlane(ma, i), b = __builtin_amdgcn_readlane(mb, i);
+                // (selects on the wave-uniform register number: no indexed access)
+                const int ra = a >> 6, rb = b >> 6;
+                const unsigned long long va = ra <= 0 ? mk0 : (ra == 1 ? mk1 : (ra == 2 ? mk2 : mk3));
+                const unsigned long long vb = rb <= 0 ? mk0 : (rb == 1 ? mk1 : (rb == 2 ? mk2 : mk3));
+                const int la = a & 63, lb = b & 63;
+                const unsigned long long ua =
+                    ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(va >> 32), la) << 32) |
+                    (uint32_t)__builtin_amdgcn_readlane((int)va, la);
+                const unsigned long long ub =
+                    ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(vb >> 32), lb) << 32) |
+                    (uint32_t)__builtin_amdgcn_readlane((int)vb, lb);
+                const unsigned long long forb = (a >= 0 ? ua : 0ull) | (b >= 0 ? ub : 0ull);
+                const int c = forb == ~0ull ? 0 : __ffsll((long long)~forb) - 1;
+                fault |= forb == ~0ull;
+                const unsigned long long bit = 1ull << c;
+                const unsigned long long sa = (a >= 0 && lane == la) ? bit : 0ull;   // (a's lane)
+                const unsigned long long sb2 = (b >= 0 && lane == lb) ? bit : 0ull;
+                mk0 |= (ra == 0 ? sa : 0ull) | (rb == 0 ? sb2 : 0ull);
+                mk1 |= (ra == 1 ? sa : 0ull) | (rb == 1 ? sb2 : 0ull);
+                mk2 |= (ra == 2 ? sa : 0ull) | (rb == 2 ? sb2 : 0ull);
+                mk3 |= (ra == 3 ? sa : 0ull) | (rb == 3 ? sb2 : 0ull);
+                ncol = max(ncol, c + 1);
+                const int rank = __builtin_amdgcn_readlane(cp, c), row = __builtin_amdgcn_readlane(cr, c);
+                const int n = __builtin_amdgcn_readlane(mn, i);
+                if (lane == c) { cp += 1; cr += n; }
+                if (lane == i) { myc = c; myrank = rank; myrow = row; }
+            }
+            if (t < g1) {
+                sb.pcolg[p] = myc;
+                sb.prank[p] = myrank;
+                sb.prowoff[p] = myrow;
+            }
+            continue;
+        }
         int a = __builtin_amdgcn_readlane(ma, 0), b = __builtin_amdgcn_readlane(mb, 0);
         unsigned long long ua = a >= 0 ? used[a] : 0ull, ub = b >= 0 ? used[b] : 0ull;
         for (int i = 0; i < m; i++) {
@@ -3640,7 +3693,8 @@ static StripeBufs *stripe_bufs(lpe_ctx *ctx, RigidDev *d) {
     if (d->cap_pairs > d->cap_stripe_pairs || !sb->pgroup) {
         const size_t P = (size_t)std::max(d->cap_pairs, 1);
         if (grow(&sb->pgroup, P) || grow(&sb->pcolg, P) || grow(&sb->prank, P) || grow(&sb->prowoff, P) ||
-            grow(&sb->glist, P) || grow(&sb->pflag, P) || grow(&sb->px, P) || grow(&sb->bred, 3 * (P / RTPB + 1)))
+            grow(&sb->glist, P) || grow(&sb->pflag, P) || grow(&sb->px, P) || grow(&sb->bred, 3 * (P / RTPB + 1)) ||
+            grow(&sb->gla, P) || grow(&sb->glb, P) || grow(&sb->gln, P))
             return nullptr;
         d->cap_stripe_pairs = d->cap_pairs;
     }

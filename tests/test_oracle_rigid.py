@@ -126,3 +126,23 @@ def test_portable_trig_within_an_ulp_of_libm(oracle_mod, path):
         np.testing.assert_array_equal(cs[k], ref[k], err_msg=k)
     for k in ("nx", "ny", "pen", "px", "py"):
         np.testing.assert_allclose(cs[k], ref[k], rtol=1e-12, atol=1e-13, err_msg=k)
+
+
+def test_stripe_rule_small_and_large(oracle_mod):
+    """The canonical striped order's stripe count: one stripe for a scene of
+    at most 1024 pairs with contacts (the box stack's 128), stripes for the
+    metric pile (8,226) -- the rule lpe_rigid.hip k_stripe_setup runs; every
+    contact appears once in the order, and a pair's step is within the
+    step count."""
+    for name, small in (("rigid_C1_t120.npz", True), ("pile_M_t250.npz", False)):
+        z = np.load(os.path.join(ROOT, "tests", "golden", name))
+        b = z["before_rigid"] if "before_rigid" in z else z["bodies"]
+        cfg = lpe.rigid_config(universe=float(z["universe"]) if "universe" in z else 32.0)
+        pairs = oracle_mod.broadphase(cfg, b, z["verts"])
+        cs = oracle_mod.narrowphase(b, z["verts"], pairs)
+        order, step, nsteps, S = oracle_mod.stripe_order(b, cs, len(pairs))
+        with_contacts = len(np.unique(cs["pair"]))
+        assert (with_contacts <= 1024) == small
+        assert (S == 1) == small, (name, S, with_contacts)
+        np.testing.assert_array_equal(np.sort(order), np.arange(len(cs)))
+        assert step.max() < nsteps and (step >= 0).sum() == with_contacts
