@@ -43,8 +43,6 @@ struct SphDev {
     uint4 *nlist = nullptr;       // per-slot neighbour list (int16, 8 per uint4), [cap/8][cap_n]: LDS indices of
                                   // the forces pass's image, or slot offsets k - s (ncount's NL_OFFS bit)
     void *fplans = nullptr;       // the density pass's block plans (Hood), for the forces pass's image
-    void *hterm = nullptr;        // the forces pass's helper items: 8 terms (float2) each, per wave HELP_Q
-    uint32_t *hmask = nullptr;    //   and their masks
     float *rgrid = nullptr;       // renderer density grid, two W*H buffers (lpe_render_density)
     size_t cap_rgrid = 0;
     uint32_t *rmax = nullptr;     // renderer: max of the blurred grid (float bits)

@@ -1735,16 +1735,6 @@ __device__ __forceinline__ bool pair_term(const PairOwn &o, const PairConst &k, 
     fy -= fVisc * vy_ij;
     return true;
 }
-// In-wave helpers for the long lists (LDS-image lists only): a particle with
-// more than HELP_OWN neighbours keeps its first HELP_OWN, and its further list
-// groups (8 entries each) become items that the wave's lanes compute after
-// their own loops -- each item's eight terms into the block's scratch
-// (hterm / hmask) -- and that the particle then adds in list order.  The
-// sums are the same additions in the same order; only where the terms are
-// computed changes.  HELP_Q items per wave at most (a particle whose items
-// would pass the quota computes the rest itself, in order).
-static constexpr int HELP_OWN = 24;
-static constexpr int HELP_Q = 128;
 
 // the coupling's per-block arrays, laid over the image once the fluid loop is done
 struct CouplePool {
@@ -1763,8 +1753,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                 const int32_t *__restrict__ rbinStart, const int32_t *__restrict__ rbinList,
                 const float4 *__restrict__ rbinAabb,
                 unsigned long long *__restrict__ acq,
-                int32_t *__restrict__ status, KickNext kn, const Hood *__restrict__ fplans,
-                float4 *__restrict__ hterm, uint32_t *__restrict__ hmask) {
+                int32_t *__restrict__ status, KickNext kn, const Hood *__restrict__ fplans) {
     // plain block order (blocks go round robin over the XCDs): the costly
     // blocks, the particles in and around the rigid pile, are one spatial
     // run that an XCD-contiguous mapping (xcd_block) would put on one XCD
@@ -1946,10 +1935,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         // order, so the heavy pair math runs only on real neighbours.
         // Software-pipelined in quads: the records of the next quad (and the
         // list word after the next) are in flight while a quad is computed.
-        // With helpers (hterm, an image list longer than HELP_OWN) the
-        // particle's own loop stops at HELP_OWN and the rest follows below.
-        const bool helped = hterm && img && !offs && cnt > HELP_OWN;
-        const int jend = helped ? HELP_OWN : cnt;
+        const int jend = cnt;
         struct Quad { FRec r[4]; };
         // records of list entries j .. j+3 held by words (wa, wb) of a list group
         auto quad = [&](uint32_t wa, uint32_t wb, int j) {
@@ -1987,86 +1973,6 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         walk_neighbours<4>(xi, yi, sp.eps, cs, walk_reach(hi, cs), g, sp.W, sp.H, sp.ox, sp.oy, start,
                            [&](int k, int) { return FRec{nbA[k], nbB[k]}; },
                            [&](int k, const FRec &o) { if (k != s) pair(o.a, o.b); });
-    }
-    if (hterm && img) {
-        // ---- the wave's helper items (wave-uniform; see HELP_OWN) ----------
-        const bool helped = live && !offs && cnt > HELP_OWN && cnt <= NLIST_CAP && !(cnt > NLIST_CAP);
-        const int e = helped ? ((cnt - HELP_OWN + 7) >> 3) : 0;   // list groups past the own ones
-        int incl = e;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int v = __shfl_up(incl, d);
-            if (lane >= d) incl += v;
-        }
-        const int excl = incl - e;
-        const int total = __shfl(incl, 63);
-        if (total > 0) {
-            const size_t base = ((size_t)lb * (HB / 64) + (threadIdx.x >> 6)) * HELP_Q;   // the wave's items
-            const int nitems = min(total, HELP_Q);
-            for (int k0 = 0; k0 < nitems; k0 += 64) {  // (every lane takes part in the shuffles)
-                const int k = k0 + lane;
-                const int kk = min(k, nitems - 1);
-                int o = 0;                             // the item's particle: lanes with incl <= kk
-#pragma unroll
-                for (int st = 32; st >= 1; st >>= 1) {
-                    const int v = __shfl(incl, min(o + st - 1, 63));
-                    if (o + st <= 64 && v <= kk) o += st;
-                }
-                const PairOwn ow{__shfl(xi, o), __shfl(yi, o), __shfl(vxi, o), __shfl(vyi, o), __shfl(pti, o),
-                                 __shfl((int)rhoi_ok, o) != 0};
-                const int so = __shfl(s, o), co = __shfl(cnt, o);
-                const int g = HELP_OWN / 8 + (kk - __shfl(excl, o));   // the item's list group
-                if (k >= nitems) continue;
-                const uint4 w = nlist[(size_t)g * ns + so];
-                const uint32_t w8[8] = {w.x & 0xffffu, w.x >> 16, w.y & 0xffffu, w.y >> 16,
-                                        w.z & 0xffffu, w.z >> 16, w.w & 0xffffu, w.w >> 16};
-                float2 t[8];
-                uint32_t msk = 0u;
-#pragma unroll
-                for (int u = 0; u < 8; u++) {
-                    t[u] = make_float2(0.f, 0.f);
-                    if (8 * g + u < co) {
-                        const int ki = (int)w8[u];
-                        float fx, fy;
-                        if (pair_term(ow, pk, fimg[ki], fimg[FCAP + ki], fx, fy)) {
-                            t[u] = make_float2(fx, fy);
-                            msk |= 1u << u;
-                        }
-                    }
-                }
-                float4 *dst = hterm + (base + k) * 4;
-#pragma unroll
-                for (int q = 0; q < 4; q++) dst[q] = make_float4(t[2 * q].x, t[2 * q].y, t[2 * q + 1].x, t[2 * q + 1].y);
-                hmask[base + k] = msk;
-            }
-            // the wave's stores before its loads of them, past this CU's L1
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            if (helped) {
-                const int ng = (cnt + 7) >> 3;
-                for (int g = HELP_OWN / 8; g < ng; g++) {
-                    const int k = excl + (g - HELP_OWN / 8);
-                    if (k < HELP_Q) {
-                        const float4 *src = hterm + (base + k) * 4;
-                        const uint32_t msk = hmask[base + k];
-#pragma unroll
-                        for (int q = 0; q < 4; q++) {
-                            const float4 v = src[q];
-                            if (msk & (1u << (2 * q))) { sumFx += v.x; sumFy += v.y; }
-                            if (msk & (1u << (2 * q + 1))) { sumFx += v.z; sumFy += v.w; }
-                        }
-                    } else {                           // (past the wave's quota: this particle itself)
-                        const uint4 w = nlist[(size_t)g * ns + s];
-                        const uint32_t w8[8] = {w.x & 0xffffu, w.x >> 16, w.y & 0xffffu, w.y >> 16,
-                                                w.z & 0xffffu, w.z >> 16, w.w & 0xffffu, w.w >> 16};
-                        for (int u = 0; u < 8 && 8 * g + u < cnt; u++) {
-                            const int ki = (int)w8[u];
-                            pair(fimg[ki], fimg[FCAP + ki]);
-                        }
-                    }
-                }
-            }
-        }
     }
     FTRMAX(5, wall_clock64());
     FTRMAX(6, cnt);
@@ -2622,7 +2528,7 @@ static void sph_free(SphDev &d) {
     void *ptrs[] = {d.ovl, d.rho, d.pr, d.rhoN, d.prN, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.refInv, d.stage, d.count, d.start, d.cursor,
                     d.rowtot, d.bucket, d.bovf,
                     d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.raabb, d.accum, d.acq, d.rbinStart, d.rgrid, d.rmax,
-                    d.rbinList, d.rbinCount, d.coupleBody, d.plans, d.fplans, d.hterm, d.hmask};
+                    d.rbinList, d.rbinCount, d.coupleBody, d.plans, d.fplans};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     hipEvent_t evs[] = {d.preReady, d.preDone, d.fbgDone};
     for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
@@ -2838,7 +2744,7 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     pstate_free(d.P);
     pstate_free(d.S);
     void *ptrs[] = {d.rho, d.pr, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.bboxPart, d.refInv,
-                    d.stage, d.rhoN, d.prN, d.fplans, d.hterm, d.hmask};
+                    d.stage, d.rhoN, d.prN, d.fplans};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     size_t N = (size_t)std::max(n, 1);
     int st = pstate_alloc(ctx, d.P, N, true);
@@ -2854,11 +2760,6 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     LPE_HIP(ctx, hipMalloc((void **)&d.nlist, sizeof(uint4) * N * (NLIST_CAP / 8)));
     LPE_HIP(ctx, hipMalloc((void **)&d.ncount, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc(&d.fplans, sizeof(Hood) * ((N + HB - 1) / HB)));
-    {
-        const size_t items = ((N + HB - 1) / HB) * (HB / 64) * (size_t)HELP_Q;
-        LPE_HIP(ctx, hipMalloc(&d.hterm, sizeof(float4) * 4 * items));
-        LPE_HIP(ctx, hipMalloc((void **)&d.hmask, sizeof(uint32_t) * items));
-    }
     LPE_HIP(ctx, hipMalloc((void **)&d.key, sizeof(uint32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpId, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpOld, sizeof(int32_t) * N));
@@ -3246,13 +3147,6 @@ static Hood *sph_fplans(SphDev &d) {
     return off ? nullptr : (Hood *)d.fplans;
 }
 
-// the forces pass's helper scratch (LPE_FORCES_NOHELP=1: none -- every
-// particle walks its whole list, for A/B measurements)
-static float4 *sph_hterm(SphDev &d) {
-    static const bool off = getenv("LPE_FORCES_NOHELP") != nullptr;
-    return off ? nullptr : (float4 *)d.hterm;
-}
-
 static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr, float *rho, float *pr, bool nl = true) {
     SphDev &d = ctx->sph;
     const lpe_fluid_config &c = d.cfg;
@@ -3550,7 +3444,7 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
                            (step == 0 && pre) ? d.gp + 1 : d.gp,
                            d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart, d.rbinList,
                            rbin_aabb(d),
-                           d.acq, d.status, kn, (const Hood *)sph_fplans(d), sph_hterm(d), d.hmask);
+                           d.acq, d.status, kn, (const Hood *)sph_fplans(d));
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
         if (sh) sh->cur = 1 - sh->cur;               // P's slots are now the ones this pass wrote
         if (hook) {                                  // (lpe_world_tick: the rigid detection)
