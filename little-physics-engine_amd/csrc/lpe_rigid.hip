@@ -2334,7 +2334,11 @@ k_stripe_setup(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict
 // forwarding), so a pair costs its compare / select chain, not LDS round
 // trips.
 // The block first lists its group's pairs in ascending order (a stable
-// compaction by all RTPB threads), then wave 0 colours them.
+// compaction by all RTPB threads), then wave 0 colours them.  (Round 4
+// measured a block-wide Jones-Plassmann colouring with ascending-order
+// priority -- the same colours as the sequential pass -- and dropped it: in
+// entity order a pair's lower neighbours form chains as long as the scene,
+// so the rounds were 2-3x slower than the chain.)
 __global__ void __launch_bounds__(RTPB)
 k_group_colour(const int32_t *__restrict__ npptr, const int32_t *__restrict__ counts, const int2 *__restrict__ pairs,
                const int32_t *__restrict__ ccount, StripeBufs sb) {
