@@ -2326,19 +2326,30 @@ k_stripe_setup(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict
 // lowest colour free on the pair's movable bodies), the pair's rank and row
 // offset inside its (group, colour), the group's colour sizes.  The bodies'
 // colour masks live in LDS by stripe-list slot (the group's bodies lie in
-// its one or two stripes).  The colouring is one sequential chain, run by
-// the whole wave on wave-uniform values: the chunk's pair bodies and row
-// counts are read across lanes (readlane), colour c's pair / row counters
-// live in lane c, and the next pair's masks are loaded before the current
-// pair's are stored (a body the two pairs share takes the stored value:
-// forwarding), so a pair costs its compare / select chain, not LDS round
-// trips.
+// its one or two stripes) between chunks of 32 pairs; inside a chunk they
+// live in the lanes of the pairs that last changed them.  The colouring is
+// one sequential chain, run by the whole wave on wave-uniform values: each
+// body's source lane is found before the chain from the chunk's body lists
+// alone, colour c's pair / row counters live in lane c, so a pair costs four
+// lane reads, the first free colour and a lane write (round 4: ~30
+// instructions a pair, from ~115 with the masks indexed by slot).
 // The block first lists its group's pairs in ascending order (a stable
 // compaction by all RTPB threads), then wave 0 colours them.  (Round 4
 // measured a block-wide Jones-Plassmann colouring with ascending-order
 // priority -- the same colours as the sequential pass -- and dropped it: in
 // entity order a pair's lower neighbours form chains as long as the scene,
 // so the rounds were 2-3x slower than the chain.)
+#ifdef LPE_PTRACE
+__device__ unsigned long long g_ctrace[SGROUPS][8];
+extern "C" int lpe_ctrace(unsigned long long *host) {
+    if (host) (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ctrace), sizeof(unsigned long long) * SGROUPS * 8);
+    return 0;
+}
+#define CTR(k, v) do { if (threadIdx.x == 0) g_ctrace[blockIdx.x][k] = (v); } while (0)
+#else
+#define CTR(k, v) do { } while (0)
+#endif
+
 __global__ void __launch_bounds__(RTPB)
 k_group_colour(const int32_t *__restrict__ npptr, const int32_t *__restrict__ counts, const int2 *__restrict__ pairs,
                const int32_t *__restrict__ ccount, StripeBufs sb) {
@@ -2346,6 +2357,7 @@ k_group_colour(const int32_t *__restrict__ npptr, const int32_t *__restrict__ co
     const int g = (int)blockIdx.x;
     const int S = counts[12];
     if (g >= S) return;                                // groups: bands 0, 2, .. and seams 1, 3, .. < S
+    CTR(0, wall_clock64());
     const int s = (g >> 1) * 2 + (g & 1);               // band j: stripes 2j, 2j+1; seam j: 2j+1, 2j+2
     const int u0 = sb.sbStart[s], u1 = sb.sbStart[min(s + 2, S)];
     {
@@ -2378,105 +2390,91 @@ k_group_colour(const int32_t *__restrict__ npptr, const int32_t *__restrict__ co
             base += tot;
         }
     }
+    CTR(1, wall_clock64());
     for (int i = (int)threadIdx.x; i < u1 - u0; i += RTPB) used[i] = 0ull;
     __syncthreads();                                   // (the list, in global memory, and the masks)
+    CTR(2, wall_clock64());
     if (threadIdx.x >= 64) return;
     const int lane = (int)threadIdx.x;
     const int g0 = sb.gstart[g], g1 = sb.gstart[g + 1];
     int ncol = 0, fault = 0;
     int cp = 0, cr = 0;                                   // lane c: colour c's pairs and rows so far
-    const bool regs = u1 - u0 <= 256;                     // (block-uniform) the masks fit four registers
-    unsigned long long mk0 = 0ull, mk1 = 0ull, mk2 = 0ull, mk3 = 0ull;
-    // chunk loads one chunk ahead (independent of the chain)
-    int np_ = -1, nma = -1, nmb = -1, nmn = 0;
-    if (g0 + lane < g1) { np_ = sb.glist[g0 + lane]; nma = sb.gla[g0 + lane]; nmb = sb.glb[g0 + lane]; nmn = sb.gln[g0 + lane]; }
-    for (int c0 = g0; c0 < g1; c0 += 64) {
-        const int t = c0 + lane;
-        const int p = np_, ma = nma, mb = nmb, mn = nmn;
-        np_ = -1; nma = -1; nmb = -1; nmn = 0;
-        if (t + 64 < g1) {
-            np_ = sb.glist[t + 64]; nma = sb.gla[t + 64]; nmb = sb.glb[t + 64]; nmn = sb.gln[t + 64];
+    // Chunks of 32 pairs; lane l is the pair (l & 31)'s body on side l >> 5
+    // (A, B).  Its register R holds that body's colour mask: on entry the
+    // mask after the earlier chunks (from LDS), after the pair its mask with
+    // the pair's colour added.  A pair reads each body's mask from the lane of
+    // the chunk's last earlier pair on that body (src: found before the
+    // chain, from the body lists alone), or from its own lane, so the chain is
+    // two 64-bit reads, the first free colour and two lane writes per pair.
+    const int side = lane >> 5, k = lane & 31;
+    auto fetch = [&](int c0, int &p, int &body, int &n) {
+        const int t = c0 + k;
+        p = -1; body = -1; n = 0;
+        if (t < g1) {
+            body = side ? sb.glb[t] : sb.gla[t];
+            if (!side) { p = sb.glist[t]; n = sb.gln[t]; }
         }
-        const int m = min(64, g1 - c0);
+    };
+    int np_, nbody, nn;
+    fetch(g0, np_, nbody, nn);                            // (one chunk ahead: off the chain)
+    for (int c0 = g0; c0 < g1; c0 += 32) {
+        const int p = np_, body = nbody, n = nn;
+        fetch(c0 + 32, np_, nbody, nn);
+        const int m = min(32, g1 - c0);
+        const unsigned long long R0 = body >= 0 ? used[body] : 0ull;
+        uint32_t Rlo = (uint32_t)R0, Rhi = (uint32_t)(R0 >> 32);
+        // (a static body's key is unique to its lane: it matches no other)
+        const int key = body >= 0 ? body : -2 - lane;
+        int src = lane;                                   // the lane holding the body's mask before the pair
+        int later = 0;                                    // a later pair of the chunk has the body
+        for (int j = 0; j < m; j++) {
+            const int s0 = __builtin_amdgcn_readlane(key, j), s1 = __builtin_amdgcn_readlane(key, j + 32);
+            const bool before = j < k;
+            src = (before && s0 == key) ? j : src;
+            src = (before && s1 == key) ? j + 32 : src;
+            later |= (j > k) & ((s0 == key) | (s1 == key));
+        }
         int myc = 0, myrank = 0, myrow = 0;
-        if (regs) {
-            // the masks in registers: slot u in lane u & 63 of mk[u >> 6]
-            // (no memory round trip in the chain)
-            for (int i = 0; i < m; i++) {
-                const int a = __builtin_amdgcn_readlane(ma, i), b = __builtin_amdgcn_readlane(mb, i);
-                // (selects on the wave-uniform register number: no indexed access)
-                const int ra = a >> 6, rb = b >> 6;
-                const unsigned long long va = ra <= 0 ? mk0 : (ra == 1 ? mk1 : (ra == 2 ? mk2 : mk3));
-                const unsigned long long vb = rb <= 0 ? mk0 : (rb == 1 ? mk1 : (rb == 2 ? mk2 : mk3));
-                const int la = a & 63, lb = b & 63;
-                const unsigned long long ua =
-                    ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(va >> 32), la) << 32) |
-                    (uint32_t)__builtin_amdgcn_readlane((int)va, la);
-                const unsigned long long ub =
-                    ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(vb >> 32), lb) << 32) |
-                    (uint32_t)__builtin_amdgcn_readlane((int)vb, lb);
-                const unsigned long long forb = (a >= 0 ? ua : 0ull) | (b >= 0 ? ub : 0ull);
-                const int c = forb == ~0ull ? 0 : __ffsll((long long)~forb) - 1;
-                fault |= forb == ~0ull;
-                const unsigned long long bit = 1ull << c;
-                const unsigned long long sa = (a >= 0 && lane == la) ? bit : 0ull;   // (a's lane)
-                const unsigned long long sb2 = (b >= 0 && lane == lb) ? bit : 0ull;
-                mk0 |= (ra == 0 ? sa : 0ull) | (rb == 0 ? sb2 : 0ull);
-                mk1 |= (ra == 1 ? sa : 0ull) | (rb == 1 ? sb2 : 0ull);
-                mk2 |= (ra == 2 ? sa : 0ull) | (rb == 2 ? sb2 : 0ull);
-                mk3 |= (ra == 3 ? sa : 0ull) | (rb == 3 ? sb2 : 0ull);
-                ncol = max(ncol, c + 1);
-                const int rank = __builtin_amdgcn_readlane(cp, c), row = __builtin_amdgcn_readlane(cr, c);
-                const int n = __builtin_amdgcn_readlane(mn, i);
-                if (lane == c) { cp += 1; cr += n; }
-                if (lane == i) { myc = c; myrank = rank; myrow = row; }
-            }
-            if (t < g1) {
-                sb.pcolg[p] = myc;
-                sb.prank[p] = myrank;
-                sb.prowoff[p] = myrow;
-            }
-            continue;
-        }
-        int a = __builtin_amdgcn_readlane(ma, 0), b = __builtin_amdgcn_readlane(mb, 0);
-        unsigned long long ua = a >= 0 ? used[a] : 0ull, ub = b >= 0 ? used[b] : 0ull;
         for (int i = 0; i < m; i++) {
-            // the next pair's bodies and masks (loads issued before this pair's stores)
-            const int a2 = i + 1 < m ? __builtin_amdgcn_readlane(ma, i + 1) : -1;
-            const int b2 = i + 1 < m ? __builtin_amdgcn_readlane(mb, i + 1) : -1;
-            // (lane 0 loads a2's mask, lane 1 b2's: a per-lane load whose wait
-            // falls after this pair's chain, where the lanes are read)
-            const int la = lane == 0 ? a2 : (lane == 1 ? b2 : -1);
-            const unsigned long long lu = la >= 0 ? used[la] : 0ull;
-            const unsigned long long forb = ua | ub;
+            const int sa = __builtin_amdgcn_readlane(src, i), sb_ = __builtin_amdgcn_readlane(src, i + 32);
+            const int ni = __builtin_amdgcn_readlane(n, i);
+            const unsigned long long ua =
+                ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)Rhi, sa) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)Rlo, sa);
+            const unsigned long long ub =
+                ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)Rhi, sb_) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)Rlo, sb_);
+            const unsigned long long forb = ua | ub;      // (a static body's lane holds 0)
             const int c = forb == ~0ull ? 0 : __ffsll((long long)~forb) - 1;
             fault |= forb == ~0ull;
             const unsigned long long bit = 1ull << c;
-            const unsigned long long na = ua | bit, nb2 = ub | bit;
-            if (a >= 0) used[a] = na;
-            if (b >= 0) used[b] = nb2;
-            unsigned long long ua2 = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(lu >> 32), 0) << 32) |
-                                     (uint32_t)__builtin_amdgcn_readlane((int)lu, 0);
-            unsigned long long ub2 = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(lu >> 32), 1) << 32) |
-                                     (uint32_t)__builtin_amdgcn_readlane((int)lu, 1);
-            if (a2 >= 0 && a2 == a) ua2 = na;
-            if (a2 >= 0 && a2 == b) ua2 = nb2;
-            if (b2 >= 0 && b2 == a) ub2 = na;
-            if (b2 >= 0 && b2 == b) ub2 = nb2;
+            const unsigned long long na = ua | bit, nb = ub | bit;
+            const bool ia = lane == i, ib = lane == i + 32;
+            Rlo = ia ? (uint32_t)na : (ib ? (uint32_t)nb : Rlo);
+            Rhi = ia ? (uint32_t)(na >> 32) : (ib ? (uint32_t)(nb >> 32) : Rhi);
             ncol = max(ncol, c + 1);
             // rank and row offset in ascending order
             const int rank = __builtin_amdgcn_readlane(cp, c), row = __builtin_amdgcn_readlane(cr, c);
-            const int n = __builtin_amdgcn_readlane(mn, i);
-            if (lane == c) { cp += 1; cr += n; }
-            if (lane == i) { myc = c; myrank = rank; myrow = row; }
-            a = a2; b = b2; ua = ua2; ub = ub2;
+            const bool ic = lane == c;
+            cp += ic ? 1 : 0;
+            cr += ic ? ni : 0;
+            myc = ia ? c : myc;
+            myrank = ia ? rank : myrank;
+            myrow = ia ? row : myrow;
         }
-        if (t < g1) {
+        // (one writer per body; read by the next chunk)
+        if (body >= 0 && !later) used[body] = ((unsigned long long)Rhi << 32) | Rlo;
+        if (!side && p >= 0) {
             sb.pcolg[p] = myc;
             sb.prank[p] = myrank;
             sb.prowoff[p] = myrow;
         }
     }
+    CTR(3, wall_clock64());
+    CTR(4, (unsigned long long)*npptr);
+    CTR(5, (unsigned long long)(g1 - g0));
+    CTR(6, (unsigned long long)(u1 - u0));
+    CTR(7, (unsigned long long)ncol);
     int32_t *gc = sb.gcnt + (size_t)g * SCOLS * 2;
     gc[2 * lane] = cp;
     gc[2 * lane + 1] = cr;
