@@ -2135,7 +2135,7 @@ static constexpr int STRIPE_MIN_PAIRS = 1024;
 struct StripeBufs {
     int32_t *bstripe;      // [nb] stripe of a movable body in a contact pair, else -1
     int32_t *bpos;         // [nb] slot of a contact-pair body in sbList, else -1
-    double *bred;          // [3 blocks of k_stripe_pairs] x min, x max, longest pair
+    double *bred;          // [4 per block of k_stripe_pairs] x min, x max, longest pair, pairs with contacts
     int32_t *pflag;        // [cap_pairs] 1 has contacts, 2 A movable, 4 B movable
     double2 *px;           // [cap_pairs] x of A and B
     int32_t *pgroup;       // [cap_pairs] group of a pair with contacts, else -1
@@ -2165,15 +2165,18 @@ __device__ __forceinline__ int stripe_of(double x, double x0, double w, int S) {
 }
 
 // per pair with contacts: which bodies move and their x; per block the range
-// of the movable bodies' x and the longest pair (sb.bred, 3 doubles a block)
+// of the movable bodies' x, the longest pair and the pairs with contacts
+// (sb.bred, 4 doubles a block)
 __global__ void __launch_bounds__(RTPB)
 k_stripe_pairs(const int32_t *__restrict__ npptr, const int2 *__restrict__ pairs,
                const int32_t *__restrict__ ccount, const lpe_body *__restrict__ bodies, StripeBufs sb) {
     __shared__ double wr[3][RTPB / 64];
+    __shared__ int wc[RTPB / 64];
     const int p = blockIdx.x * RTPB + threadIdx.x;
     const int np = *npptr;
     if ((int)(blockIdx.x * RTPB) >= np) return;
     double mn = 1.7976931348623157e308, mx = -1.7976931348623157e308, sp = 0.0;
+    bool has = false;
     if (p < np) {
         int f = 0;
         double2 x = make_double2(0.0, 0.0);
@@ -2183,6 +2186,7 @@ k_stripe_pairs(const int32_t *__restrict__ npptr, const int2 *__restrict__ pairs
             const bool da = colour_dep(A), db = colour_dep(B);
             x = make_double2(A.x, B.x);
             f = 1 | (da ? 2 : 0) | (db ? 4 : 0);
+            has = true;
             if (da) { mn = fmin(mn, x.x); mx = fmax(mx, x.x); }
             if (db) { mn = fmin(mn, x.y); mx = fmax(mx, x.y); }
             if (da && db) sp = fabs(x.x - x.y);
@@ -2196,63 +2200,83 @@ k_stripe_pairs(const int32_t *__restrict__ npptr, const int2 *__restrict__ pairs
         sp = fmax(sp, __shfl_xor(sp, off));
     }
     const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) { wr[0][w] = mn; wr[1][w] = mx; wr[2][w] = sp; }
+    const int c = __popcll(__ballot(has));
+    if ((threadIdx.x & 63) == 0) { wr[0][w] = mn; wr[1][w] = mx; wr[2][w] = sp; wc[w] = c; }
     __syncthreads();
     if (threadIdx.x == 0) {
+        int n = wc[0];
         for (int k = 1; k < RTPB / 64; k++) {
-            mn = fmin(mn, wr[0][k]); mx = fmax(mx, wr[1][k]); sp = fmax(sp, wr[2][k]);
+            mn = fmin(mn, wr[0][k]); mx = fmax(mx, wr[1][k]); sp = fmax(sp, wr[2][k]); n += wc[k];
         }
-        sb.bred[3 * blockIdx.x] = mn;
-        sb.bred[3 * blockIdx.x + 1] = mx;
-        sb.bred[3 * blockIdx.x + 2] = sp;
+        sb.bred[4 * blockIdx.x] = mn;
+        sb.bred[4 * blockIdx.x + 1] = mx;
+        sb.bred[4 * blockIdx.x + 2] = sp;
+        sb.bred[4 * blockIdx.x + 3] = (double)n;
     }
 }
 
 // One workgroup: the stripe count and width, the stripes' body lists (then
 // the static bodies of contact pairs), the pairs' groups and the groups'
-// sizes (counts[12] = S, counts[13] = workgroups).
+// sizes (counts[12] = S, counts[13] = workgroups).  The stripe count comes
+// first, from k_stripe_pairs' partials alone, so one pass over the pairs
+// marks their bodies, checks the one-stripe rule and files them in groups
+// (round 4: the pair loops batched, SETUP_U pairs a thread in flight; three
+// passes of dependent loads were ~50 us at scene M).
+static constexpr int SETUP_U = 4;
+
+#ifdef LPE_PTRACE
+__device__ unsigned long long g_ctrace[SGROUPS + 1][8];   // [SGROUPS]: k_stripe_setup's stages
+extern "C" int lpe_ctrace(unsigned long long *host) {
+    if (host) (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ctrace), sizeof(unsigned long long) * (SGROUPS + 1) * 8);
+    return 0;
+}
+#define CTR(k, v) do { if (threadIdx.x == 0) g_ctrace[blockIdx.x][k] = (v); } while (0)
+#define STP(k) do { if (threadIdx.x == 0) g_ctrace[SGROUPS][k] = wall_clock64(); } while (0)
+#else
+#define CTR(k, v) do { } while (0)
+#define STP(k) do { } while (0)
+#endif
+
 __global__ void __launch_bounds__(SOLVE_TPB)
 k_stripe_setup(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict__ pairs,
                const lpe_body *__restrict__ bodies, StripeBufs sb, int32_t *__restrict__ counts, int smax) {
     extern __shared__ unsigned int bmark[];                 // [2][words]: movable / static contact-pair bodies
     __shared__ double wr[3][SOLVE_TPB / 64];
+    __shared__ int wn[SOLVE_TPB / 64];
     __shared__ double sx0, sw;
-    __shared__ int sS, sViol, nstat, statcur, sPairs;
+    __shared__ int sS, sViol, nstat, statcur;
     __shared__ int scnt[STRIPES_MAX], scur[STRIPES_MAX], gcount[SGROUPS];
+    STP(0);
     const int np = *npptr;
     const int words = (nb + 31) >> 5;
     for (int i = threadIdx.x; i < 2 * words; i += SOLVE_TPB) bmark[i] = 0u;
     for (int i = threadIdx.x; i < STRIPES_MAX; i += SOLVE_TPB) scnt[i] = 0;
     for (int i = threadIdx.x; i < SGROUPS; i += SOLVE_TPB) gcount[i] = 0;
-    if (threadIdx.x == 0) { sViol = 0; nstat = 0; sPairs = 0; }
+    if (threadIdx.x == 0) { sViol = 0; nstat = 0; }
     double mn = 1.7976931348623157e308, mx = -1.7976931348623157e308, sp = 0.0;
+    int npairs = 0;                                        // pairs with contacts
     const int nblk = (np + RTPB - 1) / RTPB;
     for (int k = threadIdx.x; k < nblk; k += SOLVE_TPB) {
-        mn = fmin(mn, sb.bred[3 * k]); mx = fmax(mx, sb.bred[3 * k + 1]); sp = fmax(sp, sb.bred[3 * k + 2]);
+        mn = fmin(mn, sb.bred[4 * k]); mx = fmax(mx, sb.bred[4 * k + 1]); sp = fmax(sp, sb.bred[4 * k + 2]);
+        npairs += (int)sb.bred[4 * k + 3];
     }
     for (int off = 32; off > 0; off >>= 1) {
         mn = fmin(mn, __shfl_xor(mn, off));
         mx = fmax(mx, __shfl_xor(mx, off));
         sp = fmax(sp, __shfl_xor(sp, off));
+        npairs += __shfl_xor(npairs, off);
     }
-    if ((threadIdx.x & 63) == 0) { wr[0][threadIdx.x >> 6] = mn; wr[1][threadIdx.x >> 6] = mx; wr[2][threadIdx.x >> 6] = sp; }
+    if ((threadIdx.x & 63) == 0) {
+        wr[0][threadIdx.x >> 6] = mn; wr[1][threadIdx.x >> 6] = mx; wr[2][threadIdx.x >> 6] = sp;
+        wn[threadIdx.x >> 6] = npairs;
+    }
     __syncthreads();
-    int mine = 0;                                          // pairs with contacts
-    for (int p = threadIdx.x; p < np; p += SOLVE_TPB) {
-        const int f = sb.pflag[p];
-        if (!(f & 1)) continue;
-        mine++;
-        const int2 pr = pairs[p];
-        atomicOr(&bmark[((f & 2) ? 0 : words) + (pr.x >> 5)], 1u << (pr.x & 31));
-        atomicOr(&bmark[((f & 4) ? 0 : words) + (pr.y >> 5)], 1u << (pr.y & 31));
-    }
-    if (mine) atomicAdd(&sPairs, mine);
     if (threadIdx.x == 0) {
         for (int k = 1; k < SOLVE_TPB / 64; k++) {
-            mn = fmin(mn, wr[0][k]); mx = fmax(mx, wr[1][k]); sp = fmax(sp, wr[2][k]);
+            mn = fmin(mn, wr[0][k]); mx = fmax(mx, wr[1][k]); sp = fmax(sp, wr[2][k]); npairs += wn[k];
         }
         int S = 1;
-        if (mx > mn && sPairs > STRIPE_MIN_PAIRS) {
+        if (mx > mn && npairs > STRIPE_MIN_PAIRS) {
             const double q = (mx - mn) / sp;          // (span 0: +inf)
             // (smax: the two solvers' S / 2 workgroups each must be co-resident,
             // one per CU -- stripe_cap)
@@ -2263,16 +2287,49 @@ k_stripe_setup(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict
         sw = (mx - mn) / S;
     }
     __syncthreads();
+    STP(1);
     int S = sS;
     const double x0 = sx0, w = sw;
-    // a pair more than one stripe apart (a rounding edge): one stripe
-    for (int p = threadIdx.x; p < np && S > 1; p += SOLVE_TPB) {
-        if ((sb.pflag[p] & 6) != 6) continue;
-        const double2 x = sb.px[p];
-        if (abs(stripe_of(x.x, x0, w, S) - stripe_of(x.y, x0, w, S)) > 1) sViol = 1;
+    // one pass over the pairs: the bodies' marks, the one-stripe rule (a pair
+    // more than one stripe apart, a rounding edge), the groups for S
+    for (int p0 = 0; p0 < np; p0 += SETUP_U * SOLVE_TPB) {
+        int f[SETUP_U];
+        int2 pr[SETUP_U];
+        double2 x[SETUP_U];
+#pragma unroll
+        for (int u = 0; u < SETUP_U; u++) {
+            const int p = p0 + u * SOLVE_TPB + (int)threadIdx.x;
+            f[u] = 0;
+            if (p < np) { f[u] = sb.pflag[p]; pr[u] = pairs[p]; x[u] = sb.px[p]; }
+        }
+#pragma unroll
+        for (int u = 0; u < SETUP_U; u++) {
+            const int p = p0 + u * SOLVE_TPB + (int)threadIdx.x;
+            if (p >= np) continue;
+            int g = -1;
+            if (f[u] & 1) {
+                atomicOr(&bmark[((f[u] & 2) ? 0 : words) + (pr[u].x >> 5)], 1u << (pr[u].x & 31));
+                atomicOr(&bmark[((f[u] & 4) ? 0 : words) + (pr[u].y >> 5)], 1u << (pr[u].y & 31));
+                int sa = (f[u] & 2) ? stripe_of(x[u].x, x0, w, S) : -1;
+                int sb2 = (f[u] & 4) ? stripe_of(x[u].y, x0, w, S) : -1;
+                if (sa >= 0 && sb2 >= 0 && abs(sa - sb2) > 1) sViol = 1;
+                if (sa < 0) sa = sb2;
+                if (sb2 < 0) sb2 = sa;
+                if (sa < 0) sa = sb2 = 0;
+                g = (sa >> 1) == (sb2 >> 1) ? 2 * (sa >> 1) : 2 * (min(sa, sb2) >> 1) + 1;
+                atomicAdd(&gcount[g], 1);
+            }
+            sb.pgroup[p] = g;
+        }
     }
     __syncthreads();
-    if (sViol) S = 1;
+    STP(2);
+    if (sViol) {                                       // (block-uniform) one stripe after all
+        S = 1;
+        for (int p = threadIdx.x; p < np; p += SOLVE_TPB) sb.pgroup[p] = (sb.pflag[p] & 1) ? 0 : -1;
+        for (int i = threadIdx.x; i < SGROUPS; i += SOLVE_TPB) gcount[i] = i == 0 ? npairs : 0;
+        __syncthreads();
+    }
     for (int b = threadIdx.x; b < nb; b += SOLVE_TPB) {
         int s = -1;
         if ((bmark[b >> 5] >> (b & 31)) & 1u) {
@@ -2283,22 +2340,8 @@ k_stripe_setup(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict
         }
         sb.bstripe[b] = s;
     }
-    for (int p = threadIdx.x; p < np; p += SOLVE_TPB) {
-        const int f = sb.pflag[p];
-        int g = -1;
-        if (f & 1) {
-            const double2 x = sb.px[p];
-            int sa = (f & 2) ? stripe_of(x.x, x0, w, S) : -1;
-            int sb2 = (f & 4) ? stripe_of(x.y, x0, w, S) : -1;
-            if (sa < 0) sa = sb2;
-            if (sb2 < 0) sb2 = sa;
-            if (sa < 0) sa = sb2 = 0;
-            g = (sa >> 1) == (sb2 >> 1) ? 2 * (sa >> 1) : 2 * (min(sa, sb2) >> 1) + 1;
-            atomicAdd(&gcount[g], 1);
-        }
-        sb.pgroup[p] = g;
-    }
     __syncthreads();
+    STP(3);
     if (threadIdx.x == 0) {
         int acc = 0;
         for (int s = 0; s < STRIPES_MAX; s++) { sb.sbStart[s] = acc; scur[s] = acc; acc += scnt[s]; }
@@ -2312,6 +2355,7 @@ k_stripe_setup(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict
         counts[13] = (S + 1) / 2;
     }
     __syncthreads();
+    STP(4);
     for (int b = threadIdx.x; b < nb; b += SOLVE_TPB) {
         const int s = sb.bstripe[b];
         int i = -1;
@@ -2320,6 +2364,7 @@ k_stripe_setup(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict
         if (i >= 0) sb.sbList[i] = b;
         sb.bpos[b] = i;
     }
+    STP(5);
 }
 
 // one wave per group: greedy colouring of its pairs in ascending order (the
@@ -2339,16 +2384,6 @@ k_stripe_setup(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict
 // priority -- the same colours as the sequential pass -- and dropped it: in
 // entity order a pair's lower neighbours form chains as long as the scene,
 // so the rounds were 2-3x slower than the chain.)
-#ifdef LPE_PTRACE
-__device__ unsigned long long g_ctrace[SGROUPS][8];
-extern "C" int lpe_ctrace(unsigned long long *host) {
-    if (host) (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ctrace), sizeof(unsigned long long) * SGROUPS * 8);
-    return 0;
-}
-#define CTR(k, v) do { if (threadIdx.x == 0) g_ctrace[blockIdx.x][k] = (v); } while (0)
-#else
-#define CTR(k, v) do { } while (0)
-#endif
 
 __global__ void __launch_bounds__(RTPB)
 k_group_colour(const int32_t *__restrict__ npptr, const int32_t *__restrict__ counts, const int2 *__restrict__ pairs,
@@ -2360,43 +2395,62 @@ k_group_colour(const int32_t *__restrict__ npptr, const int32_t *__restrict__ co
     CTR(0, wall_clock64());
     const int s = (g >> 1) * 2 + (g & 1);               // band j: stripes 2j, 2j+1; seam j: 2j+1, 2j+2
     const int u0 = sb.sbStart[s], u1 = sb.sbStart[min(s + 2, S)];
+    const int g0 = sb.gstart[g], g1 = sb.gstart[g + 1];
     {
-        // the list, and each listed pair's body slots and contact count
-        // (the colouring chain below then reads three plain arrays)
+        // the list: wave w files the group's pairs of its quarter of the
+        // pairs in ascending order (ballots; the group tests batched LIST_U
+        // loads deep, counted in a first pass, filed in a second), then each
+        // listed pair's body slots and contact count, one pair a thread (the
+        // colouring chain below reads three plain arrays)
+        constexpr int LIST_U = 8;
+        __shared__ int wcount[RTPB / 64];
         const int np = *npptr;
-        int base = sb.gstart[g];
-        for (int p0 = 0; p0 < np; p0 += 4 * RTPB) {
-            int f[4], c = 0;
+        const int wv = (int)threadIdx.x >> 6, ln = (int)threadIdx.x & 63;
+        const int seg = ((np + RTPB - 1) / RTPB) * 64;    // (a multiple of 64 a wave)
+        const int s0 = min(np, wv * seg), s1 = min(np, s0 + seg);
+        auto pass = [&](bool file, int off) {
+            int cnt = 0;
+            for (int b0 = s0; b0 < s1; b0 += 64 * LIST_U) {
+                int gv[LIST_U];
 #pragma unroll
-            for (int k = 0; k < 4; k++) {
-                const int p = p0 + 4 * (int)threadIdx.x + k;
-                f[k] = (p < np && sb.pgroup[p] == g) ? 1 : 0;
-                c += f[k];
-            }
-            int tot;
-            int off = r_block_excl(c, &tot) + base;
-#pragma unroll
-            for (int k = 0; k < 4; k++)
-                if (f[k]) {
-                    const int p = p0 + 4 * (int)threadIdx.x + k;
-                    const int2 pr = pairs[p];
-                    const int fl = sb.pflag[p];
-                    sb.glist[off] = p;
-                    sb.gla[off] = (fl & 2) ? sb.bpos[pr.x] - u0 : -1;
-                    sb.glb[off] = (fl & 4) ? sb.bpos[pr.y] - u0 : -1;
-                    sb.gln[off] = ccount[p];
-                    off++;
+                for (int u = 0; u < LIST_U; u++) {
+                    const int p = b0 + 64 * u + ln;
+                    gv[u] = p < s1 ? sb.pgroup[p] : -1;
                 }
-            base += tot;
+#pragma unroll
+                for (int u = 0; u < LIST_U; u++) {
+                    const bool hit = gv[u] == g;
+                    const unsigned long long m = __ballot(hit);
+                    if (file && hit) sb.glist[off + cnt + __popcll(m & ((1ull << ln) - 1ull))] = b0 + 64 * u + ln;
+                    cnt += __popcll(m);
+                }
+            }
+            return cnt;
+        };
+        const int mine = pass(false, 0);
+        if (ln == 0) wcount[wv] = mine;
+        __syncthreads();
+        int off = g0;
+        for (int k = 0; k < wv; k++) off += wcount[k];
+        pass(true, off);
+        __syncthreads();                               // (the list, in global memory)
+        for (int t = g0 + (int)threadIdx.x; t < g1; t += RTPB) {
+            const int p = sb.glist[t];
+            const int2 pr = pairs[p];
+            const int fl = sb.pflag[p];
+            const int n = ccount[p];
+            const int ba = sb.bpos[pr.x], bb = sb.bpos[pr.y];
+            sb.gla[t] = (fl & 2) ? ba - u0 : -1;
+            sb.glb[t] = (fl & 4) ? bb - u0 : -1;
+            sb.gln[t] = n;
         }
     }
     CTR(1, wall_clock64());
     for (int i = (int)threadIdx.x; i < u1 - u0; i += RTPB) used[i] = 0ull;
-    __syncthreads();                                   // (the list, in global memory, and the masks)
+    __syncthreads();                                   // (the list's slots and counts, and the masks)
     CTR(2, wall_clock64());
     if (threadIdx.x >= 64) return;
     const int lane = (int)threadIdx.x;
-    const int g0 = sb.gstart[g], g1 = sb.gstart[g + 1];
     int ncol = 0, fault = 0;
     int cp = 0, cr = 0;                                   // lane c: colour c's pairs and rows so far
     // Chunks of 32 pairs; lane l is the pair (l & 31)'s body on side l >> 5
@@ -3695,7 +3749,7 @@ static StripeBufs *stripe_bufs(lpe_ctx *ctx, RigidDev *d) {
     if (d->cap_pairs > d->cap_stripe_pairs || !sb->pgroup) {
         const size_t P = (size_t)std::max(d->cap_pairs, 1);
         if (grow(&sb->pgroup, P) || grow(&sb->pcolg, P) || grow(&sb->prank, P) || grow(&sb->prowoff, P) ||
-            grow(&sb->glist, P) || grow(&sb->pflag, P) || grow(&sb->px, P) || grow(&sb->bred, 3 * (P / RTPB + 1)) ||
+            grow(&sb->glist, P) || grow(&sb->pflag, P) || grow(&sb->px, P) || grow(&sb->bred, 4 * (P / RTPB + 1)) ||
             grow(&sb->gla, P) || grow(&sb->glb, P) || grow(&sb->gln, P))
             return nullptr;
         d->cap_stripe_pairs = d->cap_pairs;

@@ -1,5 +1,6 @@
 """Per-group stage times of k_group_colour (round 4): the list compaction
-over all candidate pairs, the barrier, and wave 0's colouring chain.
+over all candidate pairs, the barrier, and wave 0's colouring chain; and the
+stages of k_stripe_setup before it.
 
     profiles/trace_build.sh rigid pt -DLPE_PTRACE
     LPE_LIB=profiles/_var/liblpe_pt.so python3 profiles/colour_trace.py
@@ -28,9 +29,13 @@ DT = 1.0 / 120.0
 
 
 def report(name):
-    buf = np.zeros(128 * 8, np.uint64)
+    buf = np.zeros(129 * 8, np.uint64)
     L.lpe_ctrace(buf.ctypes.data)
-    t = buf.reshape(128, 8).astype(np.int64)
+    t = buf.reshape(129, 8).astype(np.int64)
+    st = t[128]
+    print(f"{name}: k_stripe_setup stages (us): stripe count {(st[1] - st[0]) / 100:.2f}, pair pass "
+          f"{(st[2] - st[1]) / 100:.2f}, bodies {(st[3] - st[2]) / 100:.2f}, prefixes {(st[4] - st[3]) / 100:.2f}, "
+          f"body slots {(st[5] - st[4]) / 100:.2f}; total {(st[5] - st[0]) / 100:.2f}")
     last = t[:, 0].max()
     rows = [g for g in range(128) if t[g, 0] > 0 and last - t[g, 0] < 100000 and t[g, 3] >= t[g, 0]]
     t0 = min(t[g, 0] for g in rows)
