@@ -30,6 +30,7 @@
 #include "lpe_internal.h"
 #include "rigid_dev.h"
 #include "lpe_trig.h"
+#include "lpe_trace.h"
 #include <algorithm>
 #include <cmath>
 #include <cstring>
@@ -1155,16 +1156,6 @@ __device__ __forceinline__ void lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-#ifdef LPE_PTRACE
-__device__ unsigned long long g_ptrace[2][2048];
-extern "C" int lpe_ptrace(unsigned long long *host) {
-    if (host) (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ptrace), sizeof(unsigned long long) * 2 * 2048);
-    return 0;
-}
-#define PTR(w, k) do { if (threadIdx.x == 0 && (k) < 2048) g_ptrace[w][k] = wall_clock64(); } while (0)
-#else
-#define PTR(w, k) do {} while (0)
-#endif
 #ifndef PGS_PF
 #define PGS_PF 2    // rows of a pair prefetched with it
 #endif
@@ -1254,9 +1245,7 @@ k_pgs_colour(int nb, const int32_t *__restrict__ counts, const int32_t *__restri
     auto nslot = [&](int c) { return nslot0(c) + pad; };
     const int total = iters * (S + pad);
     PTR(0, 0);
-#ifdef LPE_PTRACE
-    if (threadIdx.x <= ncol) g_ptrace[1][1024 + threadIdx.x] = scb[threadIdx.x];
-#endif
+    if (threadIdx.x <= ncol) PTR_SET(1, 1024 + threadIdx.x, scb[threadIdx.x]);
     // slot positions (colour, slot of the colour, iteration) of slots s, s+1, s+2
     struct SP { int c, k, it; };
     auto adv = [&](SP p) {
@@ -2224,19 +2213,6 @@ k_stripe_pairs(const int32_t *__restrict__ npptr, const int2 *__restrict__ pairs
 // passes of dependent loads were ~50 us at scene M).
 static constexpr int SETUP_U = 4;
 
-#ifdef LPE_PTRACE
-__device__ unsigned long long g_ctrace[SGROUPS + 1][8];   // [SGROUPS]: k_stripe_setup's stages
-extern "C" int lpe_ctrace(unsigned long long *host) {
-    if (host) (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ctrace), sizeof(unsigned long long) * (SGROUPS + 1) * 8);
-    return 0;
-}
-#define CTR(k, v) do { if (threadIdx.x == 0) g_ctrace[blockIdx.x][k] = (v); } while (0)
-#define STP(k) do { if (threadIdx.x == 0) g_ctrace[SGROUPS][k] = wall_clock64(); } while (0)
-#else
-#define CTR(k, v) do { } while (0)
-#define STP(k) do { } while (0)
-#endif
-
 __global__ void __launch_bounds__(SOLVE_TPB)
 k_stripe_setup(int nb, const int32_t *__restrict__ npptr, const int2 *__restrict__ pairs,
                const lpe_body *__restrict__ bodies, StripeBufs sb, int32_t *__restrict__ counts, int smax) {
@@ -2672,17 +2648,6 @@ __device__ __forceinline__ void stripe_steps_lds(const StripeBufs &sb, const Str
     }
 }
 
-#ifdef LPE_PTRACE
-__device__ unsigned long long g_strace[2][32][64];
-extern "C" int lpe_strace(unsigned long long *host) {
-    if (host) (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_strace), sizeof(unsigned long long) * 2 * 32 * 64);
-    return 0;
-}
-#define STR(w, j, k) do { if (threadIdx.x == 0 && (k) < 64 && (j) < 32) g_strace[w][j][k] = wall_clock64(); } while (0)
-#else
-#define STR(w, j, k) do { } while (0)
-#endif
-
 // Does every colour step of this workgroup hold at most one wave of pairs?
 // Then wave 0 runs the steps alone (stripe_sweeps, `single`): a step's
 // pairs touch disjoint bodies, and one wave's LDS stores are visible to its
@@ -2799,11 +2764,9 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
     STR(0, j, 0);
     const StripeView v = stripe_view(sb, counts, j);
     const int NR = v.nrows(), NP = v.npairs(), NL = v.nloc(), NS = v.nsteps();
-#ifdef LPE_PTRACE
-    if (threadIdx.x == 0 && j < 32) {   // (trace slots 61-63: phase A / B steps, pairs)
-        g_strace[0][j][61] = v.a1 - v.a0; g_strace[0][j][62] = v.b1 - v.b0; g_strace[0][j][63] = NP;
+    if (threadIdx.x == 0) {   // (trace slots 61-63: phase A / B steps, pairs)
+        STR_SET(0, j, 61, v.a1 - v.a0); STR_SET(0, j, 62, v.b1 - v.b0); STR_SET(0, j, 63, NP);
     }
-#endif
     // layout: rn, rr [NR] float4 | pr [NP] int4 | pm [NP] float4 | ln, lf [NR] | lv [3 NL] | stepL [NS + 1]
     const int oRR = 16 * NR, oPR = oRR + 16 * NR, oPM = oPR + 16 * NP, oLN = oPM + 16 * NP, oLF = oLN + 4 * NR,
               oLV = oLF + 4 * NR, oST = oLV + 12 * NL, total = oST + 4 * (NS + 1);

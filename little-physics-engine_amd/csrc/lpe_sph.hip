@@ -44,6 +44,7 @@
 // to the oracle's bit for bit.
 #include "lpe_internal.h"
 #include "sph_coupling.h"
+#include "lpe_trace.h"
 #include "lpe_transport.h"
 #include <cmath>
 #include <cstring>
@@ -1696,15 +1697,6 @@ __device__ __forceinline__ void merge_prestats_dev(int32_t *__restrict__ st, int
 __global__ void k_merge_prestats(int32_t *__restrict__ st, int32_t *__restrict__ pre) {
     if (blockIdx.x == 0 && threadIdx.x == 0) merge_prestats_dev(st, pre);
 }
-#ifdef LPE_FTRACE
-__device__ unsigned long long g_ftrace[4096 * 8];
-__device__ int g_ftrace_on;
-#define FTR(k) do { if (g_ftrace_on && threadIdx.x == 0) g_ftrace[lb * 8 + (k)] = wall_clock64(); } while (0)
-#define FTRMAX(k, v) do { if (g_ftrace_on && (threadIdx.x & 63) == 0) atomicMax(&g_ftrace[lb * 8 + (k)], (unsigned long long)(v)); } while (0)
-#else
-#define FTR(k) do {} while (0)
-#define FTRMAX(k, v) do {} while (0)
-#endif
 
 // One neighbour j != i of computeForces (metal:352-399): false when the
 // reference skips it, else its force terms (the caller adds them in list
@@ -2083,14 +2075,6 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     }
     FTR(3);
 }
-#ifdef LPE_FTRACE
-extern "C" int lpe_ftrace(int on, unsigned long long *host, int n) {
-    if (host) (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ftrace), sizeof(unsigned long long) * n);
-    unsigned long long z[4096 * 8] = {};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_ftrace), z, sizeof(z));
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_ftrace_on), &on, sizeof(int)) == hipSuccess ? 0 : 1;
-}
-#endif
 
 // ---------------------------------------------------------------------------
 // x-slab decomposition.  Rank r owns the particles whose

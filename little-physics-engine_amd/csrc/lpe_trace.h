@@ -1,0 +1,66 @@
+// Profiling-only stamp machinery, kept out of the kernels' sources.
+//
+// profiles/trace_build.sh compiles ONE source with -DLPE_FTRACE (lpe_sph.hip)
+// or -DLPE_PTRACE (lpe_rigid.hip) into a variant library under profiles/_var,
+// read back by the profiles/*_trace.py scripts through the extern "C"
+// accessors below.  Without those macros (the shipped build) every stamp is an
+// empty statement and nothing here is compiled.
+//
+//   FTR(k), FTRMAX(k, v)   k_forces_couple phases, per logical block `lb`
+//   PTR(w, k), PTR_SET     k_pgs_colour / k_pos_colour colour steps
+//   STR(w, j, k), STR_SET  k_pgs_stripes / k_pos_stripes phases per workgroup j
+//   CTR(k, v), STP(k)      k_group_colour stages per group, k_stripe_setup stages
+#pragma once
+#include <hip/hip_runtime.h>
+
+#ifdef LPE_FTRACE
+__device__ unsigned long long g_ftrace[4096 * 8];
+__device__ int g_ftrace_on;
+#define FTR(k) do { if (g_ftrace_on && threadIdx.x == 0) g_ftrace[lb * 8 + (k)] = wall_clock64(); } while (0)
+#define FTRMAX(k, v) do { if (g_ftrace_on && (threadIdx.x & 63) == 0) atomicMax(&g_ftrace[lb * 8 + (k)], (unsigned long long)(v)); } while (0)
+extern "C" int lpe_ftrace(int on, unsigned long long *host, int n) {
+    if (host) (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ftrace), sizeof(unsigned long long) * n);
+    unsigned long long z[4096 * 8] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_ftrace), z, sizeof(z));
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_ftrace_on), &on, sizeof(int)) == hipSuccess ? 0 : 1;
+}
+#else
+#define FTR(k) do {} while (0)
+#define FTRMAX(k, v) do {} while (0)
+#endif
+
+#ifdef LPE_PTRACE
+__device__ unsigned long long g_ptrace[2][2048];
+extern "C" int lpe_ptrace(unsigned long long *host) {
+    if (host) (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ptrace), sizeof(unsigned long long) * 2 * 2048);
+    return 0;
+}
+#define PTR(w, k) do { if (threadIdx.x == 0 && (k) < 2048) g_ptrace[w][k] = wall_clock64(); } while (0)
+#define PTR_SET(w, k, v) do { g_ptrace[w][k] = (v); } while (0)
+
+__device__ unsigned long long g_strace[2][32][64];
+extern "C" int lpe_strace(unsigned long long *host) {
+    if (host) (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_strace), sizeof(unsigned long long) * 2 * 32 * 64);
+    return 0;
+}
+#define STR(w, j, k) do { if (threadIdx.x == 0 && (k) < 64 && (j) < 32) g_strace[w][j][k] = wall_clock64(); } while (0)
+#define STR_SET(w, j, k, v) do { if ((j) < 32) g_strace[w][j][k] = (v); } while (0)
+
+// rows 0 .. LPE_CTRACE_GROUPS - 1: k_group_colour's groups; row LPE_CTRACE_GROUPS: k_stripe_setup
+#define LPE_CTRACE_GROUPS 128
+__device__ unsigned long long g_ctrace[LPE_CTRACE_GROUPS + 1][8];
+extern "C" int lpe_ctrace(unsigned long long *host) {
+    if (host)
+        (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ctrace), sizeof(unsigned long long) * (LPE_CTRACE_GROUPS + 1) * 8);
+    return 0;
+}
+#define CTR(k, v) do { if (threadIdx.x == 0) g_ctrace[blockIdx.x][k] = (v); } while (0)
+#define STP(k) do { if (threadIdx.x == 0) g_ctrace[LPE_CTRACE_GROUPS][k] = wall_clock64(); } while (0)
+#else
+#define PTR(w, k) do {} while (0)
+#define PTR_SET(w, k, v) do {} while (0)
+#define STR(w, j, k) do {} while (0)
+#define STR_SET(w, j, k, v) do {} while (0)
+#define CTR(k, v) do {} while (0)
+#define STP(k) do {} while (0)
+#endif
