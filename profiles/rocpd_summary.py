@@ -2,7 +2,12 @@
 counts and average / total durations, and a timeline window of kernel
 dispatches (start offsets, durations, queue) to see the gaps between them.
 
-    python3 profiles/rocpd_summary.py DB [--timeline N] [--skip S] [--kernel SUBSTR]"""
+    python3 profiles/rocpd_summary.py DB [--timeline N] [--skip S] [--kernel SUBSTR]
+                                         [--window-kernel NAME --window N]
+
+--window-kernel / --window: only the dispatches between the start of NAME's
+N-th last dispatch and the end of its last one (e.g. the bench's per-kernel
+timing window: its last `steps` ticks, 10 k_forces_couple launches a tick)."""
 import argparse
 import sqlite3
 
@@ -12,6 +17,8 @@ ap.add_argument("--timeline", type=int, default=0, help="print N consecutive dis
 ap.add_argument("--skip", type=int, default=0, help="... starting at dispatch S (time order)")
 ap.add_argument("--kernel", default=None, help="only kernels whose name contains this")
 ap.add_argument("--api", type=int, default=0, help="also the N host API calls (HIP / RCCL regions) of most total time")
+ap.add_argument("--window-kernel", default=None, help="restrict to a window of this kernel's last dispatches")
+ap.add_argument("--window", type=int, default=0, help="... its last N dispatches")
 a = ap.parse_args()
 c = sqlite3.connect(a.db)
 cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
@@ -20,6 +27,12 @@ if "queue_id" in cols:
     rows = c.execute(f"select {name_col}, start, end, queue_id from kernels order by start").fetchall()
 else:
     rows = [(n, s, e, 0) for n, s, e in c.execute(f"select {name_col}, start, end from kernels order by start")]
+if a.window_kernel and a.window > 0:
+    mine = [r for r in rows if a.window_kernel in r[0]]
+    if len(mine) >= a.window:
+        w0, w1 = mine[-a.window][1], mine[-1][2]
+        rows = [r for r in rows if r[1] >= w0 and r[2] <= w1]
+        print(f"window: the last {a.window} dispatches of {a.window_kernel}, {(w1 - w0) / 1e3:.1f} us")
 if a.kernel:
     rows = [r for r in rows if a.kernel in r[0]]
 agg = {}
