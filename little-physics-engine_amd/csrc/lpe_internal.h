@@ -230,7 +230,7 @@ static inline int lpe_grow(lpe_ctx *ctx, T **p, int *cap, long want, long elems_
 
 int lpe_rigid_destroy_internal(lpe_ctx *ctx);
 // world tick: rigid collision detection overlapped with the fluid step (lpe_rigid.hip)
-int rigid_tick_begin(lpe_ctx *ctx);
+int rigid_tick_begin(lpe_ctx *ctx, bool on_main = false);   // on_main: detect on the context stream
 int rigid_tick_boundary(lpe_ctx *ctx, bool gravity = false, double dt_state = 0.0);   // + BasicGravity fused
 int rigid_tick_detect(lpe_ctx *ctx);   // host half of the detection + colouring launch
 int rigid_tick_hook(lpe_ctx *ctx, int step);   // fluid-step hook (after each sub-step's forces)

@@ -648,9 +648,13 @@ k_narrow(const int32_t *__restrict__ npptr, int cap, const int2 *__restrict__ pa
 // the solvers -- sees an empty tick and stays inside its buffers; only a
 // lagged detection gets here with an overflow (the synchronous one grows and
 // redoes first), and its check reports it from counts[15] / [14] / [6].
+// host (lagged detection): thread 0 also stores the 16 counts straight into
+// the pinned host slot the lagged check reads (no copy launch after it);
+// every other count is final by then (earlier kernels in stream order)
 __global__ void k_compact(int32_t *__restrict__ npptr, int cap_pairs, const lpe_contact *__restrict__ slots,
                           const int32_t *__restrict__ ccount, const int32_t *__restrict__ cstart,
-                          lpe_contact *__restrict__ out, int cap, int32_t *__restrict__ counts) {
+                          lpe_contact *__restrict__ out, int cap, int32_t *__restrict__ counts,
+                          int32_t *__restrict__ host) {
     int k = blockIdx.x * RTPB + threadIdx.x;
     const int raw = *npptr;
     const int np = min(raw, cap_pairs);
@@ -661,6 +665,11 @@ __global__ void k_compact(int32_t *__restrict__ npptr, int cap_pairs, const lpe_
         counts[14] = tot;
         counts[15] = raw;
         if (over) *npptr = 0;          // (blocks that read it first compact within the capacities)
+        if (host) {
+            // (npptr is counts + 0: its value as just left)
+            for (int i = 0; i < 16; i++) host[i] = i == 0 ? (over ? 0 : raw) : counts[i];
+            __threadfence_system();
+        }
     }
     if (k >= np) return;
     int s = cstart[k];
@@ -3617,9 +3626,11 @@ static int detect_launch(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pa
     LPE_KERNEL(ctx, "k_narrow", k_narrow, dim3(rblk(d->cap_pairs, 128)), dim3(128), 0, s, d->counts, d->cap_pairs, d->pairs, d->bodies, d->verts, d->cslots, d->ccount, d->counts);
     int st = rscan(ctx, d, d->counts, d->cap_pairs, d->ccount, d->cstart, nullptr, s);
     if (st) return st;
-    if (lagged)     // the compaction right away (capacity-bounded; the counts are checked later)
+    if (lagged) {   // the compaction right away (capacity-bounded; the counts are checked later)
         LPE_KERNEL(ctx, "k_compact", k_compact, dim3(rblk(d->cap_pairs)), dim3(RTPB), 0, s, d->counts, d->cap_pairs,
-                   d->cslots, d->ccount, d->cstart, d->contacts, d->cap_contacts, d->counts);
+                   d->cslots, d->ccount, d->cstart, d->contacts, d->cap_contacts, d->counts, hc);
+        return LPE_OK;
+    }
     LPE_HIP(ctx, hipMemcpyAsync(hc, d->counts, sizeof(int32_t) * 16, hipMemcpyDeviceToHost, s));
     return LPE_OK;
 }
@@ -3660,7 +3671,7 @@ static int detect_finish(lpe_ctx *ctx, RigidDev *d, hipStream_t s, const int32_t
         if (st) return st;
     }
     LPE_KERNEL(ctx, "k_compact", k_compact, dim3(rblk(d->cap_pairs)), dim3(RTPB), 0, s, d->counts, d->cap_pairs,
-               d->cslots, d->ccount, d->cstart, d->contacts, d->cap_contacts, d->counts);
+               d->cslots, d->ccount, d->cstart, d->contacts, d->cap_contacts, d->counts, nullptr);
     LPE_CHECK_LAUNCH(ctx, "detect");
     d->last_np = np;
     d->last_nc = ncv;
@@ -4071,7 +4082,7 @@ static void rigid_lag_off(lpe_ctx *ctx, RigidDev *d) {
     d->grow_pairs = d->grow_contacts = 0;
 }
 
-int rigid_tick_begin(lpe_ctx *ctx) {
+int rigid_tick_begin(lpe_ctx *ctx, bool on_main) {
     RigidDev *d = rdev(ctx);
     d->overlap_pending = false;
     d->colour_pending = false;
@@ -4113,7 +4124,8 @@ int rigid_tick_begin(lpe_ctx *ctx) {
     hipStream_t s = ctx->stream;
     LPE_KERNEL(ctx, "k_boundary_pos", k_boundary_pos, dim3(rblk(d->nb)), dim3(RTPB), 0, s, d->nb, d->bodies,
                c.marginPixels * c.metersPerPixel, c.universeSize, d->bbits);
-    LPE_HIP(ctx, hipEventRecord(d->evStart, s));
+    d->det = on_main ? s : d->side;
+    if (d->det != s) LPE_HIP(ctx, hipEventRecord(d->evStart, s));
     d->detect_launched = false;
     d->overlap_pending = true;
     return LPE_OK;
@@ -4125,23 +4137,23 @@ int rigid_tick_begin(lpe_ctx *ctx) {
 // stream without work for that long at every tick start.
 static int rigid_tick_launch(lpe_ctx *ctx, RigidDev *d) {
     if (d->detect_launched) return LPE_OK;
-    LPE_HIP(ctx, hipStreamWaitEvent(d->side, d->evStart, 0));
+    if (d->det != ctx->stream) LPE_HIP(ctx, hipStreamWaitEvent(d->det, d->evStart, 0));
     if (d->lag) {
         // lagged: the compaction follows at once and the counts go to a ring
         // slot, checked when the slot comes round again (two ticks later)
         const int slot = (int)(d->htick & 1u);
         int st = rigid_lag_check(ctx, d, slot, true);
         if (st) return st;
-        st = detect_launch(ctx, d, 0, nullptr, d->side, d->hcr + 16 * slot, true);
+        st = detect_launch(ctx, d, 0, nullptr, d->det, d->hcr + 16 * slot, true);
         if (st) return st;
-        LPE_HIP(ctx, hipEventRecord(d->evHc[slot], d->side));
+        LPE_HIP(ctx, hipEventRecord(d->evHc[slot], d->det));
         d->hpend[slot] = true;
         d->htick++;
     } else {
-        int st = detect_launch(ctx, d, 0, nullptr, d->side, d->hc);
+        int st = detect_launch(ctx, d, 0, nullptr, d->det, d->hc);
         if (st) return st;
+        LPE_HIP(ctx, hipEventRecord(d->evDetect, d->det));   // (the host waits on it: rigid_tick_detect)
     }
-    LPE_HIP(ctx, hipEventRecord(d->evDetect, d->side));
     d->detect_launched = true;
     return LPE_OK;
 }
@@ -4196,19 +4208,19 @@ int rigid_tick_detect(lpe_ctx *ctx) {
         // from the device (an empty tick colours nothing and solves nothing)
         st = solver_streams(ctx, d);
         if (!st) st = solver_lds_check(ctx, d);
-        if (!st) st = colour_launch(ctx, d, d->side);
-        if (!st) st = colour_prep(ctx, d, d->side);
+        if (!st) st = colour_launch(ctx, d, d->det);
+        if (!st) st = colour_prep(ctx, d, d->det);
         if (st) return st;
-        LPE_HIP(ctx, hipEventRecord(d->evColour, d->side));
+        if (d->det != ctx->stream) LPE_HIP(ctx, hipEventRecord(d->evColour, d->det));
         d->colour_pending = true;
         return LPE_OK;
     }
     LPE_HIP(ctx, hipEventSynchronize(d->evDetect));
     int retry = 0;
-    st = detect_finish(ctx, d, d->side, d->hc, &retry);
+    st = detect_finish(ctx, d, d->det, d->hc, &retry);
     if (st) return st;
     if (retry) {                     // the pair buffer grew: detect again (rare)
-        st = rigid_detect(ctx, d, 0, nullptr, d->side);
+        st = rigid_detect(ctx, d, 0, nullptr, d->det);
         if (st) return st;
     }
     // the next ticks check their counts after the fact once the buffers have
@@ -4227,11 +4239,12 @@ int rigid_tick_detect(lpe_ctx *ctx) {
         // the velocity-independent preparation runs here, beside the fluid
         // step: colouring, contact marks, PGS rows, position items
         st = solver_lds_check(ctx, d);
-        if (!st) st = colour_launch(ctx, d, d->side);
-        if (!st) st = colour_prep(ctx, d, d->side);
+        if (!st) st = colour_launch(ctx, d, d->det);
+        if (!st) st = colour_prep(ctx, d, d->det);
         if (st) return st;
     }
-    LPE_HIP(ctx, hipEventRecord(d->evColour, d->side));   // everything on the side stream
+    if (d->det != ctx->stream)
+        LPE_HIP(ctx, hipEventRecord(d->evColour, d->det));   // everything on the side stream
     d->colour_pending = true;
     return LPE_OK;
 }
@@ -4243,8 +4256,9 @@ int rigid_tick_finish(lpe_ctx *ctx) {
     if (st) return st;
     d->colour_pending = false;
     hipStream_t s = ctx->stream;
+    const bool joinColour = d->det != s;       // (detected on the context stream: in order already)
     if (!d->lag && d->last_nc == 0) {         // early out (rigid_body_collision.cpp:35-37)
-        LPE_HIP(ctx, hipStreamWaitEvent(s, d->evColour, 0));
+        if (joinColour) LPE_HIP(ctx, hipStreamWaitEvent(s, d->evColour, 0));
         if (d->pcol && d->last_np > 0)
             LPE_HIP(ctx, hipMemsetAsync(d->pcol, 0xff, sizeof(int32_t) * d->last_np, s));
         LPE_HIP(ctx, hipMemsetAsync(d->counts + 8, 0, sizeof(int32_t), s));
@@ -4256,7 +4270,7 @@ int rigid_tick_finish(lpe_ctx *ctx) {
     // queue with the next tick's prelaunch, which then delayed it).  (Run
     // during the fluid step instead, the one-workgroup position solver slows
     // the full-chip fluid kernels by more than it saves.)
-    LPE_HIP(ctx, hipStreamWaitEvent(s, d->evColour, 0));
+    if (joinColour) LPE_HIP(ctx, hipStreamWaitEvent(s, d->evColour, 0));
     LPE_HIP(ctx, hipEventRecord(d->evFork, s));
     LPE_HIP(ctx, hipStreamWaitEvent(d->side, d->evFork, 0));
     st = colour_pos(ctx, d, d->side);

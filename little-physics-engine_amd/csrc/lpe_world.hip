@@ -211,7 +211,7 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
             d.rig_coupled = true;
         }
         if (overlap) {          // after the gather: the fluid sees the unclamped poses
-            int st = rigid_tick_begin(ctx);
+            int st = rigid_tick_begin(ctx, !fluid);
             if (st) return st;
         }
         if (fluid) {

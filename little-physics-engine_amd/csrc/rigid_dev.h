@@ -86,6 +86,11 @@ struct RigidDev {
     int32_t *bbits = nullptr;                 // per body: boundary bounce bits of the tick
     int32_t *hc = nullptr;                    // pinned: detection counts read by the host
     hipStream_t side = nullptr;
+    // the stream the tick's detection and colouring run on: `side` beside a
+    // fluid step, the context stream in a world without fluid (nothing to
+    // overlap with: the side stream's joins would only add cross-queue
+    // packets to the serial path)
+    hipStream_t det = nullptr;
     hipEvent_t evStart = nullptr, evDetect = nullptr, evColour = nullptr;
     bool overlap_pending = false;             // detection queued on the side stream
     bool colour_pending = false;              // ... finished by the host, colouring queued
