@@ -13,7 +13,16 @@ M pool widened N times (N x 256k particles, the same 4096-pentagon pile in the
 middle, U = 32 N m), its fluid split into N equal-count x-slabs with the RCCL
 halo exchange of include/lpe.h, the rigid pass replicated on every rank (rigid
 accumulators all-reduced once per tick).  Each rank advances one M-sized SPH
-slab per tick, so `value` = N x ticks/s.  MW1 is M.  --replicas runs N
+slab per tick, so `value` = N x MW{N} ticks/s: the whole job's throughput in
+ticks/s of the 256k-particle metric scene (the contract's whole-job aggregate,
+comparable with the N = 1 line).  The same line carries `scaling_weak` (MW{N}
+ticks/s, particle-ticks/s, efficiency against scene M as one domain on one
+GPU, measured in this run) and `scaling_strong_c5`: north_star's fixed
+2M-particle scene C5 over the same N ranks, its single-GPU rate measured in
+this run, speedup and efficiency.  Slab ranks and both baselines run
+unbounded cells; the all-rank `reference_envelope` says whether the windows
+stayed inside the reference's 64-particle cells, where the two cell
+semantics are the same computation.  MW1 is M.  --replicas runs N
 independent copies of M instead.  The control plane (uid broadcast, barrier,
 max over ranks) uses gloo.
 
@@ -491,7 +500,12 @@ def config_lines(lpe, scenes, device, dt_tick, with_ref):
     reference's needs NEON) on this host's single core, and BASELINE.md's
     anchors measured in the build container."""
     out = {}
-    for name, prep in (("C2", 30), ("C4", 90)):
+    # C2 is the dam break (a transient by definition: timed right after the
+    # dam opens); C4 is timed settled, 3,000 ticks in like scene M (VERDICT r4
+    # item 4).  Both lead with the reference's own capped cells
+    # (LPE_SPH_MODE_REF_CELL_CAP, the mode tests/test_configs_gpu.py pins at
+    # these states); the unbounded rate is reported beside it.
+    for name, prep in (("C2", 30), ("C4", 3000)):
         s = scenes.scene(name)
         fl = s["fluid"]
         b, v = scenes.to_bodies(s["bodies"])
@@ -503,29 +517,24 @@ def config_lines(lpe, scenes, device, dt_tick, with_ref):
             ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
             ctx.world_set_coupling(None)
             ctx.world_tick(dt_tick, prep)
+            ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP)
+            ctx.world_tick(dt_tick, 10)
             ctx.sph_diag(False)                       # restart the window totals
             w = timed_windows(ctx, dt_tick, 500.0, nwin=3, min_s=1.0)
             st = ctx.sph_stats()
-            over = st["overCapCellsTotal"]
-            wcap = None
-            if over > 0:
-                # outside the reference's 64-slot cells: time the reference's own
-                # capped-cell semantics too (LPE_SPH_MODE_REF_CELL_CAP)
-                ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP)
-                wcap = timed_windows(ctx, dt_tick, 500.0, nwin=3, min_s=1.0)
-                ctx.sph_set_mode(0)
+            ctx.sph_set_mode(0)
+            wu = timed_windows(ctx, dt_tick, 500.0, nwin=3, min_s=1.0)
         finally:
             ctx.close()
-        out[name] = dict(desc=s["desc"], ticks_per_s=w["median"], windows=w, fluid_particles=len(fl["x"]),
-                         bodies=len(b), max_cell_occupancy=st["maxCellOccupancy"],
+        over = st["overCapCellsTotal"]
+        spread = (max(w["rates"]) - min(w["rates"])) / w["median"]
+        out[name] = dict(desc=s["desc"], ticks_per_s=w["median"], windows=w, window_spread=round(spread, 4),
+                         prep_ticks=prep, cells="the reference's 64-particle cells (LPE_SPH_MODE_REF_CELL_CAP)",
+                         fluid_particles=len(fl["x"]), bodies=len(b), max_cell_occupancy=st["maxCellOccupancy"],
                          cells_over_64=st["overCapCells"],
                          reference_envelope=dict(max_cell_occupancy_window=st["maxCellOccupancyTotal"],
-                                                 cells_over_64_window=over, inside=over == 0))
-        if wcap is not None:
-            out[name]["ref_cell_cap_mode"] = dict(ticks_per_s=wcap["median"], windows=wcap,
-                                                  note="the reference's 64-slot cell semantics (dropped inserts, "
-                                                       "cross-cell reads), bit-exact vs the oracle in "
-                                                       "tests/test_configs_gpu.py")
+                                                 cells_over_64_window=over, inside=over == 0),
+                         unbounded_cells_mode=dict(ticks_per_s=wu["median"], windows=wu))
     anchors = {"C1": (555.0, 600), "C3": (12.1, 240)}
     for name in ("C1", "C3"):
         s = scenes.rigid_scene(name)
@@ -600,6 +609,162 @@ def launch_ranks(n, cmd=None):
     return bad[0] if bad else 0
 
 
+def envelope_all_ranks(dist, st):
+    """The reference-envelope counters of the timed window over every rank
+    (ADVICE r4 / VERDICT r4 item 3): cells over the reference's 64 summed (a
+    ghost column's cells are counted by both ranks that hold it, so the sum
+    may count a cell twice; `inside` is exact), the largest occupancy the
+    maximum."""
+    over, occ = st["overCapCellsTotal"], st["maxCellOccupancyTotal"]
+    if dist is not None:
+        import torch
+        t = torch.tensor([over], dtype=torch.int64)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        m = torch.tensor([occ], dtype=torch.int64)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        over, occ = int(t.item()), int(m.item())
+    return dict(max_cell_occupancy_window=occ, cells_over_64_window=over, inside=over == 0)
+
+
+def slab_leg(lpe, scenes, slab, dist, rank, world, device, scene_name, prep, warmup, steps, transport,
+             rebalance, keep=False):
+    """One sharded run: scene `scene_name`'s fluid in `world` x-slabs (one per
+    rank), the rigid pass replicated, `prep` + `warmup`
+    untimed ticks, then exactly `steps` ticks bracketed by barriers and device
+    syncs; elapsed = the maximum over ranks.  Slab ranks run unbounded cells
+    (the reference's capped cells read particle ids past a cell's 64 slots
+    that can live on any rank, fluid_kernels.metal:281-283): the all-rank
+    envelope says whether the window stayed where both semantics are the same
+    computation.  transport: "rccl" (the product path) or "gloo" (host-staged,
+    lpe_mg_init_host: two ranks may share one GPU; rehearsal only).  Returns
+    a dict; with keep the context stays open (leg["ctx"])."""
+    s = scenes.scene(scene_name)
+    fl = s["fluid"]
+    bodies, verts = scenes.to_bodies(s["bodies"])
+    cfg = lpe.default_fluid_config()
+    ctx = lpe.Context(device)
+    ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+    ctx.rigid_upload(bodies, verts)
+    edges = slab.slab_edges(fl["x"], world, cfg)
+    slab.setup_rank(ctx, rank, world, fl, edges, cfg, rebalance=rebalance)
+    if transport == "gloo":
+        ctx.mg_init_host(world, rank, slab.GlooTransport(rank, world))
+    else:
+        uid = slab.broadcast_uid(lpe.mg_unique_id() if rank == 0 else None, rank)
+        ctx.mg_init_rccl(world, rank, uid)
+    ctx.world_set_coupling(None)
+    dt_tick = 1.0 / 120.0
+    ctx.world_tick(dt_tick, prep)
+    ctx.world_tick(dt_tick, warmup)
+    ctx.sync()
+    ctx.sph_diag(False)
+    dist.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    ctx.world_tick(dt_tick, steps)
+    ctx.sync()
+    t1 = time.perf_counter()
+    dist.barrier()
+    import torch
+    mine_s = t1 - t0
+    st = ctx.sph_stats()
+    mine = dict(rank=rank, ms_per_tick=mine_s / steps * 1e3, owned=st["slabOwned"], slots=st["slabSlots"],
+                ghosts_in=st["ghostsIn"], wire=st["haloWire"],
+                comm_ranks=ctx.mg_info()["comm_ranks"] if transport == "rccl" else world,
+                edges=[int(e) for e in ctx.sph_slab_info()["edges"][1:-1]])
+    every = [None] * world
+    dist.all_gather_object(every, mine)
+    t = torch.tensor([mine_s], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    env = envelope_all_ranks(dist, st)
+    slow = max(every, key=lambda e: e["ms_per_tick"])
+    n = len(fl["x"])
+    leg = dict(scene=scene_name, desc=s["desc"], fluid_particles=n, rigid_bodies=len(bodies), prep_ticks=prep,
+               ticks_timed=steps, elapsed=elapsed, ticks_per_s=round(steps / elapsed, 2),
+               particle_ticks_per_s=round(n * steps / elapsed, 1),
+               particle_substeps_per_s=round(10 * n * steps / elapsed, 1),
+               ranks=dict(ranks_seen=every[0]["comm_ranks"], world_size=world, transport=transport,
+                          ms_per_tick=[round(e["ms_per_tick"], 4) for e in every],
+                          slowest_rank=slow["rank"], slowest_ms_per_tick=round(slow["ms_per_tick"], 4),
+                          owned=[e["owned"] for e in every], slots=[e["slots"] for e in every],
+                          ghosts_in_max=[e["ghosts_in"] for e in every], wire_records=every[0]["wire"],
+                          edges_columns=every[0]["edges"]),
+               reference_envelope=env, cells="unbounded cells",
+               reference_semantics=env["inside"])
+    if keep:
+        leg["ctx"] = ctx
+        leg["fluid"] = fl
+        leg["U"] = s["U"]
+    else:
+        ctx.close()
+    return leg
+
+
+def single_leg(lpe, scenes, device, scene_name, prep, warmup, steps):
+    """The same scene as ONE domain on this rank's GPU, unbounded cells (the
+    slab ranks' semantics): the scaling baseline measured in the same run
+    (a ticks/s ratio must not mix the capped and unbounded
+    modes)."""
+    s = scenes.scene(scene_name)
+    fl = s["fluid"]
+    bodies, verts = scenes.to_bodies(s["bodies"])
+    ctx = lpe.Context(device)
+    try:
+        ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+        ctx.rigid_upload(bodies, verts)
+        ctx.sph_set_config(lpe.default_fluid_config())
+        ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+        ctx.world_set_coupling(None)
+        ctx.world_tick(1.0 / 120.0, prep + warmup)
+        ctx.sph_diag(False)
+        ctx.sync()
+        t0 = time.perf_counter()
+        ctx.world_tick(1.0 / 120.0, steps)
+        ctx.sync()
+        el = time.perf_counter() - t0
+        st = ctx.sph_stats()
+    finally:
+        ctx.close()
+    return dict(scene=scene_name, fluid_particles=len(fl["x"]), prep_ticks=prep, ticks_timed=steps,
+                ticks_per_s=round(steps / el, 2), cells="unbounded cells",
+                reference_envelope=dict(max_cell_occupancy_window=st["maxCellOccupancyTotal"],
+                                        cells_over_64_window=st["overCapCellsTotal"],
+                                        inside=st["overCapCellsTotal"] == 0))
+
+
+def scaling_blocks(world, primary, strong_leg, c5_one, m_one):
+    """The N-rank line's scaling blocks from its legs (slab_leg / single_leg
+    dicts): `scaling_strong_c5` -- C5 over the ranks against C5 as one domain
+    on one GPU (speedup, efficiency = rate_N / (N x rate_1)); `scaling_weak`
+    -- MW{N} (primary) against scene M as one domain (efficiency = rate_N /
+    rate_1, each rank holding an M-sized slab).  primary is the leg `value`
+    was timed on (MW{N}, or C5 itself under --scene C5, then strong_leg is
+    None and m_one is None)."""
+    out = {}
+    strong = strong_leg if strong_leg is not None else primary
+    sc = dict(scene="C5", desc="2,097,152 SPH particles (fixed) over the ranks' x-slabs",
+              fluid_particles=strong["fluid_particles"], ranks=world, ticks_per_s=strong["ticks_per_s"],
+              single_gpu=c5_one, speedup=round(strong["ticks_per_s"] / c5_one["ticks_per_s"], 3),
+              efficiency=round(strong["ticks_per_s"] / (world * c5_one["ticks_per_s"]), 4),
+              reference_envelope=strong["reference_envelope"],
+              reference_semantics=bool(strong["reference_envelope"]["inside"] and
+                                       c5_one["reference_envelope"]["inside"]),
+              slowest_ms_per_tick=strong["ranks"]["slowest_ms_per_tick"], ranks_detail=strong["ranks"])
+    out["scaling_strong_c5"] = sc
+    if m_one is not None:
+        mw = primary["ticks_per_s"]
+        n = primary["fluid_particles"]
+        out["scaling_weak"] = dict(
+            scene=primary["scene"], desc=primary["desc"], fluid_particles=n, ranks=world,
+            ticks_per_s=mw, particle_ticks_per_s=round(n * mw, 1), particle_substeps_per_s=round(10 * n * mw, 1),
+            value_is=f"{world} x {primary['scene']} ticks/s: the whole job's throughput in ticks/s of the "
+                     f"256k-particle metric scene (each rank advances one M-sized slab per tick)",
+            single_gpu=m_one, efficiency=round(mw / m_one["ticks_per_s"], 4),
+            reference_semantics=bool(primary["reference_envelope"]["inside"] and m_one["reference_envelope"]["inside"]))
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -620,6 +785,11 @@ def main():
                          "(in-process transport); prints a check line, not the metric")
     ap.add_argument("--rebalance", type=int, default=10,
                     help="N > 1: move the slab edges towards equal counts every this many ticks (0: fixed)")
+    ap.add_argument("--transport", choices=("rccl", "gloo"), default="rccl",
+                    help="N > 1: the slab exchange over RCCL (default, the product path) or the host-staged "
+                         "gloo transport (lpe_mg_init_host; ranks may share one GPU: rehearsal only)")
+    ap.add_argument("--strong-prep", type=int, default=240,
+                    help="N > 1: untimed ticks of the C5 strong-scaling leg (and its single-GPU baseline)")
     ap.add_argument("--cells", choices=("ref", "unbounded"), default="ref",
                     help="ref (default): the timed window runs the reference's 64-particle cells "
                          "(LPE_SPH_MODE_REF_CELL_CAP, fluid.hpp:56); unbounded: no per-cell cap")
@@ -649,72 +819,69 @@ def main():
         return loopback_check(args, lpe, scenes, slab, local)
     sharded = world > 1 and not args.replicas
     scene_name = f"MW{world}" if sharded and args.scene == "M" else args.scene
-    s = scenes.scene(scene_name)
-    fl = s["fluid"]
-    bodies, verts = scenes.to_bodies(s["bodies"])
     dt_tick = 1.0 / 120.0
-
-    ctx = lpe.Context(local)
-    ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
-    ctx.rigid_upload(bodies, verts)
-    if sharded:
-        cfg = lpe.default_fluid_config()
-        edges = slab.slab_edges(fl["x"], world, cfg)
-        slab.setup_rank(ctx, rank, world, fl, edges, cfg, rebalance=args.rebalance)
-        uid = slab.broadcast_uid(lpe.mg_unique_id() if rank == 0 else None, rank)
-        ctx.mg_init_rccl(world, rank, uid)
-    else:
-        ctx.sph_set_config(lpe.default_fluid_config())
-        ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
-    ctx.world_set_coupling(None)      # every body, reverse insertion (gatherRigidBodies view order)
-
-    # scene preparation: the pentagons fall into the pool and settle into a
-    # pile (the steady state: ~10k pairs, ~35k contacts); BASELINE.md times
-    # the reference's pile the same way, after 240 warm-up ticks
-    ctx.world_tick(dt_tick, args.prep)
-    # the timed window in the reference's own cell semantics (its 64-slot
-    # cells: dropped inserts, cross-cell reads; fluid.hpp:56, metal:237-240,
-    # :281-283) -- the mode tests/test_configs_gpu.py pins at this state;
-    # slab ranks run unbounded cells (the capped walk is single-domain)
-    capped = args.cells == "ref" and not sharded
-    if capped:
-        ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP)
-    ctx.world_tick(dt_tick, args.warmup)
-    ctx.sync()
 
     def barrier():
         if dist is not None:
             dist.barrier()
 
-    ctx.sph_diag(False)               # restart the window totals (cells over the reference's 64)
-    barrier()
-    ctx.sync()
-    t0 = time.perf_counter()
-    ctx.world_tick(dt_tick, args.steps)
-    ctx.sync()
-    t1 = time.perf_counter()
-    barrier()
-    elapsed = t1 - t0
-    wstats = ctx.sph_stats()
     ranks_info = None
-    if dist is not None:
-        import torch
-        mine = dict(rank=rank, ms_per_tick=elapsed / args.steps * 1e3, owned=wstats["slabOwned"],
-                    slots=wstats["slabSlots"], ghosts_in=wstats["ghostsIn"], wire=wstats["haloWire"],
-                    comm_ranks=ctx.mg_info()["comm_ranks"] if sharded else None,
-                    edges=[int(e) for e in ctx.sph_slab_info()["edges"][1:-1]] if sharded else None)
-        every = [None] * world
-        dist.all_gather_object(every, mine)
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        slow = max(every, key=lambda e: e["ms_per_tick"])
-        ranks_info = dict(ranks_seen=every[0]["comm_ranks"], world_size=world,
-                          ms_per_tick=[round(e["ms_per_tick"], 4) for e in every],
-                          slowest_rank=slow["rank"], slowest_ms_per_tick=round(slow["ms_per_tick"], 4),
-                          owned=[e["owned"] for e in every], slots=[e["slots"] for e in every],
-                          ghosts_in_max=[e["ghosts_in"] for e in every], wire_records=every[0]["wire"],
-                          edges_columns=every[0]["edges"])
+    if sharded:
+        # the sharded path: slab_leg times exactly K ticks between barriers and
+        # reports the maximum over ranks and the all-rank envelope
+        leg = slab_leg(lpe, scenes, slab, dist, rank, world, local, scene_name, args.prep, args.warmup,
+                       args.steps, args.transport, args.rebalance, keep=True)
+        ctx, fl, elapsed = leg["ctx"], leg["fluid"], leg["elapsed"]
+        s = dict(desc=leg["desc"], U=leg["U"])
+        n_bodies = leg["rigid_bodies"]
+        capped = False
+        wstats = ctx.sph_stats()
+        wstats["overCapCellsTotal"] = leg["reference_envelope"]["cells_over_64_window"]
+        wstats["maxCellOccupancyTotal"] = leg["reference_envelope"]["max_cell_occupancy_window"]
+        ranks_info = leg["ranks"]
+    else:
+        s = scenes.scene(scene_name)
+        fl = s["fluid"]
+        bodies, verts = scenes.to_bodies(s["bodies"])
+        n_bodies = len(bodies)
+        ctx = lpe.Context(local)
+        ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+        ctx.rigid_upload(bodies, verts)
+        ctx.sph_set_config(lpe.default_fluid_config())
+        ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+        ctx.world_set_coupling(None)      # every body, reverse insertion (gatherRigidBodies view order)
+
+        # scene preparation: the pentagons fall into the pool and settle into a
+        # pile (the steady state: ~10k pairs, ~35k contacts); BASELINE.md times
+        # the reference's pile the same way, after 240 warm-up ticks
+        ctx.world_tick(dt_tick, args.prep)
+        # the timed window in the reference's own cell semantics (its 64-slot
+        # cells: dropped inserts, cross-cell reads; fluid.hpp:56, metal:237-240,
+        # :281-283) -- the mode tests/test_configs_gpu.py pins at this state
+        capped = args.cells == "ref"
+        if capped:
+            ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP)
+        ctx.world_tick(dt_tick, args.warmup)
+        ctx.sync()
+
+        ctx.sph_diag(False)               # restart the window totals (cells over the reference's 64)
+        barrier()
+        ctx.sync()
+        t0 = time.perf_counter()
+        ctx.world_tick(dt_tick, args.steps)
+        ctx.sync()
+        t1 = time.perf_counter()
+        barrier()
+        elapsed = t1 - t0
+        wstats = ctx.sph_stats()
+        if dist is not None:              # replicas: the slowest replica's window
+            import torch
+            t = torch.tensor([elapsed], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+            env = envelope_all_ranks(dist, wstats)
+            wstats["overCapCellsTotal"] = env["cells_over_64_window"]
+            wstats["maxCellOccupancyTotal"] = env["max_cell_occupancy_window"]
     extras = {}
     if world == 1 and not args.no_extras:
         rate = args.steps / elapsed
@@ -746,10 +913,22 @@ def main():
     n_rank = len(out["x"])
     render = render_bench(ctx, s["U"]) if world == 1 and not args.no_density_microbench else None
 
+    strong_leg = None
+    if sharded:
+        barrier()
+        ctx.close()        # (every rank past its last collective on this communicator)
+        ctx = None
+        if scene_name != "C5":
+            # north_star's scaling claim: the fixed 2M-particle C5 scene over
+            # the same ranks (strong scaling), in the same line
+            strong_leg = slab_leg(lpe, scenes, slab, dist, rank, world, local, "C5", args.strong_prep,
+                                  args.warmup, args.steps, args.transport, args.rebalance)
+
     if rank != 0:
         if dist is not None:
             dist.barrier()
-        ctx.close()        # RCCL communicator torn down by every rank after the last barrier
+        if ctx is not None:
+            ctx.close()    # RCCL communicator torn down by every rank after the last barrier
         return
 
     assert np.isfinite(out["x"]).all() and np.isfinite(out["vy"]).all()
@@ -819,15 +998,15 @@ def main():
                                f"{args.prep + args.warmup + args.steps} (settled pile)",
                    "scene": scene_name, "fluid_particles": len(fl["x"]),
                    "fluid_particles_rank0": n, "prep_ticks": args.prep,
-                   "rigid_bodies": len(bodies), "substeps": 10, "dt": dt_tick,
+                   "rigid_bodies": n_bodies, "substeps": 10, "dt": dt_tick,
                    "systems": ["FluidSystem (SPH + coupling)", "Boundary", "Gravity",
                                "RigidBodyCollision (broadphase, GJK/EPA, PGS 10 it, position 10 it)",
                                "Rotation", "Movement", "Sleep"],
                    "mode": "resident (ECS sync skipped inside the timed region)",
                    "cells": ("the reference's 64-particle cells (LPE_SPH_MODE_REF_CELL_CAP)" if capped
                              else "unbounded cells"),
-                   "parallelism": (f"SPH x-slabs x{world} (RCCL halo + bbox/accumulator all-reduce), "
-                                   f"rigid pass replicated") if sharded else
+                   "parallelism": (f"SPH x-slabs x{world} ({'RCCL' if args.transport == 'rccl' else 'gloo host-staged'}"
+                                   f" halo + bbox/accumulator all-reduce), rigid pass replicated") if sharded else
                                   ("single GPU" if world == 1 else f"replica x{world}")},
         "roofline": roof,
         "roofline_density": roof_d,
@@ -845,9 +1024,22 @@ def main():
                     "LPE_SPH_MODE_REF_CELL_CAP (config.cells), which reproduces that behaviour exactly "
                     "(tests/test_configs_gpu.py checks both modes at this scene)"},
         "rigid": {"pairs": int(len(pairs)), "contacts": int(len(contacts)), "colours": int(ncolours)},
+        "hw_queues": lpe.hw_queues(),
     }
     if ranks_info is not None:
         line["ranks"] = ranks_info
+    if sharded:
+        # the scaling baselines, measured in this run on rank 0's GPU while the
+        # other ranks wait: each scene as ONE domain in the slab ranks' cell
+        # semantics (unbounded), so every ratio compares one computation
+        # (ADVICE r4); the driver's own N=1 line times scene M in the
+        # reference's capped cells
+        primary = dict(scene=scene_name, desc=s["desc"], fluid_particles=len(fl["x"]),
+                       ticks_per_s=round(args.steps / elapsed, 2), reference_envelope=line["reference_envelope"],
+                       ranks=ranks_info)
+        c5_one = single_leg(lpe, scenes, local, "C5", args.strong_prep, args.warmup, args.steps)
+        m_one = single_leg(lpe, scenes, local, "M", args.prep, args.warmup, args.steps) if scene_name != "C5" else None
+        line.update(scaling_blocks(world, primary, strong_leg, c5_one, m_one))
     line.update(extras)
     if world == 1 and not args.no_extras:
         # the same scene in the other cell mode

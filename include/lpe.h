@@ -247,6 +247,15 @@ int  lpe_abi_version(void);
 int  lpe_device_count(int *count);
 /* Blocks until all work queued on the context's stream is done. */
 int  lpe_sync(lpe_ctx *ctx);
+/* Hardware queues.  A context runs up to four streams (fluid step,
+ * prelaunch, collision detection, position solver; RCCL adds its own) and
+ * HIP maps streams round robin onto GPU_MAX_HW_QUEUES queues (4 by default):
+ * two streams on one queue execute in submission order and the tick's
+ * overlaps collapse (performance only, results are unchanged).  Callers
+ * should export GPU_MAX_HW_QUEUES=8 before their first HIP call; the library
+ * sets 8 when it is loaded first and the variable is unset.  Reports the
+ * value in effect (*queues) and whether the library set it. */
+int  lpe_hw_queues(int *queues, int *set_by_library);
 
 /* ---- kernel timing (bench / profiling; no reference counterpart) ------- */
 /* on = 1: every launch of a named kernel on the context's stream is

@@ -27,6 +27,7 @@
 // Orders: canonical (pairs by entity id; manifolds = pairs) by default, or
 // caller-supplied (lpe_rigid_step_ordered) to replay the reference's quadtree
 // and std::unordered_map orders bit for bit.
+#include <atomic>
 #include "lpe_internal.h"
 #include "rigid_dev.h"
 #include "lpe_trig.h"
@@ -3744,13 +3745,18 @@ static StripeBufs *stripe_bufs(lpe_ctx *ctx, RigidDev *d) {
 // between workgroups with spin waits, so all S must be resident at once:
 // S <= the device's CU count (256 on an MI355X: STRIPES_MAX binds; a smaller
 // compute partition gets fewer, wider stripes).
+// Cached per device (contexts on devices of different CU counts,
+// e.g. another compute-partition mode, must not share one bound).
 static int stripe_cap(lpe_ctx *ctx) {
-    static int cap = 0;
+    static std::atomic<int> caps[64];
+    const int dev = ctx->device;
+    int cap = (dev >= 0 && dev < 64) ? caps[dev].load(std::memory_order_relaxed) : 0;
     if (!cap) {
         int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
             cus = 2;
         cap = std::min(STRIPES_MAX, cus) & ~1;
+        if (dev >= 0 && dev < 64) caps[dev].store(cap, std::memory_order_relaxed);
     }
     return cap;
 }

@@ -42,6 +42,7 @@
 // accumulators (float atomics in the reference, metal:892-898) are exact
 // fixed-point sums rounded once (sph_coupling.h): deterministic, and equal
 // to the oracle's bit for bit.
+#include <cstdlib>
 #include "lpe_internal.h"
 #include "sph_coupling.h"
 #include "lpe_trace.h"
@@ -2527,6 +2528,26 @@ extern "C" int lpe_device_count(int *count) {
     int c = 0;
     if (hipGetDeviceCount(&c) != hipSuccess) c = 0;
     *count = c;
+    return LPE_OK;
+}
+
+// Hardware queues.  A context runs up to four streams (fluid
+// step, prelaunch, detection, position solver) and RCCL adds its own; HIP maps
+// streams round robin onto GPU_MAX_HW_QUEUES queues (4 by default) and two
+// streams on one queue run in submission order, so the tick's overlaps
+// collapse.  When the library is loaded before the host program's first HIP
+// call (the C++ drop-in, a ctypes caller), this constructor asks for 8 unless
+// the caller chose; lpe_hw_queues reports the value in effect.
+static int g_hwq_set_by_lib = 0;
+__attribute__((constructor)) static void lpe_hw_queues_default() {
+    if (!std::getenv("GPU_MAX_HW_QUEUES")) g_hwq_set_by_lib = setenv("GPU_MAX_HW_QUEUES", "8", 0) == 0;
+}
+
+extern "C" int lpe_hw_queues(int *queues, int *set_by_library) {
+    if (!queues) return LPE_ERR_ARG;
+    const char *v = std::getenv("GPU_MAX_HW_QUEUES");
+    *queues = (v && std::atoi(v) > 0) ? std::atoi(v) : 4;
+    if (set_by_library) *set_by_library = g_hwq_set_by_lib;
     return LPE_OK;
 }
 

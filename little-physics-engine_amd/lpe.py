@@ -168,6 +168,7 @@ SIGNATURES = {
     "lpe_destroy": ([C.c_void_p], C.c_int),
     "lpe_last_error": ([C.c_void_p], C.c_char_p),
     "lpe_sync": ([C.c_void_p], C.c_int),
+    "lpe_hw_queues": ([_IP, _IP], C.c_int),
     "lpe_timing_enable": ([C.c_void_p, C.c_int], C.c_int),
     "lpe_timing_reset": ([C.c_void_p], C.c_int),
     "lpe_timing_read": ([C.c_void_p, C.c_int, C.c_char_p, C.c_int, C.POINTER(C.c_double),
@@ -314,6 +315,13 @@ def mg_loopback_run(ctxs, nticks: int, dt_tick: float = 0.0, world: "WorldConfig
         msgs = [lib().lpe_last_error(c._h) for c in ctxs]
         raise LpeError(f"lpe_mg_loopback_run: {STATUS.get(st, st)}: "
                        + "; ".join(m.decode() for m in msgs if m))
+
+
+def hw_queues() -> dict:
+    """GPU_MAX_HW_QUEUES in effect (lpe_hw_queues) and whether the library set it."""
+    q, by = C.c_int32(0), C.c_int32(0)
+    lib().lpe_hw_queues(C.byref(q), C.byref(by))
+    return dict(queues=q.value, set_by_library=bool(by.value))
 
 
 def device_count() -> int:

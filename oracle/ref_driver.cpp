@@ -18,6 +18,7 @@
 
 #include <cmath>
 #include <cstring>
+#include <unordered_map>
 #include <vector>
 
 #include "entities/entity_components.hpp"
@@ -164,10 +165,16 @@ extern "C" int lpref_rigid_ticks(const lpe_rigid_config *cfg, double spt, double
         bp.smallParticleThreshold = cfg->smallParticleThreshold;
         auto cand = Broadphase::detectCollisions(s.reg, sh, bp);
         auto manifold = narrowPhase(s.reg, cand);
-        std::vector<int> idx_of;   /* entity -> body index */
+        /* entity -> body index (a table: the piles have ~10k pairs, 30k contacts) */
+        std::vector<int> idx_of;
+        for (int i = 0; i < nb; i++) {
+            size_t k = (size_t)entt::to_entity(s.ents[i]);
+            if (idx_of.size() <= k) idx_of.resize(k + 1, -1);
+            idx_of[k] = i;
+        }
         auto body_index = [&](entt::entity e) {
-            for (int i = 0; i < nb; i++) if (s.ents[i] == e) return i;
-            return -1;
+            size_t k = (size_t)entt::to_entity(e);
+            return k < idx_of.size() ? idx_of[k] : -1;
         };
         std::vector<lpe_contact> cs;
         for (size_t k = 0; k < manifold.collisions.size(); k++) {
@@ -186,10 +193,14 @@ extern "C" int lpref_rigid_ticks(const lpe_rigid_config *cfg, double spt, double
             /* manifold iteration order -> contact indices (contacts keep
              * narrowphase order inside a manifold, contact_manager.cpp:206-240) */
             std::vector<char> used(cs.size(), 0);
+            std::unordered_map<long long, std::vector<size_t>> by_pair;   /* (a, b) -> contacts, narrowphase order */
+            for (size_t k = 0; k < cs.size(); k++) by_pair[(long long)cs[k].a * nb + cs[k].b].push_back(k);
+            static const std::vector<size_t> none;
             for (const auto &m : mans) {
                 int a = body_index(m.a), b = body_index(m.b);
-                for (size_t k = 0; k < cs.size(); k++) {
-                    if (used[k] || cs[k].a != a || cs[k].b != b) continue;
+                auto it = by_pair.find((long long)a * nb + b);
+                for (size_t k : (it == by_pair.end() ? none : it->second)) {
+                    if (used[k]) continue;
                     if (std::fabs(cs[k].nx - m.normal.x) >= 1e-7 || std::fabs(cs[k].ny - m.normal.y) >= 1e-7) continue;
                     used[k] = 1;
                     order.push_back((int32_t)k);

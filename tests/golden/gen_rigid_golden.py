@@ -9,10 +9,21 @@ contact order (std::unordered_map iteration, libstdc++), the state after the
 PGS (restated: contact_solver.cpp is unbuildable here, see Makefile.ref), after
 the reference position solver, and after the full tick.
 
-    make ref && python tests/golden/gen_rigid_golden.py
+Bench-scale cases (round 5):
+  pileM_t1  -- one reference tick on the metric scene's settled pile
+               (pile_M_t250.npz: 4,100 bodies, ~10k pairs, 10 PGS iterations);
+  C3_t240   -- 240 reference ticks of the C3 random-polygon pile (4,100 bodies,
+               16 PGS iterations; the state the bench times C3 at), the last one recorded.
+The reference's ContactManager is rebuilt every tick
+(rigid_body_collision.cpp:38-40), so running nt-1 ticks and then one more from
+the extracted state is the same computation as nt ticks in one call.
+
+    make ref && python tests/golden/gen_rigid_golden.py [--out DIR] [case ...]
 """
+import argparse
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -21,25 +32,43 @@ sys.path.insert(0, os.path.dirname(HERE))
 from conftest import lpe, scenes  # noqa: E402
 import oracle  # noqa: E402
 
-CASES = [("mix6", 30), ("C1", 120), ("pile8", 60), ("pile16", 90)]
+# (name, ticks recorded at, start) -- start None: the seeded scene at tick 0
+CASES = [("mix6", 30, None), ("C1", 120, None), ("pile8", 60, None), ("pile16", 90, None),
+         ("pileM", 1, "pile_M_t250.npz"), ("C3", 240, None)]
 DT = 1.0 / 120.0
 
 
-def main():
-    assert oracle.ref_available(), "build oracle/_ref first: make ref"
-    for name, nt in CASES:
+def start_state(name, start):
+    if start is None:
         s = scenes.rigid_scene(name)
         b, v = scenes.to_bodies(s["bodies"])
-        cfg = lpe.rigid_config(universe=s["U"], pgs_iterations=s["pgs_iterations"])
-        start = oracle.ref_rigid_ticks(cfg, b, v, nt - 1, DT)["final"] if nt > 1 else b
-        R = oracle.ref_rigid_ticks(cfg, b, v, nt, DT)
+        return b, v, float(s["U"]), int(s["pgs_iterations"])
+    z = np.load(os.path.join(HERE, start))
+    return z["bodies"], z["verts"], 32.0, 10     # scene M: U = 32 m, reference default iterations
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=HERE)
+    ap.add_argument("cases", nargs="*")
+    a = ap.parse_args()
+    assert oracle.ref_available(), "build oracle/_ref first: make ref"
+    for name, nt, start in CASES:
+        if a.cases and name not in a.cases:
+            continue
+        t0 = time.time()
+        b, v, U, iters = start_state(name, start)
+        cfg = lpe.rigid_config(universe=U, pgs_iterations=iters)
+        tick_start = oracle.ref_rigid_ticks(cfg, b, v, nt - 1, DT)["final"] if nt > 1 else b
+        R = oracle.ref_rigid_ticks(cfg, tick_start, v, 1, DT)
         np.savez_compressed(
-            os.path.join(HERE, f"rigid_{name}_t{nt}.npz"), bodies_init=b, verts=v,
-            universe=s["U"], pgs_iterations=s["pgs_iterations"], nticks=nt, dt=DT,
-            tick_start=start, before_rigid=R["before_rigid"], pairs=R["pairs"],
+            os.path.join(a.out, f"rigid_{name}_t{nt}.npz"), bodies_init=b, verts=v,
+            universe=U, pgs_iterations=iters, nticks=nt, dt=DT,
+            tick_start=tick_start, before_rigid=R["before_rigid"], pairs=R["pairs"],
             contacts=R["contacts"], pgs_order=R["pgs_order"], after_pgs=R["after_pgs"],
             after_pos=R["after_pos"], final=R["final"])
-        print(name, nt, "bodies", len(b), "pairs", len(R["pairs"]), "contacts", len(R["contacts"]))
+        print(name, nt, "bodies", len(b), "pairs", len(R["pairs"]), "contacts", len(R["contacts"]),
+              "%.1fs" % (time.time() - t0))
 
 
 if __name__ == "__main__":

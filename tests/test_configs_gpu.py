@@ -8,7 +8,9 @@ sim.cpp:107-114) from that exact state runs on the device and on the oracle
 (OpenMP over particles; results are thread-count independent).  The fluid
 and the bodies must be bit-identical (the rigid path's trigonometry is the
 implementation device and oracle share, csrc/lpe_trig.h).  ("M", 3000) is
-the state bench.py times: the metric scene after its 3,000 settle ticks.
+the state bench.py times: the metric scene after its 3,000 settle ticks;
+("C4", 3000) likewise C4's timed state (round 5: C4 is timed settled, in the
+reference's capped cells).
 
 The reference cell-capacity mode (LPE_SPH_MODE_REF_CELL_CAP) is the
 reference's own grid semantics; M's settled pool compresses cells past the
@@ -70,6 +72,8 @@ def _advanced(name, prep):
 @pytest.mark.parametrize("name,prep,mode", [
     ("C2", 30, lpe.SPH_MODE_REF_CELL_CAP),
     ("C4", 90, lpe.SPH_MODE_REF_CELL_CAP),
+    ("C4", 3000, lpe.SPH_MODE_REF_CELL_CAP),
+    ("C4", 3000, 0),
     ("M", 240, lpe.SPH_MODE_REF_CELL_CAP),
     ("M", 240, 0),
     ("M", 3000, lpe.SPH_MODE_REF_CELL_CAP),
@@ -97,8 +101,8 @@ def test_config_world_tick_bit_exact(oracle_mod, name, prep, mode):
     assert st["refUndefined"] == 0
     if name == "M" and prep == 240:  # the pool is still compressed past the reference's 64 slots
         assert st["overCapCells"] > 0 and st["maxCellOccupancy"] > 64
-    if name == "M" and prep == 3000:  # the bench's timed state (a few cells may still exceed 64)
-        print(f"M@3000 mode {mode}: overCapCells {st['overCapCells']}, max occupancy {st['maxCellOccupancy']}")
+    if prep == 3000:  # the bench's timed states of M and C4 (a few cells may still exceed 64)
+        print(f"{name}@3000 mode {mode}: overCapCells {st['overCapCells']}, max occupancy {st['maxCellOccupancy']}")
     for k, col in (("x", 0), ("y", 1), ("vx", 2), ("vy", 3), ("density", 11), ("pressure", 12)):
         np.testing.assert_array_equal(out[k], p[:, col], err_msg=(name, k, st))
     for k in ("x", "y", "angle", "vx", "vy", "omega", "sleep_counter"):
