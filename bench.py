@@ -815,6 +815,9 @@ def main():
     lpe = _load("lpe", os.path.join(PKG, "lpe.py"))
     scenes = _load("scenes", os.path.join(PKG, "scenes.py"))
     slab = _load("slab", os.path.join(PKG, "slab.py"))
+    if args.transport == "gloo" and world > 1:
+        # rehearsal: ranks may share the GPUs there are (RCCL would refuse)
+        local = local % max(1, lpe.device_count())
     if args.loopback:
         return loopback_check(args, lpe, scenes, slab, local)
     sharded = world > 1 and not args.replicas
