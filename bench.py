@@ -1060,10 +1060,11 @@ def main():
         line["cpu_baseline"] = cpu_baseline(args.scene, settled)
     if world == 1 and args.scene == "M":
         line["dropin"] = dropin_record()
-    print(json.dumps(line))
+    print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()
-    ctx.close()
+    if ctx is not None:
+        ctx.close()
 
 
 if __name__ == "__main__":

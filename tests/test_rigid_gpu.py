@@ -9,7 +9,10 @@
 Bar: bit-exact contact-pair lists (and contact topology a, b, pair); the
 device uses the reference's operation order with no FMA contraction, but its
 fp64 cos/sin (ROCm device libm) can differ from glibc's by an ulp, so contact
-geometry is compared at 1e-12 relative and the solver outputs at 1e-7
+geometry is compared at 1e-12 relative / 1e-13 absolute (the bar of the CPU
+restatement against the same fixtures, test_portable_trig_within_an_ulp_of_libm:
+at the bench-scale piles a handful of near-zero penetrations and normal
+components differ by 1-3e-14 m) and the solver outputs at 1e-7
 (positions, fp64) / 1e-5 (velocities, fp32 rows) -- the north_star bar is
 1e-5 relative.  Integrators use no transcendental and stay bit-exact.
 """
@@ -70,7 +73,7 @@ def test_reference_orders_replay(gpu_ctx, path):
     ref = z["contacts"]
     assert st["contacts"] == len(ref)
     same(cs, ref, ("a", "b"))
-    same(cs, ref, GEOM, rtol=1e-12, atol=1e-14)
+    same(cs, ref, GEOM, rtol=1e-12, atol=1e-13)
     out = gpu_ctx.rigid_download()
     if len(ref):
         ref_state(out, z["after_pos"])
@@ -88,7 +91,7 @@ def test_device_own_detection_matches_reference(gpu_ctx, path):
     reference's: the broadphase pair set equal to the reference quadtree's
     (broadphase.cpp:233-295) as a set of entity pairs, bit for bit, and every
     pair's narrowphase contacts (narrowphase.cpp:352-420) equal to the
-    reference's for that pair, in order, geometry within 1e-12 (the device's
+    reference's for that pair, in order, geometry within 1e-12 rel / 1e-13 abs (the device's
     trigonometry vs glibc, test_portable_trig_within_an_ulp_of_libm).  The
     bench-scale fixtures (rigid_pileM_t1: 10,156 pairs / 29,706 contacts,
     rigid_C3_t240: 9,462 / 27,443) are one reference tick on the states the
@@ -111,7 +114,7 @@ def test_device_own_detection_matches_reference(gpu_ctx, path):
     kd, cd = grouped(cs)
     kr, cr = grouped(ref)
     np.testing.assert_array_equal(kd, kr)
-    same(cd, cr, GEOM, rtol=1e-12, atol=1e-14)
+    same(cd, cr, GEOM, rtol=1e-12, atol=1e-13)
     print(f"{os.path.basename(path)}: {len(pairs)} pairs, {len(cs)} contacts equal to the reference")
 
 
