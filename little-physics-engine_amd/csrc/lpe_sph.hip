@@ -1752,6 +1752,9 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     // run that an XCD-contiguous mapping (xcd_block) would put on one XCD
     const int lb = sp.chunk > 0 ? xcd_chunk_block(sp.nblk, sp.chunk) : (int)blockIdx.x;
     if (lb < 0) return;                       // (padding of the chunked grid)
+    const int ftb = lb;                       // (trace builds: the block's stamp slots, cleared per launch)
+    (void)ftb;
+    FTRCLR();
     if (sp.mergePre && lb == 0 && threadIdx.x == 0) merge_prestats_dev(status, sp.mergePre);   // (before the kick's reset)
     const int nn = sp.nptr ? *sp.nptr : sp.n;
     const int s0 = lb * HB, s1 = min(s0 + HB, nn);
@@ -1968,7 +1971,6 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                            [&](int k, const FRec &o) { if (k != s) pair(o.a, o.b); });
     }
     FTRMAX(5, wall_clock64());
-    FTRMAX(6, cnt);
     CoupleState st;
     st.x = xi; st.y = yi;
     st.vhx = S.vhx[sl]; st.vhy = S.vhy[sl];
@@ -1994,12 +1996,13 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
             // the particle's coupling inputs (pow only for a particle with hits)
             pool.in[threadIdx.x] = couple_in(st, cp, cp.nr > 0 && nh > 0);
             __syncthreads();
+            FTR(6);
             // ---- the pairs (geometry and impulse in one pass: the
             // velocities are final), round robin
             for (int q = threadIdx.x; q < total; q += HB) {
                 PairTerm t;
                 pool.flag[q] = (unsigned char)couple_pair(pool.in[pOwn[q]], cp, sp.dt, true, rc, pRig[q], acq,
-                                                          status, t);
+                                                          status, t, FTR_PAIRS());
                 pool.term[q] = t;
             }
             __syncthreads();

@@ -6,7 +6,7 @@
 // accessors below.  Without those macros (the shipped build) every stamp is an
 // empty statement and nothing here is compiled.
 //
-//   FTR(k), FTRMAX(k, v)   k_forces_couple phases, per logical block `lb`
+//   FTR(k), FTRMAX(k, v)   k_forces_couple phases, per trace block `ftb` (the bbox-partial slot: tiles, then heavy quarters)
 //   PTR(w, k), PTR_SET     k_pgs_colour / k_pos_colour colour steps
 //   STR(w, j, k), STR_SET  k_pgs_stripes / k_pos_stripes phases per workgroup j
 //   CTR(k, v), STP(k)      k_group_colour stages per group, k_stripe_setup stages
@@ -16,8 +16,15 @@
 #ifdef LPE_FTRACE
 __device__ unsigned long long g_ftrace[4096 * 8];
 __device__ int g_ftrace_on;
-#define FTR(k) do { if (g_ftrace_on && threadIdx.x == 0) g_ftrace[lb * 8 + (k)] = wall_clock64(); } while (0)
-#define FTRMAX(k, v) do { if (g_ftrace_on && (threadIdx.x & 63) == 0) atomicMax(&g_ftrace[lb * 8 + (k)], (unsigned long long)(v)); } while (0)
+__device__ unsigned long long g_ftrace2[4096 * 8];
+#define FTR(k) do { if (g_ftrace_on && threadIdx.x == 0) g_ftrace[ftb * 8 + (k)] = wall_clock64(); } while (0)
+#define FTRCLR() do { if (g_ftrace_on && threadIdx.x == 0) for (int k_ = 0; k_ < 8; k_++) { g_ftrace[ftb * 8 + k_] = 0; g_ftrace2[ftb * 8 + k_] = 0; } } while (0)
+// the coupling pair's stages (sph_coupling.h CPT), per block
+#define FTR_PAIRS() (g_ftrace_on ? g_ftrace2 + ftb * 8 : (unsigned long long *)nullptr)
+extern "C" int lpe_ftrace2(unsigned long long *host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ftrace2), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
+}
+#define FTRMAX(k, v) do { if (g_ftrace_on && (threadIdx.x & 63) == 0) atomicMax(&g_ftrace[ftb * 8 + (k)], (unsigned long long)(v)); } while (0)
 extern "C" int lpe_ftrace(int on, unsigned long long *host, int n) {
     if (host) (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ftrace), sizeof(unsigned long long) * n);
     unsigned long long z[4096 * 8] = {};
@@ -26,6 +33,8 @@ extern "C" int lpe_ftrace(int on, unsigned long long *host, int n) {
 }
 #else
 #define FTR(k) do {} while (0)
+#define FTRCLR() do {} while (0)
+#define FTR_PAIRS() ((unsigned long long *)nullptr)
 #define FTRMAX(k, v) do {} while (0)
 #endif
 

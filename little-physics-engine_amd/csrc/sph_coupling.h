@@ -187,6 +187,12 @@ __device__ __forceinline__ void xacc_add(unsigned long long *__restrict__ acc, f
     const unsigned long long v = (unsigned long long)M << (pos & 31);
     unsigned long long lo = v & 0xffffffffull, hi = v >> 32;
     if (u >> 31) { lo = 0ull - lo; hi = 0ull - hi; }             // two's complement limbs
+#ifdef LPE_NO_XACC_ATOMICS
+    // (profiling builds only: the adds skipped, results wrong -- what the
+    // contended atomics cost the coupling)
+    if ((lo | hi) == 0x5a5a5a5a5a5aull) acc[0] = 0;
+    return;
+#endif
     if (lo) atomicAdd(&acc[pos >> 5], lo);
     if (hi) atomicAdd(&acc[(pos >> 5) + 1], hi);
 }
@@ -343,12 +349,28 @@ struct CoupleIn {
     float x, y, vx, vy, mass, densityF, pressureF, effArea;
 };
 
+// (trace builds, -DLPE_FTRACE: the stages of one pair, each after a wait for
+// its memory operations, as the maximum over lanes of the time since the
+// pair's start -- profiles/forces_trace.py; the shipped build has no stamps)
+#if defined(LPE_FTRACE) && !defined(LPE_FTRACE_NOCPT)
+#define CPT0() const unsigned long long cpt0_ = wall_clock64()
+#define CPT(k) do { if (cp_tr) { __builtin_amdgcn_s_waitcnt(0); atomicMax(cp_tr + (k), wall_clock64() - cpt0_); } } while (0)
+#else
+#define CPT0() do {} while (0)
+#define CPT(k) do {} while (0)
+#endif
 __device__ __forceinline__ int couple_pair(const CoupleIn &in, const CoupleParams &cp, float dt, bool impulse,
                                            const float4 *__restrict__ rc, int r,
                                            unsigned long long *__restrict__ acq, int32_t *__restrict__ status,
-                                           PairTerm &t) {
+                                           PairTerm &t, unsigned long long *cp_tr = nullptr) {
+    (void)cp_tr;
+    CPT0();
     RigC rb;
     const float4 *vt = rigc_load(rc, r, rb);
+#if defined(LPE_FTRACE) && !defined(LPE_FTRACE_NOCPT)
+    if (rb.nv == 255) t.ax = rb.px;        // (consumes the record before the first stamp)
+#endif
+    CPT(0);
     const float px = in.x, py = in.y;
     CoupleState st;                    // the fields impulse_term reads
     st.x = px; st.y = py; st.vx = in.vx; st.vy = in.vy; st.mass = in.mass;
@@ -380,11 +402,13 @@ __device__ __forceinline__ int couple_pair(const CoupleIn &in, const CoupleParam
         t.ax = -(dirx * pen * cp.relaxFactor);                 // acx -= ...
         t.ay = -(diry * pen * cp.relaxFactor);
     } else if (rb.shape == 1) {
-        if (rb.nv < 3 || !pip_rec(px, py, rb.nv, vt)) return 0;
+        if (rb.nv < 3 || !pip_rec(px, py, rb.nv, vt)) { CPT(1); return 0; }
+        CPT(1);
         float cx, cy;
         closest_rec(px, py, rb.nv, vt, cx, cy);
         const float dx = px - cx, dy = py - cy;
         const float d0 = sqrtf(dx * dx + dy * dy);
+        CPT(2);
         if (doImp) {
             float d = d0;
             if (d < cp.minPenetration) d = cp.minPenetration;
@@ -396,6 +420,7 @@ __device__ __forceinline__ int couple_pair(const CoupleIn &in, const CoupleParam
                 flags |= PT_IMP;
             }
         }
+        CPT(3);
         float d = d0, cdx = dx, cdy = dy;
         if (d < cp.minSafeDistance) { d = cp.minSafeDistance; cdx = 1.0f; cdy = 0.0f; }
         const float pen = d + cp.safetyMargin;

@@ -38,22 +38,51 @@ print("forcesGlobal blocks per sub-step", (st1["forcesGlobal"] - st0["forcesGlob
 if not ftr:
     sys.exit(0)
 L.lpe_ftrace(0, buf.ctypes.data, buf.size)
-t = buf[: nb * 8].reshape(nb, 8).astype(np.int64)
+pairs = None
+if hasattr(L, "lpe_ftrace2"):
+    L.lpe_ftrace2.argtypes = [C.c_void_p, C.c_int]
+    buf2 = np.zeros(4096 * 8, np.uint64)
+    L.lpe_ftrace2(buf2.ctypes.data, buf2.size)
+    pairs = buf2[: (nb + 512) * 8].reshape(nb + 512, 8).astype(np.int64)
+# slots: the tiles' blocks, then (round 5) the heavy tiles' quarter blocks
+# (4 x HEAVY_MAX slots after the tiles); blocks that did not run a tile leave zeros
+t = buf[: (nb + 512) * 8].reshape(nb + 512, 8).astype(np.int64)
+ran = t[:, 0] > 0
+quarters = np.nonzero(ran[nb:])[0]
+print("heavy quarter blocks", len(quarters), "tiles run by quarters", len(quarters) // 4)
+isq = np.zeros(len(ran), bool)
+isq[nb:] = True
+isq = isq[ran]
+t = t[ran]
+if pairs is not None:
+    pairs = pairs[ran] / 100.0      # us since the pair's start, max over the block's lanes
+nb = len(t)
 t0 = t[:, 0].min()
 us = lambda a, b: (t[:, b] - t[:, a]) / 100.0
 start = (t[:, 0] - t0) / 100.0
 end = (t[:, 3] - t0) / 100.0
 has2 = t[:, 2] > 0
 img = t[:, 7] < 100000
+has6 = t[:, 6] > 0
+cin = np.where(has6, us(5, 6), 0.0)
+prs = np.where(has6 & has2, us(6, 2), 0.0)
+fold = np.where(has2, us(2, 4), 0.0)
 rows = [("start", start), ("stage+cand", us(0, 1)), ("fluid loop", us(1, 5)), ("coupling", us(5, 4)),
-        ("kick+write", us(4, 3)), ("end", end), ("img L", np.where(img, t[:, 7], t[:, 7] - 100000)),
-        ("lane0 cnt", t[:, 6])]
+        ("  couple_in", cin), ("  pairs", prs), ("  fold+fin", fold),
+        ("kick+write", us(4, 3)), ("end", end), ("img L", np.where(img, t[:, 7], t[:, 7] - 100000))]
 print("kernel span us", end.max(), "blocks", nb, "image blocks", int(img.sum()))
 print("pctl        " + " ".join(f"{p:>8}" for p in ("0", "50", "90", "99", "100")))
 for name, v in rows:
     q = np.percentile(v, [0, 50, 90, 99, 100])
     print(f"{name:11s}", " ".join(f"{x:8.1f}" for x in q))
-print("slowest blocks: blk img L stage fluid couple kick end cnt geo?")
+for name, sel in (("tile blocks", ~isq), ("quarter blocks", isq)):
+    if sel.any():
+        print(f"{name:15s} n {int(sel.sum()):5d}  start pctl 0/50/90/100:",
+              " ".join(f"{x:6.1f}" for x in np.percentile(start[sel], [0, 50, 90, 100])),
+              " end:", " ".join(f"{x:6.1f}" for x in np.percentile(end[sel], [0, 50, 90, 100])))
+print("slowest blocks: blk img L stage fluid couple (in pairs fold) kick end")
 for k in np.argsort(-end)[:10]:
-    print(k, int(img[k]), t[k, 7] % 100000, round(us(0, 1)[k], 1), round(us(1, 5)[k], 1), round(us(5, 4)[k], 1),
-          round(us(4, 3)[k], 1), round(end[k], 1), t[k, 6], bool(has2[k]))
+    print(("q" if isq[k] else "") + str(k), int(img[k]), t[k, 7] % 100000, round(us(0, 1)[k], 1), round(us(1, 5)[k], 1), round(us(5, 4)[k], 1),
+          "(", round(cin[k], 1), round(prs[k], 1), round(fold[k], 1), ")", round(us(4, 3)[k], 1), round(end[k], 1),
+          "" if pairs is None else "pair stages (record, pip, closest, impulse+atomics): %s" %
+          [round(float(x), 2) for x in pairs[k, :4]])
