@@ -1997,6 +1997,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
             pool.in[threadIdx.x] = couple_in(st, cp, cp.nr > 0 && nh > 0);
             __syncthreads();
             FTR(6);
+            FTR2SET(5, total);
             // ---- the pairs (geometry and impulse in one pass: the
             // velocities are final), round robin
             for (int q = threadIdx.x; q < total; q += HB) {

@@ -21,6 +21,7 @@ __device__ unsigned long long g_ftrace2[4096 * 8];
 #define FTRCLR() do { if (g_ftrace_on && threadIdx.x == 0) for (int k_ = 0; k_ < 8; k_++) { g_ftrace[ftb * 8 + k_] = 0; g_ftrace2[ftb * 8 + k_] = 0; } } while (0)
 // the coupling pair's stages (sph_coupling.h CPT), per block
 #define FTR_PAIRS() (g_ftrace_on ? g_ftrace2 + ftb * 8 : (unsigned long long *)nullptr)
+#define FTR2SET(k, v) do { if (g_ftrace_on && threadIdx.x == 0) g_ftrace2[ftb * 8 + (k)] = (unsigned long long)(v); } while (0)
 extern "C" int lpe_ftrace2(unsigned long long *host, int n) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ftrace2), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
 }
@@ -35,6 +36,7 @@ extern "C" int lpe_ftrace(int on, unsigned long long *host, int n) {
 #define FTR(k) do {} while (0)
 #define FTRCLR() do {} while (0)
 #define FTR_PAIRS() ((unsigned long long *)nullptr)
+#define FTR2SET(k, v) do {} while (0)
 #define FTRMAX(k, v) do {} while (0)
 #endif
 

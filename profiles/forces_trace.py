@@ -55,6 +55,7 @@ isq[nb:] = True
 isq = isq[ran]
 t = t[ran]
 if pairs is not None:
+    npairs_blk = pairs[ran][:, 5].copy()
     pairs = pairs[ran] / 100.0      # us since the pair's start, max over the block's lanes
 nb = len(t)
 t0 = t[:, 0].min()
@@ -85,4 +86,8 @@ for k in np.argsort(-end)[:10]:
     print(("q" if isq[k] else "") + str(k), int(img[k]), t[k, 7] % 100000, round(us(0, 1)[k], 1), round(us(1, 5)[k], 1), round(us(5, 4)[k], 1),
           "(", round(cin[k], 1), round(prs[k], 1), round(fold[k], 1), ")", round(us(4, 3)[k], 1), round(end[k], 1),
           "" if pairs is None else "pair stages (record, pip, closest, impulse+atomics): %s" %
-          [round(float(x), 2) for x in pairs[k, :4]])
+          [round(float(x), 2) for x in pairs[k, :4]], "pairs", int(npairs_blk[k]))
+if pairs is not None:
+    has = npairs_blk > 0
+    print("blocks with coupling pairs", int(has.sum()), "pairs per block pctl 50/90/99/100:",
+          np.percentile(npairs_blk[has], [50, 90, 99, 100]).round(0).tolist() if has.any() else None)
