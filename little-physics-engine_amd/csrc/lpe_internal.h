@@ -123,6 +123,10 @@ struct SphDev {
     long ovlIdx = 0;              // scans that wrote a list (parity)
     const int32_t *ovl_cur = nullptr;   // the last hash's list
     const int32_t *ovl_pre = nullptr;   // the prelaunched sub-step's
+    // the forces pass's tile scheduling (lpe_sph.hip HeavyOut / HeavyIn)
+    int32_t *heavy = nullptr;     // [2][HEAVY_WORDS]: counts, filed tiles -- by density pass parity
+    int32_t *tileHeavy = nullptr; // per tile: its filing code, or 0
+    int heavyCur = 0;             // the parity the last density pass filed into
 };
 
 // status slots

@@ -1046,6 +1046,55 @@ __device__ void ref_cap_walk(float xi, float yi, float eps, const GridParams &g,
 // canonical one.  The plan is computed by every wave from block-uniform loads
 // (no serial section, one barrier).  A block whose neighbourhood does not fit
 // walks global memory instead.
+// Tile scheduling of the forces pass.  The rigid pile's tiles carry most of
+// the coupling pairs (up to ~1400 against none for a median tile) and denser
+// neighbour lists, so their blocks ended the launch 25-30 us after the median
+// block, each wave alone on its SIMD (a round of 256 pairs takes ~5 us,
+// latency-bound).  The density pass (same sub-step, same tiles) counts each
+// particle's coupling pairs (the forces pass's AABB test on its rigid-bin
+// candidates), finds the tile's quartiles of pairs over its slots, and files
+// the tile by its total T:
+//   T >= QUARTER_PAIRS: four part blocks (at most QUARTER_MAX tiles),
+//   T >= HALF_PAIRS:    two part blocks  (at most HALF_MAX tiles),
+//   T > 0:              one block, run whole (at most COUPLED_MAX tiles),
+// a filing that finds its class full trying the next.  A part block takes
+// the slots between two of the tile's pair quartiles (so the parts share the
+// pairs, not the slots, evenly), stages the tile's image and runs its slots
+// as a whole block would.  The forces grid is [quarters][halves][coupled]
+// [every tile in order]: the costly blocks are dispatched first and the
+// late-dispatched ones (beyond the resident blocks) are light tiles; a tile's
+// own block exits when the tile was filed.  Every particle's arithmetic is
+// the same (the fold order of its pairs is its own list's), so the results
+// are bit-identical.  The lists alternate between two buffers by density
+// pass; the forces pass that reads one clears the other's counts.  A filed
+// block runs its tile only if the tile's flag holds its filing code and the
+// list entry there is the tile (a stale entry is skipped: the tile's own
+// block runs it), so every tile runs exactly once whatever the lists hold.
+// LPE_NO_HEAVY=1: off (A/B).
+static constexpr int QUARTER_PAIRS = 512, HALF_PAIRS = 256;
+static constexpr int QUARTER_MAX = 128, HALF_MAX = 160, COUPLED_MAX = 160;
+static constexpr int FILED_MAX = QUARTER_MAX + HALF_MAX + COUPLED_MAX;
+// list: [0..2] the counts by class; then per filing code c (quarters c = 1 ..,
+// halves c = QUARTER_MAX + 1 .., coupled c = QUARTER_MAX + HALF_MAX + 1 ..)
+// two words at list[2 + 2c]: the tile, and its quartile slots (9 bits each)
+static constexpr int HEAVY_WORDS = 4 + 2 * FILED_MAX;
+struct HeavyOut {             // k_density<true>: where it files the heavy tiles
+    int32_t *list;            //   [HEAVY_WORDS] of this pass's parity (null: off)
+    int32_t *tile;            //   per tile: its list position + 1, or 0
+    const int32_t *rbinStart; //   the rigid bins (candidates per bin)
+    const float4 *rbinAabb;   //   and their AABBs in bin order (the pairs: AABB hits)
+    float bcs;
+    int bx0, by0, bW, bH;
+};
+struct HeavyIn {              // k_forces_couple: the lists the density pass filed
+    const int32_t *list;      //   (null: off)
+    const int32_t *tile;
+    int32_t *clearNext;       //   the other parity's list (its counts are cleared)
+};
+// the forces grid's filed blocks ahead of the tiles' own
+static constexpr int QUARTER_BLOCKS = 4 * QUARTER_MAX, HALF_BLOCKS = 2 * HALF_MAX;
+static constexpr int HEAVY_HEAD = QUARTER_BLOCKS + HALF_BLOCKS + COUPLED_MAX;
+
 static constexpr int HB = 256;            // slots (threads) per staged block (4 waves: hood_stage)
 static constexpr int HCAP = 1536;         // records staged per block (6 per thread)
 static constexpr int HBND = 1280;         // staged cell boundaries per block (5 per thread)
@@ -1237,8 +1286,10 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
           const int32_t *__restrict__ start, const float4 *__restrict__ nbA, float2 *__restrict__ nbB,
           float *__restrict__ rho, float *__restrict__ pr, uint4 *__restrict__ nlist,
           int32_t *__restrict__ ncount, int32_t *__restrict__ status, const int32_t *__restrict__ sid,
-          const int32_t *__restrict__ refInv, const int32_t *__restrict__ ovl, Hood *__restrict__ fplans) {
+          const int32_t *__restrict__ refInv, const int32_t *__restrict__ ovl, Hood *__restrict__ fplans,
+          HeavyOut ho) {
     __shared__ float4 lrec[HCAP + 4];                     // + 4: the span walk reads up to 3 past a span
+    __shared__ int hcand[5];                              // (NL, ho.list: the waves' coupling pairs; quartiles)
     __shared__ int lbnd[HBND];
     __shared__ uint4 lnl[NL ? 2 * HB : 1];                // per thread: a ring of two groups of 8 entries
     // (a slab rank's grid is sized by its slot capacity: the XCD runs are laid
@@ -1258,6 +1309,7 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
         if (threadIdx.x == 0) {
             hd = p;
             if (NL && fplans) fplans[lb] = p;
+            hcand[4] = 0;
         }
     }
     __syncthreads();
@@ -1394,6 +1446,60 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
                         [&](int k, const float4 &o) {
                             if (term(o, true) && NL && k != s) emit(k - s, k - s >= -32768 && k - s <= 32767);
                         });
+    }
+    if (NL && ho.list) {
+        // the tile's rigid-bin candidates (the forces pass's coupling work):
+        // a heavy or coupled tile is filed for the forces pass (HeavyOut)
+        int c = 0;
+        if (live) {
+            const float fbx = fminf(fmaxf(floorf(xi / ho.bcs) - (float)ho.bx0, 0.f), (float)(ho.bW - 1));
+            const float fby = fminf(fmaxf(floorf(yi / ho.bcs) - (float)ho.by0, 0.f), (float)(ho.bH - 1));
+            const int bin = (int)fby * ho.bW + (int)fbx;
+            const int k0 = ho.rbinStart[bin], k1 = ho.rbinStart[bin + 1];
+            for (int k = k0; k < k1; k += 4) {           // (the forces pass's phase-0 test, counted)
+                float4 bb[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) bb[u] = ho.rbinAabb[min(k + u, k1 - 1)];
+#pragma unroll
+                for (int u = 0; u < 4; u++) c += (k + u < k1 && aabb_holds(bb[u], xi, yi)) ? 1 : 0;
+            }
+        }
+        int inc = c;                                     // the pairs of the block's slots up to this one
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const int v = __shfl_up(inc, off);
+            if (lane_id() >= off) inc += v;
+        }
+        const int w = threadIdx.x >> 6;
+        if (lane_id() == 63) hcand[w] = inc;
+        __syncthreads();
+        for (int u = 0; u < w; u++) inc += hcand[u];
+        const int T = hcand[0] + hcand[1] + hcand[2] + hcand[3];
+        // the quartiles: the slot after the one whose pairs reach j T / 4
+        for (int j = 1; j < 4; j++)
+            if (c && (inc - c) * 4 < j * T && j * T <= inc * 4)
+                atomicOr(&hcand[4], ((int)threadIdx.x + 1) << (9 * (j - 1)));
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int code = 0;
+            if (T >= QUARTER_PAIRS) {
+                const int t = atomicAdd(&ho.list[0], 1);
+                if (t < QUARTER_MAX) code = 1 + t;
+            }
+            if (!code && T >= HALF_PAIRS) {
+                const int t = atomicAdd(&ho.list[1], 1);
+                if (t < HALF_MAX) code = QUARTER_MAX + 1 + t;
+            }
+            if (!code && T > 0) {
+                const int t = atomicAdd(&ho.list[2], 1);
+                if (t < COUPLED_MAX) code = QUARTER_MAX + HALF_MAX + 1 + t;
+            }
+            if (code) {
+                ho.list[2 + 2 * code] = lb;
+                ho.list[3 + 2 * code] = hcand[4];
+            }
+            ho.tile[lb] = code;
+        }
     }
     if (!live) return;
     if (NL) {
@@ -1746,20 +1852,57 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                 const int32_t *__restrict__ rbinStart, const int32_t *__restrict__ rbinList,
                 const float4 *__restrict__ rbinAabb,
                 unsigned long long *__restrict__ acq,
-                int32_t *__restrict__ status, KickNext kn, const Hood *__restrict__ fplans) {
+                int32_t *__restrict__ status, KickNext kn, const Hood *__restrict__ fplans, HeavyIn hv) {
     // plain block order (blocks go round robin over the XCDs): the costly
     // blocks, the particles in and around the rigid pile, are one spatial
-    // run that an XCD-contiguous mapping (xcd_block) would put on one XCD
-    const int lb = sp.chunk > 0 ? xcd_chunk_block(sp.nblk, sp.chunk) : (int)blockIdx.x;
-    if (lb < 0) return;                       // (padding of the chunked grid)
-    const int ftb = lb;                       // (trace builds: the block's stamp slots, cleared per launch)
+    // run that an XCD-contiguous mapping (xcd_block) would put on one XCD.
+    // With tile scheduling (HeavyIn) the grid is [heavy parts][coupled][tiles].
+    const int nq = hv.list ? HEAVY_HEAD : 0;
+    const int bq = (int)blockIdx.x;
+    int slo = 0, shi = HB;                    // the block's slots of its tile: [s0 + slo, s0 + shi)
+    int lb, pb;                               // the tile; the block's bbox partial slot
+    if (bq < nq) {
+        int code, part, nparts;
+        if (bq < QUARTER_BLOCKS) {
+            code = 1 + bq / 4; part = bq % 4; nparts = 4;
+        } else if (bq < QUARTER_BLOCKS + HALF_BLOCKS) {
+            code = QUARTER_MAX + 1 + (bq - QUARTER_BLOCKS) / 2; part = (bq - QUARTER_BLOCKS) % 2; nparts = 2;
+        } else {
+            code = QUARTER_MAX + HALF_MAX + 1 + (bq - QUARTER_BLOCKS - HALF_BLOCKS); part = 0; nparts = 1;
+        }
+        pb = sp.nblk + bq;
+        lb = hv.list[2 + 2 * code];
+        if (lb < 0 || lb >= sp.nblk || hv.tile[lb] != code) {     // (no such tile this sub-step)
+            if (kn.on && threadIdx.x == 0) kn.bboxPart[pb] = make_float4(1e30f, -1e30f, 1e30f, -1e30f);
+            return;
+        }
+        if (nparts > 1) {
+            const int qs = hv.list[3 + 2 * code];
+            const int step = 4 / nparts;      // the part's quartile bounds j0 = step part, j1 = j0 + step
+            const int j0 = step * part, j1 = j0 + step;
+            slo = j0 == 0 ? 0 : (qs >> (9 * (j0 - 1))) & 511;
+            shi = j1 == 4 ? HB : (qs >> (9 * (j1 - 1))) & 511;
+        }
+    } else {
+        lb = sp.chunk > 0 ? xcd_chunk_block(sp.nblk, sp.chunk) : bq - nq;
+        if (lb < 0) return;                   // (padding of the chunked grid)
+        pb = lb;
+    }
+    const int ftb = pb;                       // (trace builds: the block's stamp slots, cleared per launch)
     (void)ftb;
     FTRCLR();
-    if (sp.mergePre && lb == 0 && threadIdx.x == 0) merge_prestats_dev(status, sp.mergePre);   // (before the kick's reset)
+    if (bq >= nq && lb == 0 && threadIdx.x == 0) {
+        if (sp.mergePre) merge_prestats_dev(status, sp.mergePre);
+        if (kn.on && kn.fk.on) status[ST_NOT_INSERTED] = 0;       // (k_scan_rows adds)
+        if (hv.clearNext) {                   // (the next density pass's lists)
+            hv.clearNext[0] = 0; hv.clearNext[1] = 0; hv.clearNext[2] = 0;
+        }
+    }
     const int nn = sp.nptr ? *sp.nptr : sp.n;
     const int s0 = lb * HB, s1 = min(s0 + HB, nn);
-    if (s0 >= s1) {
-        if (kn.on && threadIdx.x == 0) kn.bboxPart[lb] = make_float4(1e30f, -1e30f, 1e30f, -1e30f);
+    if (s0 >= s1 || (bq >= nq && hv.list && hv.tile[lb] > 0 && hv.list[2 + 2 * hv.tile[lb]] == lb)) {
+        // (past the slots in use, or a tile a filed block runs)
+        if (kn.on && threadIdx.x == 0) kn.bboxPart[pb] = make_float4(1e30f, -1e30f, 1e30f, -1e30f);
         return;
     }
     FTR(0);
@@ -1776,8 +1919,8 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     const float cs = g.cellSize;
     // every lane stays to the end (the coupling pairs are shared by the
     // block); lanes past the last slot and ghost slots only join the barriers
-    const int s = s0 + threadIdx.x;
-    bool live = s < s1;
+    const int s = s0 + slo + (int)threadIdx.x;
+    bool live = s < s1 && (int)threadIdx.x < shi - slo;
     const int out = s;                        // P slot written (P is kept in the sorted order)
     const int sl = live ? s : s0;
     const float4 meA = nbA[sl], meB = nbB[sl];
@@ -2037,7 +2180,6 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         int rowBase = 0;
         if (kn.fk.on) {
             if (threadIdx.x < 8) ltab[threadIdx.x] = 0;
-            if (lb == 0 && threadIdx.x == 0) status[ST_NOT_INSERTED] = 0;   // (k_scan_rows adds)
             rowBase = (__float_as_int(nbA[s0].w) >> 17) - 3;
         }
         float px = 0.f, py = 0.f, hx = 0.f, hy = 0.f;
@@ -2072,7 +2214,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
                 else atomicAdd(&kn.fk.rowtot[ky], len);
             }
         }
-        bbox_partial(mnx, mxx, mny, mxy, kn.bboxPart + lb);   // (a block barrier)
+        bbox_partial(mnx, mxx, mny, mxy, kn.bboxPart + pb);   // (a block barrier)
         if (kn.fk.on && threadIdx.x < 8) {
             const int v = ltab[threadIdx.x];
             if (v) atomicAdd(&kn.fk.rowtot[rowBase + threadIdx.x], v);
@@ -2517,7 +2659,7 @@ static void sph_free(SphDev &d) {
     void *ptrs[] = {d.ovl, d.rho, d.pr, d.rhoN, d.prN, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.refInv, d.stage, d.count, d.start, d.cursor,
                     d.rowtot, d.bucket, d.bovf,
                     d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.raabb, d.accum, d.acq, d.rbinStart, d.rgrid, d.rmax,
-                    d.rbinList, d.rbinCount, d.coupleBody, d.plans, d.fplans};
+                    d.rbinList, d.rbinCount, d.coupleBody, d.plans, d.fplans, d.heavy, d.tileHeavy};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     hipEvent_t evs[] = {d.preReady, d.preDone, d.fbgDone};
     for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
@@ -2781,7 +2923,16 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     LPE_HIP(ctx, hipMemsetAsync(d.bovf, 0, sizeof(int32_t) * 2 * (4 + 4 * N), ctx->stream));
 
     // bbox partials: the kick's blocks, or the forces pass's when it kicks the next sub-step
-    LPE_HIP(ctx, hipMalloc((void **)&d.bboxPart, sizeof(float4) * std::max<size_t>(MAX_KICK_BLOCKS, (N + HB - 1) / HB)));
+    LPE_HIP(ctx, hipMalloc((void **)&d.bboxPart, sizeof(float4) * std::max<size_t>(MAX_KICK_BLOCKS,
+                                                                                    (N + HB - 1) / HB + HEAVY_HEAD)));
+    // heavy tiles of the forces pass: two lists by parity, a flag per tile
+    if (d.heavy) (void)hipFree(d.heavy);
+    if (d.tileHeavy) (void)hipFree(d.tileHeavy);
+    d.heavy = d.tileHeavy = nullptr;
+    LPE_HIP(ctx, hipMalloc((void **)&d.heavy, sizeof(int32_t) * 2 * HEAVY_WORDS));
+    LPE_HIP(ctx, hipMemsetAsync(d.heavy, 0, sizeof(int32_t) * 2 * HEAVY_WORDS, ctx->stream));
+    LPE_HIP(ctx, hipMalloc((void **)&d.tileHeavy, sizeof(int32_t) * ((N + HB - 1) / HB)));
+    LPE_HIP(ctx, hipMemsetAsync(d.tileHeavy, 0, sizeof(int32_t) * ((N + HB - 1) / HB), ctx->stream));
     d.cap_n = n;
     if (!d.ovl) {
         LPE_HIP(ctx, hipMalloc((void **)&d.ovl, sizeof(int32_t) * 2 * OVL_WORDS));
@@ -3156,6 +3307,18 @@ static Hood *sph_fplans(SphDev &d) {
     return off ? nullptr : (Hood *)d.fplans;
 }
 
+// heavy tiles of the forces pass (HeavyOut / HeavyIn): with at least
+// HEAVY_MIN_RIGIDS coupling rigids and their bins, in plain block order
+// (LPE_NO_HEAVY=1: off).  A handful of rigids -- the four walls of a dam
+// break -- never make a tile heavy, and the part blocks' empty launches and
+// the count in the density pass would only cost there.
+static constexpr int HEAVY_MIN_RIGIDS = 64;
+static bool sph_heavy_on(const SphDev &d) {
+    static const bool off = getenv("LPE_NO_HEAVY") != nullptr;
+    static const bool chunked = getenv("LPE_FORCES_CHUNK") != nullptr && atoi(getenv("LPE_FORCES_CHUNK")) > 0;
+    return !off && !chunked && d.nr >= HEAVY_MIN_RIGIDS && d.rbinStart && d.heavy && d.tileHeavy;
+}
+
 static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr, float *rho, float *pr, bool nl = true) {
     SphDev &d = ctx->sph;
     const lpe_fluid_config &c = d.cfg;
@@ -3176,16 +3339,26 @@ static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr, float *rho, flo
                    d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)nullptr, rho, pr, d.stat_cur,
                    (const Hood *)d.plans);
     }
-    else if (nl)
+    else if (nl) {
+        HeavyOut ho{};
+        if (sph_heavy_on(d)) {
+            d.heavyCur ^= 1;                          // (this pass's list; the forces pass reads it)
+            ho.list = d.heavy + (size_t)d.heavyCur * HEAVY_WORDS;
+            ho.tile = d.tileHeavy;
+            ho.rbinStart = d.rbinStart;
+            ho.rbinAabb = rbin_aabb(d);
+            ho.bcs = d.bcs; ho.bx0 = d.bx0; ho.by0 = d.by0; ho.bW = d.bW; ho.bH = d.bH;
+        }
         LPE_KERNEL(ctx, "k_density", k_density<true>, dim3(xcd_grid(nblk(n, HB))), dim3(HB), 0, ctx->stream, n,
                    nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
                    c.restDensity, d.W, d.H, d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)d.nbB,
-                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d), d.ovl_cur, sph_fplans(d));
-    else
+                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d), d.ovl_cur, sph_fplans(d), ho);
+    } else
         LPE_KERNEL(ctx, "k_density", k_density<false>, dim3(xcd_grid(nblk(n, HB))), dim3(HB), 0, ctx->stream, n,
                    nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
                    c.restDensity, d.W, d.H, d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)d.nbB,
-                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d), d.ovl_cur, (Hood *)nullptr);
+                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d), d.ovl_cur, (Hood *)nullptr,
+                   HeavyOut{});
     LPE_CHECK_LAUNCH(ctx, "k_density");
     return LPE_OK;
 }
@@ -3419,7 +3592,11 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
     }();
     sp.nblk = fblocks;
     sp.chunk = fchunk;
-    const int fgrid = fchunk > 0 ? xcd_chunk_grid(fblocks, fchunk) : fblocks;
+    // tile scheduling: the filed blocks head the grid and leave their own bbox
+    // partials after the tiles' (the scan reads fblocks + HEAVY_HEAD)
+    const bool heavy = sph_heavy_on(d) && fchunk == 0;
+    const int nq = heavy ? HEAVY_HEAD : 0;
+    const int fgrid = (fchunk > 0 ? xcd_chunk_grid(fblocks, fchunk) : fblocks) + nq;
     int kicked = 0;
     for (int step = 0; step < c.numSubSteps; step++) {
         if (step == 0 && pre) {
@@ -3442,7 +3619,7 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
             kn.fk = sph_fastkick(ctx, sph_rowscan_ok(d));
             kn.sk = slab_kick(d);
         }
-        kicked = kn.on ? fblocks : 0;
+        kicked = kn.on ? fblocks + nq : 0;
         sp.mergePre = (step == 0 && pre) ? d.status + ST_COUNT : nullptr;
         if (sp.mergePre && sp.refInv) {
             LPE_KERNEL(ctx, "k_merge_prestats", k_merge_prestats, dim3(1), dim3(64), 0, s, d.status, sp.mergePre);
@@ -3453,7 +3630,10 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
                            (step == 0 && pre) ? d.gp + 1 : d.gp,
                            d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart, d.rbinList,
                            rbin_aabb(d),
-                           d.acq, d.status, kn, (const Hood *)sph_fplans(d));
+                           d.acq, d.status, kn, (const Hood *)sph_fplans(d),
+                           heavy ? HeavyIn{d.heavy + (size_t)d.heavyCur * HEAVY_WORDS, d.tileHeavy,
+                                           d.heavy + (size_t)(1 - d.heavyCur) * HEAVY_WORDS}
+                                 : HeavyIn{});
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
         if (sh) sh->cur = 1 - sh->cur;               // P's slots are now the ones this pass wrote
         if (hook) {                                  // (lpe_world_tick: the rigid detection)

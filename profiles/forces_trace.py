@@ -38,21 +38,24 @@ print("forcesGlobal blocks per sub-step", (st1["forcesGlobal"] - st0["forcesGlob
 if not ftr:
     sys.exit(0)
 L.lpe_ftrace(0, buf.ctypes.data, buf.size)
+W = 1024        # slots past the tiles' own: the filed blocks (QUARTER_BLOCKS, HALF_BLOCKS, COUPLED_MAX)
+REG = (("quarter part blocks", 0, 512), ("half part blocks", 512, 832), ("coupled whole blocks", 832, 992))
 pairs = None
 if hasattr(L, "lpe_ftrace2"):
     L.lpe_ftrace2.argtypes = [C.c_void_p, C.c_int]
     buf2 = np.zeros(4096 * 8, np.uint64)
     L.lpe_ftrace2(buf2.ctypes.data, buf2.size)
-    pairs = buf2[: (nb + 512) * 8].reshape(nb + 512, 8).astype(np.int64)
-# slots: the tiles' blocks, then (round 5) the heavy tiles' quarter blocks
-# (4 x HEAVY_MAX slots after the tiles); blocks that did not run a tile leave zeros
-t = buf[: (nb + 512) * 8].reshape(nb + 512, 8).astype(np.int64)
+    pairs = buf2[: (nb + W) * 8].reshape(nb + W, 8).astype(np.int64)
+# slots: the tiles' blocks, then (round 5) the filed blocks by class; blocks
+# that did not run a tile leave zeros
+t = buf[: (nb + W) * 8].reshape(nb + W, 8).astype(np.int64)
 ran = t[:, 0] > 0
-quarters = np.nonzero(ran[nb:])[0]
-print("heavy quarter blocks", len(quarters), "tiles run by quarters", len(quarters) // 4)
-isq = np.zeros(len(ran), bool)
-isq[nb:] = True
-isq = isq[ran]
+region = np.full(len(ran), -1)
+for r, (name, a, b) in enumerate(REG):
+    region[nb + a: nb + b] = r
+    print(name, int(ran[nb + a: nb + b].sum()))
+isq = (region >= 0)[ran]
+region = region[ran]
 t = t[ran]
 if pairs is not None:
     npairs_blk = pairs[ran][:, 5].copy()
@@ -76,9 +79,9 @@ print("pctl        " + " ".join(f"{p:>8}" for p in ("0", "50", "90", "99", "100"
 for name, v in rows:
     q = np.percentile(v, [0, 50, 90, 99, 100])
     print(f"{name:11s}", " ".join(f"{x:8.1f}" for x in q))
-for name, sel in (("tile blocks", ~isq), ("quarter blocks", isq)):
+for name, sel in [("tile blocks", ~isq)] + [(REG[r][0], region == r) for r in range(len(REG))]:
     if sel.any():
-        print(f"{name:15s} n {int(sel.sum()):5d}  start pctl 0/50/90/100:",
+        print(f"{name:20s} n {int(sel.sum()):5d}  start pctl 0/50/90/100:",
               " ".join(f"{x:6.1f}" for x in np.percentile(start[sel], [0, 50, 90, 100])),
               " end:", " ".join(f"{x:6.1f}" for x in np.percentile(end[sel], [0, 50, 90, 100])))
 print("slowest blocks: blk img L stage fluid couple (in pairs fold) kick end")
