@@ -382,30 +382,37 @@ def rigid_microbench(lpe, device, reps=10):
     pile, the committed fixture tests/golden/pile_M_t250.npz, re-uploaded
     before every repetition: the same ~10k pairs / ~30k contacts every run, so
     the rigid kernels can be compared across runs (the live pile of the tick
-    bench drifts with float-atomic summation order)."""
+    bench drifts with float-atomic summation order).  `jacobi`: the same with
+    the opt-in Jacobi contact solver (pgsMode = LPE_PGS_JACOBI, 10 iterations)."""
     z = np.load(os.path.join(ROOT, "tests", "golden", "pile_M_t250.npz"))
-    ctx = lpe.Context(device)
-    try:
-        ctx.rigid_set_config(lpe.rigid_config(universe=32.0))
-        ctx.rigid_upload(z["bodies"], z["verts"])
-        st = ctx.rigid_step()                       # warm
-        ctx.timing(1)
-        ctx.timing_reset()
-        for _ in range(reps):
+    names = ("k_bg_key", "k_bg_pairs", "k_narrow", "k_pair_colour", "k_pgs_colour", "k_pos_colour",
+             "k_stripe_pairs", "k_stripe_setup", "k_group_colour", "k_stripe_layout", "k_stripe_fill",
+             "k_pgs_stripes", "k_pos_stripes", "k_pgs_jacobi")
+
+    def run(mode):
+        ctx = lpe.Context(device)
+        try:
+            ctx.rigid_set_config(lpe.rigid_config(universe=32.0, pgsMode=mode))
             ctx.rigid_upload(z["bodies"], z["verts"])
-            ctx.rigid_step(stats=False)
-        t = ctx.timing_read()
-        ctx.timing(0)
-    finally:
-        ctx.close()
-    us = {k: round(v[0] / max(v[1], 1) * 1e3, 1) for k, v in t.items()}
-    step = sum(v[0] for v in t.values()) / reps * 1e3
+            st = ctx.rigid_step()                       # warm
+            ctx.timing(1)
+            ctx.timing_reset()
+            for _ in range(reps):
+                ctx.rigid_upload(z["bodies"], z["verts"])
+                ctx.rigid_step(stats=False)
+            t = ctx.timing_read()
+            ctx.timing(0)
+        finally:
+            ctx.close()
+        us = {k: round(v[0] / max(v[1], 1) * 1e3, 1) for k, v in t.items()}
+        step = sum(v[0] for v in t.values()) / reps * 1e3
+        return st, round(step, 1), {k: us[k] for k in names if k in us}
+
+    st, step, kus = run(lpe.PGS_GAUSS_SEIDEL)
+    _, jstep, jus = run(lpe.PGS_JACOBI)
     return dict(fixture="tests/golden/pile_M_t250.npz", pairs=st["pairs"], contacts=st["contacts"],
-                colours=st["pgsLevels"], colour_rounds=st["colourRounds"], reps=reps, step_kernels_us=round(step, 1),
-                kernels_us={k: us[k] for k in ("k_bg_key", "k_bg_pairs", "k_narrow", "k_pair_colour", "k_pgs_colour",
-                                               "k_pos_colour", "k_stripe_pairs", "k_stripe_setup",
-                                               "k_group_colour", "k_stripe_layout", "k_stripe_fill", "k_pgs_stripes",
-                                               "k_pos_stripes") if k in us})
+                colours=st["pgsLevels"], colour_rounds=st["colourRounds"], reps=reps, step_kernels_us=step,
+                kernels_us=kus, jacobi=dict(step_kernels_us=jstep, kernels_us=jus))
 
 
 def bh_bench(lpe, scenes, device, reps=5):
@@ -1050,6 +1057,15 @@ def main():
         w = timed_windows(ctx, dt_tick, args.steps / elapsed, nwin=3, min_s=1.0)
         ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP if capped else 0)
         line["unbounded_cells_mode" if capped else "ref_cell_cap_mode"] = dict(ticks_per_s=w["median"], windows=w)
+        # the opt-in Jacobi contact solver on the same live scene (after the
+        # timed windows: it changes the physics, not the reference's PGS)
+        ctx.rigid_set_config(lpe.rigid_config(universe=s["U"], pgsMode=lpe.PGS_JACOBI))
+        w = timed_windows(ctx, dt_tick, args.steps / elapsed, nwin=3, min_s=1.0)
+        ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+        line["pgs_jacobi_mode"] = dict(ticks_per_s=w["median"], windows=w,
+                                       note="opt-in Jacobi contact solver (pgsMode = LPE_PGS_JACOBI, 10 "
+                                            "iterations), timed on the live scene after the windows above; "
+                                            "not the reference's arithmetic (tests/test_jacobi_gpu.py)")
         line["configs"] = config_lines(lpe, scenes, local, dt_tick, not args.no_cpu_baseline)
     if world == 1 and not args.no_density_microbench:
         line["density_microbench"] = density_microbench(lpe, scenes, local)

@@ -230,8 +230,16 @@ typedef struct lpe_rigid_config {
     double linearSleepThreshold;  /* 0.5   (SleepConfig)                       */
     double angularSleepThreshold; /* 0.5                                       */
     int32_t sleepFramesThreshold; /* 60                                        */
-    int32_t pad;
+    int32_t pgsMode;              /* LPE_PGS_GAUSS_SEIDEL (0, default): the
+                                   * reference's sequential PGS in the canonical
+                                   * striped order; LPE_PGS_JACOBI (1): opt-in
+                                   * parallel Jacobi solve (mass-split contacts,
+                                   * pgsIterations iterations) -- not the
+                                   * reference's arithmetic, checked by the LCP
+                                   * invariants and its own restatement */
 } lpe_rigid_config;
+#define LPE_PGS_GAUSS_SEIDEL 0
+#define LPE_PGS_JACOBI 1
 
 typedef struct lpe_ctx lpe_ctx;
 
@@ -384,6 +392,12 @@ int  lpe_rigid_buffer_info(lpe_ctx *ctx, int *pairs, int *contacts, int *regrows
 /* Colour of each pair of the last lpe_rigid_step (-1: pair without contacts),
  * for the parity harness; cap entries at most, *ncolours the colour count. */
 int  lpe_rigid_download_colours(lpe_ctx *ctx, int cap, int32_t *pair_colour, int32_t *ncolours);
+/* Accumulated impulses of the last lpe_rigid_step's contact solve, per
+ * contact in lpe_rigid_download_contacts order: lamN the normal row's
+ * (>= 0), lamF the friction row's (|lamF| <= frictionCoeff * lamN) --
+ * ContactRows::normal / ::friction .lambda (contact_solver.cpp:399-437),
+ * which the reference keeps inside solveLcpPgs.  cap entries at most. */
+int  lpe_rigid_download_impulses(lpe_ctx *ctx, int cap, float *lamN, float *lamF, int32_t *nc);
 /* Same with caller-supplied orders (parity mode): `pairs` (np body-index
  * pairs) replaces the broadphase and fixes the narrowphase / position-solver
  * order; `pgs_order` (NULL = contact order) is the PGS contact visiting order,

@@ -1684,10 +1684,11 @@ __global__ void k_prep_items(const int32_t *__restrict__ ncptr, const int32_t *_
                              float4 *__restrict__ rowR, int2 *__restrict__ rowAB, float4 *__restrict__ rowM,
                              int32_t *__restrict__ sItemA, int32_t *__restrict__ sItemB, PosRows out,
                              int32_t *__restrict__ inContact, int32_t *__restrict__ inPos, double baumgarte,
-                             double slop) {
+                             double slop, int32_t *__restrict__ rowOf) {
     const int t = blockIdx.x * RTPB + threadIdx.x;
     if (t >= *ncptr) return;
     const lpe_contact c = cs[order[t]];
+    rowOf[order[t]] = t;                          // (the Jacobi solver reads the rows by contact)
     const lpe_body A = bodies[c.a], B = bodies[c.b];
     inContact[c.a] = 1;
     inContact[c.b] = 1;
@@ -2898,6 +2899,11 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
         };
         stripe_sweeps(sb, v, iters, base, sb.sflag, sb.sflag + STRIPES_MAX / 2, lv, sb.gvel, fault, solve, 0,
                       single, phase);
+        __syncthreads();
+        for (int r = threadIdx.x; r < NR; r += STPB) {    // (the impulses, lpe_rigid_download_impulses)
+            const int g = r < v.nRA ? v.rA0 + r : v.rB0 + (r - v.nRA);
+            lamN[g] = ln[r]; lamF[g] = lf[r];
+        }
     } else {
         __syncthreads();
         const bool single = stripe_single_wave(sb, v, nullptr);
@@ -2943,6 +2949,225 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
             bd.vy = o[1];
             if (can_rotate(bd)) bd.omega = o[2];
         }
+    }
+}
+
+// ---- opt-in Jacobi contact solver (lpe_rigid_config.pgsMode = LPE_PGS_JACOBI)
+// north_star's "Jacobi-style" parallel solve, beside the reference's
+// Gauss-Seidel (solveLcpPgs, contact_solver.cpp:381-440), which stays the
+// default.  The unit is a contact pair (narrowphase pair, its contacts in
+// narrowphase order): every pair of an iteration reads the bodies'
+// velocities of the previous iteration and runs its contacts' normal and
+// friction rows in order (the reference's sequence, :399-437) on its own copy
+// of its two bodies, whose inverse mass and inertia are scaled by the body's
+// pair count n (mass splitting: the copies' average is the body's new
+// velocity, which makes the iteration a relaxed block Jacobi that converges
+// for any contact graph).  The pair's impulses, applied with the unscaled
+// masses (applyImpulse, :315-356), are summed per body in 2^-40 fixed point
+// (int64 atomics: integer sums commute, so the result does not depend on the
+// order of the pairs or the schedule, and is bit-reproducible); the
+// iteration after reads v0 + sum.  Restated for the tests in
+// tests/jacobi_restated.py.
+//
+// One launch, a persistent grid (every block resident) with one grid barrier
+// an iteration.  Block j owns the pairs whose first contact lies in its
+// contact range (contacts of a pair are contiguous, cstart) and keeps their
+// rows -- built once, as k_prep_items builds them, with the effective masses
+// of the scaled copies -- and impulses in LDS for the whole solve; each
+// iteration touches global memory only for the body sums (two loads and one
+// atomic per body and velocity component).  The sums ping-pong between two
+// buffers, the one written by iteration k also taking the pair's iteration
+// k - 1 share, so no buffer is cleared inside the launch.
+static constexpr double JAC_SCALE = 0x1p40, JAC_INV = 0x1p-40;
+static constexpr int JAC_TPB = 256, JAC_BLOCKS_MAX = 256;
+static constexpr int JAC_CPB = 384;                  // contacts a block owns (at most, + one pair's)
+static constexpr int JAC_LDS_ROWS = JAC_CPB + MAXC;
+struct JacBufs {              // carved from one allocation (jac_bufs)
+    uint32_t *bar;            // grid barrier arrivals (zeroed per launch)
+    int32_t *cnt;             // [nb] pairs per body (zeroed per launch)
+    long long *S0, *S1;       // [3 nb] the velocity sums, ping-pong (zeroed per launch)
+    float *v0;                // [3 nb] the velocities the solve starts from
+};
+__device__ __forceinline__ void jac_grid_barrier(uint32_t *bar, uint32_t target, int32_t *fault) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");           // this wave's atomics are performed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned spins = 0;
+        while ((int)(__hip_atomic_load(bar, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) - target) < 0) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 22)) { atomicOr(fault, 4); break; }     // (never expected: every block is resident)
+        }
+    }
+    __syncthreads();
+}
+__device__ __forceinline__ float jac_vel(const float *v0, const long long *S, int k) {
+    const long long q = __hip_atomic_load(&S[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return v0[k] + (float)((double)q * JAC_INV);
+}
+__device__ __forceinline__ long long jac_fix(float x) { return __double2ll_rn((double)x * JAC_SCALE); }
+// the effective mass of a row on the scaled copies (computeEffectiveMass, :216-253)
+__device__ __forceinline__ float jac_eff(float rxA, float ryA, float rxB, float ryB, float dx, float dy, float mA,
+                                         float iA, float mB, float iB) {
+    const float rAxn = cross2f(rxA, ryA, dx, dy), rBxn = cross2f(rxB, ryB, dx, dy);
+    const float sum = mA + mB + (rAxn * rAxn) * iA + (rBxn * rBxn) * iB;
+    return (sum < 1e-12F) ? 0.F : 1.F / sum;
+}
+__device__ __forceinline__ int jac_lower_bound(const int32_t *a, int n, int v) {   // first i with a[i] >= v
+    int lo = 0, hi = n;
+    while (lo < hi) { const int m = (lo + hi) >> 1; if (a[m] < v) lo = m + 1; else hi = m; }
+    return lo;
+}
+__global__ void __launch_bounds__(JAC_TPB)
+k_pgs_jacobi(int nb, const int32_t *__restrict__ npptr, const int32_t *__restrict__ ncptr,
+             const int32_t *__restrict__ ccount, const int32_t *__restrict__ cstart,
+             const int32_t *__restrict__ rowOf, const float4 *__restrict__ rowN, const float4 *__restrict__ rowR,
+             const int2 *__restrict__ rowAB, const float4 *__restrict__ rowM, int iters, float mu,
+             float *__restrict__ lamN, float *__restrict__ lamF, lpe_body *__restrict__ bodies,
+             const int32_t *__restrict__ inContact, JacBufs jb, int32_t *__restrict__ fault) {
+    // the block's rows and pairs, resident in LDS for the whole solve.  The
+    // rows are k_prep_items's (rowOf: contact -> row), built before the
+    // position solver (running beside this kernel) moves the poses.
+    __shared__ float4 lrn[JAC_LDS_ROWS];        // dir, effN, effF (scaled copies)
+    __shared__ float4 lrr[JAC_LDS_ROWS];        // lever arms
+    __shared__ float2 llam[JAC_LDS_ROWS];       // lamN, lamF
+    __shared__ int4 lpr[JAC_LDS_ROWS];          // per pair: first row (block-local), rows, body a, body b (-1: static)
+    __shared__ float4 lps[JAC_LDS_ROWS];        // per pair: scaled inverse masses / inertias smA, siA, smB, siB
+    __shared__ float4 lpm[JAC_LDS_ROWS];        // per pair: imA, iiA, imB, iiB
+    __shared__ long long ldp[6 * JAC_LDS_ROWS]; // per pair: its share of the previous iteration
+    __shared__ int lrange[4], lnp;
+    const int np = *npptr, nc = *ncptr;
+    // the blocks in use: JAC_CPB contacts each (the grid is sized by the
+    // capacity when the count is on the device only; the others leave at
+    // once and take no part in the barriers, so they hold no CU)
+    const int G = max(1, min((int)gridDim.x, (nc + JAC_CPB - 1) / JAC_CPB));
+    if ((int)blockIdx.x >= G) return;
+    const int stride = G * JAC_TPB, t0 = (int)(blockIdx.x * JAC_TPB + threadIdx.x);
+    const int tid = (int)threadIdx.x;
+    uint32_t arrivals = 0;
+    for (int i = t0; i < nb; i += stride) {       // (k_pgs_bodies, what = 2: velocities, never moved by the position solver)
+        const lpe_body &b = bodies[i];
+        jb.v0[3 * i] = (float)b.vx; jb.v0[3 * i + 1] = (float)b.vy;
+        jb.v0[3 * i + 2] = can_rotate(b) ? (float)b.omega : 0.f;
+    }
+    // the block's pairs: first contact in [j C, (j + 1) C)
+    if (tid == 0) {
+        const int C = (nc + G - 1) / G;
+        const int p0 = jac_lower_bound(cstart, np, min(nc, (int)blockIdx.x * C));
+        const int p1 = jac_lower_bound(cstart, np, min(nc, ((int)blockIdx.x + 1) * C));
+        lrange[0] = p0; lrange[1] = p1;
+        lrange[2] = cstart[p0]; lrange[3] = cstart[p1];
+        lnp = 0;
+        if (cstart[p1] - cstart[p0] > JAC_LDS_ROWS) atomicOr(fault, 8);   // (never: C <= JAC_CPB by the grid)
+    }
+    __syncthreads();
+    const int p0 = lrange[0], p1 = lrange[1], k0 = lrange[2], k1 = min(lrange[3], k0 + JAC_LDS_ROWS);
+    // the block's pairs with contacts (any order: the result does not depend on
+    // it) and their movable bodies' pair counts
+    for (int p = p0 + tid; p < p1; p += JAC_TPB) {
+        const int n = ccount[p], c0 = cstart[p];
+        if (n == 0 || c0 + n > k1) continue;
+        const int2 ab = rowAB[rowOf[c0]];
+        if (ab.x >= 0) atomicAdd(&jb.cnt[ab.x], 1);
+        if (ab.y >= 0) atomicAdd(&jb.cnt[ab.y], 1);
+        lpr[atomicAdd(&lnp, 1)] = make_int4(c0 - k0, n, ab.x, ab.y);
+    }
+    arrivals += G;
+    jac_grid_barrier(jb.bar, arrivals, fault);
+    const int npl = lnp;
+    // the pairs' scaled copies, and the rows with their effective masses
+    for (int m = tid; m < npl; m += JAC_TPB) {
+        const int4 pr = lpr[m];
+        const float4 im = rowM[rowOf[k0 + pr.x]];
+        float fA = 1.f, fB = 1.f;
+        if (pr.z >= 0) fA = (float)__hip_atomic_load(&jb.cnt[pr.z], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (pr.w >= 0) fB = (float)__hip_atomic_load(&jb.cnt[pr.w], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const float4 sc = make_float4(fA * im.x, fA * im.y, fB * im.z, fB * im.w);
+        lpm[m] = im; lps[m] = sc;
+        for (int j = 0; j < pr.y; j++) {
+            const int l = pr.x + j, t = rowOf[k0 + l];
+            const float4 rn = rowN[t], rr = rowR[t];
+            lrn[l] = make_float4(rn.x, rn.y, jac_eff(rr.x, rr.y, rr.z, rr.w, rn.x, rn.y, sc.x, sc.y, sc.z, sc.w),
+                                 jac_eff(rr.x, rr.y, rr.z, rr.w, -rn.y, rn.x, sc.x, sc.y, sc.z, sc.w));
+            lrr[l] = rr;
+            llam[l] = make_float2(0.f, 0.f);
+        }
+    }
+    __syncthreads();
+    for (int it = 0; it < iters; it++) {
+        const long long *Sc = (it & 1) ? jb.S1 : jb.S0;
+        long long *Sn = (it & 1) ? jb.S0 : jb.S1;
+        for (int m = tid; m < npl; m += JAC_TPB) {
+            const int4 pr = lpr[m];
+            const int a = pr.z, b = pr.w;
+            const bool hasA = a >= 0, hasB = b >= 0;
+            float vxA = 0.f, vyA = 0.f, wA = 0.f, vxB = 0.f, vyB = 0.f, wB = 0.f;
+            if (hasA) { vxA = jac_vel(jb.v0, Sc, 3 * a); vyA = jac_vel(jb.v0, Sc, 3 * a + 1); wA = jac_vel(jb.v0, Sc, 3 * a + 2); }
+            if (hasB) { vxB = jac_vel(jb.v0, Sc, 3 * b); vyB = jac_vel(jb.v0, Sc, 3 * b + 1); wB = jac_vel(jb.v0, Sc, 3 * b + 2); }
+            const float4 im = lpm[m], sc = lps[m];
+            float DxA = 0.f, DyA = 0.f, DwA = 0.f, DxB = 0.f, DyB = 0.f, DwB = 0.f;
+            for (int j = 0; j < pr.y; j++) {
+                const int l = pr.x + j;
+                const float4 rn = lrn[l], rr = lrr[l];
+                float2 lam = llam[l];
+#pragma unroll
+                for (int row = 0; row < 2; row++) {
+                    const float dx = row == 0 ? rn.x : -rn.y, dy = row == 0 ? rn.y : rn.x;
+                    const float eff = row == 0 ? rn.z : rn.w;
+                    // getRelativeVelocity (:285-313) on the copies
+                    const float ax = vxA + (-rr.y) * wA, ay = vyA + rr.x * wA;
+                    const float bx = vxB + (-rr.w) * wB, by = vyB + rr.z * wB;
+                    const float vrel = (bx - ax) * dx + (by - ay) * dy;
+                    float old, lo, hi;
+                    if (row == 0) { old = lam.x; lo = 0.0f; hi = 1e20f; }
+                    else { old = lam.y; const float limit = mu * lam.x; lo = -limit; hi = limit; }
+                    float dl = -eff * (vrel + 0.0f);
+                    float nl = old + dl;
+                    if (nl < lo) nl = lo;
+                    if (nl > hi) nl = hi;
+                    dl = nl - old;
+                    if (row == 0) lam.x = nl; else lam.y = nl;
+                    if (fabsf(dl) < 1e-15F) continue;
+                    const float crossA = rr.x * dy - rr.y * dx, crossB = rr.z * dy - rr.w * dx;
+                    if (hasA) {
+                        vxA -= dx * (dl * sc.x); vyA -= dy * (dl * sc.x); wA -= crossA * dl * sc.y;
+                        DxA -= dx * (dl * im.x); DyA -= dy * (dl * im.x); DwA -= crossA * dl * im.y;
+                    }
+                    if (hasB) {
+                        vxB += dx * (dl * sc.z); vyB += dy * (dl * sc.z); wB += crossB * dl * sc.w;
+                        DxB += dx * (dl * im.z); DyB += dy * (dl * im.z); DwB += crossB * dl * im.w;
+                    }
+                }
+                llam[l] = lam;
+            }
+            const long long q[6] = {jac_fix(DxA), jac_fix(DyA), jac_fix(DwA), jac_fix(DxB), jac_fix(DyB), jac_fix(DwB)};
+#pragma unroll
+            for (int u = 0; u < 6; u++) {
+                const long long prev = it ? ldp[6 * m + u] : 0ll;
+                const int body = u < 3 ? a : b;
+#ifdef LPE_JAC_PLAIN_STORES   // (profiling only: the sums' stores without the atomics -- wrong results)
+                if (body >= 0) Sn[3 * body + (u % 3)] = q[u] + prev;
+#else
+                if (body >= 0) atomicAdd((unsigned long long *)&Sn[3 * body + (u % 3)],
+                                         (unsigned long long)(q[u] + prev));
+#endif
+                ldp[6 * m + u] = q[u];
+            }
+        }
+        arrivals += G;
+        jac_grid_barrier(jb.bar, arrivals, fault);
+    }
+    // the impulses by contact index (lpe_rigid_download_impulses)
+    for (int k = k0 + tid; k < k1; k += JAC_TPB) { lamN[k] = llam[k - k0].x; lamF[k] = llam[k - k0].y; }
+    // k_pgs_writeback (velocity fields only: the position solver writes the poses concurrently)
+    const long long *Sf = (iters & 1) ? jb.S1 : jb.S0;
+    for (int i = t0; i < nb; i += stride) {
+        if (!inContact[i]) continue;
+        lpe_body &bd = bodies[i];
+        if (infinite_mass(bd)) continue;
+        bd.vx = jac_vel(jb.v0, Sf, 3 * i);
+        bd.vy = jac_vel(jb.v0, Sf, 3 * i + 1);
+        if (can_rotate(bd)) bd.omega = jac_vel(jb.v0, Sf, 3 * i + 2);
     }
 }
 
@@ -3313,9 +3538,9 @@ int lpe_rigid_destroy_internal(lpe_ctx *ctx) {
                     d->pcursor, d->pairs, d->pairRankB, d->cslots, d->ccount, d->cstart, d->contacts,
                     d->bsum, d->order, d->rowN, d->rowR, d->rowAB, d->vel0, d->imii, d->inContact,
                     d->posState, d->posRec, d->posKeep, d->posStart, d->rowM, d->sItemA, d->sItemB,
-                    d->sVer, d->lamN, d->lamF, d->sBCount, d->sBStart, d->sBCursor, d->sEnt,
+                    d->sVer, d->lamN, d->lamF, d->rowOf, d->sBCount, d->sBStart, d->sBCursor, d->sEnt,
                     d->counts, d->pcol, d->cseg, d->cbase, d->bgCount, d->bgStart, d->bgCursor,
-                    d->bgList, d->bgKey, d->bgSpecial, d->bbits};
+                    d->bgList, d->bgKey, d->bgSpecial, d->bbits, d->jac};
     for (void *p : ptrs) if (p) (void)hipFree(p);
     if (StripeBufs *sb = (StripeBufs *)d->stripes) {
         void *sp[] = {sb->bstripe, sb->pgroup, sb->pcolg, sb->prank, sb->prowoff, sb->glist, sb->gstart, sb->gcnt,
@@ -3349,6 +3574,10 @@ extern "C" int lpe_rigid_config_default(lpe_rigid_config *c) {
 
 extern "C" int lpe_rigid_set_config(lpe_ctx *ctx, const lpe_rigid_config *cfg) {
     if (!ctx || !cfg) return LPE_ERR_ARG;
+    if (cfg->pgsMode != LPE_PGS_GAUSS_SEIDEL && cfg->pgsMode != LPE_PGS_JACOBI) {
+        ctx->err = "rigid config: pgsMode must be LPE_PGS_GAUSS_SEIDEL or LPE_PGS_JACOBI";
+        return LPE_ERR_ARG;
+    }
     RigidDev *d = rdev(ctx);
     // the cached mass checks stay valid across an unchanged config (the
     // resident host path re-sets it every tick)
@@ -3416,6 +3645,7 @@ static int rigid_alloc_contacts(lpe_ctx *ctx, RigidDev *d, int cap) {
     if ((st = rgrow(ctx, &d->posRec, K))) return st;
     if ((st = rgrow(ctx, &d->sVer, K))) return st;
     if ((st = rgrow(ctx, &d->lamN, K))) return st;
+    if ((st = rgrow(ctx, &d->rowOf, K))) return st;
     if ((st = rgrow(ctx, &d->lamF, K))) return st;
     int32_t **arrs[] = {&d->sItemA, &d->sItemB, &d->posKeep};
     for (int32_t **a : arrs) if ((st = rgrow(ctx, a, K))) return st;
@@ -3844,7 +4074,7 @@ static int colour_prep(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
                d->posState, d->inContact);
     LPE_KERNEL(ctx, "k_prep_items", k_prep_items, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->order,
                d->contacts, d->bodies, d->imii, d->posState, d->rowN, d->rowR, d->rowAB, d->rowM, d->sItemA, d->sItemB,
-               pos_rows(d), d->inContact, inPos, c.baumgarte, c.slop);
+               pos_rows(d), d->inContact, inPos, c.baumgarte, c.slop, d->rowOf);
     LPE_CHECK_LAUNCH(ctx, "solver preparation");
     return LPE_OK;
 }
@@ -3869,9 +4099,54 @@ static int colour_pos(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     return LPE_OK;
 }
 
+// the Jacobi solver's buffers (JacBufs), grown to nb bodies and nc contacts
+static JacBufs jac_bufs(RigidDev *d) {
+    const size_t nb = (size_t)d->cap_jac_nb;
+    char *p = (char *)d->jac;
+    JacBufs j;
+    j.bar = (uint32_t *)p;
+    j.cnt = (int32_t *)(p + 64);
+    j.S0 = (long long *)(p + 64 + 8 * ((4 * nb + 7) / 8));
+    j.S1 = j.S0 + 3 * nb;
+    j.v0 = (float *)(j.S1 + 3 * nb);
+    return j;
+}
+static size_t jac_zeroed_bytes(int nb) {           // bar, cnt, S0, S1: cleared before every launch
+    return 64 + 8 * ((4 * (size_t)nb + 7) / 8) + 48 * (size_t)nb;
+}
+static int jac_launch(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
+    const lpe_rigid_config &c = d->cfg;
+    // (lagged detection: the counts are on the device only, the sizes are the capacities)
+    const int nb = d->nb, nc = d->lag ? d->cap_contacts : d->last_nc;
+    if (!d->jac || nb > d->cap_jac_nb) {
+        if (d->jac) { LPE_HIP(ctx, hipStreamSynchronize(s)); (void)hipFree(d->jac); d->jac = nullptr; }
+        const int cnb = std::max(nb, d->cap_jac_nb);
+        LPE_HIP(ctx, hipMalloc(&d->jac, jac_zeroed_bytes(cnb) + 8 * ((12 * (size_t)cnb + 7) / 8)));
+        d->cap_jac_nb = cnb;
+    }
+    LPE_HIP(ctx, hipMemsetAsync(d->jac, 0, jac_zeroed_bytes(d->cap_jac_nb), s));
+    // blocks own at most JAC_CPB contacts each (their rows stay in LDS); in
+    // lagged detection nc is the capacity, and a tick with more than
+    // JAC_BLOCKS_MAX * JAC_CPB contacts raises the solver fault (counts[7])
+    if (!d->lag && nc > JAC_BLOCKS_MAX * JAC_CPB) {
+        ctx->err = "rigid solver (Jacobi): more than JAC_BLOCKS_MAX * JAC_CPB (98304) contacts";
+        return LPE_ERR_CAPACITY;
+    }
+    const int G = std::max(1, std::min(JAC_BLOCKS_MAX, (nc + JAC_CPB - 1) / JAC_CPB));
+    LPE_KERNEL(ctx, "k_pgs_jacobi", k_pgs_jacobi, dim3(G), dim3(JAC_TPB), 0, s, nb, d->counts, d->counts + 1,
+               d->ccount, d->cstart, d->rowOf, d->rowN, d->rowR, d->rowAB, d->rowM, c.pgsIterations,
+               c.frictionCoeff, d->lamN, d->lamF, d->bodies, (const int32_t *)d->inContact, jac_bufs(d),
+               d->counts + 7);
+    LPE_CHECK_LAUNCH(ctx, "pgs (Jacobi)");
+    d->lam_by_contact = true;
+    return LPE_OK;
+}
+
 static int colour_pgs(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     const lpe_rigid_config &c = d->cfg;
     const int nb = d->nb;
+    if (c.pgsMode == LPE_PGS_JACOBI) return jac_launch(ctx, d, s);
+    d->lam_by_contact = false;
     if (striped()) {
         StripeBufs *sb = stripe_bufs(ctx, d);
         if (!sb) return LPE_ERR_HIP;
@@ -4366,6 +4641,37 @@ extern "C" int lpe_rigid_download_contacts(lpe_ctx *ctx, int pair_cap, int32_t *
     if (contacts && d->last_nc > 0)
         LPE_HIP(ctx, hipMemcpyAsync(contacts, d->contacts, sizeof(lpe_contact) * std::min(contact_cap, d->last_nc), hipMemcpyDeviceToHost, s));
     LPE_HIP(ctx, hipStreamSynchronize(s));
+    return LPE_OK;
+}
+
+extern "C" int lpe_rigid_download_impulses(lpe_ctx *ctx, int cap, float *lamN, float *lamF, int32_t *nc_out) {
+    if (!ctx || cap < 0) return LPE_ERR_ARG;
+    RigidDev *d = rdev(ctx);
+    hipStream_t s = ctx->stream;
+    LPE_HIP(ctx, hipStreamSynchronize(s));
+    if (d->lag) {
+        int st = rigid_lag_drain(ctx, d);
+        if (st) return st;
+    }
+    const int nc = d->last_nc;
+    if (nc_out) *nc_out = nc;
+    if (nc <= 0 || cap <= 0 || !d->lamN) return LPE_OK;
+    // rows are in the solver's order: row t holds contact order[t] (the
+    // Jacobi solver keeps them by contact)
+    std::vector<int32_t> ord(nc);
+    for (int t = 0; t < nc; t++) ord[t] = t;
+    std::vector<float> ln(nc), lf(nc);
+    if (!d->lam_by_contact)
+        LPE_HIP(ctx, hipMemcpyAsync(ord.data(), d->order, sizeof(int32_t) * nc, hipMemcpyDeviceToHost, s));
+    LPE_HIP(ctx, hipMemcpyAsync(ln.data(), d->lamN, sizeof(float) * nc, hipMemcpyDeviceToHost, s));
+    LPE_HIP(ctx, hipMemcpyAsync(lf.data(), d->lamF, sizeof(float) * nc, hipMemcpyDeviceToHost, s));
+    LPE_HIP(ctx, hipStreamSynchronize(s));
+    for (int t = 0; t < nc; t++) {
+        const int k = ord[t];
+        if (k < 0 || k >= std::min(cap, nc)) continue;
+        if (lamN) lamN[k] = ln[t];
+        if (lamF) lamF[k] = lf[t];
+    }
     return LPE_OK;
 }
 

@@ -52,6 +52,7 @@ struct RigidDev {
     int32_t *inContact = nullptr;             // per body flags
     float4 *rowM = nullptr;                   // imA, iiA, imB, iiB
     float *lamN = nullptr, *lamF = nullptr;   // accumulated impulses per contact
+    int32_t *rowOf = nullptr;                 // canonical path: the PGS row of each contact (inverse of order)
     double *posState = nullptr;               // per body: invM, invI, flags (pos solver)
     PosRec *posRec = nullptr;                 // position-solver items
     int32_t *posKeep = nullptr, *posStart = nullptr;
@@ -113,6 +114,10 @@ struct RigidDev {
     void *stripes = nullptr;
     int cap_stripe_nb = 0, cap_stripe_pairs = 0;
     uint32_t sbase_pgs = 16, sbase_pos = 16;  // hand-over flag epochs of the two solvers
+    // opt-in Jacobi contact solver (lpe_rigid.hip JacBufs, allocated on first use)
+    void *jac = nullptr;
+    int cap_jac_nb = 0;
+    bool lam_by_contact = false;              // the last solve's lamN / lamF are by contact (Jacobi), not by row
     // the position solver runs beside the PGS on its own stream (rigid_solve)
     hipStream_t psolve = nullptr;
     hipEvent_t evFork = nullptr, evJoin = nullptr;

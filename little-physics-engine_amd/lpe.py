@@ -129,7 +129,10 @@ class RigidConfig(C.Structure):
                 ("maxAngularSpeed", C.c_double), ("marginPixels", C.c_double),
                 ("bounceDamping", C.c_double), ("maxSpeed", C.c_double),
                 ("linearSleepThreshold", C.c_double), ("angularSleepThreshold", C.c_double),
-                ("sleepFramesThreshold", C.c_int32), ("pad", C.c_int32)]
+                ("sleepFramesThreshold", C.c_int32), ("pgsMode", C.c_int32)]
+
+
+PGS_GAUSS_SEIDEL, PGS_JACOBI = 0, 1     # lpe_rigid_config.pgsMode
 
 
 def rigid_config(universe=6.0, pgs_iterations=10, **kw) -> RigidConfig:
@@ -197,6 +200,7 @@ SIGNATURES = {
     "lpe_rigid_download_contacts": ([C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_void_p,
                                      _IP, _IP], C.c_int),
     "lpe_rigid_download_colours": ([C.c_void_p, C.c_int, _IP, _IP], C.c_int),
+    "lpe_rigid_download_impulses": ([C.c_void_p, C.c_int, _FP, _FP, _IP], C.c_int),
     "lpe_rigid_reserve": ([C.c_void_p, C.c_int, C.c_int], C.c_int),
     "lpe_rigid_buffer_info": ([C.c_void_p, _IP, _IP, _IP], C.c_int),
 }
@@ -617,6 +621,17 @@ class Context:
         self._chk(lib().lpe_rigid_download_colours(self._h, np_.value, col.ctypes.data_as(_IP),
                                                    C.byref(n)), "lpe_rigid_download_colours")
         return col[:np_.value], n.value
+
+    def rigid_impulses(self):
+        """(lamN, lamF) of the last step's contact solve, in rigid_contacts order."""
+        n = C.c_int32(0)
+        self._chk(lib().lpe_rigid_download_impulses(self._h, 0, None, None, C.byref(n)),
+                  "lpe_rigid_download_impulses")
+        ln = np.zeros(n.value, np.float32)
+        lf = np.zeros(n.value, np.float32)
+        self._chk(lib().lpe_rigid_download_impulses(self._h, n.value, _fp(ln), _fp(lf), C.byref(n)),
+                  "lpe_rigid_download_impulses")
+        return ln, lf
 
     # ---- world (resident full tick) -------------------------------------
     def world_set_coupling(self, body_index=None):
