@@ -1301,6 +1301,16 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     if (s0 >= s1) return;
     const GridParams g = *gp;
     const float cs = g.cellSize;
+    // the tile filing's candidate range (HeavyOut), loaded before the walk so
+    // that its latency hides behind it
+    int hk0 = 0, hk1 = 0;
+    if (NL && ho.list && s0 + (int)threadIdx.x < s1) {
+        const float4 m0 = nbA[s0 + threadIdx.x];
+        const float fbx = fminf(fmaxf(floorf(m0.x / ho.bcs) - (float)ho.bx0, 0.f), (float)(ho.bW - 1));
+        const float fby = fminf(fmaxf(floorf(m0.y / ho.bcs) - (float)ho.by0, 0.f), (float)(ho.bH - 1));
+        const int bin = (int)fby * ho.bW + (int)fbx;
+        hk0 = ho.rbinStart[bin]; hk1 = ho.rbinStart[bin + 1];
+    }
     __shared__ Hood hd;                                   // (LDS: the walks index it per lane)
     {
         Hood p;
@@ -1452,10 +1462,7 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
         // a heavy or coupled tile is filed for the forces pass (HeavyOut)
         int c = 0;
         if (live) {
-            const float fbx = fminf(fmaxf(floorf(xi / ho.bcs) - (float)ho.bx0, 0.f), (float)(ho.bW - 1));
-            const float fby = fminf(fmaxf(floorf(yi / ho.bcs) - (float)ho.by0, 0.f), (float)(ho.bH - 1));
-            const int bin = (int)fby * ho.bW + (int)fbx;
-            const int k0 = ho.rbinStart[bin], k1 = ho.rbinStart[bin + 1];
+            const int k0 = hk0, k1 = hk1;
             for (int k = k0; k < k1; k += 4) {           // (the forces pass's phase-0 test, counted)
                 float4 bb[4];
 #pragma unroll
