@@ -1299,6 +1299,10 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     const int nn = nptr ? *nptr : n;
     const int s0 = lb * HB, s1 = min(s0 + HB, nn);
     if (s0 >= s1) return;
+    const int dtb = NL ? lb : 4096;           // (trace builds: the tile's stamp slots; the tick's pass only)
+    (void)dtb;
+    DTRCLR();
+    DTR(0);
     const GridParams g = *gp;
     const float cs = g.cellSize;
     // the tile filing's candidate range (HeavyOut), loaded before the walk so
@@ -1323,6 +1327,8 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
         }
     }
     __syncthreads();
+    DTR(1);
+    DTRSET(6, hd.L);
     // the list as LDS indices of the forces pass's image (block-uniform)
     const bool lidx = NL && fplans && hd.ok && hd.L <= FCAP;
     // every lane stays to the end (the span walk's trip counts are wave
@@ -1457,6 +1463,8 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
                             if (term(o, true) && NL && k != s) emit(k - s, k - s >= -32768 && k - s <= 32767);
                         });
     }
+    DTRMAX(2, wall_clock64());
+    DTRMAX(5, (unsigned long long)cnt);
     if (NL && ho.list) {
         // the tile's rigid-bin candidates (the forces pass's coupling work):
         // a heavy or coupled tile is filed for the forces pass (HeavyOut)
@@ -1508,6 +1516,7 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
             ho.tile[lb] = code;
         }
     }
+    DTR(3);
     if (!live) return;
     if (NL) {
         if (cnt <= NLIST_CAP && (cnt & 7)) nlist[(size_t)(cnt >> 3) * nstride + s] = group(cnt >> 3);
@@ -1518,6 +1527,7 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     rho[s] = acc;
     pr[s] = pres;
     nbB[2 * s + 1] = make_float2(acc, pres / (acc * acc));   // the p_j / rho_j^2 of metal:370
+    DTRMAX(4, wall_clock64());
 }
 
 // ---------------------------------------------------------------------------

@@ -6,7 +6,8 @@
 // accessors below.  Without those macros (the shipped build) every stamp is an
 // empty statement and nothing here is compiled.
 //
-//   FTR(k), FTRMAX(k, v)   k_forces_couple phases, per trace block `ftb` (the bbox-partial slot: tiles, then heavy quarters)
+//   FTR(k), FTRMAX(k, v)   k_forces_couple phases, per trace block `ftb` (the bbox-partial slot: tiles, then filed blocks)
+//   DTR(k), DTRMAX(k, v)   k_density<true> phases, per tile `dtb`
 //   PTR(w, k), PTR_SET     k_pgs_colour / k_pos_colour colour steps
 //   STR(w, j, k), STR_SET  k_pgs_stripes / k_pos_stripes phases per workgroup j
 //   CTR(k, v), STP(k)      k_group_colour stages per group, k_stripe_setup stages
@@ -32,7 +33,22 @@ extern "C" int lpe_ftrace(int on, unsigned long long *host, int n) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_ftrace), z, sizeof(z));
     return hipMemcpyToSymbol(HIP_SYMBOL(g_ftrace_on), &on, sizeof(int)) == hipSuccess ? 0 : 1;
 }
+// k_density<true> per tile (dtb = the tile): 0 start, 1 staged, 2 walk done
+// (max over waves), 3 filed, 4 end (max over waves), 5 longest list (max),
+// 6 the staged record count
+__device__ unsigned long long g_dtrace[4096 * 8];
+#define DTR(k) do { if (g_ftrace_on && threadIdx.x == 0 && dtb < 4096) g_dtrace[dtb * 8 + (k)] = wall_clock64(); } while (0)
+#define DTRSET(k, v) do { if (g_ftrace_on && threadIdx.x == 0 && dtb < 4096) g_dtrace[dtb * 8 + (k)] = (unsigned long long)(v); } while (0)
+#define DTRMAX(k, v) do { if (g_ftrace_on && (threadIdx.x & 63) == 0 && dtb < 4096) atomicMax(&g_dtrace[dtb * 8 + (k)], (unsigned long long)(v)); } while (0)
+#define DTRCLR() do { if (g_ftrace_on && threadIdx.x == 0 && dtb < 4096) for (int k_ = 0; k_ < 8; k_++) g_dtrace[dtb * 8 + k_] = 0; } while (0)
+extern "C" int lpe_dtrace(unsigned long long *host, int n) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dtrace), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
+}
 #else
+#define DTR(k) do {} while (0)
+#define DTRSET(k, v) do {} while (0)
+#define DTRMAX(k, v) do {} while (0)
+#define DTRCLR() do {} while (0)
 #define FTR(k) do {} while (0)
 #define FTRCLR() do {} while (0)
 #define FTR_PAIRS() ((unsigned long long *)nullptr)
