@@ -1433,12 +1433,18 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
                     if (NL) {
                         const bool in = term(o[j], valid);
                         ring[cnt & 15] = (int16_t)(cb + j);
-                        if (in && b + t + j != selfL[r])                          // (not itself: metal:360-366)
-                            cnt = cnt < lim ? cnt + 1 : NLIST_CAP + 1;           // (past: forces walks the bins)
+                        cnt += (in && b + t + j != selfL[r]) ? 1 : 0;            // (not itself: metal:360-366)
                     } else {
                         term0(o[j], valid);
                     }
                 }
+                // past the list's capacity (or a slot offset outside int16):
+                // the forces pass walks the bins -- the same count as capping
+                // each neighbour, cnt = cnt < lim ? cnt + 1 : NLIST_CAP + 1,
+                // since a trip adds at most 4 and only a trip with
+                // neighbours can overflow (without exec-mask branches per
+                // candidate)
+                if (NL && cnt != c0 && cnt > lim) cnt = NLIST_CAP + 1;
                 if (NL && (cnt >> 3) != (c0 >> 3) && cnt <= NLIST_CAP)
                     nlist[(size_t)(c0 >> 3) * nstride + s] = group(c0 >> 3);
             };
