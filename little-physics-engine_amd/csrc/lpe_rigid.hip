@@ -1114,6 +1114,47 @@ __device__ __forceinline__ void pgs_row_t(float4 rn, float4 rr, float imA, float
     }
     vxA = vA.x; vyA = vA.y; vxB = vB.x; vyB = vB.y;
 }
+// The striped solver's row (k_pgs_stripes): pgs_row_t's arithmetic with the
+// crosses precomputed (rowC, the same expressions) and the skipped update as
+// a zero increment instead of selects -- a body whose impulse is skipped, or
+// absent (zero inverse mass and inertia), gets v - d (0 m) = v: the same
+// value (a zero velocity may change the sign of its zero, which no later
+// operation of the tick turns into a different non-zero value)
+__device__ __forceinline__ void pgs_row_c(float4 rn, float4 rr, float4 rc, float imA, float iiA, float imB,
+                                          float iiB, float mu, float &ln, float &lf, float &vxA, float &vyA,
+                                          float &wA, float &vxB, float &vyB, float &wB) {
+    pk2 vA = {vxA, vyA}, vB = {vxB, vyB};
+    const pk2 lA = {-rr.y, rr.x}, lB = {-rr.w, rr.z};
+#pragma unroll
+    for (int row = 0; row < 2; row++) {
+        const pk2 d = row == 0 ? pk2{rn.x, rn.y} : pk2{-rn.y, rn.x};
+        const float eff = row == 0 ? rn.z : rn.w;
+        const pk2 a = vA + lA * wA, b = vB + lB * wB;
+        const pk2 rel = b - a;
+        const pk2 pr = rel * d;
+        float vrel = pr.x + pr.y;
+        float old, lo, hi;
+        if (row == 0) { old = ln; lo = 0.0f; hi = 1e20f; }
+        else {
+            old = lf;
+            float limit = mu * ln;
+            lo = -limit; hi = limit;
+        }
+        float dl = -eff * (vrel + 0.0f);
+        float nl = old + dl;
+        if (nl < lo) nl = lo;
+        if (nl > hi) nl = hi;
+        dl = nl - old;
+        if (row == 0) ln = nl; else lf = nl;
+        const float da = fabsf(dl) < 1e-15F ? 0.0f : dl;
+        const float crossA = row == 0 ? rc.x : rc.z, crossB = row == 0 ? rc.y : rc.w;
+        vA = vA - d * (da * imA);
+        vB = vB + d * (da * imB);
+        wA = wA - crossA * da * iiA;
+        wB = wB + crossB * da * iiB;
+    }
+    vxA = vA.x; vyA = vA.y; vxB = vB.x; vyB = vB.y;
+}
 __device__ __forceinline__ void pgs_row_regs(float4 rn, float4 rr, float imA, float iiA, float imB,
                                              float iiB, bool hasA, bool hasB, float mu, float &ln,
                                              float &lf, float &vxA, float &vyA, float &wA, float &vxB,
@@ -1684,7 +1725,7 @@ __global__ void k_prep_items(const int32_t *__restrict__ ncptr, const int32_t *_
                              float4 *__restrict__ rowR, int2 *__restrict__ rowAB, float4 *__restrict__ rowM,
                              int32_t *__restrict__ sItemA, int32_t *__restrict__ sItemB, PosRows out,
                              int32_t *__restrict__ inContact, int32_t *__restrict__ inPos, double baumgarte,
-                             double slop, int32_t *__restrict__ rowOf) {
+                             double slop, int32_t *__restrict__ rowOf, float4 *__restrict__ rowC) {
     const int t = blockIdx.x * RTPB + threadIdx.x;
     if (t >= *ncptr) return;
     const lpe_contact c = cs[order[t]];
@@ -1718,6 +1759,10 @@ __global__ void k_prep_items(const int32_t *__restrict__ ncptr, const int32_t *_
         rowR[t] = make_float4(rxA, ryA, rxB, ryB);
         rowAB[t] = make_int2(a, b);
         rowM[t] = make_float4(imA, iiA, imB, iiB);
+        // applyImpulse's crosses (:338-355) per direction, as pgs_row_t forms
+        // them: r x d with d = (dirX, dirY), then d = (-dirY, dirX)
+        rowC[t] = make_float4(rxA * dirY - ryA * dirX, rxB * dirY - ryB * dirX,
+                              rxA * dirX - ryA * (-dirY), rxB * dirX - ryB * (-dirY));
         sItemA[t] = a;
         sItemB[t] = b;
     }
@@ -1773,25 +1818,27 @@ __device__ __forceinline__ void pos_item_regs(double nx, double ny, double corr,
 // the same, the skip and the static-body cases as selects of the unchanged
 // values (bit-identical: every value that is kept is computed by the same
 // operations; a skipped item's arithmetic is discarded)
-__device__ __forceinline__ void pos_item_sel(double nx, double ny, double corr, double px, double py,
-                                             int flags, double invMA, double invMB, double invIA,
-                                             double invIB, double &xA, double &yA, double &tA,
-                                             double &xB, double &yB, double &tB) {
+// The striped position solver's item (pos_item's arithmetic in registers),
+// the skipped item as a zero correction instead of selects: a skipped item (flags & 1, or denom < 1e-12) gets sc = 0, and a
+// body that does not move (invM = 0) or turn (invI = 0 exactly when its
+// rotation flag is clear, k_prep_bodies) gets x - n sc 0 = x -- the same
+// value (a pose of exactly zero may change the sign of its zero, which no
+// later operation of the tick turns into a different non-zero value)
+__device__ __forceinline__ void pos_item_z(double nx, double ny, double corr, double px, double py,
+                                           int flags, double invMA, double invMB, double invIA,
+                                           double invIB, double &xA, double &yA, double &tA,
+                                           double &xB, double &yB, double &tB) {
     D2 rA = d2(px - xA, py - yA);
     D2 rB = d2(px - xB, py - yB);
     D2 n = d2(nx, ny);
     double rAn = crs(rA, n), rBn = crs(rB, n);
     double denom = invMA + invMB + (rAn * rAn) * invIA + (rBn * rBn) * invIB;
     const bool apply = !(flags & 1) && !(denom < 1e-12);
-    double sc = corr / denom;
+    const double sc = apply ? corr / denom : 0.0;
     double dx = n.x * sc, dy = n.y * sc;
-    const bool uA = apply && (invMA != 0.0 || (flags & 2)), uB = apply && (invMB != 0.0 || (flags & 4));
-    const double nxA = xA - dx * invMA, nyA = yA - dy * invMA, ntA = tA - rAn * sc * invIA;
-    const double nxB = xB + dx * invMB, nyB = yB + dy * invMB, ntB = tB + rBn * sc * invIB;
-    xA = uA ? nxA : xA; yA = uA ? nyA : yA; tA = (uA && (flags & 2)) ? ntA : tA;
-    xB = uB ? nxB : xB; yB = uB ? nyB : yB; tB = (uB && (flags & 4)) ? ntB : tB;
+    xA = xA - dx * invMA; yA = yA - dy * invMA; tA = tA - rAn * sc * invIA;
+    xB = xB + dx * invMB; yB = yB + dy * invMB; tB = tB + rBn * sc * invIB;
 }
-
 __device__ __forceinline__ void pos_item(const PosRec &q, double *sp) {
     if (q.flags & 1) return;
     const int a = q.a, b = q.b;
@@ -2765,7 +2812,8 @@ __host__ __device__ constexpr int lds_align(int b) { return (b + 15) & ~15; }
 // workgroup whose rows do not fit reads them from global memory instead.
 __global__ void __launch_bounds__(STPB)
 k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__restrict__ seg,
-              const float4 *__restrict__ rowN, const float4 *__restrict__ rowR, const int2 *__restrict__ rowAB,
+              const float4 *__restrict__ rowN, const float4 *__restrict__ rowR, const float4 *__restrict__ rowC,
+              const int2 *__restrict__ rowAB,
               const float4 *__restrict__ rowM, int iters, float mu, float *__restrict__ lamN,
               float *__restrict__ lamF, lpe_body *__restrict__ bodies, const int32_t *__restrict__ inContact,
               uint32_t base, int32_t *__restrict__ fault) {
@@ -2778,8 +2826,9 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
     if (threadIdx.x == 0) {   // (trace slots 61-63: phase A / B steps, pairs)
         STR_SET(0, j, 61, v.a1 - v.a0); STR_SET(0, j, 62, v.b1 - v.b0); STR_SET(0, j, 63, NP);
     }
-    // layout: rn, rr [NR] float4 | pr [NP] int4 | pm [NP] float4 | ln, lf [NR] | lv [3 NL] | stepL [NS + 1]
-    const int oRR = 16 * NR, oPR = oRR + 16 * NR, oPM = oPR + 16 * NP, oLN = oPM + 16 * NP, oLF = oLN + 4 * NR,
+    // layout: rn, rr, rc [NR] float4 | pr [NP] int4 | pm [NP] float4 | ln, lf [NR] | lv [3 NL] | stepL [NS + 1]
+    const int oRR = 16 * NR, oRC = oRR + 16 * NR, oPR = oRC + 16 * NR, oPM = oPR + 16 * NP, oLN = oPM + 16 * NP,
+              oLF = oLN + 4 * NR,
               oLV = oLF + 4 * NR, oST = oLV + 12 * NL, total = oST + 4 * (NS + 1);
     const bool inL = total <= STRIPE_LDS;
     float *lv = inL ? (float *)(smem + oLV) : (float *)smem;
@@ -2791,13 +2840,14 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
     const int *bpos = sb.bpos;
     auto lbody = [&](int b) { return b >= 0 ? bpos[b] - v.s0 : -1; };
     if (inL) {
-        float4 *rn = (float4 *)smem, *rr = (float4 *)(smem + oRR), *pm = (float4 *)(smem + oPM);
+        float4 *rn = (float4 *)smem, *rr = (float4 *)(smem + oRR), *rc = (float4 *)(smem + oRC),
+               *pm = (float4 *)(smem + oPM);
         int4 *pr = (int4 *)(smem + oPR);
         float *ln = (float *)(smem + oLN), *lf = (float *)(smem + oLF);
         int *stepL = (int *)(smem + oST);
         for (int r = threadIdx.x; r < NR; r += STPB) {
             const int g = r < v.nRA ? v.rA0 + r : v.rB0 + (r - v.nRA);
-            rn[r] = rowN[g]; rr[r] = rowR[g];
+            rn[r] = rowN[g]; rr[r] = rowR[g]; rc[r] = rowC[g];
             ln[r] = 0.f; lf[r] = 0.f;
         }
         for (int q = threadIdx.x; q < NP; q += STPB) {
@@ -2822,18 +2872,17 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
                 if (hasB) { vxB = lv[3 * p.w]; vyB = lv[3 * p.w + 1]; wB = lv[3 * p.w + 2]; }
                 constexpr int U = 4;                    // rows loaded together
                 for (int j0 = 0; j0 < p.y; j0 += U) {
-                    float4 a[U], c[U];
+                    float4 a[U], c[U], x[U];
                     float n[U], f[U];
 #pragma unroll
                     for (int u = 0; u < U; u++) {
                         const int t = p.x + min(j0 + u, p.y - 1);
-                        a[u] = rn[t]; c[u] = rr[t]; n[u] = ln[t]; f[u] = lf[t];
+                        a[u] = rn[t]; c[u] = rr[t]; x[u] = rc[t]; n[u] = ln[t]; f[u] = lf[t];
                     }
 #pragma unroll
                     for (int u = 0; u < U; u++) {
                         if (j0 + u >= p.y) break;
-                        pgs_row_t<true>(a[u], c[u], m.x, m.y, m.z, m.w, hasA, hasB, mu, n[u], f[u], vxA, vyA, wA,
-                                     vxB, vyB, wB);
+                        pgs_row_c(a[u], c[u], x[u], m.x, m.y, m.z, m.w, mu, n[u], f[u], vxA, vyA, wA, vxB, vyB, wB);
                         ln[p.x + j0 + u] = n[u];
                         lf[p.x + j0 + u] = f[u];
                     }
@@ -2851,7 +2900,7 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
         auto phase = [&](int s0, int s1, int) {
             if (threadIdx.x >= 64 || s0 >= s1) return;
             constexpr int U = 4;
-            struct Nx { int4 p; float4 m; float4 a[U], c[U]; float n[U], f[U]; };
+            struct Nx { int4 p; float4 m; float4 a[U], c[U], x[U]; float n[U], f[U]; };
             auto fetch = [&](int st, Nx &x) {
                 const int k = v.lstep(st);
                 const int q = stepL[k] + (int)threadIdx.x;
@@ -2861,7 +2910,7 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
 #pragma unroll
                 for (int u = 0; u < U; u++) {
                     const int t = x.p.x + max(min(u, x.p.y - 1), 0);
-                    x.a[u] = rn[t]; x.c[u] = rr[t]; x.n[u] = ln[t]; x.f[u] = lf[t];
+                    x.a[u] = rn[t]; x.c[u] = rr[t]; x.x[u] = rc[t]; x.n[u] = ln[t]; x.f[u] = lf[t];
                 }
             };
             Nx cur, nxt;
@@ -2878,16 +2927,15 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
                 for (int u = 0; u < U; u++) {
                     if (u >= p.y) break;
                     float n = cur.n[u], f = cur.f[u];
-                    pgs_row_t<true>(cur.a[u], cur.c[u], m.x, m.y, m.z, m.w, hasA, hasB, mu, n, f, vxA, vyA, wA, vxB,
-                                    vyB, wB);
+                    pgs_row_c(cur.a[u], cur.c[u], cur.x[u], m.x, m.y, m.z, m.w, mu, n, f, vxA, vyA, wA, vxB, vyB,
+                              wB);
                     ln[p.x + u] = n;
                     lf[p.x + u] = f;
                 }
                 for (int jr = U; jr < p.y; jr++) {       // (pairs of more than U rows: the rest on demand)
                     const int t = p.x + jr;
                     float n = ln[t], f = lf[t];
-                    pgs_row_t<true>(rn[t], rr[t], m.x, m.y, m.z, m.w, hasA, hasB, mu, n, f, vxA, vyA, wA, vxB, vyB,
-                                    wB);
+                    pgs_row_c(rn[t], rr[t], rc[t], m.x, m.y, m.z, m.w, mu, n, f, vxA, vyA, wA, vxB, vyB, wB);
                     ln[t] = n;
                     lf[t] = f;
                 }
@@ -2921,8 +2969,7 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
                 if (hasB) { vxB = lv[3 * lb]; vyB = lv[3 * lb + 1]; wB = lv[3 * lb + 2]; }
                 for (int t = rs; t < rs + nrow; t++) {
                     float n = it ? lamN[t] : 0.f, f = it ? lamF[t] : 0.f;
-                    pgs_row_t<true>(rowN[t], rowR[t], m.x, m.y, m.z, m.w, hasA, hasB, mu, n, f, vxA, vyA, wA, vxB,
-                                 vyB, wB);
+                    pgs_row_c(rowN[t], rowR[t], rowC[t], m.x, m.y, m.z, m.w, mu, n, f, vxA, vyA, wA, vxB, vyB, wB);
                     lamN[t] = n;
                     lamF[t] = f;
                 }
@@ -3245,7 +3292,7 @@ k_pos_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
                               const int t = r0 + k2;
                               const double2 n = ln[t], c = lc[t];
                               const int f = fl[t];
-                              pos_item_sel(n.x, n.y, c.x, c.y, py[t], f, mm.x, mm.y, ii.x, ii.y, xA, yA, tA, xB,
+                              pos_item_z(n.x, n.y, c.x, c.y, py[t], f, mm.x, mm.y, ii.x, ii.y, xA, yA, tA, xB,
                                             yB, tB);
                               return f;
                           });
@@ -3284,13 +3331,13 @@ k_pos_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
 #pragma unroll
                     for (int u = 0; u < U; u++) {
                         if (u >= p.y) break;
-                        pos_item_sel(cur.n[u].x, cur.n[u].y, cur.c[u].x, cur.c[u].y, cur.y[u], cur.f[u], mm.x, mm.y,
+                        pos_item_z(cur.n[u].x, cur.n[u].y, cur.c[u].x, cur.c[u].y, cur.y[u], cur.f[u], mm.x, mm.y,
                                      ii.x, ii.y, xA, yA, tA, xB, yB, tB);
                     }
                     for (int k2 = U; k2 < p.y; k2++) {       // (pairs of more than U rows: the rest on demand)
                         const int t = p.x + k2;
                         const double2 n = ln[t], c = lc[t];
-                        pos_item_sel(n.x, n.y, c.x, c.y, py[t], fl[t], mm.x, mm.y, ii.x, ii.y, xA, yA, tA, xB, yB, tB);
+                        pos_item_z(n.x, n.y, c.x, c.y, py[t], fl[t], mm.x, mm.y, ii.x, ii.y, xA, yA, tA, xB, yB, tB);
                     }
                     const int fl0 = cur.f[0];
                     if (mm.x != 0.0 || (fl0 & 2)) { lp[3 * a] = xA; lp[3 * a + 1] = yA; lp[3 * a + 2] = tA; }
@@ -3317,7 +3364,7 @@ k_pos_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
                               const int t = rs + k2;
                               const double2 n = rows.n[t], c = rows.c[t];
                               const int f = rows.fl[t];
-                              pos_item_sel(n.x, n.y, c.x, c.y, rows.py[t], f, mm.x, mm.y, ii.x, ii.y, xA, yA, tA,
+                              pos_item_z(n.x, n.y, c.x, c.y, rows.py[t], f, mm.x, mm.y, ii.x, ii.y, xA, yA, tA,
                                             xB, yB, tB);
                               return f;
                           });
@@ -3538,7 +3585,7 @@ int lpe_rigid_destroy_internal(lpe_ctx *ctx) {
                     d->pcursor, d->pairs, d->pairRankB, d->cslots, d->ccount, d->cstart, d->contacts,
                     d->bsum, d->order, d->rowN, d->rowR, d->rowAB, d->vel0, d->imii, d->inContact,
                     d->posState, d->posRec, d->posKeep, d->posStart, d->rowM, d->sItemA, d->sItemB,
-                    d->sVer, d->lamN, d->lamF, d->rowOf, d->sBCount, d->sBStart, d->sBCursor, d->sEnt,
+                    d->sVer, d->lamN, d->lamF, d->rowOf, d->rowC, d->sBCount, d->sBStart, d->sBCursor, d->sEnt,
                     d->counts, d->pcol, d->cseg, d->cbase, d->bgCount, d->bgStart, d->bgCursor,
                     d->bgList, d->bgKey, d->bgSpecial, d->bbits, d->jac};
     for (void *p : ptrs) if (p) (void)hipFree(p);
@@ -3642,6 +3689,7 @@ static int rigid_alloc_contacts(lpe_ctx *ctx, RigidDev *d, int cap) {
     if ((st = rgrow(ctx, &d->rowR, K))) return st;
     if ((st = rgrow(ctx, &d->rowAB, K))) return st;
     if ((st = rgrow(ctx, &d->rowM, K))) return st;
+    if ((st = rgrow(ctx, &d->rowC, K))) return st;
     if ((st = rgrow(ctx, &d->posRec, K))) return st;
     if ((st = rgrow(ctx, &d->sVer, K))) return st;
     if ((st = rgrow(ctx, &d->lamN, K))) return st;
@@ -4074,7 +4122,7 @@ static int colour_prep(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
                d->posState, d->inContact);
     LPE_KERNEL(ctx, "k_prep_items", k_prep_items, dim3(rblk(nc)), dim3(RTPB), 0, s, d->counts + 1, d->order,
                d->contacts, d->bodies, d->imii, d->posState, d->rowN, d->rowR, d->rowAB, d->rowM, d->sItemA, d->sItemB,
-               pos_rows(d), d->inContact, inPos, c.baumgarte, c.slop, d->rowOf);
+               pos_rows(d), d->inContact, inPos, c.baumgarte, c.slop, d->rowOf, d->rowC);
     LPE_CHECK_LAUNCH(ctx, "solver preparation");
     return LPE_OK;
 }
@@ -4153,8 +4201,8 @@ static int colour_pgs(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
         const uint32_t base = d->sbase_pgs;
         d->sbase_pgs += (uint32_t)c.pgsIterations + 2;
         LPE_KERNEL(ctx, "k_pgs_stripes", k_pgs_stripes, dim3(STRIPES_MAX / 2), dim3(STPB), STRIPE_LDS, s, d->counts, *sb,
-                   d->cseg, d->rowN, d->rowR, d->rowAB, d->rowM, c.pgsIterations, c.frictionCoeff, d->lamN, d->lamF,
-                   d->bodies, (const int32_t *)d->inContact, base, d->counts + 7);
+                   d->cseg, d->rowN, d->rowR, d->rowC, d->rowAB, d->rowM, c.pgsIterations, c.frictionCoeff, d->lamN,
+                   d->lamF, d->bodies, (const int32_t *)d->inContact, base, d->counts + 7);
         LPE_CHECK_LAUNCH(ctx, "pgs");
         return LPE_OK;
     }

@@ -51,6 +51,8 @@ struct RigidDev {
     float *imii = nullptr;                    // float2 per body (invMass, invInertia)
     int32_t *inContact = nullptr;             // per body flags
     float4 *rowM = nullptr;                   // imA, iiA, imB, iiB
+    float4 *rowC = nullptr;                   // canonical path: the lever arms' crosses with the normal (A, B)
+                                              // and the friction direction (A, B) -- k_pgs_stripes
     float *lamN = nullptr, *lamF = nullptr;   // accumulated impulses per contact
     int32_t *rowOf = nullptr;                 // canonical path: the PGS row of each contact (inverse of order)
     double *posState = nullptr;               // per body: invM, invI, flags (pos solver)
