@@ -1119,7 +1119,8 @@ __device__ __forceinline__ void pgs_row_t(float4 rn, float4 rr, float imA, float
 // a zero increment instead of selects -- a body whose impulse is skipped, or
 // absent (zero inverse mass and inertia), gets v - d (0 m) = v: the same
 // value (a zero velocity may change the sign of its zero, which no later
-// operation of the tick turns into a different non-zero value)
+// operation of the tick turns into a different non-zero value); for the same
+// reason vn + rhs (rhs = 0, :404) is vn
 __device__ __forceinline__ void pgs_row_c(float4 rn, float4 rr, float4 rc, float imA, float iiA, float imB,
                                           float iiB, float mu, float &ln, float &lf, float &vxA, float &vyA,
                                           float &wA, float &vxB, float &vyB, float &wB) {
@@ -1140,7 +1141,7 @@ __device__ __forceinline__ void pgs_row_c(float4 rn, float4 rr, float4 rc, float
             float limit = mu * ln;
             lo = -limit; hi = limit;
         }
-        float dl = -eff * (vrel + 0.0f);
+        float dl = -eff * vrel;          // (the reference's + rhs, rhs = 0, changes only a zero's sign)
         float nl = old + dl;
         if (nl < lo) nl = lo;
         if (nl > hi) nl = hi;
