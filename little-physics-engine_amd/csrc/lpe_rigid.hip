@@ -2202,7 +2202,7 @@ struct StripeBufs {
     int32_t *sbStart;      // [STRIPES_MAX + 2] bodies of each stripe; [STRIPES_MAX + 1]: end of the static ones
     int32_t *sbList;       // [nb] movable contact-pair bodies by stripe, then the static ones
     uint32_t *sflag;       // [2][STRIPES_MAX / 2] hand-over flags (phase A, phase B) per solver
-    float *gvel;           // [3 nb] velocities handed over (PGS), by sbList slot
+    unsigned long long *gvt;   // [3 nb] velocities handed over (PGS) with their epochs, by sbList slot
     double *gpos;          // [3 nb] poses handed over (position solver), by sbList slot
 };
 
@@ -2752,12 +2752,45 @@ __device__ __forceinline__ void wave_steps(int s0, int s1, int it, Solve &solve)
         }
     }
 }
+// Tagged hand-over (the PGS's fp32 velocities): each value travels with the
+// epoch of the phase that wrote it in one 64-bit word (value bits | epoch <<
+// 32, relaxed agent-scope atomic stores and loads), and a consumer polls the
+// values themselves until every one carries the epoch it waits for -- one
+// memory round trip instead of a flag poll followed by a reload.  A stripe's
+// words are rewritten only after their consumer has read them (the phases'
+// dependency chain), so a consumer never sees a later epoch than the one it
+// waits for.
+__device__ __forceinline__ void stripe_publish_tag(const StripeBufs &sb, int s, int s0, const float *lv,
+                                                   unsigned long long *g, uint32_t tag) {
+    const int b0 = 3 * sb.sbStart[s], b1 = 3 * sb.sbStart[s + 1];
+    for (int i = b0 + (int)threadIdx.x; i < b1; i += STPB)
+        __hip_atomic_store(&g[i], ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(lv[i - 3 * s0]),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stripe_reload_tag(const StripeBufs &sb, int s, int s0, float *lv,
+                                                  const unsigned long long *g, uint32_t tag, int32_t *fault) {
+    const int b0 = 3 * sb.sbStart[s], b1 = 3 * sb.sbStart[s + 1];
+    for (int i = b0 + (int)threadIdx.x; i < b1; i += STPB) {
+        unsigned long long w = __hip_atomic_load(&g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        unsigned spins = 0;
+        while ((uint32_t)(w >> 32) != tag) {
+            __builtin_amdgcn_s_sleep(1);
+            if (++spins > (1u << 22)) { atomicOr(fault, 2); break; }      // (as stripe_wait)
+            w = __hip_atomic_load(&g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        lv[i - 3 * s0] = __uint_as_float((uint32_t)w);
+    }
+}
+
 // single: `phase(s0, s1, it)` runs wave 0's steps (wave_steps, or a solver's
-// own pipelined loop); the workgroup joins at the phase's end.
-template <typename T, typename Solve, typename Phase>
+// own pipelined loop); the workgroup joins at the phase's end.  G = unsigned
+// long long: the tagged hand-over (T = float; the flags are not used, the
+// epochs are base + 2 it + 1 after phase A, + 2 after phase B).
+template <typename T, typename G, typename Solve, typename Phase>
 __device__ __forceinline__ void stripe_sweeps(const StripeBufs &sb, const StripeView &v, int iters, uint32_t base,
-                                              uint32_t *flagA, uint32_t *flagB, T *lv, T *g, int32_t *fault,
+                                              uint32_t *flagA, uint32_t *flagB, T *lv, G *g, int32_t *fault,
                                               Solve solve, int tw, bool single, Phase phase) {
+    constexpr bool tagged = std::is_same<G, unsigned long long>::value;
     const int j = v.j;
     const bool right = 2 * j + 2 < v.S;             // seam j (phase B) exists
     (void)tw;
@@ -2772,29 +2805,45 @@ __device__ __forceinline__ void stripe_sweeps(const StripeBufs &sb, const Stripe
     STR(tw, j, 1);
     for (int it = 0; it < iters; it++) {
         if (it > 0 && j > 0) {                    // stripe 2j, after the left neighbour's phase B of it - 1
-            stripe_wait(&flagB[j - 1], base + it, fault);
-            stripe_reload(sb, 2 * j, v.s0, lv, g);
+            if constexpr (tagged) {
+                stripe_reload_tag(sb, 2 * j, v.s0, lv, g, base + 2 * it, fault);
+            } else {
+                stripe_wait(&flagB[j - 1], base + it, fault);
+                stripe_reload(sb, 2 * j, v.s0, lv, g);
+            }
             __syncthreads();
         }
         STR(tw, j, 2 + 6 * it);
         steps(v.a0, v.a1, it);
         STR(tw, j, 3 + 6 * it);
         if (j > 0) {
-            stripe_publish(sb, 2 * j, v.s0, lv, g);
-            stripe_signal(&flagA[j], base + it + 1);
+            if constexpr (tagged) {
+                stripe_publish_tag(sb, 2 * j, v.s0, lv, g, base + 2 * it + 1);
+            } else {
+                stripe_publish(sb, 2 * j, v.s0, lv, g);
+                stripe_signal(&flagA[j], base + it + 1);
+            }
         }
         STR(tw, j, 4 + 6 * it);
         if (!right) continue;
         {                                         // stripe 2j+2, after the right neighbour's phase A of it
-            stripe_wait(&flagA[j + 1], base + it + 1, fault);
-            stripe_reload(sb, 2 * j + 2, v.s0, lv, g);
+            if constexpr (tagged) {
+                stripe_reload_tag(sb, 2 * j + 2, v.s0, lv, g, base + 2 * it + 1, fault);
+            } else {
+                stripe_wait(&flagA[j + 1], base + it + 1, fault);
+                stripe_reload(sb, 2 * j + 2, v.s0, lv, g);
+            }
             __syncthreads();
         }
         STR(tw, j, 5 + 6 * it);
         steps(v.b0, v.b1, it);
         STR(tw, j, 6 + 6 * it);
-        stripe_publish(sb, 2 * j + 2, v.s0, lv, g);
-        stripe_signal(&flagB[j], base + it + 1);
+        if constexpr (tagged) {
+            stripe_publish_tag(sb, 2 * j + 2, v.s0, lv, g, base + 2 * it + 2);
+        } else {
+            stripe_publish(sb, 2 * j + 2, v.s0, lv, g);
+            stripe_signal(&flagB[j], base + it + 1);
+        }
         STR(tw, j, 7 + 6 * it);
     }
 }
@@ -2946,7 +2995,7 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
                 cur = nxt;
             }
         };
-        stripe_sweeps(sb, v, iters, base, sb.sflag, sb.sflag + STRIPES_MAX / 2, lv, sb.gvel, fault, solve, 0,
+        stripe_sweeps(sb, v, iters, base, sb.sflag, sb.sflag + STRIPES_MAX / 2, lv, sb.gvt, fault, solve, 0,
                       single, phase);
         __syncthreads();
         for (int r = threadIdx.x; r < NR; r += STPB) {    // (the impulses, lpe_rigid_download_impulses)
@@ -2978,7 +3027,7 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
                 if (hasB) { lv[3 * lb] = vxB; lv[3 * lb + 1] = vyB; lv[3 * lb + 2] = wB; }
             }
         };
-        stripe_sweeps(sb, v, iters, base, sb.sflag, sb.sflag + STRIPES_MAX / 2, lv, sb.gvel, fault, solve, 0,
+        stripe_sweeps(sb, v, iters, base, sb.sflag, sb.sflag + STRIPES_MAX / 2, lv, sb.gvt, fault, solve, 0,
                       single,
                       [&](int a0, int a1, int itv) { wave_steps(a0, a1, itv, solve); });
     }
@@ -3593,7 +3642,7 @@ int lpe_rigid_destroy_internal(lpe_ctx *ctx) {
     if (StripeBufs *sb = (StripeBufs *)d->stripes) {
         void *sp[] = {sb->bstripe, sb->pgroup, sb->pcolg, sb->prank, sb->prowoff, sb->glist, sb->gstart, sb->gcnt,
                       sb->stepIdx, sb->stepPair, sb->stepRow, sb->wgStep, sb->sbStart, sb->sbList, sb->sflag,
-                      sb->gvel, sb->gpos, sb->bpos, sb->pflag, sb->px, sb->bred};
+                      sb->gvt, sb->gpos, sb->bpos, sb->pflag, sb->px, sb->bred};
         for (void *p : sp) if (p) (void)hipFree(p);
         delete sb;
     }
@@ -3995,9 +4044,11 @@ static StripeBufs *stripe_bufs(lpe_ctx *ctx, RigidDev *d) {
     auto grow = [&](auto **p, size_t n) { return rgrow(ctx, p, n); };
     if (d->nb > d->cap_stripe_nb || !sb->bstripe) {
         const size_t N = (size_t)std::max(d->nb, 1);
-        if (grow(&sb->bstripe, N) || grow(&sb->bpos, N) || grow(&sb->sbList, N) || grow(&sb->gvel, 3 * N) ||
+        if (grow(&sb->bstripe, N) || grow(&sb->bpos, N) || grow(&sb->sbList, N) || grow(&sb->gvt, 3 * N) ||
             grow(&sb->gpos, 3 * N))
             return nullptr;
+        // (epoch 0 never matches: the tagged hand-over's epochs start at sbase_pgs + 1 >= 17)
+        if (hipMemset(sb->gvt, 0, sizeof(unsigned long long) * 3 * N) != hipSuccess) return nullptr;
         d->cap_stripe_nb = d->nb;
     }
     if (d->cap_pairs > d->cap_stripe_pairs || !sb->pgroup) {
@@ -4200,7 +4251,7 @@ static int colour_pgs(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
         StripeBufs *sb = stripe_bufs(ctx, d);
         if (!sb) return LPE_ERR_HIP;
         const uint32_t base = d->sbase_pgs;
-        d->sbase_pgs += (uint32_t)c.pgsIterations + 2;
+        d->sbase_pgs += 2 * (uint32_t)c.pgsIterations + 4;      // (the tagged hand-over's epochs)
         LPE_KERNEL(ctx, "k_pgs_stripes", k_pgs_stripes, dim3(STRIPES_MAX / 2), dim3(STPB), STRIPE_LDS, s, d->counts, *sb,
                    d->cseg, d->rowN, d->rowR, d->rowC, d->rowAB, d->rowM, c.pgsIterations, c.frictionCoeff, d->lamN,
                    d->lamF, d->bodies, (const int32_t *)d->inContact, base, d->counts + 7);
