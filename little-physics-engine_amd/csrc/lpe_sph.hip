@@ -1085,6 +1085,7 @@ struct HeavyOut {             // k_density<true>: where it files the heavy tiles
     const float4 *rbinAabb;   //   and their AABBs in bin order (the pairs: AABB hits)
     float bcs;
     int bx0, by0, bW, bH;
+    int qpairs, hpairs;       //   the classes' thresholds (QUARTER_PAIRS, HALF_PAIRS; LPE_HEAVY_Q / _H for A/B)
 };
 struct HeavyIn {              // k_forces_couple: the lists the density pass filed
     const int32_t *list;      //   (null: off)
@@ -1503,11 +1504,11 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
         __syncthreads();
         if (threadIdx.x == 0) {
             int code = 0;
-            if (T >= QUARTER_PAIRS) {
+            if (T >= ho.qpairs) {
                 const int t = atomicAdd(&ho.list[0], 1);
                 if (t < QUARTER_MAX) code = 1 + t;
             }
-            if (!code && T >= HALF_PAIRS) {
+            if (!code && T >= ho.hpairs) {
                 const int t = atomicAdd(&ho.list[1], 1);
                 if (t < HALF_MAX) code = QUARTER_MAX + 1 + t;
             }
@@ -3371,6 +3372,9 @@ static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr, float *rho, flo
             ho.rbinStart = d.rbinStart;
             ho.rbinAabb = rbin_aabb(d);
             ho.bcs = d.bcs; ho.bx0 = d.bx0; ho.by0 = d.by0; ho.bW = d.bW; ho.bH = d.bH;
+            static const int qp = getenv("LPE_HEAVY_Q") ? std::atoi(getenv("LPE_HEAVY_Q")) : QUARTER_PAIRS;
+            static const int hp = getenv("LPE_HEAVY_H") ? std::atoi(getenv("LPE_HEAVY_H")) : HALF_PAIRS;
+            ho.qpairs = qp; ho.hpairs = hp;
         }
         LPE_KERNEL(ctx, "k_density", k_density<true>, dim3(xcd_grid(nblk(n, HB))), dim3(HB), 0, ctx->stream, n,
                    nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
