@@ -12,15 +12,36 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 from conftest import lpe
-z = np.load(os.path.join(ROOT, "tests", "golden", "pile_M_t250.npz"))
+FIX = os.environ.get("FIXTURE")          # (a rigid_*.npz fixture instead of the metric pile, e.g. the C1 stack)
+LIVE = os.environ.get("LIVE")            # (C1 / C3: the live scene after its settle, as small_probe.py runs it)
+if LIVE:
+    sys.path.insert(0, os.path.join(ROOT, "little-physics-engine_amd"))
+    import scenes
+    sc = scenes.rigid_scene(LIVE)
+    b0, v0 = scenes.to_bodies(sc["bodies"])
+    cfg = lpe.rigid_config(universe=sc["U"], pgs_iterations=sc["pgs_iterations"])
+    c0 = lpe.Context(0)
+    c0.rigid_set_config(cfg)
+    c0.rigid_upload(b0, v0)
+    c0.world_tick(1 / 120, 240 if LIVE == "C3" else 560)
+    z = {"bodies": c0.rigid_download(), "verts": v0}
+    c0.close()
+elif FIX:
+    z = dict(np.load(os.path.join(ROOT, "tests", "golden", FIX)))
+    z["bodies"] = z["before_rigid"]
+    cfg = lpe.rigid_config(universe=float(z["universe"]), pgs_iterations=int(z["pgs_iterations"]))
+else:
+    z = np.load(os.path.join(ROOT, "tests", "golden", "pile_M_t250.npz"))
+    cfg = lpe.rigid_config(universe=32.0)
 ctx = lpe.Context(0)
-ctx.rigid_set_config(lpe.rigid_config(universe=32.0))
+ctx.rigid_set_config(cfg)
 for _ in range(3):
     ctx.rigid_upload(z["bodies"], z["verts"]); st = ctx.rigid_step()
+print("pairs", st["pairs"], "contacts", st["contacts"], "colours", st["pgsLevels"])
 L = lpe.lib(); L.lpe_strace.argtypes = [C.c_void_p]
 buf = np.zeros(2 * 32 * 64, np.uint64); L.lpe_strace(buf.ctypes.data)
 buf = buf.reshape(2, 32, 64).astype(np.int64)
-it = 10
+it = cfg.pgsIterations
 for w, name in ((0, "pgs"), (1, "pos")):
     t = buf[w]
     t0 = t[:, 0].min()
