@@ -13,14 +13,29 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 from conftest import lpe
-z = np.load("/tmp/lpe_snap.npz")
+SCENE = os.environ.get("SCENE")          # (C2 / C4: that config after its prep ticks instead of the M snapshot)
 ctx = lpe.Context(0)
-ctx.rigid_set_config(lpe.rigid_config(universe=32.0))
-ctx.sph_set_config(lpe.default_fluid_config())
-ctx.rigid_upload(z["bodies"], z["verts"])
-ctx.sph_upload(z["x"], z["y"], z["vx"], z["vy"], z["mass"], z["density"], z["pressure"])
-ctx.world_set_coupling(None)
-ctx.world_tick(1 / 120, 3); ctx.sync()
+if SCENE:
+    sys.path.insert(0, os.path.join(ROOT, "little-physics-engine_amd"))
+    import scenes
+    sc = scenes.scene(SCENE)
+    b, v = scenes.to_bodies(sc["bodies"])
+    fl = sc["fluid"]
+    ctx.rigid_set_config(lpe.rigid_config(universe=sc["U"]))
+    ctx.sph_set_config(lpe.default_fluid_config())
+    ctx.rigid_upload(b, v)
+    ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+    ctx.world_set_coupling(None)
+    ctx.world_tick(1 / 120, 30 if SCENE == "C2" else 90); ctx.sync()
+    z = {"x": fl["x"]}
+else:
+    z = np.load("/tmp/lpe_snap.npz")
+    ctx.rigid_set_config(lpe.rigid_config(universe=32.0))
+    ctx.sph_set_config(lpe.default_fluid_config())
+    ctx.rigid_upload(z["bodies"], z["verts"])
+    ctx.sph_upload(z["x"], z["y"], z["vx"], z["vy"], z["mass"], z["density"], z["pressure"])
+    ctx.world_set_coupling(None)
+    ctx.world_tick(1 / 120, 3); ctx.sync()
 L = lpe.lib()
 L.lpe_ftrace.argtypes = [C.c_int, C.c_void_p, C.c_int]
 L.lpe_dtrace.argtypes = [C.c_void_p, C.c_int]
