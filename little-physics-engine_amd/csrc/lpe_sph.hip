@@ -3372,9 +3372,10 @@ static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr, float *rho, flo
             ho.rbinStart = d.rbinStart;
             ho.rbinAabb = rbin_aabb(d);
             ho.bcs = d.bcs; ho.bx0 = d.bx0; ho.by0 = d.by0; ho.bW = d.bW; ho.bH = d.bH;
-            static const int qp = getenv("LPE_HEAVY_Q") ? std::atoi(getenv("LPE_HEAVY_Q")) : QUARTER_PAIRS;
-            static const int hp = getenv("LPE_HEAVY_H") ? std::atoi(getenv("LPE_HEAVY_H")) : HALF_PAIRS;
-            ho.qpairs = qp; ho.hpairs = hp;
+            // read per pass (the overflow parity test changes them between contexts)
+            const char *qs = getenv("LPE_HEAVY_Q"), *hs = getenv("LPE_HEAVY_H");
+            ho.qpairs = qs ? std::max(1, std::atoi(qs)) : QUARTER_PAIRS;
+            ho.hpairs = hs ? std::max(1, std::atoi(hs)) : HALF_PAIRS;
         }
         LPE_KERNEL(ctx, "k_density", k_density<true>, dim3(xcd_grid(nblk(n, HB))), dim3(HB), 0, ctx->stream, n,
                    nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,

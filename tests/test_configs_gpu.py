@@ -109,6 +109,45 @@ def test_config_world_tick_bit_exact(oracle_mod, name, prep, mode):
         np.testing.assert_array_equal(got_b[k], rb[k], err_msg=(name, k))
 
 
+def _m_ticks(monkeypatch, q, h, ticks):
+    """M from its 240-tick state advanced `ticks` world ticks, the tile
+    scheduling's class thresholds set to (q, h) coupling pairs (None: default)."""
+    for var, val in (("LPE_HEAVY_Q", q), ("LPE_HEAVY_H", h)):
+        if val is None:
+            monkeypatch.delenv(var, raising=False)
+        else:
+            monkeypatch.setenv(var, str(val))
+    s, fl, bodies, verts = _advanced("M", 240)
+    ctx = _world_ctx(s["U"], fl, bodies, verts)
+    try:
+        ctx.world_tick(DT, ticks)
+        return ctx.sph_download(), ctx.rigid_download()
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("q,h", [(1, 1), (1 << 30, 1 << 30), (1, 1 << 30)],
+                         ids=["all-quarters", "all-whole", "quarters-then-whole"])
+def test_tile_scheduling_overflow_bit_exact(monkeypatch, q, h):
+    """The forces pass's tile scheduling with its classes
+    overfilled.  M couples ≈ 310 of its 1,024 tiles.  (1, 1) files every one
+    of them as four part blocks: the 128 quarter slots fill, the next 160
+    fall to halves, the rest to whole blocks.  (2^30, 2^30) files them all
+    whole: 160 fit and ≈ 150 stay unfiled, run by their own tile blocks.
+    (1, 2^30) fills the quarters and then the whole blocks, skipping halves,
+    with some tiles left unfiled again.  Tiles with a single coupling pair
+    split four ways leave empty part blocks.  Any partition of a tile's slots
+    over blocks is the same arithmetic, so 3 world ticks must be bit-identical
+    to the default thresholds (oracle-checked by
+    test_config_world_tick_bit_exact)."""
+    ref, rb_ref = _m_ticks(monkeypatch, None, None, 3)
+    got, rb = _m_ticks(monkeypatch, q, h, 3)
+    for k in ("x", "y", "vx", "vy", "density", "pressure"):
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    for k in ("x", "y", "angle", "vx", "vy", "omega"):
+        np.testing.assert_array_equal(rb[k], rb_ref[k], err_msg=k)
+
+
 def test_c5_eight_slab_ranks_bit_exact():
     """C5 (2,097,152 particles): 8 x-slab ranks (in-process transport, one
     GPU) against the single domain, 2 full world ticks: every particle and
