@@ -2870,6 +2870,7 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int j = (int)blockIdx.x;
     if (j >= counts[13]) return;
+    __builtin_amdgcn_s_setprio(3);   // (the tick's critical path: issue ahead of co-resident fluid waves)
     STR(0, j, 0);
     const StripeView v = stripe_view(sb, counts, j);
     const int NR = v.nrows(), NP = v.npairs(), NL = v.nloc(), NS = v.nsteps();
@@ -3279,6 +3280,7 @@ k_pos_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int j = (int)blockIdx.x;
     if (j >= counts[13]) return;
+    __builtin_amdgcn_s_setprio(3);
     STR(1, j, 0);
     const StripeView v = stripe_view(sb, counts, j);
     const int NR = v.nrows(), NP = v.npairs(), NS = v.nsteps();
