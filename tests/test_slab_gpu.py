@@ -302,3 +302,39 @@ def test_slab_stats_and_prelaunch_one_tick_calls():
         assert all(x["slabSlots"] >= x["slabOwned"] for x in st)
     for k in slab.FIELDS:
         np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
+
+
+def test_slab_capacity_overflow_reported():
+    """A rank's slots are fixed at upload (2 n + 4 wire_cap + 4096, lpe_sph.hip
+    slab_cap): C2's 65,536 particles drift right at 8 m/s into a
+    rank that starts empty (36,864 slots), past its capacity by tick ≈ 60.  The
+    next status check (the download) fails with the capacity error.  The domain
+    covers the drift (bbox + 10 m): a fluid that leaves the device grid is the
+    separate open issue of DESIGN.md §7c (profiles/r05/slab_capacity/)."""
+    s = scenes.scene("C2")
+    fl = dict(s["fluid"])
+    n = len(fl["x"])
+    fl["vx"] = np.full(n, 8.0)
+    cfg = lpe.default_fluid_config()
+    cs = slab.cell_size(cfg)
+    c_hi = int(slab._columns(fl["x"], cfg).max())
+    edges = np.array([-np.inf, (c_hi + 1) * cs, np.inf], np.float32)
+    pad = 10.0
+    domain = (float(fl["x"].min()) - pad, float(fl["y"].min()) - pad,
+              float(fl["x"].max()) + pad, float(fl["y"].max()) + pad)
+    ctxs = [lpe.Context(0) for _ in range(2)]
+    try:
+        for r, c in enumerate(ctxs):
+            slab.setup_rank(c, r, 2, fl, edges, cfg, np.zeros(0, lpe.RIGID_DTYPE), wire_cap=8192, domain=domain)
+        assert ctxs[1].n == 0
+        lpe.mg_loopback_run(ctxs, 80, DT)
+        errs = []
+        for c in ctxs:
+            try:
+                c.sph_download_owned(cap=n)
+            except lpe.LpeError as e:
+                errs.append(str(e))
+        assert any("outgrew its slots" in e for e in errs), errs
+    finally:
+        for c in ctxs:
+            c.close()
