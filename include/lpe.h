@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define LPE_ABI_VERSION 1
+#define LPE_ABI_VERSION 2
 
 enum lpe_status {
     LPE_OK = 0,
@@ -158,6 +158,11 @@ typedef struct lpe_sph_stats {
     int32_t forcesGlobal;       /* forces-pass blocks whose neighbourhood exceeded the LDS image, summed
                                    since the upload (their neighbours are gathered from global memory:
                                    the same sums, slower) */
+    /* the lagged checks of lpe_sph_step (ABI 2): times the device grid grew
+     * (or recentred) to stay ahead of the fluid's bbox, times a slab rank's
+     * slots grew, and the device grid in use (origin and size, cells) */
+    int32_t gridRegrows, slotRegrows;
+    int32_t deviceGrid[4];
 } lpe_sph_stats;
 
 /* ------------------------------------------------------------------------ */

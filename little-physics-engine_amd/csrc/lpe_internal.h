@@ -127,6 +127,22 @@ struct SphDev {
     int32_t *heavy = nullptr;     // [2][HEAVY_WORDS]: counts, filed tiles -- by density pass parity
     int32_t *tileHeavy = nullptr; // per tile: its filing code, or 0
     int heavyCur = 0;             // the parity the last density pass filed into
+    // lagged checks of the fluid step (lpe_sph.hip sph_lag_service), the
+    // pattern of RigidDev::lag: every call of an SPH-only or slab-rank step
+    // leaves its last sub-step's reference grid (the particles' bbox), the
+    // status words and a slab rank's slots in use in a pinned ring slot; the
+    // host reads a slot when it comes round (two calls later) or at once if it
+    // has landed.  An error a slot shows fails the call that reads it; a bbox
+    // nearing the device grid's edge grows (or recentres) the grid, a slab
+    // rank nearing its slot capacity grows the slots, before the next call.
+    int32_t *hlag = nullptr;      // pinned [2][LAG_WORDS]
+    hipEvent_t evLag[2] = {nullptr, nullptr};
+    bool lpend[2] = {false, false};
+    unsigned ltick = 0;           // records issued
+    bool lag_prev = false;        // a previous bbox sample (the drift rate)
+    int lag_box[4] = {0, 0, 0, 0};// its cells: minX, minY, maxX, maxY
+    unsigned lag_box_tick = 0;
+    long grid_regrows = 0, slot_regrows = 0;
 };
 
 // status slots
@@ -151,7 +167,8 @@ enum StatusSlot {
     ST_RX_GHOST_R = 17,     //   rank in a sub-step of the current tick (sizes the next tick's exchange)
     ST_SLAB_CAPACITY = 18,  // slab decomposition: the received ghosts did not fit the rank's slots
     ST_FORCES_GLOBAL = 19,  // forces blocks whose neighbourhood did not fit the LDS image (global gathers)
-    ST_COUNT = 20
+    ST_SLOT_PEAK = 20,      // slab decomposition: most slots a sub-step's hash wanted (own + received ghosts)
+    ST_COUNT = 21
 };
 
 }  // namespace lpe

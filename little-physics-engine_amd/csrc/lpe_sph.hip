@@ -346,6 +346,32 @@ __device__ __forceinline__ GridParams grid_from_bbox(float minX, float maxX, flo
     return g;
 }
 
+// The reference grid clipped to the device grid [ox, ox + W) x [oy, oy + H).
+// The device grid covers the particles' bbox with a margin (sph_plan_grid,
+// lpe_sph_cover_box, grown by the lagged checks of sph_lag_service), so the
+// clip is the identity in every sub-step the reference semantics hold.  A
+// reference grid past it means a particle left the device grid (its bin was
+// clamped to the edge by bin_key): the sub-step raises ST_CAP_OVERFLOW (the
+// call fails with LPE_ERR_CAPACITY), and every walk, which clips to g, stays
+// inside the bins that exist -- no access outside the grid's buffers.  A
+// slab rank (slab != 0) clips too, but its reference grid is the global one
+// (every rank's bbox) and its device grid covers only its slab's columns
+// and the ghost band (lpe_sph_cover_box): there only a clip in y is a
+// failure (a particle beyond its slab's columns is ST_HALO_DRIFT, or was
+// clamped by bin_key).
+__device__ __forceinline__ GridParams clip_grid(GridParams g, int ox, int oy, int W, int H, int slab, bool *clipped) {
+    const int x0 = max(g.gridMinX, ox), y0 = max(g.gridMinY, oy);
+    const int x1 = min(g.gridMinX + g.gridDimX - 1, ox + W - 1), y1 = min(g.gridMinY + g.gridDimY - 1, oy + H - 1);
+    const bool cx = x0 != g.gridMinX || x1 != g.gridMinX + g.gridDimX - 1;
+    const bool cy = y0 != g.gridMinY || y1 != g.gridMinY + g.gridDimY - 1;
+    *clipped = cy || (cx && !slab);
+    if (!cx && !cy) return g;
+    g.gridMinX = x0; g.gridMinY = y0;
+    g.gridMaxX = max(x1, x0); g.gridMaxY = max(y1, y0);
+    g.gridDimX = g.gridMaxX - x0 + 1; g.gridDimY = g.gridMaxY - y0 + 1;
+    return g;
+}
+
 // The sub-step's over-full reference cells (more than GPU_MAX_PER_CELL = 64,
 // fluid.hpp:56), listed by the scan as absolute (cell x, cell y): in the
 // reference cell-capacity mode a particle takes the literal capped walk only
@@ -407,7 +433,7 @@ __global__ void __launch_bounds__(TPB)
 k_scan_blocks(int nb, int32_t *__restrict__ bsum, int32_t *__restrict__ start_last,
               const float4 *__restrict__ bboxPart, int nparts, float cs,
               GridParams *__restrict__ gp, int32_t *__restrict__ status,
-              const float4 *__restrict__ bbG) {
+              const float4 *__restrict__ bbG, int ox, int oy, int W, int H) {
     int carry = 0;
     for (int b0 = 0; b0 < nb; b0 += TPB) {
         int b = b0 + threadIdx.x;
@@ -446,7 +472,9 @@ k_scan_blocks(int nb, int32_t *__restrict__ bsum, int32_t *__restrict__ start_la
             b.x = fminf(b.x, wb[w].x); b.y = fmaxf(b.y, wb[w].y);
             b.z = fminf(b.z, wb[w].z); b.w = fmaxf(b.w, wb[w].w);
         }
-        *gp = grid_from_bbox(b.x, b.y, b.z, b.w, cs);
+        bool clipped;
+        *gp = clip_grid(grid_from_bbox(b.x, b.y, b.z, b.w, cs), ox, oy, W, H, bbG != nullptr, &clipped);
+        if (clipped) atomicOr(&status[ST_CAP_OVERFLOW], 2);
         status[ST_NOT_INSERTED] = 0;
     }
 }
@@ -511,10 +539,13 @@ k_scan_final(int C, int W, int ox, int oy, int32_t *__restrict__ cnt,
             b.x = fminf(b.x, wb[w].x); b.y = fmaxf(b.y, wb[w].y);
             b.z = fminf(b.z, wb[w].z); b.w = fmaxf(b.w, wb[w].w);
         }
-        g = grid_from_bbox(b.x, b.y, b.z, b.w, gcs);
+        bool clipped = false;
+        if (fused == 1 || bbG)
+            g = clip_grid(grid_from_bbox(b.x, b.y, b.z, b.w, gcs), ox, oy, W, C / (4 * W), bbG != nullptr, &clipped);
         prefix = pre;
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             if (fused == 1) *gp = g;
+            if (clipped) atomicOr(&status[ST_CAP_OVERFLOW], 2);
             start[C] = all;
         }
     } else {
@@ -719,14 +750,19 @@ k_scan_rows(int W, int H, int ox, int oy, float eps, const int32_t *__restrict__
         b.z = fminf(b.z, wb[w].z); b.w = fmaxf(b.w, wb[w].w);
         pre += wsum[w];
     }
-    const GridParams g = grid_from_bbox(b.x, b.y, b.z, b.w, gcs);
+    bool clipped;
+    const GridParams g = clip_grid(grid_from_bbox(b.x, b.y, b.z, b.w, gcs), ox, oy, W, H, bbG != nullptr, &clipped);
     // every particle's row is in [row(minY), row(maxY)] (bin_key's row is
-    // monotone in y); the walks reach one row further, the reference
-    // cell-capacity walk stays inside the reference grid
+    // monotone in y, and clamped to the device grid like these bounds); the
+    // walks reach one row further, the reference cell-capacity walk stays
+    // inside the reference grid
     const int ylo = min((int)floorf((b.z + eps) / gcs), g.gridMinY), yhi = max((int)floorf((b.w + eps) / gcs), g.gridMaxY);
-    const int ry0 = max(ylo - oy - 2, 0), ry1 = min(yhi - oy + 2, H - 1);
+    const int ry0 = max(min(max(ylo - oy, 0), H - 1) - 2, 0), ry1 = min(max(min(yhi - oy, H - 1), 0) + 2, H - 1);
     if (r < ry0 || r > ry1) return;
-    if (r == ry0 && threadIdx.x == 0) *gp = g;
+    if (r == ry0 && threadIdx.x == 0) {
+        *gp = g;
+        if (clipped) atomicOr(&status[ST_CAP_OVERFLOW], 2);
+    }
     const int gy = r + oy;
     const bool rowIn = gy >= g.gridMinY && gy < g.gridMinY + g.gridDimY;
     // a slab rank's stats cover its own columns (the ghosts' are its neighbours')
@@ -1100,9 +1136,14 @@ static constexpr int HB = 256;            // slots (threads) per staged block (4
 static constexpr int HCAP = 1536;         // records staged per block (6 per thread)
 static constexpr int HBND = 1280;         // staged cell boundaries per block (5 per thread)
 
-__device__ __forceinline__ void cell_xy(float x, float y, float eps, float cs, int &cx, int &cy) {
-    cx = (int)floorf((x + eps) / cs);
-    cy = (int)floorf((y + eps) / cs);
+// a sorted record's cell: its bin's (nbA.w, written by the permute), i.e.
+// cell (floor((x + eps) / cs), floor((y + eps) / cs)) of its kicked position
+// clamped to the device grid (bin_key) -- so a plan made from it never
+// leaves the grid, even for a particle that did (ST_CAP_OVERFLOW)
+__device__ __forceinline__ void bin_cell(const float4 &r, int ox, int oy, int &cx, int &cy) {
+    const unsigned w = (unsigned)__float_as_int(r.w);
+    cx = ox + (int)((w >> 2) & 0x7fffu);
+    cy = oy + (int)(w >> 17);
 }
 
 struct Hood {
@@ -1121,8 +1162,8 @@ __device__ __forceinline__ void hood_plan(Hood &hd, int s0, int s1, const float4
                                           const int32_t *__restrict__ start, int cap = HCAP, int bcap = HBND) {
     const float4 f = nbA[s0], l = nbA[s1 - 1];
     int cx0, cy0, cx1, cy1;
-    cell_xy(f.x, f.y, eps, cs, cx0, cy0);
-    cell_xy(l.x, l.y, eps, cs, cx1, cy1);
+    bin_cell(f, ox, oy, cx0, cy0);
+    bin_cell(l, ox, oy, cx1, cy1);
     int xa[2] = {cx0, 0}, xb[2] = {cx1, 0};
     hd.ok = true;
     hd.cy0 = cy0;
@@ -1135,8 +1176,8 @@ __device__ __forceinline__ void hood_plan(Hood &hd, int s0, int s1, const float4
         const int rs = start[((cy1 - oy) * W) << 2];        // first slot of row cy1 (> s0)
         const float4 e0 = nbA[rs - 1], b1 = nbA[rs];
         int t;
-        cell_xy(e0.x, e0.y, eps, cs, xb[0], t);
-        cell_xy(b1.x, b1.y, eps, cs, xa[1], t);
+        bin_cell(e0, ox, oy, xb[0], t);
+        bin_cell(b1, ox, oy, xa[1], t);
         xb[1] = cx1;
     } else {
         hd.ok = false;
@@ -1818,6 +1859,14 @@ __device__ __forceinline__ void merge_prestats_dev(int32_t *__restrict__ st, int
     atomicOr(&st[ST_BUCKET_OVERFLOW], pre[ST_BUCKET_OVERFLOW]);
     atomicAdd(&st[ST_STAGE_FALLBACK], pre[ST_STAGE_FALLBACK]);
     atomicAdd(&st[ST_FORCES_GLOBAL], pre[ST_FORCES_GLOBAL]);
+    // (a slab rank's prelaunched sub-step 0 ran its exchange: its failures and maxima too)
+    atomicOr(&st[ST_HALO_OVERFLOW], pre[ST_HALO_OVERFLOW]);
+    atomicOr(&st[ST_HALO_DRIFT], pre[ST_HALO_DRIFT]);
+    atomicOr(&st[ST_SLAB_CAPACITY], pre[ST_SLAB_CAPACITY]);
+    atomicOr(&st[ST_LIST_OVERFLOW], pre[ST_LIST_OVERFLOW]);
+    atomicMax(&st[ST_RX_GHOST_L], pre[ST_RX_GHOST_L]);
+    atomicMax(&st[ST_RX_GHOST_R], pre[ST_RX_GHOST_R]);
+    atomicMax(&st[ST_SLOT_PEAK], pre[ST_SLOT_PEAK]);
     atomicAdd(&st[ST_OVER_CAP_TOTAL], pre[ST_OVER_CAP_TOTAL]);
     atomicMax(&st[ST_MAX_OCC_TOTAL], pre[ST_MAX_OCC_TOTAL]);
     for (int k = 0; k < ST_COUNT; k++) pre[k] = 0;
@@ -2306,6 +2355,14 @@ struct Shard {
     int hcol0 = 0, hcols = 0;
 };
 
+static void slab_clip_cols(const SphDev &d, long &gx0, long &gx1) {
+    if (!d.shard) return;
+    const Shard &h = *d.shard;
+    const long m = h.mv + SLAB_BAND + 8;
+    if (h.hasL) gx0 = std::max<long>(gx0, h.e0[h.rank] - m);
+    if (h.hasR) gx1 = std::min<long>(gx1, h.e0[h.rank + 1] + m);
+}
+
 // the rank's bbox record from the kick's block partials
 __global__ void __launch_bounds__(TPB)
 k_bbox_reduce(const float4 *__restrict__ part, int nparts, float4 *__restrict__ out) {
@@ -2357,6 +2414,7 @@ k_ghost_unpack(const float *__restrict__ rL, const float *__restrict__ rR, int w
         *bbG = make_float4(b.x, -b.z, b.y, -b.w);
         *nin = base + min(gL + gR, room);
         if (gL + gR > room) atomicOr(&status[ST_SLAB_CAPACITY], 1);
+        atomicMax(&status[ST_SLOT_PEAK], base + gL + gR);
         atomicMax(&status[ST_RX_GHOST_L], rL ? *(const int *)rL : 0);
         atomicMax(&status[ST_RX_GHOST_R], rR ? *(const int *)rR : 0);
         if (sL) *(int *)sL = 0;
@@ -2685,7 +2743,10 @@ static void sph_free(SphDev &d) {
                     d.blocksum, d.bboxPart, d.gp, d.status, d.rig, d.raabb, d.accum, d.acq, d.rbinStart, d.rgrid, d.rmax,
                     d.rbinList, d.rbinCount, d.coupleBody, d.plans, d.fplans, d.heavy, d.tileHeavy};
     for (void *p : ptrs) if (p) (void)hipFree(p);
-    hipEvent_t evs[] = {d.preReady, d.preDone, d.fbgDone};
+    for (int k = 0; k < 2; k++)
+        if (d.lpend[k] && d.evLag[k]) (void)hipEventSynchronize(d.evLag[k]);
+    if (d.hlag) (void)hipHostFree(d.hlag);
+    hipEvent_t evs[] = {d.preReady, d.preDone, d.fbgDone, d.evLag[0], d.evLag[1]};
     for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
     if (d.pside) (void)hipStreamDestroy(d.pside);
     d = SphDev();
@@ -2812,10 +2873,16 @@ static int sph_set_grid(lpe_ctx *ctx, int gx0, int gy0, int gx1, int gy1) {
     SphDev &d = ctx->sph;
     if (d.pside) LPE_HIP(ctx, hipStreamSynchronize(d.pside));   // the bins may be re-allocated
     d.pre = false;
+    const long nW = (long)gx1 - gx0 + 1, nH = (long)gy1 - gy0 + 1;
+    long C = 4L * nW * nH;
+    // (a sorted record's bin keeps its cell row and column in 15 bits each:
+    // bin_cell); the grid in use stays as it was
+    if (C > (1L << 29) || nW >= (1 << 15) || nH >= (1 << 15) || nW < 1 || nH < 1) {
+        ctx->err = "device grid too large (the fluid spans more than 32767 cells, or 2^27 cells in all)";
+        return LPE_ERR_CAPACITY;
+    }
     d.ox = gx0; d.oy = gy0;
-    d.W = gx1 - gx0 + 1; d.H = gy1 - gy0 + 1;
-    long C = 4L * d.W * d.H;
-    if (C > (1L << 29)) { ctx->err = "device grid too large"; return LPE_ERR_CAPACITY; }
+    d.W = (int)nW; d.H = (int)nH;
     if (C > d.cap_cells) {
         void *old[] = {d.count, d.start, d.cursor, d.blocksum};
         for (void *p : old) if (p) (void)hipFree(p);
@@ -2869,28 +2936,42 @@ static int sph_plan_grid(lpe_ctx *ctx, const float *x, const float *y, int n) {
                         (int)std::floor(mxx / cs) + pad, (int)std::floor(mxy / cs) + pad);
 }
 
+// A slab rank only ever holds particles near its slab: its edges move at
+// most mv columns (rebalancing), its ghosts lie SLAB_BAND columns beyond
+// them, a kicked particle a fraction of a column further -- so its device
+// grid covers the wanted cells only that far past its inner edges
+// (slab_clip_cols).
+
+// the device grid grown to cover the cells [gx0, gx1] x [gy0, gy1] (the
+// union with the grid in use); recentre: if that union would be more than
+// four times the wanted area, the wanted cells alone (a fluid drifting far
+// from where it started leaves the old cells empty)
+static int sph_cover_cells(lpe_ctx *ctx, long gx0, long gy0, long gx1, long gy1, bool recentre) {
+    SphDev &d = ctx->sph;
+    slab_clip_cols(d, gx0, gx1);
+    if (gx1 < gx0) gx1 = gx0;
+    long ux0 = std::min<long>(d.ox, gx0), uy0 = std::min<long>(d.oy, gy0);
+    long ux1 = std::max<long>(d.ox + d.W - 1, gx1), uy1 = std::max<long>(d.oy + d.H - 1, gy1);
+    if (ux0 == d.ox && uy0 == d.oy && ux1 == d.ox + d.W - 1 && uy1 == d.oy + d.H - 1) return LPE_OK;
+    if (recentre && (ux1 - ux0 + 1) * (uy1 - uy0 + 1) > 4 * (gx1 - gx0 + 1) * (gy1 - gy0 + 1)) {
+        ux0 = gx0; uy0 = gy0; ux1 = gx1; uy1 = gy1;
+    }
+    const long lim = 1L << 20;     // (sph_set_grid refuses more than 32767 cells a side)
+    if (ux0 < -lim || uy0 < -lim || ux1 > lim || uy1 > lim) {
+        ctx->err = "device grid too large (the fluid spans more than 32767 cells, or 2^27 cells in all)";
+        return LPE_ERR_CAPACITY;
+    }
+    return sph_set_grid(ctx, (int)ux0, (int)uy0, (int)ux1, (int)uy1);
+}
+
 // grow the device grid to cover [x0, x1] x [y0, y1] (world mode: the
 // universe the boundary system keeps every body and particle in)
 int lpe_sph_cover_box(lpe_ctx *ctx, double x0, double y0, double x1, double y1) {
     SphDev &d = ctx->sph;
     if (d.cs <= 0.f || (d.n <= 0 && !d.shard)) return LPE_OK;
-    if (d.shard) {
-        // a slab rank only ever holds particles near its slab: its edges move
-        // at most mv columns (rebalancing), its ghosts lie SLAB_BAND columns
-        // beyond them, a kicked particle a fraction of a column further
-        const Shard &h = *d.shard;
-        const double m = (h.mv + SLAB_BAND + 4) * (double)d.cs;
-        if (h.hasL) x0 = std::max(x0, h.e0[h.rank] * (double)d.cs - m);
-        if (h.hasR) x1 = std::min(x1, h.e0[h.rank + 1] * (double)d.cs + m);
-        if (x1 < x0) x1 = x0;
-    }
     const double cs = d.cs;
-    int gx0 = std::min(d.ox, (int)std::floor(x0 / cs) - 4);
-    int gy0 = std::min(d.oy, (int)std::floor(y0 / cs) - 4);
-    int gx1 = std::max(d.ox + d.W - 1, (int)std::floor(x1 / cs) + 4);
-    int gy1 = std::max(d.oy + d.H - 1, (int)std::floor(y1 / cs) + 4);
-    if (gx0 == d.ox && gy0 == d.oy && gx1 == d.ox + d.W - 1 && gy1 == d.oy + d.H - 1) return LPE_OK;
-    return sph_set_grid(ctx, gx0, gy0, gx1, gy1);
+    return sph_cover_cells(ctx, (long)std::floor(x0 / cs) - 4, (long)std::floor(y0 / cs) - 4,
+                           (long)std::floor(x1 / cs) + 4, (long)std::floor(y1 / cs) + 4, false);
 }
 
 static int pstate_alloc(lpe_ctx *ctx, PState &p, size_t N, bool with_a) {
@@ -2907,6 +2988,7 @@ static int pstate_alloc(lpe_ctx *ctx, PState &p, size_t N, bool with_a) {
 // slots per particle array: n (single domain); a slab rank's owned particles
 // and received ghosts, with room for its owned count to grow (slab_cap)
 static long slab_cap(const Shard &h, int n) { return 2L * n + 4L * h.wcap + 4096; }
+static int sph_realloc_slots(lpe_ctx *ctx, int n);
 static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     SphDev &d = ctx->sph;
     Shard *h = d.shard;
@@ -2916,6 +2998,12 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
         n = (int)want;
     }
     if (n <= d.cap_n && d.P.x) return LPE_OK;
+    return sph_realloc_slots(ctx, n);
+}
+// every per-slot array for n slots (the particle state P, rho and pr are
+// freed like the scratch: sph_grow_slots detaches them first to keep them)
+static int sph_realloc_slots(lpe_ctx *ctx, int n) {
+    SphDev &d = ctx->sph;
     pstate_free(d.P);
     pstate_free(d.S);
     void *ptrs[] = {d.rho, d.pr, d.nbA, d.nbB, d.nlist, d.ncount, d.key, d.tmpId, d.tmpOld, d.bboxPart, d.refInv,
@@ -2974,6 +3062,7 @@ static int sph_alloc_particles(lpe_ctx *ctx, int n) {
     return LPE_OK;
 }
 
+static void sph_lag_reset(lpe_ctx *ctx);
 extern "C" int lpe_sph_upload(lpe_ctx *ctx, int n, const float *x, const float *y,
                               const float *vx, const float *vy, const float *mass,
                               const float *density, const float *pressure) {
@@ -2983,6 +3072,7 @@ extern "C" int lpe_sph_upload(lpe_ctx *ctx, int n, const float *x, const float *
     SphDev &d = ctx->sph;
     if (d.pside) LPE_HIP(ctx, hipStreamSynchronize(d.pside));   // buffers may be re-allocated
     d.pre = false;
+    sph_lag_reset(ctx);                                          // (the records of the old state)
     int st = sph_alloc_particles(ctx, n);
     if (st) return st;
     d.n = n;
@@ -3108,7 +3198,7 @@ static int sph_scan(lpe_ctx *ctx, int C, int32_t *cnt, int32_t *start, int32_t *
                fused && fluid ? d.stat_cur : (int32_t *)nullptr, ovl, ovlNext);
     if (!fused)
         LPE_KERNEL(ctx, "k_scan_blocks", k_scan_blocks, dim3(1), dim3(TPB), 0, s, nb, bsum, start + C, d.bboxPart,
-                   nparts, d.cs, fluid ? d.gp_cur : (GridParams *)nullptr, d.stat_cur, bbG);
+                   nparts, d.cs, fluid ? d.gp_cur : (GridParams *)nullptr, d.stat_cur, bbG, d.ox, d.oy, d.W, d.H);
     LPE_KERNEL(ctx, "k_scan_final", k_scan_final, dim3(nb), dim3(TPB), 0, s, C, d.W, d.ox, d.oy, cnt, bsum,
                start, cursor, d.gp_cur, d.stat_cur, fluid ? 1 : 0, fused ? (fluid ? 1 : 2) : 0, (const float4 *)d.bboxPart,
                nparts, d.cs, bbG, ovl);
@@ -3288,6 +3378,7 @@ static int sph_hash_sort(lpe_ctx *ctx, int kb, bool probe, const float4 *bbG, in
 
 
 static int sph_hash_slab(lpe_ctx *ctx, float subDt, float halfDt, bool first, int kicked);
+static int status_error(lpe_ctx *ctx, const int32_t *status);
 
 // one grid hash: kick (unless probe) + histogram + scan + scatter + rank/permute
 // kicked > 0: the previous forces pass already kicked this sub-step (KickNext)
@@ -3551,6 +3642,159 @@ int sph_prelaunch(lpe_ctx *ctx, double dt_tick, const std::function<int(hipStrea
     return LPE_OK;
 }
 
+// ---- lagged checks of the fluid step (SphDev::hlag) ---------------------
+// Every lpe_sph_step call (and every world tick of a slab rank) ends with one
+// small launch that copies the last sub-step's reference grid (the bbox of
+// the particles, in cells; a slab rank's is the global one), the status words
+// and the slots in use into a pinned ring slot.  The next call's end reads the
+// previous record if it has landed, and the record two calls back (waiting
+// for it: the host runs at most two calls ahead), and then
+//   - fails with the status error the record shows (off-grid, slab slots,
+//     halo...), two calls after the fact at most, as the rigid path's lagged
+//     checks do; lpe_sph_download reports it too;
+//   - grows the device grid when the bbox, widened by a margin that covers
+//     four calls of its observed drift (16 cells at least), leaves it: the
+//     reference regrows its grid to the bbox every sub-step
+//     (fluid.cpp:740-755); here the bins are re-planned at a call boundary,
+//     where no kernel holds them (each sub-step re-sorts from its kicked
+//     positions, so the results do not depend on the device grid);
+//   - grows a slab rank's slots (keeping its state) when the most slots a
+//     sub-step wanted passes half of them.
+static constexpr int LAG_WORDS = 32;     // [0, 7) GridParams, [8, 8 + ST_COUNT) status, [30] slots in use
+static_assert(sizeof(GridParams) == 7 * sizeof(int32_t) && 8 + ST_COUNT <= 30, "lag record layout");
+
+__global__ void __launch_bounds__(64)
+k_lag_record(const GridParams *__restrict__ gp, const int32_t *__restrict__ status,
+             const int32_t *__restrict__ slots, int32_t *__restrict__ out) {
+    const int t = threadIdx.x;
+    if (t < 7) out[t] = ((const int32_t *)gp)[t];
+    if (t < ST_COUNT) out[8 + t] = status[t];
+    if (t == 0) out[30] = slots ? *slots : 0;
+}
+
+// a slab rank's slots grown to `want`, keeping the particle state (P in its
+// sorted order, rho, pr); everything else is per-sub-step scratch
+static int sph_grow_slots(lpe_ctx *ctx, long want) {
+    SphDev &d = ctx->sph;
+    if (want > (1L << 30)) { ctx->err = "slab capacity too large"; return LPE_ERR_CAPACITY; }
+    if (d.pside) LPE_HIP(ctx, hipStreamSynchronize(d.pside));
+    LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    d.pre = false;
+    const size_t old = (size_t)d.cap_n;
+    PState keep = d.P;
+    float *rho = d.rho, *pr = d.pr;
+    d.P = PState();
+    d.rho = d.pr = nullptr;
+    int st = sph_realloc_slots(ctx, (int)want);
+    if (!st) {
+        float *src[] = {keep.x, keep.y, keep.vx, keep.vy, keep.vhx, keep.vhy, keep.ax, keep.ay, keep.m, rho, pr};
+        float *dst[] = {d.P.x, d.P.y, d.P.vx, d.P.vy, d.P.vhx, d.P.vhy, d.P.ax, d.P.ay, d.P.m, d.rho, d.pr};
+        for (int k = 0; k < 11 && !st; k++)
+            if (hipMemcpyAsync(dst[k], src[k], sizeof(float) * old, hipMemcpyDeviceToDevice, ctx->stream) != hipSuccess)
+                st = LPE_ERR_HIP;
+        if (!st && hipMemcpyAsync(d.P.id, keep.id, sizeof(int32_t) * old, hipMemcpyDeviceToDevice, ctx->stream) !=
+                       hipSuccess)
+            st = LPE_ERR_HIP;
+        if (!st && hipStreamSynchronize(ctx->stream) != hipSuccess) st = LPE_ERR_HIP;
+        if (st) ctx->err = "slab slot growth: copying the particle state";
+    }
+    pstate_free(keep);
+    if (rho) (void)hipFree(rho);
+    if (pr) (void)hipFree(pr);
+    if (st) return st;
+    d.n = d.cap_n;                 // (a slab rank's kernels run over its slot capacity)
+    d.slot_regrows++;
+    return LPE_OK;
+}
+
+// one record (slot), once it has landed (wait = false: only if it has)
+static int sph_lag_check(lpe_ctx *ctx, int slot, bool wait, unsigned tick) {
+    SphDev &d = ctx->sph;
+    if (!d.lpend[slot]) return LPE_OK;
+    if (wait) {
+        LPE_HIP(ctx, hipEventSynchronize(d.evLag[slot]));
+    } else {
+        const hipError_t q = hipEventQuery(d.evLag[slot]);
+        if (q == hipErrorNotReady) return LPE_OK;
+        if (q != hipSuccess) { ctx->err = "hipEventQuery (lagged fluid check)"; return LPE_ERR_HIP; }
+    }
+    d.lpend[slot] = false;
+    const int32_t *w = d.hlag + (size_t)LAG_WORDS * slot;
+    int st = status_error(ctx, w + 8);
+    if (st) return st;
+    GridParams g;
+    std::memcpy(&g, w, sizeof(g));
+    if (d.n <= 0 && !d.shard) return LPE_OK;
+    if (g.gridDimX <= 0 || g.gridDimY <= 0 || g.cellSize != d.cs) return LPE_OK;   // (no sub-step recorded)
+    const long box[4] = {g.gridMinX, g.gridMinY, g.gridMinX + g.gridDimX - 1L, g.gridMinY + g.gridDimY - 1L};
+    // the bbox's drift per call since the previous sample (outward only)
+    long rate = 0;
+    if (d.lag_prev && tick > d.lag_box_tick) {
+        const long span = (long)(tick - d.lag_box_tick);
+        const long out = std::max(std::max(d.lag_box[0] - box[0], d.lag_box[1] - box[1]),
+                                  std::max(box[2] - d.lag_box[2], box[3] - d.lag_box[3]));
+        rate = (std::max(out, 0L) + span - 1) / span;
+    }
+    if (!d.lag_prev || tick > d.lag_box_tick) {
+        for (int k = 0; k < 4; k++) d.lag_box[k] = (int)box[k];
+        d.lag_box_tick = tick;
+        d.lag_prev = true;
+    }
+    const long m = 16 + 6 * rate;
+    long wx0 = box[0] - m, wy0 = box[1] - m, wx1 = box[2] + m, wy1 = box[3] + m;
+    slab_clip_cols(d, wx0, wx1);
+    if (wx0 < d.ox || wy0 < d.oy || wx1 > d.ox + d.W - 1 || wy1 > d.oy + d.H - 1) {
+        const long ex = std::max(box[2] - box[0], box[3] - box[1]);
+        const long M = std::max(std::max(2 * m, 64L), ex / 4);
+        if (d.pside) LPE_HIP(ctx, hipStreamSynchronize(d.pside));
+        LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));   // (nothing in flight may hold the bins)
+        st = sph_cover_cells(ctx, box[0] - M, box[1] - M, box[2] + M, box[3] + M, true);
+        if (st) return st;
+        d.grid_regrows++;
+    }
+    if (d.shard) {
+        const long peak = std::max(w[8 + ST_SLOT_PEAK], w[30]);
+        if (2 * peak > d.cap_n) {
+            st = sph_grow_slots(ctx, std::max(2L * d.cap_n, 4 * peak + 4096));
+            if (st) return st;
+        }
+    }
+    return LPE_OK;
+}
+
+// the end of a call: the pending records, then this call's
+static int sph_lag_service(lpe_ctx *ctx) {
+    SphDev &d = ctx->sph;
+    if (!d.status || !d.gp) return LPE_OK;
+    if (!d.hlag) {
+        LPE_HIP(ctx, hipHostMalloc((void **)&d.hlag, sizeof(int32_t) * 2 * LAG_WORDS, 0));
+        std::memset(d.hlag, 0, sizeof(int32_t) * 2 * LAG_WORDS);
+        LPE_HIP(ctx, hipEventCreateWithFlags(&d.evLag[0], hipEventDisableTiming));
+        LPE_HIP(ctx, hipEventCreateWithFlags(&d.evLag[1], hipEventDisableTiming));
+    }
+    const int slot = (int)(d.ltick & 1u);
+    // the older record (this slot's, two calls back: waited for), then the previous one if it is in
+    int st = sph_lag_check(ctx, slot, true, d.ltick - 2);
+    if (!st) st = sph_lag_check(ctx, 1 - slot, false, d.ltick - 1);
+    if (st) return st;
+    LPE_KERNEL(ctx, "k_lag_record", k_lag_record, dim3(1), dim3(64), 0, ctx->stream, (const GridParams *)d.gp,
+               (const int32_t *)d.status, sph_slab_slots(ctx), d.hlag + (size_t)LAG_WORDS * slot);
+    LPE_CHECK_LAUNCH(ctx, "k_lag_record");
+    LPE_HIP(ctx, hipEventRecord(d.evLag[slot], ctx->stream));
+    d.lpend[slot] = true;
+    d.ltick++;
+    return LPE_OK;
+}
+
+// every pending record (an upload or a reconfiguration starts afresh)
+static void sph_lag_reset(lpe_ctx *ctx) {
+    SphDev &d = ctx->sph;
+    for (int k = 0; k < 2; k++)
+        if (d.lpend[k] && d.evLag[k]) (void)hipEventSynchronize(d.evLag[k]);
+    d.lpend[0] = d.lpend[1] = false;
+    d.lag_prev = false;
+}
+
 extern "C" int lpe_sph_step(lpe_ctx *ctx, double dt_tick) {
     return sph_step_hooked(ctx, dt_tick, nullptr);
 }
@@ -3686,7 +3930,12 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
                            d.acq, d.accum, c.dampingFactor, (const int32_t *)d.coupleBody, d.wb_bodies);
         LPE_CHECK_LAUNCH(ctx, "k_rigid_writeback");
     }
-    if (sh) return slab_rebalance(ctx);
+    if (sh) {
+        st = slab_rebalance(ctx);
+        if (st) return st;
+    }
+    // (a world tick's single-domain grid covers the universe, lpe_sph_cover_box)
+    if (!hook || sh) return sph_lag_service(ctx);
     return LPE_OK;
 }
 
@@ -3718,8 +3967,13 @@ static int check_status(lpe_ctx *ctx) {
     if (!d.status) return LPE_OK;
     int32_t status[ST_COUNT];
     LPE_HIP(ctx, hipMemcpy(status, d.status, sizeof(status), hipMemcpyDeviceToHost));
+    return status_error(ctx, status);
+}
+
+static int status_error(lpe_ctx *ctx, const int32_t *status) {
     if (status[ST_CAP_OVERFLOW]) {
-        ctx->err = "a fluid particle left the device grid capacity";
+        ctx->err = "a fluid particle left the device grid (it moved further than the grid's margin between two "
+                   "lagged checks; lpe_sph_set_domain can cover the region the fluid reaches)";
         return LPE_ERR_CAPACITY;
     }
     if (status[ST_LIST_OVERFLOW]) {
@@ -3821,6 +4075,9 @@ extern "C" int lpe_sph_get_stats(lpe_ctx *ctx, lpe_sph_stats *out) {
     out->refUndefined = status[ST_REF_UB];
     out->overCapCellsTotal = status[ST_OVER_CAP_TOTAL];
     out->maxCellOccupancyTotal = status[ST_MAX_OCC_TOTAL];
+    out->gridRegrows = (int32_t)d.grid_regrows;
+    out->slotRegrows = (int32_t)d.slot_regrows;
+    out->deviceGrid[0] = d.ox; out->deviceGrid[1] = d.oy; out->deviceGrid[2] = d.W; out->deviceGrid[3] = d.H;
     out->haloWire[0] = (d.shard && d.shard->hasL) ? d.shard->wcap : 0;
     out->haloWire[1] = (d.shard && d.shard->hasR) ? d.shard->wcap : 0;
     if (d.shard) {

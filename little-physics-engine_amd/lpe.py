@@ -85,10 +85,11 @@ class SphStats(C.Structure):
                 ("stageFallback", C.c_int32), ("overCapCells", C.c_int32), ("refUndefined", C.c_int32),
                 ("overCapCellsTotal", C.c_int32), ("maxCellOccupancyTotal", C.c_int32),
                 ("haloWire", C.c_int32 * 2), ("slabOwned", C.c_int32), ("slabSlots", C.c_int32),
-                ("ghostsIn", C.c_int32 * 2), ("forcesGlobal", C.c_int32)]
+                ("ghostsIn", C.c_int32 * 2), ("forcesGlobal", C.c_int32),
+                ("gridRegrows", C.c_int32), ("slotRegrows", C.c_int32), ("deviceGrid", C.c_int32 * 4)]
 
     def as_dict(self):
-        return {k: (list(getattr(self, k)) if k in ("haloWire", "ghostsIn") else getattr(self, k))
+        return {k: (list(getattr(self, k)) if k in ("haloWire", "ghostsIn", "deviceGrid") else getattr(self, k))
                 for k, _ in self._fields_}
 
 
@@ -280,6 +281,9 @@ SPH_MODE_REF_CELL_CAP = 1       # LPE_SPH_MODE_REF_CELL_CAP (include/lpe.h)
 SPH_MODE_PROBE_TICK_PASS = 2    # LPE_SPH_MODE_PROBE_TICK_PASS
 
 
+ABI_VERSION = 2                 # LPE_ABI_VERSION of include/lpe.h
+
+
 def lib():
     """Load the in-tree HIP library (raises if it was not built)."""
     global _lib
@@ -291,6 +295,9 @@ def lib():
             f = getattr(L, name)
             f.argtypes = args
             f.restype = res
+        if L.lpe_abi_version() != ABI_VERSION:
+            raise LpeError(f"{LIB_PATH}: ABI version {L.lpe_abi_version()}, this binding needs {ABI_VERSION} "
+                           "(rebuild with `make`)")
         _lib = L
     return _lib
 

@@ -33,7 +33,7 @@ def test_binding_covers_header():
 
 def test_abi_version_and_no_device_status():
     L = lpe.lib()
-    assert L.lpe_abi_version() == 1
+    assert L.lpe_abi_version() == lpe.ABI_VERSION == 2
     if lpe.device_count() == 0:
         h = ctypes.c_void_p()
         assert L.lpe_create(0, ctypes.byref(h)) == 6   # LPE_ERR_NO_DEVICE

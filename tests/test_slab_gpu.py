@@ -304,37 +304,40 @@ def test_slab_stats_and_prelaunch_one_tick_calls():
         np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=k)
 
 
-def test_slab_capacity_overflow_reported():
-    """A rank's slots are fixed at upload (2 n + 4 wire_cap + 4096, lpe_sph.hip
-    slab_cap): C2's 65,536 particles drift right at 8 m/s into a
-    rank that starts empty (36,864 slots), past its capacity by tick ≈ 60.  The
-    next status check (the download) fails with the capacity error.  The domain
-    covers the drift (bbox + 10 m): a fluid that leaves the device grid is the
-    separate open issue of DESIGN.md §7c (profiles/r05/slab_capacity/)."""
+def test_slab_drift_into_empty_rank_grows_grid_and_slots():
+    """VERDICT r5 items 1-2 (profiles/r05/slab_capacity/repro.py, unpadded):
+    C2's 65,536 particles drift right at 8 m/s into a rank that starts empty,
+    with the domain at the pool's bbox + 1 m (slab.setup_rank's default) and a
+    wire of 8,192 records, so 36,864 slots.  Round 5 faulted the GPU between
+    ticks 20 and 30 (the fluid left the rank's device grid) and dropped ghosts
+    once the slots were full.  Now the lagged checks (lpe_sph.hip
+    sph_lag_service) grow the receiving rank's grid ahead of the fluid and its
+    slots past half their use: after 100 ticks every particle is owned by a
+    rank and the merged state equals the single domain's bit for bit."""
     s = scenes.scene("C2")
     fl = dict(s["fluid"])
     n = len(fl["x"])
-    fl["vx"] = np.full(n, 8.0)
+    fl["vx"] = np.full(n, 8.0, np.float32)
     cfg = lpe.default_fluid_config()
     cs = slab.cell_size(cfg)
     c_hi = int(slab._columns(fl["x"], cfg).max())
     edges = np.array([-np.inf, (c_hi + 1) * cs, np.inf], np.float32)
-    pad = 10.0
-    domain = (float(fl["x"].min()) - pad, float(fl["y"].min()) - pad,
-              float(fl["x"].max()) + pad, float(fl["y"].max()) + pad)
+    nt = 100
     ctxs = [lpe.Context(0) for _ in range(2)]
     try:
         for r, c in enumerate(ctxs):
-            slab.setup_rank(c, r, 2, fl, edges, cfg, np.zeros(0, lpe.RIGID_DTYPE), wire_cap=8192, domain=domain)
+            slab.setup_rank(c, r, 2, fl, edges, cfg, np.zeros(0, lpe.RIGID_DTYPE), wire_cap=8192)
         assert ctxs[1].n == 0
-        lpe.mg_loopback_run(ctxs, 80, DT)
-        errs = []
-        for c in ctxs:
-            try:
-                c.sph_download_owned(cap=n)
-            except lpe.LpeError as e:
-                errs.append(str(e))
-        assert any("outgrew its slots" in e for e in errs), errs
+        lpe.mg_loopback_run(ctxs, nt, DT)
+        st = [c.sph_stats() for c in ctxs]
+        parts = [c.sph_download_owned(cap=n) for c in ctxs]
     finally:
         for c in ctxs:
             c.close()
+    assert sum(x["slabOwned"] for x in st) == n
+    assert st[1]["slabOwned"] > n // 2, st[1]
+    assert st[1]["gridRegrows"] >= 1 and st[1]["slotRegrows"] >= 1, st[1]
+    got = slab.merge_owned(parts, n)
+    ref, _, _ = _single(fl, np.zeros(0, lpe.RIGID_DTYPE), nt)
+    for k in slab.FIELDS:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
