@@ -2770,12 +2770,21 @@ __device__ __forceinline__ void stripe_publish_tag(const StripeBufs &sb, int s, 
 __device__ __forceinline__ void stripe_reload_tag(const StripeBufs &sb, int s, int s0, float *lv,
                                                   const unsigned long long *g, uint32_t tag, int32_t *fault) {
     const int b0 = 3 * sb.sbStart[s], b1 = 3 * sb.sbStart[s + 1];
+    // (once a wait has timed out -- this thread's, or any, seen in
+    // the fault word -- the remaining words are not waited for: one timeout
+    // period per stuck solve, not one per word)
+    bool gave_up = (__hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2) != 0;
     for (int i = b0 + (int)threadIdx.x; i < b1; i += STPB) {
         unsigned long long w = __hip_atomic_load(&g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         unsigned spins = 0;
-        while ((uint32_t)(w >> 32) != tag) {
+        while (!gave_up && (uint32_t)(w >> 32) != tag) {
             __builtin_amdgcn_s_sleep(1);
-            if (++spins > (1u << 22)) { atomicOr(fault, 2); break; }      // (as stripe_wait)
+            ++spins;
+            if (spins > (1u << 22)) { atomicOr(fault, 2); gave_up = true; break; }      // (as stripe_wait)
+            if (!(spins & 1023u) && (__hip_atomic_load(fault, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 2)) {
+                gave_up = true;
+                break;
+            }
             w = __hip_atomic_load(&g[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         lv[i - 3 * s0] = __uint_as_float((uint32_t)w);
@@ -3243,12 +3252,8 @@ k_pgs_jacobi(int nb, const int32_t *__restrict__ npptr, const int32_t *__restric
             for (int u = 0; u < 6; u++) {
                 const long long prev = it ? ldp[6 * m + u] : 0ll;
                 const int body = u < 3 ? a : b;
-#ifdef LPE_JAC_PLAIN_STORES   // (profiling only: the sums' stores without the atomics -- wrong results)
-                if (body >= 0) Sn[3 * body + (u % 3)] = q[u] + prev;
-#else
                 if (body >= 0) atomicAdd((unsigned long long *)&Sn[3 * body + (u % 3)],
                                          (unsigned long long)(q[u] + prev));
-#endif
                 ldp[6 * m + u] = q[u];
             }
         }
@@ -4201,6 +4206,27 @@ static int colour_pos(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     return LPE_OK;
 }
 
+// k_pgs_jacobi's blocks meet at a grid barrier every iteration,
+// so all of them must be resident at once.  The most it may launch: its
+// occupancy per CU times the CUs, less one CU per workgroup the position
+// solver's stripe kernel (k_pos_stripes, up to stripe_cap / 2 workgroups of
+// most of a CU's LDS) may hold beside it -- cached per device, at most
+// JAC_BLOCKS_MAX.
+static int jac_cap(lpe_ctx *ctx) {
+    static std::atomic<int> caps[64];
+    const int dev = ctx->device;
+    int cap = (dev >= 0 && dev < 64) ? caps[dev].load(std::memory_order_relaxed) : 0;
+    if (!cap) {
+        int cus = 0, occ = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, k_pgs_jacobi, JAC_TPB, 0) != hipSuccess || occ <= 0)
+            occ = 1;
+        cap = std::max(1, std::min(JAC_BLOCKS_MAX, occ * (cus - stripe_cap(ctx) / 2)));
+        if (dev >= 0 && dev < 64) caps[dev].store(cap, std::memory_order_relaxed);
+    }
+    return cap;
+}
+
 // the Jacobi solver's buffers (JacBufs), grown to nb bodies and nc contacts
 static JacBufs jac_bufs(RigidDev *d) {
     const size_t nb = (size_t)d->cap_jac_nb;
@@ -4230,11 +4256,15 @@ static int jac_launch(lpe_ctx *ctx, RigidDev *d, hipStream_t s) {
     // blocks own at most JAC_CPB contacts each (their rows stay in LDS); in
     // lagged detection nc is the capacity, and a tick with more than
     // JAC_BLOCKS_MAX * JAC_CPB contacts raises the solver fault (counts[7])
-    if (!d->lag && nc > JAC_BLOCKS_MAX * JAC_CPB) {
-        ctx->err = "rigid solver (Jacobi): more than JAC_BLOCKS_MAX * JAC_CPB (98304) contacts";
+    // (the grid barrier needs every block resident at once: at most what
+    // the device holds beside the position solver's stripe workgroups, jac_cap)
+    const int gmax = jac_cap(ctx);
+    if (!d->lag && nc > gmax * JAC_CPB) {
+        ctx->err = "rigid solver (Jacobi): more contacts than its co-resident blocks hold (" +
+                   std::to_string(gmax) + " x JAC_CPB)";
         return LPE_ERR_CAPACITY;
     }
-    const int G = std::max(1, std::min(JAC_BLOCKS_MAX, (nc + JAC_CPB - 1) / JAC_CPB));
+    const int G = std::max(1, std::min(gmax, (nc + JAC_CPB - 1) / JAC_CPB));
     LPE_KERNEL(ctx, "k_pgs_jacobi", k_pgs_jacobi, dim3(G), dim3(JAC_TPB), 0, s, nb, d->counts, d->counts + 1,
                d->ccount, d->cstart, d->rowOf, d->rowN, d->rowR, d->rowAB, d->rowM, c.pgsIterations,
                c.frictionCoeff, d->lamN, d->lamF, d->bodies, (const int32_t *)d->inContact, jac_bufs(d),

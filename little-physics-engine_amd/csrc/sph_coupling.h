@@ -187,12 +187,6 @@ __device__ __forceinline__ void xacc_add(unsigned long long *__restrict__ acc, f
     const unsigned long long v = (unsigned long long)M << (pos & 31);
     unsigned long long lo = v & 0xffffffffull, hi = v >> 32;
     if (u >> 31) { lo = 0ull - lo; hi = 0ull - hi; }             // two's complement limbs
-#ifdef LPE_NO_XACC_ATOMICS
-    // (profiling builds only: the adds skipped, results wrong -- what the
-    // contended atomics cost the coupling)
-    if ((lo | hi) == 0x5a5a5a5a5a5aull) acc[0] = 0;
-    return;
-#endif
     if (lo) atomicAdd(&acc[pos >> 5], lo);
     if (hi) atomicAdd(&acc[(pos >> 5) + 1], hi);
 }
