@@ -30,20 +30,17 @@
 #include "systems/sleep.hpp"
 
 #include "lpe_backend.hpp"
+#include "scenarios/i_scenario.hpp"
+#include "sim.hpp"
 
-/* nticks ticks, then ntimed more with their wall time (timing, when given:
- * [0] seconds of the ntimed ticks, [1] FluidSystem::update, [2]
- * RigidBodyCollisionSystem::update, [3] the other systems (in resident mode
- * SleepSystem runs the whole device tick and the ECS syncs), [4..8] the
- * fluid system's gather / upload / device / download / write-back) */
-static int run_world(int mode, int sync_every, const lpe_rigid_config *rc, const lpe_fluid_config *fc, double spt,
-                     double time_accel, double bta, double ts, int nb, lpe_body *bodies, const double *verts, int nf,
-                     float *x, float *y, float *vx, float *vy, const float *m, float *rho, float *p, int nticks,
-                     int32_t *fluid_gather, int32_t *rigid_gather, int32_t *stats, int ntimed, double *timing) {
-    entt::registry reg;
-    auto se = reg.create();                        /* reset(): SimulatorState first (sim.cpp:93-94) */
-    reg.emplace<Components::SimulatorState>(se, bta, ts);
-    std::vector<entt::entity> bents, fents;
+/* The world's entities (bodies, then the fluid: simple_fluid.cpp's recipe) in
+ * `reg`; their handles in bents / fents. */
+static void make_entities(entt::registry &reg, int nb, const lpe_body *bodies, const double *verts, int nf,
+                          const float *x, const float *y, const float *vx, const float *vy, const float *m,
+                          const float *rho, const float *p, std::vector<entt::entity> &bents,
+                          std::vector<entt::entity> &fents) {
+    bents.clear();
+    fents.clear();
     for (int i = 0; i < nb; i++) {
         const lpe_body &b = bodies[i];
         auto e = reg.create();
@@ -92,22 +89,31 @@ static int run_world(int mode, int sync_every, const lpe_rigid_config *rc, const
         t.density = rho[i];
         t.pressure = p[i];
     }
-    /* the gather orders the drop-in FluidSystem will see (fluid.cpp:259-299, :313-435) */
-    {
-        std::unordered_map<uint32_t, int> fidx, bidx;
-        for (int i = 0; i < nf; i++) fidx[(uint32_t)entt::to_integral(fents[i])] = i;
-        for (int i = 0; i < nb; i++) bidx[(uint32_t)entt::to_integral(bents[i])] = i;
-        int k = 0;
-        auto fv = reg.view<Components::Position, Components::Velocity, Components::Mass,
-                           Components::ParticlePhase, Components::SpeedOfSound, Components::SPHTemp>();
-        for (auto e : fv) if (k < nf) fluid_gather[k++] = fidx[(uint32_t)entt::to_integral(e)];
-        k = 0;
-        auto rv = reg.view<Components::Position, Components::Shape>();
-        for (auto e : rv) if (k < nb) rigid_gather[k++] = bidx[(uint32_t)entt::to_integral(e)];
-        for (; k < nb; k++) rigid_gather[k] = -1;
-    }
+}
 
-    SharedSystemConfig sh{};                       /* every field set (no defaults, shared_system_config.hpp:10-20) */
+/* the gather orders the drop-in FluidSystem will see (fluid.cpp:259-299, :313-435) */
+static void gather_orders(entt::registry &reg, const std::vector<entt::entity> &bents,
+                          const std::vector<entt::entity> &fents, int32_t *fluid_gather, int32_t *rigid_gather) {
+    const int nb = (int)bents.size(), nf = (int)fents.size();
+    std::unordered_map<uint32_t, int> fidx, bidx;
+    for (int i = 0; i < nf; i++) fidx[(uint32_t)entt::to_integral(fents[i])] = i;
+    for (int i = 0; i < nb; i++) bidx[(uint32_t)entt::to_integral(bents[i])] = i;
+    int k = 0;
+    auto fv = reg.view<Components::Position, Components::Velocity, Components::Mass,
+                       Components::ParticlePhase, Components::SpeedOfSound, Components::SPHTemp>();
+    for (auto e : fv) if (k < nf) fluid_gather[k++] = fidx[(uint32_t)entt::to_integral(e)];
+    k = 0;
+    auto rv = reg.view<Components::Position, Components::Shape>();
+    for (auto e : rv) if (k < nb) rigid_gather[k++] = bidx[(uint32_t)entt::to_integral(e)];
+    for (; k < nb; k++) rigid_gather[k] = -1;
+}
+
+/* The scenario configuration of a world (every SharedSystemConfig field set:
+ * it has no defaults, shared_system_config.hpp:10-20) */
+static ScenarioSystemConfig scenario_config(const lpe_rigid_config *rc, const lpe_fluid_config *fc, double spt,
+                                           double time_accel) {
+    ScenarioSystemConfig c{};
+    SharedSystemConfig &sh = c.sharedConfig;
     sh.UniverseSizeMeters = rc->universeSize;
     sh.TimeAcceleration = time_accel;
     sh.MetersPerPixel = rc->metersPerPixel;
@@ -117,6 +123,72 @@ static int run_world(int mode, int sync_every, const lpe_rigid_config *rc, const
     sh.ParticleDensity = 0.0;
     sh.GridSize = 50;
     sh.CellSizePixels = 12.0;
+    static_assert(sizeof(c.fluidConfig) == sizeof(*fc), "FluidConfig mirrors lpe_fluid_config");
+    std::memcpy(&c.fluidConfig, fc, sizeof(c.fluidConfig));
+    c.boundaryConfig.marginPixels = rc->marginPixels;
+    c.boundaryConfig.bounceDamping = rc->bounceDamping;
+    c.boundaryConfig.maxSpeed = rc->maxSpeed;
+    c.gravityConfig.gravitationalAcceleration = rc->gravity;
+    c.gravityConfig.planetaryMassThreshold = rc->planetaryMassThreshold;
+    c.rotationConfig.angularDamping = rc->angularDamping;
+    c.rotationConfig.maxAngularSpeed = rc->maxAngularSpeed;
+    c.sleepConfig.linearSleepThreshold = rc->linearSleepThreshold;
+    c.sleepConfig.angularSleepThreshold = rc->angularSleepThreshold;
+    c.sleepConfig.sleepFramesThreshold = rc->sleepFramesThreshold;
+    c.rigidBodyConfig.pgsIterations = rc->pgsIterations;
+    c.rigidBodyConfig.frictionCoeff = rc->frictionCoeff;
+    c.rigidBodyConfig.positionIterations = rc->posIterations;
+    c.rigidBodyConfig.baumgarte = rc->baumgarte;
+    c.rigidBodyConfig.slop = rc->slop;
+    return c;
+}
+
+/* the bodies' and the fluid's state back from the registry */
+static void read_back(entt::registry &reg, const std::vector<entt::entity> &bents,
+                      const std::vector<entt::entity> &fents, lpe_body *bodies, float *x, float *y, float *vx,
+                      float *vy, float *rho, float *p) {
+    const int nb = (int)bents.size(), nf = (int)fents.size();
+    for (int i = 0; i < nb; i++) {
+        auto e = bents[i];
+        lpe_body &b = bodies[i];
+        const auto &pos = reg.get<Components::Position>(e);
+        b.x = pos.x; b.y = pos.y;
+        if (auto *v = reg.try_get<Components::Velocity>(e)) { b.vx = v->x; b.vy = v->y; }
+        if (auto *a = reg.try_get<Components::AngularPosition>(e)) b.angle = a->angle;
+        if (auto *w = reg.try_get<Components::AngularVelocity>(e)) b.omega = w->omega;
+        if (auto *sl = reg.try_get<Components::Sleep>(e)) {
+            b.sleep_counter = sl->sleepCounter;
+            if (sl->asleep) b.flags |= LPE_BODY_ASLEEP; else b.flags &= ~LPE_BODY_ASLEEP;
+        }
+    }
+    for (int i = 0; i < nf; i++) {
+        auto e = fents[i];
+        const auto &pos = reg.get<Components::Position>(e);
+        const auto &vel = reg.get<Components::Velocity>(e);
+        const auto &t = reg.get<Components::SPHTemp>(e);
+        x[i] = (float)pos.x; y[i] = (float)pos.y;
+        vx[i] = (float)vel.x; vy[i] = (float)vel.y;
+        rho[i] = (float)t.density; p[i] = (float)t.pressure;
+    }
+}
+
+/* nticks ticks, then ntimed more with their wall time (timing, when given:
+ * [0] seconds of the ntimed ticks, [1] FluidSystem::update, [2]
+ * RigidBodyCollisionSystem::update, [3] the other systems (in resident mode
+ * SleepSystem runs the whole device tick and the ECS syncs), [4..8] the
+ * fluid system's gather / upload / device / download / write-back) */
+static int run_world(int mode, int sync_every, const lpe_rigid_config *rc, const lpe_fluid_config *fc, double spt,
+                     double time_accel, double bta, double ts, int nb, lpe_body *bodies, const double *verts, int nf,
+                     float *x, float *y, float *vx, float *vy, const float *m, float *rho, float *p, int nticks,
+                     int32_t *fluid_gather, int32_t *rigid_gather, int32_t *stats, int ntimed, double *timing) {
+    entt::registry reg;
+    auto se = reg.create();                        /* reset(): SimulatorState first (sim.cpp:93-94) */
+    reg.emplace<Components::SimulatorState>(se, bta, ts);
+    std::vector<entt::entity> bents, fents;
+    make_entities(reg, nb, bodies, verts, nf, x, y, vx, vy, m, rho, p, bents, fents);
+    gather_orders(reg, bents, fents, fluid_gather, rigid_gather);
+
+    const ScenarioSystemConfig sc = scenario_config(rc, fc, spt, time_accel);
 
     /* ECSSimulator::createSystems (sim.cpp:103-150) */
     std::vector<std::unique_ptr<Systems::ISystem>> systems;
@@ -128,28 +200,16 @@ static int run_world(int mode, int sync_every, const lpe_rigid_config *rc, const
     systems.push_back(std::make_unique<Systems::RotationSystem>());
     systems.push_back(std::make_unique<Systems::MovementSystem>());
     systems.push_back(std::make_unique<Systems::SleepSystem>());
-    Systems::FluidConfig fcfg;
-    static_assert(sizeof(fcfg) == sizeof(*fc), "FluidConfig mirrors lpe_fluid_config");
-    std::memcpy(&fcfg, fc, sizeof(fcfg));
-    Systems::BoundaryConfig bc; bc.marginPixels = rc->marginPixels; bc.bounceDamping = rc->bounceDamping;
-    bc.maxSpeed = rc->maxSpeed;
-    Systems::GravityConfig gc; gc.gravitationalAcceleration = rc->gravity;
-    gc.planetaryMassThreshold = rc->planetaryMassThreshold;
-    Systems::RotationConfig roc; roc.angularDamping = rc->angularDamping; roc.maxAngularSpeed = rc->maxAngularSpeed;
-    Systems::SleepConfig sc; sc.linearSleepThreshold = rc->linearSleepThreshold;
-    sc.angularSleepThreshold = rc->angularSleepThreshold; sc.sleepFramesThreshold = rc->sleepFramesThreshold;
-    Systems::RigidBodyCollisionConfig rbc; rbc.pgsIterations = rc->pgsIterations;
-    rbc.frictionCoeff = rc->frictionCoeff; rbc.positionIterations = rc->posIterations;
-    rbc.baumgarte = rc->baumgarte; rbc.slop = rc->slop;
     for (auto &sys : systems) {                    /* the dynamic_cast chain of sim.cpp:116-149 */
-        sys->setSharedSystemConfig(sh);
-        if (auto *s = dynamic_cast<Systems::FluidSystem *>(sys.get())) s->setSpecificConfig(fcfg);
-        else if (auto *s = dynamic_cast<Systems::BoundarySystem *>(sys.get())) s->setSpecificConfig(bc);
-        else if (auto *s = dynamic_cast<Systems::BasicGravitySystem *>(sys.get())) s->setSpecificConfig(gc);
-        else if (auto *s = dynamic_cast<Systems::RigidBodyCollisionSystem *>(sys.get())) s->setSpecificConfig(rbc);
-        else if (auto *s = dynamic_cast<Systems::BarnesHutSystem *>(sys.get())) s->setSpecificConfig(Systems::BarnesHutConfig{});
-        else if (auto *s = dynamic_cast<Systems::RotationSystem *>(sys.get())) s->setSpecificConfig(roc);
-        else if (auto *s = dynamic_cast<Systems::SleepSystem *>(sys.get())) s->setSpecificConfig(sc);
+        sys->setSharedSystemConfig(sc.sharedConfig);
+        if (auto *s = dynamic_cast<Systems::FluidSystem *>(sys.get())) s->setSpecificConfig(sc.fluidConfig);
+        else if (auto *s = dynamic_cast<Systems::BoundarySystem *>(sys.get())) s->setSpecificConfig(sc.boundaryConfig);
+        else if (auto *s = dynamic_cast<Systems::BasicGravitySystem *>(sys.get())) s->setSpecificConfig(sc.gravityConfig);
+        else if (auto *s = dynamic_cast<Systems::RigidBodyCollisionSystem *>(sys.get()))
+            s->setSpecificConfig(sc.rigidBodyConfig);
+        else if (auto *s = dynamic_cast<Systems::BarnesHutSystem *>(sys.get())) s->setSpecificConfig(sc.barnesHutConfig);
+        else if (auto *s = dynamic_cast<Systems::RotationSystem *>(sys.get())) s->setSpecificConfig(sc.rotationConfig);
+        else if (auto *s = dynamic_cast<Systems::SleepSystem *>(sys.get())) s->setSpecificConfig(sc.sleepConfig);
     }
     lpe::host::reset();
     lpe::host::setMode(mode ? lpe::host::Mode::Resident : lpe::host::Mode::Strict, sync_every);
@@ -176,28 +236,7 @@ static int run_world(int mode, int sync_every, const lpe_rigid_config *rc, const
     }
     if (mode) lpe::host::residentSync(reg);
 
-    for (int i = 0; i < nb; i++) {
-        auto e = bents[i];
-        lpe_body &b = bodies[i];
-        const auto &pos = reg.get<Components::Position>(e);
-        b.x = pos.x; b.y = pos.y;
-        if (auto *v = reg.try_get<Components::Velocity>(e)) { b.vx = v->x; b.vy = v->y; }
-        if (auto *a = reg.try_get<Components::AngularPosition>(e)) b.angle = a->angle;
-        if (auto *w = reg.try_get<Components::AngularVelocity>(e)) b.omega = w->omega;
-        if (auto *sl = reg.try_get<Components::Sleep>(e)) {
-            b.sleep_counter = sl->sleepCounter;
-            if (sl->asleep) b.flags |= LPE_BODY_ASLEEP; else b.flags &= ~LPE_BODY_ASLEEP;
-        }
-    }
-    for (int i = 0; i < nf; i++) {
-        auto e = fents[i];
-        const auto &pos = reg.get<Components::Position>(e);
-        const auto &vel = reg.get<Components::Velocity>(e);
-        const auto &t = reg.get<Components::SPHTemp>(e);
-        x[i] = (float)pos.x; y[i] = (float)pos.y;
-        vx[i] = (float)vel.x; vy[i] = (float)vel.y;
-        rho[i] = (float)t.density; p[i] = (float)t.pressure;
-    }
+    read_back(reg, bents, fents, bodies, x, y, vx, vy, rho, p);
     auto *fs = dynamic_cast<Systems::FluidSystem *>(systems[0].get());
     auto *rs = dynamic_cast<Systems::RigidBodyCollisionSystem *>(systems[3].get());
     stats[0] = lpe::host::lastStatus();
@@ -267,4 +306,69 @@ extern "C" int lpeh_barnes_hut(double theta, double small_mass, double universe,
             vy[i] = v.y;
         }
     return lpe::host::lastStatus();
+}
+
+/* The reference's own step loop driving the drop-in: the
+ * reference's ECSSimulator (src/sim.cpp, compiled from the reference's
+ * sources against the drop-in's headers by oracle/Makefile.ref) loads a
+ * scenario that creates these entities, takes its ScenarioSystemConfig
+ * through applyConfig's dynamic_cast chain, builds its systems in reset() ->
+ * init() -> createSystems() (sim.cpp:81-150) -- the drop-in's FluidSystem,
+ * RigidBodyCollisionSystem, ... -- and steps them with its own tick()
+ * (sim.cpp:156-163).  Arguments as lpeh_world; stats[0] = the backend's
+ * status (stats[1..3] stay 0: the simulator keeps its systems private). */
+class ArrayScenario : public IScenario {
+public:
+    ScenarioSystemConfig cfg{};
+    int nb = 0, nf = 0;
+    const lpe_body *bodies = nullptr;
+    const double *verts = nullptr;
+    const float *x = nullptr, *y = nullptr, *vx = nullptr, *vy = nullptr, *m = nullptr, *rho = nullptr,
+                *p = nullptr;
+    mutable std::vector<entt::entity> bents, fents;
+    ScenarioSystemConfig getSystemsConfig() const override { return cfg; }
+    void createEntities(entt::registry &reg) const override {
+        make_entities(reg, nb, bodies, verts, nf, x, y, vx, vy, m, rho, p, bents, fents);
+    }
+};
+
+extern "C" int lpeh_ecs_sim(int mode, int sync_every, const lpe_rigid_config *rc, const lpe_fluid_config *fc,
+                            double spt, double time_accel, double bta, double ts, int nb, lpe_body *bodies,
+                            const double *verts, int nf, float *x, float *y, float *vx, float *vy, const float *m,
+                            float *rho, float *p, int nticks, int32_t *fluid_gather, int32_t *rigid_gather,
+                            int32_t *stats) {
+    auto scen = std::make_unique<ArrayScenario>();
+    ArrayScenario *sp = scen.get();
+    sp->cfg = scenario_config(rc, fc, spt, time_accel);
+    sp->nb = nb; sp->bodies = bodies; sp->verts = verts;
+    sp->nf = nf; sp->x = x; sp->y = y; sp->vx = vx; sp->vy = vy; sp->m = m; sp->rho = rho; sp->p = p;
+    ECSSimulator &sim = ECSSimulator::getInstance();
+    {
+        /* reset() carries the SimulatorState over (sim.cpp:83-95) */
+        entt::registry &r0 = sim.getRegistry();
+        auto sv = r0.view<Components::SimulatorState>();
+        if (sv.empty()) {
+            r0.emplace<Components::SimulatorState>(r0.create(), bta, ts);
+        } else {
+            auto &st = r0.get<Components::SimulatorState>(sv.front());
+            st.baseTimeAcceleration = bta;
+            st.timeScale = ts;
+        }
+    }
+    /* SimManager::selectScenario's order (sim_manager.cpp:173-181) */
+    const ScenarioSystemConfig cfg = scen->getSystemsConfig();
+    sim.applyConfig(cfg);
+    sim.loadScenario(std::move(scen));
+    sim.reset();
+    lpe::host::reset();
+    lpe::host::setMode(mode ? lpe::host::Mode::Resident : lpe::host::Mode::Strict, sync_every);
+    entt::registry &reg = sim.getRegistry();
+    gather_orders(reg, sp->bents, sp->fents, fluid_gather, rigid_gather);
+    for (int t = 0; t < nticks; t++) sim.tick();
+    if (mode) lpe::host::residentSync(reg);
+    read_back(reg, sp->bents, sp->fents, bodies, x, y, vx, vy, rho, p);
+    stats[0] = lpe::host::lastStatus();
+    stats[1] = stats[2] = stats[3] = 0;
+    lpe::host::setMode(lpe::host::Mode::Strict, 1);
+    return stats[0];
 }

@@ -24,9 +24,9 @@ needs_build = pytest.mark.skipif(not os.path.exists(HARNESS),
                                  reason="host mirror is built only where /root/reference exists")
 
 
-def _harness():
+def _harness(entry="lpeh_world"):
     L = C.CDLL(HARNESS)
-    f = L.lpeh_world
+    f = getattr(L, entry)
     f.argtypes = [C.c_int, C.c_int, C.POINTER(lpe.RigidConfig), C.POINTER(lpe.FluidConfig),
                   C.c_double, C.c_double, C.c_double, C.c_double, C.c_int, C.c_void_p, C.c_void_p,
                   C.c_int] + [C.c_void_p] * 7 + [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -37,7 +37,9 @@ def _harness():
 @needs_build
 def test_host_mirror_exports():
     L = C.CDLL(HARNESS)
-    assert hasattr(L, "lpeh_world")
+    assert hasattr(L, "lpeh_world") and hasattr(L, "lpeh_ecs_sim")
+    syms = os.popen(f"nm --defined-only -C {HARNESS}").read()
+    assert "ECSSimulator::tick()" in syms      # the reference's sim.cpp is linked in
     syms = os.popen(f"nm -D --defined-only {SYSTEMS}").read()
     for name in ("FluidSystem6update", "RigidBodyCollisionSystem6update", "BoundarySystem6update",
                  "BasicGravitySystem6update", "RotationSystem6update", "MovementSystem6update",
@@ -45,7 +47,7 @@ def test_host_mirror_exports():
         assert name in syms, name
 
 
-def run_world(name, mode, nticks, sync_every=1, expect_status=0):
+def run_world(name, mode, nticks, sync_every=1, expect_status=0, entry="lpeh_world"):
     s = scenes.scene(name) if isinstance(name, str) else name
     b, v = scenes.to_bodies(s["bodies"])
     fl = s["fluid"]
@@ -58,7 +60,7 @@ def run_world(name, mode, nticks, sync_every=1, expect_status=0):
     fg = np.zeros(n, np.int32)
     rg = np.zeros(len(b), np.int32)
     stats = np.zeros(4, np.int32)
-    st = _harness()(mode, sync_every, C.byref(rc), C.byref(fc), DT, 1.0, 1.0, 1.0, len(b),
+    st = _harness(entry)(mode, sync_every, C.byref(rc), C.byref(fc), DT, 1.0, 1.0, 1.0, len(b),
                     bodies.ctypes.data, v.ctypes.data, n,
                     *[arr[k].ctypes.data for k in ("x", "y", "vx", "vy", "mass", "density", "pressure")],
                     nticks, fg.ctypes.data, rg.ctypes.data, stats.ctypes.data)
@@ -81,6 +83,36 @@ def test_host_mirror_tick_matches_oracle(oracle_mod, mode):
     for k in ("x", "y", "angle", "vx", "vy", "omega"):
         np.testing.assert_array_equal(bodies[k], rb[k], err_msg=k)
     assert 0 < stats[1] <= 64 or mode == 1
+
+
+@needs_build
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1], ids=["strict", "resident"])
+def test_reference_ecs_simulator_drives_dropin(oracle_mod, mode):
+    """the reference's OWN step loop -- ECSSimulator from
+    /root/reference/src/sim.cpp, compiled from its sources against the
+    drop-in's headers (oracle/Makefile.ref) -- loads a scenario, applies its
+    ScenarioSystemConfig through the dynamic_cast chain (sim.cpp:41-79),
+    builds the systems in reset() -> createSystems() (sim.cpp:81-150) and
+    calls tick() (sim.cpp:156-163) over the drop-in FluidSystem,
+    RigidBodyCollisionSystem and integrator systems.  One tick equals the
+    whole-tick oracle bit for bit (fluid and bodies), and five ticks equal the
+    restated loop of tests/host_harness.cpp (lpeh_world)."""
+    s, b, v, fl, arr, bodies, fg, rg, stats, rc, fc = run_world("small64_8", mode, 1, entry="lpeh_ecs_sim")
+    assert sorted(fg.tolist()) == list(range(len(fg)))
+    p0 = scenes.particles_aos(fl)[fg]
+    couple = rg[rg >= 0].astype(np.int32)
+    p, rb = oracle_mod.world_tick(fc, rc, p0, b, v, couple, DT, 1)
+    for k, col in (("x", 0), ("y", 1), ("vx", 2), ("vy", 3), ("density", 11), ("pressure", 12)):
+        np.testing.assert_array_equal(arr[k][fg], p[:, col], err_msg=k)
+    for k in ("x", "y", "angle", "vx", "vy", "omega"):
+        np.testing.assert_array_equal(bodies[k], rb[k], err_msg=k)
+    a5 = run_world("small64_8", mode, 5, sync_every=2, entry="lpeh_ecs_sim")
+    r5 = run_world("small64_8", mode, 5, sync_every=2)
+    for k in ("x", "y", "vx", "vy", "density", "pressure"):
+        np.testing.assert_array_equal(a5[4][k], r5[4][k], err_msg=k)
+    for k in ("x", "y", "angle", "vx", "vy", "omega", "sleep_counter", "flags"):
+        np.testing.assert_array_equal(a5[5][k], r5[5][k], err_msg=k)
 
 
 @needs_build
