@@ -125,6 +125,13 @@ def pmc_valu(kernel):
     return _pmc_lookup("pmc_valu.json", kernel, "valu_wave_insts")
 
 
+def rocprof_window(kernel):
+    """(avg us, source, same_build) of `kernel` from the newest committed
+    rocprofv3 kernel trace of the bench command (profiles/r*/rocprof_window.json,
+    profiles/rocpd_summary.py --json over the bench's per-kernel timing window)."""
+    return _pmc_lookup("rocprof_window.json", kernel, "avg_us")
+
+
 def dropin_record():
     """The drop-in timed through the reference's own tick loop (the EnTT host
     harness, profiles/dropin_timing.py), from the newest committed
@@ -197,7 +204,10 @@ def cpu_baseline(scene_name, state=None, budget_s=20.0):
     many, nm = run(allc, budget_s / 2)
     oracle.set_threads(0)
     return dict(value=one, unit="ticks/s", cores=1, kind="port",
-                all_cores=dict(value=many, cores=allc, ticks=nm),
+                all_cores=dict(value=many, cores=allc, ticks=nm,
+                               label="the GPU box's per-GPU CPU share (OMP_NUM_THREADS threads of "
+                                     f"{nproc} hardware threads)" if os.environ.get("OMP_NUM_THREADS")
+                                     else "every hardware thread of the host"),
                 nproc=nproc, cpu_model=cpu_model(),
                 sample=f"{n1} full tick(s) (1 thread) and {nm} (all {allc} threads) of scene {scene_name}"
                        f"{' from the settled device state' if state is not None else ''} ({len(p0)} SPH particles, "
@@ -964,6 +974,13 @@ def main():
                                             "settled metric scene)"
             roof["traffic_same_build"] = tsame
             roof["traffic_frac_of_algorithmic"] = round(traffic / b, 3)
+        ru, rsrc, rsame = rocprof_window(dname) if world == 1 and args.scene == "M" else (None, None, False)
+        if ru:
+            # the same kernel by rocprofv3's kernel trace (the profile committed
+            # under profiles/): the tracer's own clock, beside the HIP events
+            roof["rocprof"] = dict(avg_us=ru, achieved=round(b / (ru * 1e-6) / 1e9, 1),
+                                   frac=round(b / (ru * 1e-6) / 1e9 / HBM_PEAK_GBS, 4), source=rsrc,
+                                   same_build=rsame)
         vi, vsrc, vsame = pmc_valu(dname) if world == 1 and args.scene == "M" else (None, None, False)
         if vi:
             # the compute side of the same launch: VALU instructions (PMC) over

@@ -19,6 +19,8 @@ ap.add_argument("--kernel", default=None, help="only kernels whose name contains
 ap.add_argument("--api", type=int, default=0, help="also the N host API calls (HIP / RCCL regions) of most total time")
 ap.add_argument("--window-kernel", default=None, help="restrict to a window of this kernel's last dispatches")
 ap.add_argument("--window", type=int, default=0, help="... its last N dispatches")
+ap.add_argument("--json", default=None, help="also write {kernel: {calls, avg_us}} + _build (the library's sha256) here")
+ap.add_argument("--lib", default="little-physics-engine_amd/liblpe_hip.so", help="the library profiled (--json stamp)")
 a = ap.parse_args()
 c = sqlite3.connect(a.db)
 cols = [r[1] for r in c.execute("pragma table_info(kernels)")]
@@ -45,6 +47,13 @@ tot = sum(v[1] for v in agg.values())
 print(f"{'kernel':40s} {'calls':>7s} {'avg us':>9s} {'total us':>11s} {'%':>6s}")
 for k, (n, t) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
     print(f"{k[:40]:40s} {n:7d} {t / n:9.2f} {t:11.1f} {100 * t / tot:6.2f}")
+if a.json:
+    import hashlib
+    import json
+    out = {k: dict(calls=n, avg_us=round(t / n, 3)) for k, (n, t) in agg.items()}
+    out["_build"] = dict(lib_sha256=hashlib.sha256(open(a.lib, "rb").read()).hexdigest(),
+                         window=f"last {a.window} dispatches of {a.window_kernel}" if a.window_kernel else "all")
+    json.dump(out, open(a.json, "w"), indent=1)
 if rows:
     span = (rows[-1][2] - rows[0][1]) / 1e3
     print(f"dispatches {len(rows)}, span {span:.1f} us, kernel time {tot:.1f} us")
