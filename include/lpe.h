@@ -480,6 +480,12 @@ int  lpe_sph_set_slab(lpe_ctx *ctx, int nranks, int rank, const float *edges, in
 int  lpe_sph_slab_info(lpe_ctx *ctx, int cap, int32_t *edges, int *nranks, int *move);
 /* Global particle ids of the n uploaded (owned) particles (default 0..n-1). */
 int  lpe_sph_set_ids(lpe_ctx *ctx, int n, const int32_t *ids);
+/* A slab rank: the particle count of the whole fluid (ids 0..n_global-1;
+ * the reference's particleCount, fluid.cpp:981-984, bounds the values its
+ * capped-cell loop takes for ids, fluid_kernels.metal:284-286).  Needed
+ * before LPE_SPH_MODE_REF_CELL_CAP on a slab rank, which then files ghosts
+ * in 3 columns each side instead of 2 (size wire_cap for them).  ABI 2. */
+int  lpe_sph_set_global_count(lpe_ctx *ctx, int n_global);
 /* The particles this context owns with their global ids (*n_out = count;
  * LPE_ERR_CAPACITY if it exceeds cap); in device order without a slab (ids
  * 0..n-1 permuted), in no particular order on a slab rank. */

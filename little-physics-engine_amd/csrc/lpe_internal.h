@@ -168,7 +168,8 @@ enum StatusSlot {
     ST_SLAB_CAPACITY = 18,  // slab decomposition: the received ghosts did not fit the rank's slots
     ST_FORCES_GLOBAL = 19,  // forces blocks whose neighbourhood did not fit the LDS image (global gathers)
     ST_SLOT_PEAK = 20,      // slab decomposition: most slots a sub-step's hash wanted (own + received ghosts)
-    ST_COUNT = 21
+    ST_REF_SLAB = 21,       // slab rank, reference cell-capacity mode: the literal loop needed a cell it does not hold
+    ST_COUNT = 22
 };
 
 }  // namespace lpe

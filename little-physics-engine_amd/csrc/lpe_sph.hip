@@ -193,24 +193,52 @@ __device__ __forceinline__ void bucket_file(const FastKick &fk, uint32_t k, int 
 // SLAB_BAND cell columns along an edge -- as ghost records in that
 // neighbour's send buffer.
 static constexpr int SLAB_BAND = 2;                  // ghost cell columns each side of an edge
+// ... in the reference cell-capacity mode: more, the cells the reference's
+// literal loop reads on into past an over-full cell of the relevant columns
+// (ref_cap_walk, metal:281-283): a cell of K > 64 particles reads
+// ceil((K - 64) / 65) cells further.  The sender files SLAB_BAND_CAP columns
+// plus that many for the largest cell seen so far (ST_MAX_OCC_TOTAL, one
+// column of margin), at most SLAB_BAND_MAX, and tells the receiver in the
+// wire header how many it sent (slab_band).
+static constexpr int SLAB_BAND_CAP = 3;
+static constexpr int SLAB_BAND_MAX = 8;
 static constexpr uint32_t KEY_DEAD = 0xFFFFFFFFu;    // a slot the sub-step drops (no bin)
 struct SlabKick {
     int on;
     const int32_t *edges;     // device [nranks + 1] edge cell columns
     int rank, hasL, hasR;
+    int band;                 // ghost columns filed each side (SLAB_BAND, or SLAB_BAND_CAP at least)
+    const int32_t *occ;       //   capped cells: the largest cell so far (ST_MAX_OCC_TOTAL), else null
+    int32_t *rband;           //   [2]: the columns the left / right neighbour sent last (k_ghost_unpack)
     float *sL, *sR;           // send buffers: HDR header floats, then wcap records of GREC floats
     int wcap;
     const int32_t *nslot;     // k_kick_drift: the P slots in use
 };
+// the ghost columns this sub-step files each side (wave-uniform); every
+// block that files records its band in the wire header's word [1] as
+// SLAB_BAND_MAX - band by an atomic max, so the receiver learns the fewest
+// columns any block sent completely (0, the cleared header: no block filed,
+// the sender has no particle there -- all SLAB_BAND_MAX columns are empty)
+__device__ __forceinline__ int slab_band(const SlabKick &sk) {
+    if (!sk.occ) return sk.band;
+    const int K = __builtin_amdgcn_readfirstlane(*sk.occ);
+    const int extra = K > LPE_REF_MAX_PER_CELL ? (K - LPE_REF_MAX_PER_CELL + LPE_REF_MAX_PER_CELL) / 65 : 0;
+    return min(SLAB_BAND_MAX, sk.band + extra);
+}
+__device__ __forceinline__ void slab_band_note(const SlabKick &sk, int band) {
+    if (threadIdx.x != 0) return;
+    if (sk.hasL) atomicMax((int *)sk.sL + 1, SLAB_BAND_MAX - band);
+    if (sk.hasR) atomicMax((int *)sk.sR + 1, SLAB_BAND_MAX - band);
+}
 // wave-aggregated append of this lane's particle to the send buffers of the
-// sides it is bound for (gx: its kicked bin's column); every lane of the
-// wave calls it
-__device__ __forceinline__ void slab_file(const SlabKick &sk, int cx0, int cx1, bool active, int gx, float px,
+// sides it is bound for (gx: its kicked bin's column, band: slab_band); every
+// lane of the wave calls it
+__device__ __forceinline__ void slab_file(const SlabKick &sk, int band, int cx0, int cx1, bool active, int gx, float px,
                                           float py, float vx, float vy, float hx, float hy, float ms, int id,
                                           int32_t *__restrict__ status) {
     const int lane = lane_id();
     for (int side = 0; side < 2; side++) {
-        const bool go = active && (side == 0 ? (sk.hasL && gx < cx0 + SLAB_BAND) : (sk.hasR && gx >= cx1 - SLAB_BAND));
+        const bool go = active && (side == 0 ? (sk.hasL && gx < cx0 + band) : (sk.hasR && gx >= cx1 - band));
         const unsigned long long bal = __ballot(go);
         if (!bal) continue;
         float *buf = side == 0 ? sk.sL : sk.sR;
@@ -262,8 +290,12 @@ k_kick_drift(int n, float dt, float hdt, int first, int probe, float eps, float 
     const int iters = (n + stride - 1) / stride;
     // a slab rank: its P slots in use (sk.nslot), the dead ones (id -1) skipped
     const int nn = sk.on ? min(*sk.nslot, n) : n;
-    int cx0 = 0, cx1 = 0;
-    if (sk.on) slab_cols(sk, cx0, cx1);
+    int cx0 = 0, cx1 = 0, band = 0;
+    if (sk.on) {
+        slab_cols(sk, cx0, cx1);
+        band = slab_band(sk);
+        slab_band_note(sk, band);                           // (the receiver's reach)
+    }
     for (int it = 0; it < iters; it++) {
         int i = it * stride + blockIdx.x * TPB + threadIdx.x;
         bool active = i < nn;
@@ -294,7 +326,7 @@ k_kick_drift(int n, float dt, float hdt, int first, int probe, float eps, float 
             mny = fminf(mny, py); mxy = fmaxf(mxy, py);
             if (sk.on) ms = P.m[i];
         }
-        if (sk.on) slab_file(sk, cx0, cx1, active, kx + ox, px, py, vx, vy, hx, hy, ms, id, status);
+        if (sk.on) slab_file(sk, band, cx0, cx1, active, kx + ox, px, py, vx, vy, hx, hy, ms, id, status);
         int len; bool st;
         const int first = wave_runs(k, active, &len, &st);
         if (fk.on && fk.bucket) {
@@ -354,17 +386,19 @@ __device__ __forceinline__ GridParams grid_from_bbox(float minX, float maxX, flo
 // clamped to the edge by bin_key): the sub-step raises ST_CAP_OVERFLOW (the
 // call fails with LPE_ERR_CAPACITY), and every walk, which clips to g, stays
 // inside the bins that exist -- no access outside the grid's buffers.  A
-// slab rank (slab != 0) clips too, but its reference grid is the global one
-// (every rank's bbox) and its device grid covers only its slab's columns
-// and the ghost band (lpe_sph_cover_box): there only a clip in y is a
-// failure (a particle beyond its slab's columns is ST_HALO_DRIFT, or was
-// clamped by bin_key).
+// slab rank (slab != 0) clips only in y: its reference grid is the global
+// one (every rank's bbox) while its device grid covers only its slab's
+// columns and the ghost bands (lpe_sph_cover_box), and the reference
+// cell-capacity mode's flat cell order needs the global columns -- the walks
+// that could leave the device grid in x clip to it themselves (hood_spans,
+// walk_ranges, ref_cap_walk / ref_cap_slow).
 __device__ __forceinline__ GridParams clip_grid(GridParams g, int ox, int oy, int W, int H, int slab, bool *clipped) {
-    const int x0 = max(g.gridMinX, ox), y0 = max(g.gridMinY, oy);
-    const int x1 = min(g.gridMinX + g.gridDimX - 1, ox + W - 1), y1 = min(g.gridMinY + g.gridDimY - 1, oy + H - 1);
+    const int x0 = slab ? g.gridMinX : max(g.gridMinX, ox), y0 = max(g.gridMinY, oy);
+    const int x1 = slab ? g.gridMinX + g.gridDimX - 1 : min(g.gridMinX + g.gridDimX - 1, ox + W - 1);
+    const int y1 = min(g.gridMinY + g.gridDimY - 1, oy + H - 1);
     const bool cx = x0 != g.gridMinX || x1 != g.gridMinX + g.gridDimX - 1;
     const bool cy = y0 != g.gridMinY || y1 != g.gridMinY + g.gridDimY - 1;
-    *clipped = cy || (cx && !slab);
+    *clipped = cx || cy;
     if (!cx && !cy) return g;
     g.gridMinX = x0; g.gridMinY = y0;
     g.gridMaxX = max(x1, x0); g.gridMaxY = max(y1, y0);
@@ -789,8 +823,10 @@ k_scan_rows(int W, int H, int ox, int oy, float eps, const int32_t *__restrict__
             const bool mine = gx >= ocx0 && gx < ocx1;
             if (!mine) {
             } else if (in) tmax = max(tmax, sum); else tout += sum;
-            if (in && mine && sum > LPE_REF_MAX_PER_CELL) {
-                tover++;
+            // (the over-full list covers a slab rank's ghost columns too: the
+            // first ghost column's densities walk them)
+            if (in && sum > LPE_REF_MAX_PER_CELL) {
+                if (mine) tover++;
                 if (ovl) ovl_append(ovl, gx, gy);
             }
         }
@@ -986,6 +1022,7 @@ __device__ __forceinline__ bool ref_cap_slow(float xi, float yi, float eps, cons
         for (int nx = -1; nx <= 1; nx++) {
             const int cx = cellX + nx, cy = cellY + ny;
             if (cx < 0 || cx >= g.gridDimX || cy < 0 || cy >= g.gridDimY) continue;
+            if (cx + g.gridMinX < ox || cx + g.gridMinX >= ox + W) continue;   // (slab rank: no bins there)
             const int b = ref_cell_base(cy * g.gridDimX + cx, g, W, ox, oy);
             over |= start[b + 4] - start[b] > LPE_REF_MAX_PER_CELL;
         }
@@ -1017,20 +1054,47 @@ __device__ __forceinline__ bool ref_cap_near(const int32_t *__restrict__ ovl, in
 // into the following cells' words: a count (read as an id), the next cell's
 // first members, zeros of the memset buffer.  ld(slot) loads a record,
 // f(slot, rec) consumes it, for every value read that is < n.
+// On a slab rank (sk.on) the reference's buffer is the GLOBAL grid's, of
+// which the rank holds its own columns and sk.band ghost columns each side
+// (every particle of those cells): the cells the loop reads are the 3 x 3
+// of the particle -- local for every particle whose density or forces the
+// rank keeps (its own columns and the first ghost column each side, the
+// "relevant" ones) -- and, past an over-full cell, the cells after it in
+// the flat order: with SLAB_BAND_CAP ghost columns one more column is
+// local; a read past that (a cell of more than 129, or the row wrap of the
+// global grid's last column) raises ST_REF_SLAB for a relevant particle
+// (the call fails: the rank cannot know the count of a cell it does not
+// hold).  A value read as an id is a particle of the whole fluid (n = its
+// global count); one that is not on the rank lies more than a column (2h)
+// from every relevant particle, so its term is +0 / no neighbour: skipped,
+// the sums unchanged.  nslot: the rank's sorted slots (refInv is validated
+// against sid: stale entries of particles that left are never used).
 template <int U, class L, class F>
 __device__ void ref_cap_walk(float xi, float yi, float eps, const GridParams &g, int W, int ox, int oy,
                              const int32_t *__restrict__ start, const int32_t *__restrict__ sid,
-                             const int32_t *__restrict__ refInv, int n, int32_t *__restrict__ status, L ld, F f) {
+                             const int32_t *__restrict__ refInv, int n, int32_t *__restrict__ status, L ld, F f,
+                             const SlabKick &sk = SlabKick{}, int nslot = 0) {
     constexpr int CI = LPE_REF_MAX_PER_CELL + 1;
     const int cellX = (int)floorf((xi + eps) / g.cellSize) - g.gridMinX;
     const int cellY = (int)floorf((yi + eps) / g.cellSize) - g.gridMinY;
     const long C = (long)g.gridDimX * g.gridDimY;
+    int lo = -(1 << 30), hi = 1 << 30;              // the rank's local columns (absolute)
+    bool relevant = true;
+    if (sk.on) {
+        int cx0, cx1;
+        slab_cols(sk, cx0, cx1);
+        if (sk.hasL) lo = cx0 - sk.rband[0];
+        if (sk.hasR) hi = cx1 + sk.rband[1] - 1;
+        const int pc = cellX + g.gridMinX;
+        relevant = pc >= cx0 - 1 && pc <= cx1;
+    }
     // the bin base of reference cell (cx, cy) of the flat index
     auto base = [&](int cx, int cy) { return (((cy + g.gridMinY - oy) * W) + (cx + g.gridMinX - ox)) << 2; };
     for (int ny = -1; ny <= 1; ny++)
         for (int nx = -1; nx <= 1; nx++) {
             const int cx = cellX + nx, cy = cellY + ny;
             if (cx < 0 || cx >= g.gridDimX || cy < 0 || cy >= g.gridDimY) continue;
+            if (cx + g.gridMinX < ox || cx + g.gridMinX >= ox + W) continue;   // (slab rank: no bins there)
             const int b0 = base(cx, cy);
             const int s0 = start[b0], count = start[b0 + 4] - s0;
             const int m = min(count, LPE_REF_MAX_PER_CELL);
@@ -1053,7 +1117,13 @@ __device__ void ref_cap_walk(float xi, float yi, float eps, const GridParams &g,
                     atomicOr(&status[ST_REF_UB], 1);
                 } else {
                     if (!have) {
-                        if (ccx >= g.gridDimX) { ccx = 0; ccy++; }
+                        bool wrap = false;
+                        if (ccx >= g.gridDimX) { ccx = 0; ccy++; wrap = true; }
+                        const int col = ccx + g.gridMinX;
+                        if (col < lo || col > hi) {             // (slab rank: a cell it does not hold)
+                            if (relevant) atomicOr(&status[ST_REF_SLAB], wrap ? 2 : 1);
+                            break;
+                        }
                         bb = base(ccx, ccy);
                         bcnt = start[bb + 4] - start[bb];
                         have = true;
@@ -1064,7 +1134,10 @@ __device__ void ref_cap_walk(float xi, float yi, float eps, const GridParams &g,
                 }
                 if (++j == CI) { j = 0; cc++; ccx++; have = false; }
                 if (id >= n) continue;
-                if (slot < 0) slot = refInv[id];
+                if (slot < 0) {
+                    slot = refInv[id];
+                    if (sk.on && (slot < 0 || slot >= nslot || sid[slot] != id)) continue;   // (not on the rank)
+                }
                 f(slot, ld(slot));
             }
         }
@@ -1284,13 +1357,15 @@ __device__ __forceinline__ void wave_minmax(int v, int &mn, int &mx) {
 // at most one past the exact one, so it stays inside the staged cells.
 __device__ __forceinline__ void hood_spans(const Hood &hd, const int *lbnd, float xi, float yi, float eps,
                                            float cs, float reach, int cyp, const GridParams &g, int b[3],
-                                           int e[3], int shift[3]) {
+                                           int e[3], int shift[3], int gx0, int gx1) {
     const float rcs = 2.0f / cs;
     const float u = (xi + eps) * rcs, v = (yi + eps) * rcs;
     const float wu = reach + fabsf(u) * 0x1p-20f + 1e-5f, wv = reach + fabsf(v) * 0x1p-20f + 1e-5f;
     const int bx0 = (int)floorf(u - wu), bx1 = (int)floorf(u + wu);
     const int by0 = (int)floorf(v - wv), by1 = (int)floorf(v + wv);
-    const int cxa = max(bx0 >> 1, g.gridMinX), cxb = min(bx1 >> 1, g.gridMinX + g.gridDimX - 1);
+    // (and to the device grid's columns [gx0, gx1]: a slab rank's reference
+    // grid is the global one, wider than its device grid)
+    const int cxa = max(max(bx0 >> 1, g.gridMinX), gx0), cxb = min(min(bx1 >> 1, g.gridMinX + g.gridDimX - 1), gx1);
     const int cya = max(by0 >> 1, g.gridMinY), cyb = min(by1 >> 1, g.gridMinY + g.gridDimY - 1);
     const int r3 = (cyp == hd.cy0) ? 0 : 3;
     const int qa = max(bx0 - 2 * cxa, 0), qb = min(bx1 - 2 * cxb, 1);
@@ -1329,7 +1404,7 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
           float *__restrict__ rho, float *__restrict__ pr, uint4 *__restrict__ nlist,
           int32_t *__restrict__ ncount, int32_t *__restrict__ status, const int32_t *__restrict__ sid,
           const int32_t *__restrict__ refInv, const int32_t *__restrict__ ovl, Hood *__restrict__ fplans,
-          HeavyOut ho) {
+          HeavyOut ho, SlabKick sk, int nref) {
     __shared__ float4 lrec[HCAP + 4];                     // + 4: the span walk reads up to 3 past a span
     __shared__ int hcand[5];                              // (NL, ho.list: the waves' coupling pairs; quartiles)
     __shared__ int lbnd[HBND];
@@ -1433,7 +1508,7 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
         // the wave's shortest span, masked ones up to its longest.  LDS reads
         // at immediate offsets.
         int sb[3], se[3], sh[3];
-        hood_spans(hd, lbnd, xi, yi, eps, cs, reach, cyp, g, sb, se, sh);
+        hood_spans(hd, lbnd, xi, yi, eps, cs, reach, cyp, g, sb, se, sh, ox, ox + W - 1);
 #pragma unroll
         for (int r = 0; r < 3; r++)
             if (!live || slow) sb[r] = se[r] = 0;
@@ -1505,11 +1580,12 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     if (slow) {
         // (the neighbour list in the literal order, repeats included: the
         // forces pass then sums exactly what the reference's loop visits)
-        ref_cap_walk<4>(xi, yi, eps, g, W, ox, oy, start, sid, refInv, nn, status,
+        ref_cap_walk<4>(xi, yi, eps, g, W, ox, oy, start, sid, refInv, sk.on ? nref : nn, status,
                         [&](int k) { return nbA[k]; },
                         [&](int k, const float4 &o) {
                             if (term(o, true) && NL && k != s) emit(k - s, k - s >= -32768 && k - s <= 32767);
-                        });
+                        },
+                        sk, nn);
     }
     DTRMAX(2, wall_clock64());
     DTRMAX(5, (unsigned long long)cnt);
@@ -1662,8 +1738,8 @@ __device__ __forceinline__ f2v pair_tile(const Hood &hd, const float4 *lrec, con
         const int cya = oy + (int)((unsigned)__float_as_int(pa.w) >> 17);   // the bin's cell row (k_rank_permute)
         const int cyb = oy + (int)((unsigned)__float_as_int(pb.w) >> 17);
         int Ab[3], Ae[3], Bb[3], Be[3], sh[3];
-        hood_spans(hd, lbnd, pa.x, pa.y, eps, cs, reach, cya, g, Ab, Ae, sh);
-        hood_spans(hd, lbnd, pb.x, pb.y, eps, cs, reach, cyb, g, Bb, Be, sh);
+        hood_spans(hd, lbnd, pa.x, pa.y, eps, cs, reach, cya, g, Ab, Ae, sh, ox, ox + W - 1);
+        hood_spans(hd, lbnd, pb.x, pb.y, eps, cs, reach, cyb, g, Bb, Be, sh, ox, ox + W - 1);
         const bool strad = la && lv && cya != cyb;           // one pair per tile at most
 #pragma unroll
         for (int r = 0; r < 3; r++) {
@@ -1831,6 +1907,7 @@ struct SphStepParams {
     const int32_t *ovl;       //   and the sub-step's over-cap cells (ovl_append)
     int nblk, chunk;          // forces pass: logical blocks, blocks per XCD run (0: plain order)
     int32_t *mergePre;        // sub-step 0 after a prelaunch: its stats to merge into status (else null)
+    int nref;                 // slab rank: the whole fluid's particle count (ref_cap_walk's id bound)
 };
 
 // computeForces + velocityVerletFinish + impulse + push-out; reads the sorted
@@ -1864,6 +1941,7 @@ __device__ __forceinline__ void merge_prestats_dev(int32_t *__restrict__ st, int
     atomicOr(&st[ST_HALO_DRIFT], pre[ST_HALO_DRIFT]);
     atomicOr(&st[ST_SLAB_CAPACITY], pre[ST_SLAB_CAPACITY]);
     atomicOr(&st[ST_LIST_OVERFLOW], pre[ST_LIST_OVERFLOW]);
+    atomicOr(&st[ST_REF_SLAB], pre[ST_REF_SLAB]);
     atomicMax(&st[ST_RX_GHOST_L], pre[ST_RX_GHOST_L]);
     atomicMax(&st[ST_RX_GHOST_R], pre[ST_RX_GHOST_R]);
     atomicMax(&st[ST_SLOT_PEAK], pre[ST_SLOT_PEAK]);
@@ -2139,9 +2217,10 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         // reference cell-capacity mode, the literal loop's neighbours past the
         // list's capacity: the loop itself (metal:345-351; nbrID == globalID
         // is skipped)
-        ref_cap_walk<4>(xi, yi, sp.eps, g, sp.W, sp.ox, sp.oy, start, S.id, sp.refInv, sp.n, status,
+        ref_cap_walk<4>(xi, yi, sp.eps, g, sp.W, sp.ox, sp.oy, start, S.id, sp.refInv,
+                        sp.own.on ? sp.nref : sp.n, status,
                         [&](int k) { return FRec{nbA[k], nbB[k]}; },
-                        [&](int k, const FRec &o) { if (k != s) pair(o.a, o.b); });
+                        [&](int k, const FRec &o) { if (k != s) pair(o.a, o.b); }, sp.own, nn);
     } else if (cnt <= NLIST_CAP) {
         // the density pass's list: the r^2 < h^2 neighbours in canonical
         // order, so the heavy pair math runs only on real neighbours.
@@ -2266,8 +2345,12 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
             mnx = mxx = px;
             mny = mxy = py;
         }
-        if (kn.sk.on)                                  // (the whole wave: ballots)
-            slab_file(kn.sk, ocx0, ocx1, live, kx + kn.ox, px, py, st.vx, st.vy, hx, hy, st.mass, S.id[sl], status);
+        if (kn.sk.on) {                                // (the whole wave: ballots)
+            const int band = slab_band(kn.sk);
+            slab_band_note(kn.sk, band);               // (the receiver's reach)
+            slab_file(kn.sk, band, ocx0, ocx1, live, kx + kn.ox, px, py, st.vx, st.vy, hx, hy, st.mass, S.id[sl],
+                      status);
+        }
         int len; bool stt;
         const int first = wave_runs(k, live, &len, &stt);
         if (kn.fk.on && kn.fk.bucket) {
@@ -2353,12 +2436,14 @@ struct Shard {
     float4 *bbG = nullptr;         // the global bbox (minX, maxX, minY, maxY)
     float *hist = nullptr;         // rebalancing: owned particles per universe column
     int hcol0 = 0, hcols = 0;
+    int nglobal = 0;               // the whole fluid's particle count (lpe_sph_set_global_count)
 };
 
+static int sh_nglobal(const SphDev &d) { return d.shard ? d.shard->nglobal : 0; }
 static void slab_clip_cols(const SphDev &d, long &gx0, long &gx1) {
     if (!d.shard) return;
     const Shard &h = *d.shard;
-    const long m = h.mv + SLAB_BAND + 8;
+    const long m = h.mv + SLAB_BAND_MAX + 8;
     if (h.hasL) gx0 = std::max<long>(gx0, h.e0[h.rank] - m);
     if (h.hasR) gx1 = std::min<long>(gx1, h.e0[h.rank + 1] + m);
 }
@@ -2414,11 +2499,14 @@ k_ghost_unpack(const float *__restrict__ rL, const float *__restrict__ rR, int w
         *bbG = make_float4(b.x, -b.z, b.y, -b.w);
         *nin = base + min(gL + gR, room);
         if (gL + gR > room) atomicOr(&status[ST_SLAB_CAPACITY], 1);
+        // the columns each neighbour sent (the literal capped walk's reach)
+        sk.rband[0] = rL ? SLAB_BAND_MAX - ((const int *)rL)[1] : 0;
+        sk.rband[1] = rR ? SLAB_BAND_MAX - ((const int *)rR)[1] : 0;
         atomicMax(&status[ST_SLOT_PEAK], base + gL + gR);
         atomicMax(&status[ST_RX_GHOST_L], rL ? *(const int *)rL : 0);
         atomicMax(&status[ST_RX_GHOST_R], rR ? *(const int *)rR : 0);
-        if (sL) *(int *)sL = 0;
-        if (sR) *(int *)sR = 0;
+        if (sL) { ((int *)sL)[0] = 0; ((int *)sL)[1] = 0; }
+        if (sR) { ((int *)sR)[0] = 0; ((int *)sR)[1] = 0; }
     }
     const bool active = t < gL + gR && t < room;
     uint32_t k = KEY_DEAD;
@@ -3026,7 +3114,8 @@ static int sph_realloc_slots(lpe_ctx *ctx, int n) {
     LPE_HIP(ctx, hipMalloc((void **)&d.key, sizeof(uint32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpId, sizeof(int32_t) * N));
     LPE_HIP(ctx, hipMalloc((void **)&d.tmpOld, sizeof(int32_t) * N));
-    LPE_HIP(ctx, hipMalloc((void **)&d.refInv, sizeof(int32_t) * N));
+    // (id -> sorted slot: a slab rank's ids are the whole fluid's, lpe_sph_set_global_count)
+    LPE_HIP(ctx, hipMalloc((void **)&d.refInv, sizeof(int32_t) * std::max(N, (size_t)std::max(sh_nglobal(d), 0))));
     LPE_HIP(ctx, hipMalloc((void **)&d.stage, sizeof(float) * N));
     // the grid hash's overflow lists (one entry per particle at most; both counts start at 0)
     if (d.bovf) (void)hipFree(d.bovf);
@@ -3434,6 +3523,7 @@ static bool sph_heavy_on(const SphDev &d) {
     return !off && !chunked && d.nr >= HEAVY_MIN_RIGIDS && d.rbinStart && d.heavy && d.tileHeavy;
 }
 
+static SlabKick slab_kick(const SphDev &d);
 static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr, float *rho, float *pr, bool nl = true) {
     SphDev &d = ctx->sph;
     const lpe_fluid_config &c = d.cfg;
@@ -3471,13 +3561,14 @@ static int sph_density(lpe_ctx *ctx, int n, const int32_t *nptr, float *rho, flo
         LPE_KERNEL(ctx, "k_density", k_density<true>, dim3(xcd_grid(nblk(n, HB))), dim3(HB), 0, ctx->stream, n,
                    nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
                    c.restDensity, d.W, d.H, d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)d.nbB,
-                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d), d.ovl_cur, sph_fplans(d), ho);
+                   rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d), d.ovl_cur, sph_fplans(d), ho,
+                   slab_kick(d), d.shard ? d.shard->nglobal : 0);
     } else
         LPE_KERNEL(ctx, "k_density", k_density<false>, dim3(xcd_grid(nblk(n, HB))), dim3(HB), 0, ctx->stream, n,
                    nptr, d.cap_n, c.gridConfig.smoothingLength, c.gridConfig.gridEpsilon, c.stiffness,
                    c.restDensity, d.W, d.H, d.ox, d.oy, d.gp_cur, d.start, d.nbA, (float2 *)d.nbB,
                    rho, pr, d.nlist, d.ncount, d.stat_cur, d.S.id, sph_ref_inv(d), d.ovl_cur, (Hood *)nullptr,
-                   HeavyOut{});
+                   HeavyOut{}, slab_kick(d), d.shard ? d.shard->nglobal : 0);
     LPE_CHECK_LAUNCH(ctx, "k_density");
     return LPE_OK;
 }
@@ -3499,6 +3590,10 @@ static SlabKick slab_kick(const SphDev &d) {
     sk.on = 1;
     sk.edges = h->edges;
     sk.rank = h->rank; sk.hasL = h->hasL; sk.hasR = h->hasR;
+    const bool capped = (d.mode & LPE_SPH_MODE_REF_CELL_CAP) != 0;
+    sk.band = capped ? SLAB_BAND_CAP : SLAB_BAND;
+    sk.occ = capped ? d.status + ST_MAX_OCC_TOTAL : nullptr;
+    sk.rband = h->cnt + 4;
     sk.sL = h->sL; sk.sR = h->sR; sk.wcap = h->wcap;
     sk.nslot = h->cnt + h->cur;
     return sk;
@@ -3843,6 +3938,7 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
     sp.refInv = sph_ref_inv(d);
     sp.nptr = nullptr;
     sp.own = slab_kick(d);            // (on a slab rank: the slots it owns)
+    sp.nref = sh_nglobal(d);
     sp.nstride = d.cap_n;
     Shard *sh = d.shard;
     if (sh && !ctx->transport) {
@@ -3997,6 +4093,15 @@ static int status_error(lpe_ctx *ctx, const int32_t *status) {
         ctx->err = "a rigid coupling force left the exact accumulator's range (|f| >= 2^64 or not finite)";
         return LPE_ERR_OVERFLOW;
     }
+    if (status[ST_REF_SLAB]) {
+        ctx->err = std::string("slab decomposition, reference cell-capacity mode: the reference's loop read past an "
+                               "over-full cell into a cell the rank does not hold (") +
+                   ((status[ST_REF_SLAB] & 1) ? "a cell of more than 129 particles at the ghost band's edge" : "") +
+                   ((status[ST_REF_SLAB] & 3) == 3 ? "; " : "") +
+                   ((status[ST_REF_SLAB] & 2) ? "the global grid's row wrap: an over-full cell in its last column" : "") +
+                   ")";
+        return LPE_ERR_CAPACITY;
+    }
     if (status[ST_HALO_OVERFLOW]) {
         ctx->err = "slab decomposition: more ghost records than wire_cap along a slab edge in a sub-step (raise "
                    "wire_cap of lpe_sph_set_slab)";
@@ -4101,10 +4206,13 @@ extern "C" int lpe_sph_get_stats(lpe_ctx *ctx, lpe_sph_stats *out) {
 extern "C" int lpe_sph_set_mode(lpe_ctx *ctx, int flags) {
     if (!ctx || (flags & ~(LPE_SPH_MODE_REF_CELL_CAP | LPE_SPH_MODE_PROBE_TICK_PASS))) return LPE_ERR_ARG;
     SphDev &d = ctx->sph;
-    if ((flags & LPE_SPH_MODE_REF_CELL_CAP) && d.shard) {
-        ctx->err = "the reference cell-capacity mode is single-domain only (not on a slab rank)";
+    if ((flags & LPE_SPH_MODE_REF_CELL_CAP) && d.shard && d.shard->nglobal <= 0) {
+        ctx->err = "slab rank: the reference cell-capacity mode needs the whole fluid's particle count "
+                   "(lpe_sph_set_global_count) and a wire sized for SLAB_BAND_CAP ghost columns";
         return LPE_ERR_STATE;
     }
+    // (every rank of a slab group sets the same mode at the same point: the
+    // band it files ghosts in follows it, slab_kick)
     int st = sph_void_prelaunch(ctx);        // a prelaunched sub-step ran in the old mode
     if (st) return st;
     d.mode = flags;
@@ -4237,8 +4345,9 @@ extern "C" int lpe_sph_set_slab(lpe_ctx *ctx, int nranks, int rank, const float 
     LPE_HIP(ctx, hipMalloc((void **)&h->edges0, E));
     LPE_HIP(ctx, hipMemcpy(h->edges, e.data(), E, hipMemcpyHostToDevice));
     LPE_HIP(ctx, hipMemcpy(h->edges0, e.data(), E, hipMemcpyHostToDevice));
-    LPE_HIP(ctx, hipMalloc((void **)&h->cnt, sizeof(int32_t) * 4));
-    LPE_HIP(ctx, hipMemset(h->cnt, 0, sizeof(int32_t) * 4));
+    // [0], [1] slots by parity, [2] the hash's input slots, [3] scratch, [4], [5] the ghost columns received
+    LPE_HIP(ctx, hipMalloc((void **)&h->cnt, sizeof(int32_t) * 8));
+    LPE_HIP(ctx, hipMemset(h->cnt, 0, sizeof(int32_t) * 8));
     float **wb[] = {&h->sL, &h->sR, &h->rL, &h->rR};
     for (float **q : wb) {
         LPE_HIP(ctx, hipMalloc((void **)q, wire_bytes(wire_cap)));
@@ -4278,6 +4387,24 @@ extern "C" int lpe_sph_set_ids(lpe_ctx *ctx, int n, const int32_t *ids) {
     if (st) return st;
     LPE_HIP(ctx, hipMemcpyAsync(d.P.id, ids, sizeof(int32_t) * (size_t)n, hipMemcpyHostToDevice, ctx->stream));
     LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    return LPE_OK;
+}
+
+extern "C" int lpe_sph_set_global_count(lpe_ctx *ctx, int n_global) {
+    if (!ctx || n_global < 0) return LPE_ERR_ARG;
+    SphDev &d = ctx->sph;
+    if (!d.shard) { ctx->err = "lpe_sph_set_global_count: not a slab rank (lpe_sph_set_slab)"; return LPE_ERR_STATE; }
+    int st = sph_void_prelaunch(ctx);
+    if (st) return st;
+    d.shard->nglobal = n_global;
+    if (d.P.x && n_global > d.cap_n) {          // refInv holds an entry per particle id
+        LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        if (d.refInv) (void)hipFree(d.refInv);
+        d.refInv = nullptr;
+        LPE_HIP(ctx, hipMalloc((void **)&d.refInv, sizeof(int32_t) * (size_t)n_global));
+    }
+    if (d.refInv)
+        LPE_HIP(ctx, hipMemsetAsync(d.refInv, 0xff, sizeof(int32_t) * (size_t)std::max(n_global, d.cap_n), ctx->stream));
     return LPE_OK;
 }
 

@@ -216,6 +216,7 @@ SIGNATURES["lpe_world_tick"] = ([C.c_void_p, C.POINTER(WorldConfig), C.c_int], C
 
 SIGNATURES["lpe_sph_set_slab"] = ([C.c_void_p, C.c_int, C.c_int, _FP, C.c_int, C.c_int], C.c_int)
 SIGNATURES["lpe_sph_set_ids"] = ([C.c_void_p, C.c_int, _IP], C.c_int)
+SIGNATURES["lpe_sph_set_global_count"] = ([C.c_void_p, C.c_int], C.c_int)
 SIGNATURES["lpe_sph_slab_info"] = ([C.c_void_p, C.c_int, _IP, _IP, _IP], C.c_int)
 SIGNATURES["lpe_sph_download_owned"] = ([C.c_void_p, C.c_int] + [_FP] * 6 + [_IP, _IP], C.c_int)
 SIGNATURES["lpe_sph_set_domain"] = ([C.c_void_p] + [C.c_double] * 4, C.c_int)
@@ -467,6 +468,9 @@ class Context:
     def sph_set_ids(self, ids):
         a = np.ascontiguousarray(ids, dtype=np.int32)
         self._chk(lib().lpe_sph_set_ids(self._h, len(a), a.ctypes.data_as(_IP)), "lpe_sph_set_ids")
+
+    def sph_set_global_count(self, n_global: int):
+        self._chk(lib().lpe_sph_set_global_count(self._h, int(n_global)), "lpe_sph_set_global_count")
 
     def sph_download_owned(self, cap=None):
         """{x, y, vx, vy, density, pressure, id} of the particles this context owns."""

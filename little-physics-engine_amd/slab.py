@@ -26,6 +26,9 @@ import numpy as np
 
 FIELDS = ("x", "y", "vx", "vy", "density", "pressure")
 BAND = 2                  # ghost cell columns each side of an edge (lpe_sph.hip SLAB_BAND)
+BAND_CAP = 3              # ... in the reference cell-capacity mode: at least (SLAB_BAND_CAP), one more per
+BAND_MAX = 8              #   65 particles the largest cell holds past 64, at most SLAB_BAND_MAX
+BAND_CAP_WIRE = 5         # the capped mode's default wire: cells of up to 194 (lpe_sph.hip slab_band)
 
 
 def cell_size(cfg=None) -> float:
@@ -68,11 +71,12 @@ def owners(x, edges, cfg=None) -> np.ndarray:
     return np.searchsorted(cuts, _columns(x, cfg), side="right").astype(np.int32)
 
 
-def wire_capacity(x, edges, cfg=None, factor: float = 2.0, floor: int = 2048) -> int:
+def wire_capacity(x, edges, cfg=None, factor: float = 2.0, floor: int = 2048, band: int = BAND) -> int:
     """Ghost records per direction and sub-step: `factor` times the most
-    particles in the BAND + 1 columns along any inner edge at the start (the
+    particles in the band + 1 columns along any inner edge at the start (the
     band, a column the re-balancing may move, room for compression), plus
     `floor`."""
+    BAND = band
     col = _columns(x, cfg)
     cs = cell_size(cfg)
     worst = 0
@@ -84,19 +88,24 @@ def wire_capacity(x, edges, cfg=None, factor: float = 2.0, floor: int = 2048) ->
 
 
 def setup_rank(ctx, rank: int, nranks: int, fluid: dict, edges, cfg, rigids=None, wire_cap=None,
-               domain=None, rebalance: int = 0):
+               domain=None, rebalance: int = 0, cells: str = "unbounded"):
     """Configure ctx as slab `rank` and upload the particles it owns (global
-    ids = indices into `fluid`).  Returns the owned global ids."""
+    ids = indices into `fluid`).  cells="ref": the reference's 64-particle
+    cells (LPE_SPH_MODE_REF_CELL_CAP; the global count and a wire for
+    BAND_CAP ghost columns).  Returns the owned global ids."""
     import lpe  # the in-tree binding (little-physics-engine_amd/lpe.py)
     x = np.asarray(fluid["x"], np.float32)
     if wire_cap is None:
-        wire_cap = wire_capacity(x, edges, cfg)
+        wire_cap = wire_capacity(x, edges, cfg, band=BAND_CAP_WIRE if cells == "ref" else BAND)
     own = np.nonzero(owners(x, edges, cfg) == rank)[0].astype(np.int32)
     ctx.sph_set_config(cfg)
     ctx.sph_set_slab(nranks, rank, edges, wire_cap, rebalance)
     sub = {k: np.asarray(fluid[k])[own] for k in ("x", "y", "vx", "vy", "mass", "density", "pressure")}
     ctx.sph_upload(sub["x"], sub["y"], sub["vx"], sub["vy"], sub["mass"], sub["density"], sub["pressure"])
     ctx.sph_set_ids(own)
+    if cells == "ref":
+        ctx.sph_set_global_count(len(x))
+        ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP)
     if domain is None:
         y = np.asarray(fluid["y"], np.float32)
         pad = 1.0

@@ -148,15 +148,17 @@ def test_tile_scheduling_overflow_bit_exact(monkeypatch, q, h):
         np.testing.assert_array_equal(rb[k], rb_ref[k], err_msg=k)
 
 
-def test_c5_eight_slab_ranks_bit_exact():
+@pytest.mark.parametrize("cells", ["unbounded", "ref"])
+def test_c5_eight_slab_ranks_bit_exact(cells):
     """C5 (2,097,152 particles): 8 x-slab ranks (in-process transport, one
     GPU) against the single domain, 2 full world ticks: every particle and
-    wall bit for bit."""
+    wall bit for bit, in unbounded cells and in the reference's 64-particle
+    cells (the ranks then file 3 ghost columns each side)."""
     s = scenes.scene("C5")
     fl = s["fluid"]
     n = len(fl["x"])
     b, v = scenes.to_bodies(s["bodies"])
-    one = _world_ctx(s["U"], fl, b, v)
+    one = _world_ctx(s["U"], fl, b, v, mode=lpe.SPH_MODE_REF_CELL_CAP if cells == "ref" else 0)
     try:
         one.world_tick(DT, 2)
         ref = one.sph_download()
@@ -169,7 +171,7 @@ def test_c5_eight_slab_ranks_bit_exact():
         for r, c in enumerate(ctxs):
             c.rigid_set_config(lpe.rigid_config(universe=s["U"]))
             c.rigid_upload(b, v)
-            slab.setup_rank(c, r, 8, fl, edges, lpe.default_fluid_config())
+            slab.setup_rank(c, r, 8, fl, edges, lpe.default_fluid_config(), cells=cells)
             c.world_set_coupling(np.arange(len(b) - 1, -1, -1, dtype=np.int32))
         lpe.mg_loopback_run(ctxs, 2, world=lpe.WorldConfig(DT, 1.0, 1.0, 1.0))
         parts = [c.sph_download_owned(cap=n) for c in ctxs]

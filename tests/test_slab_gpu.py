@@ -341,3 +341,85 @@ def test_slab_drift_into_empty_rank_grows_grid_and_slots():
     ref, _, _ = _single(fl, np.zeros(0, lpe.RIGID_DTYPE), nt)
     for k in slab.FIELDS:
         np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+
+
+def _m_state(prep):
+    """Scene M after `prep` single-domain world ticks: (scene, fluid, bodies, verts)."""
+    s = scenes.scene("M")
+    b, v = scenes.to_bodies(s["bodies"])
+    one = lpe.Context(0)
+    try:
+        _world_rank(one, 0, 1, s, None)
+        one.world_tick(DT, prep)
+        out = one.sph_download()
+        bodies = one.rigid_download()
+    finally:
+        one.close()
+    fl = dict(s["fluid"])
+    fl.update({k: out[k] for k in ("x", "y", "vx", "vy", "density", "pressure")})
+    return s, fl, bodies, v
+
+
+@pytest.mark.parametrize("nranks", [2, 4])
+def test_slab_capped_cells_bit_exact(nranks):
+    """the reference's 64-particle cells on slab ranks.
+    Scene M 240 ticks in (the pool compressed: cells of up to ~98), the edges
+    put beside over-full cells (the over-full column the last owned column,
+    the first ghost column, one further out), 3 world ticks in
+    LPE_SPH_MODE_REF_CELL_CAP: the ranks (at least 3 ghost columns each side,
+    one more per 65 particles the largest cell holds past 64 -- the capped
+    cells keep compressing, 182, 259, 302 particles in a cell after 1, 2, 3
+    ticks, profiles/r06/probe/capped_slab_diag.log; the literal loop's
+    cross-cell reads on the global grid's flat order; values read as ids
+    that are not on the rank skipped) equal the single domain in the same
+    mode bit for bit, fluid and bodies."""
+    s, fl, bodies, verts = _m_state(240)
+    cfg = lpe.default_fluid_config()
+    cs = slab.cell_size(cfg)
+    eps = np.float32(cfg.gridConfig.gridEpsilon)
+    col = np.floor((fl["x"] + eps) / np.float32(cs)).astype(np.int64)
+    row = np.floor((fl["y"] + eps) / np.float32(cs)).astype(np.int64)
+    cells, counts = np.unique(np.stack([col, row], 1), axis=0, return_counts=True)
+    over = np.unique(cells[counts > 64][:, 0])
+    assert len(over) >= nranks - 1, "no over-full cells at this state"
+    pick = over[np.linspace(0, len(over) - 1, nranks + 1).astype(int)[1:-1]]
+    cuts = sorted(set(int(c) + d for c, d in zip(pick, (1, 0, -1))))
+    edges = np.array([-np.inf] + [c * cs for c in cuts] + [np.inf], np.float32)
+    n = len(fl["x"])
+    sf = dict(s)
+    sf["fluid"] = fl
+    one = lpe.Context(0)
+    try:
+        one.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+        one.rigid_upload(bodies, verts)
+        one.sph_set_config(cfg)
+        one.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+        one.world_set_coupling(np.arange(len(bodies) - 1, -1, -1, dtype=np.int32))
+        one.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP)
+        one.sph_diag(True)
+        one.world_tick(DT, 3)
+        ref = one.sph_download()
+        rb_ref = one.rigid_download()
+        st1 = one.sph_stats()
+    finally:
+        one.close()
+    assert st1["overCapCellsTotal"] > 0, st1
+    ctxs = [lpe.Context(0) for _ in range(len(edges) - 1)]
+    try:
+        for r, c in enumerate(ctxs):
+            c.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+            c.rigid_upload(bodies, verts)
+            slab.setup_rank(c, r, len(ctxs), fl, edges, cfg, cells="ref",
+                            wire_cap=slab.wire_capacity(fl["x"], edges, cfg, band=slab.BAND_MAX))
+            c.world_set_coupling(np.arange(len(bodies) - 1, -1, -1, dtype=np.int32))
+        lpe.mg_loopback_run(ctxs, 3, world=lpe.WorldConfig(DT, 1.0, 1.0, 1.0))
+        got = slab.merge_owned([c.sph_download_owned(cap=n) for c in ctxs], n)
+        rbs = [c.rigid_download() for c in ctxs]
+    finally:
+        for c in ctxs:
+            c.close()
+    for k in slab.FIELDS:
+        np.testing.assert_array_equal(got[k], ref[k], err_msg=k)
+    for r in rbs:
+        for k in ("x", "y", "angle", "vx", "vy", "omega"):
+            np.testing.assert_array_equal(r[k], rb_ref[k], err_msg=k)
