@@ -644,17 +644,19 @@ def envelope_all_ranks(dist, st):
 
 
 def slab_leg(lpe, scenes, slab, dist, rank, world, device, scene_name, prep, warmup, steps, transport,
-             rebalance, keep=False):
+             rebalance, keep=False, cells="ref"):
     """One sharded run: scene `scene_name`'s fluid in `world` x-slabs (one per
     rank), the rigid pass replicated, `prep` + `warmup`
     untimed ticks, then exactly `steps` ticks bracketed by barriers and device
-    syncs; elapsed = the maximum over ranks.  Slab ranks run unbounded cells
-    (the reference's capped cells read particle ids past a cell's 64 slots
-    that can live on any rank, fluid_kernels.metal:281-283): the all-rank
-    envelope says whether the window stayed where both semantics are the same
-    computation.  transport: "rccl" (the product path) or "gloo" (host-staged,
-    lpe_mg_init_host: two ranks may share one GPU; rehearsal only).  Returns
-    a dict; with keep the context stays open (leg["ctx"])."""
+    syncs; elapsed = the maximum over ranks.  cells="ref" (as the 1-GPU
+    line): after the prep every rank switches to the reference's 64-particle
+    cells (LPE_SPH_MODE_REF_CELL_CAP with the global count; the ranks then
+    file at least 3 ghost columns, tests/test_slab_gpu.py::
+    test_slab_capped_cells_bit_exact); the all-rank envelope says how many
+    cells exceeded 64 in the window.  transport: "rccl" (the product path) or
+    "gloo" (host-staged, lpe_mg_init_host: two ranks may share one GPU;
+    rehearsal only).  Returns a dict; with keep the context stays open
+    (leg["ctx"])."""
     s = scenes.scene(scene_name)
     fl = s["fluid"]
     bodies, verts = scenes.to_bodies(s["bodies"])
@@ -663,7 +665,8 @@ def slab_leg(lpe, scenes, slab, dist, rank, world, device, scene_name, prep, war
     ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
     ctx.rigid_upload(bodies, verts)
     edges = slab.slab_edges(fl["x"], world, cfg)
-    slab.setup_rank(ctx, rank, world, fl, edges, cfg, rebalance=rebalance)
+    wire = slab.wire_capacity(fl["x"], edges, cfg, band=slab.BAND_CAP_WIRE if cells == "ref" else slab.BAND)
+    slab.setup_rank(ctx, rank, world, fl, edges, cfg, rebalance=rebalance, wire_cap=wire)
     if transport == "gloo":
         ctx.mg_init_host(world, rank, slab.GlooTransport(rank, world))
     else:
@@ -672,6 +675,9 @@ def slab_leg(lpe, scenes, slab, dist, rank, world, device, scene_name, prep, war
     ctx.world_set_coupling(None)
     dt_tick = 1.0 / 120.0
     ctx.world_tick(dt_tick, prep)
+    if cells == "ref":                    # (every rank, at the same tick: the ghost band follows the mode)
+        ctx.sph_set_global_count(len(fl["x"]))
+        ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP)
     ctx.world_tick(dt_tick, warmup)
     ctx.sync()
     ctx.sph_diag(False)
@@ -707,8 +713,10 @@ def slab_leg(lpe, scenes, slab, dist, rank, world, device, scene_name, prep, war
                           owned=[e["owned"] for e in every], slots=[e["slots"] for e in every],
                           ghosts_in_max=[e["ghosts_in"] for e in every], wire_records=every[0]["wire"],
                           edges_columns=every[0]["edges"]),
-               reference_envelope=env, cells="unbounded cells",
-               reference_semantics=env["inside"])
+               reference_envelope=env,
+               cells=("the reference's 64-particle cells (LPE_SPH_MODE_REF_CELL_CAP)" if cells == "ref"
+                      else "unbounded cells"),
+               reference_semantics=cells == "ref" or env["inside"])
     if keep:
         leg["ctx"] = ctx
         leg["fluid"] = fl
@@ -718,11 +726,10 @@ def slab_leg(lpe, scenes, slab, dist, rank, world, device, scene_name, prep, war
     return leg
 
 
-def single_leg(lpe, scenes, device, scene_name, prep, warmup, steps):
-    """The same scene as ONE domain on this rank's GPU, unbounded cells (the
-    slab ranks' semantics): the scaling baseline measured in the same run
-    (a ticks/s ratio must not mix the capped and unbounded
-    modes)."""
+def single_leg(lpe, scenes, device, scene_name, prep, warmup, steps, cells="ref"):
+    """The same scene as ONE domain on this rank's GPU, in the slab ranks'
+    cell semantics: the scaling baseline measured in the same run (ADVICE r4:
+    a ticks/s ratio must not mix the capped and unbounded modes)."""
     s = scenes.scene(scene_name)
     fl = s["fluid"]
     bodies, verts = scenes.to_bodies(s["bodies"])
@@ -733,7 +740,10 @@ def single_leg(lpe, scenes, device, scene_name, prep, warmup, steps):
         ctx.sph_set_config(lpe.default_fluid_config())
         ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
         ctx.world_set_coupling(None)
-        ctx.world_tick(1.0 / 120.0, prep + warmup)
+        ctx.world_tick(1.0 / 120.0, prep)
+        if cells == "ref":
+            ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP)
+        ctx.world_tick(1.0 / 120.0, warmup)
         ctx.sph_diag(False)
         ctx.sync()
         t0 = time.perf_counter()
@@ -744,7 +754,8 @@ def single_leg(lpe, scenes, device, scene_name, prep, warmup, steps):
     finally:
         ctx.close()
     return dict(scene=scene_name, fluid_particles=len(fl["x"]), prep_ticks=prep, ticks_timed=steps,
-                ticks_per_s=round(steps / el, 2), cells="unbounded cells",
+                ticks_per_s=round(steps / el, 2),
+                cells="the reference's 64-particle cells (LPE_SPH_MODE_REF_CELL_CAP)" if cells == "ref" else "unbounded cells",
                 reference_envelope=dict(max_cell_occupancy_window=st["maxCellOccupancyTotal"],
                                         cells_over_64_window=st["overCapCellsTotal"],
                                         inside=st["overCapCellsTotal"] == 0))
@@ -850,11 +861,11 @@ def main():
         # the sharded path: slab_leg times exactly K ticks between barriers and
         # reports the maximum over ranks and the all-rank envelope
         leg = slab_leg(lpe, scenes, slab, dist, rank, world, local, scene_name, args.prep, args.warmup,
-                       args.steps, args.transport, args.rebalance, keep=True)
+                       args.steps, args.transport, args.rebalance, keep=True, cells=args.cells)
         ctx, fl, elapsed = leg["ctx"], leg["fluid"], leg["elapsed"]
         s = dict(desc=leg["desc"], U=leg["U"])
         n_bodies = leg["rigid_bodies"]
-        capped = False
+        capped = args.cells == "ref"
         wstats = ctx.sph_stats()
         wstats["overCapCellsTotal"] = leg["reference_envelope"]["cells_over_64_window"]
         wstats["maxCellOccupancyTotal"] = leg["reference_envelope"]["max_cell_occupancy_window"]
@@ -942,7 +953,7 @@ def main():
             # north_star's scaling claim: the fixed 2M-particle C5 scene over
             # the same ranks (strong scaling), in the same line
             strong_leg = slab_leg(lpe, scenes, slab, dist, rank, world, local, "C5", args.strong_prep,
-                                  args.warmup, args.steps, args.transport, args.rebalance)
+                                  args.warmup, args.steps, args.transport, args.rebalance, cells=args.cells)
 
     if rank != 0:
         if dist is not None:
@@ -1058,14 +1069,15 @@ def main():
     if sharded:
         # the scaling baselines, measured in this run on rank 0's GPU while the
         # other ranks wait: each scene as ONE domain in the slab ranks' cell
-        # semantics (unbounded), so every ratio compares one computation
-        # (ADVICE r4); the driver's own N=1 line times scene M in the
-        # reference's capped cells
+        # semantics (args.cells: the reference's capped cells by default, as
+        # the driver's own N=1 line), so every ratio compares one computation
+        # 
         primary = dict(scene=scene_name, desc=s["desc"], fluid_particles=len(fl["x"]),
                        ticks_per_s=round(args.steps / elapsed, 2), reference_envelope=line["reference_envelope"],
                        ranks=ranks_info)
-        c5_one = single_leg(lpe, scenes, local, "C5", args.strong_prep, args.warmup, args.steps)
-        m_one = single_leg(lpe, scenes, local, "M", args.prep, args.warmup, args.steps) if scene_name != "C5" else None
+        c5_one = single_leg(lpe, scenes, local, "C5", args.strong_prep, args.warmup, args.steps, cells=args.cells)
+        m_one = (single_leg(lpe, scenes, local, "M", args.prep, args.warmup, args.steps, cells=args.cells)
+                 if scene_name != "C5" else None)
         line.update(scaling_blocks(world, primary, strong_leg, c5_one, m_one))
     line.update(extras)
     if world == 1 and not args.no_extras:
