@@ -2653,7 +2653,11 @@ __global__ void k_rbin_fill(int nr, const lpe_gpu_rigid *__restrict__ rig, float
 static constexpr int RBS_WAVES = 4;                        // bins per 256-thread block
 __global__ void __launch_bounds__(256)
 k_rbin_sort(int B, int32_t *__restrict__ start, int32_t *__restrict__ list, int cap,
-            const float4 *__restrict__ aabb, float4 *__restrict__ baabb, int32_t *__restrict__ count) {
+            const float4 *__restrict__ aabb, float4 *__restrict__ baabb, int32_t *__restrict__ count,
+            int32_t *__restrict__ st, int32_t *__restrict__ pre) {
+    // (the tick's first forces pass follows: the prelaunched sub-step's stats
+    // merged here, k_merge_prestats' work without its launch)
+    if (pre && blockIdx.x == 0 && threadIdx.x == 0) merge_prestats_dev(st, pre);
     const int b = blockIdx.x * RBS_WAVES + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (b >= B) return;                                     // (whole wave)
@@ -3316,8 +3320,10 @@ float4 *sph_rig_records(lpe_ctx *ctx, int nr) {
     return d.raabb;
 }
 
-static int sph_build_rigid_bins(lpe_ctx *ctx) {
+// pre: the prelaunched sub-step's stats to merge (k_rbin_sort does it; *merged set)
+static int sph_build_rigid_bins(lpe_ctx *ctx, int32_t *pre = nullptr, bool *merged = nullptr) {
     SphDev &d = ctx->sph;
+    if (merged) *merged = false;
     if (d.nr <= 0 || !d.rig_dirty) return LPE_OK;
     // bin grid over the fluid device grid extent; bins of 0.25 m (>= 2h cells)
     d.bcs = std::max(0.25f, d.cs);
@@ -3365,7 +3371,8 @@ static int sph_build_rigid_bins(lpe_ctx *ctx) {
     LPE_KERNEL(ctx, "k_rbin_fill", k_rbin_fill, dim3(nblk(d.nr, 4)), dim3(256), 0, s, d.nr, d.rig, d.bcs,
                        d.bx0, d.by0, d.bW, d.bH, cursor, d.rbinList, d.cap_rlist, d.status);
     LPE_KERNEL(ctx, "k_rbin_sort", k_rbin_sort, dim3((B + RBS_WAVES - 1) / RBS_WAVES), dim3(256), 0, s, B, d.rbinStart, d.rbinList, d.cap_rlist,
-               d.raabb, rbin_aabb(d), d.rbinCount);
+               d.raabb, rbin_aabb(d), d.rbinCount, d.status, pre);
+    if (merged) *merged = pre != nullptr;
     LPE_CHECK_LAUNCH(ctx, "rbin");
     d.rbin_zero = B;
     d.rig_dirty = false;
@@ -3919,10 +3926,12 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
         std::swap(d.pr, d.prN);
         LPE_HIP(ctx, hipStreamWaitEvent(s, d.preDone, 0));
     }
-    int st = sph_build_rigid_bins(ctx);
+    bool merged = false;
+    int st = sph_build_rigid_bins(ctx, pre ? d.status + ST_COUNT : nullptr, &merged);
     if (st) return st;
     if (pre) {
-        // (the first forces pass resets the step stats and merges the prelaunch's: sp.mergePre)
+        // (k_rbin_sort, or else the first forces pass, resets the step stats
+        // and merges the prelaunch's: sp.mergePre)
     } else {
         st = sph_reset_step_stats(ctx, s, d.status);
         if (st) return st;
@@ -3988,7 +3997,7 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
             kn.sk = slab_kick(d);
         }
         kicked = kn.on ? fblocks + nq : 0;
-        sp.mergePre = (step == 0 && pre) ? d.status + ST_COUNT : nullptr;
+        sp.mergePre = (step == 0 && pre && !merged) ? d.status + ST_COUNT : nullptr;
         if (sp.mergePre && sp.refInv) {
             LPE_KERNEL(ctx, "k_merge_prestats", k_merge_prestats, dim3(1), dim3(64), 0, s, d.status, sp.mergePre);
             sp.mergePre = nullptr;
