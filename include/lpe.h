@@ -260,14 +260,12 @@ int  lpe_abi_version(void);
 int  lpe_device_count(int *count);
 /* Blocks until all work queued on the context's stream is done. */
 int  lpe_sync(lpe_ctx *ctx);
-/* Hardware queues.  A context runs up to four streams (fluid step,
- * prelaunch, collision detection, position solver; RCCL adds its own) and
- * HIP maps streams round robin onto GPU_MAX_HW_QUEUES queues (4 by default):
- * two streams on one queue execute in submission order and the tick's
- * overlaps collapse (performance only, results are unchanged).  Callers
- * should export GPU_MAX_HW_QUEUES=8 before their first HIP call; the library
- * sets 8 when it is loaded first and the variable is unset.  Reports the
- * value in effect (*queues) and whether the library set it. */
+/* Hardware queues.  A context runs four streams (fluid step, prelaunch,
+ * collision detection, position solver) and HIP maps streams round robin
+ * onto GPU_MAX_HW_QUEUES queues, 4 by default: one per stream of a context.
+ * Leave it at 4: more than 4 measured every kernel ~2x slower on MI355X /
+ * ROCm 7.2 (round 6; round 4 advised 8).  Reports the value in effect
+ * (*queues); *set_by_library is always 0 since round 6. */
 int  lpe_hw_queues(int *queues, int *set_by_library);
 
 /* ---- kernel timing (bench / profiling; no reference counterpart) ------- */

@@ -2854,17 +2854,14 @@ extern "C" int lpe_device_count(int *count) {
     return LPE_OK;
 }
 
-// Hardware queues.  A context runs up to four streams (fluid
-// step, prelaunch, detection, position solver) and RCCL adds its own; HIP maps
-// streams round robin onto GPU_MAX_HW_QUEUES queues (4 by default) and two
-// streams on one queue run in submission order, so the tick's overlaps
-// collapse.  When the library is loaded before the host program's first HIP
-// call (the C++ drop-in, a ctypes caller), this constructor asks for 8 unless
-// the caller chose; lpe_hw_queues reports the value in effect.
-static int g_hwq_set_by_lib = 0;
-__attribute__((constructor)) static void lpe_hw_queues_default() {
-    if (!std::getenv("GPU_MAX_HW_QUEUES")) g_hwq_set_by_lib = setenv("GPU_MAX_HW_QUEUES", "8", 0) == 0;
-}
+// Hardware queues.  A context runs four streams (fluid step,
+// prelaunch, detection, position solver); HIP maps streams round robin onto
+// GPU_MAX_HW_QUEUES queues, 4 by default, one per stream of a context.  Round
+// 4's load-time constructor raised it to 8 when unset; round 6 measured more
+// than 4 queues running every kernel ~2x slower on MI355X / ROCm 7.2 (810
+// against 453 ticks/s, profiles/r06/hwq/sweep.txt), so the library leaves it
+// alone; lpe_hw_queues reports the value in effect.
+static const int g_hwq_set_by_lib = 0;
 
 extern "C" int lpe_hw_queues(int *queues, int *set_by_library) {
     if (!queues) return LPE_ERR_ARG;

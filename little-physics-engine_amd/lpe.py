@@ -12,14 +12,12 @@ import os
 
 import numpy as np
 
-# One hardware queue per stream.  A context runs up to four streams (the
-# fluid step, the prelaunch, the collision detection, the position solver)
-# and RCCL adds its own; HIP maps streams round robin onto
-# GPU_MAX_HW_QUEUES queues (4 by default), and two streams on one queue
-# execute in submission order: the overlaps the tick is built on (detection
-# beside the fluid step, the prelaunch beside the solvers) collapse.  Set
-# before the library initialises HIP; a value the caller set wins.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# Hardware queues: a context runs four streams (the fluid step, the
+# prelaunch, the collision detection, the position solver), which HIP maps
+# round robin onto GPU_MAX_HW_QUEUES queues -- HIP's default of 4 gives each
+# its own.  More than 4 measured the kernels ~2x slower on MI355X (ROCm 7.2,
+# profiles/r06/hwq/sweep.txt: 810 ticks/s at 4 queues, 453 at 5-8), so the
+# binding leaves the variable alone (round 4 set 8 here).
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LPE_LIB") or os.path.join(HERE, "liblpe_hip.so")   # LPE_LIB: an alternative build (A/B runs)
