@@ -1181,7 +1181,16 @@ __device__ void ref_cap_walk(float xi, float yi, float eps, const GridParams &g,
 // block runs it), so every tile runs exactly once whatever the lists hold.
 // LPE_NO_HEAVY=1: off (A/B).
 static constexpr int QUARTER_PAIRS = 512, HALF_PAIRS = 256;
-static constexpr int QUARTER_MAX = 128, HALF_MAX = 160, COUPLED_MAX = 160;
+#ifndef LPE_QUARTER_MAX
+#define LPE_QUARTER_MAX 128
+#endif
+#ifndef LPE_HALF_MAX
+#define LPE_HALF_MAX 160
+#endif
+#ifndef LPE_COUPLED_MAX
+#define LPE_COUPLED_MAX 160
+#endif
+static constexpr int QUARTER_MAX = LPE_QUARTER_MAX, HALF_MAX = LPE_HALF_MAX, COUPLED_MAX = LPE_COUPLED_MAX;
 static constexpr int FILED_MAX = QUARTER_MAX + HALF_MAX + COUPLED_MAX;
 // list: [0..2] the counts by class; then per filing code c (quarters c = 1 ..,
 // halves c = QUARTER_MAX + 1 .., coupled c = QUARTER_MAX + HALF_MAX + 1 ..)
@@ -1420,6 +1429,7 @@ k_density(int n, const int32_t *__restrict__ nptr, int nstride, float h, float e
     (void)dtb;
     DTRCLR();
     DTR(0);
+    DTRHW();
     const GridParams g = *gp;
     const float cs = g.cellSize;
     // the tile filing's candidate range (HeavyOut), loaded before the walk so
@@ -2057,6 +2067,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         return;
     }
     FTR(0);
+    FTRHW();
     // the image: records [0, FCAP) nbA, [FCAP, 2 FCAP) nbB; then the CouplePool
     __shared__ float4 fimg[2 * FCAP];
     __shared__ int hraw[64];

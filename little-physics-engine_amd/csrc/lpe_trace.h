@@ -18,15 +18,35 @@
 __device__ unsigned long long g_ftrace[4096 * 8];
 __device__ int g_ftrace_on;
 __device__ unsigned long long g_ftrace2[4096 * 8];
+// LPE_FTRACE_LITE: only the block's start / end stamps, its pair count and
+// its HW_ID (the full set leaves a 432-byte stack frame in k_forces_couple
+// since round 6 and triples its time; the lite set keeps the shipped frame)
+#ifdef LPE_FTRACE_LITE
+#define FTR(k) do { if (((k) == 0 || (k) == 3) && g_ftrace_on && threadIdx.x == 0) g_ftrace[ftb * 8 + (k)] = wall_clock64(); } while (0)
+#else
 #define FTR(k) do { if (g_ftrace_on && threadIdx.x == 0) g_ftrace[ftb * 8 + (k)] = wall_clock64(); } while (0)
+#endif
 #define FTRCLR() do { if (g_ftrace_on && threadIdx.x == 0) for (int k_ = 0; k_ < 8; k_++) { g_ftrace[ftb * 8 + k_] = 0; g_ftrace2[ftb * 8 + k_] = 0; } } while (0)
 // the coupling pair's stages (sph_coupling.h CPT), per block
+#ifdef LPE_FTRACE_LITE
+#define FTR_PAIRS() ((unsigned long long *)nullptr)
+#else
 #define FTR_PAIRS() (g_ftrace_on ? g_ftrace2 + ftb * 8 : (unsigned long long *)nullptr)
+#endif
 #define FTR2SET(k, v) do { if (g_ftrace_on && threadIdx.x == 0) g_ftrace2[ftb * 8 + (k)] = (unsigned long long)(v); } while (0)
 extern "C" int lpe_ftrace2(unsigned long long *host, int n) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ftrace2), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
 }
+#ifdef LPE_FTRACE_LITE
+#define FTRMAX(k, v) do {} while (0)
+#else
 #define FTRMAX(k, v) do { if (g_ftrace_on && (threadIdx.x & 63) == 0) atomicMax(&g_ftrace[ftb * 8 + (k)], (unsigned long long)(v)); } while (0)
+#endif
+// where the block ran: ftrace2 slot 6 = HW_ID (cu, se, ...), slot 7 = XCC_ID
+#define FTRHW() do { if (g_ftrace_on && threadIdx.x == 0) { unsigned hw_, xcc_; \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_)); \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_)); \
+    g_ftrace2[ftb * 8 + 6] = hw_; g_ftrace2[ftb * 8 + 7] = xcc_; } } while (0)
 extern "C" int lpe_ftrace(int on, unsigned long long *host, int n) {
     if (host) (void)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ftrace), sizeof(unsigned long long) * n);
     unsigned long long z[4096 * 8] = {};
@@ -41,6 +61,11 @@ __device__ unsigned long long g_dtrace[4096 * 8];
 #define DTRSET(k, v) do { if (g_ftrace_on && threadIdx.x == 0 && dtb < 4096) g_dtrace[dtb * 8 + (k)] = (unsigned long long)(v); } while (0)
 #define DTRMAX(k, v) do { if (g_ftrace_on && (threadIdx.x & 63) == 0 && dtb < 4096) atomicMax(&g_dtrace[dtb * 8 + (k)], (unsigned long long)(v)); } while (0)
 #define DTRCLR() do { if (g_ftrace_on && threadIdx.x == 0 && dtb < 4096) for (int k_ = 0; k_ < 8; k_++) g_dtrace[dtb * 8 + k_] = 0; } while (0)
+// slot 7: where the tile ran, XCC_ID << 24 | HW_ID's low 24 bits (cu, sh, se)
+#define DTRHW() do { if (g_ftrace_on && threadIdx.x == 0 && dtb < 4096) { unsigned hw_, xcc_; \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_)); \
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc_)); \
+    g_dtrace[dtb * 8 + 7] = ((unsigned long long)(xcc_ & 0xF) << 24) | (hw_ & 0xFFFFFF); } } while (0)
 extern "C" int lpe_dtrace(unsigned long long *host, int n) {
     return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dtrace), sizeof(unsigned long long) * n) == hipSuccess ? 0 : 1;
 }
@@ -49,11 +74,13 @@ extern "C" int lpe_dtrace(unsigned long long *host, int n) {
 #define DTRSET(k, v) do {} while (0)
 #define DTRMAX(k, v) do {} while (0)
 #define DTRCLR() do {} while (0)
+#define DTRHW() do {} while (0)
 #define FTR(k) do {} while (0)
 #define FTRCLR() do {} while (0)
 #define FTR_PAIRS() ((unsigned long long *)nullptr)
 #define FTR2SET(k, v) do {} while (0)
 #define FTRMAX(k, v) do {} while (0)
+#define FTRHW() do {} while (0)
 #endif
 
 #ifdef LPE_PTRACE
