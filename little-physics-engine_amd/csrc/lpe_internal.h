@@ -222,6 +222,26 @@ struct lpe_ctx {
         }                                                                                \
     } while (0)
 
+// Launch a kernel and signal `ev` at its end, on the dispatch's own
+// completion signal (hipExtLaunchKernelGGL's stop event) instead of a marker
+// packet after it: a recorded event holds the stream ~4 us at that boundary,
+// the carried one ~1.5 us (profiles/r06/probe/gap_probe.txt).  With the
+// kernel timed, or LPE_EVENT_RECORDS=1 (A/B): the launch, then a record.
+inline bool lpe_event_records() {
+    static const bool on = getenv("LPE_EVENT_RECORDS") != nullptr;
+    return on;
+}
+#define LPE_KERNEL_SIGNAL(ctx, name, ev, kernel, grid, block, shmem, stream, ...)        \
+    do {                                                                                 \
+        if (((ctx)->timer.on && (ctx)->timer.wants(name)) || lpe_event_records()) {      \
+            LPE_KERNEL(ctx, name, kernel, grid, block, shmem, stream, __VA_ARGS__);      \
+            LPE_HIP(ctx, hipEventRecord(ev, stream));                                    \
+        } else {                                                                         \
+            hipExtLaunchKernelGGL(kernel, grid, block, shmem, stream, nullptr, ev, 0,    \
+                                  __VA_ARGS__);                                          \
+        }                                                                                \
+    } while (0)
+
 #define LPE_HIP(ctx, call)                                                       \
     do {                                                                         \
         hipError_t e_ = (call);                                                  \
@@ -262,7 +282,11 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int));
 float4 *sph_rig_records(lpe_ctx *ctx, int nr);   // the coupling records buffer (nr rigids)
 // first (optional): launched on the side stream ahead of the prelaunch (the
 // tick's own fluid boundary / gravity pass); fbgDone is recorded after it
-int sph_prelaunch(lpe_ctx *ctx, double dt_tick, const std::function<int(hipStream_t)> &first = {});
+// ready: an event the context stream has signalled after its last work the
+// prelaunch depends on (null: one is recorded here)
+int sph_prelaunch(lpe_ctx *ctx, double dt_tick, const std::function<int(hipStream_t)> &first = {},
+                  hipEvent_t ready = nullptr);
+hipEvent_t rigid_boundary_event(lpe_ctx *ctx);
 int lpe_sph_cover_box(lpe_ctx *ctx, double x0, double y0, double x1, double y1);
 // a slab rank's P slots in use (device count; ids -1 mark dropped slots), else null
 const int32_t *sph_slab_slots(lpe_ctx *ctx);

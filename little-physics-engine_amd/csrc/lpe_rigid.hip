@@ -3655,7 +3655,7 @@ int lpe_rigid_destroy_internal(lpe_ctx *ctx) {
     }
     if (d->hc) (void)hipHostFree(d->hc);
     if (d->hcr) (void)hipHostFree(d->hcr);
-    hipEvent_t evs[] = {d->evStart, d->evDetect, d->evColour, d->evFork, d->evJoin, d->evHc[0], d->evHc[1]};
+    hipEvent_t evs[] = {d->evStart, d->evDetect, d->evColour, d->evFork, d->evJoin, d->evHc[0], d->evHc[1], d->evBvg};
     for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
     if (d->side) (void)hipStreamDestroy(d->side);
     if (d->psolve) (void)hipStreamDestroy(d->psolve);
@@ -4499,6 +4499,7 @@ int rigid_tick_begin(lpe_ctx *ctx, bool on_main) {
     RigidDev *d = rdev(ctx);
     d->overlap_pending = false;
     d->colour_pending = false;
+    d->bvgSignal = false;
     if (d->nb <= 0) return LPE_OK;
     const lpe_rigid_config &c = d->cfg;
     if (!d->side) {
@@ -4535,10 +4536,13 @@ int rigid_tick_begin(lpe_ctx *ctx, bool on_main) {
         d->lag_next = false;
     }
     hipStream_t s = ctx->stream;
-    LPE_KERNEL(ctx, "k_boundary_pos", k_boundary_pos, dim3(rblk(d->nb)), dim3(RTPB), 0, s, d->nb, d->bodies,
-               c.marginPixels * c.metersPerPixel, c.universeSize, d->bbits);
     d->det = on_main ? s : d->side;
-    if (d->det != s) LPE_HIP(ctx, hipEventRecord(d->evStart, s));
+    if (d->det != s)                           // (the detection's start: the clamp's launch signals it)
+        LPE_KERNEL_SIGNAL(ctx, "k_boundary_pos", d->evStart, k_boundary_pos, dim3(rblk(d->nb)), dim3(RTPB), 0, s,
+                          d->nb, d->bodies, c.marginPixels * c.metersPerPixel, c.universeSize, d->bbits);
+    else
+        LPE_KERNEL(ctx, "k_boundary_pos", k_boundary_pos, dim3(rblk(d->nb)), dim3(RTPB), 0, s, d->nb, d->bodies,
+                   c.marginPixels * c.metersPerPixel, c.universeSize, d->bbits);
     d->detect_launched = false;
     d->overlap_pending = true;
     return LPE_OK;
@@ -4584,15 +4588,23 @@ int rigid_tick_hook(lpe_ctx *ctx, int step) {
     return st;
 }
 
+// the event the world tick's boundary/gravity pass signalled this tick, or null
+hipEvent_t rigid_boundary_event(lpe_ctx *ctx) {
+    RigidDev *d = rdev(ctx);
+    return d->nb > 0 && d->bvgSignal ? d->evBvg : nullptr;
+}
+
 // the boundary system's velocity part, at its place in the tick
 int rigid_tick_boundary(lpe_ctx *ctx, bool gravity, double dt_state) {
     RigidDev *d = rdev(ctx);
     if (d->nb <= 0) return LPE_OK;
     const lpe_rigid_config &c = d->cfg;
     if (gravity) {   // the planetary-mass check (k_gravity_check) is queued before
-        LPE_KERNEL(ctx, "k_boundary_vel_gravity", k_boundary_vel_gravity, dim3(rblk(d->nb)), dim3(RTPB), 0,
-                   ctx->stream, d->nb, d->bodies, d->bbits, c.bounceDamping, c.maxSpeed, c.gravity, dt_state,
-                   d->counts + 5);
+        if (!d->evBvg) LPE_HIP(ctx, hipEventCreateWithFlags(&d->evBvg, hipEventDisableTiming));
+        LPE_KERNEL_SIGNAL(ctx, "k_boundary_vel_gravity", d->evBvg, k_boundary_vel_gravity, dim3(rblk(d->nb)),
+                          dim3(RTPB), 0, ctx->stream, d->nb, d->bodies, d->bbits, c.bounceDamping, c.maxSpeed,
+                          c.gravity, dt_state, d->counts + 5);
+        d->bvgSignal = true;
         return LPE_OK;
     }
     LPE_KERNEL(ctx, "k_boundary_vel", k_boundary_vel, dim3(rblk(d->nb)), dim3(RTPB), 0, ctx->stream, d->nb,
@@ -4684,8 +4696,16 @@ int rigid_tick_finish(lpe_ctx *ctx) {
     // during the fluid step instead, the one-workgroup position solver slows
     // the full-chip fluid kernels by more than it saves.)
     if (joinColour) LPE_HIP(ctx, hipStreamWaitEvent(s, d->evColour, 0));
-    LPE_HIP(ctx, hipEventRecord(d->evFork, s));
-    LPE_HIP(ctx, hipStreamWaitEvent(d->side, d->evFork, 0));
+    if (d->bvgSignal && joinColour) {
+        // (the boundary/gravity pass is the context stream's last rigid work
+        // before the solvers, and the side stream is past the colouring; a
+        // detection on the context stream runs after that pass: recorded)
+        LPE_HIP(ctx, hipStreamWaitEvent(d->side, d->evBvg, 0));
+    } else {
+        LPE_HIP(ctx, hipEventRecord(d->evFork, s));
+        LPE_HIP(ctx, hipStreamWaitEvent(d->side, d->evFork, 0));
+    }
+    d->bvgSignal = false;
     st = colour_pos(ctx, d, d->side);
     if (st) return st;
     LPE_HIP(ctx, hipEventRecord(d->evJoin, d->side));

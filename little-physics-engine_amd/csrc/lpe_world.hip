@@ -260,7 +260,10 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
         // after the last tick of this call, for the next call (it writes only
         // scratch, so downloads and state changes in between are safe)
         if (prelaunch) {
-            st = fbg_side ? sph_prelaunch(ctx, dt_fluid, fbg) : sph_prelaunch(ctx, dt_fluid);
+            // (with the fluid's boundary/gravity on the side stream, the bodies'
+            // pass is the context stream's last launch: its signal serves)
+            st = fbg_side ? sph_prelaunch(ctx, dt_fluid, fbg, overlap ? rigid_boundary_event(ctx) : nullptr)
+                          : sph_prelaunch(ctx, dt_fluid);
             if (st) return st;
         }
         // an error past this point still joins the side stream's fluid

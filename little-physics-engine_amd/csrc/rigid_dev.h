@@ -123,6 +123,11 @@ struct RigidDev {
     // the position solver runs beside the PGS on its own stream (rigid_solve)
     hipStream_t psolve = nullptr;
     hipEvent_t evFork = nullptr, evJoin = nullptr;
+    // the world tick's boundary/gravity pass signals evBvg itself (its launch
+    // carries the event); the position solver's fork and the next tick's
+    // prelaunch wait on it instead of recording their own (bvgSignal: this tick)
+    hipEvent_t evBvg = nullptr;
+    bool bvgSignal = false;
 };
 
 

@@ -6,6 +6,7 @@
 // prelaunch streams wait on events of the context stream while it runs the
 // sub-steps).  Measurement tooling only.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -161,6 +162,14 @@ int main(int argc, char **argv) {
         k_triv<<<1024, 256, 0, A>>>(st + (size_t)i * WGMAX);
         (void)hipEventRecord(evd, A);
     }));
+    // the event carried by the launch itself (hipExtLaunchKernelGGL's stop
+    // event: the dispatch packet's completion signal, no marker packet)
+    show("1024 WG launched with a stop event", run(A, st, n, [&](int i) {
+        hipExtLaunchKernelGGL(k_triv, dim3(1024), dim3(256), 0, A, nullptr, ev, 0, st + (size_t)i * WGMAX);
+    }));
+    show("1024 WG launched with a device-release stop event", run(A, st, n, [&](int i) {
+        hipExtLaunchKernelGGL(k_triv, dim3(1024), dim3(256), 0, A, nullptr, evd, 0, st + (size_t)i * WGMAX);
+    }));
     // a completed event of another stream waited on between launches (a join)
     k_triv<<<1, 64, 0, B>>>(st);
     CK(hipEventRecord(ev, B));
@@ -169,28 +178,37 @@ int main(int argc, char **argv) {
         (void)hipStreamWaitEvent(A, ev, 0);
         k_triv<<<1024, 256, 0, A>>>(st + (size_t)i * WGMAX);
     }));
-    // blocked barrier packets on other queues while A runs
-    const long long spin = (long long)(200000.0 / tu);  // 200 ms
-    for (int nb : {1, 2}) {
-        k_spin<<<1, 64, 0, B>>>(spin);
-        hipEvent_t eb;
-        CK(hipEventCreateWithFlags(&eb, hipEventDisableTiming));
-        CK(hipEventRecord(eb, B));
-        CK(hipStreamWaitEvent(C, eb, 0));
-        k_triv<<<1, 64, 0, C>>>(st);
-        if (nb > 1) {
-            CK(hipStreamWaitEvent(D, eb, 0));
-            k_triv<<<1, 64, 0, D>>>(st);
+    // blocked barrier packets on other queues while A runs: B spins, C / D / E
+    // wait on B's event (a barrier-AND packet at the head of their queues)
+    hipStream_t E;
+    CK(hipStreamCreateWithFlags(&E, hipStreamNonBlocking));
+    const long long spin = (long long)(300000.0 / tu);  // 300 ms
+    hipStream_t waiters[3] = {C, D, E};
+    for (int rep = 0; rep < 2; rep++)
+        for (int nb = 0; nb <= 3; nb++) {
+            k_spin<<<1, 64, 0, B>>>(spin);
+            hipEvent_t eb;
+            CK(hipEventCreateWithFlags(&eb, hipEventDisableTiming));
+            CK(hipEventRecord(eb, B));
+            for (int w = 0; w < nb; w++) {
+                CK(hipStreamWaitEvent(waiters[w], eb, 0));
+                k_triv<<<1, 64, 0, waiters[w]>>>(st);
+            }
+            char nm[96];
+            std::snprintf(nm, sizeof nm, "1024 WG, spin on B, %d stream(s) blocked on it", nb);
+            show(nm, run(A, st, n, [&](int i) { k_triv<<<1024, 256, 0, A>>>(st + (size_t)i * WGMAX); }));
+            std::snprintf(nm, sizeof nm, "  ~10 us work kernels, %d blocked", nb);
+            show(nm, run(A, st, n / 4, [&](int i) { k_lds<<<1024, 256, 38 << 10, A>>>(st + (size_t)i * WGMAX, 300); }));
+            CK(hipDeviceSynchronize());
+            CK(hipEventDestroy(eb));
         }
-        char nm[96];
-        std::snprintf(nm, sizeof nm, "1024 WG, spin on B, %d stream(s) blocked on it", nb);
-        show(nm, run(A, st, n, [&](int i) { k_triv<<<1024, 256, 0, A>>>(st + (size_t)i * WGMAX); }));
-        CK(hipDeviceSynchronize());
-        CK(hipEventDestroy(eb));
-    }
     {
+        // the waits as spinning kernels instead (C and D each run a 1-wave poller)
         k_spin<<<1, 64, 0, B>>>(spin);
-        show("1024 WG, spin kernel busy on B (nothing blocked)", run(A, st, n, [&](int i) { k_triv<<<1024, 256, 0, A>>>(st + (size_t)i * WGMAX); }));
+        k_spin<<<1, 64, 0, C>>>(spin);
+        k_spin<<<1, 64, 0, D>>>(spin);
+        show("1024 WG, three 1-wave spinners on B, C, D", run(A, st, n, [&](int i) { k_triv<<<1024, 256, 0, A>>>(st + (size_t)i * WGMAX); }));
+        show("  ~10 us work kernels, three spinners", run(A, st, n / 4, [&](int i) { k_lds<<<1024, 256, 38 << 10, A>>>(st + (size_t)i * WGMAX, 300); }));
         CK(hipDeviceSynchronize());
     }
     show("trivial 1024 WG (again, end)", run(A, st, n, [&](int i) { k_triv<<<1024, 256, 0, A>>>(st + (size_t)i * WGMAX); }));
