@@ -284,9 +284,12 @@ float4 *sph_rig_records(lpe_ctx *ctx, int nr);   // the coupling records buffer 
 // tick's own fluid boundary / gravity pass); fbgDone is recorded after it
 // ready: an event the context stream has signalled after its last work the
 // prelaunch depends on (null: one is recorded here)
+// (devwait: the side stream waits on the rigid boundary pass's device signal
+// when there is one this tick, rigid_boundary_wait)
 int sph_prelaunch(lpe_ctx *ctx, double dt_tick, const std::function<int(hipStream_t)> &first = {},
-                  hipEvent_t ready = nullptr);
+                  hipEvent_t ready = nullptr, bool devwait = false);
 hipEvent_t rigid_boundary_event(lpe_ctx *ctx);
+int rigid_boundary_wait(lpe_ctx *ctx, hipStream_t s, bool *done);
 int lpe_sph_cover_box(lpe_ctx *ctx, double x0, double y0, double x1, double y1);
 // a slab rank's P slots in use (device count; ids -1 mark dropped slots), else null
 const int32_t *sph_slab_slots(lpe_ctx *ctx);

@@ -3473,21 +3473,54 @@ __global__ void k_boundary(int nb, lpe_body *__restrict__ bodies, double m, doub
 // gathered copy of the bodies, taken before the clamp), and the velocity part
 // is applied at the boundary system's place in the tick from the recorded
 // bounce bits.  Together they equal k_boundary.
-__global__ void k_boundary_pos(int nb, lpe_body *__restrict__ bodies, double m, double U,
-                               int32_t *__restrict__ bits) {
-    int i = blockIdx.x * RTPB + threadIdx.x;
-    if (i >= nb) return;
-    lpe_body &b = bodies[i];
-    int f = 0;
-    const int flags = b.flags;
-    if ((flags & LPE_BODY_HAS_VEL) && !((flags & LPE_BODY_HAS_SLEEP) && (flags & LPE_BODY_ASLEEP))) {
-        const double x = b.x, y = b.y;
-        if (x < m) { b.x = m; f |= 1; }
-        else if (x > U - m) { b.x = U - m; f |= 2; }
-        if (y < m) { b.y = m; f |= 4; }
-        else if (y > U - m) { b.y = U - m; f |= 8; }
+// A cross-stream signal without a marker packet: the launch's last
+// workgroup (arrival count) releases its writes and every earlier launch's
+// (stream order) and stores `value` into *flag; k_wait_flag polls it.
+__device__ __forceinline__ void grid_done_signal(uint32_t *ctr, uint32_t *flag, uint32_t value) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(ctr, 1u) == gridDim.x - 1) {
+            __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __threadfence();
+            __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
     }
-    bits[i] = f;
+}
+
+// One wave on the waiting stream: returns once *flag has reached `want`
+// (wrapping compare); a watchdog (~3 s) raises counts[7] bit 64 and returns,
+// so the stream never hangs on a signal that was not launched.
+__global__ void k_wait_flag(const uint32_t *__restrict__ flag, uint32_t want, int32_t *__restrict__ fault) {
+    if (threadIdx.x != 0) return;
+    for (uint32_t n = 0;; n++) {
+        const uint32_t v = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+        if ((int32_t)(v - want) >= 0) return;
+        if (n == (1u << 24)) {
+            atomicOr(fault, 64);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+
+__global__ void k_boundary_pos(int nb, lpe_body *__restrict__ bodies, double m, double U,
+                               int32_t *__restrict__ bits, uint32_t *__restrict__ sig, uint32_t value) {
+    int i = blockIdx.x * RTPB + threadIdx.x;
+    if (i < nb) {
+        lpe_body &b = bodies[i];
+        int f = 0;
+        const int flags = b.flags;
+        if ((flags & LPE_BODY_HAS_VEL) && !((flags & LPE_BODY_HAS_SLEEP) && (flags & LPE_BODY_ASLEEP))) {
+            const double x = b.x, y = b.y;
+            if (x < m) { b.x = m; f |= 1; }
+            else if (x > U - m) { b.x = U - m; f |= 2; }
+            if (y < m) { b.y = m; f |= 4; }
+            else if (y > U - m) { b.y = U - m; f |= 8; }
+        }
+        bits[i] = f;
+    }
+    if (sig) grid_done_signal(sig + 3, sig + 2, value);
 }
 __device__ __forceinline__ void boundary_vel_one(lpe_body &b, int f, double damp, double maxSpeed) {
     double vx = b.vx, vy = b.vy;
@@ -3527,13 +3560,16 @@ __global__ void k_gravity(int nb, lpe_body *__restrict__ bodies, double g, doubl
 // tick: nothing between them touches the bodies)
 __global__ void k_boundary_vel_gravity(int nb, lpe_body *__restrict__ bodies, const int32_t *__restrict__ bits,
                                        double damp, double maxSpeed, double g, double dt,
-                                       const int32_t *__restrict__ heavy) {
+                                       const int32_t *__restrict__ heavy, uint32_t *__restrict__ sig,
+                                       uint32_t value) {
     int i = blockIdx.x * RTPB + threadIdx.x;
-    if (i >= nb) return;
-    const int f = bits[i];
-    lpe_body &b = bodies[i];
-    if (f) boundary_vel_one(b, f, damp, maxSpeed);
-    if (!*heavy && gravity_view(b)) b.vy += g * dt;
+    if (i < nb) {
+        const int f = bits[i];
+        lpe_body &b = bodies[i];
+        if (f) boundary_vel_one(b, f, damp, maxSpeed);
+        if (!*heavy && gravity_view(b)) b.vy += g * dt;
+    }
+    if (sig) grid_done_signal(sig + 1, sig, value);
 }
 // RotationSystem, MovementSystem, SleepSystem on one body (each returns
 // whether it wrote the body; the kernels below store it back only then)
@@ -3655,6 +3691,7 @@ int lpe_rigid_destroy_internal(lpe_ctx *ctx) {
     }
     if (d->hc) (void)hipHostFree(d->hc);
     if (d->hcr) (void)hipHostFree(d->hcr);
+    if (d->tsync) (void)hipFree(d->tsync);
     hipEvent_t evs[] = {d->evStart, d->evDetect, d->evColour, d->evFork, d->evJoin, d->evHc[0], d->evHc[1], d->evBvg};
     for (hipEvent_t e : evs) if (e) (void)hipEventDestroy(e);
     if (d->side) (void)hipStreamDestroy(d->side);
@@ -3972,8 +4009,12 @@ static int detect_launch(lpe_ctx *ctx, RigidDev *d, int np_in, const int32_t *pa
 }
 
 // counts[7]: bit 1 a dataflow (replay) solve made no progress, bit 2 a
-// striped solver's workgroup waited ~0.2 s for a neighbour's hand-over
+// striped solver's workgroup waited ~0.2 s for a neighbour's hand-over, bit 64
+// a k_wait_flag gave up
 static const char *watchdog_msg(int bits) {
+    if (bits & 64)
+        return "world tick: a stream waited ~3 s for the context stream's boundary pass (k_wait_flag); the tick "
+               "is wrong";
     if (bits & 2)
         return "striped rigid solver: a workgroup waited too long for its neighbour's hand-over (fewer "
                "co-resident workgroups than stripes, or CUs held by other work); that solve is wrong";
@@ -4495,6 +4536,22 @@ static void rigid_lag_off(lpe_ctx *ctx, RigidDev *d) {
     d->grow_pairs = d->grow_contacts = 0;
 }
 
+static bool device_waits() {
+    static const bool ev = getenv("LPE_EVENT_WAITS") != nullptr;
+    return !ev;
+}
+static int tsync_alloc(lpe_ctx *ctx, RigidDev *d) {
+    if (d->tsync) return LPE_OK;
+    LPE_HIP(ctx, hipMalloc((void **)&d->tsync, sizeof(uint32_t) * 8));
+    LPE_HIP(ctx, hipMemsetAsync(d->tsync, 0, sizeof(uint32_t) * 8, ctx->stream));
+    d->tsyncTick = 0;
+    return LPE_OK;
+}
+// stream `s` waits (a one-wave k_wait_flag) until the word reaches `want`
+static int wait_flag(lpe_ctx *ctx, RigidDev *d, hipStream_t s, const uint32_t *flag, uint32_t want) {
+    LPE_KERNEL(ctx, "k_wait_flag", k_wait_flag, dim3(1), dim3(64), 0, s, flag, want, d->counts + 7);
+    return LPE_OK;
+}
 int rigid_tick_begin(lpe_ctx *ctx, bool on_main) {
     RigidDev *d = rdev(ctx);
     d->overlap_pending = false;
@@ -4537,12 +4594,21 @@ int rigid_tick_begin(lpe_ctx *ctx, bool on_main) {
     }
     hipStream_t s = ctx->stream;
     d->det = on_main ? s : d->side;
-    if (d->det != s)                           // (the detection's start: the clamp's launch signals it)
+    if (device_waits()) {
+        int st = tsync_alloc(ctx, d);
+        if (st) return st;
+        d->tsyncTick++;                        // (this tick's signals carry its number)
+    }
+    if (d->det != s && device_waits())         // (the detection's start: the clamp's last workgroup signals it)
+        LPE_KERNEL(ctx, "k_boundary_pos", k_boundary_pos, dim3(rblk(d->nb)), dim3(RTPB), 0, s, d->nb, d->bodies,
+                   c.marginPixels * c.metersPerPixel, c.universeSize, d->bbits, d->tsync, d->tsyncTick);
+    else if (d->det != s)                      // (or its launch carries the event)
         LPE_KERNEL_SIGNAL(ctx, "k_boundary_pos", d->evStart, k_boundary_pos, dim3(rblk(d->nb)), dim3(RTPB), 0, s,
-                          d->nb, d->bodies, c.marginPixels * c.metersPerPixel, c.universeSize, d->bbits);
+                          d->nb, d->bodies, c.marginPixels * c.metersPerPixel, c.universeSize, d->bbits,
+                          (uint32_t *)nullptr, 0u);
     else
         LPE_KERNEL(ctx, "k_boundary_pos", k_boundary_pos, dim3(rblk(d->nb)), dim3(RTPB), 0, s, d->nb, d->bodies,
-                   c.marginPixels * c.metersPerPixel, c.universeSize, d->bbits);
+                   c.marginPixels * c.metersPerPixel, c.universeSize, d->bbits, (uint32_t *)nullptr, 0u);
     d->detect_launched = false;
     d->overlap_pending = true;
     return LPE_OK;
@@ -4554,7 +4620,14 @@ int rigid_tick_begin(lpe_ctx *ctx, bool on_main) {
 // stream without work for that long at every tick start.
 static int rigid_tick_launch(lpe_ctx *ctx, RigidDev *d) {
     if (d->detect_launched) return LPE_OK;
-    if (d->det != ctx->stream) LPE_HIP(ctx, hipStreamWaitEvent(d->det, d->evStart, 0));
+    if (d->det != ctx->stream) {
+        if (device_waits()) {
+            int st = wait_flag(ctx, d, d->det, d->tsync + 2, d->tsyncTick);
+            if (st) return st;
+        } else {
+            LPE_HIP(ctx, hipStreamWaitEvent(d->det, d->evStart, 0));
+        }
+    }
     if (d->lag) {
         // lagged: the compaction follows at once and the counts go to a ring
         // slot, checked when the slot comes round again (two ticks later)
@@ -4588,6 +4661,16 @@ int rigid_tick_hook(lpe_ctx *ctx, int step) {
     return st;
 }
 
+// stream `s` waits for this tick's boundary/gravity pass (false: there is
+// no device signal this tick; the caller waits on rigid_boundary_event)
+int rigid_boundary_wait(lpe_ctx *ctx, hipStream_t s, bool *done) {
+    RigidDev *d = rdev(ctx);
+    *done = false;
+    if (d->nb <= 0 || !d->bvgSignal || !device_waits()) return LPE_OK;
+    *done = true;
+    return wait_flag(ctx, d, s, d->tsync, d->tsyncTick);
+}
+
 // the event the world tick's boundary/gravity pass signalled this tick, or null
 hipEvent_t rigid_boundary_event(lpe_ctx *ctx) {
     RigidDev *d = rdev(ctx);
@@ -4601,9 +4684,14 @@ int rigid_tick_boundary(lpe_ctx *ctx, bool gravity, double dt_state) {
     const lpe_rigid_config &c = d->cfg;
     if (gravity) {   // the planetary-mass check (k_gravity_check) is queued before
         if (!d->evBvg) LPE_HIP(ctx, hipEventCreateWithFlags(&d->evBvg, hipEventDisableTiming));
-        LPE_KERNEL_SIGNAL(ctx, "k_boundary_vel_gravity", d->evBvg, k_boundary_vel_gravity, dim3(rblk(d->nb)),
-                          dim3(RTPB), 0, ctx->stream, d->nb, d->bodies, d->bbits, c.bounceDamping, c.maxSpeed,
-                          c.gravity, dt_state, d->counts + 5);
+        if (device_waits() && d->tsync)
+            LPE_KERNEL(ctx, "k_boundary_vel_gravity", k_boundary_vel_gravity, dim3(rblk(d->nb)), dim3(RTPB), 0,
+                       ctx->stream, d->nb, d->bodies, d->bbits, c.bounceDamping, c.maxSpeed, c.gravity, dt_state,
+                       d->counts + 5, d->tsync, d->tsyncTick);
+        else
+            LPE_KERNEL_SIGNAL(ctx, "k_boundary_vel_gravity", d->evBvg, k_boundary_vel_gravity, dim3(rblk(d->nb)),
+                              dim3(RTPB), 0, ctx->stream, d->nb, d->bodies, d->bbits, c.bounceDamping, c.maxSpeed,
+                              c.gravity, dt_state, d->counts + 5, (uint32_t *)nullptr, 0u);
         d->bvgSignal = true;
         return LPE_OK;
     }
@@ -4700,7 +4788,12 @@ int rigid_tick_finish(lpe_ctx *ctx) {
         // (the boundary/gravity pass is the context stream's last rigid work
         // before the solvers, and the side stream is past the colouring; a
         // detection on the context stream runs after that pass: recorded)
-        LPE_HIP(ctx, hipStreamWaitEvent(d->side, d->evBvg, 0));
+        if (device_waits()) {
+            st = wait_flag(ctx, d, d->side, d->tsync, d->tsyncTick);
+            if (st) return st;
+        } else {
+            LPE_HIP(ctx, hipStreamWaitEvent(d->side, d->evBvg, 0));
+        }
     } else {
         LPE_HIP(ctx, hipEventRecord(d->evFork, s));
         LPE_HIP(ctx, hipStreamWaitEvent(d->side, d->evFork, 0));

@@ -3694,7 +3694,8 @@ static int slab_rebalance(lpe_ctx *ctx) {
 // CU-masked queue (round 1 kept 16 CUs free for the solvers) cost a third of
 // the tick rate on MI355X (396 vs 554 ticks/s on the settled metric scene),
 // while the solvers start promptly without it.
-int sph_prelaunch(lpe_ctx *ctx, double dt_tick, const std::function<int(hipStream_t)> &first, hipEvent_t ready) {
+int sph_prelaunch(lpe_ctx *ctx, double dt_tick, const std::function<int(hipStream_t)> &first, hipEvent_t ready,
+                  bool devwait) {
     SphDev &d = ctx->sph;
     d.pre = false;
     if (d.n <= 0 || !d.P.x) return LPE_OK;
@@ -3713,11 +3714,18 @@ int sph_prelaunch(lpe_ctx *ctx, double dt_tick, const std::function<int(hipStrea
         LPE_HIP(ctx, hipEventCreateWithFlags(&d.preDone, hipEventDisableTiming));
         LPE_HIP(ctx, hipEventCreateWithFlags(&d.fbgDone, hipEventDisableTiming));
     }
-    if (!ready) {
-        LPE_HIP(ctx, hipEventRecord(d.preReady, ctx->stream));
-        ready = d.preReady;
+    bool waited = false;
+    if (devwait) {
+        int st = rigid_boundary_wait(ctx, d.pside, &waited);
+        if (st) return st;
     }
-    LPE_HIP(ctx, hipStreamWaitEvent(d.pside, ready, 0));
+    if (!waited) {
+        if (!ready) {
+            LPE_HIP(ctx, hipEventRecord(d.preReady, ctx->stream));
+            ready = d.preReady;
+        }
+        LPE_HIP(ctx, hipStreamWaitEvent(d.pside, ready, 0));
+    }
     if (first) {
         const int st0 = first(d.pside);
         if (st0) {

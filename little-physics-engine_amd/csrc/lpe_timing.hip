@@ -8,6 +8,8 @@ namespace lpe {
 // ahead of the device (per-kernel events on every launch make the host the
 // bottleneck and the events then time the device idling between launches)
 bool KernelTimer::wants(const char *name) const {
+    // (a cross-stream wait, k_wait_flag, is no work of the tick: never timed)
+    if (std::strcmp(name, "k_wait_flag") == 0) return false;
     if (on == 1) return true;
     static const char *hot[] = {"k_density", "k_density_plan", "k_forces_couple", "k_pgs_flow", "k_pos_flow", "k_pair_colour",
                                 "k_narrow", "k_bg_pairs"};

@@ -262,7 +262,7 @@ extern "C" int lpe_world_tick(lpe_ctx *ctx, const lpe_world_config *wc, int ntic
         if (prelaunch) {
             // (with the fluid's boundary/gravity on the side stream, the bodies'
             // pass is the context stream's last launch: its signal serves)
-            st = fbg_side ? sph_prelaunch(ctx, dt_fluid, fbg, overlap ? rigid_boundary_event(ctx) : nullptr)
+            st = fbg_side ? sph_prelaunch(ctx, dt_fluid, fbg, overlap ? rigid_boundary_event(ctx) : nullptr, overlap)
                           : sph_prelaunch(ctx, dt_fluid);
             if (st) return st;
         }

@@ -128,6 +128,13 @@ struct RigidDev {
     // prelaunch wait on it instead of recording their own (bvgSignal: this tick)
     hipEvent_t evBvg = nullptr;
     bool bvgSignal = false;
+    // device-side waits (default; LPE_EVENT_WAITS=1: the events above): the
+    // boundary passes' last workgroup stores the tick number into a word that
+    // a one-wave kernel on the waiting stream polls, so no stream holds a
+    // blocked barrier packet during the fluid step (profiles/r06/events/).
+    // tsync: [0] boundary/gravity done, [1] its arrivals, [2] clamp done, [3] its arrivals
+    uint32_t *tsync = nullptr;
+    uint32_t tsyncTick = 0;
 };
 
 
