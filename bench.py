@@ -796,8 +796,8 @@ def scaling_blocks(world, primary, strong_leg, c5_one, m_one):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--scene", default="M")
     ap.add_argument("--prep", type=int, default=None,
                     help="untimed ticks that settle the scene before warmup (the pile forms); "

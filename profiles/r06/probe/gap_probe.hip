@@ -57,6 +57,20 @@ __global__ void k_dirty(Stamp *st, float4 *buf, int per) {
     stamp_end(st);
 }
 
+// the same bytes with non-temporal stores
+__global__ void k_dirty_nt(Stamp *st, float4 *buf, int per) {
+    stamp_begin(st);
+    size_t base = ((size_t)blockIdx.x * per) * 256 + threadIdx.x;
+    for (int i = 0; i < per; i++) {
+        float *p = (float *)(buf + base + (size_t)i * 256);
+        __builtin_nontemporal_store(1.f, p);
+        __builtin_nontemporal_store(2.f, p + 1);
+        __builtin_nontemporal_store(3.f, p + 2);
+        __builtin_nontemporal_store((float)i, p + 3);
+    }
+    stamp_end(st);
+}
+
 __global__ void k_spin(long long ticks) {
     long long t0 = wall_clock64();
     while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(10);
@@ -149,6 +163,11 @@ int main(int argc, char **argv) {
         char nm[96];
         std::snprintf(nm, sizeof nm, "1024 WG, %.1f MB dirty", 1024.0 * 256 * per * 16 / 1e6);
         show(nm, run(A, st, n, [&](int i) { k_dirty<<<1024, 256, 0, A>>>(st + (size_t)i * WGMAX, buf, per); }));
+    }
+    for (int per : {4, 16}) {
+        char nm[96];
+        std::snprintf(nm, sizeof nm, "1024 WG, %.1f MB dirty, non-temporal stores", 1024.0 * 256 * per * 16 / 1e6);
+        show(nm, run(A, st, n, [&](int i) { k_dirty_nt<<<1024, 256, 0, A>>>(st + (size_t)i * WGMAX, buf, per); }));
     }
     hipEvent_t ev;
     CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
