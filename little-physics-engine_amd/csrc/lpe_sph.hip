@@ -690,6 +690,10 @@ k_bucket_permute(int n, const int32_t *__restrict__ nptr, const uint32_t *__rest
     const int o = blockIdx.x * TPB + threadIdx.x;
     if (o >= (nptr ? *nptr : n)) return;      // (slab rank: its own slots and the received ghosts)
     const uint32_t k = key[o];
+    // the record's fields do not depend on the rank: loaded here, in flight
+    // with the bin's bounds and filed ids
+    const float kx = K.x[o], ky = K.y[o], pm = P.m[o], pvx = P.vx[o], pvy = P.vy[o];
+    const float khx = K.vhx[o], khy = K.vhy[o];
     if (k == KEY_DEAD) return;                 // (slab rank: a slot the previous sub-step dropped)
     const int myid = P.id[o];
     const int b = start[k], nk = start[k + 1] - b;
@@ -706,11 +710,11 @@ k_bucket_permute(int n, const int32_t *__restrict__ nptr, const uint32_t *__rest
     }
     const int d = b + rank;
     const uint32_t cl = k >> 2, cyr = cl / (uint32_t)W, cxr = cl - cyr * (uint32_t)W;
-    nbA[d] = make_float4(K.x[o], K.y[o], P.m[o], __int_as_float((int)((cyr << 17) | (cxr << 2) | (k & 3))));
-    nbB[2 * d] = make_float2(P.vx[o], P.vy[o]);
+    nbA[d] = make_float4(kx, ky, pm, __int_as_float((int)((cyr << 17) | (cxr << 2) | (k & 3))));
+    nbB[2 * d] = make_float2(pvx, pvy);
     S.id[d] = myid;
     if (refInv) refInv[myid] = d;
-    S.vhx[d] = K.vhx[o]; S.vhy[d] = K.vhy[o];
+    S.vhx[d] = khx; S.vhy[d] = khy;
     clearCnt[k] = 0;
 }
 
@@ -755,10 +759,20 @@ k_scan_rows(int W, int H, int ox, int oy, float eps, const int32_t *__restrict__
     if (bbG) {                              // slab rank: every rank's particles (k_ghost_unpack)
         if (threadIdx.x == 0) { const float4 b = *bbG; mnx = b.x; mxx = b.y; mny = b.z; mxy = b.w; }
     } else {
-        for (int p = threadIdx.x; p < nparts; p += TPB) {
-            const float4 b = bboxPart[p];
-            mnx = fminf(mnx, b.x); mxx = fmaxf(mxx, b.y);
-            mny = fminf(mny, b.z); mxy = fmaxf(mxy, b.w);
+        // (eight partials a thread in flight at once: the forces pass leaves
+        // one per block, ~2,000 at the metric scene)
+        for (int p0 = 0; p0 < nparts; p0 += 8 * TPB) {
+            float4 bq[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const int p = p0 + u * TPB + (int)threadIdx.x;
+                bq[u] = p < nparts ? bboxPart[p] : make_float4(1e30f, -1e30f, 1e30f, -1e30f);
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                mnx = fminf(mnx, bq[u].x); mxx = fmaxf(mxx, bq[u].y);
+                mny = fminf(mny, bq[u].z); mxy = fmaxf(mxy, bq[u].w);
+            }
         }
     }
     for (int off = 32; off > 0; off >>= 1) {
