@@ -1142,9 +1142,11 @@ __device__ __forceinline__ void pgs_row_c(float4 rn, float4 rr, float4 rc, float
             lo = -limit; hi = limit;
         }
         float dl = -eff * vrel;          // (the reference's + rhs, rhs = 0, changes only a zero's sign)
-        float nl = old + dl;
-        if (nl < lo) nl = lo;
-        if (nl > hi) nl = hi;
+        // the clamp (lo <= hi) as one v_med3_f32: the compare / select pairs
+        // cost two SGPR-mask hazard waits each on one wave; for a non-zero
+        // value the same result, a zero only possibly of the other sign,
+        // which dl = nl - old and the skip test below make +0 either way
+        const float nl = __builtin_amdgcn_fmed3f(old + dl, lo, hi);
         dl = nl - old;
         if (row == 0) ln = nl; else lf = nl;
         const float da = fabsf(dl) < 1e-15F ? 0.0f : dl;
