@@ -1121,11 +1121,14 @@ __device__ __forceinline__ void pgs_row_t(float4 rn, float4 rr, float imA, float
 // value (a zero velocity may change the sign of its zero, which no later
 // operation of the tick turns into a different non-zero value); for the same
 // reason vn + rhs (rhs = 0, :404) is vn
-__device__ __forceinline__ void pgs_row_c(float4 rn, float4 rr, float4 rc, float imA, float iiA, float imB,
+// (lv: the lever arms' perpendiculars (-r_A.y, r_A.x, -r_B.y, r_B.x), as the
+// stripe workgroups stage them once per solve -- exact sign flips -- so the
+// row does not rebuild them with a negate and a move per contact)
+__device__ __forceinline__ void pgs_row_l(float4 rn, float4 lv, float4 rc, float imA, float iiA, float imB,
                                           float iiB, float mu, float &ln, float &lf, float &vxA, float &vyA,
                                           float &wA, float &vxB, float &vyB, float &wB) {
     pk2 vA = {vxA, vyA}, vB = {vxB, vyB};
-    const pk2 lA = {-rr.y, rr.x}, lB = {-rr.w, rr.z};
+    const pk2 lA = {lv.x, lv.y}, lB = {lv.z, lv.w};
 #pragma unroll
     for (int row = 0; row < 2; row++) {
         const pk2 d = row == 0 ? pk2{rn.x, rn.y} : pk2{-rn.y, rn.x};
@@ -1157,6 +1160,12 @@ __device__ __forceinline__ void pgs_row_c(float4 rn, float4 rr, float4 rc, float
         wB = wB + crossB * da * iiB;
     }
     vxA = vA.x; vyA = vA.y; vxB = vB.x; vyB = vB.y;
+}
+__device__ __forceinline__ float4 lever_perp(float4 rr) { return make_float4(-rr.y, rr.x, -rr.w, rr.z); }
+__device__ __forceinline__ void pgs_row_c(float4 rn, float4 rr, float4 rc, float imA, float iiA, float imB,
+                                          float iiB, float mu, float &ln, float &lf, float &vxA, float &vyA,
+                                          float &wA, float &vxB, float &vyB, float &wB) {
+    pgs_row_l(rn, lever_perp(rr), rc, imA, iiA, imB, iiB, mu, ln, lf, vxA, vyA, wA, vxB, vyB, wB);
 }
 __device__ __forceinline__ void pgs_row_regs(float4 rn, float4 rr, float imA, float iiA, float imB,
                                              float iiB, bool hasA, bool hasB, float mu, float &ln,
@@ -2909,7 +2918,7 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
         int *stepL = (int *)(smem + oST);
         for (int r = threadIdx.x; r < NR; r += STPB) {
             const int g = r < v.nRA ? v.rA0 + r : v.rB0 + (r - v.nRA);
-            rn[r] = rowN[g]; rr[r] = rowR[g]; rc[r] = rowC[g];
+            rn[r] = rowN[g]; rr[r] = lever_perp(rowR[g]); rc[r] = rowC[g];   // (rr: staged as lever_perp)
             ln[r] = 0.f; lf[r] = 0.f;
         }
         for (int q = threadIdx.x; q < NP; q += STPB) {
@@ -2944,7 +2953,7 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
 #pragma unroll
                     for (int u = 0; u < U; u++) {
                         if (j0 + u >= p.y) break;
-                        pgs_row_c(a[u], c[u], x[u], m.x, m.y, m.z, m.w, mu, n[u], f[u], vxA, vyA, wA, vxB, vyB, wB);
+                        pgs_row_l(a[u], c[u], x[u], m.x, m.y, m.z, m.w, mu, n[u], f[u], vxA, vyA, wA, vxB, vyB, wB);
                         ln[p.x + j0 + u] = n[u];
                         lf[p.x + j0 + u] = f[u];
                     }
@@ -2989,7 +2998,7 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
                 for (int u = 0; u < U; u++) {
                     if (u >= p.y) break;
                     float n = cur.n[u], f = cur.f[u];
-                    pgs_row_c(cur.a[u], cur.c[u], cur.x[u], m.x, m.y, m.z, m.w, mu, n, f, vxA, vyA, wA, vxB, vyB,
+                    pgs_row_l(cur.a[u], cur.c[u], cur.x[u], m.x, m.y, m.z, m.w, mu, n, f, vxA, vyA, wA, vxB, vyB,
                               wB);
                     ln[p.x + u] = n;
                     lf[p.x + u] = f;
@@ -2997,7 +3006,7 @@ k_pgs_stripes(const int32_t *__restrict__ counts, StripeBufs sb, const int2 *__r
                 for (int jr = U; jr < p.y; jr++) {       // (pairs of more than U rows: the rest on demand)
                     const int t = p.x + jr;
                     float n = ln[t], f = lf[t];
-                    pgs_row_c(rn[t], rr[t], rc[t], m.x, m.y, m.z, m.w, mu, n, f, vxA, vyA, wA, vxB, vyB, wB);
+                    pgs_row_l(rn[t], rr[t], rc[t], m.x, m.y, m.z, m.w, mu, n, f, vxA, vyA, wA, vxB, vyB, wB);
                     ln[t] = n;
                     lf[t] = f;
                 }
