@@ -1983,6 +1983,36 @@ __global__ void k_merge_prestats(int32_t *__restrict__ st, int32_t *__restrict__
 // One neighbour j != i of computeForces (metal:352-399): false when the
 // reference skips it, else its force terms (the caller adds them in list
 // order: sumFx += fx, sumFy += fy).
+// The correctly rounded fp32 quotient and square root of the pair term
+// without the general sequences' range handling.  The compiler's x / y is
+// v_div_scale(y), v_rcp, v_div_scale(x), three Newton / remainder fma pairs,
+// v_div_fmas, v_div_fixup; its sqrtf scales inputs below 2^-96, takes
+// v_sqrt and picks the correctly rounded neighbour by two fma residuals, and
+// passes zero / inf through a class test.  For the pair term's operands --
+// r^2 >= minDistanceThreshold (1e-14) > 2^-96; r >= 1e-7 and rho_j >= 1e-12
+// normal with normal reciprocals; numerators zero or far above 2^-100; the
+// quotients normal or zero -- every scaling step is the identity and the fixups
+// return their input, so these shortened sequences compute the same values
+// bit for bit (the sub-step / tick parity tests run through them).
+__device__ __forceinline__ float div_inrange(float x, float y) {
+    float r = __builtin_amdgcn_rcpf(y);
+    const float e = __builtin_fmaf(-y, r, 1.0f);
+    r = __builtin_fmaf(e, r, r);
+    float q = x * r;
+    float rem = __builtin_fmaf(-y, q, x);
+    q = __builtin_fmaf(rem, r, q);
+    rem = __builtin_fmaf(-y, q, x);
+    return __builtin_fmaf(rem, r, q);
+}
+__device__ __forceinline__ float sqrt_inrange(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __int_as_float(__float_as_int(s) - 1), sp = __int_as_float(__float_as_int(s) + 1);
+    const float rm = __builtin_fmaf(-sm, s, x), rp = __builtin_fmaf(-sp, s, x);
+    float r = (0.0f >= rm) ? sm : s;
+    r = (0.0f < rp) ? sp : r;
+    return r;
+}
+
 struct PairOwn { float xi, yi, vxi, vyi, pti; bool ok; };
 struct PairConst { float h_ij, h_ij2, spF, lapC, visc, minDist, minDens; };
 __device__ __forceinline__ bool pair_term(const PairOwn &o, const PairConst &k, const float4 &oa, const float4 &ob,
@@ -1991,20 +2021,20 @@ __device__ __forceinline__ bool pair_term(const PairOwn &o, const PairConst &k, 
     const float r2 = dx * dx + dy * dy;
     if (r2 < k.minDist) return false;
     if (r2 >= k.h_ij2) return false;
-    const float r = sqrtf(r2);
+    const float r = sqrt_inrange(r2);
     const float rhoj = ob.z;
     if (rhoj < k.minDens || !o.ok) return false;
     const float mj = oa.z;
     const float term = o.pti + ob.w;
     const float diff = (k.h_ij - r);
     const float wSpiky = k.spF * (diff * diff);
-    const float rx = dx / r, ry = dy / r;
+    const float rx = div_inrange(dx, r), ry = div_inrange(dy, r);
     const float fxPress = -mj * term * wSpiky;
     fx = fxPress * rx;
     fy = fxPress * ry;
     const float vx_ij = o.vxi - ob.x, vy_ij = o.vyi - ob.y;
     const float wVisc = k.lapC * diff;
-    const float fVisc = k.visc * mj * (wVisc / rhoj);
+    const float fVisc = k.visc * mj * div_inrange(wVisc, rhoj);
     fx -= fVisc * vx_ij;
     fy -= fVisc * vy_ij;
     return true;
