@@ -1932,6 +1932,7 @@ struct SphStepParams {
     int nblk, chunk;          // forces pass: logical blocks, blocks per XCD run (0: plain order)
     int32_t *mergePre;        // sub-step 0 after a prelaunch: its stats to merge into status (else null)
     int nref;                 // slab rank: the whole fluid's particle count (ref_cap_walk's id bound)
+    int shortDiv;             // the pair term's thresholds keep its operands in range (pair_term)
 };
 
 // computeForces + velocityVerletFinish + impulse + push-out; reads the sorted
@@ -2015,26 +2016,27 @@ __device__ __forceinline__ float sqrt_inrange(float x) {
 
 struct PairOwn { float xi, yi, vxi, vyi, pti; bool ok; };
 struct PairConst { float h_ij, h_ij2, spF, lapC, visc, minDist, minDens; };
+template <bool SHORT>
 __device__ __forceinline__ bool pair_term(const PairOwn &o, const PairConst &k, const float4 &oa, const float4 &ob,
                                           float &fx, float &fy) {
     const float dx = o.xi - oa.x, dy = o.yi - oa.y;
     const float r2 = dx * dx + dy * dy;
     if (r2 < k.minDist) return false;
     if (r2 >= k.h_ij2) return false;
-    const float r = sqrt_inrange(r2);
+    const float r = SHORT ? sqrt_inrange(r2) : sqrtf(r2);
     const float rhoj = ob.z;
     if (rhoj < k.minDens || !o.ok) return false;
     const float mj = oa.z;
     const float term = o.pti + ob.w;
     const float diff = (k.h_ij - r);
     const float wSpiky = k.spF * (diff * diff);
-    const float rx = div_inrange(dx, r), ry = div_inrange(dy, r);
+    const float rx = SHORT ? div_inrange(dx, r) : dx / r, ry = SHORT ? div_inrange(dy, r) : dy / r;
     const float fxPress = -mj * term * wSpiky;
     fx = fxPress * rx;
     fy = fxPress * ry;
     const float vx_ij = o.vxi - ob.x, vy_ij = o.vyi - ob.y;
     const float wVisc = k.lapC * diff;
-    const float fVisc = k.visc * mj * div_inrange(wVisc, rhoj);
+    const float fVisc = k.visc * mj * (SHORT ? div_inrange(wVisc, rhoj) : wVisc / rhoj);
     fx -= fVisc * vx_ij;
     fy -= fVisc * vy_ij;
     return true;
@@ -2048,6 +2050,9 @@ struct CouplePool {
 };
 static_assert(sizeof(CouplePool) <= sizeof(float4) * 2 * FCAP, "the coupling pool fits the forces image");
 
+// SHORT: the pair term's shortened quotients and square root (SphStepParams
+// shortDiv: the thresholds keep their operands in range); else the general ones
+template <bool SHORT>
 __global__ void __launch_bounds__(HB, LPE_FORCES_MINW)
 k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict__ gp,
                 const int32_t *__restrict__ start, PState S, const float4 *__restrict__ nbA,
@@ -2163,7 +2168,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     const PairConst pk{h_ij, h_ij2, spF, lapC, sp.viscosity, sp.minDist, sp.minDens};
     auto pair = [&](const float4 &oa, const float4 &ob) {
         float fx, fy;
-        if (pair_term(me, pk, oa, ob, fx, fy)) {
+        if (pair_term<SHORT>(me, pk, oa, ob, fx, fy)) {
             sumFx += fx;
             sumFy += fy;
         }
@@ -4006,6 +4011,17 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
     sp.viscosity = c.viscosity;
     sp.minDist = c.numericalConfig.minDistanceThreshold;
     sp.minDens = c.numericalConfig.minDensityThreshold;
+    {
+        // the shortened quotients / square root of pair_term need r^2 >= 2^-60
+        // (r >= 2^-30), rho_j >= 2^-60 and wVisc / rho_j <= lapC h / minDens far
+        // below 2^90 (the general sequences' scaling thresholds); positions
+        // 0 or of magnitude >= 2^-76 m keep the differences' numerators above
+        // 2^-100 (any scene: the boundary keeps particles >= its margin inside)
+        const double h = c.gridConfig.smoothingLength;
+        const double lapC = 40.0 / (3.14159265358979 * std::pow(h, 5.0));   // (viscLaplacianCoeff2D)
+        sp.shortDiv = sp.minDist >= 0x1p-60f && sp.minDens >= 0x1p-60f && h > 0.0 && h < 1e3 &&
+                      lapC * h / sp.minDens < 0x1p80;
+    }
     sp.diag = d.diag;
     sp.refInv = sph_ref_inv(d);
     sp.nptr = nullptr;
@@ -4066,14 +4082,18 @@ int sph_step_hooked(lpe_ctx *ctx, double dt_tick, int (*hook)(lpe_ctx *, int)) {
             sp.mergePre = nullptr;
         }
         sp.ovl = (step == 0 && pre) ? d.ovl_pre : d.ovl_cur;
-        LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple, dim3(fgrid), dim3(HB), 0, s, sp, cp,
-                           (step == 0 && pre) ? d.gp + 1 : d.gp,
-                           d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart, d.rbinList,
-                           rbin_aabb(d),
-                           d.acq, d.status, kn, (const Hood *)sph_fplans(d),
-                           heavy ? HeavyIn{d.heavy + (size_t)d.heavyCur * HEAVY_WORDS, d.tileHeavy,
+        const HeavyIn hv = heavy ? HeavyIn{d.heavy + (size_t)d.heavyCur * HEAVY_WORDS, d.tileHeavy,
                                            d.heavy + (size_t)(1 - d.heavyCur) * HEAVY_WORDS}
-                                 : HeavyIn{});
+                                 : HeavyIn{};
+        const GridParams *gpf = (step == 0 && pre) ? d.gp + 1 : d.gp;
+        if (sp.shortDiv)
+            LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple<true>, dim3(fgrid), dim3(HB), 0, s, sp, cp, gpf,
+                       d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart,
+                       d.rbinList, rbin_aabb(d), d.acq, d.status, kn, (const Hood *)sph_fplans(d), hv);
+        else
+            LPE_KERNEL(ctx, "k_forces_couple", k_forces_couple<false>, dim3(fgrid), dim3(HB), 0, s, sp, cp, gpf,
+                       d.start, d.S, d.nbA, d.nbB, d.pr, d.nlist, d.ncount, d.P, d.rig, d.raabb, d.rbinStart,
+                       d.rbinList, rbin_aabb(d), d.acq, d.status, kn, (const Hood *)sph_fplans(d), hv);
         LPE_CHECK_LAUNCH(ctx, "k_forces_couple");
         if (sh) sh->cur = 1 - sh->cur;               // P's slots are now the ones this pass wrote
         if (hook) {                                  // (lpe_world_tick: the rigid detection)

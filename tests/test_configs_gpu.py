@@ -186,3 +186,35 @@ def test_c5_eight_slab_ranks_bit_exact(cells):
     for r in rbs:
         for k in ("x", "y", "vx", "vy"):
             np.testing.assert_array_equal(r[k], rb_ref[k], err_msg=k)
+
+
+def test_short_division_equals_general():
+    """The forces pass's pair term takes its quotients and square root by
+    shortened sequences when the fluid config's thresholds keep the operands
+    in range (SphStepParams.shortDiv).  A minimum density of
+    1e-20 (no particle comes near it) turns them off: three world ticks of the
+    metric scene in motion (M@240, the pile in the fluid) must give the same
+    bits either way -- the shortened sequences equal the general ones."""
+    s, fl, bodies, verts = _advanced("M", 240)
+
+    def run(min_dens):
+        ctx = lpe.Context(0)
+        try:
+            cfg = lpe.default_fluid_config()
+            cfg.numericalConfig.minDensityThreshold = min_dens
+            ctx.sph_set_config(cfg)
+            ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+            ctx.rigid_upload(bodies, verts)
+            ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+            ctx.world_set_coupling(np.arange(len(bodies) - 1, -1, -1, dtype=np.int32))
+            ctx.world_tick(DT, 3)
+            return ctx.sph_download(), ctx.rigid_download()
+        finally:
+            ctx.close()
+
+    short, rb_short = run(lpe.default_fluid_config().numericalConfig.minDensityThreshold)
+    general, rb_general = run(1e-20)
+    for k in ("x", "y", "vx", "vy", "density", "pressure"):
+        np.testing.assert_array_equal(short[k], general[k], err_msg=k)
+    for k in ("x", "y", "angle", "vx", "vy", "omega"):
+        np.testing.assert_array_equal(rb_short[k], rb_general[k], err_msg=k)
