@@ -3500,19 +3500,24 @@ __device__ __forceinline__ void grid_done_signal(uint32_t *ctr, uint32_t *flag, 
 }
 
 // One wave on the waiting stream: returns once *flag has reached `want`
-// (wrapping compare); a watchdog (~3 s) raises counts[7] bit 64 and returns,
-// so the stream never hangs on a signal that was not launched.
-__global__ void k_wait_flag(const uint32_t *__restrict__ flag, uint32_t want, int32_t *__restrict__ fault) {
+// (wrapping compare); a watchdog (limit polls: ~3 s in the tick) raises
+// `bit` in *fault and returns, so the stream never hangs on a signal that was
+// not launched.
+__global__ void k_wait_flag(const uint32_t *__restrict__ flag, uint32_t want, int32_t *__restrict__ fault,
+                            uint32_t limit, int32_t bit) {
     if (threadIdx.x != 0) return;
     for (uint32_t n = 0;; n++) {
         const uint32_t v = __hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
         if ((int32_t)(v - want) >= 0) return;
-        if (n == (1u << 24)) {
-            atomicOr(fault, 64);
+        if (n == limit) {
+            atomicOr(fault, bit);
             return;
         }
         __builtin_amdgcn_s_sleep(8);
     }
+}
+__global__ void k_set_flag(uint32_t *__restrict__ flag, uint32_t value) {
+    if (threadIdx.x == 0) __hip_atomic_store(flag, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ void k_boundary_pos(int nb, lpe_body *__restrict__ bodies, double m, double U,
@@ -4547,20 +4552,37 @@ static void rigid_lag_off(lpe_ctx *ctx, RigidDev *d) {
     d->grow_pairs = d->grow_contacts = 0;
 }
 
-static bool device_waits() {
+// Device waits need the waiting and the signalling streams' kernels to run
+// at the same time.  Where dispatches are serialised (rocprofv3 counter
+// collection, AMD_SERIALIZE_KERNEL, two streams on one hardware queue) the
+// waiter would hold its queue until its watchdog: tsync_alloc probes once
+// per context (a waiter on the context stream, its signal from the detection
+// stream launched after it; ~6 ms watchdog) and falls back to the events.
+static bool device_waits(const RigidDev *d) {
     static const bool ev = getenv("LPE_EVENT_WAITS") != nullptr;
-    return !ev;
+    return !ev && d->devwait_ok;
 }
 static int tsync_alloc(lpe_ctx *ctx, RigidDev *d) {
     if (d->tsync) return LPE_OK;
     LPE_HIP(ctx, hipMalloc((void **)&d->tsync, sizeof(uint32_t) * 8));
     LPE_HIP(ctx, hipMemsetAsync(d->tsync, 0, sizeof(uint32_t) * 8, ctx->stream));
     d->tsyncTick = 0;
+    if (d->side) {
+        LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        LPE_KERNEL(ctx, "k_wait_flag", k_wait_flag, dim3(1), dim3(64), 0, ctx->stream, d->tsync + 6, 1u,
+                   (int32_t *)(d->tsync + 7), 1u << 15, 1);
+        LPE_KERNEL(ctx, "k_set_flag", k_set_flag, dim3(1), dim3(64), 0, d->side, d->tsync + 6, 1u);
+        LPE_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        LPE_HIP(ctx, hipStreamSynchronize(d->side));
+        uint32_t probe[2] = {0, 0};
+        LPE_HIP(ctx, hipMemcpy(probe, d->tsync + 6, sizeof(probe), hipMemcpyDeviceToHost));
+        d->devwait_ok = probe[1] == 0;
+    }
     return LPE_OK;
 }
 // stream `s` waits (a one-wave k_wait_flag) until the word reaches `want`
 static int wait_flag(lpe_ctx *ctx, RigidDev *d, hipStream_t s, const uint32_t *flag, uint32_t want) {
-    LPE_KERNEL(ctx, "k_wait_flag", k_wait_flag, dim3(1), dim3(64), 0, s, flag, want, d->counts + 7);
+    LPE_KERNEL(ctx, "k_wait_flag", k_wait_flag, dim3(1), dim3(64), 0, s, flag, want, d->counts + 7, 1u << 24, 64);
     return LPE_OK;
 }
 int rigid_tick_begin(lpe_ctx *ctx, bool on_main) {
@@ -4605,12 +4627,13 @@ int rigid_tick_begin(lpe_ctx *ctx, bool on_main) {
     }
     hipStream_t s = ctx->stream;
     d->det = on_main ? s : d->side;
-    if (device_waits()) {
-        int st = tsync_alloc(ctx, d);
+    static const bool evwaits = getenv("LPE_EVENT_WAITS") != nullptr;
+    if (!evwaits) {
+        int st = tsync_alloc(ctx, d);          // (the first time: the concurrency probe)
         if (st) return st;
         d->tsyncTick++;                        // (this tick's signals carry its number)
     }
-    if (d->det != s && device_waits())         // (the detection's start: the clamp's last workgroup signals it)
+    if (d->det != s && device_waits(d))         // (the detection's start: the clamp's last workgroup signals it)
         LPE_KERNEL(ctx, "k_boundary_pos", k_boundary_pos, dim3(rblk(d->nb)), dim3(RTPB), 0, s, d->nb, d->bodies,
                    c.marginPixels * c.metersPerPixel, c.universeSize, d->bbits, d->tsync, d->tsyncTick);
     else if (d->det != s)                      // (or its launch carries the event)
@@ -4632,7 +4655,7 @@ int rigid_tick_begin(lpe_ctx *ctx, bool on_main) {
 static int rigid_tick_launch(lpe_ctx *ctx, RigidDev *d) {
     if (d->detect_launched) return LPE_OK;
     if (d->det != ctx->stream) {
-        if (device_waits()) {
+        if (device_waits(d)) {
             int st = wait_flag(ctx, d, d->det, d->tsync + 2, d->tsyncTick);
             if (st) return st;
         } else {
@@ -4677,7 +4700,7 @@ int rigid_tick_hook(lpe_ctx *ctx, int step) {
 int rigid_boundary_wait(lpe_ctx *ctx, hipStream_t s, bool *done) {
     RigidDev *d = rdev(ctx);
     *done = false;
-    if (d->nb <= 0 || !d->bvgSignal || !device_waits()) return LPE_OK;
+    if (d->nb <= 0 || !d->bvgSignal || !device_waits(d)) return LPE_OK;
     *done = true;
     return wait_flag(ctx, d, s, d->tsync, d->tsyncTick);
 }
@@ -4695,7 +4718,7 @@ int rigid_tick_boundary(lpe_ctx *ctx, bool gravity, double dt_state) {
     const lpe_rigid_config &c = d->cfg;
     if (gravity) {   // the planetary-mass check (k_gravity_check) is queued before
         if (!d->evBvg) LPE_HIP(ctx, hipEventCreateWithFlags(&d->evBvg, hipEventDisableTiming));
-        if (device_waits() && d->tsync)
+        if (device_waits(d) && d->tsync)
             LPE_KERNEL(ctx, "k_boundary_vel_gravity", k_boundary_vel_gravity, dim3(rblk(d->nb)), dim3(RTPB), 0,
                        ctx->stream, d->nb, d->bodies, d->bbits, c.bounceDamping, c.maxSpeed, c.gravity, dt_state,
                        d->counts + 5, d->tsync, d->tsyncTick);
@@ -4799,7 +4822,7 @@ int rigid_tick_finish(lpe_ctx *ctx) {
         // (the boundary/gravity pass is the context stream's last rigid work
         // before the solvers, and the side stream is past the colouring; a
         // detection on the context stream runs after that pass: recorded)
-        if (device_waits()) {
+        if (device_waits(d)) {
             st = wait_flag(ctx, d, d->side, d->tsync, d->tsyncTick);
             if (st) return st;
         } else {

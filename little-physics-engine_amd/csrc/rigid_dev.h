@@ -135,6 +135,7 @@ struct RigidDev {
     // tsync: [0] boundary/gravity done, [1] its arrivals, [2] clamp done, [3] its arrivals
     uint32_t *tsync = nullptr;
     uint32_t tsyncTick = 0;
+    bool devwait_ok = false;              // (tsync_alloc's probe: kernels of two streams run together)
 };
 
 

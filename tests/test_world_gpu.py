@@ -248,3 +248,47 @@ def test_prelaunch_voided_by_probe_and_upload(gpu_ctx):
     for k in ("x", "y", "vx", "vy", "density"):
         np.testing.assert_array_equal(got[k], want[k], err_msg=k)
         np.testing.assert_array_equal(again[k], want[k], err_msg=k)
+
+
+_SERIAL_SCRIPT = r"""
+import sys, numpy as np
+sys.path.insert(0, sys.argv[1])
+from conftest import lpe, scenes
+s = scenes.scene("small96_12")
+fl = s["fluid"]
+b, v = scenes.to_bodies(s["bodies"])
+ctx = lpe.Context(0)
+ctx.sph_set_config(lpe.default_fluid_config())
+ctx.rigid_set_config(lpe.rigid_config(universe=s["U"]))
+ctx.rigid_upload(b, v)
+ctx.sph_upload(fl["x"], fl["y"], fl["vx"], fl["vy"], fl["mass"], fl["density"], fl["pressure"])
+ctx.world_set_coupling(np.arange(len(b) - 1, -1, -1, dtype=np.int32))
+ctx.world_tick(1.0 / 120.0, 6)
+f = ctx.sph_download()
+r = ctx.rigid_download()          # (raises on a cross-stream wait's watchdog)
+np.savez(sys.argv[2], **{"f_" + k: f[k] for k in ("x", "y", "vx", "vy")},
+         **{"r_" + k: r[k] for k in ("x", "y", "angle", "vx", "vy", "omega")})
+ctx.close()
+"""
+
+
+def test_world_tick_with_serialised_dispatches(tmp_path):
+    """The world tick's cross-stream waits are device polls (k_wait_flag)
+    when the context's streams run kernels together, which a probe checks
+    once per context; with every dispatch serialised (AMD_SERIALIZE_KERNEL=3,
+    as under rocprofv3 counter collection) a poller would hold its queue until
+    its watchdog, so the tick must fall back to events: same bits as the
+    overlapped tick in this process, and no watchdog fault."""
+    import os
+    import subprocess
+    import sys
+    out = tmp_path / "serial.npz"
+    env = dict(os.environ, AMD_SERIALIZE_KERNEL="3")
+    tests_dir = os.path.dirname(os.path.abspath(__file__))
+    subprocess.run([sys.executable, "-c", _SERIAL_SCRIPT, tests_dir, str(out)], env=env, check=True, timeout=240)
+    f, r = _world_run("small96_12", 6, serial=False)
+    z = np.load(out)
+    for k in ("x", "y", "vx", "vy"):
+        np.testing.assert_array_equal(z["f_" + k], f[k], err_msg=k)
+    for k in ("x", "y", "angle", "vx", "vy", "omega"):
+        np.testing.assert_array_equal(z["r_" + k], r[k], err_msg=k)
