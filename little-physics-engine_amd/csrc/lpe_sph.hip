@@ -2124,7 +2124,10 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     __shared__ unsigned char pOwn[PAIR_CAP];
     __shared__ int pCount;
     CouplePool &pool = *reinterpret_cast<CouplePool *>(fimg);
-    if (threadIdx.x == 0) pCount = 0;
+    // the coupling's constants in LDS (read where the pair math uses them):
+    // held in SGPRs across the kernel they spilled into VGPR lanes
+    __shared__ CoupleParams s_cp;
+    if (threadIdx.x == 0) { pCount = 0; s_cp = cp; }
     if (fplans) hood_fetch(fplans, lb, hraw);
     const GridParams g = *gp;
     const float cs = g.cellSize;
@@ -2334,14 +2337,15 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     st.vx = st.vhx + sp.hdt * st.ax;
     st.vy = st.vhy + sp.hdt * st.ay;
     st.mass = meA.z; st.rho = rhoi; st.p = pi;
-    const float4 *rc = raabb + cp.nr;                 // the compact records (k_rig_couple)
+    const CoupleParams &cpl = s_cp;
+    const float4 *rc = raabb + cpl.nr;                 // the compact records (k_rig_couple)
     const int total = pCount;                         // (block-uniform: final since the barrier)
     if (total > PAIR_CAP) {
         if (live) {
-            const float fbx = fminf(fmaxf(floorf(st.x / cp.bcs) - (float)cp.bx0, 0.f), (float)(cp.bW - 1));
-            const float fby = fminf(fmaxf(floorf(st.y / cp.bcs) - (float)cp.by0, 0.f), (float)(cp.bH - 1));
-            const int bin = (int)fby * cp.bW + (int)fbx;
-            couple_both(st, cp, sp.dt, cp.nr > 0, rc, rbinAabb, rbinList, rbinStart[bin], rbinStart[bin + 1], acq,
+            const float fbx = fminf(fmaxf(floorf(st.x / cpl.bcs) - (float)cpl.bx0, 0.f), (float)(cpl.bW - 1));
+            const float fby = fminf(fmaxf(floorf(st.y / cpl.bcs) - (float)cpl.by0, 0.f), (float)(cpl.bH - 1));
+            const int bin = (int)fby * cpl.bW + (int)fbx;
+            couple_both(st, cpl, sp.dt, cpl.nr > 0, rc, rbinAabb, rbinList, rbinStart[bin], rbinStart[bin + 1], acq,
                         status);
         }
     } else {
@@ -2349,7 +2353,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
         if (total > 0) {
             __syncthreads();                          // (every read of the image done: the pool replaces it)
             // the particle's coupling inputs (pow only for a particle with hits)
-            pool.in[threadIdx.x] = couple_in(st, cp, cp.nr > 0 && nh > 0);
+            pool.in[threadIdx.x] = couple_in(st, cpl, cpl.nr > 0 && nh > 0);
             __syncthreads();
             FTR(6);
             FTR2SET(5, total);
@@ -2357,7 +2361,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
             // velocities are final), round robin
             for (int q = threadIdx.x; q < total; q += HB) {
                 PairTerm t;
-                pool.flag[q] = (unsigned char)couple_pair(pool.in[pOwn[q]], cp, sp.dt, true, rc, pRig[q], acq,
+                pool.flag[q] = (unsigned char)couple_pair(pool.in[pOwn[q]], cpl, sp.dt, true, rc, pRig[q], acq,
                                                           status, t, FTR_PAIRS());
                 pool.term[q] = t;
             }
@@ -2366,7 +2370,7 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
             if (live)
                 for (int q = off; q < off + nh; q++) a.fold(pool.term[q], pool.flag[q]);
         }
-        if (live) couple_finish(st, cp, a);
+        if (live) couple_finish(st, cpl, a);
     }
     FTR(4);
     if (live) {
