@@ -689,29 +689,20 @@ k_bucket_permute(int n, const int32_t *__restrict__ nptr, const uint32_t *__rest
                  int32_t *__restrict__ status) {
     const int o = blockIdx.x * TPB + threadIdx.x;
     if (o >= (nptr ? *nptr : n)) return;      // (slab rank: its own slots and the received ghosts)
-    const uint32_t k0 = key[o];
+    const uint32_t k = key[o];
     // the record's fields do not depend on the rank: loaded here, in flight
     // with the bin's bounds and filed ids
     const float kx = K.x[o], ky = K.y[o], pm = P.m[o], pvx = P.vx[o], pvy = P.vy[o];
     const float khx = K.vhx[o], khy = K.vhy[o];
+    if (k == KEY_DEAD) return;                 // (slab rank: a slot the previous sub-step dropped)
     const int myid = P.id[o];
-    // (slab rank: KEY_DEAD, a slot the previous sub-step dropped -- it loads
-    // bin 0's words and writes nothing)
-    const bool dead = k0 == KEY_DEAD;
-    const uint32_t k = dead ? 0u : k0;
-    // the bin's bounds and its first eight filed ids in one round trip (a
-    // quadrant bin rarely holds more): the rank's loads wait on the key only
+    const int b = start[k], nk = start[k + 1] - b;
     const int4 *bk = (const int4 *)(bucket + (size_t)k * BKT_CAP);
-    const int b = start[k], e = start[k + 1];
-    const int4 qa = bk[0], qb = bk[1];
-    if (dead) return;
-    const int nk = e - b;
-    auto below = [&](const int4 &q, int j) {
-        return (j < nk && q.x < myid) + (j + 1 < nk && q.y < myid) + (j + 2 < nk && q.z < myid) +
-               (j + 3 < nk && q.w < myid);
-    };
-    int rank = below(qa, 0) + below(qb, 4);
-    for (int j = 8; j < min(nk, BKT_CAP); j += 4) rank += below(bk[j >> 2], j);
+    int rank = 0;
+    for (int j = 0; j < min(nk, BKT_CAP); j += 4) {
+        const int4 q = bk[j >> 2];
+        rank += (q.x < myid) + (j + 1 < nk && q.y < myid) + (j + 2 < nk && q.z < myid) + (j + 3 < nk && q.w < myid);
+    }
     for (int j = b + BKT_CAP; j < b + nk; j++) rank += tmpId[j] < myid ? 1 : 0;   // (a full bin's later arrivals)
     if (rank >= nk) {              // (never: the bin's filed ids are its particles) fail loudly, write nothing
         atomicOr(&status[ST_BUCKET_OVERFLOW], 2);
@@ -2081,24 +2072,17 @@ k_forces_couple(SphStepParams sp, CoupleParams cp, const GridParams *__restrict_
     int slo = 0, shi = HB;                    // the block's slots of its tile: [s0 + slo, s0 + shi)
     int lb, pb;                               // the tile; the block's bbox partial slot
     if (bq < nq) {
-        int code, part, nparts, cls, idx;
+        int code, part, nparts;
         if (bq < QUARTER_BLOCKS) {
-            cls = 0; idx = bq / 4; code = 1 + idx; part = bq % 4; nparts = 4;
+            code = 1 + bq / 4; part = bq % 4; nparts = 4;
         } else if (bq < QUARTER_BLOCKS + HALF_BLOCKS) {
-            cls = 1; idx = (bq - QUARTER_BLOCKS) / 2; code = QUARTER_MAX + 1 + idx; part = (bq - QUARTER_BLOCKS) % 2;
-            nparts = 2;
+            code = QUARTER_MAX + 1 + (bq - QUARTER_BLOCKS) / 2; part = (bq - QUARTER_BLOCKS) % 2; nparts = 2;
         } else {
-            cls = 2; idx = bq - QUARTER_BLOCKS - HALF_BLOCKS; code = QUARTER_MAX + HALF_MAX + 1 + idx; part = 0;
-            nparts = 1;
+            code = QUARTER_MAX + HALF_MAX + 1 + (bq - QUARTER_BLOCKS - HALF_BLOCKS); part = 0; nparts = 1;
         }
         pb = sp.nblk + bq;
-        // the class's filings of this sub-step's density pass (its count, cleared
-        // by the forces pass before it) and the entry, in one round trip: an
-        // entry below the count was written by that pass, the tile it names
-        // holds this code (no dependent load of the tile's flag)
-        const int filed = hv.list[cls];
         lb = hv.list[2 + 2 * code];
-        if (idx >= filed || lb < 0 || lb >= sp.nblk) {     // (no such tile this sub-step)
+        if (lb < 0 || lb >= sp.nblk || hv.tile[lb] != code) {     // (no such tile this sub-step)
             if (kn.on && threadIdx.x == 0) kn.bboxPart[pb] = make_float4(1e30f, -1e30f, 1e30f, -1e30f);
             return;
         }
