@@ -109,6 +109,43 @@ def test_config_world_tick_bit_exact(oracle_mod, name, prep, mode):
         np.testing.assert_array_equal(got_b[k], rb[k], err_msg=(name, k))
 
 
+def test_mode_switch_voids_prelaunch_with_filed_tiles():
+    """The bench's sequence: world ticks in one cell mode, then a switch to the
+    reference's capped cells (which voids the pending prelaunched sub-step, its
+    density pass having filed the heavy tiles), then world ticks.  The filing
+    lists alternate by density pass and only a forces pass clears the other
+    one's counts, so after a void the next pass files into a list whose counts
+    no forces pass cleared: the forces pass's filed blocks must still run only
+    the tiles this pass filed (the tile-flag check).  Equal, bit for bit, to
+    the same ticks from the downloaded state in a fresh context (no pending
+    prelaunch); the round-6 fault was a tile run twice, its particles counted
+    twice into the next hash."""
+    s, fl, bodies, verts = _advanced("M", 240)
+    ctx = _world_ctx(s["U"], fl, bodies, verts, 0)
+    try:
+        ctx.world_tick(DT, 2)
+        mid_f, mid_b = ctx.sph_download(), ctx.rigid_download()
+        ctx.sph_set_mode(lpe.SPH_MODE_REF_CELL_CAP)       # voids the prelaunch
+        ctx.world_tick(DT, 2)
+        got_f, got_b = ctx.sph_download(), ctx.rigid_download()
+        st = ctx.sph_stats()
+    finally:
+        ctx.close()
+    fl2 = dict(x=mid_f["x"], y=mid_f["y"], vx=mid_f["vx"], vy=mid_f["vy"], mass=fl["mass"],
+               density=mid_f["density"], pressure=mid_f["pressure"])
+    ref = _world_ctx(s["U"], fl2, mid_b, verts, lpe.SPH_MODE_REF_CELL_CAP)
+    try:
+        ref.world_tick(DT, 2)
+        want_f, want_b = ref.sph_download(), ref.rigid_download()
+    finally:
+        ref.close()
+    assert st["refUndefined"] == 0
+    for k in ("x", "y", "vx", "vy", "density", "pressure"):
+        np.testing.assert_array_equal(got_f[k], want_f[k], err_msg=k)
+    for k in ("x", "y", "angle", "vx", "vy", "omega"):
+        np.testing.assert_array_equal(got_b[k], want_b[k], err_msg=k)
+
+
 def _m_ticks(monkeypatch, q, h, ticks):
     """M from its 240-tick state advanced `ticks` world ticks, the tile
     scheduling's class thresholds set to (q, h) coupling pairs (None: default)."""
